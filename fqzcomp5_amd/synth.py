@@ -1,0 +1,156 @@
+"""Seeded synthetic FASTQ generator.
+
+The reference ships no large inputs, so every benchmark and large parity
+case is generated here from a seed.  The shapes follow SURVEY.md §8(d) d2:
+
+* ``illumina``  (config C2): 150 bp, Illumina-style names, uniform ACGT with
+  1 % of reads carrying one ``N``; qualities are a clipped random walk over
+  Q2..Q41 binned to the 8 Illumina levels {2,6,15,22,27,33,37,40}.
+* ``q40walk``   : as ``illumina`` but the walk is left un-binned (~40 levels).
+* ``novaseq``   (config C3): qualities i.i.d. from {2,12,23,37} with
+  p = {.01,.04,.10,.85}.
+
+Records are returned in the reference's in-memory SoA layout
+(``fastq`` struct, fqzcomp5.c:235-249): concatenated sequence bytes,
+concatenated quality bytes stored as ``q-33``... except that here the
+qualities are returned as *raw phred values* (already ``q-33``, exactly what
+``load_seqs_kseq`` stores at fqzcomp5.c:564), per-record lengths and flags.
+Block splitting follows ``load_seqs_kseq`` (fqzcomp5.c:471-477): a record of
+``name.l + 1 + seq.l + qual.l`` bytes starts a new block when it would push
+a non-empty block past ``blk_size``.
+"""
+from __future__ import annotations
+
+import dataclasses
+import numpy as np
+
+ILLUMINA_BINS = np.array([2, 6, 15, 22, 27, 33, 37, 40], dtype=np.uint8)
+
+
+def _illumina_bin(q: np.ndarray) -> np.ndarray:
+    # Illumina 8-level binning: 2-9 -> 6, 10-19 -> 15, 20-24 -> 22,
+    # 25-29 -> 27, 30-34 -> 33, 35-39 -> 37, >=40 -> 40; <2 -> 2.
+    edges = np.array([2, 10, 20, 25, 30, 35, 40], dtype=np.int16)
+    idx = np.searchsorted(edges, q.astype(np.int16), side="right")
+    return ILLUMINA_BINS[idx]
+
+
+@dataclasses.dataclass
+class Reads:
+    """One set of records in the reference's SoA layout."""
+    seq: np.ndarray        # uint8, concatenated bases
+    qual: np.ndarray       # uint8, concatenated phred values (q-33)
+    lens: np.ndarray       # uint32 per record
+    names: list | None     # list[bytes] without '@' (name + ' ' + comment)
+    name_l: np.ndarray     # int32: kseq name.l (name part before the space)
+
+    @property
+    def num_records(self) -> int:
+        return int(self.lens.shape[0])
+
+    @property
+    def fixed_len(self) -> int:
+        if self.num_records == 0:
+            return 0
+        l0 = int(self.lens[0])
+        return l0 if bool(np.all(self.lens == l0)) else 0
+
+    def to_fastq(self) -> bytes:
+        assert self.names is not None
+        out = []
+        off = 0
+        for i, ln in enumerate(self.lens.tolist()):
+            s = self.seq[off:off + ln].tobytes()
+            q = (self.qual[off:off + ln] + 33).astype(np.uint8).tobytes()
+            out.append(b"@" + self.names[i] + b"\n" + s + b"\n+\n" + q + b"\n")
+            off += ln
+        return b"".join(out)
+
+
+def _names(rng: np.random.Generator, n: int) -> tuple[list, np.ndarray]:
+    lane = rng.integers(1, 5, n)
+    tile = rng.integers(1101, 2679, n)
+    x = np.sort(rng.integers(1000, 32000, n))
+    y = rng.integers(1000, 40000, n)
+    names = [b"A00123:45:HXXXXXXX:%d:%d:%d:%d 1:N:0:ACGTACGT" % t
+             for t in zip(lane.tolist(), tile.tolist(), x.tolist(), y.tolist())]
+    name_l = np.array([nm.index(b" ") for nm in names], dtype=np.int32)
+    return names, name_l
+
+
+def _name_lengths(rng: np.random.Generator, n: int) -> np.ndarray:
+    # Same digit-count distribution as _names() without building strings.
+    lane = rng.integers(1, 5, n)
+    tile = rng.integers(1101, 2679, n)
+    x = rng.integers(1000, 32000, n)
+    y = rng.integers(1000, 40000, n)
+    nd = lambda v: np.floor(np.log10(v)).astype(np.int32) + 1  # noqa: E731
+    return (len(b"A00123:45:HXXXXXXX") + 4 + nd(lane) + nd(tile) + nd(x)
+            + nd(y)).astype(np.int32)
+
+
+def illumina(n_reads: int, seed: int = 1, read_len: int = 150,
+             binned: bool = True, with_names: bool = False) -> Reads:
+    rng = np.random.default_rng(seed)
+    seq = np.frombuffer(b"ACGT", dtype=np.uint8)[
+        rng.integers(0, 4, n_reads * read_len, dtype=np.uint8)].copy()
+    has_n = np.nonzero(rng.random(n_reads) < 0.01)[0]
+    seq[has_n * read_len + rng.integers(0, read_len, has_n.shape[0])] = ord("N")
+
+    start = rng.integers(30, 42, (n_reads, 1)).astype(np.int16)
+    steps = rng.choice(np.array([-3, -1, 0, 0, 0, 0, 1, 2], dtype=np.int16),
+                       size=(n_reads, read_len))
+    steps[:, 0] = 0
+    q = np.clip(start + np.cumsum(steps, axis=1), 2, 41)
+    # quality tails off towards the 3' end, like a real run
+    q = np.clip(q - (np.arange(read_len) // 30)[None, :], 2, 41)
+    q = q.reshape(-1)
+    qual = _illumina_bin(q) if binned else q.astype(np.uint8)
+    lens = np.full(n_reads, read_len, dtype=np.uint32)
+    if with_names:
+        names, name_l = _names(rng, n_reads)
+    else:
+        names, name_l = None, _name_lengths(rng, n_reads)
+    return Reads(seq, qual.astype(np.uint8), lens, names, name_l)
+
+
+def novaseq(n_reads: int, seed: int = 2, read_len: int = 150,
+            with_names: bool = False) -> Reads:
+    rng = np.random.default_rng(seed)
+    seq = np.frombuffer(b"ACGT", dtype=np.uint8)[
+        rng.integers(0, 4, n_reads * read_len, dtype=np.uint8)].copy()
+    levels = np.array([2, 12, 23, 37], dtype=np.uint8)
+    qual = levels[rng.choice(4, size=n_reads * read_len,
+                             p=[.01, .04, .10, .85])]
+    lens = np.full(n_reads, read_len, dtype=np.uint32)
+    if with_names:
+        names, name_l = _names(rng, n_reads)
+    else:
+        names, name_l = None, _name_lengths(rng, n_reads)
+    return Reads(seq, qual, lens, names, name_l)
+
+
+def split_blocks(r: Reads, blk_size: int) -> list[tuple[int, int]]:
+    """Record ranges [a, b) per block, by the load_seqs_kseq rule
+    (fqzcomp5.c:471-477): ``record_size = name.l + 1 + seq.l + qual.l``."""
+    rec = (r.name_l.astype(np.int64) + 1 + 2 * r.lens.astype(np.int64))
+    out, a, tot = [], 0, 0
+    csum = np.cumsum(rec)
+    n = r.num_records
+    while a < n:
+        base = csum[a - 1] if a else 0
+        # first index b>a with csum[b]-base > blk_size (record b overflows)
+        b = int(np.searchsorted(csum, base + blk_size, side="right"))
+        b = max(b, a + 1)
+        out.append((a, b))
+        a = b
+    del tot
+    return out
+
+
+def block(r: Reads, a: int, b: int) -> Reads:
+    offs = np.concatenate([[0], np.cumsum(r.lens.astype(np.int64))])
+    s, e = int(offs[a]), int(offs[b])
+    return Reads(r.seq[s:e], r.qual[s:e], r.lens[a:b],
+                 r.names[a:b] if r.names is not None else None,
+                 r.name_l[a:b])

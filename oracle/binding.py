@@ -1,0 +1,135 @@
+"""ctypes bindings to the CPU oracle — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module, and only as the checker.
+Nothing in ``fqzcomp5_amd`` imports it; the product path never touches it.
+
+Two libraries share the htscodecs C-ABI signatures
+(htscodecs/rANS_static4x16.h:41-50, fqzcomp_qual.h:155-170):
+
+* ``liboracle.so``        our plain-C restatement (oracle/*.c), symbols
+                          prefixed ``ora_``;
+* ``_ref/libhtsref.so``   the reference compiled from /root/reference by
+                          oracle/Makefile (absent unless built here).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libhtsref.so")
+REF_BIN = os.path.join(HERE, "_ref", "fqzcomp5")
+
+_libc = C.CDLL(None)
+_libc.free.argtypes = [C.c_void_p]
+
+
+class FqzSlice(C.Structure):
+    # htscodecs/fqzcomp_qual.h:59-64 (fork ABI)
+    _fields_ = [("num_records", C.c_int),
+                ("len", C.POINTER(C.c_uint32)),
+                ("flags", C.POINTER(C.c_uint32)),
+                ("seq", C.POINTER(C.c_void_p))]
+
+
+class _Codec:
+    def __init__(self, path: str, prefix: str):
+        self.path = path
+        self.lib = C.CDLL(path)
+        p = prefix
+        f = getattr(self.lib, p + "rans_compress_4x16")
+        f.restype = C.c_void_p
+        f.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint), C.c_int]
+        self._rc = f
+        f = getattr(self.lib, p + "rans_uncompress_4x16")
+        f.restype = C.c_void_p
+        f.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint)]
+        self._ru = f
+        self._fc = getattr(self.lib, p + "fqz_compress", None)
+        if self._fc is not None:
+            self._fc.restype = C.c_void_p
+            self._fc.argtypes = [C.c_int, C.POINTER(FqzSlice), C.c_char_p,
+                                 C.c_size_t, C.POINTER(C.c_size_t), C.c_int,
+                                 C.c_void_p]
+        self._fd = getattr(self.lib, p + "fqz_decompress", None)
+        if self._fd is not None:
+            self._fd.restype = C.c_void_p
+            self._fd.argtypes = [C.c_char_p, C.c_size_t,
+                                 C.POINTER(C.c_size_t), C.POINTER(C.c_int),
+                                 C.c_int, C.POINTER(FqzSlice)]
+
+    @staticmethod
+    def _take(ptr, n) -> bytes:
+        if not ptr:
+            raise RuntimeError("codec returned NULL")
+        b = C.string_at(ptr, n)
+        _libc.free(ptr)
+        return b
+
+    def rans_compress(self, data: bytes, order: int) -> bytes:
+        n = C.c_uint(0)
+        p = self._rc(bytes(data), len(data), C.byref(n), order)
+        return self._take(p, n.value)
+
+    def rans_uncompress(self, comp: bytes) -> bytes:
+        n = C.c_uint(0)
+        p = self._ru(bytes(comp), len(comp), C.byref(n))
+        return self._take(p, n.value)
+
+    def _slice(self, lens, flags, seq: bytes | None):
+        import numpy as np
+        nr = len(lens)
+        L = (C.c_uint32 * nr)(*[int(x) for x in lens])
+        Fl = (C.c_uint32 * nr)(*[int(x) for x in flags])
+        keep = [L, Fl]
+        S = None
+        if seq is not None:
+            sb = C.create_string_buffer(bytes(seq), len(seq) + 1)
+            keep.append(sb)
+            base = C.addressof(sb)
+            offs = np.concatenate([[0], np.cumsum(np.asarray(lens, np.int64))])
+            S = (C.c_void_p * nr)(*[base + int(o) for o in offs[:-1]])
+            keep.append(S)
+        s = FqzSlice(nr, L, Fl, S)
+        return s, keep
+
+    def fqz_compress(self, qual: bytes, lens, flags, strat: int,
+                     seq: bytes | None = None, vers: int = 4) -> bytes:
+        s, keep = self._slice(lens, flags, seq)
+        n = C.c_size_t(0)
+        p = self._fc(vers, C.byref(s), bytes(qual), len(qual), C.byref(n),
+                     strat, None)
+        return self._take(p, n.value)
+
+    def fqz_decompress(self, comp: bytes, lens, flags,
+                       seq: bytes | None = None) -> bytes:
+        s, keep = self._slice(lens, flags, seq)
+        n = C.c_size_t(0)
+        nl = len(lens)
+        Larr = (C.c_int * max(nl, 1))()
+        p = self._fd(bytes(comp), len(comp), C.byref(n), Larr, nl,
+                     C.byref(s))
+        return self._take(p, n.value)
+
+
+_cache: dict = {}
+
+
+def oracle() -> _Codec:
+    """Our restatement (liboracle.so)."""
+    if "ora" not in _cache:
+        _cache["ora"] = _Codec(ORACLE_SO, "ora_")
+    return _cache["ora"]
+
+
+def have_ref() -> bool:
+    return os.path.exists(REF_SO)
+
+
+def ref() -> _Codec:
+    """The reference itself, compiled from /root/reference (oracle/_ref)."""
+    if "ref" not in _cache:
+        _cache["ref"] = _Codec(REF_SO, "")
+    return _cache["ref"]

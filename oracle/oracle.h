@@ -1,0 +1,22 @@
+/* oracle.h — TEST ORACLE ONLY.  Prototypes of the plain-C restatement in the
+ * oracle C sources.  Symbols carry an ora_ prefix so the oracle can be loaded
+ * beside the product library and the reference without clashing. */
+#ifndef FQZ5_ORACLE_H
+#define FQZ5_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+int ora_var_put_u32(uint8_t *cp, const uint8_t *endp, uint32_t v);
+int ora_var_get_u32(const uint8_t *cp, const uint8_t *endp, uint32_t *v);
+
+unsigned int ora_rans_compress_bound_4x16(unsigned int size, int order);
+uint8_t *ora_rans_compress_to_4x16(uint8_t *in, unsigned int in_size,
+                                   uint8_t *out, unsigned int *out_size,
+                                   int order);
+uint8_t *ora_rans_compress_4x16(uint8_t *in, unsigned int in_size,
+                                unsigned int *out_size, int order);
+uint8_t *ora_rans_uncompress_to_4x16(uint8_t *in, unsigned int in_size,
+                                     uint8_t *out, unsigned int *out_size);
+uint8_t *ora_rans_uncompress_4x16(uint8_t *in, unsigned int in_size,
+                                  unsigned int *out_size);
+#endif
