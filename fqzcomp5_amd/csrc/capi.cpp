@@ -1,0 +1,208 @@
+// capi.cpp — extern "C" entry points (include/fqz5_mi355x.h).
+#include <climits>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "../../include/fqz5_mi355x.h"
+#include "rans_codec.hpp"
+#include "rans_format.hpp"
+
+namespace fqz5 {
+
+static thread_local std::string g_err;
+static thread_local std::unique_ptr<GpuCtx> g_ctx;
+
+GpuCtx &gpu() {
+    if (!g_ctx) g_ctx.reset(new GpuCtx());
+    return *g_ctx;
+}
+
+// Size a stream decodes to, from its header (needed when the caller did
+// not give an output buffer).  0 with ok=false if it cannot be known.
+static uint32_t header_size(const uint8_t *in, uint32_t len, bool *ok) {
+    *ok = false;
+    if (!len) return 0;
+    if ((in[0] & ORD_NOSZ) && !(in[0] & ORD_STRIPE)) return 0;
+    uint32_t v = 0;
+    if (!varint_get(in + 1, in + len, &v)) return 0;
+    *ok = true;
+    return v;
+}
+
+}  // namespace fqz5
+
+using namespace fqz5;
+
+#define GUARD_BEGIN try {
+#define GUARD_END(failret)                                                    \
+    }                                                                         \
+    catch (const std::exception &e) {                                         \
+        g_err = e.what();                                                     \
+        try { if (g_ctx) g_ctx->reset(); } catch (...) {}                     \
+        return failret;                                                       \
+    }
+
+extern "C" {
+
+unsigned int rans_compress_bound_4x16(unsigned int size, int order) {
+    return compress_bound(size, order);
+}
+
+unsigned char *rans_compress_to_4x16(unsigned char *in, unsigned int in_size,
+                                     unsigned char *out, unsigned int *out_size,
+                                     int order) {
+    if (in_size > unsigned(INT_MAX) || (out && *out_size == 0)) {
+        *out_size = 0;
+        return nullptr;
+    }
+    GUARD_BEGIN
+    GpuCtx &g = gpu();
+    std::vector<CompressReq> reqs(1);
+    reqs[0].d_in = g.upload(in, in_size);
+    reqs[0].n = in_size;
+    reqs[0].order = order;
+    reqs[0].cap = out ? *out_size : compress_bound(in_size, order);
+    compress_batch(g, reqs);
+    if (!reqs[0].ok) {
+        g.reset();
+        *out_size = 0;
+        return nullptr;
+    }
+    const uint32_t sz = layout_size(reqs[0].out);
+    unsigned char *dst = out;
+    if (!dst) {
+        dst = static_cast<unsigned char *>(malloc(compress_bound(in_size, order)));
+        if (!dst) { g.reset(); *out_size = 0; return nullptr; }
+    }
+    write_layout_host(g, reqs[0].out, dst);
+    g.reset();
+    *out_size = sz;
+    return dst;
+    GUARD_END((*out_size = 0, nullptr))
+}
+
+unsigned char *rans_compress_4x16(unsigned char *in, unsigned int in_size,
+                                  unsigned int *out_size, int order) {
+    return rans_compress_to_4x16(in, in_size, nullptr, out_size, order);
+}
+
+unsigned char *rans_uncompress_to_4x16(unsigned char *in, unsigned int in_size,
+                                       unsigned char *out, unsigned int *out_size) {
+    if (!in_size) return nullptr;
+    GUARD_BEGIN
+    uint32_t cap;
+    if (out) {
+        cap = *out_size;
+    } else {
+        bool ok;
+        cap = header_size(in, in_size, &ok);
+        if (!ok || cap >= unsigned(INT_MAX)) return nullptr;
+    }
+    GpuCtx &g = gpu();
+    std::vector<DecompressReq> reqs(1);
+    reqs[0].h_in = in;
+    reqs[0].d_in = g.upload(in, in_size);
+    reqs[0].in_size = in_size;
+    reqs[0].out_cap = cap;
+    reqs[0].d_out = g.arena.alloc_n<uint8_t>(size_t(cap) + 1);
+    decompress_batch(g, reqs);
+    if (!reqs[0].ok) { g.reset(); return nullptr; }
+    unsigned char *dst = out;
+    if (!dst) {
+        dst = static_cast<unsigned char *>(malloc(cap ? cap : 1));
+        if (!dst) { g.reset(); return nullptr; }
+    }
+    g.download(dst, reqs[0].d_out, reqs[0].out_size);
+    g.reset();
+    *out_size = reqs[0].out_size;
+    return dst;
+    GUARD_END(nullptr)
+}
+
+unsigned char *rans_uncompress_4x16(unsigned char *in, unsigned int in_size,
+                                    unsigned int *out_size) {
+    return rans_uncompress_to_4x16(in, in_size, nullptr, out_size);
+}
+
+void rans_set_cpu(int) {}
+
+int fqz5_rans_compress_batch(fqz5_rans_job *jobs, int n) {
+    GUARD_BEGIN
+    GpuCtx &g = gpu();
+    std::vector<CompressReq> reqs(n);
+    for (int i = 0; i < n; i++) {
+        reqs[i].d_in = jobs[i].in;
+        reqs[i].n = jobs[i].in_size;
+        reqs[i].order = jobs[i].order;
+        reqs[i].cap = jobs[i].out_cap;
+    }
+    compress_batch(g, reqs);
+    std::vector<const Layout *> ls;
+    std::vector<uint8_t *> dsts;
+    for (int i = 0; i < n; i++) {
+        jobs[i].status = reqs[i].ok ? 0 : -1;
+        jobs[i].out_size = reqs[i].ok ? layout_size(reqs[i].out) : 0;
+        if (reqs[i].ok) {
+            ls.push_back(&reqs[i].out);
+            dsts.push_back(jobs[i].out);
+        }
+    }
+    write_layouts_dev(g, ls, dsts);
+    g.reset();
+    return 0;
+    GUARD_END(-1)
+}
+
+int fqz5_rans_uncompress_batch(fqz5_rans_job *jobs, int n) {
+    GUARD_BEGIN
+    GpuCtx &g = gpu();
+    // headers are parsed on the host: bring the compressed bytes over
+    size_t tot = 0;
+    for (int i = 0; i < n; i++) tot += jobs[i].in_size;
+    std::vector<uint8_t> host(tot + 1);
+    std::vector<DecompressReq> reqs(n);
+    size_t off = 0;
+    for (int i = 0; i < n; i++) {
+        g.download(host.data() + off, jobs[i].in, jobs[i].in_size);
+        reqs[i].h_in = host.data() + off;
+        reqs[i].d_in = jobs[i].in;
+        reqs[i].in_size = jobs[i].in_size;
+        reqs[i].out_cap = jobs[i].out_cap;
+        reqs[i].d_out = jobs[i].out;
+        off += jobs[i].in_size;
+    }
+    g.sync();
+    decompress_batch(g, reqs);
+    for (int i = 0; i < n; i++) {
+        jobs[i].status = reqs[i].ok ? 0 : -1;
+        jobs[i].out_size = reqs[i].out_size;
+    }
+    g.reset();
+    return 0;
+    GUARD_END(-1)
+}
+
+void *fqz5_stream(void) {
+    try {
+        return gpu().stream;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+int fqz5_device_ok(void) {
+    try {
+        gpu();
+        return 1;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return 0;
+    }
+}
+
+const char *fqz5_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

@@ -1,0 +1,147 @@
+// gpu_ctx.hpp — per-host-thread GPU context: one HIP stream plus a device
+// bump arena that is reset after every batch.  The htscodecs entry points
+// are re-entrant and called from many worker threads at once
+// (fqzcomp5.c:2721-2729); giving each host thread its own
+// stream and arena keeps concurrent calls independent.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace fqz5 {
+
+struct GpuError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define FQZ5_HIP(expr)                                                        \
+    do {                                                                      \
+        hipError_t e_ = (expr);                                               \
+        if (e_ != hipSuccess)                                                 \
+            throw ::fqz5::GpuError(std::string(#expr) + ": " +               \
+                                   hipGetErrorString(e_));                    \
+    } while (0)
+
+// Device memory arena.  Chunks are kept across batches; reset() rewinds.
+class DevArena {
+  public:
+    ~DevArena() {
+        for (auto &c : chunks_) (void)hipFree(c.base);
+    }
+    void *alloc(size_t n, size_t align = 256) {
+        if (n == 0) n = 1;
+        for (; cur_ < chunks_.size(); cur_++) {
+            Chunk &c = chunks_[cur_];
+            size_t off = (c.used + align - 1) & ~(align - 1);
+            if (off + n <= c.size) {
+                c.used = off + n;
+                return static_cast<uint8_t *>(c.base) + off;
+            }
+        }
+        size_t sz = n + align > (size_t(256) << 20) ? n + align : (size_t(256) << 20);
+        Chunk c{nullptr, sz, 0};
+        FQZ5_HIP(hipMalloc(&c.base, sz));
+        chunks_.push_back(c);
+        cur_ = chunks_.size() - 1;
+        chunks_[cur_].used = n;
+        return c.base;
+    }
+    template <class T> T *alloc_n(size_t n) {
+        return static_cast<T *>(alloc(n * sizeof(T), alignof(T) > 256 ? alignof(T) : 256));
+    }
+    void reset() {
+        for (auto &c : chunks_) c.used = 0;
+        cur_ = 0;
+    }
+
+  private:
+    struct Chunk { void *base; size_t size, used; };
+    std::vector<Chunk> chunks_;
+    size_t cur_ = 0;
+};
+
+// Pinned host staging: every host->device upload is first copied here so
+// the caller's buffer may die before the asynchronous copy runs.
+class PinnedArena {
+  public:
+    ~PinnedArena() {
+        for (auto &c : chunks_) (void)hipHostFree(c.base);
+    }
+    uint8_t *alloc(size_t n) {
+        n = (n + 63) & ~size_t(63);
+        for (; cur_ < chunks_.size(); cur_++) {
+            Chunk &c = chunks_[cur_];
+            if (c.used + n <= c.size) {
+                uint8_t *p = c.base + c.used;
+                c.used += n;
+                return p;
+            }
+        }
+        size_t sz = n > (size_t(64) << 20) ? n : (size_t(64) << 20);
+        Chunk c{nullptr, sz, n};
+        FQZ5_HIP(hipHostMalloc(reinterpret_cast<void **>(&c.base), sz, hipHostMallocDefault));
+        chunks_.push_back(c);
+        cur_ = chunks_.size() - 1;
+        return c.base;
+    }
+    void reset() {
+        for (auto &c : chunks_) c.used = 0;
+        cur_ = 0;
+    }
+
+  private:
+    struct Chunk { uint8_t *base; size_t size, used; };
+    std::vector<Chunk> chunks_;
+    size_t cur_ = 0;
+};
+
+struct GpuCtx {
+    hipStream_t stream = nullptr;
+    DevArena arena;
+    PinnedArena staging;
+    int device = 0;
+
+    GpuCtx() {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+            throw GpuError("fqz5: no HIP device visible (this library has no CPU path)");
+        FQZ5_HIP(hipGetDevice(&device));
+        FQZ5_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    }
+    ~GpuCtx() {
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+    void sync() { FQZ5_HIP(hipStreamSynchronize(stream)); }
+
+    template <class T> T *upload(const T *h, size_t n) {
+        T *d = arena.alloc_n<T>(n ? n : 1);
+        if (n) {
+            uint8_t *st = staging.alloc(n * sizeof(T));
+            std::memcpy(st, h, n * sizeof(T));
+            FQZ5_HIP(hipMemcpyAsync(d, st, n * sizeof(T), hipMemcpyHostToDevice, stream));
+        }
+        return d;
+    }
+    // Rewind both arenas; only after everything queued has completed.
+    void reset() {
+        sync();
+        arena.reset();
+        staging.reset();
+    }
+    template <class T> T *upload(const std::vector<T> &v) { return upload(v.data(), v.size()); }
+    template <class T> void download(T *h, const T *d, size_t n) {
+        if (n) FQZ5_HIP(hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, stream));
+    }
+    void memset0(void *d, size_t n) {
+        if (n) FQZ5_HIP(hipMemsetAsync(d, 0, n, stream));
+    }
+};
+
+// The calling thread's context (created on first use).
+GpuCtx &gpu();
+
+}  // namespace fqz5

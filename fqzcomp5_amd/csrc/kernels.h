@@ -1,0 +1,131 @@
+// kernels.h — work descriptors shared by the host planner (rans_codec.cpp)
+// and the gfx950 kernels (rans_kernels.hip).  All pointers are device
+// pointers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace fqz5 {
+
+#define RANS_LOW_D (1u << 15)
+
+// One slice [begin, end) of segment `seg`; counts[seg*512 + 0..255] receive
+// the byte histogram, counts[seg*512 + 256..511] the repeat counts.
+struct HistItem {
+    const uint8_t *data;
+    uint32_t begin, end;
+    uint32_t seg, pad;
+};
+
+// Order-1 pair histogram slice over an A-symbol compacted alphabet.
+struct Hist1Item {
+    const uint8_t *data;
+    const uint8_t *remap;   // 256 entries, byte -> alphabet index
+    uint32_t begin, end;
+    uint32_t A;
+    uint32_t out_off;       // offset (u32 units) of the A*A result block
+};
+
+struct PackItem {
+    const uint8_t *in;
+    uint8_t *out;
+    const uint8_t *code;    // pack: byte -> code; unpack: code -> byte
+    uint32_t n;             // pack: input symbols; unpack: output symbols
+    int32_t per;            // symbols per byte (0, 2, 4, 8)
+};
+
+struct StripeItem {
+    const uint8_t *in;
+    uint8_t *out;
+    uint32_t n, N;
+    int32_t dir;            // 0 transpose, 1 untranspose
+    int32_t pad;
+};
+
+struct CopyItem {
+    const uint8_t *src;
+    uint8_t *dst;
+    uint32_t len;
+    uint32_t pad;
+};
+
+struct EncSym;  // rans_format.hpp
+
+struct EncJob {
+    const uint8_t *in;
+    const EncSym *tab;      // O0: [256]; O1: [A*A] (remap[ctx]*A + remap[sym])
+    const uint8_t *remap;   // O1: byte -> alphabet index
+    uint8_t *out_end;       // 2-byte aligned; stream grows downward
+    uint32_t *out_len;      // bytes written below out_end
+    uint32_t n;
+    int32_t nx;             // 4 or 32
+    int32_t bits;           // 12 (O0) or 10/12 (O1)
+    int32_t A;              // O1 alphabet size
+};
+
+// out[i] = *src[i]: single bytes fetched for host decisions.
+struct GatherItem {
+    const uint8_t *src;
+};
+
+struct DecJob {
+    const uint8_t *in;      // payload: NX states then 16-bit words
+    const uint32_t *tab;    // rows of 2^bits entries; O0 one row, O1 one
+                            // row per context in alphabet order
+    const uint8_t *alpha;   // O1: row index -> byte value
+    uint8_t *out;
+    int32_t *status;
+    uint32_t in_len;
+    uint32_t n;
+    int32_t nx;
+    int32_t bits;
+};
+
+// RLE encode of one leaf input; saved[] marks the RLE symbols.
+struct RleItem {
+    const uint8_t *in;
+    const uint8_t *saved;
+    uint8_t *lits;
+    uint8_t *runs;
+    uint32_t n;
+    uint32_t pad;
+};
+
+// RLE decode: literals + run varints -> nout bytes.
+struct UnRleItem {
+    const uint8_t *lits;
+    const uint8_t *runs;
+    const uint8_t *saved;
+    uint32_t *vend;         // scratch, one entry per varint
+    uint8_t *out;
+    uint32_t nlit, nrun, nvarint, nout;
+};
+
+constexpr uint32_t RLE_CHUNK = 65536;
+
+hipError_t launch_rle_count(const RleItem *items, const uint32_t *chunk_item,
+                            int nchunks, uint32_t *cstat, hipStream_t s);
+hipError_t launch_rle_emit(const RleItem *items, const uint32_t *chunk_item,
+                           int nchunks, const uint32_t *cmeta, hipStream_t s);
+hipError_t launch_unrle_count(const UnRleItem *items, const uint32_t *chunk_item,
+                              int nchunks, uint32_t *cstat, int what, hipStream_t s);
+hipError_t launch_unrle_vend(const UnRleItem *items, const uint32_t *chunk_item,
+                             int nchunks, const uint32_t *coff, hipStream_t s);
+hipError_t launch_unrle_expand(const UnRleItem *items, const uint32_t *chunk_item,
+                               int nchunks, const uint32_t *coff, uint32_t *cstat,
+                               int what, hipStream_t s);
+
+hipError_t launch_gather(const GatherItem *items, int n, uint8_t *out, hipStream_t s);
+hipError_t launch_hist0(const HistItem *d_items, int nitems, uint32_t *d_counts,
+                        hipStream_t s);
+hipError_t launch_hist1(const Hist1Item *d_items, int nitems, uint32_t *d_counts,
+                        hipStream_t s);
+hipError_t launch_pack(const PackItem *d_items, int nitems, uint32_t max_out,
+                       bool unpack, hipStream_t s);
+hipError_t launch_stripe(const StripeItem *d_items, int nitems, uint32_t max_n,
+                         hipStream_t s);
+hipError_t launch_copy(const CopyItem *d_items, int nitems, hipStream_t s);
+hipError_t launch_enc(const EncJob *d_jobs, int njobs, bool o1, hipStream_t s);
+hipError_t launch_dec(const DecJob *d_jobs, int njobs, bool o1, hipStream_t s);
+
+}  // namespace fqz5

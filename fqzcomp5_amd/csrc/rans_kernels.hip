@@ -1,0 +1,733 @@
+// rans_kernels.hip — CDNA4 (gfx950) kernels for the rANS 4x16/32x16 "pr"
+// codecs of htscodecs, as used by fqzcomp5's block encoder.
+//
+// Data-parallel byte work (histograms, bit-packing, stripe transposes,
+// copies) runs one thread per byte/word over many workgroups.  The entropy
+// coder is a set of NX (4 or 32) dependent rANS chains per stream: the
+// format fixes that parallelism (SURVEY.md §7 hard part (i)), so one
+// 64-lane wave owns one stream, lane z owns state z, and all chains of a
+// stream step in lock-step.  Where the reference serialises the 16-bit
+// renormalisation words of the NX states into one stream, the wave uses a
+// ballot + popcount to give each emitting lane its slot:
+//   encode: states emit in descending lane order   (rANS_static4x16pr.c:187-197,
+//                                                    rANS_static32x16pr.c:187-239)
+//   decode: states consume in ascending lane order (rANS_static4x16pr.c:320-327)
+//
+// Step geometry (shared by encoder and decoder, derived from
+// rANS_static4x16pr.c:112-232/:423-518 and rANS_static32x16pr.c:67-525):
+//   O0: step k, lane z handles byte p = NX*k + z        (valid if p < n)
+//   O1: step k, lane z handles byte p = z*isz + k        (valid if k < len_z)
+//       isz = n/NX, len_z = isz except the last lane, which owns the tail.
+// The encoder walks k from T-1 down to 0, the decoder from 0 up to T-1.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "kernels.h"
+#include "rans_format.hpp"
+
+namespace fqz5 {
+
+#define DEV __device__ __forceinline__
+
+static DEV uint32_t lane_id() { return threadIdx.x & 63; }
+
+// ---------------------------------------------------------------------------
+// Histograms (utils.h:146 hist8 and the repeat counts used by rle.c:48
+// rle_find_syms: eq[s] = #{i : d[i] == d[i-1] == s}).
+// One workgroup per work item (segment slice); LDS counters; global atomics.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hist0(const HistItem *items,
+                                               uint32_t *counts) {
+    __shared__ uint32_t h[256], e[256];
+    const HistItem it = items[blockIdx.x];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) { h[i] = 0; e[i] = 0; }
+    __syncthreads();
+    const uint8_t *d = it.data;
+    // 16 bytes per thread per iteration; the previous byte comes from the
+    // neighbouring load (or one extra read at the slice start).
+    uint32_t beg = it.begin, end = it.end;
+    for (uint32_t i = beg + threadIdx.x * 16; i < end; i += blockDim.x * 16) {
+        uint32_t lim = end - i < 16 ? end - i : 16;
+        int prev = i ? d[i - 1] : -1;
+#pragma unroll 4
+        for (uint32_t k = 0; k < lim; k++) {
+            int c = d[i + k];
+            atomicAdd(&h[c], 1u);
+            if (c == prev) atomicAdd(&e[c], 1u);
+            prev = c;
+        }
+    }
+    __syncthreads();
+    uint32_t *out = counts + size_t(it.seg) * 512;
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        if (h[i]) atomicAdd(&out[i], h[i]);
+        if (e[i]) atomicAdd(&out[256 + i], e[i]);
+    }
+}
+
+// Order-1 pair counts F[ctx][sym] over the compacted alphabet
+// (utils.h:280 hist1_4; context of byte 0 is 0).  `remap` maps a byte to
+// its alphabet index (alphabet always contains 0).  A*A <= 16384 bins in
+// LDS, otherwise straight to global memory.
+__global__ __launch_bounds__(256) void k_hist1(const Hist1Item *items,
+                                               uint32_t *counts) {
+    extern __shared__ uint32_t bins[];
+    const Hist1Item it = items[blockIdx.x];
+    const uint32_t A = it.A, nb = A * A;
+    const bool in_lds = nb <= 16384;
+    __shared__ uint8_t rm[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) rm[i] = it.remap[i];
+    if (in_lds)
+        for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) bins[i] = 0;
+    __syncthreads();
+    uint32_t *gout = counts + it.out_off;
+    const uint8_t *d = it.data;
+    for (uint32_t i = it.begin + threadIdx.x; i < it.end; i += blockDim.x) {
+        uint32_t c = rm[d[i]];
+        uint32_t p = i ? rm[d[i - 1]] : rm[0];
+        uint32_t b = p * A + c;
+        if (in_lds) atomicAdd(&bins[b], 1u);
+        else atomicAdd(&gout[b], 1u);
+    }
+    if (in_lds) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x)
+            if (bins[i]) atomicAdd(&gout[i], bins[i]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// PACK (pack.c:56-147): 2/4/8 symbols per byte, low bits first.
+// One thread per output byte.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pack(const PackItem *items) {
+    const PackItem it = items[blockIdx.y];
+    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t nout = (it.n + it.per - 1) / it.per;
+    if (j >= nout) return;
+    const int bits = 8 / it.per;
+    uint32_t i0 = j * it.per;
+    uint32_t v = 0;
+    for (int k = 0; k < it.per; k++) {
+        uint32_t i = i0 + k;
+        if (i < it.n) v |= uint32_t(it.code[it.in[i]]) << (k * bits);
+    }
+    it.out[j] = uint8_t(v);
+}
+
+// Inverse (pack.c:207-344).  One thread per output symbol.
+__global__ __launch_bounds__(256) void k_unpack(const PackItem *items) {
+    const PackItem it = items[blockIdx.y];
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= it.n) return;
+    if (it.per == 0) { it.out[i] = it.code[0]; return; }
+    const int bits = 8 / it.per;
+    uint32_t v = (it.in[i / it.per] >> ((i % it.per) * bits)) & ((1u << bits) - 1);
+    it.out[i] = it.code[v];
+}
+
+// STRIPE (rANS_static4x16pr.c:1283-1309): byte i goes to stripe i%N at
+// offset i/N.  `dir` 0 = transpose (encode), 1 = untranspose (decode,
+// utils.h:79 unstripe).  One thread per byte.
+__global__ __launch_bounds__(256) void k_stripe(const StripeItem *items) {
+    const StripeItem it = items[blockIdx.y];
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= it.n) return;
+    uint32_t s = i % it.N, o = i / it.N;
+    // start of stripe s: stripes < n%N are one longer
+    uint32_t q = it.n / it.N, r = it.n % it.N;
+    uint32_t base = s * q + (s < r ? s : r);
+    if (it.dir == 0) it.out[base + o] = it.in[i];
+    else it.out[i] = it.in[base + o];
+}
+
+__global__ __launch_bounds__(256) void k_gather(const GatherItem *items, int n,
+                                                uint8_t *out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = *items[i].src;
+}
+
+// Gather copies for final stream assembly.  One workgroup per segment
+// chunk of up to 64 KiB.
+__global__ __launch_bounds__(256) void k_copy(const CopyItem *items) {
+    const CopyItem it = items[blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < it.len; i += blockDim.x)
+        it.dst[i] = it.src[i];
+}
+
+// ---------------------------------------------------------------------------
+// Entropy encoder.  One 64-lane workgroup per stream; lanes z < NX are the
+// rANS states.  Encoder symbols (EncSym, rans_format.hpp) come from a table
+// in global memory: O0 tab[sym], O1 tab[ctx*256 + sym].  Symbol bytes and
+// their table entries do not depend on the state, so they are fetched one
+// block of ENC_B steps ahead of the dependent chain.
+//
+// Per step and lane (RansEncPutSymbol, rANS_word.h:287-336):
+//   renorm   x >= f << (31-bits)  => emit low 16 bits, x >>= 16
+//   encode   q = mulhi(x, rcp) >> sh;  x += bias + q * (2^bits - f)
+// Emitted words grow downward from J.out_end; then the states are flushed
+// below them, state 0 lowest (RansEncFlush order NX-1 .. 0).
+// ---------------------------------------------------------------------------
+constexpr int ENC_B = 16;
+
+struct EncLane {
+    uint32_t rcp[ENC_B], info[ENC_B];
+};
+
+template <bool O1>
+static DEV void enc_fetch(const EncJob &J, int z, int nx, uint32_t isz,
+                          uint32_t lenz, int64_t kb, EncLane &L,
+                          const EncSym *__restrict__ tab) {
+#pragma unroll
+    for (int j = 0; j < ENC_B; j++) {
+        int64_t k = kb - j;
+        uint32_t rcp = 0, info = 0;
+        if (k >= 0) {
+            uint32_t p;
+            bool ok;
+            if (O1) { p = z * isz + uint32_t(k); ok = uint32_t(k) < lenz; }
+            else    { p = uint32_t(nx) * uint32_t(k) + z; ok = p < J.n; }
+            if (ok && z < nx) {
+                uint32_t sym = J.in[p];
+                uint32_t idx = O1 ? uint32_t(J.remap[k ? J.in[p - 1] : 0]) * uint32_t(J.A)
+                                        + J.remap[sym]
+                                  : sym;
+                EncSym e = tab[idx];
+                rcp = e.rcp;
+                info = e.info;
+            }
+        }
+        L.rcp[j] = rcp;
+        L.info[j] = info;
+    }
+}
+
+template <bool O1>
+__global__ __launch_bounds__(64) void k_rans_enc(const EncJob *jobs) {
+    const EncJob J = jobs[blockIdx.x];
+    const int z = int(lane_id());
+    const int nx = J.nx;
+    const uint32_t n = J.n;
+    const int bits = J.bits;
+    const uint32_t M = 1u << bits;
+    const uint32_t xs = 31 - bits;            // x_max = (f << xs) - 1
+    const EncSym *__restrict__ tab = J.tab;
+
+    uint32_t isz = n / nx, lenz, T;
+    if (O1) {
+        lenz = (z == nx - 1) ? n - uint32_t(nx - 1) * isz : isz;
+        T = n - uint32_t(nx - 1) * isz;
+    } else {
+        lenz = 0;
+        T = (n + nx - 1) / nx;
+    }
+    const uint64_t lanes = (nx == 64) ? ~0ull : ((1ull << nx) - 1);
+    const uint64_t above = (z >= 63) ? 0ull : (~0ull << (z + 1));
+
+    uint16_t *out16 = reinterpret_cast<uint16_t *>(J.out_end);
+    uint32_t x = RANS_LOW_D;
+    uint32_t nw = 0;   // words emitted so far (wave-uniform)
+
+    EncLane cur, nxt;
+    int64_t kb = int64_t(T) - 1;
+    enc_fetch<O1>(J, z, nx, isz, lenz, kb, cur, tab);
+    for (; kb >= 0; kb -= ENC_B) {
+        enc_fetch<O1>(J, z, nx, isz, lenz, kb - ENC_B, nxt, tab);
+#pragma unroll
+        for (int j = 0; j < ENC_B; j++) {
+            const uint32_t info = cur.info[j];
+            const uint32_t f = info & 0x1fff;
+            const bool act = f != 0;          // inactive lanes / steps carry f = 0
+            const bool c = act && (x >> xs) >= f;
+            const uint64_t m = __ballot(c) & lanes;
+            if (c) {
+                uint32_t rank = __popcll(m & above);
+                out16[-int64_t(nw + rank) - 1] = uint16_t(x);
+                x >>= 16;
+            }
+            nw += __popcll(m);
+            if (act) {
+                const uint32_t q = __umulhi(x, cur.rcp[j]) >> (info >> 26);
+                x += ((info >> 13) & 0x1fff) + q * (M - f);
+            }
+        }
+        cur = nxt;
+    }
+    // flush: state z at bytes [-(2*nw + 4*(nx-z)), +4)
+    if (z < nx) {
+        uint16_t *s = out16 - int64_t(nw) - 2 * int64_t(nx - z);
+        s[0] = uint16_t(x);
+        s[1] = uint16_t(x >> 16);
+    }
+    if (z == 0) *J.out_len = 2 * nw + 4 * uint32_t(nx);
+}
+
+// ---------------------------------------------------------------------------
+// Entropy decoder.  One 64-lane workgroup per stream, lane z = state z.
+// Decode table entries (32 bit): (f-1) << (bits+8) | (slot-start) << 8 | s,
+// rows of 2^bits slots.  O0: one row, s = symbol.  O1: one row per context
+// in alphabet order, s = alphabet index of the symbol (which is also the
+// row of the next step); alpha[s] is the byte written out.
+//   m = x & (2^bits-1); e = row[m]; x = f*(x>>bits) + (m-start)
+//   renorm: if x < 2^15 then x = x<<16 | next word  (RansDecRenorm)
+// Words are consumed in ascending lane order; the compressed words are
+// streamed through an LDS ring one 1 KiB slab ahead of the chain.
+// ---------------------------------------------------------------------------
+constexpr uint32_t RING_WORDS = 4096;       // 8 KiB ring
+constexpr uint32_t SLAB_WORDS = 512;        // 64 lanes x 16 B
+
+template <bool O1>
+__global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
+    __shared__ uint16_t ring[RING_WORDS];
+    const DecJob J = jobs[blockIdx.x];
+    const int z = int(lane_id());
+    const int nx = J.nx;
+    const uint32_t n = J.n;
+    const int bits = J.bits;
+    const uint32_t mask = (1u << bits) - 1;
+    const uint32_t *__restrict__ tab = J.tab;
+
+    // states: 4*nx bytes at the start of the payload
+    uint32_t x = 0;
+    if (z < nx) {
+        const uint8_t *p = J.in + 4 * z;
+        x = p[0] | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+    }
+    const uint8_t *wbase = J.in + 4 * nx;
+    const uint32_t nwords = (J.in_len - 4 * uint32_t(nx)) / 2;
+
+    // slab loader: lane l fetches 16 bytes (8 words) of slab s
+    auto load_slab = [&](uint32_t s) -> uint4 {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        uint32_t w0 = s * SLAB_WORDS + uint32_t(z) * 8;
+        uint32_t tmp[4] = {0, 0, 0, 0};
+        for (int b = 0; b < 8; b++) {
+            uint32_t w = w0 + b;
+            uint32_t val = 0;
+            if (w < nwords) val = wbase[2 * w] | (uint32_t(wbase[2 * w + 1]) << 8);
+            tmp[b >> 1] |= val << ((b & 1) * 16);
+        }
+        v.x = tmp[0]; v.y = tmp[1]; v.z = tmp[2]; v.w = tmp[3];
+        return v;
+    };
+    auto store_slab = [&](uint32_t s, uint4 v) {
+        uint32_t w0 = (s * SLAB_WORDS + uint32_t(z) * 8) & (RING_WORDS - 1);
+        uint32_t *r32 = reinterpret_cast<uint32_t *>(ring + w0);
+        r32[0] = v.x; r32[1] = v.y; r32[2] = v.z; r32[3] = v.w;
+    };
+
+    uint32_t slabs_in_ring = 0;             // slabs written to the ring
+    uint4 pf = load_slab(0);
+    // fill the first two slabs
+    store_slab(0, pf); slabs_in_ring = 1;
+    pf = load_slab(1);
+    store_slab(1, pf); slabs_in_ring = 2;
+    pf = load_slab(2);
+
+    uint32_t isz = n / nx, lenz, T;
+    if (O1) {
+        lenz = (z == nx - 1) ? n - uint32_t(nx - 1) * isz : isz;
+        T = n - uint32_t(nx - 1) * isz;
+    } else {
+        lenz = 0;
+        T = (n + nx - 1) / nx;
+    }
+    const uint64_t lanes = (nx == 64) ? ~0ull : ((1ull << nx) - 1);
+    uint32_t row = 0;                       // O1 context row (previous symbol)
+    uint32_t ptr = 0;                       // words consumed (wave-uniform)
+    const uint32_t G = nx >= 32 ? 8 : 64;   // steps between ring refills
+
+    for (uint32_t t0 = 0; t0 < T; t0 += G) {
+        // keep >= G*nx words + one slab ahead of the read pointer
+        while (slabs_in_ring * SLAB_WORDS < ptr + G * uint32_t(nx) + SLAB_WORDS &&
+               slabs_in_ring * SLAB_WORDS < nwords + SLAB_WORDS) {
+            store_slab(slabs_in_ring, pf);
+            slabs_in_ring++;
+            pf = load_slab(slabs_in_ring);
+        }
+        const uint32_t t1 = (T - t0 < G) ? T : t0 + G;
+        for (uint32_t t = t0; t < t1; t++) {
+            uint32_t p;
+            bool act;
+            if (O1) { p = z * isz + t; act = z < nx && t < lenz; }
+            else    { p = uint32_t(nx) * t + z; act = z < nx && p < n; }
+            bool c = false;
+            if (act) {
+                const uint32_t e = tab[(row << bits) + (x & mask)];
+                const uint32_t f1 = e >> (bits + 8);
+                const uint32_t y = (e >> 8) & mask;
+                const uint32_t xh = x >> bits;
+                x = f1 * xh + xh + y;
+                if (O1) {
+                    row = e & 0xff;                 // alphabet index of the symbol
+                    J.out[p] = J.alpha[row];
+                } else {
+                    J.out[p] = uint8_t(e);
+                }
+                c = x < RANS_LOW_D;
+            }
+            const uint64_t m = __ballot(c) & lanes;
+            if (c) {
+                uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32),
+                                 __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+                uint32_t w = ptr + rank;
+                uint32_t word = (w < nwords) ? ring[w & (RING_WORDS - 1)] : 0u;
+                if (w < nwords) x = (x << 16) | word;
+            }
+            ptr += __popcll(m);
+        }
+    }
+    if (z == 0) *J.status = (ptr <= nwords) ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
+// RLE (rle.c:100-189).  Byte i starts a literal unless it repeats the
+// previous byte and that byte is an RLE symbol; the run length stored for
+// an RLE-symbol literal is the number of repeats that follow it, i.e. the
+// distance to the next literal minus one, as a big-endian varint.
+// Work is cut into chunks of RLE_CH bytes (one 256-thread workgroup each,
+// RLE_PT consecutive bytes per thread).  Pass 1 counts literals and varint
+// bytes per chunk; the host scans the per-chunk totals; pass 2 writes.
+// ---------------------------------------------------------------------------
+constexpr uint32_t RLE_PT = 256;
+constexpr uint32_t RLE_CH = 256 * RLE_PT;
+constexpr uint32_t NONE = 0xffffffffu;
+
+static DEV uint32_t vlen32(uint32_t r) {
+    return 1u + (r >= (1u << 7)) + (r >= (1u << 14)) + (r >= (1u << 21)) + (r >= (1u << 28));
+}
+
+static DEV bool rle_is_lit(const uint8_t *d, uint32_t i, const uint8_t *saved) {
+    return i == 0 || d[i] != d[i - 1] || !saved[d[i]];
+}
+
+// Inclusive block-wide suffix minimum over 256 threads (Hillis-Steele).
+static DEV uint32_t block_suffix_min(uint32_t v, uint32_t *tmp) {
+    const int t = threadIdx.x;
+    tmp[t] = v;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        uint32_t w = (t + o < 256) ? tmp[t + o] : NONE;
+        __syncthreads();
+        v = v < w ? v : w;
+        tmp[t] = v;
+        __syncthreads();
+    }
+    return v;
+}
+
+// Exclusive block-wide prefix sum over 256 threads.
+static DEV uint32_t block_excl_sum(uint32_t v, uint32_t *tmp, uint32_t *total) {
+    const int t = threadIdx.x;
+    tmp[t] = v;
+    __syncthreads();
+    uint32_t acc = v;
+    for (int o = 1; o < 256; o <<= 1) {
+        uint32_t w = (t >= o) ? tmp[t - o] : 0;
+        __syncthreads();
+        acc += w;
+        tmp[t] = acc;
+        __syncthreads();
+    }
+    if (total) *total = tmp[255];
+    __syncthreads();
+    return acc - v;
+}
+
+// Per-thread scan of [a, b): literal count, first/last literal and the
+// varint bytes of every RLE literal whose successor lies inside [a, b).
+struct RleThr { uint32_t cnt, first, last, vsum; };
+
+static DEV RleThr rle_thread_scan(const uint8_t *d, uint32_t a, uint32_t b,
+                                  const uint8_t *saved) {
+    RleThr r{0, NONE, NONE, 0};
+    for (uint32_t i = a; i < b; i++) {
+        if (!rle_is_lit(d, i, saved)) continue;
+        if (r.last != NONE && saved[d[r.last]]) r.vsum += vlen32(i - r.last - 1);
+        if (r.first == NONE) r.first = i;
+        r.last = i;
+        r.cnt++;
+    }
+    return r;
+}
+
+// Pass 1: per chunk {lit count, first lit, last lit, varint bytes excluding
+// the chunk's last literal, whether that literal is an RLE symbol}.
+__global__ __launch_bounds__(256) void k_rle_count(const RleItem *items,
+                                                   const uint32_t *chunk_item,
+                                                   uint32_t *cstat) {
+    __shared__ uint32_t tmp[256];
+    __shared__ uint8_t saved[256];
+    const uint32_t c = blockIdx.x;
+    const RleItem it = items[chunk_item[2 * c]];
+    const uint32_t lc = chunk_item[2 * c + 1];
+    saved[threadIdx.x] = it.saved[threadIdx.x];
+    __syncthreads();
+    const uint32_t c0 = lc * RLE_CH, c1 = min(it.n, c0 + RLE_CH);
+    const uint32_t a = min(c1, c0 + threadIdx.x * RLE_PT), b = min(c1, a + RLE_PT);
+    RleThr r = rle_thread_scan(it.in, a, b, saved);
+    // successor of my last literal inside the chunk = first literal of a later thread
+    // suffix minimum of first-literal positions over the threads after me
+    block_suffix_min(r.first, tmp);
+    uint32_t later = (threadIdx.x < 255) ? tmp[threadIdx.x + 1] : NONE;
+    __syncthreads();
+    uint32_t vs = r.vsum;
+    if (r.last != NONE && later != NONE && saved[it.in[r.last]])
+        vs += vlen32(later - r.last - 1);
+    uint32_t tot_cnt, tot_vs;
+    block_excl_sum(r.cnt, tmp, &tot_cnt);
+    block_excl_sum(vs, tmp, &tot_vs);
+    // chunk first / last literal
+    __shared__ uint32_t cf, cl1;           // first literal, last literal + 1
+    if (threadIdx.x == 0) { cf = NONE; cl1 = 0; }
+    __syncthreads();
+    if (r.first != NONE) atomicMin(&cf, r.first);
+    if (r.last != NONE) atomicMax(&cl1, r.last + 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t *o = cstat + 5 * c;
+        o[0] = tot_cnt; o[1] = cf; o[2] = cl1 ? cl1 - 1 : NONE; o[3] = tot_vs;
+        o[4] = cl1 ? saved[it.in[cl1 - 1]] : 0;
+    }
+}
+
+// Pass 2: write literals and varints.  cmeta per chunk: {lit_off,
+// run_off, next literal after the chunk (or n)}.
+__global__ __launch_bounds__(256) void k_rle_emit(const RleItem *items,
+                                                  const uint32_t *chunk_item,
+                                                  const uint32_t *cmeta) {
+    __shared__ uint32_t tmp[256];
+    __shared__ uint8_t saved[256];
+    const uint32_t c = blockIdx.x;
+    const RleItem it = items[chunk_item[2 * c]];
+    const uint32_t lc = chunk_item[2 * c + 1];
+    saved[threadIdx.x] = it.saved[threadIdx.x];
+    __syncthreads();
+    const uint32_t c0 = lc * RLE_CH, c1 = min(it.n, c0 + RLE_CH);
+    const uint32_t a = min(c1, c0 + threadIdx.x * RLE_PT), b = min(c1, a + RLE_PT);
+    const uint32_t lit_off = cmeta[3 * c], run_off = cmeta[3 * c + 1],
+                   chunk_next = cmeta[3 * c + 2];
+    RleThr r = rle_thread_scan(it.in, a, b, saved);
+    // successor of this thread's last literal
+    block_suffix_min(r.first, tmp);
+    uint32_t later = (threadIdx.x < 255) ? tmp[threadIdx.x + 1] : NONE;
+    __syncthreads();
+    if (later == NONE) later = chunk_next;
+    uint32_t vs = r.vsum;
+    if (r.last != NONE && saved[it.in[r.last]]) vs += vlen32(later - r.last - 1);
+    uint32_t lo = block_excl_sum(r.cnt, tmp, nullptr) + lit_off;
+    uint32_t ro = block_excl_sum(vs, tmp, nullptr) + run_off;
+    // sequential write of this thread's literals and run varints
+    uint32_t prev = NONE;
+    auto put_run = [&](uint32_t rl) {
+        int nb = int(vlen32(rl));
+        for (int k = nb - 1; k >= 0; k--)
+            it.runs[ro++] = uint8_t(((rl >> (7 * k)) & 0x7f) | (k ? 0x80 : 0));
+    };
+    for (uint32_t i = a; i < b; i++) {
+        if (!rle_is_lit(it.in, i, saved)) continue;
+        if (prev != NONE && saved[it.in[prev]]) put_run(i - prev - 1);
+        it.lits[lo++] = it.in[i];
+        prev = i;
+    }
+    if (prev != NONE && saved[it.in[prev]]) put_run(later - prev - 1);
+}
+
+// ---------------------------------------------------------------------------
+// RLE decode (rle.c:142-189), three passes over chunks of literals:
+//   1. per chunk: number of RLE-symbol literals                (host scans)
+//   2. per chunk of run bytes: positions of varint terminators  (host scans)
+//      -> vend[k] = byte index of the last byte of varint k
+//   3. per chunk of literals: run lengths -> output sizes       (host scans)
+//   4. per chunk of literals: write the expanded bytes
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_unrle_count(const UnRleItem *items,
+                                                     const uint32_t *chunk_item,
+                                                     uint32_t *cstat, int what) {
+    __shared__ uint32_t tmp[256];
+    __shared__ uint8_t saved[256];
+    const uint32_t c = blockIdx.x;
+    const UnRleItem it = items[chunk_item[2 * c]];
+    const uint32_t lc = chunk_item[2 * c + 1];
+    saved[threadIdx.x] = it.saved[threadIdx.x];
+    __syncthreads();
+    uint32_t cnt = 0;
+    if (what == 0) {            // RLE literals per chunk of literals
+        const uint32_t c0 = lc * RLE_CH, c1 = min(it.nlit, c0 + RLE_CH);
+        const uint32_t a = min(c1, c0 + threadIdx.x * RLE_PT), b = min(c1, a + RLE_PT);
+        for (uint32_t i = a; i < b; i++) cnt += saved[it.lits[i]];
+    } else {                    // varint terminators per chunk of run bytes
+        const uint32_t c0 = lc * RLE_CH, c1 = min(it.nrun, c0 + RLE_CH);
+        const uint32_t a = min(c1, c0 + threadIdx.x * RLE_PT), b = min(c1, a + RLE_PT);
+        for (uint32_t i = a; i < b; i++) cnt += !(it.runs[i] & 0x80);
+    }
+    uint32_t tot;
+    block_excl_sum(cnt, tmp, &tot);
+    if (threadIdx.x == 0) cstat[c] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_unrle_vend(const UnRleItem *items,
+                                                    const uint32_t *chunk_item,
+                                                    const uint32_t *coff) {
+    __shared__ uint32_t tmp[256];
+    const uint32_t c = blockIdx.x;
+    const UnRleItem it = items[chunk_item[2 * c]];
+    const uint32_t lc = chunk_item[2 * c + 1];
+    const uint32_t c0 = lc * RLE_CH, c1 = min(it.nrun, c0 + RLE_CH);
+    const uint32_t a = min(c1, c0 + threadIdx.x * RLE_PT), b = min(c1, a + RLE_PT);
+    uint32_t cnt = 0;
+    for (uint32_t i = a; i < b; i++) cnt += !(it.runs[i] & 0x80);
+    uint32_t k = block_excl_sum(cnt, tmp, nullptr) + coff[c];
+    for (uint32_t i = a; i < b; i++)
+        if (!(it.runs[i] & 0x80)) it.vend[k++] = i;
+}
+
+static DEV uint32_t unrle_run(const UnRleItem &it, uint32_t k) {
+    // varint k spans (vend[k-1], vend[k]]
+    uint32_t s = k ? it.vend[k - 1] + 1 : 0, e = it.vend[k];
+    uint32_t v = 0;
+    for (uint32_t i = s; i <= e; i++) v = (v << 7) | (it.runs[i] & 0x7f);
+    return v;
+}
+
+// what 0: per chunk output length; what 1: write.  coff: {rle-literal
+// offset, output offset} per chunk.
+__global__ __launch_bounds__(256) void k_unrle_expand(const UnRleItem *items,
+                                                      const uint32_t *chunk_item,
+                                                      const uint32_t *coff,
+                                                      uint32_t *cstat, int what) {
+    __shared__ uint32_t tmp[256];
+    __shared__ uint8_t saved[256];
+    const uint32_t c = blockIdx.x;
+    const UnRleItem it = items[chunk_item[2 * c]];
+    const uint32_t lc = chunk_item[2 * c + 1];
+    saved[threadIdx.x] = it.saved[threadIdx.x];
+    __syncthreads();
+    const uint32_t c0 = lc * RLE_CH, c1 = min(it.nlit, c0 + RLE_CH);
+    const uint32_t a = min(c1, c0 + threadIdx.x * RLE_PT), b = min(c1, a + RLE_PT);
+    uint32_t ns = 0;
+    for (uint32_t i = a; i < b; i++) ns += saved[it.lits[i]];
+    uint32_t k = block_excl_sum(ns, tmp, nullptr) + coff[2 * c];
+    uint32_t olen = 0, k0 = k;
+    for (uint32_t i = a; i < b; i++) {
+        uint32_t r = 0;
+        if (saved[it.lits[i]]) { r = k < it.nvarint ? unrle_run(it, k) : 0; k++; }
+        olen += r + 1;
+    }
+    uint32_t tot;
+    uint32_t o = block_excl_sum(olen, tmp, &tot) + coff[2 * c + 1];
+    if (what == 0) {
+        if (threadIdx.x == 0) cstat[c] = tot;
+        return;
+    }
+    k = k0;
+    for (uint32_t i = a; i < b; i++) {
+        uint32_t r = 0;
+        uint8_t ch = it.lits[i];
+        if (saved[ch]) { r = k < it.nvarint ? unrle_run(it, k) : 0; k++; }
+        for (uint32_t j = 0; j <= r; j++)
+            if (o + j < it.nout) it.out[o + j] = ch;
+        o += r + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_gather(const GatherItem *items, int n, uint8_t *out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_gather, dim3((n + 255) / 256), dim3(256), 0, s, items, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_hist0(const HistItem *d_items, int nitems, uint32_t *d_counts,
+                        hipStream_t s) {
+    if (!nitems) return hipSuccess;
+    hipLaunchKernelGGL(k_hist0, dim3(nitems), dim3(256), 0, s, d_items, d_counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_hist1(const Hist1Item *d_items, int nitems, uint32_t *d_counts,
+                        hipStream_t s) {
+    if (!nitems) return hipSuccess;
+    hipLaunchKernelGGL(k_hist1, dim3(nitems), dim3(256), 16384 * 4, s, d_items,
+                       d_counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack(const PackItem *d_items, int nitems, uint32_t max_out,
+                       bool unpack, hipStream_t s) {
+    if (!nitems || !max_out) return hipSuccess;
+    dim3 g((max_out + 255) / 256, nitems);
+    if (unpack) hipLaunchKernelGGL(k_unpack, g, dim3(256), 0, s, d_items);
+    else hipLaunchKernelGGL(k_pack, g, dim3(256), 0, s, d_items);
+    return hipGetLastError();
+}
+
+hipError_t launch_stripe(const StripeItem *d_items, int nitems, uint32_t max_n,
+                         hipStream_t s) {
+    if (!nitems || !max_n) return hipSuccess;
+    dim3 g((max_n + 255) / 256, nitems);
+    hipLaunchKernelGGL(k_stripe, g, dim3(256), 0, s, d_items);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy(const CopyItem *d_items, int nitems, hipStream_t s) {
+    if (!nitems) return hipSuccess;
+    hipLaunchKernelGGL(k_copy, dim3(nitems), dim3(256), 0, s, d_items);
+    return hipGetLastError();
+}
+
+hipError_t launch_enc(const EncJob *d_jobs, int njobs, bool o1, hipStream_t s) {
+    if (!njobs) return hipSuccess;
+    if (o1) hipLaunchKernelGGL(k_rans_enc<true>, dim3(njobs), dim3(64), 0, s, d_jobs);
+    else    hipLaunchKernelGGL(k_rans_enc<false>, dim3(njobs), dim3(64), 0, s, d_jobs);
+    return hipGetLastError();
+}
+
+hipError_t launch_dec(const DecJob *d_jobs, int njobs, bool o1, hipStream_t s) {
+    if (!njobs) return hipSuccess;
+    if (o1) hipLaunchKernelGGL(k_rans_dec<true>, dim3(njobs), dim3(64), 0, s, d_jobs);
+    else    hipLaunchKernelGGL(k_rans_dec<false>, dim3(njobs), dim3(64), 0, s, d_jobs);
+    return hipGetLastError();
+}
+
+hipError_t launch_rle_count(const RleItem *items, const uint32_t *chunk_item,
+                            int nchunks, uint32_t *cstat, hipStream_t s) {
+    if (!nchunks) return hipSuccess;
+    hipLaunchKernelGGL(k_rle_count, dim3(nchunks), dim3(256), 0, s, items, chunk_item, cstat);
+    return hipGetLastError();
+}
+
+hipError_t launch_rle_emit(const RleItem *items, const uint32_t *chunk_item,
+                           int nchunks, const uint32_t *cmeta, hipStream_t s) {
+    if (!nchunks) return hipSuccess;
+    hipLaunchKernelGGL(k_rle_emit, dim3(nchunks), dim3(256), 0, s, items, chunk_item, cmeta);
+    return hipGetLastError();
+}
+
+hipError_t launch_unrle_count(const UnRleItem *items, const uint32_t *chunk_item,
+                              int nchunks, uint32_t *cstat, int what, hipStream_t s) {
+    if (!nchunks) return hipSuccess;
+    hipLaunchKernelGGL(k_unrle_count, dim3(nchunks), dim3(256), 0, s, items, chunk_item,
+                       cstat, what);
+    return hipGetLastError();
+}
+
+hipError_t launch_unrle_vend(const UnRleItem *items, const uint32_t *chunk_item,
+                             int nchunks, const uint32_t *coff, hipStream_t s) {
+    if (!nchunks) return hipSuccess;
+    hipLaunchKernelGGL(k_unrle_vend, dim3(nchunks), dim3(256), 0, s, items, chunk_item, coff);
+    return hipGetLastError();
+}
+
+hipError_t launch_unrle_expand(const UnRleItem *items, const uint32_t *chunk_item,
+                               int nchunks, const uint32_t *coff, uint32_t *cstat,
+                               int what, hipStream_t s) {
+    if (!nchunks) return hipSuccess;
+    hipLaunchKernelGGL(k_unrle_expand, dim3(nchunks), dim3(256), 0, s, items, chunk_item,
+                       coff, cstat, what);
+    return hipGetLastError();
+}
+
+}  // namespace fqz5

@@ -1,0 +1,146 @@
+"""ctypes binding of libfqz5_mi355x.so (include/fqz5_mi355x.h).
+
+This is the only way the Python side reaches the codec: every call goes to
+the HIP library.  There is no fallback — if the library or a GPU is missing
+the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfqz5_mi355x.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "fqz5_mi355x.h")
+
+_libc = C.CDLL(None)
+_libc.free.argtypes = [C.c_void_p]
+
+
+class RansJob(C.Structure):
+    _fields_ = [("in_", C.c_void_p), ("out", C.c_void_p),
+                ("in_size", C.c_uint32), ("out_cap", C.c_uint32),
+                ("order", C.c_int32), ("out_size", C.c_uint32),
+                ("status", C.c_int32), ("pad", C.c_int32)]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load the native library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f"{LIB_PATH} missing: run __graft_entry__.build()")
+    lib = C.CDLL(LIB_PATH)
+    lib.rans_compress_bound_4x16.restype = C.c_uint
+    lib.rans_compress_bound_4x16.argtypes = [C.c_uint, C.c_int]
+    lib.rans_compress_to_4x16.restype = C.c_void_p
+    lib.rans_compress_to_4x16.argtypes = [C.c_char_p, C.c_uint, C.c_void_p,
+                                          C.POINTER(C.c_uint), C.c_int]
+    lib.rans_compress_4x16.restype = C.c_void_p
+    lib.rans_compress_4x16.argtypes = [C.c_char_p, C.c_uint,
+                                       C.POINTER(C.c_uint), C.c_int]
+    lib.rans_uncompress_to_4x16.restype = C.c_void_p
+    lib.rans_uncompress_to_4x16.argtypes = [C.c_char_p, C.c_uint, C.c_void_p,
+                                            C.POINTER(C.c_uint)]
+    lib.rans_uncompress_4x16.restype = C.c_void_p
+    lib.rans_uncompress_4x16.argtypes = [C.c_char_p, C.c_uint,
+                                         C.POINTER(C.c_uint)]
+    lib.fqz5_rans_compress_batch.restype = C.c_int
+    lib.fqz5_rans_compress_batch.argtypes = [C.POINTER(RansJob), C.c_int]
+    lib.fqz5_rans_uncompress_batch.restype = C.c_int
+    lib.fqz5_rans_uncompress_batch.argtypes = [C.POINTER(RansJob), C.c_int]
+    lib.fqz5_stream.restype = C.c_void_p
+    lib.fqz5_device_ok.restype = C.c_int
+    lib.fqz5_last_error.restype = C.c_char_p
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().fqz5_last_error().decode()
+
+
+def device_ok() -> bool:
+    return bool(load().fqz5_device_ok())
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/fqz5_mi355x.h."""
+    import re
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b([a-z_0-9]+)\s*\(", txt))
+                  - {"if", "sizeof", "return"})
+
+
+def compress_bound(n: int, order: int) -> int:
+    return load().rans_compress_bound_4x16(n, order)
+
+
+def rans_compress(data: bytes, order: int) -> bytes:
+    """rans_compress_4x16 on the GPU (host buffers)."""
+    lib = load()
+    n = C.c_uint(0)
+    p = lib.rans_compress_4x16(bytes(data), len(data), C.byref(n), order)
+    if not p:
+        raise NativeError("rans_compress_4x16 failed: " + last_error())
+    out = C.string_at(p, n.value)
+    _libc.free(p)
+    return out
+
+
+def rans_compress_to(data: bytes, order: int, cap: int) -> bytes | None:
+    """rans_compress_to_4x16 with a caller buffer of `cap` bytes."""
+    lib = load()
+    buf = C.create_string_buffer(max(cap, 1))
+    n = C.c_uint(cap)
+    p = lib.rans_compress_to_4x16(bytes(data), len(data), buf, C.byref(n),
+                                  order)
+    if not p:
+        return None
+    return buf.raw[:n.value]
+
+
+def rans_uncompress(comp: bytes) -> bytes:
+    lib = load()
+    n = C.c_uint(0)
+    p = lib.rans_uncompress_4x16(bytes(comp), len(comp), C.byref(n))
+    if not p:
+        raise NativeError("rans_uncompress_4x16 failed: " + last_error())
+    out = C.string_at(p, n.value)
+    _libc.free(p)
+    return out
+
+
+def rans_uncompress_to(comp: bytes, size: int) -> bytes | None:
+    lib = load()
+    buf = C.create_string_buffer(max(size, 1))
+    n = C.c_uint(size)
+    p = lib.rans_uncompress_to_4x16(bytes(comp), len(comp), buf, C.byref(n))
+    if not p:
+        return None
+    return buf.raw[:n.value]
+
+
+def compress_batch_dev(jobs: list[RansJob]) -> None:
+    arr = (RansJob * len(jobs))(*jobs)
+    if load().fqz5_rans_compress_batch(arr, len(jobs)) != 0:
+        raise NativeError("fqz5_rans_compress_batch: " + last_error())
+    for i, j in enumerate(jobs):
+        j.out_size, j.status = arr[i].out_size, arr[i].status
+
+
+def uncompress_batch_dev(jobs: list[RansJob]) -> None:
+    arr = (RansJob * len(jobs))(*jobs)
+    if load().fqz5_rans_uncompress_batch(arr, len(jobs)) != 0:
+        raise NativeError("fqz5_rans_uncompress_batch: " + last_error())
+    for i, j in enumerate(jobs):
+        j.out_size, j.status = arr[i].out_size, arr[i].status

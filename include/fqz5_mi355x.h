@@ -1,0 +1,87 @@
+/*
+ * fqz5_mi355x.h — C-ABI of the MI355X-native fqzcomp5 block codec.
+ *
+ * Part 1 re-exports the htscodecs entry points that fqzcomp5 binds, with
+ * identical names, argument meaning, ownership and error behaviour, so a
+ * fqzcomp5 build links this library in place of htscodecs' CPU objects:
+ *   rANS 4x16/32x16  /root/reference/htscodecs/rANS_static4x16.h:41-66
+ * (fqz_compress / arith_compress_to follow in later rounds; see DESIGN.md.)
+ *
+ * Part 2 is the batched, device-resident API used by the block codec and
+ * the benchmark: many streams per call, inputs and outputs in HBM.
+ *
+ * Every entry point runs its byte work on the GPU.  There is no CPU path:
+ * without a visible HIP device the calls fail (NULL / negative status) and
+ * fqz5_last_error() says why.
+ */
+#ifndef FQZ5_MI355X_H
+#define FQZ5_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- Part 1: htscodecs drop-in (rANS_static4x16.h:41-66) -------------- */
+
+/* Replaces rans_compress_bound_4x16 (rANS_static4x16pr.c:93). */
+unsigned int rans_compress_bound_4x16(unsigned int size, int order);
+
+/* Replaces rans_compress_to_4x16 (rANS_static4x16pr.c:1224).
+ * out == NULL: a buffer of rans_compress_bound_4x16() bytes is malloc()ed
+ * and returned (caller free()s).  Otherwise *out_size is the capacity on
+ * entry and the used size on return.  NULL and *out_size = 0 on failure. */
+unsigned char *rans_compress_to_4x16(unsigned char *in, unsigned int in_size,
+                                     unsigned char *out, unsigned int *out_size,
+                                     int order);
+
+/* Replaces rans_compress_4x16 (rANS_static4x16pr.c:1602). */
+unsigned char *rans_compress_4x16(unsigned char *in, unsigned int in_size,
+                                  unsigned int *out_size, int order);
+
+/* Replaces rans_uncompress_to_4x16 (rANS_static4x16pr.c:1607). */
+unsigned char *rans_uncompress_to_4x16(unsigned char *in, unsigned int in_size,
+                                       unsigned char *out, unsigned int *out_size);
+
+/* Replaces rans_uncompress_4x16 (rANS_static4x16pr.c:1896). */
+unsigned char *rans_uncompress_4x16(unsigned char *in, unsigned int in_size,
+                                    unsigned int *out_size);
+
+/* Replaces rans_set_cpu (rANS_static4x16pr.c:1212).  Accepted and ignored:
+ * the GPU kernels produce the same bytes as every reference CPU variant. */
+void rans_set_cpu(int opts);
+
+/* ---- Part 2: batched device API --------------------------------------- */
+
+/* One stream.  `in`/`out` are device pointers. */
+typedef struct {
+    const uint8_t *in;
+    uint8_t *out;
+    uint32_t in_size;
+    uint32_t out_cap;    /* compress: capacity (0 = bound); decompress: size */
+    int32_t order;       /* compress only: htscodecs order word */
+    uint32_t out_size;   /* result */
+    int32_t status;      /* result: 0 ok, -1 failed (reference NULL) */
+    int32_t pad;
+} fqz5_rans_job;
+
+/* Compress / decompress `n` streams in one batch on the calling thread's
+ * GPU context; returns 0, or -1 on a device error (see fqz5_last_error). */
+int fqz5_rans_compress_batch(fqz5_rans_job *jobs, int n);
+int fqz5_rans_uncompress_batch(fqz5_rans_job *jobs, int n);
+
+/* HIP stream (hipStream_t) that the calling thread's batches run on. */
+void *fqz5_stream(void);
+
+/* 1 if a HIP device is usable, else 0 (and fqz5_last_error() is set). */
+int fqz5_device_ok(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char *fqz5_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,31 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line(
+        "markers", "gpu: needs an MI355X (run on the GPU box via gpurun)")
+
+
+@pytest.fixture(scope="session")
+def golden_rans():
+    """The reference-generated rANS vectors (tests/golden/make_golden.py)."""
+    import json
+    g = os.path.join(ROOT, "tests", "golden")
+    man = json.load(open(os.path.join(g, "rans.json")))
+    blob_in = open(os.path.join(g, "rans_inputs.bin"), "rb").read()
+    blob_out = open(os.path.join(g, "rans_outputs.bin"), "rb").read()
+    inputs = {k: blob_in[o:o + n] for k, (o, n, _) in man["inputs"].items()}
+    cases = []
+    for c in man["cases"]:
+        exp = None
+        if "off" in c:
+            exp = blob_out[c["off"]:c["off"] + c["len"]]
+        cases.append((c["input"], c["order"], c["len"], c["md5"], exp))
+    return inputs, cases

@@ -1,0 +1,118 @@
+"""GPU parity: the HIP rANS path through the C-ABI against the reference's
+golden vectors and the oracle (bit-exact), plus round trips."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from fqzcomp5_amd import lib
+from oracle import binding
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not lib.device_ok():
+        pytest.fail("no GPU: " + lib.last_error())
+
+
+def test_golden_compress(golden_rans):
+    inputs, cases = golden_rans
+    bad = []
+    for name, order, ln, md5, exp in cases:
+        out = lib.rans_compress(inputs[name], order)
+        if hashlib.md5(out).hexdigest() != md5:
+            bad.append((name, hex(order), len(out), ln))
+    assert not bad, f"{len(bad)} mismatches: {bad[:25]}"
+
+
+def test_golden_decompress(golden_rans):
+    inputs, cases = golden_rans
+    bad = []
+    for name, order, ln, md5, exp in cases:
+        if exp is None:
+            continue
+        try:
+            back = lib.rans_uncompress(exp)
+        except lib.NativeError as e:
+            bad.append((name, hex(order), str(e)[:80]))
+            continue
+        if back != inputs[name]:
+            bad.append((name, hex(order), "mismatch"))
+    assert not bad, f"{len(bad)} failures: {bad[:25]}"
+
+
+def _rand_case(rng, it):
+    n = int(rng.choice([rng.integers(0, 64), rng.integers(0, 4000),
+                        rng.integers(0, 300000)]))
+    k = it % 5
+    if k == 0:
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+    elif k == 1:
+        d = (rng.integers(0, 1 + it % 17, n) + 30).astype(np.uint8)
+    elif k == 2:
+        d = np.repeat(rng.integers(0, 4, n), rng.integers(1, 25, n))[:n]
+    elif k == 3:
+        d = np.minimum(rng.zipf(1.4, n), 255)
+    else:
+        d = rng.choice(np.array([2, 12, 23, 37]), n, p=[.01, .04, .1, .85])
+    o = int(rng.choice([0, 1, 4, 5, 64, 65, 68, 69, 128, 129, 132, 133,
+                        192, 193, 196, 197]))
+    if it % 6 == 0:
+        o = (int(rng.integers(1, 300)) << 8) | int(rng.choice([8, 9, 13]))
+    return d.astype(np.uint8).tobytes(), o
+
+
+def test_random_vs_oracle():
+    ora = binding.oracle()
+    rng = np.random.default_rng(2024)
+    bad = []
+    for it in range(150):
+        d, o = _rand_case(rng, it)
+        exp = ora.rans_compress(d, o)
+        got = lib.rans_compress(d, o)
+        if got != exp:
+            bad.append((len(d), hex(o), len(got), len(exp)))
+            continue
+        if lib.rans_uncompress(got) != d:
+            bad.append((len(d), hex(o), "roundtrip"))
+    assert not bad, bad[:20]
+
+
+def test_capacity_semantics_vs_oracle():
+    """rans_compress_to_4x16 with tight caller buffers fails exactly when
+    the reference does."""
+    ora = binding.oracle()
+    rng = np.random.default_rng(7)
+    import ctypes as C
+    olib = ora.lib
+    olib.ora_rans_compress_to_4x16.restype = C.c_void_p
+    olib.ora_rans_compress_to_4x16.argtypes = [C.c_char_p, C.c_uint, C.c_void_p,
+                                               C.POINTER(C.c_uint), C.c_int]
+    for it in range(60):
+        d, o = _rand_case(rng, it)
+        if len(d) > 20000:
+            d = d[:20000]
+        full = ora.rans_compress(d, o)
+        for cap in (len(full), len(full) - 1, len(full) + 3, 1,
+                    lib.compress_bound(len(d), o) // 2):
+            if cap <= 0:
+                continue
+            buf = C.create_string_buffer(cap)
+            n = C.c_uint(cap)
+            p = olib.ora_rans_compress_to_4x16(d, len(d), buf, C.byref(n), o)
+            exp = buf.raw[:n.value] if p else None
+            got = lib.rans_compress_to(d, o, cap)
+            assert got == exp, (len(d), hex(o), cap)
+
+
+def test_large_q40_roundtrip():
+    from fqzcomp5_amd import synth
+    r = synth.illumina(20000, seed=3, binned=False)
+    q = r.qual.tobytes()
+    ora = binding.oracle()
+    for o in (0, 1, 129, 193, (150 << 8) | 9):
+        got = lib.rans_compress(q, o)
+        assert got == ora.rans_compress(q, o), hex(o)
+        assert lib.rans_uncompress(got) == q
