@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Benchmark: fqzcomp5 -3 sequence+quality section coding on MI355X.
+
+Metric (BASELINE.json): input MB/s encode+decode, 100 MB blocks, -3;
+bit-exact vs CPU.  Workload (configs[1]): a synthetic 1 GB Illumina 150 bp
+FASTQ with 8-level binned qualities, split into 100 MB blocks by the
+reference's record rule (fqzcomp5.c:471-477).  One step is one pass of the
+hot path over the whole workload, inputs resident in HBM:
+
+    encode  every block's seq and qual section with the -3 rANS method sets
+            and the codec-trial state machine (fqzcomp5.c:1899-2144)
+    decode  every chosen stream back to bytes.
+
+`value` = seq+qual section bytes of all ranks / step time (max over ranks).
+Names (tok3/LZP) and LZP3 for sequences are the next rows of SURVEY §8f
+and are not in the workload.  Multi-GPU: one process per GPU, weak scaling
+(each rank adds its own 1 GB file to the run); the only collective is the
+all-gather of candidate sizes that the trial state needs.
+
+Also reported: the roofline of the dominant kernel from live HIP events on
+the library's stream, and the reference CPU path (oracle/_ref, compiled
+from the reference sources) timed on the host cores on the same bytes,
+whose output bytes are compared with the GPU's.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FASTQ_REC = 346          # bytes per synthetic 150 bp FASTQ record (avg)
+BLK = 100_000_000        # -3 block size (fqzcomp5.c:4913)
+HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8 TB/s spec
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def make_blocks(gb: float, seed: int):
+    from fqzcomp5_amd import synth
+    n_reads = int(gb * 1e9 / FASTQ_REC)
+    r = synth.illumina(n_reads, seed=seed)
+    return r, synth.split_blocks(r, BLK)
+
+
+def method_order(m: int, fixed_len: int) -> int:
+    return [0, 1, 64, 65, 128, 129, 192, 193][m - 1] if m <= 8 else (fixed_len << 8) + 9
+
+
+def cpu_baseline(host_secs, tried, meth, gpu_out, threads):
+    """The reference (oracle/_ref) on the same sections and schedule: every
+    tried method of every section is compressed, the chosen stream is
+    checked against the GPU's bytes and decoded again."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import binding
+    kind = "reference" if binding.have_ref() else "port"
+    codec = binding.ref() if kind == "reference" else binding.oracle()
+
+    def enc(i):
+        data, fixed = host_secs[i]
+        best = None
+        for m in range(1, 31):
+            if tried[i] & (1 << m) and (m != 9 or fixed):
+                out = codec.rans_compress(data, method_order(m, fixed))
+                if m == meth[i]:
+                    best = out
+        return best
+
+    with ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        chosen = list(ex.map(enc, range(len(host_secs))))
+        t1 = time.perf_counter()
+        back = list(ex.map(codec.rans_uncompress, chosen))
+        t2 = time.perf_counter()
+    same = all(c == g for c, g in zip(chosen, gpu_out))
+    rt = all(b == h[0] for b, h in zip(back, host_secs))
+    nbytes = sum(len(h[0]) for h in host_secs)
+    return {"value": round(nbytes / (t2 - t0) / 1e6, 2), "unit": "MB/s",
+            "cores": threads, "kind": kind,
+            "sample": f"all {len(host_secs)} seq+qual sections of the rank-0 "
+                      f"workload, the -t1 trial schedule (every tried "
+                      f"candidate encoded), {threads} host threads",
+            "enc_s": round(t1 - t0, 3), "dec_s": round(t2 - t1, 3),
+            "bytes_match_gpu": bool(same), "roundtrip": bool(rt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--gb", type=float, default=1.0)
+    ap.add_argument("--level", type=int, default=3)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from fqzcomp5_amd import lib, sections as S
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if not lib.device_ok():
+        raise SystemExit("no GPU: " + lib.last_error())
+
+    t0 = time.time()
+    reads, blocks = make_blocks(args.gb, seed=1 + rank)
+    log(f"[bench] generated {len(blocks)} blocks/rank in {time.time()-t0:.1f}s")
+    fixed = reads.fixed_len
+    offs = np.concatenate([[0], np.cumsum(reads.lens.astype(np.int64))])
+    dev = torch.device("cuda", local)
+    seq_d = torch.from_numpy(reads.seq).to(dev)
+    qual_d = torch.from_numpy(reads.qual).to(dev)
+
+    # sections in file order: per block seq then qual (encode_block order)
+    spans = []
+    for a, b in blocks:
+        s, e = int(offs[a]), int(offs[b])
+        fl = int(reads.lens[a]) if np.all(reads.lens[a:b] == reads.lens[a]) else 0
+        spans.append((S.SEC_SEQ, s, e, fl))
+        spans.append((S.SEC_QUAL, s, e, fl))
+    caps = [9 + max(lib.compress_bound(e - s, method_order(m, fl))
+                    for m in range(1, 10)) for _, s, e, fl in spans]
+    enc_buf = torch.empty(sum(caps), dtype=torch.uint8, device=dev)
+    dec_buf = torch.empty(sum(e - s for _, s, e, _ in spans), dtype=torch.uint8, device=dev)
+    enc_secs, dec_out = [], []
+    eo = do = 0
+    for (sec, s, e, fl), cap in zip(spans, caps):
+        src = seq_d if sec == S.SEC_SEQ else qual_d
+        enc_secs.append(S.Section(src.data_ptr() + s, enc_buf.data_ptr() + eo,
+                                  e - s, cap, fl, sec))
+        dec_out.append((dec_buf.data_ptr() + do, e - s, eo, cap))
+        eo += cap
+        do += e - s
+    avail = S.masks(args.level)
+    in_bytes_local = sum(e - s for _, s, e, _ in spans)
+
+    def step():
+        state = S.new_state()
+        res, meth_all, sizes, tried, off = S.encode_run(enc_secs, avail, state)
+        dsecs = [S.Section(enc_buf.data_ptr() + eo_, dp, 9 + r.clen, n, 0, es.sec)
+                 for (dp, n, eo_, cap), r, es in zip(dec_out, res, enc_secs)]
+        dres = S.decode(dsecs)
+        return res, dres, meth_all, tried, off
+
+    for _ in range(args.warmup):
+        step()
+    so = lib.load()
+    so.fqz5_profile(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res, dres, meth_all, tried, off = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    prof = (C.c_double * 6)()
+    so.fqz5_profile_read(prof)
+    so.fqz5_profile(0)
+    t_max = torch.tensor([dt], dtype=torch.float64, device=dev)
+    tot_bytes = torch.tensor([float(in_bytes_local)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot_bytes, op=dist.ReduceOp.SUM)
+    dt = float(t_max.item())
+
+    # ---- correctness: every decoded section equals its input -------------
+    ok = all(r.status == 0 for r in res) and all(r.status == 0 for r in dres)
+    for (sec, s, e, _), (dp, n, _, _) in zip(spans, dec_out):
+        src = seq_d if sec == S.SEC_SEQ else qual_d
+        ok = ok and bool(torch.equal(dec_buf[dp - dec_buf.data_ptr():][:n], src[s:e]))
+    comp_bytes = sum(9 + r.clen for r in res)
+
+    out = {
+        "metric": "input MB/s encode+decode, 100MB blocks, -3 and -5; bit-exact vs CPU",
+        "value": round(float(tot_bytes.item()) * args.steps / dt / 1e6, 2),
+        "unit": "MB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded Illumina 150 bp, 8-level binned quals)",
+        "config": {"workload": f"fqzcomp5 -{args.level} seq+qual sections of a "
+                               f"{args.gb:g} GB FASTQ per GPU, 100 MB blocks",
+                   "blocks_per_gpu": len(blocks), "level": args.level,
+                   "section_bytes_per_gpu": in_bytes_local,
+                   "compressed_bytes_per_gpu": comp_bytes,
+                   "methods": sorted({int(m) for m in meth_all}),
+                   "roundtrip_ok": bool(ok),
+                   "parallelism": f"blocks sharded over {world} GPU(s)"},
+    }
+    # ---- roofline of the dominant kernel ---------------------------------
+    enc_ms, enc_n, enc_b, dec_ms, dec_n, dec_b = list(prof)
+    if enc_ms >= dec_ms:
+        name, ms, n, b = "k_rans_enc", enc_ms, enc_n, enc_b
+    else:
+        name, ms, n, b = "k_rans_dec", dec_ms, dec_n, dec_b
+    avg_ms = ms / max(n, 1)
+    ach = (b / max(n, 1)) / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
+    out["roofline"] = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 6),
+                       "traffic": None, "kernel": name,
+                       "avg_launch_ms": round(avg_ms, 3),
+                       "bytes_per_launch": int(b / max(n, 1)),
+                       "enc_avg_ms": round(enc_ms / max(enc_n, 1), 3),
+                       "dec_avg_ms": round(dec_ms / max(dec_n, 1), 3)}
+    # ---- CPU baseline (rank 0, N=1) -----------------------------------------
+    if rank == 0 and world == 1 and not args.no_cpu:
+        host_secs = []
+        for sec, s, e, fl in spans:
+            arr = reads.seq if sec == S.SEC_SEQ else reads.qual
+            host_secs.append((arr[s:e].tobytes(), fl))
+        gpu_streams = []
+        enc_host = enc_buf.cpu().numpy()
+        for (dp, n, eo_, cap), r in zip(dec_out, res):
+            gpu_streams.append(enc_host[eo_ + 9:eo_ + 9 + r.clen].tobytes())
+        threads = min(args.cpu_threads, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(host_secs, tried[off:off + len(spans)],
+                                           meth_all[off:off + len(spans)],
+                                           gpu_streams, threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

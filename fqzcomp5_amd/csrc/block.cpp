@@ -1,0 +1,275 @@
+// block.cpp — fqzcomp5's per-block section coder for the sequence and
+// quality sections (fqzcomp5.c:1899-2280), driving the batched GPU rANS
+// codec.
+//
+// The reference encodes one block at a time per worker thread, trying every
+// method of the section's mask while the codec trial is running
+// (metrics_method / compress_with_methods, fqzcomp5.c:1899-2144).  Here a
+// whole run of blocks is handed over at once: every candidate method of
+// every block is compressed speculatively in ONE GPU batch (the chains run
+// side by side, so the extra candidates cost little wall time), then the
+// trial state machine is replayed on the host in block order, which gives
+// exactly the choices of a single-threaded (-t1) reference run.
+#include <cstring>
+#include <vector>
+
+#include "../../include/fqz5_block.h"
+#include "rans_codec.hpp"
+#include "rans_format.hpp"
+
+namespace fqz5 {
+
+GpuCtx &gpu();
+void fqz5_set_error(const char *msg);
+
+namespace {
+
+// fqzcomp5.c:185-208
+enum Method {
+    RANS0 = 1, RANS1, RANS64, RANS65, RANS128, RANS129, RANS192, RANS193,
+    RANSXN1, LZP3, M_LAST = 31
+};
+constexpr uint32_t RANS_MASK =
+    (1u << RANS0) | (1u << RANS1) | (1u << RANS64) | (1u << RANS65) |
+    (1u << RANS128) | (1u << RANS129) | (1u << RANS192) | (1u << RANS193) |
+    (1u << RANSXN1);
+
+// order word per rANS method (fqzcomp5.c:1992-2010)
+int method_order(int m, uint32_t fixed_len) {
+    static const int ord[] = {0, 1, 64, 65, 128, 129, 192, 193};
+    if (m >= RANS0 && m <= RANS193) return ord[m - RANS0];
+    return int((fixed_len << 8) + 9);   // RANSXN1, incl. the >=256 aliasing
+}
+
+// metrics_method (fqzcomp5.c:1899-1946)
+uint32_t metrics_method(fqz5_trial_state &st, int sec, uint32_t avail) {
+    fqz5_section_stats &s = st.sec[sec];
+    if (s.review <= 0) {
+        s.review = FQZ5_METRICS_REVIEW;
+        s.trial = FQZ5_METRICS_TRIAL;
+        std::memset(s.usize, 0, sizeof s.usize);
+        std::memset(s.csize, 0, sizeof s.csize);
+        std::memset(s.count, 0, sizeof s.count);
+    }
+    if (s.trial > 0) return avail;
+    if (s.trial > -99999) {
+        int best_m = 0;
+        double best = 1e30;
+        for (int m = 0; m < FQZ5_M_LAST; m++) {
+            if (s.usize[m] && best > (s.csize[m] + 1.0) / s.usize[m]) {
+                best = (s.csize[m] + 1.0) / s.usize[m];
+                best_m = m;
+            }
+        }
+        s.method_used = best_m;
+        s.trial = -99999;
+        return 1u << best_m;
+    }
+    s.review--;
+    return 1u << s.method_used;
+}
+
+}  // namespace
+
+// Speculative candidates of the last fqz5_sections_try on this thread; they
+// live in the thread's GPU arena until fqz5_sections_commit.
+struct TrySession {
+    std::vector<CompressReq> reqs;
+    std::vector<std::vector<int>> req_of;
+    bool open = false;
+};
+thread_local TrySession t_sess;
+
+}  // namespace fqz5
+
+using namespace fqz5;
+
+extern "C" {
+
+void fqz5_trial_init(fqz5_trial_state *st) { std::memset(st, 0, sizeof *st); }
+
+int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *avail,
+                      uint32_t *sizes) {
+    try {
+        GpuCtx &g = gpu();
+        if (t_sess.open) g.reset();
+        t_sess = TrySession();
+        for (int s = 0; s < FQZ5_SEC_LAST; s++)
+            if (avail[s] & ~RANS_MASK)
+                throw GpuError("fqz5_sections_try: method mask has non-rANS methods "
+                               "(LZP/tok3/seq-CM/fqz are not in this build)");
+        std::vector<CompressReq> &reqs = t_sess.reqs;
+        t_sess.req_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
+        for (int i = 0; i < nsec; i++) {
+            const fqz5_section &S = secs[i];
+            for (int m = 1; m < FQZ5_M_LAST; m++) {
+                if (!(avail[S.sec] & (1u << m))) continue;
+                if (m == RANSXN1 && !S.fixed_len) continue;   // out = NULL (:2004-2007)
+                CompressReq r;
+                r.d_in = S.in;
+                r.n = S.in_size;
+                r.order = method_order(m, S.fixed_len);
+                r.cap = compress_bound(r.n, r.order);
+                t_sess.req_of[i][m] = int(reqs.size());
+                reqs.push_back(std::move(r));
+            }
+        }
+        compress_batch(g, reqs);
+        t_sess.open = true;
+        // sizes as compress_with_methods sees them: UINT_MAX when not run,
+        // 0 when the codec returned NULL (out_len = *out_size = 0)
+        for (int i = 0; i < nsec; i++)
+            for (int m = 0; m < FQZ5_M_LAST; m++) {
+                const int ri = t_sess.req_of[i][m];
+                sizes[size_t(i) * FQZ5_M_LAST + m] =
+                    ri < 0 ? UINT32_MAX : (reqs[ri].ok ? layout_size(reqs[ri].out) : 0);
+            }
+        return 0;
+    } catch (const std::exception &e) {
+        fqz5_set_error(e.what());
+        t_sess = TrySession();
+        try { gpu().reset(); } catch (...) {}
+        return -1;
+    }
+}
+
+void fqz5_trial_replay(const int32_t *sec_ids, const uint32_t *in_sizes,
+                       const uint32_t *sizes, int nsec, const uint32_t *avail,
+                       fqz5_trial_state *st, int32_t *methods_out,
+                       uint32_t *tried_out) {
+    for (int i = 0; i < nsec; i++) {
+        const int sec = sec_ids[i];
+        fqz5_section_stats &ss = st->sec[sec];
+        const uint32_t methods = metrics_method(*st, sec, avail[sec]);
+        const bool in_trial = ss.trial > 0;           // compress_with_methods
+        uint32_t best_sz = UINT32_MAX;
+        int best_m = 0;
+        for (int m = 0; m < FQZ5_M_LAST; m++) {
+            if (!(methods & (1u << m))) continue;
+            const uint32_t out_len = sizes[size_t(i) * FQZ5_M_LAST + m];
+            if (best_sz > out_len) { best_sz = out_len; best_m = m; }
+        }
+        if (in_trial) {                                 // metrics_update, :2121-2130
+            for (int m = 0; m < FQZ5_M_LAST; m++) {
+                if (!(methods & (1u << m)) || ss.trial <= 0) continue;
+                ss.usize[m] += in_sizes[i];
+                ss.csize[m] += sizes[size_t(i) * FQZ5_M_LAST + m];
+                ss.count[m]++;
+            }
+            ss.trial--;
+        }
+        methods_out[i] = best_m;
+        if (tried_out) tried_out[i] = methods;
+    }
+}
+
+int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *methods,
+                         fqz5_section_result *res) {
+    try {
+        GpuCtx &g = gpu();
+        if (!t_sess.open || int(t_sess.req_of.size()) != nsec)
+            throw GpuError("fqz5_sections_commit: no matching fqz5_sections_try");
+        std::vector<const Layout *> ls;
+        std::vector<uint8_t *> dsts;
+        std::vector<Layout> framed(nsec);
+        for (int i = 0; i < nsec; i++) {
+            const fqz5_section &S = secs[i];
+            fqz5_section_result &R = res[i];
+            const int m = methods[i];
+            const int ri = (m > 0 && m < FQZ5_M_LAST) ? t_sess.req_of[i][m] : -1;
+            R.method = m;
+            R.strat = 0;
+            R.status = -1;
+            R.clen = 0;
+            R.usize = S.in_size;
+            if (ri < 0 || !t_sess.reqs[ri].ok) continue;
+            const uint32_t clen = layout_size(t_sess.reqs[ri].out);
+            R.clen = clen;
+            if (9ull + clen > S.out_cap) continue;
+            // section framing [strat u8][u32 usize][u32 csize] (:2224-2229)
+            Piece h;
+            h.host.resize(9);
+            std::memcpy(&h.host[1], &S.in_size, 4);
+            std::memcpy(&h.host[5], &clen, 4);
+            framed[i].push_back(std::move(h));
+            for (auto &p : t_sess.reqs[ri].out) framed[i].push_back(p);
+            ls.push_back(&framed[i]);
+            dsts.push_back(S.out);
+            R.status = 0;
+        }
+        write_layouts_dev(g, ls, dsts);
+        g.reset();
+        t_sess = TrySession();
+        return 0;
+    } catch (const std::exception &e) {
+        fqz5_set_error(e.what());
+        t_sess = TrySession();
+        try { gpu().reset(); } catch (...) {}
+        return -1;
+    }
+}
+
+int fqz5_encode_sections(const fqz5_section *secs, int nsec, const uint32_t *avail,
+                         fqz5_trial_state *st, fqz5_section_result *res) {
+    std::vector<uint32_t> sizes(size_t(nsec) * FQZ5_M_LAST);
+    if (fqz5_sections_try(secs, nsec, avail, sizes.data())) return -1;
+    std::vector<int32_t> ids(nsec), meth(nsec);
+    std::vector<uint32_t> ins(nsec);
+    for (int i = 0; i < nsec; i++) { ids[i] = secs[i].sec; ins[i] = secs[i].in_size; }
+    fqz5_trial_replay(ids.data(), ins.data(), sizes.data(), nsec, avail, st, meth.data(),
+                      nullptr);
+    return fqz5_sections_commit(secs, nsec, meth.data(), res);
+}
+
+int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result *res) {
+    try {
+        GpuCtx &g = gpu();
+        // section headers to the host, then the rANS payloads
+        size_t tot = 0;
+        for (int i = 0; i < nsec; i++) tot += secs[i].in_size;
+        std::vector<uint8_t> host(tot + 1);
+        size_t off = 0;
+        for (int i = 0; i < nsec; i++) {
+            g.download(host.data() + off, secs[i].in, secs[i].in_size);
+            off += secs[i].in_size;
+        }
+        g.sync();
+        std::vector<DecompressReq> reqs;
+        std::vector<int> who;
+        off = 0;
+        for (int i = 0; i < nsec; i++) {
+            const uint8_t *h = host.data() + off;
+            off += secs[i].in_size;
+            res[i].status = -1;
+            if (secs[i].in_size < 9) continue;
+            uint32_t ulen, clen;
+            std::memcpy(&ulen, h + 1, 4);
+            std::memcpy(&clen, h + 5, 4);
+            res[i].strat = h[0];
+            res[i].clen = clen;
+            if (h[0] != 0 || 9ull + clen > secs[i].in_size || ulen > secs[i].out_cap) continue;
+            DecompressReq r;
+            r.h_in = h + 9;
+            r.d_in = secs[i].in + 9;
+            r.in_size = clen;
+            r.out_cap = ulen;
+            r.d_out = secs[i].out;
+            reqs.push_back(r);
+            who.push_back(i);
+        }
+        decompress_batch(g, reqs);
+        for (size_t k = 0; k < reqs.size(); k++) {
+            fqz5_section_result &R = res[who[k]];
+            R.status = reqs[k].ok ? 0 : -1;
+            R.usize = reqs[k].out_size;
+        }
+        g.reset();
+        return 0;
+    } catch (const std::exception &e) {
+        fqz5_set_error(e.what());
+        try { gpu().reset(); } catch (...) {}
+        return -1;
+    }
+}
+
+}  // extern "C"

@@ -44,6 +44,10 @@ using namespace fqz5;
         return failret;                                                       \
     }
 
+namespace fqz5 {
+void fqz5_set_error(const char *msg) { g_err = msg; }
+}
+
 extern "C" {
 
 unsigned int rans_compress_bound_4x16(unsigned int size, int order) {
@@ -204,5 +208,25 @@ int fqz5_device_ok(void) {
 }
 
 const char *fqz5_last_error(void) { return g_err.c_str(); }
+
+void fqz5_profile(int on) {
+    try {
+        GpuCtx &g = gpu();
+        g.prof = KernelProfile();
+        g.prof.on = on != 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+    }
+}
+
+void fqz5_profile_read(double *out6) {
+    try {
+        const KernelProfile &p = gpu().prof;
+        out6[0] = p.enc_ms; out6[1] = p.enc_launches; out6[2] = p.enc_bytes;
+        out6[3] = p.dec_ms; out6[4] = p.dec_launches; out6[5] = p.dec_bytes;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+    }
+}
 
 }  // extern "C"

@@ -99,7 +99,42 @@ class PinnedArena {
     size_t cur_ = 0;
 };
 
+// Live per-kernel timing (HIP events on the context stream), read by the
+// benchmark for the roofline of the rANS chain kernels.
+struct KernelProfile {
+    bool on = false;
+    double enc_ms = 0, dec_ms = 0;
+    double enc_launches = 0, dec_launches = 0;
+    double enc_bytes = 0, dec_bytes = 0;   // algorithmic: input + output
+};
+
+// Brackets one launch with events when profiling is on.
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    bool on = false;
+    EventPair(bool enable, hipStream_t s) : on(enable) {
+        if (!on) return;
+        FQZ5_HIP(hipEventCreate(&a));
+        FQZ5_HIP(hipEventCreate(&b));
+        FQZ5_HIP(hipEventRecord(a, s));
+    }
+    void stop(hipStream_t s) {
+        if (on) FQZ5_HIP(hipEventRecord(b, s));
+    }
+    double ms() {   // after the stream has been synchronised
+        if (!on) return 0;
+        float t = 0;
+        FQZ5_HIP(hipEventElapsedTime(&t, a, b));
+        return t;
+    }
+    ~EventPair() {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+};
+
 struct GpuCtx {
+    KernelProfile prof;
     hipStream_t stream = nullptr;
     DevArena arena;
     PinnedArena staging;

@@ -54,7 +54,7 @@ struct EncSym;  // rans_format.hpp
 struct EncJob {
     const uint8_t *in;
     const EncSym *tab;      // O0: [256]; O1: [A*A] (remap[ctx]*A + remap[sym])
-    const uint8_t *remap;   // O1: byte -> alphabet index
+    const uint8_t *remap;   // O1: byte -> alphabet index (nullptr for O0)
     uint8_t *out_end;       // 2-byte aligned; stream grows downward
     uint32_t *out_len;      // bytes written below out_end
     uint32_t n;
@@ -72,7 +72,7 @@ struct DecJob {
     const uint8_t *in;      // payload: NX states then 16-bit words
     const uint32_t *tab;    // rows of 2^bits entries; O0 one row, O1 one
                             // row per context in alphabet order
-    const uint8_t *alpha;   // O1: row index -> byte value
+    const uint8_t *alpha;   // O1: row index -> byte value (nullptr for O0)
     uint8_t *out;
     int32_t *status;
     uint32_t in_len;
@@ -125,7 +125,8 @@ hipError_t launch_pack(const PackItem *d_items, int nitems, uint32_t max_out,
 hipError_t launch_stripe(const StripeItem *d_items, int nitems, uint32_t max_n,
                          hipStream_t s);
 hipError_t launch_copy(const CopyItem *d_items, int nitems, hipStream_t s);
-hipError_t launch_enc(const EncJob *d_jobs, int njobs, bool o1, hipStream_t s);
-hipError_t launch_dec(const DecJob *d_jobs, int njobs, bool o1, hipStream_t s);
+// One launch for all jobs; O1 jobs are the ones with remap / alpha set.
+hipError_t launch_enc(const EncJob *d_jobs, int njobs, hipStream_t s);
+hipError_t launch_dec(const DecJob *d_jobs, int njobs, hipStream_t s);
 
 }  // namespace fqz5

@@ -473,27 +473,36 @@ void Compressor::stage_encode() {
         jobs_.push_back(std::move(h));
         jobs_[i].hdr_job = int(jobs_.size()) - 1;
     }
-    std::vector<EncJob> e0, e1;
-    std::vector<int> id0, id1;
+    std::vector<EncJob> ej;
+    std::vector<int> order;
+    for (size_t i = 0; i < jobs_.size(); i++)
+        if (jobs_[i].n) order.push_back(int(i));
+    // longest chains first so they start in the first dispatch wave
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        return jobs_[a].n / jobs_[a].nx > jobs_[b].n / jobs_[b].nx;
+    });
     uint32_t *d_lens = g_.arena.alloc_n<uint32_t>(jobs_.size());
-    for (size_t i = 0; i < jobs_.size(); i++) {
+    for (int i : order) {
         EJ &j = jobs_[i];
-        if (!j.n) continue;
         if (!j.h_in.empty()) j.d_in = g_.upload(j.h_in);
         const EncSym *d_tab = g_.upload(j.syms);
         const size_t cap = 2 * size_t(j.n) + 16 * size_t(j.nx) + 64;
         uint8_t *base = g_.arena.alloc_n<uint8_t>(cap);
         j.d_end = base + (cap & ~size_t(1));
         const uint8_t *d_remap = j.o1 ? g_.upload(j.remap, 256) : nullptr;
-        EncJob e{j.d_in, d_tab, d_remap, j.d_end, d_lens + i, j.n, j.nx, j.bits, j.A};
-        if (j.o1) e1.push_back(e);
-        else e0.push_back(e);
+        ej.push_back(EncJob{j.d_in, d_tab, d_remap, j.d_end, d_lens + i, j.n, j.nx, j.bits, j.A});
     }
-    if (!e0.empty()) FQZ5_HIP(launch_enc(g_.upload(e0), int(e0.size()), false, g_.stream));
-    if (!e1.empty()) FQZ5_HIP(launch_enc(g_.upload(e1), int(e1.size()), true, g_.stream));
+    EventPair ev(g_.prof.on && !ej.empty(), g_.stream);
+    if (!ej.empty()) FQZ5_HIP(launch_enc(g_.upload(ej), int(ej.size()), g_.stream));
+    ev.stop(g_.stream);
     std::vector<uint32_t> lens(jobs_.size(), 0);
     g_.download(lens.data(), d_lens, jobs_.size());
     g_.sync();
+    if (ev.on) {
+        g_.prof.enc_ms += ev.ms();
+        g_.prof.enc_launches += 1;
+        for (int i : order) g_.prof.enc_bytes += double(jobs_[i].n) + lens[i];
+    }
     for (size_t i = 0; i < jobs_.size(); i++) jobs_[i].payload = jobs_[i].n ? lens[i] : 0;
     for (size_t i = nmain; i < jobs_.size(); i++) finish_job(jobs_[i]);
     for (size_t i = 0; i < nmain; i++) finish_job(jobs_[i]);

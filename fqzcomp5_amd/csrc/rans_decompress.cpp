@@ -286,7 +286,6 @@ int Decompressor::parse(const uint8_t *h, const uint8_t *d, uint32_t len, uint8_
 }
 
 void Decompressor::run_djs(const std::vector<int> &ids) {
-    std::vector<DecJob> j0, j1;
     std::vector<uint32_t> tabs;
     std::vector<uint8_t> alphas;
     struct Off { size_t tab, alpha; };
@@ -325,19 +324,35 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
     const uint8_t *d_alpha = alphas.empty() ? nullptr : g_.upload(alphas);
     int32_t *d_status = g_.arena.alloc_n<int32_t>(used.size());
     g_.memset0(d_status, used.size() * 4);
+    std::vector<DecJob> dj;
+    std::vector<size_t> ord;
     for (size_t k = 0; k < used.size(); k++) {
         DJ &j = djs_[used[k]];
         if (j.len < j.tab_len + 4u * j.nx) { j.ok = false; continue; }
-        DecJob e{j.d + j.tab_len, d_tabs + offs[k].tab,
-                 j.o1 ? d_alpha + offs[k].alpha : nullptr, j.d_out, d_status + k,
-                 j.len - j.tab_len, j.n, j.nx, j.bits};
-        (j.o1 ? j1 : j0).push_back(e);
+        ord.push_back(k);
     }
-    if (!j0.empty()) FQZ5_HIP(launch_dec(g_.upload(j0), int(j0.size()), false, g_.stream));
-    if (!j1.empty()) FQZ5_HIP(launch_dec(g_.upload(j1), int(j1.size()), true, g_.stream));
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+        return djs_[used[a]].n / djs_[used[a]].nx > djs_[used[b]].n / djs_[used[b]].nx;
+    });
+    double bytes = 0;
+    for (size_t k : ord) {
+        DJ &j = djs_[used[k]];
+        dj.push_back(DecJob{j.d + j.tab_len, d_tabs + offs[k].tab,
+                            j.o1 ? d_alpha + offs[k].alpha : nullptr, j.d_out, d_status + k,
+                            j.len - j.tab_len, j.n, j.nx, j.bits});
+        bytes += double(j.n) + (j.len - j.tab_len);
+    }
+    EventPair ev(g_.prof.on && !dj.empty(), g_.stream);
+    if (!dj.empty()) FQZ5_HIP(launch_dec(g_.upload(dj), int(dj.size()), g_.stream));
+    ev.stop(g_.stream);
     std::vector<int32_t> st(used.size());
     g_.download(st.data(), d_status, st.size());
     g_.sync();
+    if (ev.on) {
+        g_.prof.dec_ms += ev.ms();
+        g_.prof.dec_launches += 1;
+        g_.prof.dec_bytes += bytes;
+    }
     for (size_t k = 0; k < used.size(); k++)
         if (st[k]) djs_[used[k]].ok = false;
 }

@@ -203,8 +203,7 @@ static DEV void enc_fetch(const EncJob &J, int z, int nx, uint32_t isz,
 }
 
 template <bool O1>
-__global__ __launch_bounds__(64) void k_rans_enc(const EncJob *jobs) {
-    const EncJob J = jobs[blockIdx.x];
+static DEV void enc_body(const EncJob &J) {
     const int z = int(lane_id());
     const int nx = J.nx;
     const uint32_t n = J.n;
@@ -262,6 +261,13 @@ __global__ __launch_bounds__(64) void k_rans_enc(const EncJob *jobs) {
     if (z == 0) *J.out_len = 2 * nw + 4 * uint32_t(nx);
 }
 
+// One launch for every stream of the batch; the order is wave-uniform.
+__global__ __launch_bounds__(64) void k_rans_enc(const EncJob *jobs) {
+    const EncJob J = jobs[blockIdx.x];
+    if (J.remap) enc_body<true>(J);
+    else enc_body<false>(J);
+}
+
 // ---------------------------------------------------------------------------
 // Entropy decoder.  One 64-lane workgroup per stream, lane z = state z.
 // Decode table entries (32 bit): (f-1) << (bits+8) | (slot-start) << 8 | s,
@@ -277,9 +283,7 @@ constexpr uint32_t RING_WORDS = 4096;       // 8 KiB ring
 constexpr uint32_t SLAB_WORDS = 512;        // 64 lanes x 16 B
 
 template <bool O1>
-__global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
-    __shared__ uint16_t ring[RING_WORDS];
-    const DecJob J = jobs[blockIdx.x];
+static DEV void dec_body(const DecJob &J, uint16_t *ring) {
     const int z = int(lane_id());
     const int nx = J.nx;
     const uint32_t n = J.n;
@@ -378,6 +382,13 @@ __global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
         }
     }
     if (z == 0) *J.status = (ptr <= nwords) ? 0 : -1;
+}
+
+__global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
+    __shared__ uint16_t ring[RING_WORDS];
+    const DecJob J = jobs[blockIdx.x];
+    if (J.alpha) dec_body<true>(J, ring);
+    else dec_body<false>(J, ring);
 }
 
 // ---------------------------------------------------------------------------
@@ -678,17 +689,15 @@ hipError_t launch_copy(const CopyItem *d_items, int nitems, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_enc(const EncJob *d_jobs, int njobs, bool o1, hipStream_t s) {
+hipError_t launch_enc(const EncJob *d_jobs, int njobs, hipStream_t s) {
     if (!njobs) return hipSuccess;
-    if (o1) hipLaunchKernelGGL(k_rans_enc<true>, dim3(njobs), dim3(64), 0, s, d_jobs);
-    else    hipLaunchKernelGGL(k_rans_enc<false>, dim3(njobs), dim3(64), 0, s, d_jobs);
+    hipLaunchKernelGGL(k_rans_enc, dim3(njobs), dim3(64), 0, s, d_jobs);
     return hipGetLastError();
 }
 
-hipError_t launch_dec(const DecJob *d_jobs, int njobs, bool o1, hipStream_t s) {
+hipError_t launch_dec(const DecJob *d_jobs, int njobs, hipStream_t s) {
     if (!njobs) return hipSuccess;
-    if (o1) hipLaunchKernelGGL(k_rans_dec<true>, dim3(njobs), dim3(64), 0, s, d_jobs);
-    else    hipLaunchKernelGGL(k_rans_dec<false>, dim3(njobs), dim3(64), 0, s, d_jobs);
+    hipLaunchKernelGGL(k_rans_dec, dim3(njobs), dim3(64), 0, s, d_jobs);
     return hipGetLastError();
 }
 

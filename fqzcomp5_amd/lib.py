@@ -11,7 +11,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfqz5_mi355x.so")
-HEADER = os.path.join(os.path.dirname(HERE), "include", "fqz5_mi355x.h")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 _libc = C.CDLL(None)
 _libc.free.argtypes = [C.c_void_p]
@@ -73,9 +73,10 @@ def device_ok() -> bool:
 
 
 def header_symbols() -> list[str]:
-    """Function names declared in include/fqz5_mi355x.h."""
+    """Function names declared in include/*.h."""
+    import glob
     import re
-    txt = open(HEADER).read()
+    txt = "".join(open(f).read() for f in sorted(glob.glob(os.path.join(INCLUDE, "*.h"))))
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b([a-z_0-9]+)\s*\(", txt))
                   - {"if", "sizeof", "return"})

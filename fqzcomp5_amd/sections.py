@@ -1,0 +1,198 @@
+"""Block-section coding on the GPU (include/fqz5_block.h) from Python.
+
+A "run" is a list of blocks in file order; each block has a sequence and a
+quality section (fqzcomp5.c:2217-2257).  Encoding follows fqzcomp5's codec
+trial (metrics_method / compress_with_methods, fqzcomp5.c:1899-2144):
+
+    sizes  = try(local sections)            # all candidates, one GPU batch
+    sizes  = exchange(sizes)                # multi-GPU: all_gather (RCCL)
+    meth   = replay(all sections, sizes)    # host state machine, file order
+    commit(local sections, meth)            # chosen streams, framed
+
+so the choices are those of a single-threaded reference run over the whole
+file, whichever GPU holds which block.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import lib as _lib
+
+M_LAST = 31
+SEC_SEQ, SEC_QUAL = 2, 3
+RANS0, RANS1, RANS64, RANS65, RANS128, RANS129, RANS192, RANS193, RANSXN1 = range(1, 10)
+LZP3 = 10
+
+# Method masks of the level presets (fqzcomp5.c:4886-4932) restricted to the
+# rANS methods this build implements (LZP3 is the next row).
+LEVEL_MASKS = {
+    1: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193],
+        SEC_QUAL: [RANS0, RANS1, RANS129, RANS193]},
+    3: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193],
+        SEC_QUAL: [RANS0, RANS1, RANS129, RANS193, RANSXN1]},
+}
+
+
+class Section(C.Structure):
+    _fields_ = [("in_", C.c_void_p), ("out", C.c_void_p),
+                ("in_size", C.c_uint32), ("out_cap", C.c_uint32),
+                ("fixed_len", C.c_uint32), ("sec", C.c_int32)]
+
+
+class SectionResult(C.Structure):
+    _fields_ = [("method", C.c_int32), ("strat", C.c_int32),
+                ("status", C.c_int32), ("clen", C.c_uint32),
+                ("usize", C.c_uint32)]
+
+
+class SectionStats(C.Structure):
+    _fields_ = [("usize", C.c_uint64 * M_LAST), ("csize", C.c_uint64 * M_LAST),
+                ("review", C.c_int32), ("trial", C.c_int32),
+                ("count", C.c_int32 * M_LAST), ("method_used", C.c_int32)]
+
+
+class TrialState(C.Structure):
+    _fields_ = [("sec", SectionStats * 4)]
+
+
+_bound = False
+
+
+def _load():
+    global _bound
+    so = _lib.load()
+    if not _bound:
+        so.fqz5_trial_init.argtypes = [C.POINTER(TrialState)]
+        so.fqz5_sections_try.argtypes = [C.POINTER(Section), C.c_int,
+                                         C.POINTER(C.c_uint32),
+                                         C.POINTER(C.c_uint32)]
+        so.fqz5_sections_try.restype = C.c_int
+        so.fqz5_trial_replay.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
+                                         C.POINTER(C.c_uint32), C.c_int,
+                                         C.POINTER(C.c_uint32), C.POINTER(TrialState),
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_uint32)]
+        so.fqz5_sections_commit.argtypes = [C.POINTER(Section), C.c_int,
+                                            C.POINTER(C.c_int32),
+                                            C.POINTER(SectionResult)]
+        so.fqz5_sections_commit.restype = C.c_int
+        so.fqz5_decode_sections.argtypes = [C.POINTER(Section), C.c_int,
+                                            C.POINTER(SectionResult)]
+        so.fqz5_decode_sections.restype = C.c_int
+        _bound = True
+    return so
+
+
+def masks(level: int) -> np.ndarray:
+    av = np.zeros(4, np.uint32)
+    for sec, ms in LEVEL_MASKS[level].items():
+        for m in ms:
+            av[sec] |= np.uint32(1 << m)
+    return av
+
+
+def new_state() -> TrialState:
+    st = TrialState()
+    _load().fqz5_trial_init(C.byref(st))
+    return st
+
+
+def _arr(t, xs):
+    return (t * len(xs))(*xs)
+
+
+def sections_try(secs: list[Section], avail: np.ndarray) -> np.ndarray:
+    so = _load()
+    sizes = np.zeros(len(secs) * M_LAST, np.uint32)
+    av = np.ascontiguousarray(avail, np.uint32)
+    rc = so.fqz5_sections_try(_arr(Section, secs), len(secs),
+                              av.ctypes.data_as(C.POINTER(C.c_uint32)),
+                              sizes.ctypes.data_as(C.POINTER(C.c_uint32)))
+    if rc:
+        raise _lib.NativeError("fqz5_sections_try: " + _lib.last_error())
+    return sizes.reshape(len(secs), M_LAST)
+
+
+def trial_replay(sec_ids, in_sizes, sizes: np.ndarray, avail: np.ndarray,
+                 state: TrialState, tried: np.ndarray | None = None) -> np.ndarray:
+    """Host-only replay of metrics_method/compress_with_methods; `tried`
+    (optional, uint32[n]) receives the method mask each section tried."""
+    so = _load()
+    n = len(sec_ids)
+    ids = np.ascontiguousarray(sec_ids, np.int32)
+    ins = np.ascontiguousarray(in_sizes, np.uint32)
+    sz = np.ascontiguousarray(sizes, np.uint32).reshape(-1)
+    av = np.ascontiguousarray(avail, np.uint32)
+    out = np.zeros(n, np.int32)
+    so.fqz5_trial_replay(ids.ctypes.data_as(C.POINTER(C.c_int32)),
+                         ins.ctypes.data_as(C.POINTER(C.c_uint32)),
+                         sz.ctypes.data_as(C.POINTER(C.c_uint32)), n,
+                         av.ctypes.data_as(C.POINTER(C.c_uint32)),
+                         C.byref(state), out.ctypes.data_as(C.POINTER(C.c_int32)),
+                         None if tried is None else
+                         tried.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return out
+
+
+def sections_commit(secs: list[Section], methods: np.ndarray) -> list[SectionResult]:
+    so = _load()
+    res = (SectionResult * len(secs))()
+    m = np.ascontiguousarray(methods, np.int32)
+    rc = so.fqz5_sections_commit(_arr(Section, secs), len(secs),
+                                 m.ctypes.data_as(C.POINTER(C.c_int32)), res)
+    if rc:
+        raise _lib.NativeError("fqz5_sections_commit: " + _lib.last_error())
+    return list(res)
+
+
+def decode(secs: list[Section]) -> list[SectionResult]:
+    so = _load()
+    res = (SectionResult * len(secs))()
+    if so.fqz5_decode_sections(_arr(Section, secs), len(secs), res):
+        raise _lib.NativeError("fqz5_decode_sections: " + _lib.last_error())
+    return list(res)
+
+
+def exchange_sizes(local: np.ndarray, in_sizes: np.ndarray, sec_ids: np.ndarray,
+                   group=None):
+    """All-gather the candidate sizes of every rank's sections (rank-major =
+    file order).  This is the only collective on the encode path: the trial
+    state of later blocks depends on the first blocks' candidates."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return local, in_sizes, sec_ids, 0
+    ws, rk = dist.get_world_size(group), dist.get_rank(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) \
+        if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(ws)]
+    dist.all_gather(ns, n, group=group)
+    nmax = int(max(int(x) for x in ns))
+    pack = np.zeros((nmax, M_LAST + 2), np.int64)
+    pack[:local.shape[0], :M_LAST] = local
+    pack[:local.shape[0], M_LAST] = in_sizes
+    pack[:local.shape[0], M_LAST + 1] = sec_ids
+    t = torch.from_numpy(pack).to(dev)
+    outs = [torch.zeros_like(t) for _ in range(ws)]
+    dist.all_gather(outs, t, group=group)
+    rows = [o[:int(k)].cpu().numpy() for o, k in zip(outs, ns)]
+    allp = np.concatenate(rows, 0)
+    off = sum(int(k) for k in ns[:rk])
+    return (allp[:, :M_LAST].astype(np.uint32), allp[:, M_LAST].astype(np.uint32),
+            allp[:, M_LAST + 1].astype(np.int32), off)
+
+
+def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
+               group=None):
+    """try -> (exchange) -> replay -> commit for this rank's sections."""
+    local = sections_try(secs, avail)
+    ins = np.array([s.in_size for s in secs], np.uint32)
+    ids = np.array([s.sec for s in secs], np.int32)
+    g_sizes, g_ins, g_ids, off = exchange_sizes(local, ins, ids, group)
+    tried = np.zeros(len(g_ids), np.uint32)
+    meth_all = trial_replay(g_ids, g_ins, g_sizes, avail, state, tried)
+    meth = meth_all[off:off + len(secs)]
+    res = sections_commit(secs, meth)
+    return res, meth_all, g_sizes, tried, off

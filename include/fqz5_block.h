@@ -1,0 +1,89 @@
+/*
+ * fqz5_block.h — fqzcomp5 block-section coder on the GPU (C-ABI).
+ *
+ * Restates the per-section part of fqzcomp5's encode_block/decode_block
+ * (fqzcomp5.c:2147-2547) for the sequence and quality sections: method
+ * choice by the codec-trial state machine (metrics_method/metrics_update,
+ * fqzcomp5.c:1899-1958), compress_with_methods' candidate loop
+ * (fqzcomp5.c:1961-2144) and the section framing
+ * [strat u8][u32 usize][u32 csize][stream] (fqzcomp5.c:2217-2257).
+ * A caller hands over a run of blocks at once; the choices equal those of a
+ * single-threaded reference run over the same blocks in the same order.
+ * This build implements the rANS methods (RANS0..RANS193, RANSXN1); masks
+ * with LZP/tok3/seq-CM/fqz bits are rejected.
+ */
+#ifndef FQZ5_BLOCK_H
+#define FQZ5_BLOCK_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FQZ5_M_LAST 31            /* methods enum size, fqzcomp5.c:185-208 */
+#define FQZ5_SEC_NAME 0           /* sections, fqzcomp5.c:177-183 */
+#define FQZ5_SEC_LEN 1
+#define FQZ5_SEC_SEQ 2
+#define FQZ5_SEC_QUAL 3
+#define FQZ5_SEC_LAST 4
+#define FQZ5_METRICS_REVIEW 100   /* fqzcomp5.c:151 */
+#define FQZ5_METRICS_TRIAL 3      /* fqzcomp5.c:152 */
+
+typedef struct {                  /* the reference's `metrics` (fqzcomp5.c:221-225) */
+    uint64_t usize[FQZ5_M_LAST], csize[FQZ5_M_LAST];
+    int32_t review, trial;
+    int32_t count[FQZ5_M_LAST];
+    int32_t method_used;          /* method_used[sec] (fqzcomp5.c:232) */
+} fqz5_section_stats;
+
+typedef struct {
+    fqz5_section_stats sec[FQZ5_SEC_LAST];
+} fqz5_trial_state;
+
+typedef struct {                  /* one section of one block (device data) */
+    const uint8_t *in;            /* encode: raw bytes; decode: framed section */
+    uint8_t *out;                 /* encode: framed section; decode: raw bytes */
+    uint32_t in_size;
+    uint32_t out_cap;
+    uint32_t fixed_len;           /* fq->fixed_len (0 = variable) */
+    int32_t sec;                  /* FQZ5_SEC_SEQ or FQZ5_SEC_QUAL */
+} fqz5_section;
+
+typedef struct {
+    int32_t method;               /* chosen method (encode) */
+    int32_t strat;                /* section strat byte */
+    int32_t status;               /* 0 ok */
+    uint32_t clen;                /* compressed stream bytes (excl. 9-byte frame) */
+    uint32_t usize;               /* decoded bytes (decode) */
+} fqz5_section_result;
+
+void fqz5_trial_init(fqz5_trial_state *st);
+
+/* Encode `n` sections given in block order; avail[sec] are the method masks
+ * (1<<method).  st carries the trial state across calls.  Returns 0 or -1. */
+int fqz5_encode_sections(const fqz5_section *secs, int n, const uint32_t *avail,
+                         fqz5_trial_state *st, fqz5_section_result *res);
+
+/* The same in three phases, for callers that replay the trial state over
+ * sections held by several processes (multi-GPU, bench.py):
+ *   try     compress every candidate of every section; sizes[i*FQZ5_M_LAST+m]
+ *           = candidate size, UINT32_MAX when not run (compress_with_methods'
+ *           out_len); the candidates stay on the GPU until commit;
+ *   replay  the host-only trial state machine over sections in file order;
+ *   commit  write the chosen candidates, framed, to the outputs. */
+int fqz5_sections_try(const fqz5_section *secs, int n, const uint32_t *avail,
+                      uint32_t *sizes);
+void fqz5_trial_replay(const int32_t *sec_ids, const uint32_t *in_sizes,
+                       const uint32_t *sizes, int n, const uint32_t *avail,
+                       fqz5_trial_state *st, int32_t *methods_out,
+                       uint32_t *tried_out /* nullable: mask tried per section */);
+int fqz5_sections_commit(const fqz5_section *secs, int n, const int32_t *methods,
+                         fqz5_section_result *res);
+
+/* Decode framed sections (strat 0 = rANS) into their outputs. */
+int fqz5_decode_sections(const fqz5_section *secs, int n, fqz5_section_result *res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -81,6 +81,13 @@ int fqz5_device_ok(void);
 /* Last error message of the calling thread ("" if none). */
 const char *fqz5_last_error(void);
 
+/* Kernel timing with HIP events on fqz5_stream() (benchmark roofline).
+ * fqz5_profile(1) resets and enables; fqz5_profile_read fills
+ * {enc_ms, enc_launches, enc_bytes, dec_ms, dec_launches, dec_bytes} for
+ * the rANS chain kernels, bytes = algorithmic input + output bytes. */
+void fqz5_profile(int on);
+void fqz5_profile_read(double *out6);
+
 #ifdef __cplusplus
 }
 #endif

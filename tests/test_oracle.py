@@ -68,3 +68,35 @@ def test_oracle_vs_reference_fuzz():
         except RuntimeError:
             b = None
         assert a == b, (n, k, hex(o))
+
+
+@pytest.mark.skipif(not binding.have_ref(), reason="oracle/_ref not built")
+def test_oracle_capacity_semantics_vs_reference():
+    """rans_compress_to_4x16 with tight caller buffers: the restatement
+    fails (NULL) exactly when the reference does, else same bytes."""
+    import ctypes as C
+    ora, ref = binding.oracle(), binding.ref()
+    fo = ora.lib.ora_rans_compress_to_4x16
+    fr = ref.lib.rans_compress_to_4x16
+    for f in (fo, fr):
+        f.restype = C.c_void_p
+        f.argtypes = [C.c_char_p, C.c_uint, C.c_void_p, C.POINTER(C.c_uint), C.c_int]
+    rng = np.random.default_rng(5)
+    for it in range(200):
+        n = int(rng.integers(0, 3000))
+        d = (rng.integers(0, 1 + it % 20, n) + it % 3).astype(np.uint8).tobytes()
+        o = int(rng.choice([0, 1, 5, 65, 128, 129, 193, (12 << 8) | 9, (40 << 8) | 9]))
+        try:
+            full = len(ref.rans_compress(d, o))
+        except RuntimeError:
+            continue
+        for cap in (full, full - 1, full + 2, 1, 6, full // 2):
+            if cap <= 0:
+                continue
+            res = []
+            for f in (fo, fr):
+                buf = C.create_string_buffer(cap + 4096)
+                k = C.c_uint(cap)
+                p = f(d, len(d), buf, C.byref(k), o)
+                res.append(buf.raw[:k.value] if p else None)
+            assert res[0] == res[1], (n, hex(o), cap)
