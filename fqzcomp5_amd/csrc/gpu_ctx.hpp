@@ -136,6 +136,8 @@ struct EventPair {
 struct GpuCtx {
     KernelProfile prof;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;   // second queue for concurrent launches
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     DevArena arena;
     PinnedArena staging;
     int device = 0;
@@ -146,9 +148,25 @@ struct GpuCtx {
             throw GpuError("fqz5: no HIP device visible (this library has no CPU path)");
         FQZ5_HIP(hipGetDevice(&device));
         FQZ5_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        FQZ5_HIP(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+        FQZ5_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+        FQZ5_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
     }
     ~GpuCtx() {
+        if (fork_ev) (void)hipEventDestroy(fork_ev);
+        if (join_ev) (void)hipEventDestroy(join_ev);
+        if (stream2) (void)hipStreamDestroy(stream2);
         if (stream) (void)hipStreamDestroy(stream);
+    }
+    // stream2 waits for everything queued on stream so far
+    void fork() {
+        FQZ5_HIP(hipEventRecord(fork_ev, stream));
+        FQZ5_HIP(hipStreamWaitEvent(stream2, fork_ev, 0));
+    }
+    // stream waits for everything queued on stream2 so far
+    void join() {
+        FQZ5_HIP(hipEventRecord(join_ev, stream2));
+        FQZ5_HIP(hipStreamWaitEvent(stream, join_ev, 0));
     }
     void sync() { FQZ5_HIP(hipStreamSynchronize(stream)); }
 

@@ -79,6 +79,8 @@ struct DecJob {
     uint32_t n;
     int32_t nx;
     int32_t bits;
+    uint32_t rows;          // table rows (1 for O0)
+    uint32_t pad;
 };
 
 // RLE encode of one leaf input; saved[] marks the RLE symbols.
@@ -126,7 +128,11 @@ hipError_t launch_stripe(const StripeItem *d_items, int nitems, uint32_t max_n,
                          hipStream_t s);
 hipError_t launch_copy(const CopyItem *d_items, int nitems, hipStream_t s);
 // One launch for all jobs; O1 jobs are the ones with remap / alpha set.
-hipError_t launch_enc(const EncJob *d_jobs, int njobs, hipStream_t s);
-hipError_t launch_dec(const DecJob *d_jobs, int njobs, hipStream_t s);
+// `lds` = dynamic LDS bytes: the maximum of enc_lds_bytes/dec_lds_bytes
+// over the launch's jobs.
+uint32_t enc_lds_bytes(int o1, uint32_t A);
+uint32_t dec_lds_bytes(uint32_t rows, int bits);
+hipError_t launch_enc(const EncJob *d_jobs, int njobs, uint32_t lds, hipStream_t s);
+hipError_t launch_dec(const DecJob *d_jobs, int njobs, uint32_t lds, hipStream_t s);
 
 }  // namespace fqz5

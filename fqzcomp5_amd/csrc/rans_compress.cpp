@@ -350,7 +350,7 @@ void Compressor::build_o0(EJ &j) {
     j.table.resize(put_freq0(j.table.data(), F));
     normalise_freq(F, int(mv), 4096);
     j.bits = 12;
-    j.syms.assign(256, EncSym{0, 0});
+    j.syms.assign(256, EncSym{0, 0, 0, 0});
     for (uint32_t s = 0, x = 0; s < 256; s++)
         if (F[s]) { j.syms[s] = make_encsym(x, F[s], 12); x += F[s]; }
 }
@@ -382,7 +382,7 @@ void Compressor::build_o1(EJ &j, const uint32_t *cnt) {
     uint32_t rowmax[256] = {0};
     const int shift = o1_pick_shift(T, F, rowmax);
     j.bits = shift;
-    j.syms.assign(size_t(j.A) * j.A, EncSym{0, 0});
+    j.syms.assign(size_t(j.A) * j.A, EncSym{0, 0, 0, 0});
     for (int i = 0; i < 256; i++) {
         if (!T[i]) continue;
         uint32_t mv = rowmax[i];
@@ -473,7 +473,10 @@ void Compressor::stage_encode() {
         jobs_.push_back(std::move(h));
         jobs_[i].hdr_job = int(jobs_.size()) - 1;
     }
-    std::vector<EncJob> ej;
+    // Two launches on two queues: jobs whose tables fit a small LDS
+    // footprint (many waves per CU) and the rest.
+    std::vector<EncJob> ejs, ejb;
+    uint32_t lds_s = 0, lds_b = 0;
     std::vector<int> order;
     for (size_t i = 0; i < jobs_.size(); i++)
         if (jobs_[i].n) order.push_back(int(i));
@@ -486,14 +489,23 @@ void Compressor::stage_encode() {
         EJ &j = jobs_[i];
         if (!j.h_in.empty()) j.d_in = g_.upload(j.h_in);
         const EncSym *d_tab = g_.upload(j.syms);
-        const size_t cap = 2 * size_t(j.n) + 16 * size_t(j.nx) + 64;
+        const size_t cap = 2 * size_t(j.n) + 16 * size_t(j.nx) + 1088;
         uint8_t *base = g_.arena.alloc_n<uint8_t>(cap);
-        j.d_end = base + (cap & ~size_t(1));
+        j.d_end = base + (cap & ~size_t(15));
         const uint8_t *d_remap = j.o1 ? g_.upload(j.remap, 256) : nullptr;
-        ej.push_back(EncJob{j.d_in, d_tab, d_remap, j.d_end, d_lens + i, j.n, j.nx, j.bits, j.A});
+        const EncJob e{j.d_in, d_tab, d_remap, j.d_end, d_lens + i, j.n, j.nx, j.bits, j.A};
+        const uint32_t lds = enc_lds_bytes(j.o1, uint32_t(j.A));
+        if (lds <= 24 * 1024) { ejs.push_back(e); lds_s = std::max(lds_s, lds); }
+        else { ejb.push_back(e); lds_b = std::max(lds_b, lds); }
     }
-    EventPair ev(g_.prof.on && !ej.empty(), g_.stream);
-    if (!ej.empty()) FQZ5_HIP(launch_enc(g_.upload(ej), int(ej.size()), g_.stream));
+    EventPair ev(g_.prof.on && !order.empty(), g_.stream);
+    if (!ejs.empty()) {
+        const EncJob *d = g_.upload(ejs);
+        g_.fork();
+        FQZ5_HIP(launch_enc(d, int(ejs.size()), lds_s, g_.stream2));
+        g_.join();
+    }
+    if (!ejb.empty()) FQZ5_HIP(launch_enc(g_.upload(ejb), int(ejb.size()), lds_b, g_.stream));
     ev.stop(g_.stream);
     std::vector<uint32_t> lens(jobs_.size(), 0);
     g_.download(lens.data(), d_lens, jobs_.size());

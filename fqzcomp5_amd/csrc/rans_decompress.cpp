@@ -324,7 +324,8 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
     const uint8_t *d_alpha = alphas.empty() ? nullptr : g_.upload(alphas);
     int32_t *d_status = g_.arena.alloc_n<int32_t>(used.size());
     g_.memset0(d_status, used.size() * 4);
-    std::vector<DecJob> dj;
+    std::vector<DecJob> djs, djb;
+    uint32_t lds_s = 0, lds_b = 0;
     std::vector<size_t> ord;
     for (size_t k = 0; k < used.size(); k++) {
         DJ &j = djs_[used[k]];
@@ -337,13 +338,23 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
     double bytes = 0;
     for (size_t k : ord) {
         DJ &j = djs_[used[k]];
-        dj.push_back(DecJob{j.d + j.tab_len, d_tabs + offs[k].tab,
-                            j.o1 ? d_alpha + offs[k].alpha : nullptr, j.d_out, d_status + k,
-                            j.len - j.tab_len, j.n, j.nx, j.bits});
+        const uint32_t rows = j.o1 ? uint32_t(j.alpha.size()) : 1u;
+        const DecJob e{j.d + j.tab_len, d_tabs + offs[k].tab,
+                       j.o1 ? d_alpha + offs[k].alpha : nullptr, j.d_out, d_status + k,
+                       j.len - j.tab_len, j.n, j.nx, j.bits, rows, 0};
         bytes += double(j.n) + (j.len - j.tab_len);
+        const uint32_t lds = dec_lds_bytes(rows, j.bits);
+        if (lds <= 40 * 1024) { djs.push_back(e); lds_s = std::max(lds_s, lds); }
+        else { djb.push_back(e); lds_b = std::max(lds_b, lds); }
     }
-    EventPair ev(g_.prof.on && !dj.empty(), g_.stream);
-    if (!dj.empty()) FQZ5_HIP(launch_dec(g_.upload(dj), int(dj.size()), g_.stream));
+    EventPair ev(g_.prof.on && !ord.empty(), g_.stream);
+    if (!djs.empty()) {
+        const DecJob *d = g_.upload(djs);
+        g_.fork();
+        FQZ5_HIP(launch_dec(d, int(djs.size()), lds_s, g_.stream2));
+        g_.join();
+    }
+    if (!djb.empty()) FQZ5_HIP(launch_dec(g_.upload(djb), int(djb.size()), lds_b, g_.stream));
     ev.stop(g_.stream);
     std::vector<int32_t> st(used.size());
     g_.download(st.data(), d_status, st.size());

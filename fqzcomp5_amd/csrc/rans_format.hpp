@@ -270,28 +270,30 @@ inline int o1_pick_shift(const uint32_t *T, const uint32_t (*F)[256],
     return (c10 / c12 < 1.01 || maxall <= 1024) ? 10 : 12;
 }
 
-// Packed encoder symbol used by the GPU encode kernel (8 bytes).
-// Derived from RansEncSymbolInit (rANS_word.h:201-272):
+// Encoder symbol of the GPU encode kernel (16 bytes), from
+// RansEncSymbolInit (rANS_word.h:201-272):
+//   x_max = ((L >> bits) << 16) * f - 1
 //   rcp   = ceil(2^(s+31)/f) with s = ceil(log2 f), or ~0 when f < 2
-//   info  = f (13 b) | bias << 13 (13 b) | (rcp_shift-32) << 26 (6 b)
-// x_max and cmpl_freq are recomputed from f and the scale bits.
-struct EncSym { uint32_t rcp, info; };
+//   bias  = start (f >= 2) or start + 2^bits - 1 (f < 2)
+//   cmpl_sh = (2^bits - f) | (rcp_shift - 32) << 16
+struct EncSym { uint32_t rcp, xmax, bias, cmpl_sh; };
 
 inline EncSym make_encsym(uint32_t start, uint32_t f, int bits) {
     EncSym e;
-    uint32_t bias, sh;
+    uint32_t sh;
+    e.xmax = ((RANS_LOW >> bits) << 16) * f - 1;
     if (f < 2) {
         e.rcp = ~0u;
         sh = 0;
-        bias = start + (1u << bits) - 1;
+        e.bias = start + (1u << bits) - 1;
     } else {
         uint32_t s = 0;
         while (f > (1u << s)) s++;
         e.rcp = uint32_t(((1ull << (s + 31)) + f - 1) / f);
         sh = s - 1;
-        bias = start;
+        e.bias = start;
     }
-    e.info = (f & 0x1fff) | ((bias & 0x1fff) << 13) | (sh << 26);
+    e.cmpl_sh = (((1u << bits) - f) & 0xffff) | (sh << 16);
     return e;
 }
 

@@ -156,242 +156,6 @@ __global__ __launch_bounds__(256) void k_copy(const CopyItem *items) {
 }
 
 // ---------------------------------------------------------------------------
-// Entropy encoder.  One 64-lane workgroup per stream; lanes z < NX are the
-// rANS states.  Encoder symbols (EncSym, rans_format.hpp) come from a table
-// in global memory: O0 tab[sym], O1 tab[ctx*256 + sym].  Symbol bytes and
-// their table entries do not depend on the state, so they are fetched one
-// block of ENC_B steps ahead of the dependent chain.
-//
-// Per step and lane (RansEncPutSymbol, rANS_word.h:287-336):
-//   renorm   x >= f << (31-bits)  => emit low 16 bits, x >>= 16
-//   encode   q = mulhi(x, rcp) >> sh;  x += bias + q * (2^bits - f)
-// Emitted words grow downward from J.out_end; then the states are flushed
-// below them, state 0 lowest (RansEncFlush order NX-1 .. 0).
-// ---------------------------------------------------------------------------
-constexpr int ENC_B = 16;
-
-struct EncLane {
-    uint32_t rcp[ENC_B], info[ENC_B];
-};
-
-template <bool O1>
-static DEV void enc_fetch(const EncJob &J, int z, int nx, uint32_t isz,
-                          uint32_t lenz, int64_t kb, EncLane &L,
-                          const EncSym *__restrict__ tab) {
-#pragma unroll
-    for (int j = 0; j < ENC_B; j++) {
-        int64_t k = kb - j;
-        uint32_t rcp = 0, info = 0;
-        if (k >= 0) {
-            uint32_t p;
-            bool ok;
-            if (O1) { p = z * isz + uint32_t(k); ok = uint32_t(k) < lenz; }
-            else    { p = uint32_t(nx) * uint32_t(k) + z; ok = p < J.n; }
-            if (ok && z < nx) {
-                uint32_t sym = J.in[p];
-                uint32_t idx = O1 ? uint32_t(J.remap[k ? J.in[p - 1] : 0]) * uint32_t(J.A)
-                                        + J.remap[sym]
-                                  : sym;
-                EncSym e = tab[idx];
-                rcp = e.rcp;
-                info = e.info;
-            }
-        }
-        L.rcp[j] = rcp;
-        L.info[j] = info;
-    }
-}
-
-template <bool O1>
-static DEV void enc_body(const EncJob &J) {
-    const int z = int(lane_id());
-    const int nx = J.nx;
-    const uint32_t n = J.n;
-    const int bits = J.bits;
-    const uint32_t M = 1u << bits;
-    const uint32_t xs = 31 - bits;            // x_max = (f << xs) - 1
-    const EncSym *__restrict__ tab = J.tab;
-
-    uint32_t isz = n / nx, lenz, T;
-    if (O1) {
-        lenz = (z == nx - 1) ? n - uint32_t(nx - 1) * isz : isz;
-        T = n - uint32_t(nx - 1) * isz;
-    } else {
-        lenz = 0;
-        T = (n + nx - 1) / nx;
-    }
-    const uint64_t lanes = (nx == 64) ? ~0ull : ((1ull << nx) - 1);
-    const uint64_t above = (z >= 63) ? 0ull : (~0ull << (z + 1));
-
-    uint16_t *out16 = reinterpret_cast<uint16_t *>(J.out_end);
-    uint32_t x = RANS_LOW_D;
-    uint32_t nw = 0;   // words emitted so far (wave-uniform)
-
-    EncLane cur, nxt;
-    int64_t kb = int64_t(T) - 1;
-    enc_fetch<O1>(J, z, nx, isz, lenz, kb, cur, tab);
-    for (; kb >= 0; kb -= ENC_B) {
-        enc_fetch<O1>(J, z, nx, isz, lenz, kb - ENC_B, nxt, tab);
-#pragma unroll
-        for (int j = 0; j < ENC_B; j++) {
-            const uint32_t info = cur.info[j];
-            const uint32_t f = info & 0x1fff;
-            const bool act = f != 0;          // inactive lanes / steps carry f = 0
-            const bool c = act && (x >> xs) >= f;
-            const uint64_t m = __ballot(c) & lanes;
-            if (c) {
-                uint32_t rank = __popcll(m & above);
-                out16[-int64_t(nw + rank) - 1] = uint16_t(x);
-                x >>= 16;
-            }
-            nw += __popcll(m);
-            if (act) {
-                const uint32_t q = __umulhi(x, cur.rcp[j]) >> (info >> 26);
-                x += ((info >> 13) & 0x1fff) + q * (M - f);
-            }
-        }
-        cur = nxt;
-    }
-    // flush: state z at bytes [-(2*nw + 4*(nx-z)), +4)
-    if (z < nx) {
-        uint16_t *s = out16 - int64_t(nw) - 2 * int64_t(nx - z);
-        s[0] = uint16_t(x);
-        s[1] = uint16_t(x >> 16);
-    }
-    if (z == 0) *J.out_len = 2 * nw + 4 * uint32_t(nx);
-}
-
-// One launch for every stream of the batch; the order is wave-uniform.
-__global__ __launch_bounds__(64) void k_rans_enc(const EncJob *jobs) {
-    const EncJob J = jobs[blockIdx.x];
-    if (J.remap) enc_body<true>(J);
-    else enc_body<false>(J);
-}
-
-// ---------------------------------------------------------------------------
-// Entropy decoder.  One 64-lane workgroup per stream, lane z = state z.
-// Decode table entries (32 bit): (f-1) << (bits+8) | (slot-start) << 8 | s,
-// rows of 2^bits slots.  O0: one row, s = symbol.  O1: one row per context
-// in alphabet order, s = alphabet index of the symbol (which is also the
-// row of the next step); alpha[s] is the byte written out.
-//   m = x & (2^bits-1); e = row[m]; x = f*(x>>bits) + (m-start)
-//   renorm: if x < 2^15 then x = x<<16 | next word  (RansDecRenorm)
-// Words are consumed in ascending lane order; the compressed words are
-// streamed through an LDS ring one 1 KiB slab ahead of the chain.
-// ---------------------------------------------------------------------------
-constexpr uint32_t RING_WORDS = 4096;       // 8 KiB ring
-constexpr uint32_t SLAB_WORDS = 512;        // 64 lanes x 16 B
-
-template <bool O1>
-static DEV void dec_body(const DecJob &J, uint16_t *ring) {
-    const int z = int(lane_id());
-    const int nx = J.nx;
-    const uint32_t n = J.n;
-    const int bits = J.bits;
-    const uint32_t mask = (1u << bits) - 1;
-    const uint32_t *__restrict__ tab = J.tab;
-
-    // states: 4*nx bytes at the start of the payload
-    uint32_t x = 0;
-    if (z < nx) {
-        const uint8_t *p = J.in + 4 * z;
-        x = p[0] | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
-    }
-    const uint8_t *wbase = J.in + 4 * nx;
-    const uint32_t nwords = (J.in_len - 4 * uint32_t(nx)) / 2;
-
-    // slab loader: lane l fetches 16 bytes (8 words) of slab s
-    auto load_slab = [&](uint32_t s) -> uint4 {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        uint32_t w0 = s * SLAB_WORDS + uint32_t(z) * 8;
-        uint32_t tmp[4] = {0, 0, 0, 0};
-        for (int b = 0; b < 8; b++) {
-            uint32_t w = w0 + b;
-            uint32_t val = 0;
-            if (w < nwords) val = wbase[2 * w] | (uint32_t(wbase[2 * w + 1]) << 8);
-            tmp[b >> 1] |= val << ((b & 1) * 16);
-        }
-        v.x = tmp[0]; v.y = tmp[1]; v.z = tmp[2]; v.w = tmp[3];
-        return v;
-    };
-    auto store_slab = [&](uint32_t s, uint4 v) {
-        uint32_t w0 = (s * SLAB_WORDS + uint32_t(z) * 8) & (RING_WORDS - 1);
-        uint32_t *r32 = reinterpret_cast<uint32_t *>(ring + w0);
-        r32[0] = v.x; r32[1] = v.y; r32[2] = v.z; r32[3] = v.w;
-    };
-
-    uint32_t slabs_in_ring = 0;             // slabs written to the ring
-    uint4 pf = load_slab(0);
-    // fill the first two slabs
-    store_slab(0, pf); slabs_in_ring = 1;
-    pf = load_slab(1);
-    store_slab(1, pf); slabs_in_ring = 2;
-    pf = load_slab(2);
-
-    uint32_t isz = n / nx, lenz, T;
-    if (O1) {
-        lenz = (z == nx - 1) ? n - uint32_t(nx - 1) * isz : isz;
-        T = n - uint32_t(nx - 1) * isz;
-    } else {
-        lenz = 0;
-        T = (n + nx - 1) / nx;
-    }
-    const uint64_t lanes = (nx == 64) ? ~0ull : ((1ull << nx) - 1);
-    uint32_t row = 0;                       // O1 context row (previous symbol)
-    uint32_t ptr = 0;                       // words consumed (wave-uniform)
-    const uint32_t G = nx >= 32 ? 8 : 64;   // steps between ring refills
-
-    for (uint32_t t0 = 0; t0 < T; t0 += G) {
-        // keep >= G*nx words + one slab ahead of the read pointer
-        while (slabs_in_ring * SLAB_WORDS < ptr + G * uint32_t(nx) + SLAB_WORDS &&
-               slabs_in_ring * SLAB_WORDS < nwords + SLAB_WORDS) {
-            store_slab(slabs_in_ring, pf);
-            slabs_in_ring++;
-            pf = load_slab(slabs_in_ring);
-        }
-        const uint32_t t1 = (T - t0 < G) ? T : t0 + G;
-        for (uint32_t t = t0; t < t1; t++) {
-            uint32_t p;
-            bool act;
-            if (O1) { p = z * isz + t; act = z < nx && t < lenz; }
-            else    { p = uint32_t(nx) * t + z; act = z < nx && p < n; }
-            bool c = false;
-            if (act) {
-                const uint32_t e = tab[(row << bits) + (x & mask)];
-                const uint32_t f1 = e >> (bits + 8);
-                const uint32_t y = (e >> 8) & mask;
-                const uint32_t xh = x >> bits;
-                x = f1 * xh + xh + y;
-                if (O1) {
-                    row = e & 0xff;                 // alphabet index of the symbol
-                    J.out[p] = J.alpha[row];
-                } else {
-                    J.out[p] = uint8_t(e);
-                }
-                c = x < RANS_LOW_D;
-            }
-            const uint64_t m = __ballot(c) & lanes;
-            if (c) {
-                uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32),
-                                 __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
-                uint32_t w = ptr + rank;
-                uint32_t word = (w < nwords) ? ring[w & (RING_WORDS - 1)] : 0u;
-                if (w < nwords) x = (x << 16) | word;
-            }
-            ptr += __popcll(m);
-        }
-    }
-    if (z == 0) *J.status = (ptr <= nwords) ? 0 : -1;
-}
-
-__global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
-    __shared__ uint16_t ring[RING_WORDS];
-    const DecJob J = jobs[blockIdx.x];
-    if (J.alpha) dec_body<true>(J, ring);
-    else dec_body<false>(J, ring);
-}
-
-// ---------------------------------------------------------------------------
 // RLE (rle.c:100-189).  Byte i starts a literal unless it repeats the
 // previous byte and that byte is an RLE symbol; the run length stored for
 // an RLE-symbol literal is the number of repeats that follow it, i.e. the
@@ -686,18 +450,6 @@ hipError_t launch_stripe(const StripeItem *d_items, int nitems, uint32_t max_n,
 hipError_t launch_copy(const CopyItem *d_items, int nitems, hipStream_t s) {
     if (!nitems) return hipSuccess;
     hipLaunchKernelGGL(k_copy, dim3(nitems), dim3(256), 0, s, d_items);
-    return hipGetLastError();
-}
-
-hipError_t launch_enc(const EncJob *d_jobs, int njobs, hipStream_t s) {
-    if (!njobs) return hipSuccess;
-    hipLaunchKernelGGL(k_rans_enc, dim3(njobs), dim3(64), 0, s, d_jobs);
-    return hipGetLastError();
-}
-
-hipError_t launch_dec(const DecJob *d_jobs, int njobs, hipStream_t s) {
-    if (!njobs) return hipSuccess;
-    hipLaunchKernelGGL(k_rans_dec, dim3(njobs), dim3(64), 0, s, d_jobs);
     return hipGetLastError();
 }
 
