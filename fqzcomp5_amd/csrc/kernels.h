@@ -57,11 +57,19 @@ struct EncJob {
     const uint8_t *remap;   // O1: byte -> alphabet index (nullptr for O0)
     uint8_t *out_end;       // 2-byte aligned; stream grows downward
     uint32_t *out_len;      // bytes written below out_end
+    uint32_t *ck;           // (nchunks + 1) * nx state checkpoints
+    uint32_t *cnt;          // nchunks word counts, then exclusive offsets
     uint32_t n;
     int32_t nx;             // 4 or 32
     int32_t bits;           // 12 (O0) or 10/12 (O1)
     int32_t A;              // O1 alphabet size
+    uint32_t nchunks;       // ceil(steps / enc_chunk_steps(nx))
 };
+
+// Encoder chunk: steps between state checkpoints (chain and replay agree).
+inline uint32_t enc_chunk_steps(int nx) { return 1024u / uint32_t(nx); }
+// Replay: chunks handled by one 1024-thread workgroup.
+inline uint32_t enc_replay_chunks(int nx) { return 16u * uint32_t(64 / nx); }
 
 // out[i] = *src[i]: single bytes fetched for host decisions.
 struct GatherItem {
@@ -80,8 +88,33 @@ struct DecJob {
     int32_t nx;
     int32_t bits;
     uint32_t rows;          // table rows (1 for O0)
-    uint32_t pad;
+    uint32_t mode;          // DEC_TAB_* (dec_table_mode)
 };
+
+// Decoder table placement (rans_chain.hip).  Per slot of a row of 2^bits:
+//   LDS / GLOBAL  u32 (f-1) << (bits+8) | (slot - start) << 8 | symbol
+//                 (alphabet index for O1), in LDS or read from global memory;
+//   SPLIT (O1)    u8 symbol per slot, then u32 (f-1) << 16 | start per
+//                 (context, symbol) in rows of 2^dec_rp_log(rows) entries.
+enum : uint32_t { DEC_TAB_LDS = 0, DEC_TAB_GLOBAL = 1, DEC_TAB_SPLIT = 2 };
+constexpr uint32_t DEC_TAB_LDS_MAX = 147456;
+__host__ __device__ inline uint32_t dec_rp_log(uint32_t rows) {
+    uint32_t r = 0;
+    while ((1u << r) < rows) r++;
+    return r;
+}
+// 32-bit words of the table image for a mode
+__host__ __device__ inline uint32_t dec_tab_words(uint32_t mode, uint32_t rows, int bits) {
+    const uint32_t slots = rows << bits;
+    if (mode == DEC_TAB_SPLIT) return slots / 4 + (rows << dec_rp_log(rows));
+    return slots;
+}
+inline uint32_t dec_table_mode(bool o1, uint32_t rows, int bits) {
+    if (dec_tab_words(DEC_TAB_LDS, rows, bits) * 4u <= DEC_TAB_LDS_MAX) return DEC_TAB_LDS;
+    if (o1 && dec_tab_words(DEC_TAB_SPLIT, rows, bits) * 4u <= DEC_TAB_LDS_MAX)
+        return DEC_TAB_SPLIT;
+    return DEC_TAB_GLOBAL;
+}
 
 // RLE encode of one leaf input; saved[] marks the RLE symbols.
 struct RleItem {
@@ -131,8 +164,13 @@ hipError_t launch_copy(const CopyItem *d_items, int nitems, hipStream_t s);
 // `lds` = dynamic LDS bytes: the maximum of enc_lds_bytes/dec_lds_bytes
 // over the launch's jobs.
 uint32_t enc_lds_bytes(int o1, uint32_t A);
-uint32_t dec_lds_bytes(uint32_t rows, int bits);
-hipError_t launch_enc(const EncJob *d_jobs, int njobs, uint32_t lds, hipStream_t s);
+uint32_t enc_replay_lds_bytes(int o1, uint32_t A);
+uint32_t dec_lds_bytes(uint32_t rows, int bits, int mode);
+hipError_t launch_enc_chain(const EncJob *d_jobs, int njobs, uint32_t lds, hipStream_t s);
+// d_items: uint32 pairs {job index, first chunk}
+hipError_t launch_enc_replay(const EncJob *d_jobs, const uint32_t *d_items, int nitems,
+                             bool emit, uint32_t lds, hipStream_t s);
+hipError_t launch_enc_scan(const EncJob *d_jobs, int njobs, hipStream_t s);
 hipError_t launch_dec(const DecJob *d_jobs, int njobs, uint32_t lds, hipStream_t s);
 
 }  // namespace fqz5

@@ -4,11 +4,15 @@
 // 16-bit renormalisation words are interleaved into one byte stream; that
 // parallelism is fixed by the format (SURVEY.md §7 hard part (i)).  One
 // 64-lane wave owns one stream and lane z owns state z; throughput comes
-// from running every stream of a batch at once, so the per-step cost of a
-// single chain is what these kernels minimise:
-//   * symbol tables live in LDS (template TLDS) and are read with ds_read;
-//   * everything that does not depend on the state (symbol bytes, table
-//     entries, output bytes) is staged by all 64 lanes outside the chain;
+// from running every stream of a batch at once, so the per-step latency of
+// a single chain is what these kernels minimise.  A wave64 VALU instruction
+// costs at least 4 cycles whatever its exec mask, so the rule is: the fewest
+// instructions per step on the chain, everything else amortised over
+// chunks of steps and done by all 64 lanes (measured with tools/ubench.hip
+// and tools/chain_probe.hip):
+//   * symbol tables live in LDS and are read with ds_read;
+//   * symbol bytes are fetched with bounds-checked buffer loads (reads past
+//     the end return 0), one chunk ahead, by all lanes;
 //   * word emission / consumption order across states comes from a ballot
 //     and an in-register rank, with no branches on the chain.
 //
@@ -31,6 +35,20 @@ namespace fqz5 {
 #define DEV __device__ __forceinline__
 
 extern __shared__ uint4 chain_lds[];
+#ifdef FQZ5_CHAIN_PROBE
+__device__ uint64_t g_probe[8];
+#endif
+
+// Raw buffer over [p, p+n): loads past n return 0, stores past n are dropped.
+static DEV __amdgpu_buffer_rsrc_t buf(const void *p, uint32_t n) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, n, 0x00020000);
+}
+static DEV uint32_t ld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+}
+static DEV void st8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v), r, off, 0, 0);
+}
 
 // ===========================================================================
 // Encoder
@@ -41,21 +59,43 @@ extern __shared__ uint4 chain_lds[];
 //   encode  q = mulhi(x, rcp) >> shift;  x += bias + q * cmpl
 // q < 2^21 (x <= x_max < f << 21) so q * cmpl is a 24-bit multiply.
 // Steps outside the input carry the identity symbol {0, ~0, 0, 0}.
-constexpr int ENC_W = 16;                  // steps staged per lane per chunk
-constexpr uint32_t WRING = 2048;           // renorm-word ring (words)
-constexpr uint32_t ENC_ENT_BYTES = 16384;  // S * NX * 16 (S*NX = 1024)
-constexpr uint32_t ENC_RING_BYTES = 2 * (WRING + 64);
-constexpr uint32_t ENC_LDS_BASE = ENC_ENT_BYTES + ENC_RING_BYTES + 256;
+//
+// Encoding is split so that the only sequential work is the bare chain:
+//   1. k_enc_chain   one wave per stream runs the NX chains (7 VALU ops and
+//                    one LDS read per step) and checkpoints the states at
+//                    every chunk of S = 1024/NX steps;
+//   2. k_enc_replay  every chunk of every stream is re-run from its
+//                    checkpoint in parallel (64/NX chunks per wave), counting
+//                    the renormalisation words each chunk emits;
+//   3. k_enc_scan    per stream, exclusive scan of the chunk word counts;
+//   4. k_enc_replay  again, writing every word straight to its final place
+//                    (and the final states after the last chunk).
+// Chunks are aligned to S from step 0: chunk j holds steps [jS, jS+S) and is
+// processed in descending j; checkpoint c (= jtop - j) is the state before
+// chunk j.  The word order is the reference's: steps from the top of the
+// input down, within a step the lanes in descending order, the stream
+// growing downward from out_end.
+constexpr uint32_t ENC_ENT = 1024;                        // entries per chunk
+constexpr uint32_t ENC_ENT_BYTES = (ENC_ENT + 512) * 16;  // + chain over-read
+constexpr uint32_t ENC_LDS_BASE = ENC_ENT_BYTES + 256;    // + remap
 constexpr uint32_t ENC_TAB_LDS_MAX = 65536;
+constexpr int REPLAY_THREADS = 1024;
+constexpr int ENC_W = 16;                    // replay: steps per byte batch
+
+template <int NX> constexpr uint32_t enc_chunk() { return ENC_ENT / NX; }
+
+template <bool O1, int NX>
+static DEV uint32_t enc_steps(uint32_t n) {
+    return O1 ? n - uint32_t(NX - 1) * (n / NX) : (n + NX - 1) / NX;
+}
 
 template <bool O1, int NX, bool TLDS>
-static DEV void enc_body(const EncJob &J) {
-    constexpr uint32_t S = uint32_t(64 / NX) * ENC_W;   // steps per chunk
-    constexpr uint64_t LANES = (1ull << NX) - 1;
+static DEV void chain_body(const EncJob &J) {
+    constexpr uint32_t S = enc_chunk<NX>();
+    constexpr int R = int(ENC_ENT / 64);           // entries staged per lane
     uint8_t *lds = reinterpret_cast<uint8_t *>(chain_lds);
     uint4 *ent = reinterpret_cast<uint4 *>(lds);
-    uint16_t *wring = reinterpret_cast<uint16_t *>(lds + ENC_ENT_BYTES);
-    uint8_t *rm = lds + ENC_ENT_BYTES + ENC_RING_BYTES;
+    uint8_t *rm = lds + ENC_ENT_BYTES;
     uint4 *ltab = reinterpret_cast<uint4 *>(lds + ENC_LDS_BASE);
 
     const int l = int(threadIdx.x);
@@ -71,133 +111,264 @@ static DEV void enc_body(const EncJob &J) {
     const uint4 *tab = TLDS ? ltab : gtab;
 
     const uint32_t isz = n / NX;
-    const uint32_t T = O1 ? n - uint32_t(NX - 1) * isz : (n + NX - 1) / NX;
-    // staging: lane l stages chain zs for steps kh - sub*W - w, w < W
-    const int zs = l % NX, sub = l / NX;
-    const uint32_t lens = O1 ? ((zs == NX - 1) ? T : isz) : 0;
-    const uint8_t *__restrict__ in = J.in;
+    const uint32_t T = enc_steps<O1, NX>(n);
+    const uint32_t jtop = (T - 1) / S;
+    const auto in = buf(J.in, n);
 
-    // b[w] = symbol of step k_w;  b[W] = context byte of step k_{W-1} (O1)
-    auto load_bytes = [&](int64_t kh, uint32_t *b) {
+    // Staged entry r of lane l is i = l + 64r: O0 (step kk, lane z) with
+    // i = kk*NX + z; O1 chain-major, i = z*S + kk.  It lands at
+    // ent[(S-1-kk)*NX + z] so that the chain reads ascending addresses.
+    uint32_t sb[R], cb[R];
+    auto issue = [&](uint32_t j) {
 #pragma unroll
-        for (int w = 0; w <= ENC_W; w++) {
-            const int64_t k = kh - int64_t(sub) * ENC_W - w;
-            uint32_t v = 0;
+        for (int r = 0; r < R; r++) {
+            const uint32_t i = uint32_t(l) + 64u * r;
             if (O1) {
-                if (k >= 0 && k < int64_t(lens)) v = in[zs * isz + uint32_t(k)];
-            } else if (w < ENC_W && k >= 0) {
-                const uint64_t p = uint64_t(NX) * uint64_t(k) + zs;
-                if (p < n) v = in[p];
+                const uint32_t z = i / S, k = j * S + i % S;
+                sb[r] = ld8(in, z * isz + k);
+                cb[r] = ld8(in, z * isz + k - 1u);
+            } else {
+                sb[r] = ld8(in, NX * S * j + i);
             }
-            b[w] = v;
+        }
+    };
+    const uint4 ID = make_uint4(0, 0xffffffffu, 0, 0);
+    auto stage = [&](uint32_t j) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const uint32_t i = uint32_t(l) + 64u * r;
+            uint32_t z, kk, idx;
+            bool ok;
+            if (O1) {
+                z = i / S;
+                kk = i % S;
+                const uint32_t k = j * S + kk;
+                ok = k < ((z == NX - 1) ? T : isz);
+                const uint32_t ctx = k ? cb[r] : 0u;
+                idx = uint32_t(rm[ctx]) * A + rm[sb[r]];
+            } else {
+                z = i % NX;
+                kk = i / NX;
+                ok = NX * S * j + i < n;
+                idx = sb[r];
+            }
+            uint4 e = tab[ok ? idx : 0u];
+            if (!ok) e = ID;
+            ent[(S - 1 - kk) * NX + z] = e;
         }
     };
 
-    uint32_t cb[ENC_W + 1], nb[ENC_W + 1];
-    int64_t kh = int64_t(T) - 1;
-    load_bytes(kh, cb);
+    issue(jtop);
     __syncthreads();
+    stage(jtop);
 
     const int zl = l & (NX - 1);
-    const bool chain = l < NX;
-    const uint64_t above = (l >= 63) ? 0ull : (LANES & (~0ull << (l + 1)));
+    const bool writer = l < NX;
     uint32_t x = RANS_LOW_D;
-    uint32_t nw = 0, flushed = 0;       // words emitted / written out
-    uint16_t *out16 = reinterpret_cast<uint16_t *>(J.out_end);
-    const uint4 ID = make_uint4(0, 0xffffffffu, 0, 0);
+    uint32_t *ck = J.ck + zl;
+    const uint4 *ep = ent + zl;
 
     auto step = [&](const uint4 e) {
-        const uint32_t xo = x;
-        const bool c = xo > e.y;
-        const uint32_t xr = c ? (xo >> 16) : xo;
+        const bool c = x > e.y;
+        const uint32_t xr = c ? (x >> 16) : x;
         const uint32_t q = __umulhi(xr, e.x) >> (e.w >> 16);
         x = __umul24(q, e.w & 0xffffu) + (xr + e.z);
-        const uint64_t m = __ballot(c) & LANES;
-        const uint32_t g = nw + __popcll(m & above);
-        wring[(c && chain) ? (g & (WRING - 1)) : (WRING + l)] = uint16_t(xo);
-        nw += __popcll(m);
     };
 
-    for (; kh >= 0; kh -= int64_t(S)) {
-        load_bytes(kh - int64_t(S), nb);              // next chunk, in flight
-        // ---- stage the encoder symbols of this chunk ----
+#ifdef FQZ5_CHAIN_PROBE
+    uint64_t t_stage = 0, t_chain = 0;
+#endif
+    for (int32_t j = int32_t(jtop); j >= 0; j--) {
+        __syncthreads();
+#ifdef FQZ5_CHAIN_PROBE
+        const uint64_t tp0 = __builtin_amdgcn_s_memtime();
+#endif
+        if (writer) *ck = x;
+        ck += NX;
+        if (j > 0) issue(uint32_t(j - 1));
+        // ---- the chain: entries of block b+1 are read while block b runs
+        // (at most 16 reads in flight, within what lgkmcnt can track);
+        // sched_barrier keeps the compiler from batching all reads up front
+        // The reads of block b+1 are issued after the first step of block b:
+        // the compiler's (conservative) lgkmcnt(0) before that step then
+        // only waits for block b's own reads, issued a block earlier.  (All
+        // 64 lanes run it: limiting exec to the NX state lanes measured
+        // slower here, unlike the decoder.)
+        constexpr int CB = 8;
+        uint4 E[2][CB];
 #pragma unroll
-        for (int w = 0; w < ENC_W; w++) {
-            const int64_t k = kh - int64_t(sub) * ENC_W - w;
-            bool ok;
-            if (O1) ok = k >= 0 && k < int64_t(lens);
-            else ok = k >= 0 && uint64_t(NX) * uint64_t(k) + zs < n;
-            uint4 e = ID;
-            if (ok) {
-                uint32_t idx;
-                if (O1) {
-                    const uint32_t ctx = k ? cb[w + 1] : 0u;
-                    idx = uint32_t(rm[ctx]) * A + rm[cb[w]];
-                } else {
-                    idx = cb[w];
-                }
-                e = tab[idx];
-            }
-            ent[(uint32_t(sub) * ENC_W + w) * NX + zs] = e;
+        for (int i = 0; i < CB; i++) E[0][i] = ep[i * NX];
+#pragma unroll
+        for (uint32_t b = 0; b < S / CB; b++) {
+            step(E[b & 1][0]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < CB; i++) E[(b + 1) & 1][i] = ep[(CB * (b + 1) + i) * NX];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 1; i < CB; i++) step(E[b & 1][i]);
+            __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();
-        // ---- the chain: entries are read 8 steps ahead ----
-        uint4 E0[8], E1[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) E0[j] = ent[j * NX + zl];
-        for (uint32_t t = 0; t < S; t += 16) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) E1[j] = ent[(t + 8 + j) * NX + zl];
-#pragma unroll
-            for (int j = 0; j < 8; j++) step(E0[j]);
-            if (t + 16 < S) {
-#pragma unroll
-                for (int j = 0; j < 8; j++) E0[j] = ent[(t + 16 + j) * NX + zl];
-            }
-#pragma unroll
-            for (int j = 0; j < 8; j++) step(E1[j]);
-        }
-        __syncthreads();
-        // ---- complete 512-word groups: 16-byte stores, words reversed ----
-        while (nw - flushed >= 512) {
-            // words f .. f+511 live at ring[f & mask ...]; memory order is
-            // descending word index: lane l covers words f+504-8l .. f+511-8l
-            const uint32_t base = (flushed + 504 - 8 * l) & (WRING - 1);
-            const uint4 v = *reinterpret_cast<const uint4 *>(wring + base);
-            uint4 r;
-            r.x = __builtin_amdgcn_alignbit(v.w, v.w, 16);
-            r.y = __builtin_amdgcn_alignbit(v.z, v.z, 16);
-            r.z = __builtin_amdgcn_alignbit(v.y, v.y, 16);
-            r.w = __builtin_amdgcn_alignbit(v.x, v.x, 16);
-            reinterpret_cast<uint4 *>(out16 - int64_t(flushed) - 512)[l] = r;
-            flushed += 512;
-        }
-#pragma unroll
-        for (int w = 0; w <= ENC_W; w++) cb[w] = nb[w];
+#ifdef FQZ5_CHAIN_PROBE
+        const uint64_t tp1 = __builtin_amdgcn_s_memtime();
+        t_chain += tp1 - tp0;
+#endif
+        if (j > 0) stage(uint32_t(j - 1));
+#ifdef FQZ5_CHAIN_PROBE
+        t_stage += __builtin_amdgcn_s_memtime() - tp1;
+#endif
     }
-    __syncthreads();
-    for (uint32_t g = flushed + l; g < nw; g += 64)
-        out16[-int64_t(g) - 1] = wring[g & (WRING - 1)];
-    // states: state z at bytes [-(2*nw + 4*(NX-z)), +4) (RansEncFlush order)
-    if (chain) {
-        uint16_t *s = out16 - int64_t(nw) - 2 * int64_t(NX - l);
-        s[0] = uint16_t(x);
-        s[1] = uint16_t(x >> 16);
-    }
-    if (l == 0) *J.out_len = 2 * nw + 4 * uint32_t(NX);
+    if (writer) *ck = x;                              // checkpoint nchunks
+#ifdef FQZ5_CHAIN_PROBE
+    if (l == 0) { g_probe[0] += t_stage; g_probe[1] += t_chain; }
+#endif
 }
 
-__global__ __launch_bounds__(64) void k_rans_enc(const EncJob *jobs) {
+__global__ __launch_bounds__(64) void k_enc_chain(const EncJob *jobs) {
     const EncJob J = jobs[blockIdx.x];
     const bool o1 = J.remap != nullptr;
     const uint32_t ntab = o1 ? uint32_t(J.A) * uint32_t(J.A) : 256u;
     const bool tl = ntab * 16u <= ENC_TAB_LDS_MAX;
     if (o1) {
-        if (J.nx == 32) { if (tl) enc_body<true, 32, true>(J); else enc_body<true, 32, false>(J); }
-        else            { if (tl) enc_body<true, 4, true>(J);  else enc_body<true, 4, false>(J); }
+        if (J.nx == 32) { if (tl) chain_body<true, 32, true>(J); else chain_body<true, 32, false>(J); }
+        else            { if (tl) chain_body<true, 4, true>(J);  else chain_body<true, 4, false>(J); }
     } else {
-        if (J.nx == 32) enc_body<false, 32, true>(J);
-        else            enc_body<false, 4, true>(J);
+        if (J.nx == 32) chain_body<false, 32, true>(J);
+        else            chain_body<false, 4, true>(J);
+    }
+}
+
+// Replay of chunks c0 .. c0 + 16*(64/NX) - 1 of one stream; wave w, lane l
+// re-runs state z = l % NX of chunk c0 + w*(64/NX) + l/NX from its
+// checkpoint.  Without EMIT it stores the chunk's word count; with EMIT the
+// counts have become exclusive offsets and the words are written.
+template <bool O1, int NX, bool TLDS, bool EMIT>
+static DEV void replay_body(const EncJob &J, uint32_t c0) {
+    constexpr uint32_t S = enc_chunk<NX>();
+    constexpr uint32_t G = 64 / NX;
+    constexpr uint64_t LANES = (NX == 32) ? 0xffffffffull : ((1ull << NX) - 1);
+    uint8_t *lds = reinterpret_cast<uint8_t *>(chain_lds);
+    uint8_t *rm = lds;
+    uint4 *ltab = reinterpret_cast<uint4 *>(lds + 256);
+    const int tid = int(threadIdx.x);
+    const uint32_t n = J.n;
+    const uint32_t A = uint32_t(J.A);
+    const uint4 *gtab = reinterpret_cast<const uint4 *>(J.tab);
+    if (TLDS) {
+        const uint32_t ntab = O1 ? A * A : 256u;
+        for (uint32_t i = tid; i < ntab; i += REPLAY_THREADS) ltab[i] = gtab[i];
+    }
+    if (O1)
+        for (int i = tid; i < 256; i += REPLAY_THREADS) rm[i] = J.remap[i];
+    __syncthreads();
+    const uint4 *tab = TLDS ? ltab : gtab;
+
+    const int l = tid & 63;
+    const uint32_t c = c0 + uint32_t(tid >> 6) * G + uint32_t(l / NX);
+    if (c0 + uint32_t(tid >> 6) * G >= J.nchunks) return;   // whole wave idle
+    const int z = l % NX;
+    const int gsh = (l / NX) * NX;
+    const bool act = c < J.nchunks;
+    const uint32_t isz = n / NX;
+    const uint32_t T = enc_steps<O1, NX>(n);
+    const uint32_t lens = O1 ? ((z == NX - 1) ? T : isz) : 0;
+    const uint8_t *__restrict__ in = J.in;
+    uint32_t x = act ? J.ck[uint64_t(c) * NX + z] : RANS_LOW_D;
+    // chunk c covers steps [j*S, j*S + S) with j = nchunks - 1 - c
+    const int64_t khi = (int64_t(J.nchunks) - int64_t(c)) * S - 1;
+    const uint32_t base = (EMIT && act) ? J.cnt[c] : 0u;
+    uint32_t cnt = 0;
+    uint16_t *out16 = reinterpret_cast<uint16_t *>(J.out_end);
+
+    for (uint32_t t0 = 0; t0 < S; t0 += ENC_W) {
+        uint32_t b[ENC_W + 1];
+        bool ok[ENC_W];
+#pragma unroll
+        for (int w = 0; w <= ENC_W; w++) {
+            const int64_t k = khi - int64_t(t0) - w;
+            uint32_t v = 0;
+            bool o;
+            if (O1) {
+                o = act && k >= 0 && k < int64_t(lens);
+                if (o) v = in[z * isz + uint32_t(k)];
+            } else {
+                o = act && w < ENC_W && k >= 0 && uint64_t(NX) * uint64_t(k) + z < n;
+                if (o) v = in[uint64_t(NX) * uint64_t(k) + z];
+            }
+            b[w] = v;
+            if (w < ENC_W) ok[w] = o;
+        }
+#pragma unroll
+        for (int w = 0; w < ENC_W; w++) {
+            uint4 e = make_uint4(0, 0xffffffffu, 0, 0);
+            if (ok[w]) {
+                const int64_t k = khi - int64_t(t0) - w;
+                const uint32_t idx = O1 ? uint32_t(rm[k ? b[w + 1] : 0u]) * A + rm[b[w]] : b[w];
+                e = tab[idx];
+            }
+            const uint32_t xo = x;
+            const bool cf = xo > e.y;
+            const uint32_t xr = cf ? (xo >> 16) : xo;
+            const uint32_t q = __umulhi(xr, e.x) >> (e.w >> 16);
+            x = __umul24(q, e.w & 0xffffu) + (xr + e.z);
+            const uint64_t gm = (__ballot(cf) >> gsh) & LANES;
+            if (EMIT && cf)
+                out16[-int64_t(base + cnt + uint32_t(__popcll(gm >> (z + 1)))) - 1] = uint16_t(xo);
+            cnt += uint32_t(__popcll(gm));
+        }
+    }
+    if (!EMIT) {
+        if (act && z == 0) J.cnt[c] = cnt;
+    } else if (act && c == J.nchunks - 1) {
+        // states: state z at bytes [-(2*nw + 4*(NX-z)), +4) (RansEncFlush order)
+        const uint32_t tot = base + cnt;
+        uint16_t *s = out16 - int64_t(tot) - 2 * int64_t(NX - z);
+        s[0] = uint16_t(x);
+        s[1] = uint16_t(x >> 16);
+        if (z == 0) *J.out_len = 2 * tot + 4 * uint32_t(NX);
+    }
+}
+
+template <bool EMIT>
+__global__ __launch_bounds__(REPLAY_THREADS) void k_enc_replay(const EncJob *jobs,
+                                                              const uint2 *items) {
+    const uint2 it = items[blockIdx.x];
+    const EncJob J = jobs[it.x];
+    const bool o1 = J.remap != nullptr;
+    const uint32_t ntab = o1 ? uint32_t(J.A) * uint32_t(J.A) : 256u;
+    const bool tl = ntab * 16u <= ENC_TAB_LDS_MAX;
+    if (o1) {
+        if (J.nx == 32) { if (tl) replay_body<true, 32, true, EMIT>(J, it.y); else replay_body<true, 32, false, EMIT>(J, it.y); }
+        else            { if (tl) replay_body<true, 4, true, EMIT>(J, it.y);  else replay_body<true, 4, false, EMIT>(J, it.y); }
+    } else {
+        if (J.nx == 32) replay_body<false, 32, true, EMIT>(J, it.y);
+        else            replay_body<false, 4, true, EMIT>(J, it.y);
+    }
+}
+
+// Exclusive scan of one stream's chunk word counts, in place.
+__global__ __launch_bounds__(1024) void k_enc_scan(const EncJob *jobs) {
+    __shared__ uint32_t part[1024];
+    const EncJob J = jobs[blockIdx.x];
+    const uint32_t nc = J.nchunks, t = threadIdx.x;
+    const uint32_t per = (nc + 1023) / 1024;
+    const uint32_t b = min(nc, t * per), e = min(nc, b + per);
+    uint32_t s = 0;
+    for (uint32_t i = b; i < e; i++) s += J.cnt[i];
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint32_t v = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - s;
+    for (uint32_t i = b; i < e; i++) {
+        const uint32_t v = J.cnt[i];
+        J.cnt[i] = run;
+        run += v;
     }
 }
 
@@ -206,25 +377,38 @@ uint32_t enc_lds_bytes(int o1, uint32_t A) {
     return ENC_LDS_BASE + (ntab * 16u <= ENC_TAB_LDS_MAX ? ntab * 16u : 0u);
 }
 
+uint32_t enc_replay_lds_bytes(int o1, uint32_t A) {
+    const uint32_t ntab = o1 ? A * A : 256u;
+    return 256u + (ntab * 16u <= ENC_TAB_LDS_MAX ? ntab * 16u : 0u);
+}
+
 // ===========================================================================
 // Decoder
 // ===========================================================================
-// Table entries (32 bit): (f-1) << (bits+8) | (slot-start) << 8 | s, rows of
-// 2^bits slots.  O0: one row, s = symbol.  O1: one row per context in
-// alphabet order, s = alphabet index of the symbol, which is also the next
-// step's row; alpha[s] is the output byte.  Per step (RansDecAdvance +
-// RansDecRenorm, rANS_word.h:145-161, :439-448):
-//   e = row[x & (2^bits-1)];  x = f*(x>>bits) + (slot-start)
+// Per step (RansDecAdvance + RansDecRenorm, rANS_word.h:145-161, :439-448):
+//   slot = x & (2^bits-1);  x = f*(x>>bits) + slot - start
 //   if x < 2^15: x = x << 16 | next word
-constexpr uint32_t RING_WORDS = 4096;      // words per ring copy
-constexpr uint32_t SLAB_WORDS = 512;       // 64 lanes x 8 words
-constexpr uint32_t DEC_OBUF = 1024;        // staged output bytes per group
-constexpr uint32_t DEC_TAB_LDS_MAX = 114688;
-// LDS: 4 ring copies (NX=4 window) | obuf (+64 dummy bytes) | alpha | table
-constexpr uint32_t DEC_LDS_BASE = 4 * 2 * RING_WORDS + DEC_OBUF + 64 + 256;
+// Tables (kernels.h dec_table_mode): LDS/GLOBAL hold per slot the u32
+// (f-1) << 16 | (slot-start) and the u8 symbol; SPLIT (O1 tables too big
+// for that in LDS) holds the u8 symbol per slot and (f-1) << 16 | start per
+// (context, symbol), two dependent LDS reads.  For O1 the symbol is the
+// alphabet index, which is also the next step's row; alpha[] maps it back.
+//
+// Words are staged from global memory into an LDS ring in slabs of 512.
+// NX=4: each step reads the 4-word window at the (uniform) read pointer
+// with one unaligned ds_read_b64 issued a step ahead, and lane z takes the
+// word at its rank among the renormalising lanes, from a 64-bit shift.
+// NX=32: the renormalising lanes read ring[ptr + rank] directly.
+constexpr uint32_t RING_WORDS = 4096;
+constexpr uint32_t SLAB_WORDS = 512;                      // 64 lanes x 8 words
+constexpr uint32_t DEC_OBUF = 1024;                       // output bytes / group
+constexpr uint32_t DEC_RING_BYTES = RING_WORDS * 2 + 16;  // + wrap copy
+constexpr uint32_t DEC_OBUF_BYTES = DEC_OBUF + 2048 + 128;  // + idle-lane sink
+constexpr uint32_t DEC_LDS_BASE = DEC_RING_BYTES + DEC_OBUF_BYTES + 256;
+static_assert(DEC_LDS_BASE % 16 == 0, "table alignment");
 
 struct DecShared {
-    uint16_t *ring;     // NX=4: 4 copies, copy k holds word (i + k) at i
+    uint16_t *ring;
     uint8_t *obuf;
     uint8_t *alpha;
     uint32_t *ltab;
@@ -234,213 +418,341 @@ static DEV DecShared dec_shared() {
     uint8_t *lds = reinterpret_cast<uint8_t *>(chain_lds);
     DecShared d;
     d.ring = reinterpret_cast<uint16_t *>(lds);
-    d.obuf = lds + 8 * RING_WORDS;
-    d.alpha = d.obuf + DEC_OBUF + 64;
+    d.obuf = lds + DEC_RING_BYTES;
+    d.alpha = d.obuf + DEC_OBUF_BYTES;
     d.ltab = reinterpret_cast<uint32_t *>(lds + DEC_LDS_BASE);
     return d;
 }
 
-// Lane z fetches words [s*512 + 8z, +8) of the payload (beyond the end: 0).
-static DEV uint4 load_slab(const uint8_t *wbase, uint32_t nwords, uint32_t s, int z) {
-    uint32_t t[4] = {0, 0, 0, 0};
-    const uint32_t w0 = s * SLAB_WORDS + uint32_t(z) * 8;
+// Lane z fetches words [s*512 + 8z, +8) of the payload (past the end: 0).
+static DEV uint4 load_slab(__amdgpu_buffer_rsrc_t w, uint32_t s, int z) {
+    uint32_t t[4];
+    const uint32_t b0 = (s * SLAB_WORDS + uint32_t(z) * 8) * 2;
 #pragma unroll
-    for (int b = 0; b < 8; b++) {
-        const uint32_t w = w0 + b;
-        uint32_t v = 0;
-        if (w < nwords) v = wbase[2 * w] | (uint32_t(wbase[2 * w + 1]) << 8);
-        t[b >> 1] |= v << ((b & 1) * 16);
-    }
+    for (int b = 0; b < 4; b++)
+        t[b] = ld8(w, b0 + 4 * b) | (ld8(w, b0 + 4 * b + 1) << 8) |
+               (ld8(w, b0 + 4 * b + 2) << 16) | (ld8(w, b0 + 4 * b + 3) << 24);
     return make_uint4(t[0], t[1], t[2], t[3]);
 }
 
-// Write one slab into the ring; COPIES = 4 keeps the shifted copies of the
-// NX=4 window (copy k, position i = word i+k).
-template <int COPIES>
+// Ring slot = word index mod RING_WORDS; words 0..7 are mirrored past the
+// end so that a 4-word window never wraps.
 static DEV void store_slab(uint16_t *ring, uint32_t s, int z, uint4 v) {
-    const uint32_t w0 = s * SLAB_WORDS + uint32_t(z) * 8;
-    *reinterpret_cast<uint4 *>(ring + (w0 & (RING_WORDS - 1))) = v;
-    if (COPIES > 1) {
-        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 1; k < COPIES; k++)
-#pragma unroll
-            for (int b = 0; b < 8; b++)
-                ring[k * RING_WORDS + ((w0 + b - k) & (RING_WORDS - 1))] =
-                    uint16_t(wd[b >> 1] >> ((b & 1) * 16));
+    const uint32_t w0 = (s * SLAB_WORDS + uint32_t(z) * 8) & (RING_WORDS - 1);
+    *reinterpret_cast<uint4 *>(ring + w0) = v;
+    if (w0 == 0) *reinterpret_cast<uint4 *>(ring + RING_WORDS) = v;
+}
+
+static DEV uint64_t ring_win(const uint16_t *ring, uint32_t ptr) {
+    const uint2 v = *reinterpret_cast<const uint2 *>(
+        __builtin_assume_aligned(ring + (ptr & (RING_WORDS - 1)), 8));
+    return (uint64_t(v.y) << 32) | v.x;
+}
+
+struct DecTabs {
+    const uint32_t *ta;     // LDS/GLOBAL: u32 per slot
+    const uint8_t *ts;      // SPLIT: u8 symbol per slot
+    const uint32_t *fb;     // SPLIT: (f-1) << 16 | start
+};
+
+template <int TM>
+static DEV DecTabs dec_tables(const DecJob &J, const DecShared &sh, int l) {
+    const uint32_t rows = J.rows, slots = rows << J.bits;
+    if (TM != DEC_TAB_GLOBAL) {
+        const uint32_t nw = dec_tab_words(TM, rows, J.bits);
+        for (uint32_t i = l; i < nw; i += 64) sh.ltab[i] = J.tab[i];
+    }
+    const uint32_t *base = TM == DEC_TAB_GLOBAL ? J.tab : sh.ltab;
+    DecTabs t;
+    t.ta = base;
+    t.ts = reinterpret_cast<const uint8_t *>(base);
+    t.fb = base + slots / 4;
+    return t;
+}
+
+// One decode step's table work, split so the caller can order the LDS
+// reads: dec_read issues the (first) table read, dec_finish completes the
+// symbol and the pre-renorm state xd.
+// rowoff: byte offset of the row (row << bits, times 4 for u32 slots).
+template <int TM>
+static DEV uint32_t dec_read(const DecTabs &t, uint32_t rowoff, uint32_t x, uint32_t mask) {
+    if (TM == DEC_TAB_SPLIT) return t.ts[rowoff + (x & mask)];
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(t.ta) + rowoff +
+                                               ((x & mask) << 2));
+}
+template <int TM>
+static DEV uint32_t dec_rowoff(uint32_t sy, int bits) {
+    return (sy & 0xffu) << (TM == DEC_TAB_SPLIT ? bits : bits + 2);
+}
+template <int TM>
+static DEV uint32_t dec_finish(const DecTabs &t, uint32_t rd, uint32_t rowfb, uint32_t x,
+                               int bits, uint32_t mask, uint32_t &xd) {
+    const uint32_t xh = x >> bits;
+    if (TM == DEC_TAB_SPLIT) {
+        const uint32_t e = t.fb[rowfb + rd];
+        xd = __umul24(e >> 16, xh) + xh + (x & mask) - (e & 0xffffu);
+        return rd;
+    } else {
+        xd = __umul24(rd >> (bits + 8), xh) + (xh + ((rd >> 8) & mask));
+        return rd;                       // symbol in the low byte
     }
 }
 
-template <bool O1, int NX, bool TLDS>
-static DEV void dec_body(const DecJob &J) {
+// Output of one group [t0, t0+steps).  LM (NX=4): obuf is lane-major,
+// byte (tt, z) at z*G + tt; otherwise step-major at tt*NX + z.
+template <bool O1, int NX, bool LM>
+static DEV void dec_flush(const DecJob &J, const DecShared &sh, uint32_t t0, uint32_t steps,
+                          int l) {
+    constexpr uint32_t G = DEC_OBUF / NX;
+    const uint32_t n = J.n, isz = n / NX;
+    const auto out = buf(J.out, n);
+    if (O1) {
+        for (uint32_t zc = 0; zc < uint32_t(NX); zc++) {
+            const uint32_t lz = (zc == NX - 1) ? n - uint32_t(NX - 1) * isz : isz;
+            for (uint32_t tt = l; tt < steps; tt += 64) {
+                const uint32_t v = LM ? sh.obuf[zc * G + tt] : sh.obuf[tt * NX + zc];
+                if (t0 + tt < lz) st8(out, zc * isz + t0 + tt, sh.alpha[v]);
+            }
+        }
+    } else {
+        const uint32_t cnt = steps * NX;
+        for (uint32_t i = l; i < cnt; i += 64) {
+            const uint32_t v = LM ? sh.obuf[(i % NX) * G + i / NX] : sh.obuf[i];
+            st8(out, NX * t0 + i, v);          // past n: dropped
+        }
+    }
+}
+
+template <bool O1, int TM>
+static DEV void dec4_body(const DecJob &J) {
+    constexpr int NX = 4;
     constexpr uint32_t G = DEC_OBUF / NX;     // steps per output group
-    constexpr int COPIES = NX == 4 ? 4 : 1;
-    constexpr uint64_t LANES = (1ull << NX) - 1;
     const DecShared sh = dec_shared();
-    const int z = int(threadIdx.x);
+    const int l = int(threadIdx.x);
+    const int z = l & 3;
     const uint32_t n = J.n;
     const int bits = J.bits;
     const uint32_t mask = (1u << bits) - 1;
-    if (TLDS) {
-        const uint32_t ntab = J.rows << bits;
-        for (uint32_t i = z; i < ntab; i += 64) sh.ltab[i] = J.tab[i];
-    }
+    const uint32_t rpl = dec_rp_log(J.rows);
+    const DecTabs tb = dec_tables<TM>(J, sh, l);
     if (O1)
-        for (int i = z; i < 256; i += 64) sh.alpha[i] = i < int(J.rows) ? J.alpha[i] : 0;
-    const uint32_t *tab = TLDS ? sh.ltab : J.tab;
+        for (int i = l; i < 256; i += 64) sh.alpha[i] = i < int(J.rows) ? J.alpha[i] : 0;
 
-    uint32_t x = 0;
-    if (z < NX) {
-        const uint8_t *p = J.in + 4 * z;
+    uint32_t x = 1u << 16;                    // idle lanes: any in-range state
+    if (l < NX) {
+        const uint8_t *p = J.in + 4 * l;
         x = p[0] | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
     }
-    const uint8_t *wbase = J.in + 4 * NX;
     const uint32_t nwords = (J.in_len - 4 * uint32_t(NX)) / 2;
+    const auto wsrc = buf(J.in + 4 * NX, nwords * 2);
     uint32_t slabs = 0;
-    uint4 pf = load_slab(wbase, nwords, 0, z);
-    store_slab<COPIES>(sh.ring, 0, z, pf);
-    pf = load_slab(wbase, nwords, 1, z);
-    store_slab<COPIES>(sh.ring, 1, z, pf);
-    slabs = 2;
-    pf = load_slab(wbase, nwords, 2, z);
+    uint4 pf = load_slab(wsrc, 0, l);
 
     const uint32_t isz = n / NX;
     const uint32_t lenz = O1 ? ((z == NX - 1) ? n - uint32_t(NX - 1) * isz : isz) : 0;
     const uint32_t T = O1 ? n - uint32_t(NX - 1) * isz : (n + NX - 1) / NX;
-    // steps where every lane is active (then a short tail, <= NX-1 steps)
-    const uint32_t Tfull = O1 ? isz : n / NX;
-    uint32_t rowbase = 0;
+    const uint32_t Tfull = O1 ? isz : n / NX;   // steps with all lanes active
+    uint32_t rowbase = 0, rowfb = 0;
     uint32_t ptr = 0;                        // words consumed (uniform)
-    const bool lane_ok = z < NX;
-    __syncthreads();
+    // lane z < NX owns obuf[z*G, +G); idle lanes store into a sink
+    uint8_t *myob = sh.obuf + (l < NX ? uint32_t(l) * G : DEC_OBUF + 64);
+
+    // One step on all lanes.  Order of the LDS traffic: the table read (on
+    // the chain) first, then the window of the next words; the symbol is
+    // packed into acc (byte u&3) and 16 symbols go out in one store.
+    auto fstep = [&](uint32_t &acc, int u) {
+        const uint32_t rd = dec_read<TM>(tb, rowbase, x, mask);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t win = ring_win(sh.ring, ptr);
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t xd;
+        const uint32_t sy = dec_finish<TM>(tb, rd, rowfb, x, bits, mask, xd);
+        const bool c = xd < RANS_LOW_D;
+        const uint64_t m = __ballot(c);
+        const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
+        const uint32_t w = uint32_t(win >> r16);
+        x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
+        ptr += uint32_t(__popcll(m & 15u));
+        // acc byte (u&3) <- sy byte 0, other bytes kept
+        constexpr uint32_t SEL[4] = {0x07060500u, 0x07060004u, 0x07000504u, 0x00060504u};
+        acc = __builtin_amdgcn_perm(acc, sy, SEL[u & 3]);
+        if (O1) { rowbase = dec_rowoff<TM>(sy, bits); rowfb = (sy & 0xffu) << rpl; }
+    };
 
     for (uint32_t t0 = 0; t0 < T; t0 += G) {
-        while (slabs * SLAB_WORDS < ptr + G * uint32_t(NX) + SLAB_WORDS &&
-               slabs * SLAB_WORDS < nwords + SLAB_WORDS) {
-            store_slab<COPIES>(sh.ring, slabs, z, pf);
+        // keep the ring 2.5 groups of words ahead, never overwriting unread words
+        while (slabs * SLAB_WORDS < ptr + 2560 && slabs * SLAB_WORDS < nwords + SLAB_WORDS) {
+            store_slab(sh.ring, slabs, l, pf);
             slabs++;
-            pf = load_slab(wbase, nwords, slabs, z);
+            pf = load_slab(wsrc, slabs, l);
         }
         __syncthreads();
         const uint32_t t1 = (T - t0 < G) ? T : t0 + G;
         const uint32_t tf = t1 < Tfull ? t1 : (t0 > Tfull ? t0 : Tfull);
         uint32_t t = t0;
-        // ---- all lanes active ----
-        if (NX == 4) {
-            // 4-word window at ptr, read from copy (ptr & 3) before each step
-            for (; t < tf; t++) {
-                const uint32_t k = ptr & 3;
-                const uint2 wv = *reinterpret_cast<const uint2 *>(
-                    sh.ring + k * RING_WORDS + ((ptr - k) & (RING_WORDS - 1)));
-                const uint64_t win = (uint64_t(wv.y) << 32) | wv.x;
-                const uint32_t e = tab[rowbase + (x & mask)];
-                const uint32_t xh = x >> bits;
-                const uint32_t xd = __umul24(e >> (bits + 8), xh) + xh + ((e >> 8) & mask);
-                const bool c = xd < RANS_LOW_D;
-                const uint64_t m = __ballot(c) & LANES;
-                const uint32_t rank = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u);
-                const uint32_t w = uint32_t(win >> (rank * 16));
-                x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
-                ptr += __popcll(m);
-                // lanes >= NX write to a dummy byte
-                sh.obuf[lane_ok ? (t - t0) * NX + z : DEC_OBUF + z] = uint8_t(e);
-                if (O1) rowbase = (e & 0xffu) << bits;
-            }
-        } else {
-            for (; t < tf; t++) {
-                const uint32_t e = tab[rowbase + (x & mask)];
-                const uint32_t xh = x >> bits;
-                const uint32_t xd = __umul24(e >> (bits + 8), xh) + xh + ((e >> 8) & mask);
-                const bool c = lane_ok && xd < RANS_LOW_D;
-                const uint64_t m = __ballot(c) & LANES;
-                const uint32_t rank = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u);
-                const uint32_t w = sh.ring[(ptr + rank) & (RING_WORDS - 1)];
-                x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
-                ptr += __popcll(m);
-                if (lane_ok) sh.obuf[(t - t0) * NX + z] = uint8_t(e);
-                if (O1) rowbase = (e & 0xffu) << bits;
+        // Full steps on the 4 state lanes only (LDS traffic scales with the
+        // active lanes); ptr stays uniform among them and is re-broadcast.
+        if (l < NX) {
+            for (; t + 16 <= tf; t += 16) {
+                uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll
+                for (int u = 0; u < 4; u++) fstep(a0, u);
+#pragma unroll
+                for (int u = 4; u < 8; u++) fstep(a1, u);
+#pragma unroll
+                for (int u = 8; u < 12; u++) fstep(a2, u);
+#pragma unroll
+                for (int u = 12; u < 16; u++) fstep(a3, u);
+                *reinterpret_cast<uint4 *>(myob + (t - t0)) = make_uint4(a0, a1, a2, a3);
             }
         }
-        // ---- tail: only some lanes active ----
+        ptr = __builtin_amdgcn_readfirstlane(ptr);
+        t = __builtin_amdgcn_readfirstlane(t);
+        // rest: byte stores; the last <= NX-1 steps have idle lanes
         for (; t < t1; t++) {
-            const bool act = lane_ok && (O1 ? t < lenz : uint32_t(NX) * t + z < n);
-            uint32_t w = 0;
-            const uint32_t e = tab[rowbase + (x & mask)];
-            const uint32_t xh = x >> bits;
-            const uint32_t xd = __umul24(e >> (bits + 8), xh) + xh + ((e >> 8) & mask);
+            const bool act = l < NX && (O1 ? t < lenz : uint32_t(NX) * t + z < n);
+            const uint32_t rd = dec_read<TM>(tb, rowbase, x, mask);
+            uint32_t xd;
+            const uint32_t sy = dec_finish<TM>(tb, rd, rowfb, x, bits, mask, xd);
+            const uint64_t win = ring_win(sh.ring, ptr);
             const bool c = act && xd < RANS_LOW_D;
-            const uint64_t m = __ballot(c) & LANES;
-            if (c) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u);
-                w = sh.ring[(ptr + rank) & (RING_WORDS - 1)];
-            }
-            ptr += __popcll(m);
+            const uint64_t m = __ballot(c);
+            const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
+            const uint32_t w = uint32_t(win >> r16);
             if (act) {
                 x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
-                sh.obuf[(t - t0) * NX + z] = uint8_t(e);
-                if (O1) rowbase = (e & 0xffu) << bits;
+                myob[t - t0] = uint8_t(sy);
+                if (O1) { rowbase = dec_rowoff<TM>(sy, bits); rowfb = (sy & 0xffu) << rpl; }
             }
+            ptr += uint32_t(__popcll(m & 15u));
         }
         __syncthreads();
-        // ---- write the group out, chain-major for O1 ----
-        const uint32_t steps = t1 - t0, cnt = steps * uint32_t(NX);
-        for (uint32_t i = z; i < cnt; i += 64) {
-            uint32_t zc, tt;
-            if (O1) { zc = i / steps; tt = i % steps; }
-            else    { tt = i / NX; zc = i % NX; }
-            const uint32_t tg = t0 + tt;
-            const uint8_t v = sh.obuf[tt * NX + zc];
-            if (O1) {
-                const uint32_t lz = (int(zc) == NX - 1) ? n - uint32_t(NX - 1) * isz : isz;
-                if (tg < lz) J.out[zc * isz + tg] = sh.alpha[v];
-            } else {
-                const uint32_t p = uint32_t(NX) * tg + zc;
-                if (p < n) J.out[p] = v;
-            }
-        }
+        dec_flush<O1, NX, true>(J, sh, t0, t1 - t0, l);
         __syncthreads();
     }
-    if (z == 0) *J.status = (ptr <= nwords) ? 0 : -1;
+    if (l == 0) *J.status = (ptr <= nwords) ? 0 : -1;
+}
+
+// NX = 32: lanes 0..31 are the states; each renormalising lane reads its
+// word from the ring at ptr + rank.
+template <bool O1, int TM>
+static DEV void dec32_body(const DecJob &J) {
+    constexpr int NX = 32;
+    constexpr uint32_t G = DEC_OBUF / NX;
+    const DecShared sh = dec_shared();
+    const int l = int(threadIdx.x);
+    const int z = l & 31;
+    const uint32_t n = J.n;
+    const int bits = J.bits;
+    const uint32_t mask = (1u << bits) - 1;
+    const uint32_t rpl = dec_rp_log(J.rows);
+    const DecTabs tb = dec_tables<TM>(J, sh, l);
+    if (O1)
+        for (int i = l; i < 256; i += 64) sh.alpha[i] = i < int(J.rows) ? J.alpha[i] : 0;
+    uint32_t x = 1u << 16;
+    if (l < NX) {
+        const uint8_t *p = J.in + 4 * l;
+        x = p[0] | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+    }
+    const uint32_t nwords = (J.in_len - 4 * uint32_t(NX)) / 2;
+    const auto wsrc = buf(J.in + 4 * NX, nwords * 2);
+    uint32_t slabs = 0;
+    uint4 pf = load_slab(wsrc, 0, l);
+    const uint32_t isz = n / NX;
+    const uint32_t lenz = O1 ? ((z == NX - 1) ? n - uint32_t(NX - 1) * isz : isz) : 0;
+    const uint32_t T = O1 ? n - uint32_t(NX - 1) * isz : (n + NX - 1) / NX;
+    uint32_t rowbase = 0, rowfb = 0, ptr = 0;
+    for (uint32_t t0 = 0; t0 < T; t0 += G) {
+        while (slabs * SLAB_WORDS < ptr + 2560 && slabs * SLAB_WORDS < nwords + SLAB_WORDS) {
+            store_slab(sh.ring, slabs, l, pf);
+            slabs++;
+            pf = load_slab(wsrc, slabs, l);
+        }
+        __syncthreads();
+        const uint32_t t1 = (T - t0 < G) ? T : t0 + G;
+        for (uint32_t t = t0; t < t1; t++) {
+            const bool act = l < NX && (O1 ? t < lenz : uint32_t(NX) * t + z < n);
+            uint32_t xd;
+            const uint32_t rd = dec_read<TM>(tb, rowbase, x, mask);
+            const uint32_t sy = dec_finish<TM>(tb, rd, rowfb, x, bits, mask, xd) & 0xffu;
+            const bool c = act && xd < RANS_LOW_D;
+            const uint64_t m = __ballot(c);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u);
+            const uint32_t w = sh.ring[(ptr + rank) & (RING_WORDS - 1)];
+            if (act) {
+                x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
+                sh.obuf[(t - t0) * NX + z] = uint8_t(sy);
+                if (O1) { rowbase = dec_rowoff<TM>(sy, bits); rowfb = sy << rpl; }
+            }
+            ptr += uint32_t(__popcll(m & 0xffffffffull));
+        }
+        __syncthreads();
+        dec_flush<O1, NX, false>(J, sh, t0, t1 - t0, l);
+        __syncthreads();
+    }
+    if (l == 0) *J.status = (ptr <= nwords) ? 0 : -1;
+}
+
+template <bool O1, int TM>
+static DEV void dec_any(const DecJob &J) {
+    if (J.nx == 32) dec32_body<O1, TM>(J);
+    else            dec4_body<O1, TM>(J);
 }
 
 __global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
     const DecJob J = jobs[blockIdx.x];
-    const bool o1 = J.alpha != nullptr;
-    const bool tl = (J.rows << J.bits) * 4u <= DEC_TAB_LDS_MAX;
-    if (o1) {
-        if (J.nx == 32) { if (tl) dec_body<true, 32, true>(J); else dec_body<true, 32, false>(J); }
-        else            { if (tl) dec_body<true, 4, true>(J);  else dec_body<true, 4, false>(J); }
+    const int tm = int(J.mode);
+    if (J.alpha != nullptr) {
+        if (tm == DEC_TAB_LDS) dec_any<true, DEC_TAB_LDS>(J);
+        else if (tm == DEC_TAB_SPLIT) dec_any<true, DEC_TAB_SPLIT>(J);
+        else dec_any<true, DEC_TAB_GLOBAL>(J);
     } else {
-        if (J.nx == 32) dec_body<false, 32, true>(J);
-        else            dec_body<false, 4, true>(J);
+        dec_any<false, DEC_TAB_LDS>(J);
     }
 }
 
-uint32_t dec_lds_bytes(uint32_t rows, int bits) {
-    const uint32_t ntab = rows << bits;
-    return DEC_LDS_BASE + (ntab * 4u <= DEC_TAB_LDS_MAX ? ntab * 4u : 0u);
+uint32_t dec_lds_bytes(uint32_t rows, int bits, int mode) {
+    if (mode == DEC_TAB_GLOBAL) return DEC_LDS_BASE;
+    return DEC_LDS_BASE + dec_tab_words(uint32_t(mode), rows, bits) * 4u;
 }
 
-hipError_t launch_enc(const EncJob *d_jobs, int njobs, uint32_t lds, hipStream_t s) {
+static void lds_attr(const void *f) {
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+hipError_t launch_enc_chain(const EncJob *d_jobs, int njobs, uint32_t lds, hipStream_t s) {
     if (!njobs) return hipSuccess;
     static bool attr = false;
+    if (!attr) { lds_attr(reinterpret_cast<const void *>(k_enc_chain)); attr = true; }
+    hipLaunchKernelGGL(k_enc_chain, dim3(njobs), dim3(64), lds, s, d_jobs);
+    return hipGetLastError();
+}
+
+hipError_t launch_enc_replay(const EncJob *d_jobs, const uint32_t *d_items, int nitems,
+                             bool emit, uint32_t lds, hipStream_t s) {
+    if (!nitems) return hipSuccess;
+    static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_rans_enc),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        lds_attr(reinterpret_cast<const void *>(k_enc_replay<false>));
+        lds_attr(reinterpret_cast<const void *>(k_enc_replay<true>));
         attr = true;
     }
-    hipLaunchKernelGGL(k_rans_enc, dim3(njobs), dim3(64), lds, s, d_jobs);
+    const uint2 *it = reinterpret_cast<const uint2 *>(d_items);
+    if (emit) hipLaunchKernelGGL(k_enc_replay<true>, dim3(nitems), dim3(REPLAY_THREADS), lds, s, d_jobs, it);
+    else      hipLaunchKernelGGL(k_enc_replay<false>, dim3(nitems), dim3(REPLAY_THREADS), lds, s, d_jobs, it);
+    return hipGetLastError();
+}
+
+hipError_t launch_enc_scan(const EncJob *d_jobs, int njobs, hipStream_t s) {
+    if (!njobs) return hipSuccess;
+    hipLaunchKernelGGL(k_enc_scan, dim3(njobs), dim3(1024), 0, s, d_jobs);
     return hipGetLastError();
 }
 
 hipError_t launch_dec(const DecJob *d_jobs, int njobs, uint32_t lds, hipStream_t s) {
     if (!njobs) return hipSuccess;
     static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_rans_dec),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
+    if (!attr) { lds_attr(reinterpret_cast<const void *>(k_rans_dec)); attr = true; }
     hipLaunchKernelGGL(k_rans_dec, dim3(njobs), dim3(64), lds, s, d_jobs);
     return hipGetLastError();
 }

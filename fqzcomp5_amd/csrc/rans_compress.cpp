@@ -473,10 +473,12 @@ void Compressor::stage_encode() {
         jobs_.push_back(std::move(h));
         jobs_[i].hdr_job = int(jobs_.size()) - 1;
     }
-    // Two launches on two queues: jobs whose tables fit a small LDS
-    // footprint (many waves per CU) and the rest.
-    std::vector<EncJob> ejs, ejb;
-    uint32_t lds_s = 0, lds_b = 0;
+    // Chain pass: two launches on two queues, jobs whose tables fit a small
+    // LDS footprint (many waves per CU) and the rest.  Then the replay
+    // passes over all chunks of all jobs (rans_chain.hip).
+    std::vector<EncJob> ejs, ejb, eall;
+    std::vector<uint32_t> items;
+    uint32_t lds_s = 0, lds_b = 0, lds_r = 0;
     std::vector<int> order;
     for (size_t i = 0; i < jobs_.size(); i++)
         if (jobs_[i].n) order.push_back(int(i));
@@ -493,19 +495,44 @@ void Compressor::stage_encode() {
         uint8_t *base = g_.arena.alloc_n<uint8_t>(cap);
         j.d_end = base + (cap & ~size_t(15));
         const uint8_t *d_remap = j.o1 ? g_.upload(j.remap, 256) : nullptr;
-        const EncJob e{j.d_in, d_tab, d_remap, j.d_end, d_lens + i, j.n, j.nx, j.bits, j.A};
+        const uint32_t steps = j.o1 ? j.n - uint32_t(j.nx - 1) * (j.n / uint32_t(j.nx))
+                                    : (j.n + uint32_t(j.nx) - 1) / uint32_t(j.nx);
+        const uint32_t S = enc_chunk_steps(j.nx);
+        const uint32_t nch = (steps + S - 1) / S;
+        uint32_t *d_ck = g_.arena.alloc_n<uint32_t>(size_t(nch + 1) * uint32_t(j.nx));
+        uint32_t *d_cnt = g_.arena.alloc_n<uint32_t>(nch);
+        const EncJob e{j.d_in, d_tab, d_remap, j.d_end, d_lens + i, d_ck, d_cnt,
+                       j.n, j.nx, j.bits, j.A, nch};
         const uint32_t lds = enc_lds_bytes(j.o1, uint32_t(j.A));
         if (lds <= 24 * 1024) { ejs.push_back(e); lds_s = std::max(lds_s, lds); }
         else { ejb.push_back(e); lds_b = std::max(lds_b, lds); }
+        const uint32_t per = enc_replay_chunks(j.nx);
+        for (uint32_t c0 = 0; c0 < nch; c0 += per) {
+            items.push_back(uint32_t(eall.size()));
+            items.push_back(c0);
+        }
+        eall.push_back(e);
+        lds_r = std::max(lds_r, enc_replay_lds_bytes(j.o1, uint32_t(j.A)));
     }
     EventPair ev(g_.prof.on && !order.empty(), g_.stream);
     if (!ejs.empty()) {
         const EncJob *d = g_.upload(ejs);
+        const EncJob *db = ejb.empty() ? nullptr : g_.upload(ejb);
         g_.fork();
-        FQZ5_HIP(launch_enc(d, int(ejs.size()), lds_s, g_.stream2));
+        FQZ5_HIP(launch_enc_chain(d, int(ejs.size()), lds_s, g_.stream2));
+        if (db) FQZ5_HIP(launch_enc_chain(db, int(ejb.size()), lds_b, g_.stream));
         g_.join();
+    } else if (!ejb.empty()) {
+        FQZ5_HIP(launch_enc_chain(g_.upload(ejb), int(ejb.size()), lds_b, g_.stream));
     }
-    if (!ejb.empty()) FQZ5_HIP(launch_enc(g_.upload(ejb), int(ejb.size()), lds_b, g_.stream));
+    if (!eall.empty()) {
+        const EncJob *d_all = g_.upload(eall);
+        const uint32_t *d_items = g_.upload(items);
+        const int nit = int(items.size() / 2);
+        FQZ5_HIP(launch_enc_replay(d_all, d_items, nit, false, lds_r, g_.stream));
+        FQZ5_HIP(launch_enc_scan(d_all, int(eall.size()), g_.stream));
+        FQZ5_HIP(launch_enc_replay(d_all, d_items, nit, true, lds_r, g_.stream));
+    }
     ev.stop(g_.stream);
     std::vector<uint32_t> lens(jobs_.size(), 0);
     g_.download(lens.data(), d_lens, jobs_.size());

@@ -296,9 +296,14 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
         if (!j.ok || !j.n) continue;
         const uint32_t M = 1u << j.bits;
         const size_t rows = j.o1 ? j.alpha.size() : 1;
+        const uint32_t mode = dec_table_mode(j.o1, uint32_t(rows), j.bits);
         Off o{tabs.size(), alphas.size()};
-        tabs.resize(tabs.size() + rows * M, 0);
+        tabs.resize(tabs.size() + dec_tab_words(mode, uint32_t(rows), j.bits), 0);
         uint32_t *t = &tabs[o.tab];
+        // LDS/GLOBAL: [u32 per slot];  SPLIT: [u8 per slot][u32 fb]
+        uint8_t *tsym = reinterpret_cast<uint8_t *>(t);
+        uint32_t *tfb = t + rows * M / 4;
+        const uint32_t rpl = dec_rp_log(uint32_t(rows));
         for (size_t r = 0; r < rows; r++) {
             const uint32_t *F = &j.F[r * 256];
             uint32_t x = 0;
@@ -310,8 +315,13 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
                     if (it == j.alpha.end() || *it != s) { j.ok = false; break; }
                     sym = uint32_t(it - j.alpha.begin());
                 }
-                for (uint32_t y = 0; y < F[s] && x + y < M; y++)
-                    t[r * M + x + y] = ((F[s] - 1) << (j.bits + 8)) | (y << 8) | sym;
+                if (mode == DEC_TAB_SPLIT) tfb[(r << rpl) + sym] = ((F[s] - 1) << 16) | x;
+                for (uint32_t y = 0; y < F[s] && x + y < M; y++) {
+                    if (mode == DEC_TAB_SPLIT)
+                        tsym[r * M + x + y] = uint8_t(sym);
+                    else
+                        t[r * M + x + y] = ((F[s] - 1) << (j.bits + 8)) | (y << 8) | sym;
+                }
                 x += F[s];
             }
         }
@@ -339,22 +349,26 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
     for (size_t k : ord) {
         DJ &j = djs_[used[k]];
         const uint32_t rows = j.o1 ? uint32_t(j.alpha.size()) : 1u;
+        const uint32_t mode = dec_table_mode(j.o1, rows, j.bits);
         const DecJob e{j.d + j.tab_len, d_tabs + offs[k].tab,
                        j.o1 ? d_alpha + offs[k].alpha : nullptr, j.d_out, d_status + k,
-                       j.len - j.tab_len, j.n, j.nx, j.bits, rows, 0};
+                       j.len - j.tab_len, j.n, j.nx, j.bits, rows, mode};
         bytes += double(j.n) + (j.len - j.tab_len);
-        const uint32_t lds = dec_lds_bytes(rows, j.bits);
+        const uint32_t lds = dec_lds_bytes(rows, j.bits, int(mode));
         if (lds <= 40 * 1024) { djs.push_back(e); lds_s = std::max(lds_s, lds); }
         else { djb.push_back(e); lds_b = std::max(lds_b, lds); }
     }
     EventPair ev(g_.prof.on && !ord.empty(), g_.stream);
     if (!djs.empty()) {
         const DecJob *d = g_.upload(djs);
+        const DecJob *db = djb.empty() ? nullptr : g_.upload(djb);
         g_.fork();
         FQZ5_HIP(launch_dec(d, int(djs.size()), lds_s, g_.stream2));
+        if (db) FQZ5_HIP(launch_dec(db, int(djb.size()), lds_b, g_.stream));
         g_.join();
+    } else if (!djb.empty()) {
+        FQZ5_HIP(launch_dec(g_.upload(djb), int(djb.size()), lds_b, g_.stream));
     }
-    if (!djb.empty()) FQZ5_HIP(launch_dec(g_.upload(djb), int(djb.size()), lds_b, g_.stream));
     ev.stop(g_.stream);
     std::vector<int32_t> st(used.size());
     g_.download(st.data(), d_status, st.size());
