@@ -53,6 +53,21 @@ def make_blocks(gb: float, seed: int):
     return r, synth.split_blocks(r, BLK)
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per dispatch of `kernel` from the newest committed PMC
+    summary (profiles/rNN_pmc.json, written by tools/pmc_summary.py from
+    separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    if not files:
+        return None, None
+    ks = json.load(open(files[-1]))["kernels"]
+    for k, v in ks.items():
+        if f"::{kernel}(" in k:
+            return int(v["hbm_bytes_per_dispatch"]), os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def method_order(m: int, fixed_len: int) -> int:
     return [0, 1, 64, 65, 128, 129, 192, 193][m - 1] if m <= 8 else (fixed_len << 8) + 9
 
@@ -219,13 +234,21 @@ def main():
         name, ms, n, b = "k_rans_dec", dec_ms, dec_n, dec_b
     avg_ms = ms / max(n, 1)
     ach = (b / max(n, 1)) / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
+    traffic, tsrc = pmc_traffic(name)
+    # the decode launch is bound by its longest rANS chain: one step = one
+    # symbol on each of the 4 interleaved states
+    longest = max((e - s) for _, s, e, _ in spans)
     out["roofline"] = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 6),
-                       "traffic": None, "kernel": name,
+                       "traffic": traffic, "traffic_source": tsrc, "kernel": name,
                        "avg_launch_ms": round(avg_ms, 3),
                        "bytes_per_launch": int(b / max(n, 1)),
                        "enc_avg_ms": round(enc_ms / max(enc_n, 1), 3),
-                       "dec_avg_ms": round(dec_ms / max(dec_n, 1), 3)}
+                       "dec_avg_ms": round(dec_ms / max(dec_n, 1), 3),
+                       "chains": {"streams_per_launch": len(spans),
+                                  "longest_stream_steps": longest // 4,
+                                  "dec_ns_per_step_longest": round(
+                                      dec_ms / max(dec_n, 1) * 1e6 / max(longest // 4, 1), 2)}}
     # ---- CPU baseline (rank 0, N=1) -----------------------------------------
     if rank == 0 and world == 1 and not args.no_cpu:
         host_secs = []

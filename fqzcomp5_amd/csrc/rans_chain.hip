@@ -488,8 +488,9 @@ template <int TM>
 static DEV uint32_t dec_finish(const DecTabs &t, uint32_t rd, uint32_t rowfb, uint32_t x,
                                int bits, uint32_t mask, uint32_t &xd) {
     const uint32_t xh = x >> bits;
-    if (TM == DEC_TAB_SPLIT) {
-        const uint32_t e = t.fb[rowfb + rd];
+    if (TM == DEC_TAB_SPLIT) {      // rowfb: byte offset of the fb row
+        const uint32_t e = *reinterpret_cast<const uint32_t *>(
+            reinterpret_cast<const uint8_t *>(t.fb) + rowfb + (rd << 2));
         xd = __umul24(e >> 16, xh) + xh + (x & mask) - (e & 0xffffu);
         return rd;
     } else {
@@ -561,12 +562,25 @@ static DEV void dec4_body(const DecJob &J) {
     // the chain) first, then the window of the next words; the symbol is
     // packed into acc (byte u&3) and 16 symbols go out in one store.
     auto fstep = [&](uint32_t &acc, int u) {
-        const uint32_t rd = dec_read<TM>(tb, rowbase, x, mask);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint64_t win = ring_win(sh.ring, ptr);
-        __builtin_amdgcn_sched_barrier(0);
-        uint32_t xd;
-        const uint32_t sy = dec_finish<TM>(tb, rd, rowfb, x, bits, mask, xd);
+        uint32_t xd, sy;
+        uint64_t win;
+        if (TM == DEC_TAB_SPLIT) {
+            // both table reads, then the window (rowfb is a byte offset)
+            sy = tb.ts[rowbase + (x & mask)];
+            const uint32_t e = *reinterpret_cast<const uint32_t *>(
+                reinterpret_cast<const uint8_t *>(tb.fb) + rowfb + (sy << 2));
+            __builtin_amdgcn_sched_barrier(0);
+            win = ring_win(sh.ring, ptr);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t xh = x >> bits;
+            xd = __umul24(e >> 16, xh) + xh + (x & mask) - (e & 0xffffu);
+        } else {
+            const uint32_t rd = dec_read<TM>(tb, rowbase, x, mask);
+            __builtin_amdgcn_sched_barrier(0);
+            win = ring_win(sh.ring, ptr);
+            __builtin_amdgcn_sched_barrier(0);
+            sy = dec_finish<TM>(tb, rd, rowfb, x, bits, mask, xd);
+        }
         const bool c = xd < RANS_LOW_D;
         const uint64_t m = __ballot(c);
         const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
@@ -576,7 +590,10 @@ static DEV void dec4_body(const DecJob &J) {
         // acc byte (u&3) <- sy byte 0, other bytes kept
         constexpr uint32_t SEL[4] = {0x07060500u, 0x07060004u, 0x07000504u, 0x00060504u};
         acc = __builtin_amdgcn_perm(acc, sy, SEL[u & 3]);
-        if (O1) { rowbase = dec_rowoff<TM>(sy, bits); rowfb = (sy & 0xffu) << rpl; }
+        if (O1) {
+            rowbase = dec_rowoff<TM>(sy, bits);
+            rowfb = (sy & 0xffu) << (TM == DEC_TAB_SPLIT ? rpl + 2 : rpl);
+        }
     };
 
     for (uint32_t t0 = 0; t0 < T; t0 += G) {
@@ -622,7 +639,10 @@ static DEV void dec4_body(const DecJob &J) {
             if (act) {
                 x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
                 myob[t - t0] = uint8_t(sy);
-                if (O1) { rowbase = dec_rowoff<TM>(sy, bits); rowfb = (sy & 0xffu) << rpl; }
+                if (O1) {
+                    rowbase = dec_rowoff<TM>(sy, bits);
+                    rowfb = (sy & 0xffu) << (TM == DEC_TAB_SPLIT ? rpl + 2 : rpl);
+                }
             }
             ptr += uint32_t(__popcll(m & 15u));
         }
@@ -682,7 +702,7 @@ static DEV void dec32_body(const DecJob &J) {
             if (act) {
                 x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
                 sh.obuf[(t - t0) * NX + z] = uint8_t(sy);
-                if (O1) { rowbase = dec_rowoff<TM>(sy, bits); rowfb = sy << rpl; }
+                if (O1) { rowbase = dec_rowoff<TM>(sy, bits); rowfb = sy << (rpl + 2); }
             }
             ptr += uint32_t(__popcll(m & 0xffffffffull));
         }

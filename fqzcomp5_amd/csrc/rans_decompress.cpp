@@ -334,14 +334,17 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
     const uint8_t *d_alpha = alphas.empty() ? nullptr : g_.upload(alphas);
     int32_t *d_status = g_.arena.alloc_n<int32_t>(used.size());
     g_.memset0(d_status, used.size() * 4);
-    std::vector<DecJob> djs, djb;
-    uint32_t lds_s = 0, lds_b = 0;
+    // One launch: every stream is a latency-bound chain on its own wave, so
+    // occupancy does not matter and the launch carries the largest table.
+    std::vector<DecJob> djs;
+    uint32_t lds = 0;
     std::vector<size_t> ord;
     for (size_t k = 0; k < used.size(); k++) {
         DJ &j = djs_[used[k]];
         if (j.len < j.tab_len + 4u * j.nx) { j.ok = false; continue; }
         ord.push_back(k);
     }
+    // longest chains first so they start in the first dispatch wave
     std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
         return djs_[used[a]].n / djs_[used[a]].nx > djs_[used[b]].n / djs_[used[b]].nx;
     });
@@ -350,25 +353,14 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
         DJ &j = djs_[used[k]];
         const uint32_t rows = j.o1 ? uint32_t(j.alpha.size()) : 1u;
         const uint32_t mode = dec_table_mode(j.o1, rows, j.bits);
-        const DecJob e{j.d + j.tab_len, d_tabs + offs[k].tab,
-                       j.o1 ? d_alpha + offs[k].alpha : nullptr, j.d_out, d_status + k,
-                       j.len - j.tab_len, j.n, j.nx, j.bits, rows, mode};
+        djs.push_back(DecJob{j.d + j.tab_len, d_tabs + offs[k].tab,
+                             j.o1 ? d_alpha + offs[k].alpha : nullptr, j.d_out, d_status + k,
+                             j.len - j.tab_len, j.n, j.nx, j.bits, rows, mode});
         bytes += double(j.n) + (j.len - j.tab_len);
-        const uint32_t lds = dec_lds_bytes(rows, j.bits, int(mode));
-        if (lds <= 40 * 1024) { djs.push_back(e); lds_s = std::max(lds_s, lds); }
-        else { djb.push_back(e); lds_b = std::max(lds_b, lds); }
+        lds = std::max(lds, dec_lds_bytes(rows, j.bits, int(mode)));
     }
     EventPair ev(g_.prof.on && !ord.empty(), g_.stream);
-    if (!djs.empty()) {
-        const DecJob *d = g_.upload(djs);
-        const DecJob *db = djb.empty() ? nullptr : g_.upload(djb);
-        g_.fork();
-        FQZ5_HIP(launch_dec(d, int(djs.size()), lds_s, g_.stream2));
-        if (db) FQZ5_HIP(launch_dec(db, int(djb.size()), lds_b, g_.stream));
-        g_.join();
-    } else if (!djb.empty()) {
-        FQZ5_HIP(launch_dec(g_.upload(djb), int(djb.size()), lds_b, g_.stream));
-    }
+    if (!djs.empty()) FQZ5_HIP(launch_dec(g_.upload(djs), int(djs.size()), lds, g_.stream));
     ev.stop(g_.stream);
     std::vector<int32_t> st(used.size());
     g_.download(st.data(), d_status, st.size());
