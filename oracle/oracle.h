@@ -19,4 +19,16 @@ uint8_t *ora_rans_uncompress_to_4x16(uint8_t *in, unsigned int in_size,
                                      uint8_t *out, unsigned int *out_size);
 uint8_t *ora_rans_uncompress_4x16(uint8_t *in, unsigned int in_size,
                                   unsigned int *out_size);
+/* fqzcomp_qual (fork ABI, htscodecs/fqzcomp_qual.h:59-64,155-170) */
+typedef struct {
+    int num_records;
+    uint32_t *len;
+    uint32_t *flags;
+    unsigned char **seq;
+} ora_fqz_slice;
+
+uint8_t *ora_fqz_compress(int vers, ora_fqz_slice *s, uint8_t *in, size_t in_size,
+                          size_t *out_size, int strat, void *gp);
+uint8_t *ora_fqz_decompress(uint8_t *in, size_t in_size, size_t *out_size,
+                            int *lengths, int nlengths, ora_fqz_slice *s);
 #endif
