@@ -46,9 +46,32 @@ using namespace fqz5;
 
 namespace fqz5 {
 void fqz5_set_error(const char *msg) { g_err = msg; }
+// fqz_codec.cpp
+uint8_t *fqz_encode_gpu(int vers, fqz_slice *s, const uint8_t *in, size_t n, size_t *out_size,
+                        int strat, fqz_gparams *gp);
+uint8_t *fqz_decode_gpu(const uint8_t *in, size_t in_size, size_t *out_size, int *lengths,
+                        int nlengths, fqz_slice *s);
 }
 
 extern "C" {
+
+char *fqz_compress(int vers, fqz_slice *s, char *in, size_t in_size, size_t *out_size,
+                   int strat, fqz_gparams *gp) {
+    GUARD_BEGIN
+    if (!s || !out_size || (!in && in_size)) return nullptr;
+    return reinterpret_cast<char *>(fqz_encode_gpu(
+        vers, s, reinterpret_cast<const uint8_t *>(in), in_size, out_size, strat, gp));
+    GUARD_END(nullptr)
+}
+
+char *fqz_decompress(char *in, size_t in_size, size_t *out_size, int *lengths, int nlengths,
+                     fqz_slice *s) {
+    GUARD_BEGIN
+    if (!in || !out_size) return nullptr;
+    return reinterpret_cast<char *>(fqz_decode_gpu(
+        reinterpret_cast<const uint8_t *>(in), in_size, out_size, lengths, nlengths, s));
+    GUARD_END(nullptr)
+}
 
 unsigned int rans_compress_bound_4x16(unsigned int size, int order) {
     return compress_bound(size, order);

@@ -1,0 +1,515 @@
+// fqz_codec.cpp — fqz_compress / fqz_decompress on the GPU
+// (htscodecs fqzcomp_qual.c:1008-1646, fork ABI).
+//
+// Encode: the block's bytes go to HBM once; the statistics of
+// fqz_qual_stats are gathered by kernels (fqz_kernels.hip); the host makes
+// the reference's decisions from them (entropy comparisons in double, the
+// same expressions in the same order), serialises the parameters and the
+// serial model + range-coder kernel writes the stream.  Decode parses the
+// parameters on the host and runs the serial decode kernel.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "../../include/fqz5_mi355x.h"
+#include "fqz_format.hpp"
+#include "fqz_kernels.h"
+#include "gpu_ctx.hpp"
+#include "rans_format.hpp"
+
+namespace fqz5 {
+using namespace fqz;
+
+namespace {
+
+struct Records {
+    std::vector<uint32_t> len, flags;
+    std::vector<uint64_t> off;
+    uint32_t walked = 0;      // records the statistics loop visits
+};
+
+// Records as fqz_qual_stats walks them (fqzcomp_qual.c:464-501): every
+// record starting before the end of the data; with no records the whole
+// buffer is one.
+Records walk_records(int nrec, const uint32_t *lens, const uint32_t *flags, size_t n) {
+    Records R;
+    if (nrec <= 0) {
+        R.len.assign(1, uint32_t(n));
+        R.flags.assign(1, 0);
+        R.off.assign(1, 0);
+        R.walked = n ? 1 : 0;
+        return R;
+    }
+    R.len.assign(lens, lens + nrec);
+    R.flags.assign(flags, flags + nrec);
+    R.off.resize(size_t(nrec));
+    uint64_t o = 0;
+    for (int r = 0; r < nrec; r++) {
+        R.off[size_t(r)] = o;
+        if (o < n) R.walked = uint32_t(r + 1);
+        o += R.len[size_t(r)];
+    }
+    return R;
+}
+
+// The statistics and auto-tuning of fqz_qual_stats (fqzcomp_qual.c:424-704)
+// with the histograms from the GPU.  Updates pm and the caller's flags.
+void tune(GpuCtx &g, Param &pm, int nrec, uint32_t *flags, const Records &R,
+          const uint8_t *d_q, size_t n, uint32_t qhist[256]) {
+    int max_sel = 0, has_r2 = 0;
+    for (int r = 0; r < nrec; r++) {
+        max_sel = std::max(max_sel, int(flags[r] >> 16));
+        if (flags[r] & F_READ2) has_r2 = 1;
+    }
+    const uint32_t W = R.walked;
+    // ---- GPU: per-record averages / dups, (len & 127, q) histograms ----
+    std::vector<uint2> chunks;
+    for (uint32_t r = 0; r < W;) {
+        uint32_t e = r, bytes = 0;
+        while (e < W && (e == r || bytes + R.len[e] <= 65535u)) bytes += R.len[e++];
+        chunks.push_back(make_uint2(r, e));
+        r = e;
+    }
+    FqzStatJob J{};
+    J.q = d_q;
+    J.off = g.upload(R.off);
+    J.len = g.upload(R.len);
+    J.flags = g.upload(R.flags);
+    J.nrec = W;
+    J.rec_avg = g.arena.alloc_n<uint32_t>(W + 1);
+    J.avg_hist = g.arena.alloc_n<uint32_t>(NAVG);
+    J.dups = g.arena.alloc_n<uint32_t>(1);
+    J.chunks = g.upload(chunks);
+    J.h1 = g.arena.alloc_n<uint32_t>(NPOS * 256);
+    J.h2 = g.arena.alloc_n<uint32_t>(NPOS * 256);
+    J.b4 = g.arena.alloc_n<uint32_t>(4 * NPOS * 256);
+    g.memset0(J.rec_avg, (W + 1) * 4);
+    g.memset0(J.avg_hist, NAVG * 4);
+    g.memset0(J.dups, 4);
+    g.memset0(J.h1, NPOS * 256 * 4);
+    g.memset0(J.h2, NPOS * 256 * 4);
+    g.memset0(J.b4, 4 * NPOS * 256 * 4);
+    FQZ5_HIP(launch_fqz_records(J, g.stream));
+    FQZ5_HIP(launch_fqz_hist(J, int(chunks.size()), 0, g.stream));
+    std::vector<uint32_t> h1(NPOS * 256), h2(NPOS * 256), ahist(NAVG), ravg(W + 1);
+    uint32_t dups = 0;
+    g.download(h1.data(), J.h1, h1.size());
+    g.download(h2.data(), J.h2, h2.size());
+    g.download(ahist.data(), J.avg_hist, ahist.size());
+    g.download(ravg.data(), J.rec_avg, ravg.size());
+    g.download(&dups, J.dups, 1);
+    g.sync();
+
+    std::vector<uint64_t> t1(NPOS, 0), t2(NPOS, 0);
+    for (int j = 0; j < NPOS; j++)
+        for (int s = 0; s < 256; s++) {
+            const uint32_t a = h1[size_t(j) * 256 + s], b = h2[size_t(j) * 256 + s];
+            qhist[s] += a + b;
+            t1[size_t(j)] += a;
+            t2[size_t(j)] += b;
+        }
+    pm.dedup = ((W + 1) / (dups + 1) < 500);
+    pm.max_sym = pm.nsym = 0;
+    for (int s = 0; s < 256; s++)
+        if (qhist[s]) pm.max_sym = s, pm.nsym++;
+
+    // per-record average of every record (unwalked ones: 0, as calloc)
+    auto rec_avg = [&](int r) -> uint32_t {
+        if (nrec <= 0) return ravg[0];
+        return uint32_t(r) < W ? ravg[size_t(r)] : 0u;
+    };
+
+    if (pm.qa != 0) {
+        // rank the averages into four classes (fqzcomp_qual.c:522-557)
+        const double f0 = pm.nsym > 8 ? 0.2 : 0.05;
+        const double f1 = pm.nsym > 8 ? 0.5 : 0.22;
+        const double f2 = pm.nsym > 8 ? 0.8 : 0.60;
+        std::vector<uint32_t> amap(ahist);
+        const double cut[3] = {f0, f1, f2};
+        int total = 0, k = 0;
+        for (int cls = 0; cls < 3; cls++) {
+            while (k < NAVG) {
+                total += int(amap[size_t(k)]);
+                if (total > cut[cls] * nrec) break;
+                amap[size_t(k++)] = uint32_t(cls);
+            }
+        }
+        while (k < NAVG) amap[size_t(k++)] = 3;
+        // ---- GPU: histograms per class ----
+        J.amap = g.upload(amap);
+        FQZ5_HIP(launch_fqz_hist(J, int(chunks.size()), 1, g.stream));
+        FQZ5_HIP(launch_fqz_hist(J, int(chunks.size()), 2, g.stream));
+        std::vector<uint32_t> b4(4 * NPOS * 256);
+        g.download(b4.data(), J.b4, b4.size());
+        g.sync();
+        auto B4 = [&](int c, int j, int s) { return double(b4[(size_t(c) * NPOS + j) * 256 + s]); };
+        // counts per (class, position) and the merged 2-class / 1-class bins
+        std::vector<double> n4(4 * NPOS, 0);
+        for (int c = 0; c < 4; c++)
+            for (int j = 0; j < NPOS; j++)
+                for (int s = 0; s < 256; s++) n4[size_t(c) * NPOS + j] += B4(c, j, s);
+        double e1 = 0, e2 = 0, e4 = 0;
+        for (int j = 0; j < NPOS; j++) {
+            const double c20 = n4[size_t(0) * NPOS + j] + n4[size_t(1) * NPOS + j];
+            const double c21 = n4[size_t(2) * NPOS + j] + n4[size_t(3) * NPOS + j];
+            const double c1 = c20 + c21;
+            for (int s = 0; s < 256; s++) {
+                const double a0 = B4(0, j, s), a1 = B4(1, j, s), a2 = B4(2, j, s), a3 = B4(3, j, s);
+                const double q20 = a0 + a1, q21 = a2 + a3, q1 = q20 + q21;
+                if (q1) e1 += q1 * std::log(q1 / c1);
+                if (q20) e2 += q20 * std::log(q20 / c20);
+                if (q21) e2 += q21 * std::log(q21 / c21);
+                if (a0) e4 += a0 * std::log(a0 / n4[size_t(0) * NPOS + j]);
+                if (a1) e4 += a1 * std::log(a1 / n4[size_t(1) * NPOS + j]);
+                if (a2) e4 += a2 * std::log(a2 / n4[size_t(2) * NPOS + j]);
+                if (a3) e4 += a3 * std::log(a3 / n4[size_t(3) * NPOS + j]);
+            }
+        }
+        e1 /= -std::log(2) / 8;
+        e2 /= -std::log(2) / 8;
+        e4 /= -std::log(2) / 8;
+        const double m = pm.qa > 0 ? 1 : 0.98;
+        if ((pm.qa == -1 || pm.qa >= 4) && e4 + nrec / 4 < e2 * m + nrec / 8 && e4 + nrec / 4 < e1 * m) {
+            for (int r = 0; r < nrec; r++) flags[r] |= amap[std::min(2559u, rec_avg(r))] << 16;
+            pm.sel = true;
+            max_sel = 3;
+        } else if ((pm.qa == -1 || pm.qa >= 2) && e2 + nrec / 8 < e1 * m) {
+            for (int r = 0; r < nrec; r++) flags[r] |= (amap[std::min(2559u, rec_avg(r))] >> 1) << 16;
+            pm.sel = true;
+            max_sel = 1;
+        }
+        if (pm.qa == -1) {
+            if (pm.pbits > 0 && pm.dbits > 0) {
+                pm.sloc = pm.dloc - 1;
+                pm.pbits--;
+                pm.dbits--;
+                pm.dloc++;
+            } else if (pm.dbits >= 2) {
+                pm.sloc = pm.dloc;
+                pm.dbits -= 2;
+                pm.dloc += 2;
+            } else if (pm.qbits >= 2) {
+                pm.qbits -= 2;
+                pm.ploc -= 2;
+                pm.sloc = unsigned(16 - 2 - pm.r2);
+                if (pm.qbits == 6 && pm.qshift == 5) pm.qbits--;
+            }
+            pm.qa = 4;
+        }
+    }
+
+    if (has_r2 || pm.r2) {   // READ1 / READ2 split (fqzcomp_qual.c:658-695)
+        double e1 = 0, e2 = 0;
+        for (int j = 0; j < NPOS; j++) {
+            if (!t1[size_t(j)] || !t2[size_t(j)]) continue;
+            for (int s = 0; s < 256; s++) {
+                const double a = h1[size_t(j) * 256 + s], b = h2[size_t(j) * 256 + s];
+                const double ab = a + b;
+                if (!ab) continue;
+                e1 -= ab * std::log(ab / double(t1[size_t(j)] + t2[size_t(j)]));
+                if (a) e2 -= a * std::log(a / double(t1[size_t(j)]));
+                if (b) e2 -= b * std::log(b / double(t2[size_t(j)]));
+            }
+        }
+        e1 /= std::log(2) * 8;
+        e2 /= std::log(2) * 8;
+        const double m = pm.r2 > 0 ? 1 : 0.95;
+        if (e2 + (8 + nrec / 8) < e1 * m) {
+            for (int r = 0; r < nrec; r++) {
+                const uint32_t sel = flags[r] >> 16;
+                flags[r] = (flags[r] & 0xffff) | ((sel * 2 + ((flags[r] & F_READ2) ? 1 : 0)) << 16);
+                max_sel = std::max(max_sel, int(flags[r] >> 16));
+            }
+        }
+    }
+    if (max_sel > 0) {
+        pm.sel = true;
+        pm.max_sel = max_sel;
+    }
+}
+
+// The rest of fqz_pick_parameters (fqzcomp_qual.c:842-1000).
+void pick_finish(Global &g, Param &pm, int strat, int nrec, const uint32_t *lens,
+                 const uint32_t *flags, size_t n, const uint32_t qhist[256]) {
+    if (strat >= NSTRATS) strat = NSTRATS - 1;
+    int dsq[64] = {0, 1, 1, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3,
+                   4, 4, 4, 4, 4, 4, 4, 4, 4, 5, 5, 5, 5, 5, 5, 5,
+                   5, 5, 5, 5, 6, 6, 6, 6, 6, 6, 6, 6, 6, 6, 6, 6,
+                   6, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7};
+    pm.qmap_stored = (pm.nsym <= 8 && pm.nsym * 2 < pm.max_sym);
+    int r = 1;
+    while (r < nrec && lens[r] == lens[0]) r++;
+    pm.fixed = (r == nrec);
+    pm.qtab_on = false;
+    if (strat < NSTRATS - 1) {
+        if (pm.pshift < 0) {
+            const double v = std::log(double(lens[0]) / (1 << pm.pbits)) / std::log(2) + .5;
+            pm.pshift = v > 0 ? int(v) : 0;
+        }
+        if (pm.nsym <= 4) {
+            pm.qshift = 2;
+            if (n < 5000000) pm.pbits = 2, pm.pshift = 5;
+        } else if (pm.nsym <= 8) {
+            pm.qbits = std::min(pm.qbits, 9u);
+            pm.qshift = 3;
+            if (n < 5000000) pm.qbits = 6;
+        }
+        if (n < 300000) {
+            pm.qbits = unsigned(pm.qshift);
+            pm.dbits = 2;
+        }
+    }
+    for (int k = 0; k < 64; k++) dsq[k] = std::min(dsq[k], (1 << pm.dbits) - 1);
+    if (pm.qmap_stored) {
+        int j = 0;
+        for (int s = 0; s < 256; s++) pm.qmap[s] = qhist[s] ? unsigned(j++) : unsigned(INT_MAX);
+        pm.max_sym = pm.nsym;
+    } else {
+        pm.nsym = 255;
+        for (int s = 0; s < 256; s++) pm.qmap[s] = unsigned(s);
+    }
+    g.max_sym = std::max(g.max_sym, pm.max_sym);
+    if (pm.qbits)
+        for (int s = 0; s < 256; s++) pm.qtab[s] = unsigned(s);
+    if (size_t(qhist['~' - '!']) * 2 > n && strat == 3) {     // HiFi qtab
+        pm.qtab_on = true;
+        unsigned v = 0;
+        for (int s = 0; s < 256; s++) {
+            if (s == '~' - '!' || s == '~' - '!' + 1 || s % 16 == 0) v++;
+            pm.qtab[s] = v;
+        }
+        pm.qbits = 9, pm.qshift = 3;
+        pm.bbits = 6, pm.bloc = 9, pm.boff = 2;
+    }
+    if (pm.pbits)
+        for (int k = 0; k < 1024; k++)
+            pm.ptab[k] = std::min((1u << pm.pbits) - 1, unsigned(k >> pm.pshift));
+    if (pm.dbits)
+        for (int k = 0; k < 256; k++) pm.dtab[k] = unsigned(dsq[std::min(63, k >> pm.dshift)]);
+    pm.ptab_on = pm.pbits > 0;
+    pm.dtab_on = pm.dbits > 0;
+    pm.pflags = (pm.qtab_on ? PF_QTAB : 0) | (pm.dtab_on ? PF_DTAB : 0) |
+                (pm.ptab_on ? PF_PTAB : 0) | (pm.sel ? PF_SEL : 0) | (pm.fixed ? PF_LEN : 0) |
+                (pm.dedup ? PF_DEDUP : 0) | (pm.qmap_stored ? PF_QMAP : 0);
+    g.max_sel = 0;
+    if (pm.sel) {
+        g.gflags |= GF_STAB;
+        int mx = 0;
+        for (int k = 0; k < nrec; k++) mx = std::max(mx, int(flags[k] >> 16));
+        g.max_sel = mx;
+    }
+}
+
+// Parameters as the kernels read them; position / delta tables shifted to
+// their context location (fqzcomp_qual.c:1067-1076).
+FqzDevGlobal dev_params(const Global &g) {
+    if (g.nparam > FQZ_MAX_PARAMS) throw std::runtime_error("fqz: too many parameter blocks");
+    FqzDevGlobal d;
+    std::memset(&d, 0, sizeof d);
+    d.gflags = g.gflags;
+    d.nparam = uint32_t(g.nparam);
+    d.max_sel = uint32_t(g.max_sel);
+    d.max_sym = uint32_t(g.max_sym);
+    for (int i = 0; i < 256; i++) d.stab[i] = uint8_t(g.stab[i]);
+    for (int k = 0; k < g.nparam; k++) {
+        const Param &pm = g.p[size_t(k)];
+        FqzDevParam &o = d.p[k];
+        o.ctx0 = pm.ctx0;
+        o.qshift = unsigned(pm.qshift);
+        o.qloc = pm.qloc;
+        o.sloc = pm.sloc;
+        o.bbits = pm.bbits;
+        o.bloc = pm.bloc;
+        o.boff = pm.boff;
+        o.qmask = pm.qmask();
+        o.sel = pm.sel;
+        o.dedup = pm.dedup;
+        o.fixed = pm.fixed;
+        for (int i = 0; i < 256; i++) {
+            o.qtab[i] = pm.qtab[i];
+            o.dtab[i] = pm.dtab[i] << pm.dloc;
+            o.qmap[i] = uint8_t(pm.qmap[i]);
+        }
+        for (int i = 0; i < 1024; i++) o.ptab[i] = pm.ptab[i] << pm.ploc;
+    }
+    return d;
+}
+
+// Sequence bytes per record as the coder reads them: the reference reads
+// seq[r][0 .. max(len, boff)) (fqzcomp_qual.c:1163-1173).  Records without
+// a sequence get offset ~0.
+void gather_seq(GpuCtx &g, unsigned char **seq, int nrec, const uint32_t *lens,
+                unsigned boff, const uint8_t **d_seq, const uint64_t **d_off) {
+    std::vector<uint64_t> off(size_t(std::max(nrec, 1)), ~0ull);
+    uint64_t tot = 0;
+    for (int r = 0; r < nrec; r++)
+        if (seq[r]) {
+            off[size_t(r)] = tot;
+            tot += std::max<uint64_t>(lens[r], boff);
+        }
+    std::vector<uint8_t> buf(size_t(tot) + 1, 0);
+    for (int r = 0; r < nrec; r++)
+        if (seq[r]) std::memcpy(&buf[off[size_t(r)]], seq[r], std::max<size_t>(lens[r], boff));
+    *d_seq = g.upload(buf);
+    *d_off = g.upload(off);
+}
+
+}  // namespace
+
+uint8_t *fqz_encode_gpu(int vers, fqz_slice *s, const uint8_t *in, size_t n, size_t *out_size,
+                        int strat, fqz_gparams *gp) {
+    GpuCtx &g = gpu();
+    const int nrec = s ? s->num_records : 0;
+    const size_t cap = size_t(double(n) * 1.1 + 100000);
+    uint8_t *out = static_cast<uint8_t *>(std::malloc(cap));
+    if (!out) throw std::runtime_error("fqz: out of host memory");
+    g.reset();
+    const uint8_t *d_q = g.upload(in, n);
+    Global G;
+    if (!gp) {
+        pick_begin(G, vers, strat, nrec, s->len, n);
+        uint32_t qhist[256] = {0};
+        const Records R = walk_records(nrec, s->len, s->flags, n);
+        tune(g, G.p[0], nrec, s->flags, R, d_q, n, qhist);
+        pick_finish(G, G.p[0], strat, nrec, s->len, s->flags, n, qhist);
+    } else {
+        // caller-supplied parameters (fqzcomp_qual.c:1040-1045)
+        G.vers = gp->vers;
+        G.gflags = gp->gflags;
+        G.nparam = gp->nparam;
+        G.max_sel = gp->max_sel;
+        G.max_sym = gp->max_sym;
+        for (int i = 0; i < 256; i++) G.stab[i] = gp->stab[i];
+        G.p.assign(size_t(gp->nparam), Param());
+        for (int k = 0; k < gp->nparam; k++) {
+            const fqz_param &a = gp->p[k];
+            Param &b = G.p[size_t(k)];
+            b.ctx0 = a.context;
+            b.pflags = a.pflags;
+            b.sel = a.do_sel, b.dedup = a.do_dedup, b.qmap_stored = a.store_qmap,
+            b.fixed = a.fixed_len;
+            b.qtab_on = a.use_qtab, b.dtab_on = a.use_dtab, b.ptab_on = a.use_ptab;
+            b.qbits = a.qbits, b.qloc = a.qloc, b.pbits = a.pbits, b.ploc = a.ploc;
+            b.dbits = a.dbits, b.dloc = a.dloc, b.sloc = a.sloc;
+            b.bbits = a.bbits, b.bloc = a.bloc, b.boff = a.boff;
+            b.max_sym = a.max_sym, b.nsym = a.nsym, b.max_sel = a.max_sel;
+            b.qshift = a.qshift, b.pshift = a.pshift, b.dshift = a.dshift;
+            std::memcpy(b.qmap, a.qmap, sizeof b.qmap);
+            std::memcpy(b.qtab, a.qtab, sizeof b.qtab);
+            std::memcpy(b.ptab, a.ptab, sizeof b.ptab);
+            std::memcpy(b.dtab, a.dtab, sizeof b.dtab);
+        }
+    }
+    const bool have_seq = s && s->seq && nrec > 0 && s->seq[0];
+    if (!have_seq) {
+        for (Param &pm : G.p) pm.bbits = pm.bloc = 0;
+        G.gflags &= ~unsigned(GF_SEQ);
+    } else {
+        for (Param &pm : G.p)
+            if (pm.bbits) G.gflags |= GF_SEQ;
+    }
+    if (gp) {   // the reference edits the caller's block in place
+        gp->gflags = G.gflags;
+        for (int k = 0; k < gp->nparam; k++) {
+            gp->p[k].bbits = G.p[size_t(k)].bbits;
+            gp->p[k].bloc = G.p[size_t(k)].bloc;
+            for (int i = 0; i < 1024; i++) gp->p[k].ptab[i] <<= gp->p[k].ploc;
+            for (int i = 0; i < 256; i++) gp->p[k].dtab[i] <<= gp->p[k].dloc;
+        }
+    }
+    size_t hdr = size_t(varint_put(out, out + cap, uint32_t(n)));
+    hdr += size_t(put_params(G, out + hdr));
+
+    const FqzDevGlobal dg = dev_params(G);
+    FqzEncJob E{};
+    E.g = g.upload(&dg, 1);
+    E.q = d_q;
+    E.n = n;
+    std::vector<uint32_t> lens(s ? s->len : nullptr, s ? s->len + nrec : nullptr);
+    std::vector<uint32_t> sels(static_cast<size_t>(nrec)), fl(static_cast<size_t>(nrec));
+    for (int r = 0; r < nrec; r++) {
+        sels[size_t(r)] = s->flags[r] >> 16;
+        fl[size_t(r)] = s->flags[r];
+    }
+    lens.push_back(0);
+    sels.push_back(0);
+    fl.push_back(0);
+    E.len = g.upload(lens);
+    E.sel = g.upload(sels);
+    E.flags = g.upload(fl);
+    E.nrec = uint32_t(nrec);
+    if (have_seq) {
+        unsigned boff = 0;
+        for (const Param &pm : G.p) boff = std::max(boff, pm.boff);
+        gather_seq(g, s->seq, nrec, s->len, boff, &E.seq, &E.seq_off);
+    }
+    E.models = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * FQZ_QMODEL_BYTES);
+    FQZ5_HIP(launch_fqz_model_init(E.models, G.max_sym + 1, g.stream));
+    const size_t room = cap - hdr;
+    E.out = g.arena.alloc_n<uint8_t>(room);
+    E.out_len = g.arena.alloc_n<uint32_t>(1);
+    FQZ5_HIP(launch_fqz_encode(E, g.stream));
+    uint32_t clen = 0;
+    g.download(&clen, E.out_len, 1);
+    g.sync();
+    if (clen > room) throw std::runtime_error("fqz: output overflow");
+    g.download(out + hdr, E.out, clen);
+    g.sync();
+    for (int r = 0; r < nrec; r++) s->flags[r] &= 0xffff;
+    *out_size = hdr + clen;
+    return out;
+}
+
+uint8_t *fqz_decode_gpu(const uint8_t *in, size_t in_size, size_t *out_size, int *lengths,
+                        int nlengths, fqz_slice *s) {
+    GpuCtx &g = gpu();
+    uint32_t total = 0;
+    size_t k = size_t(varint_get(in, in + in_size, &total));
+    *out_size = total;
+    Global G;
+    const int u = get_params(G, in + k, in_size - k);
+    if (u < 0) return nullptr;
+    k += size_t(u);
+    g.reset();
+    const FqzDevGlobal dg = dev_params(G);
+    FqzDecJob D{};
+    D.g = g.upload(&dg, 1);
+    D.in = g.upload(in + k, in_size - k);
+    D.in_len = in_size - k;
+    D.n = total;
+    const int nrec = s ? s->num_records : 0;
+    if (s && s->seq && nrec > 0 && s->len) {
+        unsigned boff = 0;
+        for (const Param &pm : G.p) boff = std::max(boff, pm.boff);
+        gather_seq(g, s->seq, nrec, s->len, boff, &D.seq, &D.seq_off);
+        D.nseq = uint32_t(nrec);
+    }
+    // upper bound on records: every record holds at least one byte
+    D.max_rec = (G.gflags & GF_REV) ? uint32_t(std::min<uint64_t>(total + 1, 1u << 30)) : 0;
+    D.nlengths = lengths && nlengths > 0 ? uint32_t(nlengths) : 0;
+    D.lengths = g.arena.alloc_n<uint32_t>(std::max<uint32_t>(D.nlengths, 1));
+    D.rev = g.arena.alloc_n<uint8_t>(std::max<uint32_t>(D.max_rec, 1));
+    D.rlen = g.arena.alloc_n<uint32_t>(std::max<uint32_t>(D.max_rec, 1));
+    D.models = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * FQZ_QMODEL_BYTES);
+    D.out = g.arena.alloc_n<uint8_t>(std::max<uint32_t>(total, 1));
+    D.status = g.arena.alloc_n<int32_t>(1);
+    D.nrec_out = g.arena.alloc_n<uint32_t>(1);
+    FQZ5_HIP(launch_fqz_model_init(D.models, G.max_sym + 1, g.stream));
+    FQZ5_HIP(launch_fqz_decode(D, g.stream));
+    int32_t st = 0;
+    g.download(&st, D.status, 1);
+    g.sync();
+    if (st) return nullptr;
+    uint8_t *out = static_cast<uint8_t *>(std::malloc(total ? total : 1));
+    if (!out) throw std::runtime_error("fqz: out of host memory");
+    g.download(out, D.out, total);
+    std::vector<uint32_t> lens(D.nlengths);
+    g.download(lens.data(), D.lengths, lens.size());
+    g.sync();
+    for (uint32_t r = 0; r < D.nlengths; r++) lengths[r] = int(lens[r]);
+    return out;
+}
+
+}  // namespace fqz5

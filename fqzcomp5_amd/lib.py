@@ -24,6 +24,14 @@ class RansJob(C.Structure):
                 ("status", C.c_int32), ("pad", C.c_int32)]
 
 
+class FqzSlice(C.Structure):
+    """fqz_slice (include/fqz5_mi355x.h; htscodecs fqzcomp_qual.h:59-64)."""
+    _fields_ = [("num_records", C.c_int),
+                ("len", C.POINTER(C.c_uint32)),
+                ("flags", C.POINTER(C.c_uint32)),
+                ("seq", C.POINTER(C.c_void_p))]
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -60,6 +68,12 @@ def load() -> C.CDLL:
     lib.fqz5_stream.restype = C.c_void_p
     lib.fqz5_device_ok.restype = C.c_int
     lib.fqz5_last_error.restype = C.c_char_p
+    lib.fqz_compress.restype = C.c_void_p
+    lib.fqz_compress.argtypes = [C.c_int, C.POINTER(FqzSlice), C.c_char_p, C.c_size_t,
+                                 C.POINTER(C.c_size_t), C.c_int, C.c_void_p]
+    lib.fqz_decompress.restype = C.c_void_p
+    lib.fqz_decompress.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t),
+                                   C.POINTER(C.c_int), C.c_int, C.POINTER(FqzSlice)]
     _lib = lib
     return lib
 
@@ -145,3 +159,54 @@ def uncompress_batch_dev(jobs: list[RansJob]) -> None:
         raise NativeError("fqz5_rans_uncompress_batch: " + last_error())
     for i, j in enumerate(jobs):
         j.out_size, j.status = arr[i].out_size, arr[i].status
+
+
+def _fqz_slice(lens, flags, seq: bytes | None):
+    """Build an fqz_slice over numpy-like lens/flags (uint32, modified in
+    place by fqz_compress as the reference does) and optional sequences."""
+    import numpy as np
+    lens = np.ascontiguousarray(lens, np.uint32)
+    flags = np.ascontiguousarray(flags, np.uint32)
+    nr = len(lens)
+    keep = [lens, flags]
+    S = None
+    if seq is not None:
+        sb = C.create_string_buffer(bytes(seq), len(seq) + 1)
+        keep.append(sb)
+        base = C.addressof(sb)
+        offs = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+        S = (C.c_void_p * max(nr, 1))(*[base + int(o) for o in offs[:-1]])
+        keep.append(S)
+    s = FqzSlice(nr, lens.ctypes.data_as(C.POINTER(C.c_uint32)),
+                 flags.ctypes.data_as(C.POINTER(C.c_uint32)), S)
+    return s, keep, lens, flags
+
+
+def fqz_compress(qual: bytes, lens, flags, strat: int, seq: bytes | None = None,
+                 vers: int = 4) -> bytes:
+    """fqz_compress on the GPU (host buffers; values are q-33)."""
+    s, keep, _, _ = _fqz_slice(lens, flags, seq)
+    n = C.c_size_t(0)
+    p = load().fqz_compress(vers, C.byref(s), bytes(qual), len(qual), C.byref(n), strat, None)
+    if not p:
+        raise NativeError("fqz_compress failed: " + last_error())
+    out = C.string_at(p, n.value)
+    _libc.free(p)
+    return out
+
+
+def fqz_decompress(comp: bytes, lens=None, flags=None, seq: bytes | None = None):
+    """fqz_decompress on the GPU; returns (bytes, record lengths)."""
+    import numpy as np
+    lens = np.zeros(0, np.uint32) if lens is None else lens
+    flags = np.zeros(len(lens), np.uint32) if flags is None else flags
+    s, keep, lens_a, _ = _fqz_slice(lens, flags, seq)
+    n = C.c_size_t(0)
+    nl = len(lens_a)
+    L = (C.c_int * max(nl, 1))()
+    p = load().fqz_decompress(bytes(comp), len(comp), C.byref(n), L, nl, C.byref(s))
+    if not p:
+        raise NativeError("fqz_decompress failed: " + last_error())
+    out = C.string_at(p, n.value)
+    _libc.free(p)
+    return out, [L[i] for i in range(nl)]

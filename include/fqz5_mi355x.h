@@ -5,7 +5,9 @@
  * identical names, argument meaning, ownership and error behaviour, so a
  * fqzcomp5 build links this library in place of htscodecs' CPU objects:
  *   rANS 4x16/32x16  /root/reference/htscodecs/rANS_static4x16.h:41-66
- * (fqz_compress / arith_compress_to follow in later rounds; see DESIGN.md.)
+ *   fqzcomp_qual     /root/reference/htscodecs/fqzcomp_qual.h:59-170
+ *                    (the fork's ABI: fqz_slice carries the sequences)
+ * (arith_compress_to follows in a later round; see DESIGN.md.)
  *
  * Part 2 is the batched, device-resident API used by the block codec and
  * the benchmark: many streams per call, inputs and outputs in HBM.
@@ -52,6 +54,73 @@ unsigned char *rans_uncompress_4x16(unsigned char *in, unsigned int in_size,
 /* Replaces rans_set_cpu (rANS_static4x16pr.c:1212).  Accepted and ignored:
  * the GPU kernels produce the same bytes as every reference CPU variant. */
 void rans_set_cpu(int opts);
+
+/* ---- fqzcomp_qual (htscodecs/fqzcomp_qual.h) -------------------------- */
+
+#define FQZ_FREVERSE 16          /* fqzcomp_qual.h:37 */
+#define FQZ_FREAD2 128           /* fqzcomp_qual.h:38 */
+#define FQZ_VERS 5
+
+/* fqzcomp_qual.h:59-64 (fork ABI): per-record lengths, flags (READ2 /
+ * REVERSE; bits 16+ are used as selectors during fqz_compress) and the
+ * record sequences (for sequence-context strategies, may be NULL). */
+typedef struct {
+    int num_records;
+    uint32_t *len;
+    uint32_t *flags;
+    unsigned char **seq;
+} fqz_slice;
+
+/* fqzcomp_qual.h:92-139: one parameter block / the global parameters. */
+typedef struct {
+    uint16_t context;
+    unsigned int pflags;
+    unsigned int do_sel, do_dedup, store_qmap, fixed_len;
+    unsigned char use_qtab, use_dtab, use_ptab;
+    unsigned int qbits, qloc;
+    unsigned int pbits, ploc;
+    unsigned int dbits, dloc;
+    unsigned int sbits, sloc;
+    unsigned int bbits, bloc, boff;
+    int max_sym, nsym, max_sel;
+    unsigned int qmap[256];
+    unsigned int qtab[256];
+    unsigned int ptab[1024];
+    unsigned int dtab[256];
+    int qshift;
+    int pshift;
+    int dshift;
+    int sshift;
+    unsigned int qmask;
+    int do_r2, do_qa;
+} fqz_param;
+
+typedef struct {
+    int vers;
+    unsigned int gflags;
+    int nparam;
+    int max_sel;
+    unsigned int stab[256];
+    int max_sym;
+    fqz_param *p;
+} fqz_gparams;
+
+/* Replaces fqz_compress (fqzcomp_qual.c:1636).  Encodes in_size quality
+ * bytes (values q-33) of s->num_records records.  Like the reference it
+ * may rewrite s->len[] to fit in_size and uses the top 16 bits of
+ * s->flags[] as selectors while running (cleared on return).  gp == NULL
+ * picks parameters from the data (strat 0..4); a caller-supplied gp is used
+ * as is (and, as in the reference, its position / delta tables are
+ * shifted in place).  Returns a malloc()ed stream (caller frees), NULL on
+ * failure. */
+char *fqz_compress(int vers, fqz_slice *s, char *in, size_t in_size,
+                   size_t *out_size, int strat, fqz_gparams *gp);
+
+/* Replaces fqz_decompress (fqzcomp_qual.c:1642).  lengths[0..nlengths)
+ * receive the record lengths; s may carry the decoded sequences for
+ * sequence-context streams.  malloc()ed result, NULL on failure. */
+char *fqz_decompress(char *in, size_t in_size, size_t *out_size,
+                     int *lengths, int nlengths, fqz_slice *s);
 
 /* ---- Part 2: batched device API --------------------------------------- */
 

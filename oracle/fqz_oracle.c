@@ -533,7 +533,7 @@ static int pick_params(fglobal *g, int vers, int strat, int nrec, uint32_t *lens
     pm->qmap_stored = (pm->nsym <= 8 && pm->nsym * 2 < pm->max_sym);
     int r = 1;
     while (r < nrec && lens[r] == lens[0]) r++;
-    pm->fixed = (r >= nrec);
+    pm->fixed = (r == nrec);
     pm->qtab_on = 0;
 
     if (strat < NSTRATS - 1) {

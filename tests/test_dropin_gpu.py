@@ -1,9 +1,10 @@
 """Drop-in integration on the GPU: the reference fqzcomp5 CLI relinked with
-libfqz5_mi355x.so in place of its rANS 4x16/32x16 objects (oracle/Makefile
-target _ref/fqzcomp5_gpu) must write the same .fqz5 bytes
-as the CLI built as shipped, and decode them back to the input.  Every
-rANS call fqzcomp5 makes (sequence, quality, lengths, tok3 name columns,
-compressed O1 headers) then runs on the GPU."""
+libfqz5_mi355x.so in place of its rANS 4x16/32x16 and fqzcomp_qual objects
+(oracle/Makefile target _ref/fqzcomp5_gpu) must write the
+same .fqz5 bytes as the CLI built as shipped, and decode them back to the
+input.  Every rANS call fqzcomp5 makes (sequence, quality, lengths, tok3
+name columns, compressed O1 headers) and every fqz_compress /
+fqz_decompress (-5 quality methods) then runs on the GPU."""
 import os
 import subprocess
 
