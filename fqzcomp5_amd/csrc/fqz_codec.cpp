@@ -356,6 +356,90 @@ void gather_seq(GpuCtx &g, unsigned char **seq, int nrec, const uint32_t *lens,
     *d_off = g.upload(off);
 }
 
+// The parallel encoder (fqz_kernels.hip "parallel encoder"): events per
+// record, scan, stable sort by model, per-model pass, range coder.
+void encode_events(GpuCtx &g, const FqzEncJob &E, const Global &G, int nrec) {
+    FqzEvJob J{};
+    J.g = E.g;
+    J.q = E.q;
+    J.len = E.len;
+    J.sel = E.sel;
+    J.flags = E.flags;
+    J.nrec = uint32_t(nrec);
+    J.seq = E.seq;
+    J.seq_off = E.seq_off;
+    std::vector<uint64_t> off(static_cast<size_t>(nrec));
+    uint64_t o = 0;
+    std::vector<uint32_t> lens(static_cast<size_t>(nrec));
+    g.download(lens.data(), E.len, lens.size());
+    g.sync();
+    for (int r = 0; r < nrec; r++) off[size_t(r)] = o, o += lens[size_t(r)];
+    J.off = g.upload(off);
+    J.nev_rec = g.arena.alloc_n<uint32_t>(size_t(nrec));
+    uint32_t *ev_off = g.arena.alloc_n<uint32_t>(size_t(nrec));
+    J.ev_off = ev_off;
+    J.dup = g.arena.alloc_n<uint8_t>(size_t(nrec));
+    FQZ5_HIP(launch_fqz_events(J, 0, g.stream));
+    size_t tb = 0;
+    FQZ5_HIP(fqz_exclusive_scan(J.nev_rec, ev_off, nrec, nullptr, tb, g.stream));
+    void *tmp = g.arena.alloc_n<uint8_t>(tb);
+    FQZ5_HIP(fqz_exclusive_scan(J.nev_rec, ev_off, nrec, tmp, tb, g.stream));
+    uint32_t last[2] = {0, 0};
+    g.download(&last[0], ev_off + nrec - 1, 1);
+    g.download(&last[1], J.nev_rec + nrec - 1, 1);
+    g.sync();
+    const uint64_t nev = uint64_t(last[0]) + last[1];
+    if (nev >= (1ull << 31)) throw std::runtime_error("fqz: block too large");
+    J.nev = uint32_t(nev);
+    J.key = g.arena.alloc_n<uint32_t>(nev);
+    J.val = g.arena.alloc_n<uint64_t>(nev);
+    uint32_t *skey = g.arena.alloc_n<uint32_t>(nev);
+    uint64_t *sval = g.arena.alloc_n<uint64_t>(nev);
+    J.skey = skey;
+    J.sval = sval;
+    J.code = g.arena.alloc_n<uint64_t>(nev);
+    FQZ5_HIP(launch_fqz_events(J, 1, g.stream));
+    tb = 0;
+    FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(nev), int(FQZ_MODEL_BITS), nullptr,
+                               tb, g.stream));
+    tmp = g.arena.alloc_n<uint8_t>(tb);
+    FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(nev), int(FQZ_MODEL_BITS), tmp, tb,
+                               g.stream));
+    J.seg_lo = g.arena.alloc_n<uint32_t>(FQZ_NMODELS);
+    J.seg_hi = g.arena.alloc_n<uint32_t>(FQZ_NMODELS);
+    g.memset0(J.seg_lo, FQZ_NMODELS * 4);
+    g.memset0(J.seg_hi, FQZ_NMODELS * 4);
+    FQZ5_HIP(launch_fqz_events(J, 2, g.stream));
+    J.scratch = g.arena.alloc_n<uint8_t>(8192);
+    FQZ5_HIP(launch_fqz_model_pass(J, g.stream));
+    // the range chain, then the output bytes as a big-number sum
+    J.rec = g.arena.alloc_n<uint4>(nev);
+    FQZ5_HIP(launch_fqz_expand(J, g.stream));
+    J.addend = g.arena.alloc_n<uint32_t>(nev);
+    J.shifts = g.arena.alloc_n<uint32_t>(nev + 1);
+    FQZ5_HIP(launch_fqz_rc(J, g.stream));
+    uint32_t *pos = g.arena.alloc_n<uint32_t>(nev + 1);
+    g.memset0(J.shifts + nev, 4);
+    tb = 0;
+    FQZ5_HIP(fqz_exclusive_scan(J.shifts, pos, int(nev + 1), nullptr, tb, g.stream));
+    tmp = g.arena.alloc_n<uint8_t>(tb);
+    FQZ5_HIP(fqz_exclusive_scan(J.shifts, pos, int(nev + 1), tmp, tb, g.stream));
+    J.pos = pos;
+    J.nshift = pos + nev;
+    uint32_t P = 0;
+    g.download(&P, pos + nev, 1);
+    g.sync();
+    J.nwords = (P + 5 + 3) / 4 + 2;
+    J.acc = reinterpret_cast<unsigned long long *>(g.arena.alloc_n<uint64_t>(J.nwords));
+    g.memset0(J.acc, size_t(J.nwords) * 8);
+    J.out = E.out;
+    J.out_len = E.out_len;
+    FQZ5_HIP(launch_fqz_bytes(J, 0, g.stream));
+    FQZ5_HIP(launch_fqz_bytes(J, 1, g.stream));
+    FQZ5_HIP(launch_fqz_bytes(J, 2, g.stream));
+    (void)G;
+}
+
 }  // namespace
 
 uint8_t *fqz_encode_gpu(int vers, fqz_slice *s, const uint8_t *in, size_t n, size_t *out_size,
@@ -445,12 +529,21 @@ uint8_t *fqz_encode_gpu(int vers, fqz_slice *s, const uint8_t *in, size_t n, siz
         for (const Param &pm : G.p) boff = std::max(boff, pm.boff);
         gather_seq(g, s->seq, nrec, s->len, boff, &E.seq, &E.seq_off);
     }
-    E.models = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * FQZ_QMODEL_BYTES);
-    FQZ5_HIP(launch_fqz_model_init(E.models, G.max_sym + 1, g.stream));
     const size_t room = cap - hdr;
     E.out = g.arena.alloc_n<uint8_t>(room);
     E.out_len = g.arena.alloc_n<uint32_t>(1);
-    FQZ5_HIP(launch_fqz_encode(E, g.stream));
+    // The parallel encoder covers one parameter block and non-empty records
+    // (the reference's loop codes the next record's first byte inside an
+    // empty record, which only its literal serial form reproduces).
+    bool parallel = G.nparam == 1 && !(G.gflags & GF_MULTI) && nrec > 0;
+    for (int r = 0; parallel && r < nrec; r++) parallel = s->len[r] > 0;
+    if (parallel) {
+        encode_events(g, E, G, nrec);
+    } else {
+        E.models = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * FQZ_QMODEL_BYTES);
+        FQZ5_HIP(launch_fqz_model_init(E.models, G.max_sym + 1, g.stream));
+        FQZ5_HIP(launch_fqz_encode(E, g.stream));
+    }
     uint32_t clen = 0;
     g.download(&clen, E.out_len, 1);
     g.sync();

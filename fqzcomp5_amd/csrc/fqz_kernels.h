@@ -74,6 +74,56 @@ struct FqzDecJob {
     uint32_t *nrec_out;
 };
 
+// Parallel encoder (fqz_kernels.hip): the block becomes a list of coding
+// events (record headers and quality symbols) in stream order; events are
+// stably sorted by the model they use, every model runs over its own
+// events in parallel to produce (cum, freq, total), and one lane range-codes
+// the events in stream order.  Model ids: quality contexts 0..65535, then:
+constexpr uint32_t FQZ_M_SEL = 65536, FQZ_M_LEN = 65537, FQZ_M_REV = 65541,
+                   FQZ_M_DUP = 65542, FQZ_NMODELS = 65543, FQZ_MODEL_BITS = 17;
+
+struct FqzEvJob {
+    const FqzDevGlobal *g;
+    const uint8_t *q;
+    const uint64_t *off;        // record offsets
+    const uint32_t *len, *sel, *flags;
+    uint32_t nrec, nev;
+    const uint8_t *seq;
+    const uint64_t *seq_off;
+    uint32_t *nev_rec;          // per-record event counts
+    const uint32_t *ev_off;     // their exclusive scan
+    uint8_t *dup;               // per-record duplicate flag
+    uint32_t *key;              // events: model id
+    uint64_t *val;              // events: index << 8 | symbol
+    const uint32_t *skey;       // events sorted by model
+    const uint64_t *sval;
+    uint32_t *seg_lo, *seg_hi;  // per model: its range in the sorted order
+    uint64_t *code;             // per sorted event: cum | freq << 16 | total << 32
+    uint8_t *scratch;           // the non-quality models
+    uint4 *rec;                 // per event: {RN(1/total) (2 words), freq | cum << 16, 0}
+    uint32_t *addend;           // per event: cum * (range / total)
+    uint32_t *shifts;           // per event: coder byte shifts, then their scan
+    const uint32_t *pos;        // exclusive scan of shifts
+    uint32_t *nshift;           // total shifts
+    unsigned long long *acc;    // little-endian 32-bit columns of the sum
+    uint32_t nwords;
+    uint32_t pad2;
+    uint8_t *out;
+    uint32_t *out_len;
+};
+
+hipError_t launch_fqz_events(const FqzEvJob &j, int phase, hipStream_t s);
+hipError_t launch_fqz_model_pass(const FqzEvJob &j, hipStream_t s);
+hipError_t launch_fqz_expand(const FqzEvJob &j, hipStream_t s);
+hipError_t launch_fqz_rc(const FqzEvJob &j, hipStream_t s);
+hipError_t launch_fqz_bytes(const FqzEvJob &j, int phase, hipStream_t s);
+// fqz_sort.hip
+hipError_t fqz_exclusive_scan(const uint32_t *in, uint32_t *out, int n, void *tmp, size_t &bytes,
+                              hipStream_t s);
+hipError_t fqz_sort_by_model(const uint32_t *k_in, uint32_t *k_out, const uint64_t *v_in,
+                             uint64_t *v_out, int n, int key_bits, void *tmp, size_t &bytes,
+                             hipStream_t s);
+
 hipError_t launch_fqz_records(const FqzStatJob &j, hipStream_t s);
 hipError_t launch_fqz_hist(const FqzStatJob &j, int nchunks, int mode, hipStream_t s);
 hipError_t launch_fqz_model_init(uint8_t *models, int live, hipStream_t s);

@@ -407,6 +407,333 @@ __global__ __launch_bounds__(64) void k_fqz_decode(FqzDecJob J) {
 }
 
 // --------------------------------------------------------------------------
+// parallel encoder
+// --------------------------------------------------------------------------
+// Records of a block are independent except through the models and the
+// coder: the duplicate test compares a record with its predecessor only,
+// and the context of every quality symbol depends only on its own record
+// (the context state resets at each record, fqzcomp_qual.c:1154-1173).
+
+// Phase 0: per-record duplicate flag and event count.
+__global__ void k_fqz_ev_count(FqzEvJob J) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= J.nrec) return;
+    const FqzDevGlobal &g = *J.g;
+    const FqzDevParam &pm = g.p[0];
+    const uint32_t len = J.len[r];
+    const uint64_t off = J.off[r];
+    bool dup = false;
+    if (pm.dedup && off > 0 && J.len[r - 1] == len) {
+        const uint8_t *a = J.q + off - len, *b = J.q + off;
+        uint32_t t = 0;
+        while (t < len && a[t] == b[t]) t++;
+        dup = t == len;
+    }
+    J.dup[r] = dup;
+    uint32_t n = 0;
+    if (pm.sel || (g.gflags & 1u)) n++;
+    if (!pm.fixed || r == 0) n += 4;
+    if (g.gflags & 4u) n++;
+    if (pm.dedup) n++;
+    if (!dup) n += len;
+    J.nev_rec[r] = n;
+}
+
+// Phase 1: the events of each record in stream order (compress_block_fqz2f
+// record header, fqzcomp_qual.c:1119-1192, then one event per quality).
+__global__ void k_fqz_ev_fill(FqzEvJob J) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= J.nrec) return;
+    const FqzDevGlobal &g = *J.g;
+    const FqzDevParam &pm = g.p[0];
+    uint32_t e = J.ev_off[r];
+    const uint32_t len = J.len[r];
+    const bool dup = J.dup[r];
+    auto put = [&](uint32_t model, uint32_t sym) {
+        J.key[e] = model;
+        J.val[e] = (uint64_t(e) << 8) | sym;
+        e++;
+    };
+    Ctx st{};
+    if (pm.sel || (g.gflags & 1u)) {
+        st.sel = J.sel[r];
+        put(FQZ_M_SEL, st.sel);
+    }
+    if (!pm.fixed || r == 0)
+        for (uint32_t b = 0; b < 4; b++) put(FQZ_M_LEN + b, (len >> (8 * b)) & 0xffu);
+    if (g.gflags & 4u) put(FQZ_M_REV, (J.flags[r] & 16u) ? 1u : 0u);
+    if (pm.dedup) put(FQZ_M_DUP, dup);
+    if (dup) return;
+    st.left = len;
+    const uint8_t *sp = nullptr, *se = nullptr;
+    if (J.seq && J.seq_off[r] != ~0ull) {
+        const uint8_t *s0 = J.seq + J.seq_off[r];
+        sp = s0 + pm.boff;
+        se = s0 + len;
+        for (uint32_t b = 0; b < pm.boff; b++) st.seq = (st.seq << 2) | base2(s0[b]);
+    }
+    const uint8_t *q = J.q + J.off[r];
+    uint32_t ctx = pm.ctx0;
+    for (uint32_t t = 0; t < len; t++) {
+        const uint32_t sym = pm.qmap[q[t]];
+        const uint32_t base = sp && sp < se ? base2(*sp++) : 0u;
+        put(ctx, sym);
+        ctx = next_ctx(pm, st, sym, base);
+    }
+}
+
+// Phase 2 (after the sort): each model's range in the sorted events.
+__global__ void k_fqz_segments(FqzEvJob J) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= J.nev) return;
+    const uint32_t k = J.skey[i];
+    if (i == 0 || J.skey[i - 1] != k) J.seg_lo[k] = i;
+    if (i == J.nev - 1 || J.skey[i + 1] != k) J.seg_hi[k] = i + 1;
+}
+
+// Phase 3: every model over its own events, in stream order, writing the
+// codes in sorted order.  Quality models live in LDS (one per lane); the
+// header models in global scratch.  Events go in batches of 32: the loads
+// of a batch are issued together and its stores after it, so a lane waits
+// for memory once per batch.
+template <int CAP> DEV void model_run(FList<CAP> *m, const FqzEvJob &J, uint32_t lo, uint32_t hi) {
+    constexpr uint32_t B = 32;
+    // Slot 1 (the head) and the total are kept in registers while the
+    // symbols hit the head; LDS is synchronised before any other update.
+    // The head never bubbles (slot 0 always wins the comparison).
+    uint32_t s1 = m->sy[1], f1 = m->fr[1], tot = m->total;
+    for (uint32_t k0 = lo; k0 < hi; k0 += B) {
+        const uint32_t nb = min(B, hi - k0);
+        uint32_t sv[B];
+#pragma unroll
+        for (uint32_t u = 0; u < B; u++) sv[u] = u < nb ? uint32_t(J.sval[k0 + u]) & 0xffu : 0u;
+        uint64_t cd[B];
+#pragma unroll
+        for (uint32_t u = 0; u < B; u++) {
+            cd[u] = 0;
+            if (u < nb) {
+                const uint32_t sym = sv[u];
+                if (sym == s1 && tot + FL_STEP <= FL_MAX) {
+                    cd[u] = (uint64_t(f1) << 16) | (uint64_t(tot) << 32);
+                    f1 += FL_STEP;
+                    tot += FL_STEP;
+                } else {
+                    m->fr[1] = uint16_t(f1);
+                    m->total = tot;
+                    uint32_t acc = 0;
+                    int s = 1;
+                    while (m->sy[s] != sym) acc += m->fr[s++];
+                    cd[u] = uint64_t(acc) | (uint64_t(m->fr[s]) << 16) | (uint64_t(tot) << 32);
+                    fl_bump(m, s);
+                    s1 = m->sy[1];
+                    f1 = m->fr[1];
+                    tot = m->total;
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < B; u++)
+            if (u < nb) J.code[k0 + u] = cd[u];
+    }
+    m->fr[1] = uint16_t(f1);
+    m->total = tot;
+}
+
+__global__ __launch_bounds__(256) void k_fqz_model_pass(FqzEvJob J) {
+    FList<FQZ_QSYMS> *lm = reinterpret_cast<FList<FQZ_QSYMS> *>(fqz_lds);   // 256 models
+    const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= FQZ_NMODELS) return;
+    const uint32_t lo = J.seg_lo[m], hi = J.seg_hi[m];
+    if (lo >= hi) return;
+    const FqzDevGlobal &g = *J.g;
+    if (m < FQZ_M_SEL) {
+        FList<FQZ_QSYMS> *ml = &lm[threadIdx.x];
+        fl_init(ml, int(g.max_sym) + 1);
+        model_run(ml, J, lo, hi);
+    } else if (m < FQZ_M_REV) {
+        FList<256> *mg = reinterpret_cast<FList<256> *>(J.scratch) + (m - FQZ_M_SEL);
+        fl_init(mg, m == FQZ_M_SEL ? int(g.max_sel) + 1 : 256);
+        model_run(mg, J, lo, hi);
+    } else {
+        FList<2> *mg = reinterpret_cast<FList<2> *>(J.scratch + 5 * sizeof(FList<256>)) +
+                       (m - FQZ_M_REV);
+        fl_init(mg, 2);
+        model_run(mg, J, lo, hi);
+    }
+}
+
+// Phase 3b: per event (in stream order) the record the range chain reads:
+// {RN(1/total) as two words, freq, cum}.
+__global__ void k_fqz_expand(FqzEvJob J) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= J.nev) return;
+    const uint32_t e = uint32_t(J.sval[k] >> 8);
+    const uint64_t c = J.code[k];
+    const double rd = 1.0 / double(uint32_t(c >> 32));
+    const uint64_t bits = uint64_t(__double_as_longlong(rd));
+    J.rec[e] = make_uint4(uint32_t(bits), uint32_t(bits >> 32), uint32_t(c >> 16) & 0xffffu,
+                          uint32_t(c) & 0xffffu);
+}
+
+// Phase 4: the range coder over the events in stream order (RC_Encode,
+// c_range_coder.h:133-145).  The only serial dependence is the range:
+//   q = range / total;  range = renorm(q * freq)
+// so one lane computes just that chain and records per event the amount
+// added to `low` (cum * q, < 2^32) and the number of byte shifts.  The
+// division is exact through the double reciprocal: for range < 2^32 and
+// total <= 65519, |range * RN(1/total) - range/total| < 2^-20, below the
+// distance 1/total to the next integer, so adding 2^-19 and truncating
+// gives floor(range/total).  Blocks of events are staged through LDS by all
+// lanes (coalesced), lane 0 runs the chain from LDS, and its outputs are
+// flushed by all lanes: the lane's reads never wait behind global stores
+// (CDNA's vmcnt counts both).
+constexpr uint32_t RC_BLK = 4096;
+
+__global__ __launch_bounds__(64) void k_fqz_rc(FqzEvJob J) {
+    __shared__ uint4 in[RC_BLK + 8];
+    __shared__ uint4 o_q[RC_BLK / 4];
+    __shared__ uint2 o_k[RC_BLK / 8];
+    const int l = int(threadIdx.x);
+    uint32_t rng = 0xFFFFFFFFu;
+    const double bias = 1.0 / 524288.0;           // 2^-19
+    for (uint32_t base = 0; base < J.nev; base += RC_BLK) {
+        const uint32_t cnt = min(RC_BLK, J.nev - base);
+        for (uint32_t i = l; i < cnt; i += 64) in[i] = J.rec[base + i];
+        __syncthreads();
+        if (l == 0) {
+            // q and the shift count of one event; renorm: shifts = clz / 8
+            // (range >= 1 always), i.e. range <<= clz & 24
+            auto step = [&](const uint4 r, uint32_t &q, uint32_t &k) {
+                const double rd = __longlong_as_double((long long)(uint64_t(r.y) << 32 | r.x));
+                q = uint32_t(__fma_rn(double(rng), rd, bias));
+                rng = q * r.z;
+                const uint32_t z = uint32_t(__builtin_clz(rng)) & 24u;
+                rng <<= z;
+                k = z >> 3;
+            };
+            const uint32_t full = cnt & ~7u;
+            for (uint32_t i = 0; i < full; i += 8) {
+                uint4 r[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) r[u] = in[i + u];
+                uint32_t q[8], k[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) step(r[u], q[u], k[u]);
+                o_q[i / 4] = make_uint4(q[0], q[1], q[2], q[3]);
+                o_q[i / 4 + 1] = make_uint4(q[4], q[5], q[6], q[7]);
+                o_k[i / 8] = make_uint2(k[0] | k[1] << 8 | k[2] << 16 | k[3] << 24,
+                                        k[4] | k[5] << 8 | k[6] << 16 | k[7] << 24);
+            }
+            uint32_t *oq = reinterpret_cast<uint32_t *>(o_q);
+            uint8_t *ok = reinterpret_cast<uint8_t *>(o_k);
+            for (uint32_t i = full; i < cnt; i++) {
+                uint32_t q, k;
+                step(in[i], q, k);
+                oq[i] = q;
+                ok[i] = uint8_t(k);
+            }
+        }
+        __syncthreads();
+        const uint32_t *oq = reinterpret_cast<const uint32_t *>(o_q);
+        const uint8_t *ok = reinterpret_cast<const uint8_t *>(o_k);
+        for (uint32_t i = l; i < cnt; i += 64) {
+            J.addend[base + i] = oq[i];          // q here; cum * q in k_fqz_accum
+            J.shifts[base + i] = ok[i];
+        }
+        __syncthreads();
+    }
+}
+
+// The coder's output is the base-256 number S = sum_i addend_i *
+// 256^(P - P_i) written as P + 5 bytes, most significant first (P_i: shifts
+// before event i, P: all shifts): low is a 4-byte window that moves one byte
+// per shift, and the pending-byte / FF-run / carry logic of RC_ShiftLow
+// (c_range_coder.h:78-101) is exactly the carry propagation of that sum.
+// Phase A: add every addend into little-endian 32-bit columns (u64 each).
+__global__ void k_fqz_accum(FqzEvJob J) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= J.nev) return;
+    const uint32_t e = *J.nshift - J.pos[i];          // byte index of the LSB
+    const uint32_t cum = J.rec[i].w;
+    const uint64_t v = uint64_t(cum * J.addend[i]) << (8 * (e & 3));
+    atomicAdd(&J.acc[e >> 2], (unsigned long long)(v & 0xffffffffull));
+    if (v >> 32) atomicAdd(&J.acc[(e >> 2) + 1], (unsigned long long)(v >> 32));
+}
+
+// Phase B: carry propagation through the columns.  The wave loads 64
+// columns at a time; the carry walks them in lane order on scalar registers.
+__global__ __launch_bounds__(64) void k_fqz_carry(FqzEvJob J) {
+    const int l = int(threadIdx.x);
+    unsigned long long carry = 0;
+    for (uint32_t w0 = 0; w0 < J.nwords; w0 += 64) {
+        const uint32_t w = w0 + uint32_t(l);
+        const unsigned long long v = w < J.nwords ? J.acc[w] : 0ull;
+        uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32), res = 0;
+        for (int k = 0; k < 64; k++) {
+            const uint32_t h = uint32_t(__builtin_amdgcn_readlane(int(hi), k));
+            const uint32_t w32 = uint32_t(__builtin_amdgcn_readlane(int(lo), k));
+            const unsigned long long t = ((unsigned long long)h << 32 | w32) + carry;
+            if (l == k) res = uint32_t(t);
+            carry = t >> 32;
+        }
+        if (w < J.nwords) J.acc[w] = res;
+    }
+}
+
+// Phase C: bytes, most significant first.
+__global__ void k_fqz_emit(FqzEvJob J) {
+    const uint32_t nb = *J.nshift + 5;
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d == 0) *J.out_len = nb;
+    if (d >= nb) return;
+    const uint32_t e = nb - 1 - d;
+    J.out[d] = uint8_t(J.acc[e >> 2] >> (8 * (e & 3)));
+}
+
+hipError_t launch_fqz_events(const FqzEvJob &j, int phase, hipStream_t s) {
+    if (phase == 0 && j.nrec)
+        hipLaunchKernelGGL(k_fqz_ev_count, dim3((j.nrec + 255) / 256), dim3(256), 0, s, j);
+    else if (phase == 1 && j.nrec)
+        hipLaunchKernelGGL(k_fqz_ev_fill, dim3((j.nrec + 255) / 256), dim3(256), 0, s, j);
+    else if (phase == 2 && j.nev)
+        hipLaunchKernelGGL(k_fqz_segments, dim3((j.nev + 255) / 256), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_fqz_expand(const FqzEvJob &j, hipStream_t s) {
+    if (j.nev) hipLaunchKernelGGL(k_fqz_expand, dim3((j.nev + 255) / 256), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_fqz_model_pass(const FqzEvJob &j, hipStream_t s) {
+    constexpr uint32_t lds = 256 * sizeof(FList<FQZ_QSYMS>);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_fqz_model_pass),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_fqz_model_pass, dim3((FQZ_NMODELS + 255) / 256), dim3(256), lds, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_fqz_rc(const FqzEvJob &j, hipStream_t s) {
+    hipLaunchKernelGGL(k_fqz_rc, dim3(1), dim3(64), 0, s, j);
+    return hipGetLastError();
+}
+
+// phase 0: columns; 1: carries; 2: bytes (grid from the host's bound)
+hipError_t launch_fqz_bytes(const FqzEvJob &j, int phase, hipStream_t s) {
+    if (phase == 0 && j.nev)
+        hipLaunchKernelGGL(k_fqz_accum, dim3((j.nev + 255) / 256), dim3(256), 0, s, j);
+    else if (phase == 1)
+        hipLaunchKernelGGL(k_fqz_carry, dim3(1), dim3(64), 0, s, j);
+    else if (phase == 2)
+        hipLaunchKernelGGL(k_fqz_emit, dim3((4 * j.nwords + 255) / 256), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------------------------
 hipError_t launch_fqz_records(const FqzStatJob &j, hipStream_t s) {
     if (!j.nrec) return hipSuccess;
     hipLaunchKernelGGL(k_fqz_records, dim3((j.nrec + 255) / 256), dim3(256), 0, s, j);

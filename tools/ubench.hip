@@ -96,6 +96,29 @@ __global__ void k(uint32_t *out, uint64_t *cyc, uint32_t a, uint32_t b) {
             x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
             nw = __builtin_amdgcn_mbcnt_lo(uint32_t(m) & 15u, nw + 0u * l) + 0;
         }
+        if (T == 12) {                                           // f64 fma dep chain
+            double d = double(x);
+            d = __fma_rn(d, 1.0000001, 0.5);
+            x = uint32_t(__double_as_longlong(d));
+        }
+        if (T == 13) {                                           // u32 -> f64 -> fma -> u32
+            x = uint32_t(__fma_rn(double(x), 0.999999, 1.0 / 524288.0));
+        }
+        if (T == 14) {                                           // mul_lo u32 dep
+            x = x * y + 1;
+        }
+        if (T == 15) {                                           // fqz range step
+            const uint32_t q = uint32_t(__fma_rn(double(x | 0x1000000u), 1.0 / 3000.0, 1.0 / 524288.0));
+            uint32_t r = q * (y & 0xfff);
+            const uint32_t k = r < (1u << 24) ? (__clz(r) >> 3) : 0u;
+            x = r << (8 * k);
+        }
+        if (T == 16) {                                           // f32 rcp-based u32 div + fix
+            const float fq = float(x) * __builtin_amdgcn_rcpf(float(y | 1));
+            uint32_t q = uint32_t(fq);
+            q += (x - q * (y | 1)) >= (y | 1);
+            x = q + 12345;
+        }
         if (T == 11) {                                           // dec: table lookup + arith only
             const uint32_t e = lds[x & 4095];
             const uint32_t xh = x >> 12;
@@ -137,5 +160,10 @@ int main() {
     run<9>("dec step, DPP quad rank");
     run<10>("dec step, mbcnt ptr");
     run<11>("dec lookup+arith only");
+    run<12>("f64 fma dep (+bitcast)");
+    run<13>("u32->f64 fma->u32 dep");
+    run<14>("mul_lo u32 + add dep");
+    run<15>("fqz range step");
+    run<16>("f32 rcp div + 1 fix");
     return 0;
 }
