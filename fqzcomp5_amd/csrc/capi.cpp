@@ -8,6 +8,7 @@
 #include "../../include/fqz5_mi355x.h"
 #include "rans_codec.hpp"
 #include "rans_format.hpp"
+#include "fqz_kernels.h"
 
 namespace fqz5 {
 
@@ -249,6 +250,24 @@ void fqz5_profile_read(double *out6) {
         out6[3] = p.dec_ms; out6[4] = p.dec_launches; out6[5] = p.dec_bytes;
     } catch (const std::exception &e) {
         g_err = e.what();
+    }
+}
+
+long fqz5_fqz_div_selftest(void) {
+    try {
+        GpuCtx &g = gpu();
+        g.reset();
+        uint32_t *d = g.arena.alloc_n<uint32_t>(1);
+        g.memset0(d, sizeof(uint32_t));
+        FQZ5_HIP(fqz_div_selftest(d, g.stream));
+        uint32_t bad = 0;
+        g.download(&bad, d, 1);
+        g.sync();
+        g.reset();
+        return long(bad);
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
     }
 }
 

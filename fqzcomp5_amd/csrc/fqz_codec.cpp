@@ -579,21 +579,59 @@ uint8_t *fqz_decode_gpu(const uint8_t *in, size_t in_size, size_t *out_size, int
         gather_seq(g, s->seq, nrec, s->len, boff, &D.seq, &D.seq_off);
         D.nseq = uint32_t(nrec);
     }
-    // upper bound on records: every record holds at least one byte
-    D.max_rec = (G.gflags & GF_REV) ? uint32_t(std::min<uint64_t>(total + 1, 1u << 30)) : 0;
     D.nlengths = lengths && nlengths > 0 ? uint32_t(nlengths) : 0;
     D.lengths = g.arena.alloc_n<uint32_t>(std::max<uint32_t>(D.nlengths, 1));
-    D.rev = g.arena.alloc_n<uint8_t>(std::max<uint32_t>(D.max_rec, 1));
-    D.rlen = g.arena.alloc_n<uint32_t>(std::max<uint32_t>(D.max_rec, 1));
-    D.models = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * FQZ_QMODEL_BYTES);
     D.out = g.arena.alloc_n<uint8_t>(std::max<uint32_t>(total, 1));
     D.status = g.arena.alloc_n<int32_t>(1);
     D.nrec_out = g.arena.alloc_n<uint32_t>(1);
-    FQZ5_HIP(launch_fqz_model_init(D.models, G.max_sym + 1, g.stream));
-    FQZ5_HIP(launch_fqz_decode(D, g.stream));
+    D.counts = g.arena.alloc_n<uint32_t>(32);
+    g.memset0(D.counts, 32 * sizeof(uint32_t));
+    const uint32_t live = uint32_t(G.max_sym) + 1;
+    if (live > FQZ_DEC_MAX_LIVE) return nullptr;
+    D.ment = fqz_dec_model_bytes(live);
+    D.nsets = FQZ_DEC_CACHE_BYTES / D.ment;
+    D.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * D.ment);
+    bool seq_ctx = false, dedup = false, map = false, qid = true;
+    for (const Param &pm : G.p) {
+        seq_ctx = seq_ctx || pm.bbits > 0;
+        for (int i = 0; i < 256; i++) qid = qid && (pm.qtab[i] & 0xffffu) == unsigned(i);
+        dedup = dedup || pm.dedup;
+        for (int i = 0; i < 256; i++) map = map || pm.qmap[i] != unsigned(i);
+    }
+    seq_ctx = seq_ctx && D.seq;
+    const bool rev = (G.gflags & GF_REV) != 0;
+    const int map_mode = !map ? 0 : G.nparam > 1 ? 2 : 1;
+    // record lists: sized for the records the caller announced, grown to
+    // the byte count (every record holds at least one byte) on overflow
+    uint32_t cap = std::max<uint32_t>({D.nlengths, D.nseq, 1u}) + 1024;
     int32_t st = 0;
-    g.download(&st, D.status, 1);
-    g.sync();
+    for (int attempt = 0; attempt < 2; attempt++) {
+        D.cap_list = (dedup || rev || map_mode == 2) ? std::min<uint32_t>(cap, total + 1) : 0;
+        const size_t c = std::max<uint32_t>(D.cap_list, 1);
+        D.recs = g.arena.alloc_n<uint4>(map_mode == 2 ? c : 1);
+        D.dups = g.arena.alloc_n<uint2>(dedup ? c : 1);
+        D.revs = g.arena.alloc_n<uint2>(rev ? c : 1);
+        FQZ5_HIP(launch_fqz_dec(D, live + 2 <= 64 ? 1 : 2, seq_ctx, qid, g.stream));
+        FQZ5_HIP(launch_fqz_dec_fix(D, map_mode, dedup, rev, g.stream));
+        g.download(&st, D.status, 1);
+        g.sync();
+        if (st != -2) break;
+        cap = total + 1;
+    }
+    if (std::getenv("FQZ5_DEBUG")) {
+        uint32_t c[5];
+        g.download(c, D.counts, 5);
+        g.sync();
+        std::fprintf(stderr, "[fqz dec] n=%u live=%u ment=%u sets=%u recs=%u dups=%u revs=%u misses=%u slow=%u\n",
+                     total, live, D.ment, D.nsets, c[0], c[1], c[2], c[3], c[4]);
+        uint64_t pr[6];
+        g.download(pr, reinterpret_cast<const uint64_t *>(D.counts + 8), 6);
+        g.sync();
+        if (pr[0] | pr[1])
+            std::fprintf(stderr, "[fqz dec] cycles/symbol: wait %.1f chain %.1f coder %.1f update %.1f tail %.1f loop %.1f\n",
+                         double(pr[0]) / total, double(pr[1]) / total, double(pr[2]) / total,
+                         double(pr[3]) / total, double(pr[4]) / total, double(pr[5]) / total);
+    }
     if (st) return nullptr;
     uint8_t *out = static_cast<uint8_t *>(std::malloc(total ? total : 1));
     if (!out) throw std::runtime_error("fqz: out of host memory");

@@ -1,0 +1,720 @@
+// fqz_decode.hip — fqzcomp_qual decoder (uncompress_block_fqz2f,
+// fqzcomp_qual.c:1410-1634) on one wavefront per block.
+//
+// Decoding is one dependent chain per block: every symbol needs the coder
+// state and the model of its context, both left by the previous symbol.  A
+// single wave issues roughly one instruction every four cycles, so the loop
+// is built to minimise instructions per symbol rather than latency alone:
+//
+//  * the coder (range, code, input window) is uniform scalar state;
+//  * the quality model of the current context sits in lanes: lane j holds
+//    list slot j as freq | cum << 16 and its symbol, with a sentinel slot
+//    `live` whose cum is the list total.  The reference's linear scan
+//    (c_simple_model.h:136-171) becomes one ballot: with q = range / total,
+//    the decoded slot k is the last j with cum_j * q <= code, since
+//    t = code / q >= cum_j  <=>  code >= cum_j * q.  k == live means
+//    t >= total (only in corrupt streams: symbol 0, no update).  The new
+//    range is p_{k+1} - p_k = freq_k * q without another multiply;
+//  * q = floor(range / total) is (u32)fma(range, RN(1/total), 2^-19), exact
+//    for range < 2^32 and total < 2^16 whenever the stored reciprocal is
+//    within one ulp (see fqz_div_selftest);
+//  * while the ballot runs, every lane computes the context its own symbol
+//    would lead to (fqz_update_ctx, fqzcomp_qual.c:361-418) and that
+//    context's cache address, so the next model read waits only for a
+//    readlane;
+//  * models live in a direct-mapped LDS cache (~125 KB) backed by HBM;
+//    blocks touch a few thousand of the 65536 contexts;
+//  * output symbols go through LDS in 4 KB pages; qmap, duplicate records
+//    and GFLAG_DO_REV reversal are applied by parallel fix-up kernels.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "fqz_kernels.h"
+#include "fqz_model.hpp"
+
+namespace fqz5 {
+namespace {
+
+constexpr uint32_t RING = 4096, HALF = 2048;   // staged input bytes
+constexpr uint32_t OBUF = 4096;                // output page
+constexpr uint32_t SEQB = 2048;                // staged sequence bases
+constexpr uint32_t TAG_EMPTY = 0xffffffffu;
+constexpr uint32_t PBYTES = 3072;              // qtab u16[256], ptab u16[1024], dtab u16[256]
+constexpr uint32_t P_QTAB = 0, P_PTAB = 512, P_DTAB = 2560;
+
+constexpr uint32_t L_SMALL = 0;
+constexpr uint32_t L_PAR = 4096;
+constexpr uint32_t L_RING = L_PAR + FQZ_MAX_PARAMS * PBYTES;   // 16384
+constexpr uint32_t L_OBUF = L_RING + RING + 16;
+constexpr uint32_t L_DUMMY = L_OBUF + OBUF;                     // lanes != 0 write here
+constexpr uint32_t L_SEQ = L_DUMMY + 256;
+constexpr uint32_t L_BITS = L_SEQ + SEQB;                       // evicted-model bitmap
+constexpr uint32_t L_CACHE = L_BITS + FQZ_CTX / 8;
+constexpr uint32_t LDS_BYTES = 163840;
+static_assert(L_CACHE == 35088, "keep FQZ_DEC_CACHE_BYTES in step");
+static_assert(sizeof(SmallModels) <= L_PAR, "small models");
+static_assert(L_CACHE + FQZ_DEC_CACHE_BYTES + 1024 == LDS_BYTES, "cache bytes");
+
+DEV __amdgpu_buffer_rsrc_t rsrc(const void *p, uint32_t n) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, n, 0x00020000);
+}
+DEV uint32_t ld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+}
+DEV void st8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b8(uint8_t(v), r, off, 0, 0);
+}
+DEV uint32_t U(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+#ifdef FQZ5_DEC_PROBE   // cycle stamps per stage of the fast loop (tools/)
+#define PROBE_DECL uint64_t pr_t = 0, pr[6] = {0, 0, 0, 0, 0, 0};
+#define PROBE_START pr_t = __builtin_amdgcn_s_memtime();
+#define PROBE(i)                                        \
+    {                                                   \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+        pr[i] += t_ - pr_t;                             \
+        pr_t = t_;                                      \
+    }
+#define PROBE_OUT                                                            \
+    if (l == 0)                                                              \
+        for (int i = 0; i < 6; i++) reinterpret_cast<uint64_t *>(J.counts + 8)[i] = pr[i];
+#else
+#define PROBE_DECL
+#define PROBE_START
+#define PROBE(i)
+#define PROBE_OUT
+#endif
+DEV uint32_t RL(uint32_t v, uint32_t lane) { return __builtin_amdgcn_readlane(v, lane); }
+
+// RN(1/t) to within one ulp: hardware reciprocal plus one Newton step.
+DEV double recip(uint32_t t) {
+    const double d = double(t);
+    const double r = __builtin_amdgcn_rcp(d);
+    const double e = __fma_rn(-d, r, 1.0);
+    return __fma_rn(r, e, r);
+}
+DEV uint32_t quot(uint32_t rng, double rd) { return uint32_t(__fma_rn(double(rng), rd, 0x1p-19)); }
+
+// ---------------------------------------------------------------------------
+// input: a 4 KB LDS ring refilled 2 KB at a time, read through a 64-bit
+// big-endian window W: `vb` bytes from stream position `rb` were valid at the
+// last refill, `ub` bits have been shifted out since.
+// ---------------------------------------------------------------------------
+struct In {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t len, rb, ub, vb, lp;
+    uint64_t W;
+    DEV uint32_t rp() const { return rb + (ub >> 3); }
+    DEV uint32_t avail() const { return vb - (ub >> 3); }
+};
+
+DEV void stage(uint8_t *lds, const In &in) {
+    const uint32_t l = threadIdx.x;
+    const uint32_t src = in.lp + 32 * l;
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        w[i] = ld8(in.r, src + 4 * i) | ld8(in.r, src + 4 * i + 1) << 8 |
+               ld8(in.r, src + 4 * i + 2) << 16 | ld8(in.r, src + 4 * i + 3) << 24;
+    const uint32_t at = L_RING + (in.lp & (RING - 1)) + 32 * l;
+    *reinterpret_cast<uint4 *>(lds + at) = make_uint4(w[0], w[1], w[2], w[3]);
+    *reinterpret_cast<uint4 *>(lds + at + 16) = make_uint4(w[4], w[5], w[6], w[7]);
+    if ((in.lp & (RING - 1)) == 0 && l == 0)   // mirror for reads across the end
+        *reinterpret_cast<uint4 *>(lds + L_RING + RING) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+DEV void refill(uint8_t *lds, In &in) {
+    const uint32_t rp = in.rp();
+    if (in.lp - rp < HALF) {
+        stage(lds, in);
+        in.lp += HALF;
+    }
+    const uint32_t i = rp & (RING - 1), a = i & ~7u, sh = (i & 7u) * 8u;
+    const uint64_t lo = *reinterpret_cast<const uint64_t *>(lds + L_RING + a);
+    const uint64_t hi = *reinterpret_cast<const uint64_t *>(lds + L_RING + a + 8);
+    const uint64_t v = sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+    const uint64_t be = __builtin_bswap64(v);
+    in.W = (uint64_t(U(uint32_t(be >> 32))) << 32) | U(uint32_t(be));
+    const uint32_t rem = in.len - rp;
+    in.vb = rem < 8u ? rem : 8u;
+    in.rb = rp;
+    in.ub = 0;
+}
+
+// one byte into the coder (the reference's renormalisation reads, with its
+// end-of-input stop, c_range_coder.h RC_GetFreq / RC_Decode)
+DEV bool take_byte(uint8_t *lds, In &in, uint32_t &code) {
+    if (in.rp() >= in.len) return false;
+    code = (code << 8) | uint32_t(in.W >> 56);
+    in.W <<= 8;
+    in.ub += 8;
+    if (in.avail() < 4u) refill(lds, in);
+    return true;
+}
+
+DEV void renorm_slow(uint8_t *lds, In &in, uint32_t &rng, uint32_t &code) {
+    while (rng < (1u << 24)) {
+        if (!take_byte(lds, in, code)) break;
+        rng <<= 8;
+    }
+}
+
+// a small model (selector / length bytes / reverse / duplicate) in LDS,
+// decoded serially with the reference's arithmetic
+template <int CAP> DEV uint32_t small_decode(FList<CAP> *m, uint8_t *lds, In &in, uint32_t &rng,
+                                             uint32_t &code) {
+    const uint32_t tot = U(m->total);
+    uint32_t t = 0;
+    if (tot && rng >= tot) {
+        rng /= tot;
+        t = code / rng;
+    }
+    if (t > FL_MAX) return 0;
+    uint32_t acc = 0;
+    int k = 1;
+    while ((acc += U(m->fr[k])) <= t) k++;
+    if (k - 1 > CAP) return 0;
+    const uint32_t f = U(m->fr[k]);
+    acc -= f;
+    code -= acc * rng;
+    rng *= f;
+    renorm_slow(lds, in, rng, code);
+    const uint32_t s = U(m->sy[k]);
+    if (threadIdx.x == 0) fl_bump(m, k);
+    __builtin_amdgcn_wave_barrier();
+    return s;
+}
+
+template <int CAP> DEV void small_init(FList<CAP> *m, int live) {
+    const int l = threadIdx.x;
+    if (l == 0) {
+        m->fr[0] = uint16_t(FL_MAX);
+        m->sy[0] = 0;
+        m->fr[CAP + 1] = 0;
+        m->sy[CAP + 1] = 0;
+        m->fr[CAP + 2] = uint16_t(FL_MAX);
+        m->sy[CAP + 2] = 0;
+        m->total = uint32_t(live);
+    }
+    for (int k = l; k < CAP; k += 64) {
+        m->sy[k + 1] = uint8_t(k);
+        m->fr[k + 1] = k < live ? 1 : 0;
+    }
+}
+
+// per-record parameter scalars (fqzcomp_qual.c:1067-1076)
+struct PS {
+    uint32_t x, ctx0, qshift, qloc, qmask, sloc, bbits, bloc, boff, sel, dedup, fixed;
+};
+
+DEV PS load_ps(const FqzDevGlobal &g, uint32_t x) {
+    const FqzDevParam &p = g.p[x];
+    return PS{x, p.ctx0, p.qshift, p.qloc, p.qmask, p.sloc, p.bbits, p.bloc, p.boff, p.sel, p.dedup,
+              p.fixed};
+}
+
+// cache set of a context: multiplicative hash with 24-bit multiplies
+// (full rate), then a 24-bit fraction scaled to the set count
+DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
+    const uint32_t h = (ctx * 0x9E3779u) >> 8;                     // 24 bits
+    const uint32_t set = uint32_t((uint64_t(h & 0xffffffu) * (ns8 & 0xffffffu)) >> 32);
+    return L_CACHE + __umul24(set, me);
+}
+
+// ---------------------------------------------------------------------------
+// the decoder.  Model in lanes: lane j holds dword j of the cached model,
+// [tag | entry of slot 0 .. entry of slot L], entries freq | cum << 16, the
+// sentinel slot L with freq 0 and cum = total; symbol bytes follow.
+// ---------------------------------------------------------------------------
+template <int NE, bool SEQ, bool QID>
+__global__ __launch_bounds__(64) void k_fqz_dec(FqzDecJob J) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t l = threadIdx.x;
+    const FqzDevGlobal &g = *J.g;
+    SmallModels &sm = *reinterpret_cast<SmallModels *>(lds + L_SMALL);
+    const uint32_t gfl = g.gflags, nparam = g.nparam;
+    const uint32_t L = g.max_sym + 1;                 // live symbols per quality model
+    const uint32_t ME = J.ment, NS = J.nsets, NS8 = NS << 8;
+    const uint32_t soff = 4u * (L + 2u);              // symbol bytes within a model
+    const uint32_t n = uint32_t(J.n);
+
+    // ---- set-up: small models, parameter tables, cache tags, bitmap ------
+    for (int b = 0; b < 4; b++) small_init(&sm.len[b], 256);
+    small_init(&sm.rev, 2);
+    small_init(&sm.dup, 2);
+    if (g.max_sel > 0) small_init(&sm.sel, int(g.max_sel) + 1);
+    for (uint32_t x = 0; x < nparam; x++) {
+        uint16_t *pt = reinterpret_cast<uint16_t *>(lds + L_PAR + x * PBYTES);
+        for (uint32_t i = l; i < 256; i += 64) pt[(P_QTAB >> 1) + i] = uint16_t(g.p[x].qtab[i]);
+        for (uint32_t i = l; i < 1024; i += 64) pt[(P_PTAB >> 1) + i] = uint16_t(g.p[x].ptab[i]);
+        for (uint32_t i = l; i < 256; i += 64) pt[(P_DTAB >> 1) + i] = uint16_t(g.p[x].dtab[i]);
+    }
+    for (uint32_t i = l; i < FQZ_CTX / 32; i += 64) reinterpret_cast<uint32_t *>(lds + L_BITS)[i] = 0;
+    for (uint32_t s = l; s < NS; s += 64) *reinterpret_cast<uint32_t *>(lds + L_CACHE + s * ME) = TAG_EMPTY;
+
+    In in;
+    in.r = rsrc(J.in, uint32_t(J.in_len));
+    in.len = uint32_t(J.in_len);
+    in.lp = 0;
+    stage(lds, in);
+    in.lp = HALF;
+    stage(lds, in);
+    in.lp = RING;
+    in.rb = in.ub = in.vb = 0;
+    in.W = 0;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t rng = 0xFFFFFFFFu, code = 0;
+    if (in.len >= 5) {
+        refill(lds, in);
+        for (int k = 0; k < 5; k++) {
+            code = (code << 8) | uint32_t(in.W >> 56);
+            in.W <<= 8;
+        }
+        in.ub = 40;
+        refill(lds, in);
+    } else {
+        in.rb = in.len;
+    }
+
+    const __amdgpu_buffer_rsrc_t orsrc = rsrc(J.out, n);
+    uint32_t obase = 0, fill = 0;             // output page covers [obase, obase + fill)
+    uint32_t rec = 0, prev_len = 0, left = 0;
+    uint32_t nrecs = 0, ndups = 0, nrevs = 0, nmiss = 0, nslow = 0;
+    PROBE_DECL
+    bool first_len = true;
+    int status = 0;
+    PS ps = load_ps(g, 0);
+    uint32_t qctx = 0, delta = 0, prevq = 0, sel = 0, seq = 0, selterm = 0;
+    uint32_t ctx = 0, maddr = L_CACHE;
+    const uint8_t *sbase = nullptr;           // record's sequence (SEQ)
+    uint32_t rlen = 0, sb0 = 0;               // record length, first staged base index
+    uint32_t tpos = 0;                        // symbol index within the record
+    const uint32_t dlane = L_DUMMY + 4 * l;
+    // lanes holding dwords 0 .. L+1 (write-back) and slots 0 .. L (ballot)
+    const uint32_t nd = L + 2;
+    const uint64_t wm0 = nd >= 64 ? ~0ull : ((1ull << nd) - 1);
+    const uint64_t wm1 = NE == 2 && nd > 64 ? (nd >= 128 ? ~0ull : ((1ull << (nd - 64)) - 1)) : 0ull;
+    const uint64_t lm0 = wm0 & ~1ull, lm1 = wm1;
+    const bool wr[2] = {l < nd, l + 64 < nd};
+
+    auto flush = [&]() {
+        for (uint32_t o = l * 4; o < fill; o += 256) {
+            const uint32_t w = *reinterpret_cast<const uint32_t *>(lds + L_OBUF + o);
+#pragma unroll
+            for (uint32_t b = 0; b < 4; b++)
+                if (o + b < fill) st8(orsrc, obase + o + b, w >> (8 * b));
+        }
+        obase += fill;
+        fill = 0;
+    };
+    auto stage_seq = [&]() {   // bases of symbols [sb0, sb0 + SEQB) of the record
+        for (uint32_t j = l; j < SEQB; j += 64) {
+            const uint32_t pos = ps.boff + sb0 + j;
+            lds[L_SEQ + j] = uint8_t(sbase && pos < rlen ? base2(sbase[pos]) : 0u);
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    const uint8_t *ptab = nullptr;            // this record's tables (LDS)
+    const uint16_t *pt16 = nullptr;
+    auto seq_next = [&]() -> uint32_t {       // context bits of the sequence, next symbol
+        if (!SEQ) return 0u;
+        const uint32_t b = U(lds[L_SEQ + (tpos - sb0)]);
+        return ((seq << 2) | b) & ((1u << ps.bbits) - 1u);
+    };
+    // the context after symbol `sym`, uniform (slow paths)
+    auto next_uniform = [&](uint32_t sym) {
+        const uint32_t seqn = seq_next();
+        uint32_t u = U(pt16[(P_PTAB >> 1) + (left < 1023u ? left : 1023u)]);
+        u += U(pt16[(P_DTAB >> 1) + (delta < 255u ? delta : 255u)]);
+        u += selterm + (seqn << ps.bloc);
+        qctx = (qctx << ps.qshift) + U(pt16[(P_QTAB >> 1) + sym]);
+        ctx = (((qctx & ps.qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1);
+        maddr = set_addr(ctx, NS8, ME);
+        seq = seqn;
+        delta += prevq != sym;
+        prevq = sym;
+        left--;
+        tpos++;
+    };
+
+    // model registers
+    uint32_t v[NE], s[NE];
+    auto rlane = [&](const uint32_t (&x)[NE], uint32_t dw) -> uint32_t {
+        if (NE == 1) return RL(x[0], dw);
+        const uint32_t a = RL(x[0], dw & 63u), b = RL(x[NE - 1], dw & 63u);
+        return dw < 64 ? a : b;
+    };
+    auto issue_model = [&]() {
+#pragma unroll
+        for (int r = 0; r < NE; r++) {
+            v[r] = *reinterpret_cast<const uint32_t *>(lds + maddr + 4 * (l + 64 * r));
+            s[r] = lds[maddr + soff - 1 + l + 64 * r];
+        }
+    };
+    // miss: write the resident model back to HBM, fetch or create ctx
+    auto miss = [&](uint32_t tag) {
+        nmiss++;
+        uint32_t *m32 = reinterpret_cast<uint32_t *>(lds + maddr);
+        uint32_t *bits = reinterpret_cast<uint32_t *>(lds + L_BITS);
+        if (tag != TAG_EMPTY) {
+            uint32_t *dst = reinterpret_cast<uint32_t *>(J.back + size_t(tag) * ME);
+            for (uint32_t o = l; o < ME / 4; o += 64)
+                __hip_atomic_store(dst + o, m32[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (l == 0) bits[tag >> 5] |= 1u << (tag & 31);
+            __builtin_amdgcn_wave_barrier();
+        }
+        if ((U(bits[ctx >> 5]) >> (ctx & 31)) & 1u) {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(J.back + size_t(ctx) * ME);
+            for (uint32_t o = l; o < ME / 4; o += 64)
+                m32[o] = __hip_atomic_load(src + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            for (uint32_t j = l; j <= L; j += 64) {   // slot j: freq 1 (live) or 0, cum j
+                m32[1 + j] = (j < L ? 1u : 0u) | (j << 16);
+                lds[maddr + soff + j] = uint8_t(j < L ? j : 0u);
+            }
+            if (l == 0) m32[0] = ctx;
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    auto load_model = [&]() {
+        for (;;) {
+            issue_model();
+            const uint32_t tag = RL(v[0], 0);
+            if (tag == ctx) return;
+            miss(tag);
+        }
+    };
+    // the list update after coding the slot in lane kl (fl_bump): +16,
+    // halve past FL_MAX, one bubble step; written back to the cache
+    auto update = [&](uint32_t kl, uint32_t total) {
+#pragma unroll
+        for (int r = 0; r < NE; r++) {
+            const uint32_t dw = l + 64 * r;
+            v[r] += dw > kl ? 0x100000u : (dw == kl ? FL_STEP : 0u);
+        }
+        if (total + FL_STEP > FL_MAX) {
+            uint32_t carry = 0;
+#pragma unroll
+            for (int r = 0; r < NE; r++) {
+                const uint32_t dw = l + 64 * r;
+                uint32_t f = dw >= 1 && dw <= L ? (v[r] & 0xffffu) : 0u;
+                f -= f >> 1;
+                uint32_t inc = f;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t o = __shfl_up(inc, d, 64);
+                    if (int(l) >= d) inc += o;
+                }
+                if (dw >= 1) v[r] = f | ((carry + inc - f) << 16);
+                carry += RL(inc, 63);
+            }
+        }
+        if (kl >= 2) {
+            const uint32_t ek = rlane(v, kl), ep = rlane(v, kl - 1);
+            const uint32_t fk = ek & 0xffffu, fp = ep & 0xffffu;
+            if (fk > fp) {
+                const uint32_t cp = ep >> 16;
+                const uint32_t sk = rlane(s, kl), sp = rlane(s, kl - 1);
+#pragma unroll
+                for (int r = 0; r < NE; r++) {
+                    const uint32_t dw = l + 64 * r;
+                    if (dw == kl - 1) { v[r] = fk | (cp << 16); s[r] = sk; }
+                    if (dw == kl) { v[r] = fp | ((cp + fk) << 16); s[r] = sp; }
+                    if (dw == kl - 1 || dw == kl) lds[maddr + soff - 1 + dw] = uint8_t(s[r]);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < NE; r++)
+            if (wr[r]) *reinterpret_cast<uint32_t *>(lds + maddr + 4 * (l + 64 * r)) = v[r];
+    };
+    auto put = [&](uint32_t sym) {
+        lds[l ? dlane : L_OBUF + fill] = uint8_t(sym);
+        fill++;
+    };
+    // one symbol with the reference's arithmetic, any state (corrupt or
+    // truncated streams, the last bytes of the input)
+    auto slow_symbol = [&]() {
+        nslow++;
+        load_model();
+        const uint32_t total = rlane(v, L + 1) >> 16;
+        uint32_t t = 0;
+        if (total && rng >= total) {   // the division stays even when no symbol follows
+            rng /= total;
+            t = code / rng;
+        }
+        uint32_t sym = 0;
+        if (t < total) {   // (t > FL_MAX implies t >= total)
+            uint32_t kl = 1;
+            while (kl < L && (rlane(v, kl + 1) >> 16) <= t) kl++;
+            const uint32_t ek = rlane(v, kl);
+            code -= (ek >> 16) * rng;
+            rng *= ek & 0xffffu;
+            renorm_slow(lds, in, rng, code);
+            sym = rlane(s, kl);
+            update(kl, total);
+        }
+        put(sym);
+        next_uniform(sym);
+    };
+
+    for (;;) {
+        if (left == 0) {
+            // ---- record header (fqzcomp_qual.c:1484-1540) --------------------
+            if (obase + fill >= n) break;
+            if (fill == OBUF) flush();
+            const uint32_t i = obase + fill;
+            sel = (ps.sel || (gfl & 1u)) ? small_decode(&sm.sel, lds, in, rng, code) : 0u;
+            const uint32_t x = (gfl & 2u) ? g.stab[sel < 255u ? sel : 255u] : sel;
+            if (x >= nparam) { status = -1; break; }
+            ps = load_ps(g, x);
+            uint32_t len = prev_len;
+            if (!ps.fixed || first_len) {
+                len = 0;
+                for (int b = 0; b < 4; b++) len |= small_decode(&sm.len[b], lds, in, rng, code) << (8 * b);
+                first_len = false;
+                prev_len = len;
+            }
+            if (len > n - i || len == 0) { status = -1; break; }
+            if (rec < J.nlengths && l == 0) J.lengths[rec] = len;
+            if (gfl & 4u) {
+                if (small_decode(&sm.rev, lds, in, rng, code)) {
+                    if (nrevs >= J.cap_list) { status = -2; break; }
+                    if (l == 0) J.revs[nrevs] = make_uint2(i, len);
+                    nrevs++;
+                }
+            }
+            rec++;
+            if (ps.dedup && small_decode(&sm.dup, lds, in, rng, code)) {
+                if (len > i) { status = -1; break; }
+                if (ndups >= J.cap_list) { status = -2; break; }
+                if (l == 0) J.dups[ndups] = make_uint2(i, len);
+                ndups++;
+                flush();
+                obase += len;
+                continue;
+            }
+            if (nparam > 1) {
+                if (nrecs >= J.cap_list) { status = -2; break; }
+                if (l == 0) J.recs[nrecs] = make_uint4(i, len, x, 0u);
+                nrecs++;
+            }
+            left = len;
+            rlen = len;
+            tpos = 0;
+            delta = prevq = qctx = 0;
+            seq = 0;
+            selterm = sel << ps.sloc;
+            ptab = lds + L_PAR + ps.x * PBYTES;
+            pt16 = reinterpret_cast<const uint16_t *>(ptab);
+            if (SEQ) {
+                sbase = nullptr;
+                if (J.seq && rec - 1 < J.nseq && J.seq_off[rec - 1] != ~0ull) {
+                    sbase = J.seq + J.seq_off[rec - 1];
+                    for (uint32_t b = 0; b < ps.boff; b++) seq = (seq << 2) | base2(sbase[b]);
+                }
+                sb0 = 0;
+                stage_seq();
+            }
+            ctx = ps.ctx0;
+            maddr = set_addr(ctx, NS8, ME);
+        }
+        if (in.avail() < 4u) {   // the last bytes of the input: reference arithmetic
+            slow_symbol();
+            if (fill == OBUF) flush();
+            if (SEQ && tpos - sb0 == SEQB) { sb0 = tpos; stage_seq(); }
+            continue;
+        }
+        // ---- fast loop: symbols of this record within the output page ------
+        uint32_t lim = left < OBUF - fill ? left : OBUF - fill;
+        if (SEQ && lim > SEQB - (tpos - sb0)) lim = SEQB - (tpos - sb0);
+        uint32_t ulim = (in.vb - 4u) * 8u;
+        bool to_slow = false;
+        uint32_t done = 0;
+        PROBE_START
+        do {
+            // all reads of the step in flight together: model dwords and
+            // symbols, the position and delta table entries
+            const uint32_t pa = (P_PTAB >> 1) + (left < 1023u ? left : 1023u);
+            const uint32_t da = (P_DTAB >> 1) + (delta < 255u ? delta : 255u);
+            issue_model();
+            const uint32_t pv = pt16[pa], dv = pt16[da];
+            uint32_t sq = 0;
+            if (SEQ) sq = lds[L_SEQ + (tpos - sb0)];
+            asm volatile("" ::"v"(v[0]), "v"(s[0]), "v"(pv), "v"(dv), "v"(sq));
+            const uint32_t tag = RL(v[0], 0);
+            if (tag != ctx) {
+                miss(tag);
+                load_model();
+            }
+            PROBE(0)
+            const uint32_t total = rlane(v, L + 1) >> 16;
+            const uint32_t q = quot(rng, recip(total));
+            uint32_t seqn = 0;
+            if (SEQ) seqn = ((seq << 2) | U(sq)) & ((1u << ps.bbits) - 1u);
+            const uint32_t u = pv + dv + selterm + (seqn << ps.bloc);
+            const uint32_t qs = qctx << ps.qshift;
+            uint32_t qt[NE], an[NE], cn[NE], p[NE];
+            uint32_t cnt = 0;
+#pragma unroll
+            for (int r = 0; r < NE; r++) {
+                qt[r] = QID ? s[r] : uint32_t(pt16[(P_QTAB >> 1) + s[r]]);
+                cn[r] = ((((qs + qt[r]) & ps.qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1);
+                an[r] = set_addr(cn[r], NS8, ME);
+                p[r] = (v[r] >> 16) * q;
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(p[r] <= code) & (r == 0 ? lm0 : lm1);
+                cnt += __builtin_popcountll(bal);
+            }
+            const uint32_t kl = cnt;          // lane of the decoded slot (slot kl - 1)
+            PROBE(1)
+            if (kl > L) {   // t >= total or range < total: reference arithmetic
+                to_slow = true;
+                break;
+            }
+            const uint32_t pk = rlane(p, kl), pk1 = rlane(p, kl + 1);
+            const uint32_t sym = rlane(s, kl);
+            const uint32_t qtk = rlane(qt, kl), cnk = rlane(cn, kl), ank = rlane(an, kl);
+            code -= pk;
+            rng = pk1 - pk;
+            const uint32_t z = uint32_t(__builtin_clz(rng)) & 24u;
+            rng <<= z;
+            code = uint32_t(((uint64_t(code) << 32) | uint32_t(in.W >> 32)) >> (32u - z));
+            in.W <<= z;
+            in.ub += z;
+            PROBE(2)
+            update(kl, total);
+            PROBE(3)
+            put(sym);
+            qctx = qs + qtk;
+            delta += prevq != sym;
+            prevq = sym;
+            seq = seqn;
+            left--;
+            if (SEQ) tpos++;
+            ctx = cnk;
+            maddr = ank;
+            done++;
+            PROBE(4)
+            if (in.ub > ulim) {
+                refill(lds, in);
+                if (in.vb < 4u) break;
+                ulim = (in.vb - 4u) * 8u;
+            }
+            PROBE(5)
+        } while (done != lim);
+        if (to_slow) slow_symbol();
+        if (fill == OBUF) flush();
+        if (SEQ && left && tpos - sb0 == SEQB) { sb0 = tpos; stage_seq(); }
+    }
+    if (status == 0) flush();
+    if (l == 0) {
+        *J.status = status;
+        *J.nrec_out = rec;
+        J.counts[0] = nrecs;
+        J.counts[1] = ndups;
+        J.counts[2] = nrevs;
+        J.counts[3] = nmiss;
+        J.counts[4] = nslow;
+    }
+    PROBE_OUT
+}
+
+// ---------------------------------------------------------------------------
+// fix-ups, in the reference's order: symbols -> qmap (during decode in the
+// reference), duplicate copies (during decode), reversal (after decode,
+// fqzcomp_qual.c:1597-1611)
+// ---------------------------------------------------------------------------
+__global__ void k_fqz_map_all(FqzDecJob J) {
+    const uint8_t *qm = J.g->p[0].qmap;
+    for (uint64_t i = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; i < J.n;
+         i += uint64_t(gridDim.x) * blockDim.x)
+        J.out[i] = qm[J.out[i]];
+}
+
+__global__ void k_fqz_map_recs(FqzDecJob J) {
+    const uint32_t nr = J.counts[0];
+    for (uint32_t r = blockIdx.x; r < nr; r += gridDim.x) {
+        const uint4 R = J.recs[r];
+        const uint8_t *qm = J.g->p[R.z].qmap;
+        for (uint32_t t = threadIdx.x; t < R.y; t += blockDim.x) J.out[R.x + t] = qm[J.out[R.x + t]];
+    }
+}
+
+// duplicates copy the `len` bytes before them, in record order
+__global__ __launch_bounds__(256) void k_fqz_dups(FqzDecJob J) {
+    const uint32_t nd = J.counts[1];
+    for (uint32_t d = 0; d < nd; d++) {
+        const uint2 D = J.dups[d];
+        for (uint32_t t = threadIdx.x; t < D.y; t += blockDim.x)
+            J.out[D.x + t] = __hip_atomic_load(J.out + D.x - D.y + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence();
+        __syncthreads();
+    }
+}
+
+__global__ void k_fqz_revs(FqzDecJob J) {
+    const uint32_t nr = J.counts[2];
+    for (uint32_t r = blockIdx.x; r < nr; r += gridDim.x) {
+        const uint2 R = J.revs[r];
+        uint8_t *o = J.out + R.x;
+        for (uint32_t a = threadIdx.x; a < R.y / 2; a += blockDim.x) {
+            const uint32_t b = R.y - 1 - a;
+            const uint8_t t = o[a];
+            o[a] = o[b];
+            o[b] = t;
+        }
+    }
+}
+
+// q = (u32)fma(n, recip(t), 2^-19) against n / t for every total t and a
+// spread of numerators (including multiples of t and their neighbours)
+__global__ void k_fqz_div_selftest(uint32_t *bad) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x + 1;
+    if (t > 65535u) return;
+    const double rd = recip(t);
+    uint32_t nb = 0;
+    uint32_t x = t * 2654435761u;
+    for (int i = 0; i < 512; i++) {
+        x = x * 1664525u + 1013904223u;
+        const uint32_t m = x / t;
+        const uint32_t cands[4] = {x, m * t, m * t - 1u, m * t + t - 1u};
+        for (int c = 0; c < 4; c++) nb += quot(cands[c], rd) != cands[c] / t;
+    }
+    nb += quot(0xFFFFFFFFu, rd) != 0xFFFFFFFFu / t;
+    if (nb) atomicAdd(bad, nb);
+}
+
+}  // namespace
+
+template <int NE, bool SEQ, bool QID> static hipError_t launch_dec(const FqzDecJob &j, hipStream_t s) {
+    auto *f = k_fqz_dec<NE, SEQ, QID>;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(f),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(f, dim3(1), dim3(64), LDS_BYTES, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_fqz_dec(const FqzDecJob &j, int ne, bool seq, bool qid, hipStream_t s) {
+    if (ne == 1) {
+        if (seq) return qid ? launch_dec<1, true, true>(j, s) : launch_dec<1, true, false>(j, s);
+        return qid ? launch_dec<1, false, true>(j, s) : launch_dec<1, false, false>(j, s);
+    }
+    if (seq) return qid ? launch_dec<2, true, true>(j, s) : launch_dec<2, true, false>(j, s);
+    return qid ? launch_dec<2, false, true>(j, s) : launch_dec<2, false, false>(j, s);
+}
+
+hipError_t launch_fqz_dec_fix(const FqzDecJob &j, int map_mode, bool dups, bool revs, hipStream_t s) {
+    if (map_mode == 1) hipLaunchKernelGGL(k_fqz_map_all, dim3(1024), dim3(256), 0, s, j);
+    if (map_mode == 2) hipLaunchKernelGGL(k_fqz_map_recs, dim3(4096), dim3(64), 0, s, j);
+    if (dups) hipLaunchKernelGGL(k_fqz_dups, dim3(1), dim3(256), 0, s, j);
+    if (revs) hipLaunchKernelGGL(k_fqz_revs, dim3(4096), dim3(64), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t fqz_div_selftest(uint32_t *d_bad, hipStream_t s) {
+    hipLaunchKernelGGL(k_fqz_div_selftest, dim3(256), dim3(256), 0, s, d_bad);
+    return hipGetLastError();
+}
+
+}  // namespace fqz5

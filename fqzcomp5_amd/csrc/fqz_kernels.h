@@ -64,15 +64,31 @@ struct FqzDecJob {
     uint64_t n;                 // decoded size
     const uint8_t *seq;
     const uint64_t *seq_off;
-    uint32_t nseq, nlengths, max_rec, pad;
-    uint8_t *models;
+    uint32_t nseq, nlengths;
     uint8_t *out;
     uint32_t *lengths;          // out: record lengths (nlengths)
-    uint8_t *rev;               // GFLAG_DO_REV bookkeeping (max_rec)
-    uint32_t *rlen;
     int32_t *status;
     uint32_t *nrec_out;
+    // the decoder (fqz_decode.hip) keeps quality models in an LDS cache
+    // backed by FQZ_CTX x ment bytes in HBM; qmap / duplicate / reversal
+    // fix-ups are applied afterwards from the record lists it writes.
+    uint8_t *back;
+    uint32_t ment, nsets;       // cached model bytes, direct-mapped sets
+    uint32_t cap_list, pad2;    // capacity of each record list
+    uint4 *recs;                // nparam > 1: non-duplicate records {start, len, param, 0}
+    uint2 *dups;                // duplicate records {start, len}
+    uint2 *revs;                // reversed records {start, len}
+    uint32_t *counts;           // out: [nrecs, ndups, nrevs, misses, slow symbols]
 };
+
+// Bytes of one cached quality model for `live` symbols: the context tag,
+// live+1 entries freq | cum << 16 (the last one a sentinel with freq 0 and
+// cum = total), live+1 symbol bytes; 4-byte aligned.
+constexpr uint32_t fqz_dec_model_bytes(uint32_t live) {
+    return (4u * (live + 2u) + (live + 1u) + 3u) & ~3u;
+}
+constexpr uint32_t FQZ_DEC_CACHE_BYTES = 163840u - 35088u - 1024u;
+constexpr uint32_t FQZ_DEC_MAX_LIVE = 126u;   // tag + entries in two lane registers
 
 // Parallel encoder (fqz_kernels.hip): the block becomes a list of coding
 // events (record headers and quality symbols) in stream order; events are
@@ -128,6 +144,11 @@ hipError_t launch_fqz_records(const FqzStatJob &j, hipStream_t s);
 hipError_t launch_fqz_hist(const FqzStatJob &j, int nchunks, int mode, hipStream_t s);
 hipError_t launch_fqz_model_init(uint8_t *models, int live, hipStream_t s);
 hipError_t launch_fqz_encode(const FqzEncJob &j, hipStream_t s);
-hipError_t launch_fqz_decode(const FqzDecJob &j, hipStream_t s);
+// fqz_decode.hip: ne = lane registers per model (live + 2 <= 64 ? 1 : 2),
+// seq = sequence bases in the context, qid = identity qtab in every
+// parameter block; map_mode 0 none / 1 one qmap / 2 per record
+hipError_t launch_fqz_dec(const FqzDecJob &j, int ne, bool seq, bool qid, hipStream_t s);
+hipError_t launch_fqz_dec_fix(const FqzDecJob &j, int map_mode, bool dups, bool revs, hipStream_t s);
+hipError_t fqz_div_selftest(uint32_t *d_bad, hipStream_t s);
 
 }  // namespace fqz5

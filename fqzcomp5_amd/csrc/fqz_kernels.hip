@@ -7,19 +7,18 @@
 // privatised in LDS per workgroup (128 x 256 packed u16 pairs = 128 KiB)
 // and flushed with global atomics.
 //
-// Serial part (a13/a16/a18): the adaptive frequency lists and the range
-// coder are one dependent chain per block (every symbol updates the model of
-// its context and the coder state).  One lane runs the block; the 65536
-// quality-context models live in HBM (304 B each), the length / selector /
-// duplicate models in LDS.
+// Encoder (a13/a16): the parallel path (events sorted by model, per-model
+// frequency pass, range-only serial chain, big-number byte assembly) and
+// the serial literal encoder for multi-parameter blocks.  The decoder
+// (a18) is fqz_decode.hip.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
 #include "fqz_kernels.h"
+#include "fqz_model.hpp"
 
 namespace fqz5 {
 
-#define DEV __device__ __forceinline__
 
 // --------------------------------------------------------------------------
 // statistics
@@ -81,57 +80,6 @@ __global__ __launch_bounds__(256) void k_fqz_hist(FqzStatJob J, int mode) {
         const uint32_t v = h[i];
         if (v & 0xffffu) atomicAdd(&g0[i], v & 0xffffu);
         if (v >> 16) atomicAdd(&g1[i], v >> 16);
-    }
-}
-
-// --------------------------------------------------------------------------
-// adaptive frequency lists (c_simple_model.h:63-171)
-// --------------------------------------------------------------------------
-// Slot 0: permanent head (never loses the bubble comparison); slots 1..CAP:
-// symbols in approximate descending frequency; CAP+1: zero terminator of
-// the halving loop; CAP+2: maximal terminator of a decode scan.
-constexpr uint32_t FL_MAX = 65519u;   // (1<<16)-17
-constexpr uint32_t FL_STEP = 16u;
-
-template <int CAP> struct FList {
-    uint32_t total;
-    uint16_t fr[CAP + 3];
-    uint8_t sy[CAP + 3];
-};
-static_assert(sizeof(FList<FQZ_QSYMS>) == FQZ_QMODEL_BYTES, "qual model size");
-
-template <int CAP> DEV void fl_init(FList<CAP> *m, int live) {
-    m->fr[0] = uint16_t(FL_MAX);
-    m->sy[0] = 0;
-    for (int k = 0; k < CAP; k++) {
-        m->sy[k + 1] = uint8_t(k);
-        m->fr[k + 1] = k < live ? 1 : 0;
-    }
-    m->fr[CAP + 1] = 0;
-    m->sy[CAP + 1] = 0;
-    m->fr[CAP + 2] = uint16_t(FL_MAX);
-    m->sy[CAP + 2] = 0;
-    m->total = uint32_t(live);
-}
-
-template <int CAP> DEV void fl_bump(FList<CAP> *m, int k) {
-    m->fr[k] += FL_STEP;
-    m->total += FL_STEP;
-    if (m->total > FL_MAX) {
-        uint32_t t = 0;
-        for (int i = 1; m->fr[i]; i++) {
-            m->fr[i] = uint16_t(m->fr[i] - (m->fr[i] >> 1));
-            t += m->fr[i];
-        }
-        m->total = t;
-    }
-    if (m->fr[k] > m->fr[k - 1]) {
-        const uint16_t f = m->fr[k];
-        const uint8_t s = m->sy[k];
-        m->fr[k] = m->fr[k - 1];
-        m->sy[k] = m->sy[k - 1];
-        m->fr[k - 1] = f;
-        m->sy[k - 1] = s;
     }
 }
 
@@ -227,20 +175,6 @@ DEV uint32_t next_ctx(const FqzDevParam &pm, Ctx &st, uint32_t q, uint32_t base)
     return c & uint32_t(FQZ_CTX - 1);
 }
 
-DEV uint32_t base2(uint8_t b) {
-    switch (b) {
-    case 'C': case 'c': return 1;
-    case 'G': case 'g': return 2;
-    case 'T': case 't': case 'U': case 'u': return 3;
-    default: return 0;
-    }
-}
-
-struct SmallModels {
-    FList<256> len[4], sel;
-    FList<2> rev, dup;
-};
-
 // --------------------------------------------------------------------------
 // encoder (compress_block_fqz2f, fqzcomp_qual.c:1112-1208)
 // --------------------------------------------------------------------------
@@ -312,98 +246,6 @@ __global__ __launch_bounds__(64) void k_fqz_encode(FqzEncJob J) {
     }
     for (int k = 0; k < 5; k++) rc_shift(rc);
     *J.out_len = uint32_t(rc.p - J.out);
-}
-
-// --------------------------------------------------------------------------
-// decoder (uncompress_block_fqz2f, fqzcomp_qual.c:1480-1585)
-// --------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_fqz_decode(FqzDecJob J) {
-    __shared__ SmallModels sm;
-    if (threadIdx.x) return;
-    const FqzDevGlobal &g = *J.g;
-    for (int b = 0; b < 4; b++) fl_init(&sm.len[b], 256);
-    fl_init(&sm.rev, 2);
-    fl_init(&sm.dup, 2);
-    if (g.max_sel > 0) fl_init(&sm.sel, int(g.max_sel) + 1);
-    FList<FQZ_QSYMS> *qm = reinterpret_cast<FList<FQZ_QSYMS> *>(J.models);
-
-    RC rc{};
-    rc.rng = 0xFFFFFFFFu;
-    rc.in = J.in;
-    rc.end = J.in + J.in_len;
-    if (J.in_len < 5) {
-        rc.in = rc.end;
-    } else {
-        for (int k = 0; k < 5; k++) rc.code = (rc.code << 8) | *rc.in++;
-    }
-    const FqzDevParam *pm = &g.p[0];
-    Ctx st{};
-    bool first_len = true;
-    uint32_t rec = 0, prev_len = 0, ctx = 0;
-    const uint8_t *sp = nullptr, *se = nullptr;
-    uint8_t *out = J.out;
-    int status = 0;
-    for (uint64_t i = 0; i < J.n; i++) {
-        if (st.left == 0) {
-            st.sel = (pm->sel || (g.gflags & 1u)) ? fl_decode(&sm.sel, rc) : 0u;
-            const uint32_t x = (g.gflags & 2u) ? g.stab[st.sel < 255u ? st.sel : 255u] : st.sel;
-            if (x >= g.nparam) { status = -1; break; }
-            pm = &g.p[x];
-            uint32_t len = prev_len;
-            if (!pm->fixed || first_len) {
-                len = 0;
-                for (int b = 0; b < 4; b++) len |= fl_decode(&sm.len[b], rc) << (8 * b);
-                first_len = false;
-                prev_len = len;
-            }
-            if (uint64_t(len) > J.n - i || len == 0) { status = -1; break; }
-            if (rec < J.nlengths) J.lengths[rec] = len;
-            if (g.gflags & 4u) {
-                const uint32_t rv = fl_decode(&sm.rev, rc);
-                if (rec < J.max_rec) { J.rev[rec] = uint8_t(rv); J.rlen[rec] = len; }
-            }
-            if (pm->dedup && fl_decode(&sm.dup, rc)) {
-                if (len > i) { status = -1; break; }
-                for (uint32_t t = 0; t < len; t++) out[i + t] = out[i - len + t];
-                i += len - 1;
-                st.left = 0;
-                rec++;
-                continue;
-            }
-            st.left = len;
-            st.delta = st.prevq = st.qctx = 0;
-            if (J.seq && rec < J.nseq && J.seq_off[rec] != ~0ull) {
-                const uint8_t *s0 = J.seq + J.seq_off[rec];
-                sp = s0 + pm->boff;
-                se = s0 + len;
-                st.seq = 0;
-                for (uint32_t b = 0; b < pm->boff; b++) st.seq = (st.seq << 2) | base2(s0[b]);
-            } else {
-                sp = se = nullptr;
-                st.seq = 0;
-            }
-            rec++;
-            ctx = pm->ctx0;
-        }
-        const uint32_t sym = fl_decode(&qm[ctx], rc) & 0xffu;
-        out[i] = pm->qmap[sym];
-        const uint32_t base = sp && sp < se ? base2(*sp++) : 0u;
-        ctx = next_ctx(*pm, st, sym, base);
-    }
-    // GFLAG_DO_REV: reverse the flagged records back (fqzcomp_qual.c:1597-1611)
-    if (status == 0 && (g.gflags & 4u)) {
-        uint64_t i = 0;
-        for (uint32_t r = 0; i < J.n && r < rec && r < J.max_rec; i += J.rlen[r++]) {
-            if (!J.rev[r]) continue;
-            for (uint32_t a = 0, b = J.rlen[r] - 1; a < b; a++, b--) {
-                const uint8_t t = out[i + a];
-                out[i + a] = out[i + b];
-                out[i + b] = t;
-            }
-        }
-    }
-    *J.status = status;
-    *J.nrec_out = rec;
 }
 
 // --------------------------------------------------------------------------
@@ -762,9 +604,5 @@ hipError_t launch_fqz_encode(const FqzEncJob &j, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_fqz_decode(const FqzDecJob &j, hipStream_t s) {
-    hipLaunchKernelGGL(k_fqz_decode, dim3(1), dim3(64), 0, s, j);
-    return hipGetLastError();
-}
 
 }  // namespace fqz5

@@ -44,9 +44,10 @@ def load() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise NativeError(f"{LIB_PATH} missing: run __graft_entry__.build()")
-    lib = C.CDLL(LIB_PATH)
+    path = os.environ.get("FQZ5_LIB_VARIANT") or LIB_PATH   # tools/build_variant.sh
+    if not os.path.exists(path):
+        raise NativeError(f"{path} missing: run __graft_entry__.build()")
+    lib = C.CDLL(path)
     lib.rans_compress_bound_4x16.restype = C.c_uint
     lib.rans_compress_bound_4x16.argtypes = [C.c_uint, C.c_int]
     lib.rans_compress_to_4x16.restype = C.c_void_p
@@ -80,6 +81,13 @@ def load() -> C.CDLL:
 
 def last_error() -> str:
     return load().fqz5_last_error().decode()
+
+
+def fqz_div_selftest() -> int:
+    """Mismatches of the fqz decoder's division on the device (0 expected)."""
+    so = load()
+    so.fqz5_fqz_div_selftest.restype = C.c_long
+    return int(so.fqz5_fqz_div_selftest())
 
 
 def device_ok() -> bool:

@@ -157,6 +157,11 @@ const char *fqz5_last_error(void);
 void fqz5_profile(int on);
 void fqz5_profile_read(double *out6);
 
+/* Device check of the fqz decoder's division: floor(n / t) computed as
+ * (u32)fma(n, recip(t), 2^-19) for every t < 2^16 and ~2000 n each.
+ * Returns the number of mismatches (0), or -1 on a device error. */
+long fqz5_fqz_div_selftest(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -85,3 +85,43 @@ def test_fqz_large_roundtrip(golden):
         assert hashlib.md5(out).hexdigest() == want[st]["md5"]
         back, _ = lib.fqz_decompress(out, lens.copy(), flags.copy(), seq)
         assert back == q
+
+
+def test_fqz_div_selftest():
+    assert lib.fqz_div_selftest() == 0
+
+
+def test_fqz_truncated_vs_oracle(golden):
+    """Damaged streams: the decoder follows the reference's arithmetic past
+    the end of the input and on out-of-range targets."""
+    ora = binding.oracle()
+    cs, _, _ = golden
+    name, q, lens, flags, seq = cs["q40_var"]
+    rng = np.random.default_rng(5)
+    for strat in (0, 1, 3):
+        comp = ora.fqz_compress(q, lens.copy(), flags.copy(), strat, seq)
+        for cut in (1, 3, 9, 40):
+            bad = comp[:-cut]
+            try:
+                exp = ora.fqz_decompress(bad, lens.copy(), flags.copy(), seq)
+            except RuntimeError:
+                exp = None
+            try:
+                got, _ = lib.fqz_decompress(bad, lens.copy(), flags.copy(), seq)
+            except RuntimeError:
+                got = None
+            assert got == exp, (strat, cut)
+        # flipped bytes in the coder payload
+        for _ in range(3):
+            b = bytearray(comp)
+            at = int(rng.integers(len(b) // 2, len(b)))
+            b[at] ^= 0x5A
+            try:
+                exp = ora.fqz_decompress(bytes(b), lens.copy(), flags.copy(), seq)
+            except RuntimeError:
+                exp = None
+            try:
+                got, _ = lib.fqz_decompress(bytes(b), lens.copy(), flags.copy(), seq)
+            except RuntimeError:
+                got = None
+            assert got == exp, (strat, at)
