@@ -88,14 +88,37 @@ extern "C" {
 
 void fqz5_trial_init(fqz5_trial_state *st) { std::memset(st, 0, sizeof *st); }
 
-int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *avail,
+void fqz5_trial_schedule(const int32_t *sec_ids, int nsec, const uint32_t *avail,
+                         const fqz5_trial_state *st, uint32_t *masks_out) {
+    // metrics_method's counters without the sizes: which sections try every
+    // method (trial and re-trial blocks) does not depend on the outcomes
+    fqz5_trial_state s = *st;
+    for (int i = 0; i < nsec; i++) {
+        fqz5_section_stats &ss = s.sec[sec_ids[i]];
+        if (ss.review <= 0) {
+            ss.review = FQZ5_METRICS_REVIEW;
+            ss.trial = FQZ5_METRICS_TRIAL;
+        }
+        masks_out[i] = 0;
+        if (ss.trial > 0) {
+            masks_out[i] = avail[sec_ids[i]];
+            ss.trial--;
+        } else if (ss.trial > -99999) {
+            ss.trial = -99999;
+        } else {
+            ss.review--;
+        }
+    }
+}
+
+int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                       uint32_t *sizes) {
     try {
         GpuCtx &g = gpu();
         if (t_sess.open) g.reset();
         t_sess = TrySession();
-        for (int s = 0; s < FQZ5_SEC_LAST; s++)
-            if (avail[s] & ~RANS_MASK)
+        for (int i = 0; i < nsec; i++)
+            if (masks[i] & ~RANS_MASK)
                 throw GpuError("fqz5_sections_try: method mask has non-rANS methods "
                                "(LZP/tok3/seq-CM/fqz are not in this build)");
         std::vector<CompressReq> &reqs = t_sess.reqs;
@@ -103,7 +126,7 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *avail,
         for (int i = 0; i < nsec; i++) {
             const fqz5_section &S = secs[i];
             for (int m = 1; m < FQZ5_M_LAST; m++) {
-                if (!(avail[S.sec] & (1u << m))) continue;
+                if (!(masks[i] & (1u << m))) continue;
                 if (m == RANSXN1 && !S.fixed_len) continue;   // out = NULL (:2004-2007)
                 CompressReq r;
                 r.d_in = S.in;
@@ -149,6 +172,9 @@ void fqz5_trial_replay(const int32_t *sec_ids, const uint32_t *in_sizes,
             const uint32_t out_len = sizes[size_t(i) * FQZ5_M_LAST + m];
             if (best_sz > out_len) { best_sz = out_len; best_m = m; }
         }
+        // outside the trial the one method is run whatever its size (the
+        // caller encodes it at commit: its size is not known here)
+        if (!in_trial && __builtin_popcount(methods) == 1) best_m = __builtin_ctz(methods);
         if (in_trial) {                                 // metrics_update, :2121-2130
             for (int m = 0; m < FQZ5_M_LAST; m++) {
                 if (!(methods & (1u << m)) || ss.trial <= 0) continue;
@@ -169,6 +195,22 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         GpuCtx &g = gpu();
         if (!t_sess.open || int(t_sess.req_of.size()) != nsec)
             throw GpuError("fqz5_sections_commit: no matching fqz5_sections_try");
+        // sections outside the trial: their one method, encoded now
+        std::vector<CompressReq> late;
+        std::vector<int> late_of(nsec, -1);
+        for (int i = 0; i < nsec; i++) {
+            const int m = methods[i];
+            if (m <= 0 || m >= FQZ5_M_LAST || t_sess.req_of[i][m] >= 0) continue;
+            if (!(RANS_MASK & (1u << m)) || (m == RANSXN1 && !secs[i].fixed_len)) continue;
+            CompressReq r;
+            r.d_in = secs[i].in;
+            r.n = secs[i].in_size;
+            r.order = method_order(m, secs[i].fixed_len);
+            r.cap = compress_bound(r.n, r.order);
+            late_of[i] = int(late.size());
+            late.push_back(std::move(r));
+        }
+        if (!late.empty()) compress_batch(g, late);
         std::vector<const Layout *> ls;
         std::vector<uint8_t *> dsts;
         std::vector<Layout> framed(nsec);
@@ -177,13 +219,14 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             fqz5_section_result &R = res[i];
             const int m = methods[i];
             const int ri = (m > 0 && m < FQZ5_M_LAST) ? t_sess.req_of[i][m] : -1;
+            const CompressReq *rq = ri >= 0 ? &t_sess.reqs[ri] : late_of[i] >= 0 ? &late[late_of[i]] : nullptr;
             R.method = m;
             R.strat = 0;
             R.status = -1;
             R.clen = 0;
             R.usize = S.in_size;
-            if (ri < 0 || !t_sess.reqs[ri].ok) continue;
-            const uint32_t clen = layout_size(t_sess.reqs[ri].out);
+            if (!rq || !rq->ok) continue;
+            const uint32_t clen = layout_size(rq->out);
             R.clen = clen;
             if (9ull + clen > S.out_cap) continue;
             // section framing [strat u8][u32 usize][u32 csize] (:2224-2229)
@@ -192,7 +235,7 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             std::memcpy(&h.host[1], &S.in_size, 4);
             std::memcpy(&h.host[5], &clen, 4);
             framed[i].push_back(std::move(h));
-            for (auto &p : t_sess.reqs[ri].out) framed[i].push_back(p);
+            for (auto &p : rq->out) framed[i].push_back(p);
             ls.push_back(&framed[i]);
             dsts.push_back(S.out);
             R.status = 0;
@@ -211,11 +254,13 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
 
 int fqz5_encode_sections(const fqz5_section *secs, int nsec, const uint32_t *avail,
                          fqz5_trial_state *st, fqz5_section_result *res) {
-    std::vector<uint32_t> sizes(size_t(nsec) * FQZ5_M_LAST);
-    if (fqz5_sections_try(secs, nsec, avail, sizes.data())) return -1;
+    std::vector<uint32_t> sizes(size_t(nsec) * FQZ5_M_LAST), masks(nsec);
     std::vector<int32_t> ids(nsec), meth(nsec);
     std::vector<uint32_t> ins(nsec);
     for (int i = 0; i < nsec; i++) { ids[i] = secs[i].sec; ins[i] = secs[i].in_size; }
+    // every method of every section in one launch (see sections.encode_run)
+    for (int i = 0; i < nsec; i++) masks[i] = avail[secs[i].sec];
+    if (fqz5_sections_try(secs, nsec, masks.data(), sizes.data())) return -1;
     fqz5_trial_replay(ids.data(), ins.data(), sizes.data(), nsec, avail, st, meth.data(),
                       nullptr);
     return fqz5_sections_commit(secs, nsec, meth.data(), res);

@@ -4,10 +4,12 @@ A "run" is a list of blocks in file order; each block has a sequence and a
 quality section (fqzcomp5.c:2217-2257).  Encoding follows fqzcomp5's codec
 trial (metrics_method / compress_with_methods, fqzcomp5.c:1899-2144):
 
-    sizes  = try(local sections)            # all candidates, one GPU batch
-    sizes  = exchange(sizes)                # multi-GPU: all_gather (RCCL)
+    ids    = exchange(section ids)          # multi-GPU: all_gather (RCCL)
+    masks  = schedule(all sections)         # which sections try every method
+    sizes  = try(local sections, masks)     # trial candidates, one GPU batch
+    sizes  = exchange(sizes)
     meth   = replay(all sections, sizes)    # host state machine, file order
-    commit(local sections, meth)            # chosen streams, framed
+    commit(local sections, meth)            # the rest encoded once, framed
 
 so the choices are those of a single-threaded reference run over the whole
 file, whichever GPU holds which block.
@@ -65,6 +67,9 @@ def _load():
     so = _lib.load()
     if not _bound:
         so.fqz5_trial_init.argtypes = [C.POINTER(TrialState)]
+        so.fqz5_trial_schedule.argtypes = [C.POINTER(C.c_int32), C.c_int,
+                                           C.POINTER(C.c_uint32), C.POINTER(TrialState),
+                                           C.POINTER(C.c_uint32)]
         so.fqz5_sections_try.argtypes = [C.POINTER(Section), C.c_int,
                                          C.POINTER(C.c_uint32),
                                          C.POINTER(C.c_uint32)]
@@ -102,10 +107,25 @@ def _arr(t, xs):
     return (t * len(xs))(*xs)
 
 
-def sections_try(secs: list[Section], avail: np.ndarray) -> np.ndarray:
+def trial_schedule(sec_ids, avail: np.ndarray, state: TrialState) -> np.ndarray:
+    """Per section (file order) the methods it tries: avail in trial and
+    re-trial blocks, 0 where the trial sizes decide (state unchanged)."""
+    so = _load()
+    ids = np.ascontiguousarray(sec_ids, np.int32)
+    av = np.ascontiguousarray(avail, np.uint32)
+    out = np.zeros(len(ids), np.uint32)
+    so.fqz5_trial_schedule(ids.ctypes.data_as(C.POINTER(C.c_int32)), len(ids),
+                           av.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(state),
+                           out.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return out
+
+
+def sections_try(secs: list[Section], masks: np.ndarray) -> np.ndarray:
+    """Candidates of masks[i] (per section) for every section."""
     so = _load()
     sizes = np.zeros(len(secs) * M_LAST, np.uint32)
-    av = np.ascontiguousarray(avail, np.uint32)
+    av = np.ascontiguousarray(masks, np.uint32)
+    assert len(av) == len(secs)
     rc = so.fqz5_sections_try(_arr(Section, secs), len(secs),
                               av.ctypes.data_as(C.POINTER(C.c_uint32)),
                               sizes.ctypes.data_as(C.POINTER(C.c_uint32)))
@@ -185,11 +205,24 @@ def exchange_sizes(local: np.ndarray, in_sizes: np.ndarray, sec_ids: np.ndarray,
 
 
 def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
-               group=None):
-    """try -> (exchange) -> replay -> commit for this rank's sections."""
-    local = sections_try(secs, avail)
+               group=None, speculate: bool = True):
+    """try -> (exchange) -> replay -> commit for this rank's sections.
+
+    speculate: every section tries every method in one GPU launch.  A launch
+    lasts as long as its longest rANS chain, so the extra candidates cost
+    little, while encoding the non-trial sections after the replay would add
+    a second chain-length launch.  speculate=False tries only the sections
+    the schedule names (trial and re-trial blocks) and encodes the others
+    once at commit, for candidates that do cost in proportion to their work."""
     ins = np.array([s.in_size for s in secs], np.uint32)
     ids = np.array([s.sec for s in secs], np.int32)
+    if speculate:
+        masks = np.asarray(avail, np.uint32)[ids]
+    else:
+        blank = np.zeros((len(secs), M_LAST), np.uint32)
+        _, _, g_ids0, off = exchange_sizes(blank, ins, ids, group)
+        masks = trial_schedule(g_ids0, avail, state)[off:off + len(secs)]
+    local = sections_try(secs, masks)
     g_sizes, g_ins, g_ids, off = exchange_sizes(local, ins, ids, group)
     tried = np.zeros(len(g_ids), np.uint32)
     meth_all = trial_replay(g_ids, g_ins, g_sizes, avail, state, tried)

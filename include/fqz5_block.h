@@ -64,14 +64,21 @@ void fqz5_trial_init(fqz5_trial_state *st);
 int fqz5_encode_sections(const fqz5_section *secs, int n, const uint32_t *avail,
                          fqz5_trial_state *st, fqz5_section_result *res);
 
-/* The same in three phases, for callers that replay the trial state over
+/* The same in four phases, for callers that replay the trial state over
  * sections held by several processes (multi-GPU, bench.py):
- *   try     compress every candidate of every section; sizes[i*FQZ5_M_LAST+m]
- *           = candidate size, UINT32_MAX when not run (compress_with_methods'
- *           out_len); the candidates stay on the GPU until commit;
- *   replay  the host-only trial state machine over sections in file order;
- *   commit  write the chosen candidates, framed, to the outputs. */
-int fqz5_sections_try(const fqz5_section *secs, int n, const uint32_t *avail,
+ *   schedule  host only: per section (file order) the method mask it tries,
+ *             avail[sec] in trial / re-trial blocks and 0 elsewhere (their
+ *             one method follows from the trial sizes); st is not changed;
+ *   try       compress every method of masks[i] for each section;
+ *             sizes[i*FQZ5_M_LAST+m] = candidate size, UINT32_MAX when not
+ *             run (compress_with_methods' out_len); the candidates stay on
+ *             the GPU until commit;
+ *   replay    the host-only trial state machine over sections in file order;
+ *   commit    encode the sections whose chosen method was not tried, then
+ *             write every chosen stream, framed, to the outputs. */
+void fqz5_trial_schedule(const int32_t *sec_ids, int n, const uint32_t *avail,
+                         const fqz5_trial_state *st, uint32_t *masks_out);
+int fqz5_sections_try(const fqz5_section *secs, int n, const uint32_t *masks,
                       uint32_t *sizes);
 void fqz5_trial_replay(const int32_t *sec_ids, const uint32_t *in_sizes,
                        const uint32_t *sizes, int n, const uint32_t *avail,

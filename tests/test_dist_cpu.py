@@ -68,3 +68,21 @@ def test_two_ranks_match_single_process_replay():
     assert got[0][0] == 0 and got[1][0] == len(parts[0][0])
     assert got[0][2] == ids.tolist() == got[1][2]
     assert got[0][1] + got[1][1] == ref
+
+
+def test_schedule_matches_replay():
+    """The size-free schedule names exactly the sections that try every
+    method in a full replay (trial and re-trial blocks: 3 per 100)."""
+    rng = np.random.default_rng(9)
+    ids = np.array([S.SEC_SEQ, S.SEC_QUAL] * 230, np.int32)
+    ins = rng.integers(10_000, 100_000, len(ids)).astype(np.uint32)
+    sizes = np.full((len(ids), S.M_LAST), 0xFFFFFFFF, np.uint32)
+    sizes[:, 1:10] = rng.integers(1_000, 50_000, (len(ids), 9))
+    av = S.masks(3)
+    sched = S.trial_schedule(ids, av, S.new_state())
+    tried = np.zeros(len(ids), np.uint32)
+    S.trial_replay(ids, ins, sizes, av, S.new_state(), tried)
+    multi = np.array([bin(int(t)).count("1") > 1 for t in tried])
+    assert (sched[multi] == tried[multi]).all()
+    assert (sched[~multi] == 0).all()
+    assert multi.sum() == 2 * 3 * 3        # blocks 1-3, 104-106, 207-209 per section
