@@ -11,10 +11,12 @@
 // trial state machine is replayed on the host in block order, which gives
 // exactly the choices of a single-threaded (-t1) reference run.
 #include <cstring>
+#include <deque>
 #include <vector>
 
 #include "../../include/fqz5_block.h"
 #include "rans_codec.hpp"
+#include "fqz_codec.hpp"
 #include "rans_format.hpp"
 
 namespace fqz5 {
@@ -27,12 +29,16 @@ namespace {
 // fqzcomp5.c:185-208
 enum Method {
     RANS0 = 1, RANS1, RANS64, RANS65, RANS128, RANS129, RANS192, RANS193,
-    RANSXN1, LZP3, M_LAST = 31
+    RANSXN1, LZP3, FQZ0 = 26, FQZ1, FQZ2, FQZ3, FQZ4, M_LAST = 31
 };
 constexpr uint32_t RANS_MASK =
     (1u << RANS0) | (1u << RANS1) | (1u << RANS64) | (1u << RANS65) |
     (1u << RANS128) | (1u << RANS129) | (1u << RANS192) | (1u << RANS193) |
     (1u << RANSXN1);
+constexpr uint32_t FQZ_MASK =
+    (1u << FQZ0) | (1u << FQZ1) | (1u << FQZ2) | (1u << FQZ3) | (1u << FQZ4);
+
+bool is_fqz(int m) { return m >= FQZ0 && m <= FQZ4; }
 
 // order word per rANS method (fqzcomp5.c:1992-2010)
 int method_order(int m, uint32_t fixed_len) {
@@ -76,8 +82,31 @@ uint32_t metrics_method(fqz5_trial_state &st, int sec, uint32_t avail) {
 struct TrySession {
     std::vector<CompressReq> reqs;
     std::vector<std::vector<int>> req_of;
+    std::vector<FqzEncReq> fqz;                   // FQZ candidates
+    std::vector<std::vector<int>> fqz_of;
+    std::deque<std::vector<uint32_t>> recs;       // their (rewritable) lengths / flags
     bool open = false;
 };
+
+// fqz_compress(4, slice, in, size, &len, m - FQZ0, NULL) for a section
+// (compress_with_methods, fqzcomp5.c:2071-2092)
+FqzEncReq fqz_req(const fqz5_section &S, int m, std::deque<std::vector<uint32_t>> &keep) {
+    FqzEncReq r;
+    r.d_in = S.in;
+    r.n = S.in_size;
+    r.nrec = S.nrec;
+    keep.emplace_back(S.rec_len, S.rec_len + std::max(S.nrec, 0));
+    r.lens = keep.back().data();
+    if (S.rec_flags)
+        keep.emplace_back(S.rec_flags, S.rec_flags + std::max(S.nrec, 0));
+    else
+        keep.emplace_back(size_t(std::max(S.nrec, 0)), 0u);
+    r.flags = keep.back().data();
+    r.d_seq = S.seq;
+    r.vers = 4;
+    r.strat = m - FQZ0;
+    return r;
+}
 thread_local TrySession t_sess;
 
 }  // namespace fqz5
@@ -117,16 +146,25 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         GpuCtx &g = gpu();
         if (t_sess.open) g.reset();
         t_sess = TrySession();
-        for (int i = 0; i < nsec; i++)
-            if (masks[i] & ~RANS_MASK)
-                throw GpuError("fqz5_sections_try: method mask has non-rANS methods "
-                               "(LZP/tok3/seq-CM/fqz are not in this build)");
+        for (int i = 0; i < nsec; i++) {
+            if (masks[i] & ~(RANS_MASK | FQZ_MASK))
+                throw GpuError("fqz5_sections_try: method mask has LZP/tok3/seq-CM methods "
+                               "(not in this build)");
+            if ((masks[i] & FQZ_MASK) && (secs[i].sec != FQZ5_SEC_QUAL || !secs[i].rec_len))
+                throw GpuError("fqz5_sections_try: FQZ methods need a quality section with records");
+        }
         std::vector<CompressReq> &reqs = t_sess.reqs;
         t_sess.req_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
+        t_sess.fqz_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
         for (int i = 0; i < nsec; i++) {
             const fqz5_section &S = secs[i];
             for (int m = 1; m < FQZ5_M_LAST; m++) {
                 if (!(masks[i] & (1u << m))) continue;
+                if (is_fqz(m)) {
+                    t_sess.fqz_of[i][m] = int(t_sess.fqz.size());
+                    t_sess.fqz.push_back(fqz_req(S, m, t_sess.recs));
+                    continue;
+                }
                 if (m == RANSXN1 && !S.fixed_len) continue;   // out = NULL (:2004-2007)
                 CompressReq r;
                 r.d_in = S.in;
@@ -138,14 +176,17 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             }
         }
         compress_batch(g, reqs);
+        if (!t_sess.fqz.empty()) fqz_encode_batch(g, t_sess.fqz);
         t_sess.open = true;
         // sizes as compress_with_methods sees them: UINT_MAX when not run,
         // 0 when the codec returned NULL (out_len = *out_size = 0)
         for (int i = 0; i < nsec; i++)
             for (int m = 0; m < FQZ5_M_LAST; m++) {
-                const int ri = t_sess.req_of[i][m];
-                sizes[size_t(i) * FQZ5_M_LAST + m] =
-                    ri < 0 ? UINT32_MAX : (reqs[ri].ok ? layout_size(reqs[ri].out) : 0);
+                const int ri = t_sess.req_of[i][m], fi = t_sess.fqz_of[i][m];
+                uint32_t sz = UINT32_MAX;
+                if (ri >= 0) sz = reqs[ri].ok ? layout_size(reqs[ri].out) : 0;
+                if (fi >= 0) sz = t_sess.fqz[size_t(fi)].ok ? layout_size(t_sess.fqz[size_t(fi)].out) : 0;
+                sizes[size_t(i) * FQZ5_M_LAST + m] = sz;
             }
         return 0;
     } catch (const std::exception &e) {
@@ -197,10 +238,17 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             throw GpuError("fqz5_sections_commit: no matching fqz5_sections_try");
         // sections outside the trial: their one method, encoded now
         std::vector<CompressReq> late;
-        std::vector<int> late_of(nsec, -1);
+        std::vector<int> late_of(nsec, -1), late_fqz_of(nsec, -1);
+        std::vector<FqzEncReq> late_fqz;
         for (int i = 0; i < nsec; i++) {
             const int m = methods[i];
-            if (m <= 0 || m >= FQZ5_M_LAST || t_sess.req_of[i][m] >= 0) continue;
+            if (m <= 0 || m >= FQZ5_M_LAST || t_sess.req_of[i][m] >= 0 || t_sess.fqz_of[i][m] >= 0)
+                continue;
+            if (is_fqz(m) && secs[i].sec == FQZ5_SEC_QUAL && secs[i].rec_len) {
+                late_fqz_of[i] = int(late_fqz.size());
+                late_fqz.push_back(fqz_req(secs[i], m, t_sess.recs));
+                continue;
+            }
             if (!(RANS_MASK & (1u << m)) || (m == RANSXN1 && !secs[i].fixed_len)) continue;
             CompressReq r;
             r.d_in = secs[i].in;
@@ -211,6 +259,7 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             late.push_back(std::move(r));
         }
         if (!late.empty()) compress_batch(g, late);
+        if (!late_fqz.empty()) fqz_encode_batch(g, late_fqz);
         std::vector<const Layout *> ls;
         std::vector<uint8_t *> dsts;
         std::vector<Layout> framed(nsec);
@@ -219,23 +268,29 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             fqz5_section_result &R = res[i];
             const int m = methods[i];
             const int ri = (m > 0 && m < FQZ5_M_LAST) ? t_sess.req_of[i][m] : -1;
-            const CompressReq *rq = ri >= 0 ? &t_sess.reqs[ri] : late_of[i] >= 0 ? &late[late_of[i]] : nullptr;
+            const int fi = (m > 0 && m < FQZ5_M_LAST) ? t_sess.fqz_of[i][m] : -1;
+            const Layout *lay = nullptr;
+            if (ri >= 0 && t_sess.reqs[ri].ok) lay = &t_sess.reqs[ri].out;
+            if (late_of[i] >= 0 && late[late_of[i]].ok) lay = &late[late_of[i]].out;
+            if (fi >= 0 && t_sess.fqz[size_t(fi)].ok) lay = &t_sess.fqz[size_t(fi)].out;
+            if (late_fqz_of[i] >= 0 && late_fqz[late_fqz_of[i]].ok) lay = &late_fqz[late_fqz_of[i]].out;
             R.method = m;
-            R.strat = 0;
+            R.strat = is_fqz(m) ? 1 : 0;   // compress_with_methods' *strat
             R.status = -1;
             R.clen = 0;
             R.usize = S.in_size;
-            if (!rq || !rq->ok) continue;
-            const uint32_t clen = layout_size(rq->out);
+            if (!lay) continue;
+            const uint32_t clen = layout_size(*lay);
             R.clen = clen;
             if (9ull + clen > S.out_cap) continue;
             // section framing [strat u8][u32 usize][u32 csize] (:2224-2229)
             Piece h;
             h.host.resize(9);
+            h.host[0] = uint8_t(R.strat);
             std::memcpy(&h.host[1], &S.in_size, 4);
             std::memcpy(&h.host[5], &clen, 4);
             framed[i].push_back(std::move(h));
-            for (auto &p : rq->out) framed[i].push_back(p);
+            for (auto &p : *lay) framed[i].push_back(p);
             ls.push_back(&framed[i]);
             dsts.push_back(S.out);
             R.status = 0;
@@ -280,7 +335,8 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         }
         g.sync();
         std::vector<DecompressReq> reqs;
-        std::vector<int> who;
+        std::vector<FqzDecReq> fqz;
+        std::vector<int> who, who_fqz;
         off = 0;
         for (int i = 0; i < nsec; i++) {
             const uint8_t *h = host.data() + off;
@@ -292,7 +348,22 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             std::memcpy(&clen, h + 5, 4);
             res[i].strat = h[0];
             res[i].clen = clen;
-            if (h[0] != 0 || 9ull + clen > secs[i].in_size || ulen > secs[i].out_cap) continue;
+            if (9ull + clen > secs[i].in_size || ulen > secs[i].out_cap) continue;
+            if (h[0] == 1 && secs[i].sec == FQZ5_SEC_QUAL) {   // fqz_decompress (:2498-2530)
+                FqzDecReq f;
+                f.h_in = h + 9;
+                f.d_in = secs[i].in + 9;
+                f.in_size = clen;
+                f.nrec = secs[i].rec_len ? secs[i].nrec : 0;
+                f.lens = secs[i].rec_len;
+                f.d_seq = secs[i].seq;
+                f.d_out = secs[i].out;
+                f.out_cap = secs[i].out_cap;
+                fqz.push_back(f);
+                who_fqz.push_back(i);
+                continue;
+            }
+            if (h[0] != 0) continue;
             DecompressReq r;
             r.h_in = h + 9;
             r.d_in = secs[i].in + 9;
@@ -303,10 +374,18 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             who.push_back(i);
         }
         decompress_batch(g, reqs);
+        // after the rANS sections: a quality section's sequence context may
+        // be the output of this call's sequence section
+        if (!fqz.empty()) fqz_decode_batch(g, fqz);
         for (size_t k = 0; k < reqs.size(); k++) {
             fqz5_section_result &R = res[who[k]];
             R.status = reqs[k].ok ? 0 : -1;
             R.usize = reqs[k].out_size;
+        }
+        for (size_t k = 0; k < fqz.size(); k++) {
+            fqz5_section_result &R = res[who_fqz[k]];
+            R.status = fqz[k].ok ? 0 : -1;
+            R.usize = uint32_t(fqz[k].out_size);
         }
         g.reset();
         return 0;

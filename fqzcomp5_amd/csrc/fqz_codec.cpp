@@ -8,6 +8,8 @@
 // serial model + range-coder kernel writes the stream.  Decode parses the
 // parameters on the host and runs the serial decode kernel.
 #include <algorithm>
+#include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -18,6 +20,7 @@
 #include "fqz_kernels.h"
 #include "gpu_ctx.hpp"
 #include "rans_format.hpp"
+#include "fqz_codec.hpp"
 
 namespace fqz5 {
 using namespace fqz;
@@ -356,290 +359,456 @@ void gather_seq(GpuCtx &g, unsigned char **seq, int nrec, const uint32_t *lens,
     *d_off = g.upload(off);
 }
 
-// The parallel encoder (fqz_kernels.hip "parallel encoder"): events per
-// record, scan, stable sort by model, per-model pass, range coder.
-void encode_events(GpuCtx &g, const FqzEncJob &E, const Global &G, int nrec) {
-    FqzEvJob J{};
-    J.g = E.g;
-    J.q = E.q;
-    J.len = E.len;
-    J.sel = E.sel;
-    J.flags = E.flags;
-    J.nrec = uint32_t(nrec);
-    J.seq = E.seq;
-    J.seq_off = E.seq_off;
-    std::vector<uint64_t> off(static_cast<size_t>(nrec));
+// Device sequence bytes laid out back to back: record r at the sum of the
+// earlier lengths (fqzcomp5 passes pointers into its contiguous seq_buf).
+const uint64_t *seq_offsets(GpuCtx &g, int nrec, const uint32_t *lens) {
+    std::vector<uint64_t> off(size_t(std::max(nrec, 1)), ~0ull);
     uint64_t o = 0;
-    std::vector<uint32_t> lens(static_cast<size_t>(nrec));
-    g.download(lens.data(), E.len, lens.size());
-    g.sync();
-    for (int r = 0; r < nrec; r++) off[size_t(r)] = o, o += lens[size_t(r)];
-    J.off = g.upload(off);
-    J.nev_rec = g.arena.alloc_n<uint32_t>(size_t(nrec));
-    uint32_t *ev_off = g.arena.alloc_n<uint32_t>(size_t(nrec));
-    J.ev_off = ev_off;
-    J.dup = g.arena.alloc_n<uint8_t>(size_t(nrec));
-    FQZ5_HIP(launch_fqz_events(J, 0, g.stream));
-    size_t tb = 0;
-    FQZ5_HIP(fqz_exclusive_scan(J.nev_rec, ev_off, nrec, nullptr, tb, g.stream));
-    void *tmp = g.arena.alloc_n<uint8_t>(tb);
-    FQZ5_HIP(fqz_exclusive_scan(J.nev_rec, ev_off, nrec, tmp, tb, g.stream));
-    uint32_t last[2] = {0, 0};
-    g.download(&last[0], ev_off + nrec - 1, 1);
-    g.download(&last[1], J.nev_rec + nrec - 1, 1);
-    g.sync();
-    const uint64_t nev = uint64_t(last[0]) + last[1];
-    if (nev >= (1ull << 31)) throw std::runtime_error("fqz: block too large");
-    J.nev = uint32_t(nev);
-    J.key = g.arena.alloc_n<uint32_t>(nev);
-    J.val = g.arena.alloc_n<uint64_t>(nev);
-    uint32_t *skey = g.arena.alloc_n<uint32_t>(nev);
-    uint64_t *sval = g.arena.alloc_n<uint64_t>(nev);
-    J.skey = skey;
-    J.sval = sval;
-    J.code = g.arena.alloc_n<uint64_t>(nev);
-    FQZ5_HIP(launch_fqz_events(J, 1, g.stream));
-    tb = 0;
-    FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(nev), int(FQZ_MODEL_BITS), nullptr,
-                               tb, g.stream));
-    tmp = g.arena.alloc_n<uint8_t>(tb);
-    FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(nev), int(FQZ_MODEL_BITS), tmp, tb,
-                               g.stream));
-    J.seg_lo = g.arena.alloc_n<uint32_t>(FQZ_NMODELS);
-    J.seg_hi = g.arena.alloc_n<uint32_t>(FQZ_NMODELS);
-    g.memset0(J.seg_lo, FQZ_NMODELS * 4);
-    g.memset0(J.seg_hi, FQZ_NMODELS * 4);
-    FQZ5_HIP(launch_fqz_events(J, 2, g.stream));
-    J.scratch = g.arena.alloc_n<uint8_t>(8192);
-    FQZ5_HIP(launch_fqz_model_pass(J, g.stream));
-    // the range chain, then the output bytes as a big-number sum
-    J.rec = g.arena.alloc_n<uint4>(nev);
-    FQZ5_HIP(launch_fqz_expand(J, g.stream));
-    J.addend = g.arena.alloc_n<uint32_t>(nev);
-    J.shifts = g.arena.alloc_n<uint32_t>(nev + 1);
-    FQZ5_HIP(launch_fqz_rc(J, g.stream));
-    uint32_t *pos = g.arena.alloc_n<uint32_t>(nev + 1);
-    g.memset0(J.shifts + nev, 4);
-    tb = 0;
-    FQZ5_HIP(fqz_exclusive_scan(J.shifts, pos, int(nev + 1), nullptr, tb, g.stream));
-    tmp = g.arena.alloc_n<uint8_t>(tb);
-    FQZ5_HIP(fqz_exclusive_scan(J.shifts, pos, int(nev + 1), tmp, tb, g.stream));
-    J.pos = pos;
-    J.nshift = pos + nev;
-    uint32_t P = 0;
-    g.download(&P, pos + nev, 1);
-    g.sync();
-    J.nwords = (P + 5 + 3) / 4 + 2;
-    J.acc = reinterpret_cast<unsigned long long *>(g.arena.alloc_n<uint64_t>(J.nwords));
-    g.memset0(J.acc, size_t(J.nwords) * 8);
-    J.out = E.out;
-    J.out_len = E.out_len;
-    FQZ5_HIP(launch_fqz_bytes(J, 0, g.stream));
-    FQZ5_HIP(launch_fqz_bytes(J, 1, g.stream));
-    FQZ5_HIP(launch_fqz_bytes(J, 2, g.stream));
-    (void)G;
+    for (int r = 0; r < nrec; r++) off[size_t(r)] = o, o += lens[r];
+    return g.upload(off);
+}
+
+void copy_gparams(Global &G, const fqz_gparams *gp) {
+    // caller-supplied parameters (fqzcomp_qual.c:1040-1045)
+    G.vers = gp->vers;
+    G.gflags = gp->gflags;
+    G.nparam = gp->nparam;
+    G.max_sel = gp->max_sel;
+    G.max_sym = gp->max_sym;
+    for (int i = 0; i < 256; i++) G.stab[i] = gp->stab[i];
+    G.p.assign(size_t(gp->nparam), Param());
+    for (int k = 0; k < gp->nparam; k++) {
+        const fqz_param &a = gp->p[k];
+        Param &b = G.p[size_t(k)];
+        b.ctx0 = a.context;
+        b.pflags = a.pflags;
+        b.sel = a.do_sel, b.dedup = a.do_dedup, b.qmap_stored = a.store_qmap,
+        b.fixed = a.fixed_len;
+        b.qtab_on = a.use_qtab, b.dtab_on = a.use_dtab, b.ptab_on = a.use_ptab;
+        b.qbits = a.qbits, b.qloc = a.qloc, b.pbits = a.pbits, b.ploc = a.ploc;
+        b.dbits = a.dbits, b.dloc = a.dloc, b.sloc = a.sloc;
+        b.bbits = a.bbits, b.bloc = a.bloc, b.boff = a.boff;
+        b.max_sym = a.max_sym, b.nsym = a.nsym, b.max_sel = a.max_sel;
+        b.qshift = a.qshift, b.pshift = a.pshift, b.dshift = a.dshift;
+        std::memcpy(b.qmap, a.qmap, sizeof b.qmap);
+        std::memcpy(b.qtab, a.qtab, sizeof b.qtab);
+        std::memcpy(b.ptab, a.ptab, sizeof b.ptab);
+        std::memcpy(b.dtab, a.dtab, sizeof b.dtab);
+    }
 }
 
 }  // namespace
 
+struct FqzEncReq::Work {
+    Global G;
+    std::vector<uint8_t> hdr;
+    FqzEncJob E{};
+    FqzEvJob J{};
+    bool parallel = false;
+    size_t room = 0;
+    uint32_t last[2] = {0, 0};          // last record's event offset and count
+    uint32_t P = 0, clen = 0;
+};
+
+// Every block of the batch goes through each stage before the next one:
+// parameters (statistics kernels, host decisions), events, sort, the
+// per-model pass (one launch for all blocks), the range chain (one launch,
+// one wave per block), the big-number bytes (carry: one launch).
+void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
+    std::vector<FqzEncReq *> par;
+    for (FqzEncReq &R : reqs) {
+        R.ok = false;
+        R.out.clear();
+        R.w = std::make_shared<FqzEncReq::Work>();
+        FqzEncReq::Work &W = *R.w;
+        Global &G = W.G;
+        const int nrec = R.nrec;
+        const size_t n = R.n;
+        const uint64_t *d_soff =
+            (R.d_seq && nrec > 0) ? seq_offsets(g, nrec, R.lens) : nullptr;
+        if (!R.gp) {
+            pick_begin(G, R.vers, R.strat, nrec, R.lens, n);
+            uint32_t qhist[256] = {0};
+            const Records Rec = walk_records(nrec, R.lens, R.flags, n);
+            tune(g, G.p[0], nrec, R.flags, Rec, R.d_in, n, qhist);
+            pick_finish(G, G.p[0], R.strat, nrec, R.lens, R.flags, n, qhist);
+        } else {
+            copy_gparams(G, R.gp);
+        }
+        const bool have_seq = nrec > 0 && (R.d_seq || (R.h_seq && R.h_seq[0]));
+        if (!have_seq) {
+            for (Param &pm : G.p) pm.bbits = pm.bloc = 0;
+            G.gflags &= ~unsigned(GF_SEQ);
+        } else {
+            for (Param &pm : G.p)
+                if (pm.bbits) G.gflags |= GF_SEQ;
+        }
+        if (R.gp) {   // the reference edits the caller's block in place
+            R.gp->gflags = G.gflags;
+            for (int k = 0; k < R.gp->nparam; k++) {
+                R.gp->p[k].bbits = G.p[size_t(k)].bbits;
+                R.gp->p[k].bloc = G.p[size_t(k)].bloc;
+                for (int i = 0; i < 1024; i++) R.gp->p[k].ptab[i] <<= R.gp->p[k].ploc;
+                for (int i = 0; i < 256; i++) R.gp->p[k].dtab[i] <<= R.gp->p[k].dloc;
+            }
+        }
+        W.hdr.assign(16 + 8192 * size_t(std::max(G.nparam, 1)), 0);
+        size_t hdr = size_t(varint_put(W.hdr.data(), W.hdr.data() + W.hdr.size(), uint32_t(n)));
+        hdr += size_t(put_params(G, W.hdr.data() + hdr));
+        W.hdr.resize(hdr);
+
+        const FqzDevGlobal dg = dev_params(G);
+        FqzEncJob &E = W.E;
+        E.g = g.upload(&dg, 1);
+        E.q = R.d_in;
+        E.n = n;
+        std::vector<uint32_t> lens(R.lens, R.lens + std::max(nrec, 0));
+        std::vector<uint32_t> sels(size_t(std::max(nrec, 0))), fl(size_t(std::max(nrec, 0)));
+        for (int r = 0; r < nrec; r++) {
+            sels[size_t(r)] = R.flags[r] >> 16;
+            fl[size_t(r)] = R.flags[r];
+        }
+        lens.push_back(0);
+        sels.push_back(0);
+        fl.push_back(0);
+        E.len = g.upload(lens);
+        E.sel = g.upload(sels);
+        E.flags = g.upload(fl);
+        E.nrec = uint32_t(std::max(nrec, 0));
+        if (have_seq && R.d_seq) {
+            E.seq = R.d_seq;
+            E.seq_off = d_soff;
+        } else if (have_seq) {
+            unsigned boff = 0;
+            for (const Param &pm : G.p) boff = std::max(boff, pm.boff);
+            gather_seq(g, R.h_seq, nrec, R.lens, boff, &E.seq, &E.seq_off);
+        }
+        W.room = size_t(double(n) * 1.1 + 100000);
+        E.out = g.arena.alloc_n<uint8_t>(W.room);
+        E.out_len = g.arena.alloc_n<uint32_t>(1);
+        // The parallel encoder covers one parameter block and non-empty
+        // records (the reference's loop codes the next record's first byte
+        // inside an empty record, which only its literal serial form
+        // reproduces).
+        W.parallel = G.nparam == 1 && !(G.gflags & GF_MULTI) && nrec > 0;
+        for (int r = 0; W.parallel && r < nrec; r++) W.parallel = R.lens[r] > 0;
+        if (!W.parallel) {
+            E.models = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * FQZ_QMODEL_BYTES);
+            FQZ5_HIP(launch_fqz_model_init(E.models, G.max_sym + 1, g.stream));
+            FQZ5_HIP(launch_fqz_encode(E, g.stream));
+            continue;
+        }
+        par.push_back(&R);
+        FqzEvJob &J = W.J;
+        J.g = E.g;
+        J.q = E.q;
+        J.len = E.len;
+        J.sel = E.sel;
+        J.flags = E.flags;
+        J.nrec = uint32_t(nrec);
+        J.seq = E.seq;
+        J.seq_off = E.seq_off;
+        std::vector<uint64_t> off(static_cast<size_t>(nrec));
+        uint64_t o = 0;
+        for (int r = 0; r < nrec; r++) off[size_t(r)] = o, o += R.lens[r];
+        J.off = g.upload(off);
+        J.nev_rec = g.arena.alloc_n<uint32_t>(size_t(nrec));
+        uint32_t *ev_off = g.arena.alloc_n<uint32_t>(size_t(nrec));
+        J.ev_off = ev_off;
+        J.dup = g.arena.alloc_n<uint8_t>(size_t(nrec));
+        FQZ5_HIP(launch_fqz_events(J, 0, g.stream));
+        size_t tb = 0;
+        FQZ5_HIP(fqz_exclusive_scan(J.nev_rec, ev_off, nrec, nullptr, tb, g.stream));
+        void *tmp = g.arena.alloc_n<uint8_t>(tb);
+        FQZ5_HIP(fqz_exclusive_scan(J.nev_rec, ev_off, nrec, tmp, tb, g.stream));
+        g.download(&W.last[0], ev_off + nrec - 1, 1);
+        g.download(&W.last[1], J.nev_rec + nrec - 1, 1);
+    }
+    g.sync();
+
+    // events of every block, sorted by model; then one model pass for all
+    std::vector<FqzEvJob> jobs;
+    for (FqzEncReq *R : par) {
+        FqzEvJob &J = R->w->J;
+        const uint64_t nev = uint64_t(R->w->last[0]) + R->w->last[1];
+        if (nev >= (1ull << 31)) throw std::runtime_error("fqz: block too large");
+        J.nev = uint32_t(nev);
+        J.key = g.arena.alloc_n<uint32_t>(nev);
+        J.val = g.arena.alloc_n<uint64_t>(nev);
+        uint32_t *skey = g.arena.alloc_n<uint32_t>(nev);
+        uint64_t *sval = g.arena.alloc_n<uint64_t>(nev);
+        J.skey = skey;
+        J.sval = sval;
+        J.code = g.arena.alloc_n<uint64_t>(nev);
+        FQZ5_HIP(launch_fqz_events(J, 1, g.stream));
+        size_t tb = 0;
+        FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(nev), int(FQZ_MODEL_BITS),
+                                   nullptr, tb, g.stream));
+        void *tmp = g.arena.alloc_n<uint8_t>(tb);
+        FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(nev), int(FQZ_MODEL_BITS), tmp,
+                                   tb, g.stream));
+        J.seg_lo = g.arena.alloc_n<uint32_t>(FQZ_NMODELS);
+        J.seg_hi = g.arena.alloc_n<uint32_t>(FQZ_NMODELS);
+        g.memset0(J.seg_lo, FQZ_NMODELS * 4);
+        g.memset0(J.seg_hi, FQZ_NMODELS * 4);
+        FQZ5_HIP(launch_fqz_events(J, 2, g.stream));
+        J.scratch = g.arena.alloc_n<uint8_t>(8192);
+        jobs.push_back(J);
+    }
+    const int np = int(par.size());
+    if (np) FQZ5_HIP(launch_fqz_model_pass(g.upload(jobs), np, g.stream));
+    // the range chain of every block (one wave each), then the output bytes
+    for (int k = 0; k < np; k++) {
+        FqzEvJob &J = par[size_t(k)]->w->J;
+        J.rec = g.arena.alloc_n<uint4>(J.nev);
+        FQZ5_HIP(launch_fqz_expand(J, g.stream));
+        J.addend = g.arena.alloc_n<uint32_t>(J.nev);
+        J.shifts = g.arena.alloc_n<uint32_t>(J.nev + 1);
+        jobs[size_t(k)] = J;
+    }
+    if (np) FQZ5_HIP(launch_fqz_rc(g.upload(jobs), np, g.stream));
+    for (int k = 0; k < np; k++) {
+        FqzEncReq::Work &W = *par[size_t(k)]->w;
+        FqzEvJob &J = W.J;
+        uint32_t *pos = g.arena.alloc_n<uint32_t>(J.nev + 1);
+        g.memset0(J.shifts + J.nev, 4);
+        size_t tb = 0;
+        FQZ5_HIP(fqz_exclusive_scan(J.shifts, pos, int(J.nev + 1), nullptr, tb, g.stream));
+        void *tmp = g.arena.alloc_n<uint8_t>(tb);
+        FQZ5_HIP(fqz_exclusive_scan(J.shifts, pos, int(J.nev + 1), tmp, tb, g.stream));
+        J.pos = pos;
+        J.nshift = pos + J.nev;
+        g.download(&W.P, pos + J.nev, 1);
+    }
+    g.sync();
+    for (int k = 0; k < np; k++) {
+        FqzEncReq::Work &W = *par[size_t(k)]->w;
+        FqzEvJob &J = W.J;
+        J.nwords = (W.P + 5 + 3) / 4 + 2;
+        J.acc = reinterpret_cast<unsigned long long *>(g.arena.alloc_n<uint64_t>(J.nwords));
+        g.memset0(J.acc, size_t(J.nwords) * 8);
+        J.out = W.E.out;
+        J.out_len = W.E.out_len;
+        FQZ5_HIP(launch_fqz_bytes(J, 0, g.stream));
+        jobs[size_t(k)] = J;
+    }
+    if (np) FQZ5_HIP(launch_fqz_carry(g.upload(jobs), np, g.stream));
+    for (int k = 0; k < np; k++) FQZ5_HIP(launch_fqz_bytes(par[size_t(k)]->w->J, 2, g.stream));
+
+    for (FqzEncReq &R : reqs) g.download(&R.w->clen, R.w->E.out_len, 1);
+    g.sync();
+    for (FqzEncReq &R : reqs) {
+        FqzEncReq::Work &W = *R.w;
+        for (int r = 0; r < R.nrec; r++) R.flags[r] &= 0xffff;
+        if (W.clen > W.room) continue;   // (cannot happen: the bound covers the coder)
+        Piece h;
+        h.host = W.hdr;
+        Piece d;
+        d.dev = W.E.out;
+        d.len = W.clen;
+        R.out.push_back(std::move(h));
+        R.out.push_back(d);
+        R.ok = true;
+    }
+}
+
 uint8_t *fqz_encode_gpu(int vers, fqz_slice *s, const uint8_t *in, size_t n, size_t *out_size,
                         int strat, fqz_gparams *gp) {
     GpuCtx &g = gpu();
-    const int nrec = s ? s->num_records : 0;
-    const size_t cap = size_t(double(n) * 1.1 + 100000);
-    uint8_t *out = static_cast<uint8_t *>(std::malloc(cap));
-    if (!out) throw std::runtime_error("fqz: out of host memory");
     g.reset();
-    const uint8_t *d_q = g.upload(in, n);
-    Global G;
-    if (!gp) {
-        pick_begin(G, vers, strat, nrec, s->len, n);
-        uint32_t qhist[256] = {0};
-        const Records R = walk_records(nrec, s->len, s->flags, n);
-        tune(g, G.p[0], nrec, s->flags, R, d_q, n, qhist);
-        pick_finish(G, G.p[0], strat, nrec, s->len, s->flags, n, qhist);
-    } else {
-        // caller-supplied parameters (fqzcomp_qual.c:1040-1045)
-        G.vers = gp->vers;
-        G.gflags = gp->gflags;
-        G.nparam = gp->nparam;
-        G.max_sel = gp->max_sel;
-        G.max_sym = gp->max_sym;
-        for (int i = 0; i < 256; i++) G.stab[i] = gp->stab[i];
-        G.p.assign(size_t(gp->nparam), Param());
-        for (int k = 0; k < gp->nparam; k++) {
-            const fqz_param &a = gp->p[k];
-            Param &b = G.p[size_t(k)];
-            b.ctx0 = a.context;
-            b.pflags = a.pflags;
-            b.sel = a.do_sel, b.dedup = a.do_dedup, b.qmap_stored = a.store_qmap,
-            b.fixed = a.fixed_len;
-            b.qtab_on = a.use_qtab, b.dtab_on = a.use_dtab, b.ptab_on = a.use_ptab;
-            b.qbits = a.qbits, b.qloc = a.qloc, b.pbits = a.pbits, b.ploc = a.ploc;
-            b.dbits = a.dbits, b.dloc = a.dloc, b.sloc = a.sloc;
-            b.bbits = a.bbits, b.bloc = a.bloc, b.boff = a.boff;
-            b.max_sym = a.max_sym, b.nsym = a.nsym, b.max_sel = a.max_sel;
-            b.qshift = a.qshift, b.pshift = a.pshift, b.dshift = a.dshift;
-            std::memcpy(b.qmap, a.qmap, sizeof b.qmap);
-            std::memcpy(b.qtab, a.qtab, sizeof b.qtab);
-            std::memcpy(b.ptab, a.ptab, sizeof b.ptab);
-            std::memcpy(b.dtab, a.dtab, sizeof b.dtab);
-        }
-    }
-    const bool have_seq = s && s->seq && nrec > 0 && s->seq[0];
-    if (!have_seq) {
-        for (Param &pm : G.p) pm.bbits = pm.bloc = 0;
-        G.gflags &= ~unsigned(GF_SEQ);
-    } else {
-        for (Param &pm : G.p)
-            if (pm.bbits) G.gflags |= GF_SEQ;
-    }
-    if (gp) {   // the reference edits the caller's block in place
-        gp->gflags = G.gflags;
-        for (int k = 0; k < gp->nparam; k++) {
-            gp->p[k].bbits = G.p[size_t(k)].bbits;
-            gp->p[k].bloc = G.p[size_t(k)].bloc;
-            for (int i = 0; i < 1024; i++) gp->p[k].ptab[i] <<= gp->p[k].ploc;
-            for (int i = 0; i < 256; i++) gp->p[k].dtab[i] <<= gp->p[k].dloc;
-        }
-    }
-    size_t hdr = size_t(varint_put(out, out + cap, uint32_t(n)));
-    hdr += size_t(put_params(G, out + hdr));
-
-    const FqzDevGlobal dg = dev_params(G);
-    FqzEncJob E{};
-    E.g = g.upload(&dg, 1);
-    E.q = d_q;
-    E.n = n;
-    std::vector<uint32_t> lens(s ? s->len : nullptr, s ? s->len + nrec : nullptr);
-    std::vector<uint32_t> sels(static_cast<size_t>(nrec)), fl(static_cast<size_t>(nrec));
-    for (int r = 0; r < nrec; r++) {
-        sels[size_t(r)] = s->flags[r] >> 16;
-        fl[size_t(r)] = s->flags[r];
-    }
-    lens.push_back(0);
-    sels.push_back(0);
-    fl.push_back(0);
-    E.len = g.upload(lens);
-    E.sel = g.upload(sels);
-    E.flags = g.upload(fl);
-    E.nrec = uint32_t(nrec);
-    if (have_seq) {
-        unsigned boff = 0;
-        for (const Param &pm : G.p) boff = std::max(boff, pm.boff);
-        gather_seq(g, s->seq, nrec, s->len, boff, &E.seq, &E.seq_off);
-    }
-    const size_t room = cap - hdr;
-    E.out = g.arena.alloc_n<uint8_t>(room);
-    E.out_len = g.arena.alloc_n<uint32_t>(1);
-    // The parallel encoder covers one parameter block and non-empty records
-    // (the reference's loop codes the next record's first byte inside an
-    // empty record, which only its literal serial form reproduces).
-    bool parallel = G.nparam == 1 && !(G.gflags & GF_MULTI) && nrec > 0;
-    for (int r = 0; parallel && r < nrec; r++) parallel = s->len[r] > 0;
-    if (parallel) {
-        encode_events(g, E, G, nrec);
-    } else {
-        E.models = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * FQZ_QMODEL_BYTES);
-        FQZ5_HIP(launch_fqz_model_init(E.models, G.max_sym + 1, g.stream));
-        FQZ5_HIP(launch_fqz_encode(E, g.stream));
-    }
-    uint32_t clen = 0;
-    g.download(&clen, E.out_len, 1);
-    g.sync();
-    if (clen > room) throw std::runtime_error("fqz: output overflow");
-    g.download(out + hdr, E.out, clen);
-    g.sync();
-    for (int r = 0; r < nrec; r++) s->flags[r] &= 0xffff;
-    *out_size = hdr + clen;
+    std::vector<FqzEncReq> reqs(1);
+    FqzEncReq &R = reqs[0];
+    R.d_in = g.upload(in, n);
+    R.n = n;
+    R.nrec = s ? s->num_records : 0;
+    R.lens = s ? s->len : nullptr;
+    R.flags = s ? s->flags : nullptr;
+    R.h_seq = s ? s->seq : nullptr;
+    R.vers = vers;
+    R.strat = strat;
+    R.gp = gp;
+    fqz_encode_batch(g, reqs);
+    if (!R.ok) throw std::runtime_error("fqz: output overflow");
+    const uint32_t sz = layout_size(R.out);
+    uint8_t *out = static_cast<uint8_t *>(std::malloc(sz ? sz : 1));
+    if (!out) throw std::runtime_error("fqz: out of host memory");
+    write_layout_host(g, R.out, out);
+    *out_size = sz;
     return out;
+}
+
+struct FqzDecReq::Work {
+    Global G;
+    FqzDecJob D{};
+    int ne = 1, map_mode = 0;
+    bool seq_ctx = false, qid = true, dedup = false, rev = false;
+    uint32_t total = 0, cap = 0;
+    int32_t st = 0;
+};
+
+namespace {
+
+void dec_lists(GpuCtx &g, FqzDecReq::Work &W) {
+    FqzDecJob &D = W.D;
+    D.cap_list = (W.dedup || W.rev || W.map_mode == 2) ? std::min<uint32_t>(W.cap, W.total + 1) : 0;
+    const size_t c = std::max<uint32_t>(D.cap_list, 1);
+    D.recs = g.arena.alloc_n<uint4>(W.map_mode == 2 ? c : 1);
+    D.dups = g.arena.alloc_n<uint2>(W.dedup ? c : 1);
+    D.revs = g.arena.alloc_n<uint2>(W.rev ? c : 1);
+}
+
+}  // namespace
+
+// All blocks of the batch decode in one launch per decoder variant (one
+// workgroup each), then the qmap / duplicate / reversal fix-ups.
+void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
+    std::vector<FqzDecReq *> live;
+    for (FqzDecReq &R : reqs) {
+        R.ok = false;
+        R.out_size = 0;
+        R.w = std::make_shared<FqzDecReq::Work>();
+        FqzDecReq::Work &W = *R.w;
+        uint32_t total = 0;
+        const int vk = varint_get(R.h_in, R.h_in + R.in_size, &total);
+        if (vk <= 0) continue;
+        size_t k = size_t(vk);
+        const int u = get_params(W.G, R.h_in + k, R.in_size - k);
+        if (u < 0) continue;
+        k += size_t(u);
+        const Global &G = W.G;
+        const uint32_t nlive = uint32_t(G.max_sym) + 1;
+        if (nlive > FQZ_DEC_MAX_LIVE) continue;
+        if (R.d_out && R.out_cap < total) continue;
+        W.total = total;
+        R.out_size = total;
+        const FqzDevGlobal dg = dev_params(G);
+        FqzDecJob &D = W.D;
+        D.g = g.upload(&dg, 1);
+        D.in = R.d_in + k;
+        D.in_len = R.in_size - k;
+        D.n = total;
+        const int nrec = R.nrec;
+        if (nrec > 0 && R.d_seq) {
+            D.seq = R.d_seq;
+            D.seq_off = seq_offsets(g, nrec, R.lens);
+            D.nseq = uint32_t(nrec);
+        } else if (nrec > 0 && R.h_seq && R.lens) {
+            unsigned boff = 0;
+            for (const Param &pm : G.p) boff = std::max(boff, pm.boff);
+            gather_seq(g, R.h_seq, nrec, R.lens, boff, &D.seq, &D.seq_off);
+            D.nseq = uint32_t(nrec);
+        }
+        D.nlengths = R.lengths && R.nlengths > 0 ? uint32_t(R.nlengths) : 0;
+        D.lengths = g.arena.alloc_n<uint32_t>(std::max<uint32_t>(D.nlengths, 1));
+        D.out = R.d_out ? R.d_out : g.arena.alloc_n<uint8_t>(std::max<uint32_t>(total, 1));
+        R.d_out = D.out;
+        D.status = g.arena.alloc_n<int32_t>(1);
+        D.nrec_out = g.arena.alloc_n<uint32_t>(1);
+        D.counts = g.arena.alloc_n<uint32_t>(32);
+        g.memset0(D.counts, 32 * sizeof(uint32_t));
+        D.ment = fqz_dec_model_bytes(nlive);
+        D.nsets = FQZ_DEC_CACHE_BYTES / D.ment;
+        D.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * D.ment);
+        for (const Param &pm : G.p) {
+            W.seq_ctx = W.seq_ctx || pm.bbits > 0;
+            W.dedup = W.dedup || pm.dedup;
+            for (int i = 0; i < 256; i++) {
+                W.qid = W.qid && (pm.qtab[i] & 0xffffu) == unsigned(i);
+                W.map_mode = W.map_mode || pm.qmap[i] != unsigned(i);
+            }
+        }
+        W.seq_ctx = W.seq_ctx && D.seq;
+        W.rev = (G.gflags & GF_REV) != 0;
+        if (W.map_mode) W.map_mode = G.nparam > 1 ? 2 : 1;
+        W.ne = nlive + 2 <= 64 ? 1 : 2;
+        // record lists: sized for the records the caller announced, grown to
+        // the byte count (every record holds at least one byte) on overflow
+        W.cap = std::max<uint32_t>({D.nlengths, D.nseq, 1u}) + 1024;
+        dec_lists(g, W);
+        live.push_back(&R);
+    }
+    auto launch_group = [&](const std::vector<FqzDecReq *> &rs) {
+        for (int ne = 1; ne <= 2; ne++)
+            for (int sq = 0; sq < 2; sq++)
+                for (int qi = 0; qi < 2; qi++) {
+                    std::vector<FqzDecJob> js;
+                    for (FqzDecReq *R : rs)
+                        if (R->w->ne == ne && int(R->w->seq_ctx) == sq && int(R->w->qid) == qi)
+                            js.push_back(R->w->D);
+                    if (!js.empty())
+                        FQZ5_HIP(launch_fqz_dec(g.upload(js), int(js.size()), ne, sq != 0,
+                                                qi != 0, g.stream));
+                }
+        for (FqzDecReq *R : rs) {
+            FqzDecReq::Work &W = *R->w;
+            FQZ5_HIP(launch_fqz_dec_fix(W.D, W.map_mode, W.dedup, W.rev, g.stream));
+            g.download(&W.st, W.D.status, 1);
+        }
+        g.sync();
+    };
+    launch_group(live);
+    std::vector<FqzDecReq *> again;
+    for (FqzDecReq *R : live)
+        if (R->w->st == -2) {
+            R->w->cap = R->w->total + 1;
+            dec_lists(g, *R->w);
+            again.push_back(R);
+        }
+    if (!again.empty()) launch_group(again);
+    if (std::getenv("FQZ5_DEBUG"))
+        for (FqzDecReq *R : live) {
+            const FqzDecReq::Work &W = *R->w;
+            uint32_t c[5];
+            uint64_t pr[6];
+            g.download(c, W.D.counts, 5);
+            g.download(pr, reinterpret_cast<const uint64_t *>(W.D.counts + 8), 6);
+            g.sync();
+            std::fprintf(stderr, "[fqz dec] n=%u ment=%u sets=%u recs=%u dups=%u revs=%u misses=%u slow=%u\n",
+                         W.total, W.D.ment, W.D.nsets, c[0], c[1], c[2], c[3], c[4]);
+            if (pr[0] | pr[1])
+                std::fprintf(stderr, "[fqz dec] cycles/symbol: wait %.1f chain %.1f coder %.1f update %.1f tail %.1f loop %.1f\n",
+                             double(pr[0]) / W.total, double(pr[1]) / W.total, double(pr[2]) / W.total,
+                             double(pr[3]) / W.total, double(pr[4]) / W.total, double(pr[5]) / W.total);
+        }
+    std::vector<std::vector<uint32_t>> lens(live.size());
+    for (size_t i = 0; i < live.size(); i++) {
+        FqzDecReq &R = *live[i];
+        if (R.w->st) continue;
+        lens[i].resize(R.w->D.nlengths);
+        g.download(lens[i].data(), R.w->D.lengths, lens[i].size());
+    }
+    g.sync();
+    for (size_t i = 0; i < live.size(); i++) {
+        FqzDecReq &R = *live[i];
+        if (R.w->st) continue;
+        for (size_t r = 0; r < lens[i].size(); r++) R.lengths[r] = int(lens[i][r]);
+        R.ok = true;
+    }
 }
 
 uint8_t *fqz_decode_gpu(const uint8_t *in, size_t in_size, size_t *out_size, int *lengths,
                         int nlengths, fqz_slice *s) {
     GpuCtx &g = gpu();
-    uint32_t total = 0;
-    size_t k = size_t(varint_get(in, in + in_size, &total));
-    *out_size = total;
-    Global G;
-    const int u = get_params(G, in + k, in_size - k);
-    if (u < 0) return nullptr;
-    k += size_t(u);
     g.reset();
-    const FqzDevGlobal dg = dev_params(G);
-    FqzDecJob D{};
-    D.g = g.upload(&dg, 1);
-    D.in = g.upload(in + k, in_size - k);
-    D.in_len = in_size - k;
-    D.n = total;
-    const int nrec = s ? s->num_records : 0;
-    if (s && s->seq && nrec > 0 && s->len) {
-        unsigned boff = 0;
-        for (const Param &pm : G.p) boff = std::max(boff, pm.boff);
-        gather_seq(g, s->seq, nrec, s->len, boff, &D.seq, &D.seq_off);
-        D.nseq = uint32_t(nrec);
+    std::vector<FqzDecReq> reqs(1);
+    FqzDecReq &R = reqs[0];
+    R.h_in = in;
+    R.d_in = g.upload(in, in_size);
+    R.in_size = in_size;
+    R.lengths = lengths;
+    R.nlengths = nlengths;
+    if (s && s->seq && s->num_records > 0 && s->len) {
+        R.nrec = s->num_records;
+        R.lens = s->len;
+        R.h_seq = s->seq;
     }
-    D.nlengths = lengths && nlengths > 0 ? uint32_t(nlengths) : 0;
-    D.lengths = g.arena.alloc_n<uint32_t>(std::max<uint32_t>(D.nlengths, 1));
-    D.out = g.arena.alloc_n<uint8_t>(std::max<uint32_t>(total, 1));
-    D.status = g.arena.alloc_n<int32_t>(1);
-    D.nrec_out = g.arena.alloc_n<uint32_t>(1);
-    D.counts = g.arena.alloc_n<uint32_t>(32);
-    g.memset0(D.counts, 32 * sizeof(uint32_t));
-    const uint32_t live = uint32_t(G.max_sym) + 1;
-    if (live > FQZ_DEC_MAX_LIVE) return nullptr;
-    D.ment = fqz_dec_model_bytes(live);
-    D.nsets = FQZ_DEC_CACHE_BYTES / D.ment;
-    D.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * D.ment);
-    bool seq_ctx = false, dedup = false, map = false, qid = true;
-    for (const Param &pm : G.p) {
-        seq_ctx = seq_ctx || pm.bbits > 0;
-        for (int i = 0; i < 256; i++) qid = qid && (pm.qtab[i] & 0xffffu) == unsigned(i);
-        dedup = dedup || pm.dedup;
-        for (int i = 0; i < 256; i++) map = map || pm.qmap[i] != unsigned(i);
-    }
-    seq_ctx = seq_ctx && D.seq;
-    const bool rev = (G.gflags & GF_REV) != 0;
-    const int map_mode = !map ? 0 : G.nparam > 1 ? 2 : 1;
-    // record lists: sized for the records the caller announced, grown to
-    // the byte count (every record holds at least one byte) on overflow
-    uint32_t cap = std::max<uint32_t>({D.nlengths, D.nseq, 1u}) + 1024;
-    int32_t st = 0;
-    for (int attempt = 0; attempt < 2; attempt++) {
-        D.cap_list = (dedup || rev || map_mode == 2) ? std::min<uint32_t>(cap, total + 1) : 0;
-        const size_t c = std::max<uint32_t>(D.cap_list, 1);
-        D.recs = g.arena.alloc_n<uint4>(map_mode == 2 ? c : 1);
-        D.dups = g.arena.alloc_n<uint2>(dedup ? c : 1);
-        D.revs = g.arena.alloc_n<uint2>(rev ? c : 1);
-        FQZ5_HIP(launch_fqz_dec(D, live + 2 <= 64 ? 1 : 2, seq_ctx, qid, g.stream));
-        FQZ5_HIP(launch_fqz_dec_fix(D, map_mode, dedup, rev, g.stream));
-        g.download(&st, D.status, 1);
-        g.sync();
-        if (st != -2) break;
-        cap = total + 1;
-    }
-    if (std::getenv("FQZ5_DEBUG")) {
-        uint32_t c[5];
-        g.download(c, D.counts, 5);
-        g.sync();
-        std::fprintf(stderr, "[fqz dec] n=%u live=%u ment=%u sets=%u recs=%u dups=%u revs=%u misses=%u slow=%u\n",
-                     total, live, D.ment, D.nsets, c[0], c[1], c[2], c[3], c[4]);
-        uint64_t pr[6];
-        g.download(pr, reinterpret_cast<const uint64_t *>(D.counts + 8), 6);
-        g.sync();
-        if (pr[0] | pr[1])
-            std::fprintf(stderr, "[fqz dec] cycles/symbol: wait %.1f chain %.1f coder %.1f update %.1f tail %.1f loop %.1f\n",
-                         double(pr[0]) / total, double(pr[1]) / total, double(pr[2]) / total,
-                         double(pr[3]) / total, double(pr[4]) / total, double(pr[5]) / total);
-    }
-    if (st) return nullptr;
-    uint8_t *out = static_cast<uint8_t *>(std::malloc(total ? total : 1));
+    fqz_decode_batch(g, reqs);
+    *out_size = R.out_size;
+    if (!R.ok) return nullptr;
+    uint8_t *out = static_cast<uint8_t *>(std::malloc(R.out_size ? R.out_size : 1));
     if (!out) throw std::runtime_error("fqz: out of host memory");
-    g.download(out, D.out, total);
-    std::vector<uint32_t> lens(D.nlengths);
-    g.download(lens.data(), D.lengths, lens.size());
+    g.download(out, R.d_out, R.out_size);
     g.sync();
-    for (uint32_t r = 0; r < D.nlengths; r++) lengths[r] = int(lens[r]);
     return out;
 }
 

@@ -227,8 +227,9 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 // sentinel slot L with freq 0 and cum = total; symbol bytes follow.
 // ---------------------------------------------------------------------------
 template <int NE, bool SEQ, bool QID>
-__global__ __launch_bounds__(64) void k_fqz_dec(FqzDecJob J) {
+__global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const FqzDecJob J = Js[blockIdx.x];   // one block of a batch per workgroup
     const uint32_t l = threadIdx.x;
     const FqzDevGlobal &g = *J.g;
     SmallModels &sm = *reinterpret_cast<SmallModels *>(lds + L_SMALL);
@@ -686,22 +687,23 @@ __global__ void k_fqz_div_selftest(uint32_t *bad) {
 
 }  // namespace
 
-template <int NE, bool SEQ, bool QID> static hipError_t launch_dec(const FqzDecJob &j, hipStream_t s) {
+template <int NE, bool SEQ, bool QID>
+static hipError_t launch_dec(const FqzDecJob *j, int n, hipStream_t s) {
     auto *f = k_fqz_dec<NE, SEQ, QID>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(f),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(f, dim3(1), dim3(64), LDS_BYTES, s, j);
+    if (n) hipLaunchKernelGGL(f, dim3(n), dim3(64), LDS_BYTES, s, j);
     return hipGetLastError();
 }
 
-hipError_t launch_fqz_dec(const FqzDecJob &j, int ne, bool seq, bool qid, hipStream_t s) {
+hipError_t launch_fqz_dec(const FqzDecJob *j, int n, int ne, bool seq, bool qid, hipStream_t s) {
     if (ne == 1) {
-        if (seq) return qid ? launch_dec<1, true, true>(j, s) : launch_dec<1, true, false>(j, s);
-        return qid ? launch_dec<1, false, true>(j, s) : launch_dec<1, false, false>(j, s);
+        if (seq) return qid ? launch_dec<1, true, true>(j, n, s) : launch_dec<1, true, false>(j, n, s);
+        return qid ? launch_dec<1, false, true>(j, n, s) : launch_dec<1, false, false>(j, n, s);
     }
-    if (seq) return qid ? launch_dec<2, true, true>(j, s) : launch_dec<2, true, false>(j, s);
-    return qid ? launch_dec<2, false, true>(j, s) : launch_dec<2, false, false>(j, s);
+    if (seq) return qid ? launch_dec<2, true, true>(j, n, s) : launch_dec<2, true, false>(j, n, s);
+    return qid ? launch_dec<2, false, true>(j, n, s) : launch_dec<2, false, false>(j, n, s);
 }
 
 hipError_t launch_fqz_dec_fix(const FqzDecJob &j, int map_mode, bool dups, bool revs, hipStream_t s) {

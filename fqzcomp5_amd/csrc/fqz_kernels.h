@@ -129,9 +129,11 @@ struct FqzEvJob {
 };
 
 hipError_t launch_fqz_events(const FqzEvJob &j, int phase, hipStream_t s);
-hipError_t launch_fqz_model_pass(const FqzEvJob &j, hipStream_t s);
+// batched over the blocks of a request list: d_jobs in device memory
+hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
+hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
+hipError_t launch_fqz_carry(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
 hipError_t launch_fqz_expand(const FqzEvJob &j, hipStream_t s);
-hipError_t launch_fqz_rc(const FqzEvJob &j, hipStream_t s);
 hipError_t launch_fqz_bytes(const FqzEvJob &j, int phase, hipStream_t s);
 // fqz_sort.hip
 hipError_t fqz_exclusive_scan(const uint32_t *in, uint32_t *out, int n, void *tmp, size_t &bytes,
@@ -147,7 +149,8 @@ hipError_t launch_fqz_encode(const FqzEncJob &j, hipStream_t s);
 // fqz_decode.hip: ne = lane registers per model (live + 2 <= 64 ? 1 : 2),
 // seq = sequence bases in the context, qid = identity qtab in every
 // parameter block; map_mode 0 none / 1 one qmap / 2 per record
-hipError_t launch_fqz_dec(const FqzDecJob &j, int ne, bool seq, bool qid, hipStream_t s);
+hipError_t launch_fqz_dec(const FqzDecJob *d_jobs, int njobs, int ne, bool seq, bool qid,
+                          hipStream_t s);
 hipError_t launch_fqz_dec_fix(const FqzDecJob &j, int map_mode, bool dups, bool revs, hipStream_t s);
 hipError_t fqz_div_selftest(uint32_t *d_bad, hipStream_t s);
 

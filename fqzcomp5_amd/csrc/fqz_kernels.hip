@@ -381,9 +381,12 @@ template <int CAP> DEV void model_run(FList<CAP> *m, const FqzEvJob &J, uint32_t
     m->total = tot;
 }
 
-__global__ __launch_bounds__(256) void k_fqz_model_pass(FqzEvJob J) {
+// one launch for a batch of blocks: workgroup b handles models
+// [256 (b % nblk), +256) of block b / nblk
+__global__ __launch_bounds__(256) void k_fqz_model_pass(const FqzEvJob *Js, uint32_t nblk) {
     FList<FQZ_QSYMS> *lm = reinterpret_cast<FList<FQZ_QSYMS> *>(fqz_lds);   // 256 models
-    const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    const FqzEvJob J = Js[blockIdx.x / nblk];
+    const uint32_t m = (blockIdx.x % nblk) * blockDim.x + threadIdx.x;
     if (m >= FQZ_NMODELS) return;
     const uint32_t lo = J.seg_lo[m], hi = J.seg_hi[m];
     if (lo >= hi) return;
@@ -431,7 +434,8 @@ __global__ void k_fqz_expand(FqzEvJob J) {
 // (CDNA's vmcnt counts both).
 constexpr uint32_t RC_BLK = 4096;
 
-__global__ __launch_bounds__(64) void k_fqz_rc(FqzEvJob J) {
+__global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
+    const FqzEvJob J = Js[blockIdx.x];   // one wave per block of a batch
     __shared__ uint4 in[RC_BLK + 8];
     __shared__ uint4 o_q[RC_BLK / 4];
     __shared__ uint2 o_k[RC_BLK / 8];
@@ -504,7 +508,8 @@ __global__ void k_fqz_accum(FqzEvJob J) {
 
 // Phase B: carry propagation through the columns.  The wave loads 64
 // columns at a time; the carry walks them in lane order on scalar registers.
-__global__ __launch_bounds__(64) void k_fqz_carry(FqzEvJob J) {
+__global__ __launch_bounds__(64) void k_fqz_carry(const FqzEvJob *Js) {
+    const FqzEvJob J = Js[blockIdx.x];   // one wave per block of a batch
     const int l = int(threadIdx.x);
     unsigned long long carry = 0;
     for (uint32_t w0 = 0; w0 < J.nwords; w0 += 64) {
@@ -547,29 +552,35 @@ hipError_t launch_fqz_expand(const FqzEvJob &j, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_fqz_model_pass(const FqzEvJob &j, hipStream_t s) {
+hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, hipStream_t s) {
     constexpr uint32_t lds = 256 * sizeof(FList<FQZ_QSYMS>);
+    constexpr uint32_t nblk = (FQZ_NMODELS + 255) / 256;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_fqz_model_pass),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr = true;
     }
-    hipLaunchKernelGGL(k_fqz_model_pass, dim3((FQZ_NMODELS + 255) / 256), dim3(256), lds, s, j);
+    if (njobs)
+        hipLaunchKernelGGL(k_fqz_model_pass, dim3(nblk * uint32_t(njobs)), dim3(256), lds, s,
+                           d_jobs, nblk);
     return hipGetLastError();
 }
 
-hipError_t launch_fqz_rc(const FqzEvJob &j, hipStream_t s) {
-    hipLaunchKernelGGL(k_fqz_rc, dim3(1), dim3(64), 0, s, j);
+hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, hipStream_t s) {
+    if (njobs) hipLaunchKernelGGL(k_fqz_rc, dim3(njobs), dim3(64), 0, s, d_jobs);
     return hipGetLastError();
 }
 
-// phase 0: columns; 1: carries; 2: bytes (grid from the host's bound)
+hipError_t launch_fqz_carry(const FqzEvJob *d_jobs, int njobs, hipStream_t s) {
+    if (njobs) hipLaunchKernelGGL(k_fqz_carry, dim3(njobs), dim3(64), 0, s, d_jobs);
+    return hipGetLastError();
+}
+
+// phase 0: columns; 2: bytes (grid from the host's bound); carries: launch_fqz_carry
 hipError_t launch_fqz_bytes(const FqzEvJob &j, int phase, hipStream_t s) {
     if (phase == 0 && j.nev)
         hipLaunchKernelGGL(k_fqz_accum, dim3((j.nev + 255) / 256), dim3(256), 0, s, j);
-    else if (phase == 1)
-        hipLaunchKernelGGL(k_fqz_carry, dim3(1), dim3(64), 0, s, j);
     else if (phase == 2)
         hipLaunchKernelGGL(k_fqz_emit, dim3((4 * j.nwords + 255) / 256), dim3(256), 0, s, j);
     return hipGetLastError();

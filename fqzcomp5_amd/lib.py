@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfqz5_mi355x.so")
@@ -45,6 +46,12 @@ def load() -> C.CDLL:
     if _lib is not None:
         return _lib
     path = os.environ.get("FQZ5_LIB_VARIANT") or LIB_PATH   # tools/build_variant.sh
+    # torch bundles its own HIP runtime: when the caller uses torch, its
+    # runtime must own the device before this library's runtime starts
+    if "torch" in sys.modules:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
     if not os.path.exists(path):
         raise NativeError(f"{path} missing: run __graft_entry__.build()")
     lib = C.CDLL(path)

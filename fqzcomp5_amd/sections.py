@@ -26,21 +26,31 @@ M_LAST = 31
 SEC_SEQ, SEC_QUAL = 2, 3
 RANS0, RANS1, RANS64, RANS65, RANS128, RANS129, RANS192, RANS193, RANSXN1 = range(1, 10)
 LZP3 = 10
+FQZ0, FQZ1, FQZ2, FQZ3, FQZ4 = range(26, 31)
+RANS_MASK = sum(1 << m for m in range(RANS0, RANSXN1 + 1))
+FQZ_MASK = sum(1 << m for m in range(FQZ0, FQZ4 + 1))
 
 # Method masks of the level presets (fqzcomp5.c:4886-4932) restricted to the
-# rANS methods this build implements (LZP3 is the next row).
+# methods this build implements: rANS and fqzcomp_qual.  LZP3 and the
+# sequence context models (SEQ10/SEQ12B) are the next rows.
 LEVEL_MASKS = {
     1: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193],
         SEC_QUAL: [RANS0, RANS1, RANS129, RANS193]},
     3: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193],
         SEC_QUAL: [RANS0, RANS1, RANS129, RANS193, RANSXN1]},
+    5: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193],
+        SEC_QUAL: [RANS0, RANS1, RANS129, RANS193, RANSXN1, FQZ1, FQZ3]},
 }
 
 
 class Section(C.Structure):
+    """fqz5_section; the record fields are needed by the FQZ methods only
+    (host lengths / flags, the block's device sequence bytes)."""
     _fields_ = [("in_", C.c_void_p), ("out", C.c_void_p),
                 ("in_size", C.c_uint32), ("out_cap", C.c_uint32),
-                ("fixed_len", C.c_uint32), ("sec", C.c_int32)]
+                ("fixed_len", C.c_uint32), ("sec", C.c_int32),
+                ("rec_len", C.POINTER(C.c_uint32)), ("rec_flags", C.POINTER(C.c_uint32)),
+                ("nrec", C.c_int32), ("seq", C.c_void_p)]
 
 
 class SectionResult(C.Structure):
@@ -216,12 +226,17 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
     once at commit, for candidates that do cost in proportion to their work."""
     ins = np.array([s.in_size for s in secs], np.uint32)
     ids = np.array([s.sec for s in secs], np.int32)
-    if speculate:
-        masks = np.asarray(avail, np.uint32)[ids]
+    av = np.asarray(avail, np.uint32)
+    if speculate and not (av & FQZ_MASK).any():
+        masks = av[ids]
     else:
         blank = np.zeros((len(secs), M_LAST), np.uint32)
         _, _, g_ids0, off = exchange_sizes(blank, ins, ids, group)
-        masks = trial_schedule(g_ids0, avail, state)[off:off + len(secs)]
+        sched = trial_schedule(g_ids0, avail, state)[off:off + len(secs)]
+        # rANS candidates stay speculative (chain-bound, nearly free in one
+        # launch); fqz candidates cost in proportion to their work, so only
+        # the scheduled trial sections try them
+        masks = (av[ids] & RANS_MASK) | (sched & FQZ_MASK) if speculate else sched
     local = sections_try(secs, masks)
     g_sizes, g_ins, g_ids, off = exchange_sizes(local, ins, ids, group)
     tried = np.zeros(len(g_ids), np.uint32)
@@ -229,3 +244,86 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
     meth = meth_all[off:off + len(secs)]
     res = sections_commit(secs, meth)
     return res, meth_all, g_sizes, tried, off
+
+
+def fqz_bound(n: int) -> int:
+    """Room the fqz encoder needs: the coder's bound (fqz_codec.cpp) plus
+    the parameter header."""
+    return int(n * 1.1) + 100000 + 16384
+
+
+class Run:
+    """Device buffers and sections of a run of blocks in file order, each
+    block a sequence then a quality section (encode_block order).  The
+    quality sections carry the records (FQZ methods) and point at their
+    block's sequence bytes: the input when encoding, the decoded sequence
+    section when decoding."""
+
+    def __init__(self, reads, blocks, device):
+        import torch
+        self.reads, self.blocks = reads, blocks
+        offs = np.concatenate([[0], np.cumsum(reads.lens.astype(np.int64))])
+        self.seq_d = torch.from_numpy(reads.seq).to(device)
+        self.qual_d = torch.from_numpy(reads.qual).to(device)
+        self.spans, self.lens = [], []
+        for a, b in blocks:
+            s, e = int(offs[a]), int(offs[b])
+            ln = np.ascontiguousarray(reads.lens[a:b], np.uint32)
+            fl = int(ln[0]) if len(ln) and bool(np.all(ln == ln[0])) else 0
+            self.lens.append(ln)
+            self.spans.append((SEC_SEQ, s, e, fl, len(self.lens) - 1))
+            self.spans.append((SEC_QUAL, s, e, fl, len(self.lens) - 1))
+        caps = []
+        for sec, s, e, fl, _ in self.spans:
+            n = e - s
+            caps.append(9 + max(max(_lib.compress_bound(n, o) for o in
+                                    (0, 1, 64, 65, 128, 129, 192, 193, (fl << 8) + 9)),
+                                fqz_bound(n)))
+        self.enc_buf = torch.empty(sum(caps), dtype=torch.uint8, device=device)
+        self.dec_buf = torch.empty(sum(e - s for _, s, e, _, _ in self.spans),
+                                   dtype=torch.uint8, device=device)
+        self.enc, self.dec = [], []
+        eo = do = 0
+        for (sec, s, e, fl, k), cap in zip(self.spans, caps):
+            self.enc.append((eo, cap))
+            self.dec.append(do)
+            eo += cap
+            do += e - s
+        self.in_bytes = sum(e - s for _, s, e, _, _ in self.spans)
+
+    def _rec(self, k):
+        ln = self.lens[k]
+        return ln.ctypes.data_as(C.POINTER(C.c_uint32)), len(ln)
+
+    def enc_secs(self) -> list[Section]:
+        out = []
+        for (sec, s, e, fl, k), (eo, cap) in zip(self.spans, self.enc):
+            src = self.seq_d if sec == SEC_SEQ else self.qual_d
+            rl, nr = self._rec(k)
+            out.append(Section(src.data_ptr() + s, self.enc_buf.data_ptr() + eo, e - s, cap,
+                               fl, sec, rl, None, nr,
+                               self.seq_d.data_ptr() + s if sec == SEC_QUAL else None))
+        return out
+
+    def dec_secs(self, res) -> list[Section]:
+        out = []
+        for i, ((sec, s, e, fl, k), (eo, cap), do, r) in enumerate(
+                zip(self.spans, self.enc, self.dec, res)):
+            rl, nr = self._rec(k)
+            seq = self.dec_buf.data_ptr() + self.dec[i - 1] if sec == SEC_QUAL else None
+            out.append(Section(self.enc_buf.data_ptr() + eo, self.dec_buf.data_ptr() + do,
+                               9 + r.clen, e - s, 0, sec, rl, None, nr, seq))
+        return out
+
+    def chosen(self, res, i) -> bytes:
+        """The i-th section's chosen stream (without the 9-byte frame)."""
+        eo, _ = self.enc[i]
+        return self.enc_buf[eo + 9:eo + 9 + res[i].clen].cpu().numpy().tobytes()
+
+    def roundtrip_ok(self) -> bool:
+        import torch
+        ok = True
+        for (sec, s, e, _, _), do in zip(self.spans, self.dec):
+            src = self.seq_d if sec == SEC_SEQ else self.qual_d
+            ok = ok and bool(torch.equal(self.dec_buf[do:do + e - s], src[s:e]))
+        return ok

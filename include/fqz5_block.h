@@ -9,8 +9,9 @@
  * [strat u8][u32 usize][u32 csize][stream] (fqzcomp5.c:2217-2257).
  * A caller hands over a run of blocks at once; the choices equal those of a
  * single-threaded reference run over the same blocks in the same order.
- * This build implements the rANS methods (RANS0..RANS193, RANSXN1); masks
- * with LZP/tok3/seq-CM/fqz bits are rejected.
+ * This build implements the rANS methods (RANS0..RANS193, RANSXN1) and the
+ * fqzcomp_qual methods FQZ0..FQZ4 (quality sections, strat byte 1); masks
+ * with LZP/tok3/seq-CM bits are rejected.
  */
 #ifndef FQZ5_BLOCK_H
 #define FQZ5_BLOCK_H
@@ -47,6 +48,13 @@ typedef struct {                  /* one section of one block (device data) */
     uint32_t out_cap;
     uint32_t fixed_len;           /* fq->fixed_len (0 = variable) */
     int32_t sec;                  /* FQZ5_SEC_SEQ or FQZ5_SEC_QUAL */
+    /* records of the block, for the FQZ methods (fqzcomp5.c:2071-2092):
+     * host lengths and flags (flags may be NULL), and the block's sequence
+     * bytes on the device, records back to back (NULL: no sequence) */
+    const uint32_t *rec_len;
+    const uint32_t *rec_flags;
+    int32_t nrec;
+    const uint8_t *seq;
 } fqz5_section;
 
 typedef struct {

@@ -11,6 +11,13 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line(
         "markers", "gpu: needs an MI355X (run on the GPU box via gpurun)")
+    # torch's wheel bundles its own HIP runtime next to the one the library
+    # links (/opt/rocm): whichever initialises the device second still works
+    # only if torch went first, so sessions start torch's runtime before
+    # any test loads the library (a no-op without a GPU)
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
 
 
 @pytest.fixture(scope="session")

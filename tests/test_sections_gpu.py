@@ -1,0 +1,65 @@
+"""The section coder on the GPU (include/fqz5_block.h) at -3 and -5: the
+codec trial over a run of blocks, every chosen stream byte-equal to the
+reference's codec for that method (oracle/_ref when built, else the oracle
+restatement), and every section decoded back.  -5 adds the FQZ1/FQZ3
+quality methods: trial blocks try them, later blocks are encoded with the
+chosen method at commit."""
+import numpy as np
+import torch
+import pytest
+
+from fqzcomp5_amd import lib, sections as S, synth
+from oracle import binding
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not lib.device_ok():
+        pytest.fail("no GPU: " + lib.last_error())
+
+
+def _order(m, fl):
+    return [0, 1, 64, 65, 128, 129, 192, 193][m - 1] if m <= 8 else (fl << 8) + 9
+
+
+# fqz beats rANS on the random-walk (Illumina) qualities from ~2 MB blocks
+# on; on i.i.d. NovaSeq qualities rANS O0 stays ahead at every size
+@pytest.mark.parametrize("level,kind,nreads,blk", [(3, "illumina", 6000, 200_000),
+                                                   (5, "novaseq", 6000, 200_000),
+                                                   (5, "illumina", 72000, 4_000_000)])
+def test_run_vs_reference(level, kind, nreads, blk):
+    codec = binding.ref() if binding.have_ref() else binding.oracle()
+    reads = (synth.novaseq if kind == "novaseq" else synth.illumina)(nreads, seed=11)
+    blocks = synth.split_blocks(reads, blk)
+    assert len(blocks) >= 5
+    run = S.Run(reads, blocks, torch.device("cuda", 0))
+    res, meth_all, _, tried, _ = S.encode_run(run.enc_secs(), S.masks(level), S.new_state())
+    assert all(r.status == 0 for r in res)
+    offs = np.concatenate([[0], np.cumsum(reads.lens.astype(np.int64))])
+    used = set()
+    for i, ((sec, s, e, fl, k), r) in enumerate(zip(run.spans, res)):
+        m = int(meth_all[i])
+        used.add(m)
+        data = (reads.seq if sec == S.SEC_SEQ else reads.qual)[s:e].tobytes()
+        if m >= S.FQZ0:
+            a, b = blocks[k]
+            exp = codec.fqz_compress(data, reads.lens[a:b].copy(), np.zeros(b - a, np.uint32),
+                                     m - S.FQZ0, reads.seq[s:e].tobytes())
+            assert r.strat == 1
+        else:
+            exp = codec.rans_compress(data, _order(m, fl))
+            assert r.strat == 0
+        assert run.chosen(res, i) == exp, (i, m)
+    if level == 5:
+        fqz_bits = (1 << S.FQZ1) | (1 << S.FQZ3)
+        assert all(int(t) & fqz_bits for t, (sec, *_) in zip(tried[:6], run.spans)
+                   if sec == S.SEC_QUAL)            # the trial blocks tried fqz
+        if kind == "illumina":                      # random-walk qualities: fqz wins
+            assert used & {S.FQZ1, S.FQZ3}, used
+    dres = S.decode(run.dec_secs(res))
+    assert all(r.status == 0 for r in dres)
+    torch.cuda.synchronize()
+    assert run.roundtrip_ok()
+    del offs

@@ -119,6 +119,33 @@ __global__ void k(uint32_t *out, uint64_t *cyc, uint32_t a, uint32_t b) {
             q += (x - q * (y | 1)) >= (y | 1);
             x = q + 12345;
         }
+        if (T == 17) {                                           // ballot -> popc -> readlane -> SALU
+            const uint64_t m = __ballot(x > y);
+            const uint32_t k = uint32_t(__popcll(m)) & 63u;
+            y = __builtin_amdgcn_readlane(x, k) + 1u;
+        }
+        if (T == 18) {                                           // LDS read -> readlane -> address
+            const uint32_t v = lds[(y + l) & 4095];
+            y = __builtin_amdgcn_readlane(v, 0) & 4095u;
+        }
+        if (T == 19) {                                           // LDS write then dependent read
+            lds[(y + l) & 4095] = x;
+            x = lds[(y + l + 1) & 4095] + 1u;
+            y = __builtin_amdgcn_readfirstlane(x) & 4095u;
+        }
+        if (T == 20) {                                           // recip: cvt, rcp, 2 fma, use
+            const double d = double(x | 1u);
+            const double r0 = __builtin_amdgcn_rcp(d);
+            const double e = __fma_rn(-d, r0, 1.0);
+            x = uint32_t(__fma_rn(r0, e, r0) * 1e9);
+        }
+        if (T == 21) {                                           // model step skeleton, no LDS
+            const uint64_t m = __ballot(x * 3u <= y) & 0x3eull;
+            const uint32_t k = uint32_t(__popcll(m));
+            const uint32_t pk = __builtin_amdgcn_readlane(x, k), pk1 = __builtin_amdgcn_readlane(x, k + 1);
+            y = (y - pk) + (pk1 - pk);
+            x += l > k ? 0x100000u : (l == k ? 16u : 0u);
+        }
         if (T == 11) {                                           // dec: table lookup + arith only
             const uint32_t e = lds[x & 4095];
             const uint32_t xh = x >> 12;
@@ -165,5 +192,10 @@ int main() {
     run<14>("mul_lo u32 + add dep");
     run<15>("fqz range step");
     run<16>("f32 rcp div + 1 fix");
+    run<17>("ballot->popc->readlane->s");
+    run<18>("LDS rd->readlane->addr");
+    run<19>("LDS wr + dep rd + rfl");
+    run<20>("f64 recip (rcp+2fma)+use");
+    run<21>("ballot/readlane step");
     return 0;
 }
