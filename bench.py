@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
-"""Benchmark: fqzcomp5 -3 sequence+quality section coding on MI355X.
+"""Benchmark: fqzcomp5 sequence+quality section coding on MI355X.
 
-Metric (BASELINE.json): input MB/s encode+decode, 100 MB blocks, -3;
-bit-exact vs CPU.  Workload (configs[1]): a synthetic 1 GB Illumina 150 bp
-FASTQ with 8-level binned qualities, split into 100 MB blocks by the
-reference's record rule (fqzcomp5.c:471-477).  One step is one pass of the
-hot path over the whole workload, inputs resident in HBM:
+Metric (BASELINE.json): input MB/s encode+decode, 100 MB blocks, -3 and -5;
+bit-exact vs CPU.  Default workload (configs[1]): a synthetic 1 GB Illumina
+150 bp FASTQ with 8-level binned qualities at -3, split into 100 MB blocks
+by the reference's record rule (fqzcomp5.c:471-477).  `--level 5 --kind
+novaseq --gb 4` is configs[2] (the quality methods add FQZ1/FQZ3).  One step
+is one pass of the hot path over the whole workload, inputs resident in HBM:
 
-    encode  every block's seq and qual section with the -3 rANS method sets
+    encode  every block's seq and qual section with the level's method sets
             and the codec-trial state machine (fqzcomp5.c:1899-2144)
     decode  every chosen stream back to bytes.
 
@@ -46,10 +47,10 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def make_blocks(gb: float, seed: int):
+def make_blocks(gb: float, seed: int, kind: str):
     from fqzcomp5_amd import synth
     n_reads = int(gb * 1e9 / FASTQ_REC)
-    r = synth.illumina(n_reads, seed=seed)
+    r = (synth.novaseq if kind == "novaseq" else synth.illumina)(n_reads, seed=seed)
     return r, synth.split_blocks(r, BLK)
 
 
@@ -72,37 +73,57 @@ def method_order(m: int, fixed_len: int) -> int:
     return [0, 1, 64, 65, 128, 129, 192, 193][m - 1] if m <= 8 else (fixed_len << 8) + 9
 
 
-def cpu_baseline(host_secs, tried, meth, gpu_out, threads):
+def cpu_baseline(run, tried, meth, gpu_out, threads):
     """The reference (oracle/_ref) on the same sections and schedule: every
     tried method of every section is compressed, the chosen stream is
     checked against the GPU's bytes and decoded again."""
     from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
     from oracle import binding
+    from fqzcomp5_amd import sections as S
     kind = "reference" if binding.have_ref() else "port"
     codec = binding.ref() if kind == "reference" else binding.oracle()
+    reads = run.reads
+    secs = []
+    for sec, s, e, fl, k in run.spans:
+        arr = reads.seq if sec == S.SEC_SEQ else reads.qual
+        a, b = run.blocks[k]
+        secs.append((arr[s:e].tobytes(), fl, reads.lens[a:b].copy(),
+                     reads.seq[s:e].tobytes()))
 
     def enc(i):
-        data, fixed = host_secs[i]
+        data, fixed, lens, seq = secs[i]
         best = None
-        for m in range(1, 31):
-            if tried[i] & (1 << m) and (m != 9 or fixed):
+        for m in range(1, S.M_LAST):
+            if not tried[i] & (1 << m) or (m == S.RANSXN1 and not fixed):
+                continue
+            if m >= S.FQZ0:
+                out = codec.fqz_compress(data, lens.copy(), np.zeros(len(lens), np.uint32),
+                                         m - S.FQZ0, seq)
+            else:
                 out = codec.rans_compress(data, method_order(m, fixed))
-                if m == meth[i]:
-                    best = out
+            if m == meth[i]:
+                best = out
         return best
+
+    def dec(i):
+        data, fixed, lens, seq = secs[i]
+        if meth[i] >= S.FQZ0:
+            return codec.fqz_decompress(chosen[i], lens.copy(), np.zeros(len(lens), np.uint32), seq)
+        return codec.rans_uncompress(chosen[i])
 
     with ThreadPoolExecutor(threads) as ex:
         t0 = time.perf_counter()
-        chosen = list(ex.map(enc, range(len(host_secs))))
+        chosen = list(ex.map(enc, range(len(secs))))
         t1 = time.perf_counter()
-        back = list(ex.map(codec.rans_uncompress, chosen))
+        back = list(ex.map(dec, range(len(secs))))
         t2 = time.perf_counter()
     same = all(c == g for c, g in zip(chosen, gpu_out))
-    rt = all(b == h[0] for b, h in zip(back, host_secs))
-    nbytes = sum(len(h[0]) for h in host_secs)
+    rt = all(b == h[0] for b, h in zip(back, secs))
+    nbytes = sum(len(h[0]) for h in secs)
     return {"value": round(nbytes / (t2 - t0) / 1e6, 2), "unit": "MB/s",
             "cores": threads, "kind": kind,
-            "sample": f"all {len(host_secs)} seq+qual sections of the rank-0 "
+            "sample": f"all {len(secs)} seq+qual sections of the rank-0 "
                       f"workload, the -t1 trial schedule (every tried "
                       f"candidate encoded), {threads} host threads",
             "enc_s": round(t1 - t0, 3), "dec_s": round(t2 - t1, 3),
@@ -115,7 +136,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--gb", type=float, default=1.0)
-    ap.add_argument("--level", type=int, default=3)
+    ap.add_argument("--level", type=int, default=3, choices=[1, 3, 5])
+    ap.add_argument("--kind", default="illumina", choices=["illumina", "novaseq"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
@@ -134,43 +156,18 @@ def main():
         raise SystemExit("no GPU: " + lib.last_error())
 
     t0 = time.time()
-    reads, blocks = make_blocks(args.gb, seed=1 + rank)
+    reads, blocks = make_blocks(args.gb, seed=1 + rank, kind=args.kind)
     log(f"[bench] generated {len(blocks)} blocks/rank in {time.time()-t0:.1f}s")
-    fixed = reads.fixed_len
-    offs = np.concatenate([[0], np.cumsum(reads.lens.astype(np.int64))])
     dev = torch.device("cuda", local)
-    seq_d = torch.from_numpy(reads.seq).to(dev)
-    qual_d = torch.from_numpy(reads.qual).to(dev)
-
-    # sections in file order: per block seq then qual (encode_block order)
-    spans = []
-    for a, b in blocks:
-        s, e = int(offs[a]), int(offs[b])
-        fl = int(reads.lens[a]) if np.all(reads.lens[a:b] == reads.lens[a]) else 0
-        spans.append((S.SEC_SEQ, s, e, fl))
-        spans.append((S.SEC_QUAL, s, e, fl))
-    caps = [9 + max(lib.compress_bound(e - s, method_order(m, fl))
-                    for m in range(1, 10)) for _, s, e, fl in spans]
-    enc_buf = torch.empty(sum(caps), dtype=torch.uint8, device=dev)
-    dec_buf = torch.empty(sum(e - s for _, s, e, _ in spans), dtype=torch.uint8, device=dev)
-    enc_secs, dec_out = [], []
-    eo = do = 0
-    for (sec, s, e, fl), cap in zip(spans, caps):
-        src = seq_d if sec == S.SEC_SEQ else qual_d
-        enc_secs.append(S.Section(src.data_ptr() + s, enc_buf.data_ptr() + eo,
-                                  e - s, cap, fl, sec))
-        dec_out.append((dec_buf.data_ptr() + do, e - s, eo, cap))
-        eo += cap
-        do += e - s
+    run = S.Run(reads, blocks, dev)
+    enc_secs = run.enc_secs()
     avail = S.masks(args.level)
-    in_bytes_local = sum(e - s for _, s, e, _ in spans)
+    in_bytes_local = run.in_bytes
 
     def step():
         state = S.new_state()
         res, meth_all, sizes, tried, off = S.encode_run(enc_secs, avail, state)
-        dsecs = [S.Section(enc_buf.data_ptr() + eo_, dp, 9 + r.clen, n, 0, es.sec)
-                 for (dp, n, eo_, cap), r, es in zip(dec_out, res, enc_secs)]
-        dres = S.decode(dsecs)
+        dres = S.decode(run.dec_secs(res))
         return res, dres, meth_all, tried, off
 
     for _ in range(args.warmup):
@@ -199,10 +196,9 @@ def main():
 
     # ---- correctness: every decoded section equals its input -------------
     ok = all(r.status == 0 for r in res) and all(r.status == 0 for r in dres)
-    for (sec, s, e, _), (dp, n, _, _) in zip(spans, dec_out):
-        src = seq_d if sec == S.SEC_SEQ else qual_d
-        ok = ok and bool(torch.equal(dec_buf[dp - dec_buf.data_ptr():][:n], src[s:e]))
+    ok = ok and run.roundtrip_ok()
     comp_bytes = sum(9 + r.clen for r in res)
+    quals = "8-level binned quals" if args.kind == "illumina" else "NovaSeq 4-level i.i.d. quals"
 
     out = {
         "metric": "input MB/s encode+decode, 100MB blocks, -3 and -5; bit-exact vs CPU",
@@ -216,7 +212,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded Illumina 150 bp, 8-level binned quals)",
+        "data": f"synthetic (seeded {args.kind} 150 bp, {quals})",
         "config": {"workload": f"fqzcomp5 -{args.level} seq+qual sections of a "
                                f"{args.gb:g} GB FASTQ per GPU, 100 MB blocks",
                    "blocks_per_gpu": len(blocks), "level": args.level,
@@ -237,7 +233,7 @@ def main():
     traffic, tsrc = pmc_traffic(name)
     # the decode launch is bound by its longest rANS chain: one step = one
     # symbol on each of the 4 interleaved states
-    longest = max((e - s) for _, s, e, _ in spans)
+    longest = max((e - s) for _, s, e, _, _ in run.spans)
     out["roofline"] = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 6),
                        "traffic": traffic, "traffic_source": tsrc, "kernel": name,
@@ -245,24 +241,16 @@ def main():
                        "bytes_per_launch": int(b / max(n, 1)),
                        "enc_avg_ms": round(enc_ms / max(enc_n, 1), 3),
                        "dec_avg_ms": round(dec_ms / max(dec_n, 1), 3),
-                       "chains": {"streams_per_launch": len(spans),
+                       "chains": {"streams_per_launch": len(run.spans),
                                   "longest_stream_steps": longest // 4,
                                   "dec_ns_per_step_longest": round(
                                       dec_ms / max(dec_n, 1) * 1e6 / max(longest // 4, 1), 2)}}
     # ---- CPU baseline (rank 0, N=1) -----------------------------------------
     if rank == 0 and world == 1 and not args.no_cpu:
-        host_secs = []
-        for sec, s, e, fl in spans:
-            arr = reads.seq if sec == S.SEC_SEQ else reads.qual
-            host_secs.append((arr[s:e].tobytes(), fl))
-        gpu_streams = []
-        enc_host = enc_buf.cpu().numpy()
-        for (dp, n, eo_, cap), r in zip(dec_out, res):
-            gpu_streams.append(enc_host[eo_ + 9:eo_ + 9 + r.clen].tobytes())
+        gpu_streams = [run.chosen(res, i) for i in range(len(res))]
         threads = min(args.cpu_threads, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(host_secs, tried[off:off + len(spans)],
-                                           meth_all[off:off + len(spans)],
-                                           gpu_streams, threads)
+        out["cpu_baseline"] = cpu_baseline(run, tried[off:off + len(res)],
+                                           meth_all[off:off + len(res)], gpu_streams, threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
