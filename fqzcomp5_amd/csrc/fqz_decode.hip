@@ -209,8 +209,8 @@ struct PS {
 
 DEV PS load_ps(const FqzDevGlobal &g, uint32_t x) {
     const FqzDevParam &p = g.p[x];
-    return PS{x, p.ctx0, p.qshift, p.qloc, p.qmask, p.sloc, p.bbits, p.bloc, p.boff, p.sel, p.dedup,
-              p.fixed};
+    return PS{x, U(p.ctx0), U(p.qshift), U(p.qloc), U(p.qmask), U(p.sloc), U(p.bbits), U(p.bloc),
+              U(p.boff), U(p.sel), U(p.dedup), U(p.fixed)};
 }
 
 // cache set of a context: multiplicative hash with 24-bit multiplies
@@ -229,12 +229,12 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 template <int NE, bool SEQ, bool QID>
 __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const FqzDecJob J = Js[blockIdx.x];   // one block of a batch per workgroup
+    const FqzDecJob J = load_job(Js + blockIdx.x);   // one block of a batch per workgroup
     const uint32_t l = threadIdx.x;
     const FqzDevGlobal &g = *J.g;
     SmallModels &sm = *reinterpret_cast<SmallModels *>(lds + L_SMALL);
-    const uint32_t gfl = g.gflags, nparam = g.nparam;
-    const uint32_t L = g.max_sym + 1;                 // live symbols per quality model
+    const uint32_t gfl = U(g.gflags), nparam = U(g.nparam);
+    const uint32_t L = U(g.max_sym) + 1;              // live symbols per quality model
     const uint32_t ME = J.ment, NS = J.nsets, NS8 = NS << 8;
     const uint32_t soff = 4u * (L + 2u);              // symbol bytes within a model
     const uint32_t n = uint32_t(J.n);
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     for (int b = 0; b < 4; b++) small_init(&sm.len[b], 256);
     small_init(&sm.rev, 2);
     small_init(&sm.dup, 2);
-    if (g.max_sel > 0) small_init(&sm.sel, int(g.max_sel) + 1);
+    if (U(g.max_sel) > 0) small_init(&sm.sel, int(U(g.max_sel)) + 1);
     for (uint32_t x = 0; x < nparam; x++) {
         uint16_t *pt = reinterpret_cast<uint16_t *>(lds + L_PAR + x * PBYTES);
         for (uint32_t i = l; i < 256; i += 64) pt[(P_QTAB >> 1) + i] = uint16_t(g.p[x].qtab[i]);
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             if (fill == OBUF) flush();
             const uint32_t i = obase + fill;
             sel = (ps.sel || (gfl & 1u)) ? small_decode(&sm.sel, lds, in, rng, code) : 0u;
-            const uint32_t x = (gfl & 2u) ? g.stab[sel < 255u ? sel : 255u] : sel;
+            const uint32_t x = (gfl & 2u) ? U(g.stab[sel < 255u ? sel : 255u]) : sel;
             if (x >= nparam) { status = -1; break; }
             ps = load_ps(g, x);
             uint32_t len = prev_len;

@@ -385,7 +385,7 @@ template <int CAP> DEV void model_run(FList<CAP> *m, const FqzEvJob &J, uint32_t
 // [256 (b % nblk), +256) of block b / nblk
 __global__ __launch_bounds__(256) void k_fqz_model_pass(const FqzEvJob *Js, uint32_t nblk) {
     FList<FQZ_QSYMS> *lm = reinterpret_cast<FList<FQZ_QSYMS> *>(fqz_lds);   // 256 models
-    const FqzEvJob J = Js[blockIdx.x / nblk];
+    const FqzEvJob J = load_job(Js + blockIdx.x / nblk);
     const uint32_t m = (blockIdx.x % nblk) * blockDim.x + threadIdx.x;
     if (m >= FQZ_NMODELS) return;
     const uint32_t lo = J.seg_lo[m], hi = J.seg_hi[m];
@@ -435,7 +435,7 @@ __global__ void k_fqz_expand(FqzEvJob J) {
 constexpr uint32_t RC_BLK = 4096;
 
 __global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
-    const FqzEvJob J = Js[blockIdx.x];   // one wave per block of a batch
+    const FqzEvJob J = load_job(Js + blockIdx.x);   // one wave per block of a batch
     __shared__ uint4 in[RC_BLK + 8];
     __shared__ uint4 o_q[RC_BLK / 4];
     __shared__ uint2 o_k[RC_BLK / 8];
@@ -509,7 +509,7 @@ __global__ void k_fqz_accum(FqzEvJob J) {
 // Phase B: carry propagation through the columns.  The wave loads 64
 // columns at a time; the carry walks them in lane order on scalar registers.
 __global__ __launch_bounds__(64) void k_fqz_carry(const FqzEvJob *Js) {
-    const FqzEvJob J = Js[blockIdx.x];   // one wave per block of a batch
+    const FqzEvJob J = load_job(Js + blockIdx.x);   // one wave per block of a batch
     const int l = int(threadIdx.x);
     unsigned long long carry = 0;
     for (uint32_t w0 = 0; w0 < J.nwords; w0 += 64) {

@@ -11,6 +11,20 @@ namespace fqz5 {
 
 #define DEV __device__ __forceinline__
 
+// A job struct from device memory (one per block of a batched launch), read
+// word by word through readfirstlane: every field is then a scalar register
+// and the compiler keeps the code that depends on it uniform, as with a
+// by-value kernel argument.
+template <class T> DEV T load_job(const T *p) {
+    static_assert(sizeof(T) % 4 == 0, "job size");
+    T v;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(p);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(&v);
+#pragma unroll
+    for (unsigned i = 0; i < sizeof(T) / 4; i++) dst[i] = __builtin_amdgcn_readfirstlane(src[i]);
+    return v;
+}
+
 // --------------------------------------------------------------------------
 // adaptive frequency lists (c_simple_model.h:63-171)
 // --------------------------------------------------------------------------
