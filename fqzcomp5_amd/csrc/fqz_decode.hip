@@ -533,13 +533,13 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         bool to_slow = false;
         uint32_t done = 0;
         PROBE_START
+        // the first step's reads: model dwords and symbols, the position
+        // and delta table entries (later steps read them at the end of the
+        // step before, or take the speculative read of slot 0's model)
+        issue_model();
+        uint32_t pv = pt16[(P_PTAB >> 1) + (left < 1023u ? left : 1023u)];
+        uint32_t dv = pt16[(P_DTAB >> 1) + (delta < 255u ? delta : 255u)];
         do {
-            // all reads of the step in flight together: model dwords and
-            // symbols, the position and delta table entries
-            const uint32_t pa = (P_PTAB >> 1) + (left < 1023u ? left : 1023u);
-            const uint32_t da = (P_DTAB >> 1) + (delta < 255u ? delta : 255u);
-            issue_model();
-            const uint32_t pv = pt16[pa], dv = pt16[da];
             uint32_t sq = 0;
             if (SEQ) sq = lds[L_SEQ + (tpos - sb0)];
             asm volatile("" ::"v"(v[0]), "v"(s[0]), "v"(pv), "v"(dv), "v"(sq));
@@ -563,6 +563,9 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 cn[r] = ((((qs + qt[r]) & ps.qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1);
                 an[r] = set_addr(cn[r], NS8, ME);
                 p[r] = (v[r] >> 16) * q;
+            }
+#pragma unroll
+            for (int r = 0; r < NE; r++) {
                 const uint64_t bal = __builtin_amdgcn_ballot_w64(p[r] <= code) & (r == 0 ? lm0 : lm1);
                 cnt += __builtin_popcountll(bal);
             }
@@ -601,8 +604,15 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 if (in.vb < 4u) break;
                 ulim = (in.vb - 4u) * 8u;
             }
+            if (done == lim) break;
+            // the next step's reads, in flight while the loop closes (a
+            // speculative read of slot 0's next model measured slower: the
+            // volatile loads that keep it in place are waited for at once)
+            issue_model();
+            pv = pt16[(P_PTAB >> 1) + (left < 1023u ? left : 1023u)];
+            dv = pt16[(P_DTAB >> 1) + (delta < 255u ? delta : 255u)];
             PROBE(5)
-        } while (done != lim);
+        } while (true);
         if (to_slow) slow_symbol();
         if (fill == OBUF) flush();
         if (SEQ && left && tpos - sb0 == SEQB) { sb0 = tpos; stage_seq(); }
