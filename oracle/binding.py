@@ -38,6 +38,7 @@ class _Codec:
     def __init__(self, path: str, prefix: str):
         self.path = path
         self.lib = C.CDLL(path)
+        self._prefix = prefix
         p = prefix
         f = getattr(self.lib, p + "rans_compress_4x16")
         f.restype = C.c_void_p
@@ -59,6 +60,50 @@ class _Codec:
             self._fd.argtypes = [C.c_char_p, C.c_size_t,
                                  C.POINTER(C.c_size_t), C.POINTER(C.c_int),
                                  C.c_int, C.POINTER(FqzSlice)]
+
+    def _arith(self):
+        if getattr(self, "_ac", None) is None:
+            p = self._prefix
+            f = getattr(self.lib, p + "arith_compress_to")
+            f.restype = C.c_void_p
+            f.argtypes = [C.c_char_p, C.c_uint, C.c_void_p, C.POINTER(C.c_uint), C.c_int]
+            self._ac = f
+            g = getattr(self.lib, p + "arith_uncompress_to")
+            g.restype = C.c_void_p
+            g.argtypes = [C.c_char_p, C.c_uint, C.c_void_p, C.POINTER(C.c_uint)]
+            self._au = g
+            b = getattr(self.lib, p + "arith_compress_bound")
+            b.restype = C.c_uint
+            b.argtypes = [C.c_uint, C.c_int]
+            self._ab = b
+        return self._ac, self._au, self._ab
+
+    def arith_compress_bound(self, n: int, order: int) -> int:
+        return int(self._arith()[2](n, order))
+
+    def arith_compress(self, data: bytes, order: int, cap: int | None = None):
+        """arith_compress_to; None when it returns NULL.  cap: caller buffer."""
+        ac, _, _ = self._arith()
+        if cap is None:
+            n = C.c_uint(0)
+            p = ac(bytes(data), len(data), None, C.byref(n), order)
+            return None if not p else self._take(p, n.value)
+        buf = C.create_string_buffer(max(cap, 1))
+        n = C.c_uint(cap)
+        p = ac(bytes(data), len(data), buf, C.byref(n), order)
+        return None if not p else buf.raw[:n.value]
+
+    def arith_uncompress(self, comp: bytes, out_size: int | None = None):
+        """arith_uncompress_to; with out_size a caller buffer of that size."""
+        _, au, _ = self._arith()
+        if out_size is None:
+            n = C.c_uint(0)
+            p = au(bytes(comp), len(comp), None, C.byref(n))
+            return None if not p else self._take(p, n.value)
+        buf = C.create_string_buffer(max(out_size, 1))
+        n = C.c_uint(out_size)
+        p = au(bytes(comp), len(comp), buf, C.byref(n))
+        return None if not p else buf.raw[:n.value]
 
     @staticmethod
     def _take(ptr, n) -> bytes:

@@ -19,6 +19,19 @@ uint8_t *ora_rans_uncompress_to_4x16(uint8_t *in, unsigned int in_size,
                                      uint8_t *out, unsigned int *out_size);
 uint8_t *ora_rans_uncompress_4x16(uint8_t *in, unsigned int in_size,
                                   unsigned int *out_size);
+/* hts_pack / hts_unpack_meta / hts_unpack (pack.c:56-344), shared */
+uint8_t *ora_pack(const uint8_t *d, uint32_t n, uint8_t *meta, int *meta_len, uint32_t *out_len);
+int ora_unpack_meta(const uint8_t *d, uint32_t len, uint8_t *map, int *per);
+int ora_unpack(const uint8_t *d, uint32_t len, uint8_t *out, uint32_t n, int per,
+               const uint8_t *map);
+
+/* arith_dynamic (htscodecs/arith_dynamic.h:41-55) */
+unsigned int ora_arith_compress_bound(unsigned int size, int order);
+uint8_t *ora_arith_compress_to(uint8_t *in, unsigned int in_size, uint8_t *out,
+                               unsigned int *out_size, int order);
+uint8_t *ora_arith_uncompress_to(uint8_t *in, unsigned int in_size, uint8_t *out,
+                                 unsigned int *out_size);
+
 /* fqzcomp_qual (fork ABI, htscodecs/fqzcomp_qual.h:59-64,155-170) */
 typedef struct {
     int num_records;

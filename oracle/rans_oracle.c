@@ -661,6 +661,18 @@ static int unpack(const uint8_t *d, uint32_t len, uint8_t *out, uint32_t n,
     return 0;
 }
 
+/* shared with arith_oracle.c */
+uint8_t *ora_pack(const uint8_t *d, uint32_t n, uint8_t *meta, int *meta_len, uint32_t *out_len) {
+    return pack(d, n, meta, meta_len, out_len);
+}
+int ora_unpack_meta(const uint8_t *d, uint32_t len, uint8_t *map, int *per) {
+    return unpack_meta(d, len, map, per);
+}
+int ora_unpack(const uint8_t *d, uint32_t len, uint8_t *out, uint32_t n, int per,
+               const uint8_t *map) {
+    return unpack(d, len, out, n, per, map);
+}
+
 /* ---------------------------------------------------------------------- */
 /* RLE: rle.c:48-189                                                      */
 
