@@ -9,6 +9,7 @@
 #include "rans_codec.hpp"
 #include "rans_format.hpp"
 #include "fqz_kernels.h"
+#include "arith_kernels.h"
 
 namespace fqz5 {
 
@@ -155,6 +156,34 @@ unsigned char *rans_uncompress_4x16(unsigned char *in, unsigned int in_size,
 }
 
 void rans_set_cpu(int) {}
+
+unsigned int arith_compress_bound(unsigned int size, int order) {
+    return arith_compress_bound_ref(size, order);
+}
+
+unsigned char *arith_compress_to(unsigned char *in, unsigned int in_size, unsigned char *out,
+                                 unsigned int *out_size, int order) {
+    GUARD_BEGIN
+    return arith_compress_gpu(in, in_size, out, out_size, order);
+    GUARD_END(nullptr)
+}
+
+unsigned char *arith_compress(unsigned char *in, unsigned int in_size, unsigned int *out_size,
+                              int order) {
+    return arith_compress_to(in, in_size, nullptr, out_size, order);
+}
+
+unsigned char *arith_uncompress_to(unsigned char *in, unsigned int in_size, unsigned char *out,
+                                   unsigned int *out_sz) {
+    GUARD_BEGIN
+    return arith_uncompress_gpu(in, in_size, out, out_sz);
+    GUARD_END(nullptr)
+}
+
+unsigned char *arith_uncompress(unsigned char *in, unsigned int in_size,
+                                unsigned int *out_size) {
+    return arith_uncompress_to(in, in_size, nullptr, out_size);
+}
 
 int fqz5_rans_compress_batch(fqz5_rans_job *jobs, int n) {
     GUARD_BEGIN

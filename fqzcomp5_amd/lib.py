@@ -82,6 +82,18 @@ def load() -> C.CDLL:
     lib.fqz_decompress.restype = C.c_void_p
     lib.fqz_decompress.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t),
                                    C.POINTER(C.c_int), C.c_int, C.POINTER(FqzSlice)]
+    lib.arith_compress_bound.restype = C.c_uint
+    lib.arith_compress_bound.argtypes = [C.c_uint, C.c_int]
+    lib.arith_compress_to.restype = C.c_void_p
+    lib.arith_compress_to.argtypes = [C.c_char_p, C.c_uint, C.c_void_p,
+                                      C.POINTER(C.c_uint), C.c_int]
+    lib.arith_compress.restype = C.c_void_p
+    lib.arith_compress.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint), C.c_int]
+    lib.arith_uncompress_to.restype = C.c_void_p
+    lib.arith_uncompress_to.argtypes = [C.c_char_p, C.c_uint, C.c_void_p,
+                                        C.POINTER(C.c_uint)]
+    lib.arith_uncompress.restype = C.c_void_p
+    lib.arith_uncompress.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint)]
     _lib = lib
     return lib
 
@@ -158,6 +170,42 @@ def rans_uncompress_to(comp: bytes, size: int) -> bytes | None:
     if not p:
         return None
     return buf.raw[:n.value]
+
+
+def arith_compress(data: bytes, order: int, cap: int | None = None) -> bytes | None:
+    """arith_compress (cap None) or arith_compress_to with a caller buffer
+    of `cap` bytes, on the GPU; None where the reference returns NULL."""
+    lib = load()
+    if cap is None:
+        n = C.c_uint(0)
+        p = lib.arith_compress(bytes(data), len(data), C.byref(n), order)
+        if not p:
+            return None
+        out = C.string_at(p, n.value)
+        _libc.free(p)
+        return out
+    buf = C.create_string_buffer(max(cap, 1))
+    n = C.c_uint(cap)
+    p = lib.arith_compress_to(bytes(data), len(data), buf, C.byref(n), order)
+    return None if not p else buf.raw[:n.value]
+
+
+def arith_uncompress(comp: bytes, out_size: int | None = None) -> bytes | None:
+    """arith_uncompress (out_size None) or arith_uncompress_to into a
+    buffer of out_size bytes, on the GPU; None on failure."""
+    lib = load()
+    if out_size is None:
+        n = C.c_uint(0)
+        p = lib.arith_uncompress(bytes(comp), len(comp), C.byref(n))
+        if not p:
+            return None
+        out = C.string_at(p, n.value)
+        _libc.free(p)
+        return out
+    buf = C.create_string_buffer(max(out_size, 1))
+    n = C.c_uint(out_size)
+    p = lib.arith_uncompress_to(bytes(comp), len(comp), buf, C.byref(n))
+    return None if not p else buf.raw[:n.value]
 
 
 def compress_batch_dev(jobs: list[RansJob]) -> None:

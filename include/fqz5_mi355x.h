@@ -7,7 +7,7 @@
  *   rANS 4x16/32x16  /root/reference/htscodecs/rANS_static4x16.h:41-66
  *   fqzcomp_qual     /root/reference/htscodecs/fqzcomp_qual.h:59-170
  *                    (the fork's ABI: fqz_slice carries the sequences)
- * (arith_compress_to follows in a later round; see DESIGN.md.)
+ *   arith_dynamic    /root/reference/htscodecs/arith_dynamic.h:41-54
  *
  * Part 2 is the batched, device-resident API used by the block codec and
  * the benchmark: many streams per call, inputs and outputs in HBM.
@@ -121,6 +121,31 @@ char *fqz_compress(int vers, fqz_slice *s, char *in, size_t in_size,
  * sequence-context streams.  malloc()ed result, NULL on failure. */
 char *fqz_decompress(char *in, size_t in_size, size_t *out_size,
                      int *lengths, int nlengths, fqz_slice *s);
+
+/* ---- arith_dynamic (arith_dynamic.h:41-54) ----------------------------- */
+
+/* Replaces arith_compress_bound (arith_dynamic.c:77). */
+unsigned int arith_compress_bound(unsigned int size, int order);
+
+/* Replaces arith_compress_to (arith_dynamic.c:730).  order = 0/1 | PACK 0x80
+ * | RLE 0x40 | CAT 0x20 | NOSZ 0x10 | STRIPE 0x08 (stripes in bits 8-15);
+ * EXT 0x04 (bzip2) fails as in a reference build without libbz2.
+ * out == NULL: a buffer of arith_compress_bound() bytes is malloc()ed. */
+unsigned char *arith_compress_to(unsigned char *in, unsigned int in_size,
+                                 unsigned char *out, unsigned int *out_size,
+                                 int order);
+
+/* Replaces arith_compress (arith_dynamic.c:1027). */
+unsigned char *arith_compress(unsigned char *in, unsigned int in_size,
+                              unsigned int *out_size, int order);
+
+/* Replaces arith_uncompress_to (arith_dynamic.c:1032). */
+unsigned char *arith_uncompress_to(unsigned char *in, unsigned int in_size,
+                                   unsigned char *out, unsigned int *out_sz);
+
+/* Replaces arith_uncompress (arith_dynamic.c:1279). */
+unsigned char *arith_uncompress(unsigned char *in, unsigned int in_size,
+                                unsigned int *out_size);
 
 /* ---- Part 2: batched device API --------------------------------------- */
 
