@@ -713,9 +713,189 @@ static DEV void dec32_body(const DecJob &J) {
     if (l == 0) *J.status = (ptr <= nwords) ? 0 : -1;
 }
 
+// ---------------------------------------------------------------------------
+// O0, NX = 4: the lean chain.  The order-0 symbol does not feed the chain, so
+// the step carries only what the next state needs and the slot is emitted in
+// place of the symbol (mapped to the symbol at the group flush):
+//   LDS entry per slot   {f, slot - start} as two u32 (no symbol byte)
+//   xd   = f * (x >> bits) + (slot - start)             (one mad24)
+//   ptr  lives in a VGPR and advances with one v_bcnt of the renorm ballot;
+//        the ring is linear over a group (a mirrored head), so the window
+//        address is one shift-add of ptr.
+// Per step: 2 VALU for the table address, the table and window reads, 2 for
+// xd, the ballot, 6 for the renorm select and ptr (slots stay in VGPRs): no
+// SALU on the chain (a wave issues one instruction per ~4 cycles whatever the
+// unit, so SALU round trips cost as much as VALU ones).
+constexpr uint32_t O0_G = 256;                         // steps per group
+constexpr uint32_t O0_MIRROR = 1040;                   // >= 4*G + 4, slab-unit multiple of 8
+constexpr uint32_t O0_RING_BYTES = (RING_WORDS + O0_MIRROR) * 2;
+constexpr uint32_t O0_OBUF_BYTES = 4 * O0_G * 2;       // u16 slots, lane-major
+constexpr uint32_t O0_SYM_OFF = O0_RING_BYTES + O0_OBUF_BYTES;
+constexpr uint32_t O0_TAB_OFF = O0_SYM_OFF + 4096;     // u32 entries, 16-B aligned
+static_assert(O0_TAB_OFF % 16 == 0, "O0 table alignment");
+constexpr uint32_t O0_LDS_BYTES = O0_TAB_OFF + 4096 * 8;
+
+static DEV void store_slab_o0(uint16_t *ring, uint32_t s, int z, uint4 v) {
+    const uint32_t w0 = (s * SLAB_WORDS + uint32_t(z) * 8) & (RING_WORDS - 1);
+    *reinterpret_cast<uint4 *>(ring + w0) = v;
+    if (w0 < O0_MIRROR) *reinterpret_cast<uint4 *>(ring + RING_WORDS + w0) = v;
+}
+
+// A 32-bit LDS byte address as a pointer (an unaligned 8-byte window is read
+// with one ds_read_b64: gfx950 LDS runs in unaligned mode).
+template <typename T>
+static DEV const __attribute__((address_space(3))) T *lds_ptr(uint32_t a) {
+    return reinterpret_cast<const __attribute__((address_space(3))) T *>(size_t(a));
+}
+
+// acc + popcount(m) in one VALU op.  `after` ties it behind the mbcnt of
+// the same ballot, which already waited out the VALU-writes-SGPR hazard
+// that the hazard recognizer does not see through inline asm.
+static DEV uint32_t vbcnt(uint32_t m, uint32_t acc, uint32_t after) {
+    uint32_t r;
+    asm volatile("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "s"(m), "v"(acc), "v"(after));
+    return r;
+}
+
+static DEV void dec4_o0_body(const DecJob &J) {
+    constexpr int NX = 4;
+    constexpr uint32_t G = O0_G;
+    uint8_t *lds = reinterpret_cast<uint8_t *>(chain_lds);
+    uint16_t *ring = reinterpret_cast<uint16_t *>(lds);
+    uint16_t *obuf = reinterpret_cast<uint16_t *>(lds + O0_RING_BYTES);
+    uint8_t *s2sym = lds + O0_SYM_OFF;
+    uint2 *tab = reinterpret_cast<uint2 *>(lds + O0_TAB_OFF);
+    const int l = int(threadIdx.x);
+    const uint32_t n = J.n;
+    const int bits = J.bits;
+    const uint32_t mask = (1u << bits) - 1;
+    // (f-1) << (bits+8) | (slot-start) << 8 | sym  ->  {f, slot-start}
+    for (uint32_t i = l; i <= mask; i += 64) {
+        const uint32_t e = J.tab[i];
+        tab[i] = make_uint2((e >> (bits + 8)) + 1, (e >> 8) & mask);
+        s2sym[i] = uint8_t(e);
+    }
+    uint32_t x = 1u << 16;
+    if (l < NX) {
+        const uint8_t *p = J.in + 4 * l;
+        x = p[0] | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+    }
+    const uint32_t nwords = (J.in_len - 4 * uint32_t(NX)) / 2;
+    const auto wsrc = buf(J.in + 4 * NX, nwords * 2);
+    uint32_t slabs = 0;
+    uint4 pf = load_slab(wsrc, 0, l);
+    const uint32_t T = (n + NX - 1) / NX, Tfull = n / NX;
+    uint32_t ptr = 0;                                  // words consumed (uniform)
+    const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(
+        (__attribute__((address_space(3))) uint16_t *)(ring)));
+    const uint32_t tab_lds = uint32_t(reinterpret_cast<uintptr_t>(
+        (__attribute__((address_space(3))) uint2 *)(tab)));
+    uint16_t *myob = obuf + (l & 3) * G;
+#ifdef FQZ5_CHAIN_PROBE
+    const uint64_t pr0 = __builtin_amdgcn_s_memtime(), rr0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_steps = 0, n_steps = 0;
+#endif
+
+    for (uint32_t t0 = 0; t0 < T; t0 += G) {
+        while (slabs * SLAB_WORDS < ptr + 2560 && slabs * SLAB_WORDS < nwords + SLAB_WORDS) {
+            store_slab_o0(ring, slabs, l, pf);
+            slabs++;
+            pf = load_slab(wsrc, slabs, l);
+        }
+        __syncthreads();
+        // word p of this group sits at byte wbase + 2p of the LDS (p - gp < 1028)
+        const uint32_t gp = ptr;
+        const uint32_t wbase = ring_lds + 2 * ((gp & (RING_WORDS - 1)) - gp);
+        const uint32_t t1 = (T - t0 < G) ? T : t0 + G;
+        const uint32_t tf = t1 < Tfull ? t1 : (t0 > Tfull ? t0 : Tfull);
+        uint32_t t = t0;
+#ifdef FQZ5_CHAIN_PROBE
+        const uint64_t ps0 = __builtin_amdgcn_s_memtime();
+#endif
+        if (l < NX) {
+            for (; t + 16 <= tf; t += 16) {
+                uint32_t a[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    a[u] = x & mask;
+                    const uint64_t e = *lds_ptr<uint64_t>(tab_lds + (a[u] << 3));
+                    const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
+                    const uint32_t xd = __umul24(uint32_t(e), x >> bits) + uint32_t(e >> 32);
+                    const uint64_t m = __ballot(xd < RANS_LOW_D);
+                    const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
+                    const uint32_t w = uint32_t(win >> r16);
+                    x = (xd < RANS_LOW_D) ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
+                    ptr = vbcnt(uint32_t(m), ptr, r16);
+                }
+                uint4 *o = reinterpret_cast<uint4 *>(myob + (t - t0));
+                o[0] = make_uint4(a[0] | a[1] << 16, a[2] | a[3] << 16, a[4] | a[5] << 16,
+                                  a[6] | a[7] << 16);
+                o[1] = make_uint4(a[8] | a[9] << 16, a[10] | a[11] << 16, a[12] | a[13] << 16,
+                                  a[14] | a[15] << 16);
+            }
+#ifdef FQZ5_CHAIN_PROBE
+            t_steps += __builtin_amdgcn_s_memtime() - ps0;
+            n_steps += t - t0;
+#endif
+            // rest of the group: single steps; in the last step only lanes
+            // z < n % 4 are active
+            for (; t < t1; t++) {
+                const bool act = uint32_t(NX) * t + uint32_t(l) < n;
+                const uint32_t s = x & mask;
+                const uint2 e = tab[s];
+                const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
+                const uint32_t xd = __umul24(e.x, x >> bits) + e.y;
+                const bool c = act && xd < RANS_LOW_D;
+                const uint64_t m = __ballot(c);
+                const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
+                const uint32_t w = uint32_t(win >> r16);
+                if (act) {
+                    x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
+                    myob[t - t0] = uint16_t(s);
+                }
+                ptr += uint32_t(__popcll(m));
+            }
+        }
+        ptr = __builtin_amdgcn_readfirstlane(ptr);
+        __syncthreads();
+        const uint32_t cnt = (t1 - t0) * NX;
+        if (cnt == NX * G && NX * t0 + NX * G <= n && (reinterpret_cast<uintptr_t>(J.out) & 15) == 0) {
+            // a whole group: lane l writes output bytes [16l, 16l+16), i.e.
+            // steps 4l..4l+3 of the 4 states, as one 16-byte store
+            uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int z = 0; z < NX; z++) {
+                const uint2 q = *reinterpret_cast<const uint2 *>(obuf + z * G + 4 * l);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t sl = (k & 2 ? q.y : q.x) >> (16 * (k & 1)) & 0xffffu;
+                    v[k] |= uint32_t(s2sym[sl]) << (8 * z);
+                }
+            }
+            *reinterpret_cast<uint4 *>(J.out + NX * t0 + 16 * l) = make_uint4(v[0], v[1], v[2], v[3]);
+        } else {
+            const auto out = buf(J.out, n);
+            for (uint32_t i = l; i < cnt; i += 64)
+                st8(out, NX * t0 + i, s2sym[obuf[(i & 3) * G + (i >> 2)]]);   // past n: dropped
+        }
+        __syncthreads();
+    }
+    if (l == 0) *J.status = (ptr <= nwords) ? 0 : -1;
+#ifdef FQZ5_CHAIN_PROBE
+    if (l == 0 && blockIdx.x == 0) {
+        g_probe[2] = __builtin_amdgcn_s_memtime() - pr0;
+        g_probe[3] = __builtin_amdgcn_s_memrealtime() - rr0;
+        g_probe[4] = t_steps;
+        g_probe[5] = n_steps;
+        g_probe[6] = T;
+    }
+#endif
+}
+
 template <bool O1, int TM>
 static DEV void dec_any(const DecJob &J) {
     if (J.nx == 32) dec32_body<O1, TM>(J);
+    else if (!O1)   dec4_o0_body(J);
     else            dec4_body<O1, TM>(J);
 }
 
@@ -733,7 +913,8 @@ __global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
 
 uint32_t dec_lds_bytes(uint32_t rows, int bits, int mode) {
     if (mode == DEC_TAB_GLOBAL) return DEC_LDS_BASE;
-    return DEC_LDS_BASE + dec_tab_words(uint32_t(mode), rows, bits) * 4u;
+    const uint32_t b = DEC_LDS_BASE + dec_tab_words(uint32_t(mode), rows, bits) * 4u;
+    return rows == 1 && b < O0_LDS_BYTES ? O0_LDS_BYTES : b;   // O0 (dec4_o0_body)
 }
 
 static void lds_attr(const void *f) {
@@ -776,5 +957,11 @@ hipError_t launch_dec(const DecJob *d_jobs, int njobs, uint32_t lds, hipStream_t
     hipLaunchKernelGGL(k_rans_dec, dim3(njobs), dim3(64), lds, s, d_jobs);
     return hipGetLastError();
 }
+
+#ifdef FQZ5_CHAIN_PROBE
+extern "C" int fqz5_chain_probe_read(uint64_t *out) {
+    return int(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe), sizeof(g_probe)));
+}
+#endif
 
 }  // namespace fqz5

@@ -1,0 +1,92 @@
+// ub2.hip — cycles per dependent step of the pieces of the O0 decode step,
+// one wave, exec limited to the 4 state lanes (as in dec4_o0_body).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+#define N 4096
+typedef __attribute__((address_space(3))) uint64_t lds64_t;
+
+template <int T>
+__global__ void k(uint32_t *out, uint64_t *cyc, uint32_t a, uint32_t b) {
+    __shared__ uint64_t lds[4096];
+    const int l = threadIdx.x;
+    for (int i = l; i < 4096; i += 64) lds[i] = (uint64_t((i * 40503u) & 4095) << 32) | ((i * 2654435761u) & 4095);
+    __syncthreads();
+    uint32_t x = a + l, y = b, p = 0;
+    uint64_t win = (uint64_t(b) << 32) | a;
+    uint64_t t0 = 0, t1 = 0;
+    if (l < 4) {
+        __builtin_amdgcn_s_waitcnt(0);
+        t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll 16
+        for (int i = 0; i < N; i++) {
+            if (T == 0) x = uint32_t(lds[x & 4095]);                       // LDS b64 chain
+            if (T == 1) x = x + y;                                          // v_add chain
+            if (T == 2) x = __umul24(x, y) + p;                            // mad chain
+            if (T == 3) x = uint32_t(win >> (x & 48)) + x;                  // 64-bit shift + add
+            if (T == 4) x = __builtin_amdgcn_perm(x, y, 0x05040100u) + 1;  // perm + add
+            if (T == 5) x = __builtin_amdgcn_mbcnt_lo(uint32_t(__ballot(x < y)), x);   // cmp + mbcnt
+            if (T == 6) x = (x < y) ? (x >> 1) : (x + 3);                   // cmp + cndmask
+            if (T == 7) {                                                   // fast path no branch
+                const uint64_t e = lds[x & 4095];
+                x = __umul24(uint32_t(e), x >> 12) + uint32_t(e >> 32);
+            }
+            if (T == 8) {                                                   // fast path + never-taken branch
+                const uint64_t e = lds[x & 4095];
+                x = __umul24(uint32_t(e), x >> 12) + uint32_t(e >> 32);
+                if (__ballot(x == 0xdeadbeefu)) { p += x; y ^= p; }
+            }
+            if (T == 9) {                                                   // fast path + ~50% taken branch
+                const uint64_t e = lds[x & 4095];
+                x = __umul24(uint32_t(e), x >> 12) + uint32_t(e >> 32);
+                if (__ballot((x & 3) == 0)) { p += x; y ^= p; }
+            }
+            if (T == 11) {                                                  // encoder step, cmp + cndmask
+                const uint32_t xr = (x > y) ? (x >> 16) : x;
+                const uint32_t q = __umulhi(xr, 0x9e3779b1u) >> (a & 7);
+                x = __umul24(q, 3u) + (xr + 12345u);
+            }
+            if (T == 12) {                                                  // encoder step, shift from the sign of y - x
+                const uint32_t s = ((y - x) >> 27) & 16u;
+                const uint32_t xr = x >> s;
+                const uint32_t q = __umulhi(xr, 0x9e3779b1u) >> (a & 7);
+                x = __umul24(q, 3u) + (xr + 12345u);
+            }
+            if (T == 13) {                                                  // encoder step, v_sub_co borrow
+                uint32_t d;
+                const bool c = __builtin_sub_overflow(y, x, &d);
+                const uint32_t xr = c ? (x >> 16) : x;
+                const uint32_t q = __umulhi(xr, 0x9e3779b1u) >> (a & 7);
+                x = __umul24(q, 3u) + (xr + 12345u);
+            }
+            if (T == 10) {                                                  // full renorm select chain
+                const uint64_t m = __ballot(x < y);
+                const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
+                const uint32_t w = uint32_t(win >> r16);
+                x = (x < y) ? __builtin_amdgcn_perm(x, w, 0x05040100u) : x + 7;
+            }
+        }
+        t1 = __builtin_amdgcn_s_memtime();
+    }
+    out[l] = x + p + y;
+    if (l == 0) cyc[T] = t1 - t0;
+}
+
+int main() {
+    uint32_t *out; uint64_t *cyc;
+    hipMalloc(&out, 64 * 4); hipMalloc(&cyc, 32 * 8);
+    const char *names[] = {"ds_read_b64 chain", "v_add", "mad24", "lshr_b64+add", "perm+add",
+                           "cmp+mbcnt", "cmp+cndmask", "and,lshl_add,ds_read,mad", "same + never-taken branch",
+                           "same + ~68%-taken branch", "renorm select (cmp,mbcnt,lshl,lshr64,perm,cndmask)",
+                           "enc step cmp+cndmask", "enc step sign shift", "enc step sub borrow"};
+#define RUN(T) hipLaunchKernelGGL(k<T>, dim3(1), dim3(64), 0, 0, out, cyc, 12345u, 99999u);
+    for (int rep = 0; rep < 2; rep++) {
+        RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13)
+    }
+    hipDeviceSynchronize();
+    uint64_t h[32];
+    hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
+    for (int t = 0; t <= 13; t++) printf("T%-2d %-55s %7.1f cyc/step\n", t, names[t], double(h[t]) / N);
+    return 0;
+}
