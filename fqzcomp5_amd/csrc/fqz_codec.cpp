@@ -556,6 +556,20 @@ void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         jobs.push_back(J);
     }
     const int np = int(par.size());
+    if (np && std::getenv("FQZ5_FQZ_SEGSTATS")) {   // diagnostics: events per model
+        for (int k = 0; k < np; k++) {
+            std::vector<uint32_t> lo(FQZ_NMODELS), hi(FQZ_NMODELS);
+            g.download(lo.data(), jobs[size_t(k)].seg_lo, FQZ_NMODELS);
+            g.download(hi.data(), jobs[size_t(k)].seg_hi, FQZ_NMODELS);
+            g.sync();
+            std::vector<uint32_t> c;
+            for (uint32_t m = 0; m < FQZ_NMODELS; m++) if (hi[m] > lo[m]) c.push_back(hi[m] - lo[m]);
+            std::sort(c.rbegin(), c.rend());
+            std::fprintf(stderr, "fqz job %d: %u events, %zu models, top:", k, jobs[size_t(k)].nev, c.size());
+            for (size_t i = 0; i < c.size() && i < 12; i++) std::fprintf(stderr, " %u", c[i]);
+            std::fprintf(stderr, "\n");
+        }
+    }
     if (np) FQZ5_HIP(launch_fqz_model_pass(g.upload(jobs), np, g.stream));
     // the range chain of every block (one wave each), then the output bytes
     for (int k = 0; k < np; k++) {

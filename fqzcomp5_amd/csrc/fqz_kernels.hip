@@ -343,12 +343,26 @@ template <int CAP> DEV void model_run(FList<CAP> *m, const FqzEvJob &J, uint32_t
     // Slot 1 (the head) and the total are kept in registers while the
     // symbols hit the head; LDS is synchronised before any other update.
     // The head never bubbles (slot 0 always wins the comparison).
+    // The next batch's symbols are loaded (bounds-checked buffer loads over
+    // all events: a lane may read past its model, never past the array)
+    // while this batch is coded, so a lane waits for memory only when a
+    // batch codes faster than a load returns.
     uint32_t s1 = m->sy[1], f1 = m->fr[1], tot = m->total;
+    const auto rsv = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(J.sval), 0,
+                                                       J.nev * 8u, 0x00020000);
+    uint32_t sn[B];
+    auto fetch = [&](uint32_t k) {
+#pragma unroll
+        for (uint32_t u = 0; u < B; u++)
+            sn[u] = __builtin_amdgcn_raw_buffer_load_b32(rsv, (k + u) * 8u, 0, 0);
+    };
+    fetch(lo);
     for (uint32_t k0 = lo; k0 < hi; k0 += B) {
         const uint32_t nb = min(B, hi - k0);
         uint32_t sv[B];
 #pragma unroll
-        for (uint32_t u = 0; u < B; u++) sv[u] = u < nb ? uint32_t(J.sval[k0 + u]) & 0xffu : 0u;
+        for (uint32_t u = 0; u < B; u++) sv[u] = sn[u] & 0xffu;
+        if (k0 + B < hi) fetch(k0 + B);
         uint64_t cd[B];
 #pragma unroll
         for (uint32_t u = 0; u < B; u++) {
@@ -428,66 +442,117 @@ __global__ void k_fqz_expand(FqzEvJob J) {
 // division is exact through the double reciprocal: for range < 2^32 and
 // total <= 65519, |range * RN(1/total) - range/total| < 2^-20, below the
 // distance 1/total to the next integer, so adding 2^-19 and truncating
-// gives floor(range/total).  Blocks of events are staged through LDS by all
-// lanes (coalesced), lane 0 runs the chain from LDS, and its outputs are
-// flushed by all lanes: the lane's reads never wait behind global stores
-// (CDNA's vmcnt counts both).
-constexpr uint32_t RC_BLK = 4096;
+// gives floor(range/total).  Events go through LDS in blocks of RC_BLK:
+// all lanes load block b+1 into registers (coalesced) before lane 0 runs
+// the chain over block b, then flush block b's outputs and stage block b+1,
+// so the chain never waits for memory.  The chain carries only the range
+// (7 dependent instructions per event: cvt, fma, cvt, mul, ffbh, and,
+// shift) and records q; the flush recomputes each event's byte-shift count
+// from q * freq in parallel.  The staged events are split into reciprocals
+// and frequencies so that lane 0 reads 8 events with 10 LDS instructions.
+constexpr uint32_t RC_BLK = 1024;
+constexpr uint32_t RC_PER = RC_BLK / 64;         // events per lane per block
+
+#ifdef FQZ5_RC_PROBE
+__device__ uint64_t g_rcprobe[4];
+extern "C" int fqz5_rc_probe_read(uint64_t *out) {
+    return int(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rcprobe), sizeof(g_rcprobe)));
+}
+#endif
 
 __global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
     const FqzEvJob J = load_job(Js + blockIdx.x);   // one wave per block of a batch
-    __shared__ uint4 in[RC_BLK + 8];
-    __shared__ uint4 o_q[RC_BLK / 4];
-    __shared__ uint2 o_k[RC_BLK / 8];
+    __shared__ double s_rd[RC_BLK];
+    __shared__ uint32_t s_f[RC_BLK];
+    __shared__ uint32_t s_q[RC_BLK];
     const int l = int(threadIdx.x);
     uint32_t rng = 0xFFFFFFFFu;
     const double bias = 1.0 / 524288.0;           // 2^-19
-    for (uint32_t base = 0; base < J.nev; base += RC_BLK) {
-        const uint32_t cnt = min(RC_BLK, J.nev - base);
-        for (uint32_t i = l; i < cnt; i += 64) in[i] = J.rec[base + i];
-        __syncthreads();
+    const uint32_t nev = J.nev;
+    // bounds-checked buffer accesses: loads past the end read 0, stores past
+    // the end are dropped, so the staging has no branches
+    const auto rrec = __builtin_amdgcn_make_buffer_rsrc(J.rec, 0, nev * 16u, 0x00020000);
+    const auto radd = __builtin_amdgcn_make_buffer_rsrc(J.addend, 0, nev * 4u, 0x00020000);
+    const auto rsh = __builtin_amdgcn_make_buffer_rsrc(J.shifts, 0, nev * 4u, 0x00020000);
+    uint4 pf[RC_PER];
+    auto fetch = [&](uint32_t base) {
+#pragma unroll
+        for (uint32_t r = 0; r < RC_PER; r++) {
+            const uint32_t i = base + uint32_t(l) + 64u * r;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rrec, i * 16u, 0, 0);
+            pf[r] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+    };
+    auto stage = [&]() {
+#pragma unroll
+        for (uint32_t r = 0; r < RC_PER; r++) {
+            const uint32_t i = uint32_t(l) + 64u * r;
+            s_rd[i] = __longlong_as_double((long long)(uint64_t(pf[r].y) << 32 | pf[r].x));
+            s_f[i] = pf[r].z;
+        }
+    };
+    fetch(0);
+    stage();
+    __syncthreads();
+#ifdef FQZ5_RC_PROBE
+    uint64_t pc = 0;
+    const uint64_t p0 = __builtin_amdgcn_s_memtime();
+#endif
+    for (uint32_t base = 0; base < nev; base += RC_BLK) {
+        const uint32_t cnt = min(RC_BLK, nev - base);
+        if (base + RC_BLK < nev) fetch(base + RC_BLK);
+#ifdef FQZ5_RC_PROBE
+        const uint64_t c0 = __builtin_amdgcn_s_memtime();
+#endif
         if (l == 0) {
-            // q and the shift count of one event; renorm: shifts = clz / 8
-            // (range >= 1 always), i.e. range <<= clz & 24
-            auto step = [&](const uint4 r, uint32_t &q, uint32_t &k) {
-                const double rd = __longlong_as_double((long long)(uint64_t(r.y) << 32 | r.x));
-                q = uint32_t(__fma_rn(double(rng), rd, bias));
-                rng = q * r.z;
-                const uint32_t z = uint32_t(__builtin_clz(rng)) & 24u;
-                rng <<= z;
-                k = z >> 3;
+            // renorm: range <<= clz & 24 (range >= 1 always)
+            auto step = [&](double rd, uint32_t f) {
+                const uint32_t q = uint32_t(__fma_rn(double(rng), rd, bias));
+                rng = q * f;
+                rng <<= uint32_t(__builtin_clz(rng)) & 24u;
+                return q;
             };
-            const uint32_t full = cnt & ~7u;
-            for (uint32_t i = 0; i < full; i += 8) {
-                uint4 r[8];
+            for (uint32_t i = 0; i < cnt; i += 8) {     // past cnt: harmless (rng unused after)
+                double rd[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) r[u] = in[i + u];
-                uint32_t q[8], k[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) step(r[u], q[u], k[u]);
-                o_q[i / 4] = make_uint4(q[0], q[1], q[2], q[3]);
-                o_q[i / 4 + 1] = make_uint4(q[4], q[5], q[6], q[7]);
-                o_k[i / 8] = make_uint2(k[0] | k[1] << 8 | k[2] << 16 | k[3] << 24,
-                                        k[4] | k[5] << 8 | k[6] << 16 | k[7] << 24);
-            }
-            uint32_t *oq = reinterpret_cast<uint32_t *>(o_q);
-            uint8_t *ok = reinterpret_cast<uint8_t *>(o_k);
-            for (uint32_t i = full; i < cnt; i++) {
-                uint32_t q, k;
-                step(in[i], q, k);
-                oq[i] = q;
-                ok[i] = uint8_t(k);
+                for (int u = 0; u < 8; u++) rd[u] = s_rd[i + u];
+                const uint4 f0 = *reinterpret_cast<const uint4 *>(s_f + i);
+                const uint4 f1 = *reinterpret_cast<const uint4 *>(s_f + i + 4);
+                uint4 q0, q1;
+                q0.x = step(rd[0], f0.x);
+                q0.y = step(rd[1], f0.y);
+                q0.z = step(rd[2], f0.z);
+                q0.w = step(rd[3], f0.w);
+                q1.x = step(rd[4], f1.x);
+                q1.y = step(rd[5], f1.y);
+                q1.z = step(rd[6], f1.z);
+                q1.w = step(rd[7], f1.w);
+                *reinterpret_cast<uint4 *>(s_q + i) = q0;
+                *reinterpret_cast<uint4 *>(s_q + i + 4) = q1;
             }
         }
         __syncthreads();
-        const uint32_t *oq = reinterpret_cast<const uint32_t *>(o_q);
-        const uint8_t *ok = reinterpret_cast<const uint8_t *>(o_k);
-        for (uint32_t i = l; i < cnt; i += 64) {
-            J.addend[base + i] = oq[i];          // q here; cum * q in k_fqz_accum
-            J.shifts[base + i] = ok[i];
+#ifdef FQZ5_RC_PROBE
+        pc += __builtin_amdgcn_s_memtime() - c0;
+#endif
+#pragma unroll
+        for (uint32_t r = 0; r < RC_PER; r++) {
+            const uint32_t i = uint32_t(l) + 64u * r;   // q here; cum * q in k_fqz_accum
+            const uint32_t q = s_q[i];
+            const uint32_t k = (uint32_t(__builtin_clz((q * s_f[i]) | 1u)) & 24u) >> 3;
+            __builtin_amdgcn_raw_buffer_store_b32(q, radd, (base + i) * 4u, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(k, rsh, (base + i) * 4u, 0, 0);
         }
+        if (base + RC_BLK < nev) stage();
         __syncthreads();
     }
+#ifdef FQZ5_RC_PROBE
+    if (l == 0 && blockIdx.x == 0) {
+        g_rcprobe[0] = __builtin_amdgcn_s_memtime() - p0;
+        g_rcprobe[1] = pc;
+        g_rcprobe[2] = nev;
+    }
+#endif
 }
 
 // The coder's output is the base-256 number S = sum_i addend_i *

@@ -153,7 +153,8 @@ hipError_t launch_unrle_expand(const UnRleItem *items, const uint32_t *chunk_ite
 hipError_t launch_gather(const GatherItem *items, int n, uint8_t *out, hipStream_t s);
 hipError_t launch_hist0(const HistItem *d_items, int nitems, uint32_t *d_counts,
                         hipStream_t s);
-hipError_t launch_hist1(const Hist1Item *d_items, int nitems, uint32_t *d_counts,
+// big: items with A*A >= 16384 (16-bit LDS counters; slices < 65536 bytes)
+hipError_t launch_hist1(const Hist1Item *d_items, int nitems, uint32_t *d_counts, bool big,
                         hipStream_t s);
 hipError_t launch_pack(const PackItem *d_items, int nitems, uint32_t max_out,
                        bool unpack, hipStream_t s);

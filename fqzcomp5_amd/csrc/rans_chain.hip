@@ -37,6 +37,7 @@ namespace fqz5 {
 extern __shared__ uint4 chain_lds[];
 #ifdef FQZ5_CHAIN_PROBE
 __device__ uint64_t g_probe[8];
+__device__ uint64_t g_jobt[512][6];   // per decode job: start, end (100 MHz), cycles, info, loop cycles, loop steps
 #endif
 
 // Raw buffer over [p, p+n): loads past n return 0, stores past n are dropped.
@@ -882,6 +883,7 @@ static DEV void dec4_o0_body(const DecJob &J) {
     }
     if (l == 0) *J.status = (ptr <= nwords) ? 0 : -1;
 #ifdef FQZ5_CHAIN_PROBE
+    if (l == 0 && blockIdx.x < 512) { g_jobt[blockIdx.x][4] = t_steps; g_jobt[blockIdx.x][5] = n_steps; }
     if (l == 0 && blockIdx.x == 0) {
         g_probe[2] = __builtin_amdgcn_s_memtime() - pr0;
         g_probe[3] = __builtin_amdgcn_s_memrealtime() - rr0;
@@ -901,6 +903,23 @@ static DEV void dec_any(const DecJob &J) {
 
 __global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
     const DecJob J = jobs[blockIdx.x];
+#ifdef FQZ5_CHAIN_PROBE
+    const uint64_t jt0 = __builtin_amdgcn_s_memrealtime(), jc0 = __builtin_amdgcn_s_memtime();
+    struct End {
+        uint64_t t0, c0; const DecJob &J;
+        __device__ ~End() {
+            if (threadIdx.x == 0 && blockIdx.x < 512) {
+                uint32_t hw, xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                g_jobt[blockIdx.x][0] = t0;
+                g_jobt[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+                g_jobt[blockIdx.x][2] = __builtin_amdgcn_s_memtime() - c0;
+                g_jobt[blockIdx.x][3] = uint64_t(J.n) << 32 | (xcc & 0xf) << 24 | ((hw >> 8) & 0xf) << 16 | ((hw >> 13) & 0x7) << 8 | ((hw >> 4) & 3);
+            }
+        }
+    } end_{jt0, jc0, J};
+#endif
     const int tm = int(J.mode);
     if (J.alpha != nullptr) {
         if (tm == DEC_TAB_LDS) dec_any<true, DEC_TAB_LDS>(J);
@@ -961,6 +980,9 @@ hipError_t launch_dec(const DecJob *d_jobs, int njobs, uint32_t lds, hipStream_t
 #ifdef FQZ5_CHAIN_PROBE
 extern "C" int fqz5_chain_probe_read(uint64_t *out) {
     return int(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe), sizeof(g_probe)));
+}
+extern "C" int fqz5_chain_jobs_read(uint64_t *out) {
+    return int(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_jobt), sizeof(g_jobt)));
 }
 #endif
 

@@ -29,6 +29,7 @@ namespace fqz5 {
 namespace {
 
 constexpr uint32_t HIST_SLICE = 1u << 17;
+constexpr uint32_t HIST1_BIG_SLICE = (1u << 16) - 64;   // 16-bit counters (k_hist1<true>)
 constexpr uint32_t NONE32 = 0xffffffffu;
 
 struct EJ {                       // one rANS entropy stream to encode
@@ -429,20 +430,23 @@ void Compressor::stage_tables() {
     for (size_t k = 0; k < o1jobs.size(); k++)
         std::memcpy(&remaps[k * 256], jobs_[o1jobs[k]].remap, 256);
     uint8_t *d_remaps = g_.upload(remaps);
-    std::vector<Hist1Item> items;
+    std::vector<Hist1Item> items, big;
     std::vector<const uint8_t *> probes;
     for (size_t k = 0; k < o1jobs.size(); k++) {
         EJ &j = jobs_[o1jobs[k]];
-        for (uint32_t b = 0; b < j.n; b += HIST_SLICE)
-            items.push_back({j.d_in, d_remaps + 256 * k, b, std::min(j.n, b + HIST_SLICE),
-                             uint32_t(j.A), j.f1_off});
+        const bool isbig = uint32_t(j.A) * uint32_t(j.A) >= 16384;
+        const uint32_t sl = isbig ? HIST1_BIG_SLICE : HIST_SLICE;
+        for (uint32_t b = 0; b < j.n; b += sl)
+            (isbig ? big : items).push_back({j.d_in, d_remaps + 256 * k, b, std::min(j.n, b + sl),
+                                             uint32_t(j.A), j.f1_off});
         uint32_t isz = j.n / j.nx;
         for (int z = 1; z < j.nx; z++) probes.push_back(j.d_in + size_t(z) * isz);
         probes.push_back(j.d_in + j.n - 1);
     }
     uint32_t *d_cnt = g_.arena.alloc_n<uint32_t>(total);
     g_.memset0(d_cnt, size_t(total) * 4);
-    FQZ5_HIP(launch_hist1(g_.upload(items), int(items.size()), d_cnt, g_.stream));
+    if (!items.empty()) FQZ5_HIP(launch_hist1(g_.upload(items), int(items.size()), d_cnt, false, g_.stream));
+    if (!big.empty()) FQZ5_HIP(launch_hist1(g_.upload(big), int(big.size()), d_cnt, true, g_.stream));
     std::vector<uint32_t> h(total);
     g_.download(h.data(), d_cnt, total);
     std::vector<uint8_t> pb;
@@ -515,6 +519,8 @@ void Compressor::stage_encode() {
         lds_r = std::max(lds_r, enc_replay_lds_bytes(j.o1, uint32_t(j.A)));
     }
     EventPair ev(g_.prof.on && !order.empty(), g_.stream);
+    lds_s = g_.chain_lds(lds_s, ejs.size() + ejb.size());
+    lds_b = g_.chain_lds(lds_b, ejs.size() + ejb.size());
     if (!ejs.empty()) {
         const EncJob *d = g_.upload(ejs);
         const EncJob *db = ejb.empty() ? nullptr : g_.upload(ejb);

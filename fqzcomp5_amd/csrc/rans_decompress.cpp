@@ -360,6 +360,7 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
         lds = std::max(lds, dec_lds_bytes(rows, j.bits, int(mode)));
     }
     EventPair ev(g_.prof.on && !ord.empty(), g_.stream);
+    lds = g_.chain_lds(lds, djs.size());
     if (!djs.empty()) FQZ5_HIP(launch_dec(g_.upload(djs), int(djs.size()), lds, g_.stream));
     ev.stop(g_.stream);
     std::vector<int32_t> st(used.size());

@@ -36,63 +36,80 @@ static DEV uint32_t lane_id() { return threadIdx.x & 63; }
 // rle_find_syms: eq[s] = #{i : d[i] == d[i-1] == s}).
 // One workgroup per work item (segment slice); LDS counters; global atomics.
 // ---------------------------------------------------------------------------
+// Counting is privatised: thread t adds into copy t % C of the bins (rows
+// padded by one word so that the copies of a bin fall in different LDS
+// banks), so a wave's atomics on one bin (the common case on skewed quality
+// or base data) conflict at most 64 / C ways instead of 64.
+constexpr uint32_t HIST0_C = 16;
+constexpr uint32_t HIST0_ROW = 513;                  // h[256], e[256], pad
+
 __global__ __launch_bounds__(256) void k_hist0(const HistItem *items,
                                                uint32_t *counts) {
-    __shared__ uint32_t h[256], e[256];
+    __shared__ uint32_t h[HIST0_C * HIST0_ROW];
     const HistItem it = items[blockIdx.x];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) { h[i] = 0; e[i] = 0; }
+    for (uint32_t i = threadIdx.x; i < HIST0_C * HIST0_ROW; i += blockDim.x) h[i] = 0;
     __syncthreads();
     const uint8_t *d = it.data;
-    // 16 bytes per thread per iteration; the previous byte comes from the
-    // neighbouring load (or one extra read at the slice start).
-    uint32_t beg = it.begin, end = it.end;
-    for (uint32_t i = beg + threadIdx.x * 16; i < end; i += blockDim.x * 16) {
-        uint32_t lim = end - i < 16 ? end - i : 16;
-        int prev = i ? d[i - 1] : -1;
-#pragma unroll 4
-        for (uint32_t k = 0; k < lim; k++) {
-            int c = d[i + k];
-            atomicAdd(&h[c], 1u);
-            if (c == prev) atomicAdd(&e[c], 1u);
-            prev = c;
-        }
+    uint32_t *mine = h + (threadIdx.x % HIST0_C) * HIST0_ROW;
+    // e[c]: bytes equal to their predecessor (hist8e's run count)
+    for (uint32_t i = it.begin + threadIdx.x; i < it.end; i += blockDim.x) {
+        const uint32_t c = d[i];
+        const int prev = i ? int(d[i - 1]) : -1;
+        atomicAdd(&mine[c], 1u);
+        if (int(c) == prev) atomicAdd(&mine[256 + c], 1u);
     }
     __syncthreads();
     uint32_t *out = counts + size_t(it.seg) * 512;
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        if (h[i]) atomicAdd(&out[i], h[i]);
-        if (e[i]) atomicAdd(&out[256 + i], e[i]);
+    for (uint32_t b = threadIdx.x; b < 512; b += blockDim.x) {
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < HIST0_C; c++) v += h[c * HIST0_ROW + b];
+        if (v) atomicAdd(&out[b], v);
     }
 }
 
 // Order-1 pair counts F[ctx][sym] over the compacted alphabet
 // (utils.h:280 hist1_4; context of byte 0 is 0).  `remap` maps a byte to
-// its alphabet index (alphabet always contains 0).  A*A <= 16384 bins in
-// LDS, otherwise straight to global memory.
+// its alphabet index (alphabet always contains 0).
+//   A*A < 16384: the bins live in LDS in C privatised copies (C = 32 down
+//                to 1 as A*A grows, within 64 KB);
+//   larger (packed bytes, A up to 256): 16-bit counters, two per LDS word,
+//                128 KB for all 65536 bins; a slice holds fewer than 65536
+//                bytes (HIST_SLICE) so no counter overflows.
+template <bool BIG>
 __global__ __launch_bounds__(256) void k_hist1(const Hist1Item *items,
                                                uint32_t *counts) {
     extern __shared__ uint32_t bins[];
     const Hist1Item it = items[blockIdx.x];
     const uint32_t A = it.A, nb = A * A;
-    const bool in_lds = nb <= 16384;
+    uint32_t C = 1;
+    if (!BIG)
+        while (C < 32 && 2 * C * (nb + 1) <= 16384) C *= 2;
+    const uint32_t row = nb + 1;
+    const uint32_t words = BIG ? (nb + 1) / 2 : C * row;
     __shared__ uint8_t rm[256];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) rm[i] = it.remap[i];
-    if (in_lds)
-        for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) bins[i] = 0;
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) bins[i] = 0;
     __syncthreads();
     uint32_t *gout = counts + it.out_off;
+    uint32_t *mine = bins + (threadIdx.x & (C - 1)) * row;
     const uint8_t *d = it.data;
     for (uint32_t i = it.begin + threadIdx.x; i < it.end; i += blockDim.x) {
         uint32_t c = rm[d[i]];
         uint32_t p = i ? rm[d[i - 1]] : rm[0];
         uint32_t b = p * A + c;
-        if (in_lds) atomicAdd(&bins[b], 1u);
-        else atomicAdd(&gout[b], 1u);
+        if (BIG) atomicAdd(&bins[b >> 1], 1u << (16 * (b & 1)));
+        else atomicAdd(&mine[b], 1u);
     }
-    if (in_lds) {
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x)
-            if (bins[i]) atomicAdd(&gout[i], bins[i]);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
+        uint32_t v = 0;
+        if (BIG) {
+            v = (bins[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+        } else {
+            for (uint32_t c = 0; c < C; c++) v += bins[c * row + i];
+        }
+        if (v) atomicAdd(&gout[i], v);
     }
 }
 
@@ -422,11 +439,17 @@ hipError_t launch_hist0(const HistItem *d_items, int nitems, uint32_t *d_counts,
     return hipGetLastError();
 }
 
-hipError_t launch_hist1(const Hist1Item *d_items, int nitems, uint32_t *d_counts,
+hipError_t launch_hist1(const Hist1Item *d_items, int nitems, uint32_t *d_counts, bool big,
                         hipStream_t s) {
     if (!nitems) return hipSuccess;
-    hipLaunchKernelGGL(k_hist1, dim3(nitems), dim3(256), 16384 * 4, s, d_items,
-                       d_counts);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_hist1<true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+        attr = true;
+    }
+    if (big) hipLaunchKernelGGL(k_hist1<true>, dim3(nitems), dim3(256), 131072, s, d_items, d_counts);
+    else hipLaunchKernelGGL(k_hist1<false>, dim3(nitems), dim3(256), 16384 * 4, s, d_items, d_counts);
     return hipGetLastError();
 }
 

@@ -9,11 +9,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ.setdefault("FQZ5_LIB_VARIANT", os.path.join(ROOT, "tools/variants/libfqz5_cprobe.so"))
 sys.path.insert(0, ROOT)
+import torch  # noqa: E402  (torch's HIP runtime first, as in tests/conftest.py)
+torch.cuda.init()
 from fqzcomp5_amd import lib, synth  # noqa: E402
 
 r = synth.illumina(int(sys.argv[1]) if len(sys.argv) > 1 else 290000, seed=1)
 so = lib.load()
-for name, data in (("seq", r.seq.tobytes()), ("qual", r.qual.tobytes())):
+for name, data in (("seq", r.seq.tobytes()), ("qual", r.qual.tobytes()))[:1 if "bench" in sys.argv else 2]:
     comp = lib.rans_compress(data, 0)
     back = lib.rans_uncompress(comp)
     p = (C.c_uint64 * 8)()
@@ -23,3 +25,34 @@ for name, data in (("seq", r.seq.tobytes()), ("qual", r.qual.tobytes())):
     print(f"{name} O0 ok={back == data} steps={T} total {tot} cyc ({tot/max(T,1):.1f}/step) "
           f"loop {ts} cyc over {ns} steps ({ts/max(ns,1):.1f}/step) clock {ghz:.3f} GHz "
           f"wall {real/100:.0f} us", flush=True)
+
+if len(sys.argv) > 2 and sys.argv[2] == "bench":
+    # the bench's -3 workload: the longest stream is job 0 of the decode launch
+    sys.argv = sys.argv[:1]
+    import bench
+    from fqzcomp5_amd import sections as S
+    reads, blocks = bench.make_blocks(1.0, seed=1, kind="illumina")
+    run = S.Run(reads, blocks, torch.device("cuda", 0))
+    enc_secs = run.enc_secs()
+    for rep in range(2):
+        res, meth_all, sizes, tried, off = S.encode_run(enc_secs, S.masks(3), S.new_state())
+        so.fqz5_profile(1)
+        dres = S.decode(run.dec_secs(res))
+        pr = (C.c_double * 6)()
+        so.fqz5_profile_read(pr)
+        so.fqz5_profile(0)
+        p = (C.c_uint64 * 8)()
+        so.fqz5_chain_probe_read(p)
+        tot, real, ts, ns, T = p[2], p[3], p[4], p[5], p[6]
+        print(f"bench launch: dec {pr[3]:.1f} ms; job0 steps={T} {tot/max(T,1):.1f} cyc/step "
+              f"loop {ts/max(ns,1):.1f}/step clock {tot/(real*10.0):.3f} GHz wall {real/100:.0f} us",
+              flush=True)
+        jt = (C.c_uint64 * (512 * 6))()
+        so.fqz5_chain_jobs_read(jt)
+        t0 = min(jt[6 * i] for i in range(len(dres)) if jt[6 * i])
+        for i in range(len(dres)):
+            a, b, cyc, k, lc, ls = jt[6 * i:6 * i + 6]
+            n = k >> 32
+            print(f"  job {i:2d} n={n:9d} xcc={(k >> 24) & 15} cu={(k >> 16) & 15} se={(k >> 8) & 7} "
+                  f"simd={k & 3} end {(b - t0) / 100:8.0f} us ns/step {(b - a) * 10 / max(n / 4, 1):.1f} "
+                  f"cyc/step {cyc / max(n / 4, 1):.1f} loop {lc / max(ls, 1):.1f} clock {cyc / max((b - a) * 10, 1):.3f} GHz")

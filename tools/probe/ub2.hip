@@ -60,6 +60,19 @@ __global__ void k(uint32_t *out, uint64_t *cyc, uint32_t a, uint32_t b) {
                 const uint32_t q = __umulhi(xr, 0x9e3779b1u) >> (a & 7);
                 x = __umul24(q, 3u) + (xr + 12345u);
             }
+            if (T == 14) {                                                  // fqz range step, f64 reciprocal
+                const double rd = __longlong_as_double((long long)(uint64_t(b) << 32 | a));
+                const uint32_t q = uint32_t(__fma_rn(double(x), rd, 1.0 / 524288.0));
+                x = q * (y | 1u);
+                x <<= __builtin_clz(x | 1u) & 24u;
+            }
+            if (T == 15) {                                                  // fqz range step, 48-bit magic
+                const uint32_t hi = __umulhi(x, a);
+                const uint64_t P = uint64_t(x) * (b & 0xffffu) + hi;
+                const uint32_t q = uint32_t(P >> 16);
+                x = q * (y | 1u);
+                x <<= __builtin_clz(x | 1u) & 24u;
+            }
             if (T == 10) {                                                  // full renorm select chain
                 const uint64_t m = __ballot(x < y);
                 const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
@@ -79,14 +92,15 @@ int main() {
     const char *names[] = {"ds_read_b64 chain", "v_add", "mad24", "lshr_b64+add", "perm+add",
                            "cmp+mbcnt", "cmp+cndmask", "and,lshl_add,ds_read,mad", "same + never-taken branch",
                            "same + ~68%-taken branch", "renorm select (cmp,mbcnt,lshl,lshr64,perm,cndmask)",
-                           "enc step cmp+cndmask", "enc step sign shift", "enc step sub borrow"};
+                           "enc step cmp+cndmask", "enc step sign shift", "enc step sub borrow",
+                           "fqz range step f64", "fqz range step int magic"};
 #define RUN(T) hipLaunchKernelGGL(k<T>, dim3(1), dim3(64), 0, 0, out, cyc, 12345u, 99999u);
     for (int rep = 0; rep < 2; rep++) {
-        RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13)
+        RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15)
     }
     hipDeviceSynchronize();
     uint64_t h[32];
     hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
-    for (int t = 0; t <= 13; t++) printf("T%-2d %-55s %7.1f cyc/step\n", t, names[t], double(h[t]) / N);
+    for (int t = 0; t <= 15; t++) printf("T%-2d %-55s %7.1f cyc/step\n", t, names[t], double(h[t]) / N);
     return 0;
 }
