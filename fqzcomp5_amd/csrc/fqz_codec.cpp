@@ -570,7 +570,20 @@ void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
             std::fprintf(stderr, "\n");
         }
     }
-    if (np) FQZ5_HIP(launch_fqz_model_pass(g.upload(jobs), np, g.stream));
+    if (np) {
+        // FQZ5_HOT_MIN overrides the hot-model threshold (tests: 1 sends every
+        // eligible quality model through k_fqz_model_hot; 0 disables it)
+        static const uint32_t hot_min = [] {
+            const char *e = std::getenv("FQZ5_HOT_MIN");
+            return e ? uint32_t(std::strtoul(e, nullptr, 10)) : FQZ_HOT_MIN;
+        }();
+        uint32_t stride = 1;
+        for (const FqzEvJob &J : jobs)
+            stride = std::max(stride, 1u + std::min(FQZ_M_SEL, J.nev / std::max(hot_min, 1u) + 1));
+        uint32_t *hot = g.arena.alloc_n<uint32_t>(size_t(stride) * size_t(np));
+        g.memset0(hot, size_t(stride) * size_t(np) * 4);
+        FQZ5_HIP(launch_fqz_model_pass(g.upload(jobs), np, hot, stride, hot_min, g.stream));
+    }
     // the range chain of every block (one wave each), then the output bytes
     for (int k = 0; k < np; k++) {
         FqzEvJob &J = par[size_t(k)]->w->J;

@@ -130,7 +130,12 @@ struct FqzEvJob {
 
 hipError_t launch_fqz_events(const FqzEvJob &j, int phase, hipStream_t s);
 // batched over the blocks of a request list: d_jobs in device memory
-hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
+// hot: per job a list of stride words (zeroed); models with at least hot_min
+// events go to the one-wave-per-model kernel (hot_min = 0: none do)
+constexpr uint32_t FQZ_HOT_GRID = 64;            // waves per job for hot models
+constexpr uint32_t FQZ_HOT_MIN = 16384;
+hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t *hot,
+                                 uint32_t stride, uint32_t hot_min, hipStream_t s);
 hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
 hipError_t launch_fqz_carry(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
 hipError_t launch_fqz_expand(const FqzEvJob &j, hipStream_t s);

@@ -397,7 +397,15 @@ template <int CAP> DEV void model_run(FList<CAP> *m, const FqzEvJob &J, uint32_t
 
 // one launch for a batch of blocks: workgroup b handles models
 // [256 (b % nblk), +256) of block b / nblk
-__global__ __launch_bounds__(256) void k_fqz_model_pass(const FqzEvJob *Js, uint32_t nblk) {
+// Hot quality models (at least hot_min events, at most FQZ_HOT_LIVE live
+// symbols) go to k_fqz_model_hot instead; hot_min = 0 disables that path.
+constexpr uint32_t FQZ_HOT_LIVE = 62;            // slots 0..live+1 in 64 lanes
+DEV bool fqz_is_hot(uint32_t m, uint32_t cnt, uint32_t live, uint32_t hot_min) {
+    return hot_min && m < FQZ_M_SEL && live <= FQZ_HOT_LIVE && cnt >= hot_min;
+}
+
+__global__ __launch_bounds__(256) void k_fqz_model_pass(const FqzEvJob *Js, uint32_t nblk,
+                                                        uint32_t hot_min) {
     FList<FQZ_QSYMS> *lm = reinterpret_cast<FList<FQZ_QSYMS> *>(fqz_lds);   // 256 models
     const FqzEvJob J = load_job(Js + blockIdx.x / nblk);
     const uint32_t m = (blockIdx.x % nblk) * blockDim.x + threadIdx.x;
@@ -405,6 +413,7 @@ __global__ __launch_bounds__(256) void k_fqz_model_pass(const FqzEvJob *Js, uint
     const uint32_t lo = J.seg_lo[m], hi = J.seg_hi[m];
     if (lo >= hi) return;
     const FqzDevGlobal &g = *J.g;
+    if (fqz_is_hot(m, hi - lo, g.max_sym + 1, hot_min)) return;
     if (m < FQZ_M_SEL) {
         FList<FQZ_QSYMS> *ml = &lm[threadIdx.x];
         fl_init(ml, int(g.max_sym) + 1);
@@ -418,6 +427,117 @@ __global__ __launch_bounds__(256) void k_fqz_model_pass(const FqzEvJob *Js, uint
                        (m - FQZ_M_REV);
         fl_init(mg, 2);
         model_run(mg, J, lo, hi);
+    }
+}
+
+// The hot models of each block: list[0] = count, list[1..] = model ids.
+__global__ void k_fqz_hot_list(const FqzEvJob *Js, uint32_t *hot, uint32_t stride,
+                               uint32_t hot_min) {
+    const FqzEvJob &J = Js[blockIdx.y];
+    const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= FQZ_M_SEL) return;
+    const uint32_t lo = J.seg_lo[m], hi = J.seg_hi[m];
+    if (hi <= lo || !fqz_is_hot(m, hi - lo, J.g->max_sym + 1, hot_min)) return;
+    uint32_t *list = hot + size_t(blockIdx.y) * stride;
+    const uint32_t k = atomicAdd(list, 1u);
+    if (k + 1 < stride) list[1 + k] = m;
+}
+
+// Phase 3, hot models: one wave per model with the list in lanes (lane k =
+// slot k: fr, cum = the sum of fr over slots 1..k-1, sy) and the model's
+// events in chunks of 64, one per lane.  Runs of events that hit the head
+// symbol are coded in parallel in closed form (event n of a run: cum 0,
+// freq f1 + 16n, total tot + 16n, while no halving is due), every other
+// event takes the list update (fl_bump: +16, halve past FL_MAX, one bubble
+// step) with ballots and readlanes.  Codes are identical to
+// model_run's.
+__global__ __launch_bounds__(64) void k_fqz_model_hot(const FqzEvJob *Js, const uint32_t *hot,
+                                                      uint32_t stride) {
+    const FqzEvJob J = load_job(Js + blockIdx.y);
+    const uint32_t *list = hot + size_t(blockIdx.y) * stride;
+    const uint32_t nh = min(__builtin_amdgcn_readfirstlane(list[0]), stride - 1);
+    const uint32_t L = __builtin_amdgcn_readfirstlane(J.g->max_sym) + 1;   // live symbols
+    const uint32_t l = threadIdx.x;
+    const auto rsv = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(J.sval), 0,
+                                                       J.nev * 8u, 0x00020000);
+    const uint64_t slots = ((L >= 63 ? ~0ull : (2ull << L) - 1)) & ~1ull;   // lanes 1..L
+    for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
+        const uint32_t m = __builtin_amdgcn_readfirstlane(list[1 + h]);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane(J.seg_lo[m]);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane(J.seg_hi[m]);
+        // fl_init(live = L)
+        uint32_t fr = l == 0 ? FL_MAX : (l <= L ? 1u : 0u);
+        uint32_t cum = l == 0 ? 0u : (l <= L + 1 ? l - 1 : L);
+        uint32_t sy = l ? l - 1 : 0u;
+        uint32_t tot = L;
+        uint32_t sn = __builtin_amdgcn_raw_buffer_load_b32(rsv, (lo + l) * 8u, 0, 0);
+        for (uint32_t k0 = lo; k0 < hi; k0 += 64) {
+            const uint32_t sym = sn & 0xffu;
+            if (k0 + 64 < hi) sn = __builtin_amdgcn_raw_buffer_load_b32(rsv, (k0 + 64 + l) * 8u, 0, 0);
+            const uint32_t nv = min(64u, hi - k0);
+            uint64_t P = nv == 64 ? ~0ull : ((1ull << nv) - 1);
+            uint32_t s1 = __builtin_amdgcn_readlane(sy, 1), f1 = __builtin_amdgcn_readlane(fr, 1);
+            uint64_t *code = J.code + k0;
+            while (P) {
+                // ---- a run of head hits, coded in parallel ----------------
+                const uint32_t start = uint32_t(__builtin_ctzll(P));
+                const uint64_t miss = P & ~uint64_t(__ballot(sym == s1));
+                uint32_t run = (miss ? uint32_t(__builtin_ctzll(miss)) : nv) - start;
+                const uint32_t cap = tot < FL_MAX ? (FL_MAX - tot) / FL_STEP : 0u;
+                run = min(run, cap);
+                if (run) {
+                    if (l >= start && l < start + run) {
+                        const uint32_t n = l - start;
+                        code[l] = (uint64_t(f1 + FL_STEP * n) << 16) |
+                                  (uint64_t(tot + FL_STEP * n) << 32);
+                    }
+                    fr += l == 1 ? FL_STEP * run : 0u;
+                    cum += l >= 2 ? FL_STEP * run : 0u;
+                    f1 += FL_STEP * run;
+                    tot += FL_STEP * run;
+                    P &= ~(((run == 64) ? ~0ull : ((1ull << run) - 1)) << start);
+                    if (!P) break;
+                }
+                // ---- one event through fl_bump ----------------------------
+                const uint32_t j0 = uint32_t(__builtin_ctzll(P));
+                const uint32_t sj = __builtin_amdgcn_readlane(sym, j0);
+                const uint64_t sm = uint64_t(__ballot(sy == sj)) & slots;
+                const uint32_t sl = sm ? uint32_t(__builtin_ctzll(sm)) : L + 1;   // always found
+                const uint32_t fs = __builtin_amdgcn_readlane(fr, sl);
+                const uint32_t cs = __builtin_amdgcn_readlane(cum, sl);
+                if (l == j0) code[l] = uint64_t(cs) | (uint64_t(fs) << 16) | (uint64_t(tot) << 32);
+                fr += l == sl ? FL_STEP : 0u;
+                cum += l > sl ? FL_STEP : 0u;
+                tot += FL_STEP;
+                if (tot > FL_MAX) {                 // halve slots 1..L, rebuild cum
+                    const bool live = l >= 1 && l <= L;
+                    if (live) fr -= fr >> 1;
+                    const uint32_t x = live ? fr : 0u;
+                    uint32_t inc = x;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t o = __shfl_up(inc, d, 64);
+                        if (int(l) >= d) inc += o;
+                    }
+                    if (l >= 1) cum = inc - x;
+                    tot = __builtin_amdgcn_readlane(inc, 63);
+                }
+                if (sl >= 2) {                      // one bubble step
+                    const uint32_t fa = __builtin_amdgcn_readlane(fr, sl - 1);
+                    const uint32_t fb = __builtin_amdgcn_readlane(fr, sl);
+                    if (fb > fa) {
+                        const uint32_t sa = __builtin_amdgcn_readlane(sy, sl - 1);
+                        const uint32_t sb = __builtin_amdgcn_readlane(sy, sl);
+                        const uint32_t ca = __builtin_amdgcn_readlane(cum, sl - 1);
+                        if (l == sl - 1) { fr = fb; sy = sb; }
+                        if (l == sl) { fr = fa; sy = sa; cum = ca + fb; }
+                    }
+                }
+                s1 = __builtin_amdgcn_readlane(sy, 1);
+                f1 = __builtin_amdgcn_readlane(fr, 1);
+                P &= ~(1ull << j0);
+            }
+        }
     }
 }
 
@@ -617,7 +737,8 @@ hipError_t launch_fqz_expand(const FqzEvJob &j, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, hipStream_t s) {
+hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t *hot,
+                                 uint32_t stride, uint32_t hot_min, hipStream_t s) {
     constexpr uint32_t lds = 256 * sizeof(FList<FQZ_QSYMS>);
     constexpr uint32_t nblk = (FQZ_NMODELS + 255) / 256;
     static bool attr = false;
@@ -626,9 +747,15 @@ hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, hipStream_t 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr = true;
     }
-    if (njobs)
-        hipLaunchKernelGGL(k_fqz_model_pass, dim3(nblk * uint32_t(njobs)), dim3(256), lds, s,
-                           d_jobs, nblk);
+    if (!njobs) return hipSuccess;
+    if (hot_min) {
+        hipLaunchKernelGGL(k_fqz_hot_list, dim3((FQZ_M_SEL + 255) / 256, njobs), dim3(256), 0, s,
+                           d_jobs, hot, stride, hot_min);
+        hipLaunchKernelGGL(k_fqz_model_hot, dim3(FQZ_HOT_GRID, njobs), dim3(64), 0, s, d_jobs,
+                           hot, stride);
+    }
+    hipLaunchKernelGGL(k_fqz_model_pass, dim3(nblk * uint32_t(njobs)), dim3(256), lds, s,
+                       d_jobs, nblk, hot_min);
     return hipGetLastError();
 }
 
