@@ -10,7 +10,10 @@
 // side by side, so the extra candidates cost little wall time), then the
 // trial state machine is replayed on the host in block order, which gives
 // exactly the choices of a single-threaded (-t1) reference run.
+#include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <thread>
 #include <deque>
 #include <vector>
 
@@ -144,7 +147,10 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                       uint32_t *sizes) {
     try {
         GpuCtx &g = gpu();
-        if (t_sess.open) g.reset();
+        if (t_sess.open) {
+            g.reset();
+            gpu_aux().reset();
+        }
         t_sess = TrySession();
         for (int i = 0; i < nsec; i++) {
             if (masks[i] & ~(RANS_MASK | FQZ_MASK))
@@ -175,8 +181,34 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 reqs.push_back(std::move(r));
             }
         }
-        compress_batch(g, reqs);
-        if (!t_sess.fqz.empty()) fqz_encode_batch(g, t_sess.fqz);
+        // The fqz candidates (trial blocks) run on the thread's second
+        // context from a helper thread, beside the rANS candidates: both are
+        // a few long chains that leave most of the GPU idle.
+        static const bool no_aux = std::getenv("FQZ5_NO_AUX") != nullptr;
+        if (!t_sess.fqz.empty() && !no_aux) {
+            GpuCtx &ga = gpu_aux();
+            std::vector<FqzEncReq> &fq = t_sess.fqz;   // (t_sess is this thread's)
+            std::exception_ptr err;
+            std::thread th([&ga, &fq, &err] {
+                try {
+                    FQZ5_HIP(hipSetDevice(ga.device));
+                    fqz_encode_batch(ga, fq);
+                } catch (...) {
+                    err = std::current_exception();
+                }
+            });
+            try {
+                compress_batch(g, reqs);
+            } catch (...) {
+                th.join();
+                throw;
+            }
+            th.join();
+            if (err) std::rethrow_exception(err);
+        } else {
+            compress_batch(g, reqs);
+            if (!t_sess.fqz.empty()) fqz_encode_batch(g, t_sess.fqz);
+        }
         t_sess.open = true;
         // sizes as compress_with_methods sees them: UINT_MAX when not run,
         // 0 when the codec returned NULL (out_len = *out_size = 0)
@@ -193,6 +225,7 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         fqz5_set_error(e.what());
         t_sess = TrySession();
         try { gpu().reset(); } catch (...) {}
+        try { gpu_aux().reset(); } catch (...) {}
         return -1;
     }
 }

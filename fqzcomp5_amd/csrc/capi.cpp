@@ -21,6 +21,15 @@ GpuCtx &gpu() {
     return *g_ctx;
 }
 
+// The calling thread's second context: its own streams and arenas, for
+// work the thread hands to a helper thread to run beside its own
+// (fqz5_sections_try: fqz candidates beside the rANS candidates).
+static thread_local std::unique_ptr<GpuCtx> g_aux;
+GpuCtx &gpu_aux() {
+    if (!g_aux) g_aux.reset(new GpuCtx());
+    return *g_aux;
+}
+
 // Size a stream decodes to, from its header (needed when the caller did
 // not give an output buffer).  0 with ok=false if it cannot be known.
 static uint32_t header_size(const uint8_t *in, uint32_t len, bool *ok) {

@@ -207,5 +207,8 @@ struct GpuCtx {
 
 // The calling thread's context (created on first use).
 GpuCtx &gpu();
+// A second context of the calling thread, for work run by a helper thread
+// concurrently with the thread's own (created on first use).
+GpuCtx &gpu_aux();
 
 }  // namespace fqz5
