@@ -13,6 +13,9 @@ is one pass of the hot path over the whole workload, inputs resident in HBM:
     decode  every chosen stream back to bytes.
 
 `value` = seq+qual section bytes of all ranks / step time (max over ranks).
+The default run adds configs[2] as the `level5` line item: a synthetic 4 GB
+NovaSeq FASTQ per GPU at -5 (fqzcomp_qual FQZ1/FQZ3 in the codec trial),
+timed with the same rules (`--no-level5` skips it).
 Names (tok3/LZP) and LZP3 for sequences are the next rows of SURVEY §8f
 and are not in the workload.  Multi-GPU: one process per GPU, weak scaling
 (each rank adds its own 1 GB file to the run); the only collective is the
@@ -130,38 +133,20 @@ def cpu_baseline(run, tried, meth, gpu_out, threads):
             "bytes_match_gpu": bool(same), "roundtrip": bool(rt)}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--gb", type=float, default=1.0)
-    ap.add_argument("--level", type=int, default=3, choices=[1, 3, 5])
-    ap.add_argument("--kind", default="illumina", choices=["illumina", "novaseq"])
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    args = ap.parse_args()
-
+def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local, dist):
+    """One workload: warmup + `steps` timed steps (barrier + synchronize on
+    both sides, max over ranks) and the result fields of the JSON line."""
     import torch
-    import torch.distributed as dist
     from fqzcomp5_amd import lib, sections as S
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    if not lib.device_ok():
-        raise SystemExit("no GPU: " + lib.last_error())
-
     t0 = time.time()
-    reads, blocks = make_blocks(args.gb, seed=1 + rank, kind=args.kind)
-    log(f"[bench] generated {len(blocks)} blocks/rank in {time.time()-t0:.1f}s")
+    reads, blocks = make_blocks(gb, seed=(1 if level <= 3 else 2) + rank, kind=kind)
+    log(f"[bench] -{level} {kind} {gb:g} GB: generated {len(blocks)} blocks/rank in "
+        f"{time.time()-t0:.1f}s")
     dev = torch.device("cuda", local)
     run = S.Run(reads, blocks, dev)
     enc_secs = run.enc_secs()
-    avail = S.masks(args.level)
+    avail = S.masks(level)
     in_bytes_local = run.in_bytes
 
     def step():
@@ -170,7 +155,7 @@ def main():
         dres = S.decode(run.dec_secs(res))
         return res, dres, meth_all, tried, off
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     so = lib.load()
     so.fqz5_profile(1)
@@ -178,7 +163,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         res, dres, meth_all, tried, off = step()
     torch.cuda.synchronize()
     if world > 1:
@@ -198,24 +183,14 @@ def main():
     ok = all(r.status == 0 for r in res) and all(r.status == 0 for r in dres)
     ok = ok and run.roundtrip_ok()
     comp_bytes = sum(9 + r.clen for r in res)
-    quals = "8-level binned quals" if args.kind == "illumina" else "NovaSeq 4-level i.i.d. quals"
-
+    quals = "8-level binned quals" if kind == "illumina" else "NovaSeq 4-level i.i.d. quals"
     out = {
-        "metric": "input MB/s encode+decode, 100MB blocks, -3 and -5; bit-exact vs CPU",
-        "value": round(float(tot_bytes.item()) * args.steps / dt / 1e6, 2),
-        "unit": "MB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 2),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": f"synthetic (seeded {args.kind} 150 bp, {quals})",
-        "config": {"workload": f"fqzcomp5 -{args.level} seq+qual sections of a "
-                               f"{args.gb:g} GB FASTQ per GPU, 100 MB blocks",
-                   "blocks_per_gpu": len(blocks), "level": args.level,
+        "value": round(float(tot_bytes.item()) * steps / dt / 1e6, 2),
+        "ms_per_step": round(dt / steps * 1e3, 2),
+        "data": f"synthetic (seeded {kind} 150 bp, {quals})",
+        "config": {"workload": f"fqzcomp5 -{level} seq+qual sections of a "
+                               f"{gb:g} GB FASTQ per GPU, 100 MB blocks",
+                   "blocks_per_gpu": len(blocks), "level": level,
                    "section_bytes_per_gpu": in_bytes_local,
                    "compressed_bytes_per_gpu": comp_bytes,
                    "methods": sorted({int(m) for m in meth_all}),
@@ -246,11 +221,59 @@ def main():
                                   "dec_ns_per_step_longest": round(
                                       dec_ms / max(dec_n, 1) * 1e6 / max(longest // 4, 1), 2)}}
     # ---- CPU baseline (rank 0, N=1) -----------------------------------------
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and cpu:
         gpu_streams = [run.chosen(res, i) for i in range(len(res))]
-        threads = min(args.cpu_threads, os.cpu_count() or 1)
+        threads = min(cpu_threads, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(run, tried[off:off + len(res)],
                                            meth_all[off:off + len(res)], gpu_streams, threads)
+    del run, reads
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--gb", type=float, default=1.0)
+    ap.add_argument("--level", type=int, default=3, choices=[1, 3, 5])
+    ap.add_argument("--kind", default="illumina", choices=["illumina", "novaseq"])
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-level5", action="store_true",
+                    help="skip the configs[2] (-5 NovaSeq 4 GB) line item")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from fqzcomp5_amd import lib
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if not lib.device_ok():
+        raise SystemExit("no GPU: " + lib.last_error())
+
+    m = measure(args.level, args.kind, args.gb, args.steps, args.warmup, not args.no_cpu,
+                args.cpu_threads, world, rank, local, dist)
+    out = {"metric": "input MB/s encode+decode, 100MB blocks, -3 and -5; bit-exact vs CPU",
+           "value": m["value"], "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": m["ms_per_step"], "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": m["data"],
+           "config": m["config"], "roofline": m["roofline"]}
+    if "cpu_baseline" in m:
+        out["cpu_baseline"] = m["cpu_baseline"]
+    # The metric covers -3 and -5: the default run adds configs[2] (-5,
+    # fqzcomp_qual candidates in the trial, 4 GB NovaSeq per GPU) as its own
+    # line item with the same timing rules; `value` stays configs[1] (-3).
+    if not args.no_level5 and args.level == 3:
+        m5 = measure(5, "novaseq", 4.0, args.steps, args.warmup, not args.no_cpu,
+                     args.cpu_threads, world, rank, local, dist)
+        out["level5"] = m5
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

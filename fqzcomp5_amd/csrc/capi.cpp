@@ -2,7 +2,10 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
+#include <cstdio>
 #include <string>
 
 #include "../../include/fqz5_mi355x.h"
@@ -10,6 +13,7 @@
 #include "rans_format.hpp"
 #include "fqz_kernels.h"
 #include "arith_kernels.h"
+#include "fqz_codec.hpp"
 
 namespace fqz5 {
 
@@ -20,6 +24,22 @@ GpuCtx &gpu() {
     if (!g_ctx) g_ctx.reset(new GpuCtx());
     return *g_ctx;
 }
+
+#ifdef FQZ5_COPY_STATS
+// diagnostics build (tools/build_variant.sh): host<->device copies per call site
+struct CopyStats {
+    std::mutex mu;
+    std::map<std::string, uint64_t> n;
+    ~CopyStats() {
+        for (auto &kv : n) std::fprintf(stderr, "copies %8llu %s\n", (unsigned long long)kv.second, kv.first.c_str());
+    }
+};
+static CopyStats g_cs;
+void GpuCtx::copy_stat(const char *kind, const char *file, int line) {
+    std::lock_guard<std::mutex> lk(g_cs.mu);
+    g_cs.n[std::string(kind) + " " + file + ":" + std::to_string(line)]++;
+}
+#endif
 
 // The calling thread's second context: its own streams and arenas, for
 // work the thread hands to a helper thread to run beside its own
@@ -270,6 +290,8 @@ int fqz5_device_ok(void) {
 }
 
 const char *fqz5_last_error(void) { return g_err.c_str(); }
+
+unsigned fqz5_set_hot_min(unsigned min_events) { return fqz_set_hot_min(min_events); }
 
 void fqz5_profile(int on) {
     try {

@@ -1,3 +1,4 @@
+#include <atomic>
 // fqz_codec.cpp — fqz_compress / fqz_decompress on the GPU
 // (htscodecs fqzcomp_qual.c:1008-1646, fork ABI).
 //
@@ -414,6 +415,19 @@ struct FqzEncReq::Work {
 // parameters (statistics kernels, host decisions), events, sort, the
 // per-model pass (one launch for all blocks), the range chain (one launch,
 // one wave per block), the big-number bytes (carry: one launch).
+// The hot-model threshold (fqz5_set_hot_min; $FQZ5_HOT_MIN overrides the
+// default; 1 sends every eligible quality model through k_fqz_model_hot,
+// 0 none).
+static std::atomic<uint32_t> &hot_min_var() {
+    static std::atomic<uint32_t> v([] {
+        const char *e = std::getenv("FQZ5_HOT_MIN");
+        return e ? uint32_t(std::strtoul(e, nullptr, 10)) : FQZ_HOT_MIN;
+    }());
+    return v;
+}
+uint32_t fqz_hot_min() { return hot_min_var().load(); }
+uint32_t fqz_set_hot_min(uint32_t v) { return hot_min_var().exchange(v); }
+
 void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
     std::vector<FqzEncReq *> par;
     for (FqzEncReq &R : reqs) {
@@ -571,12 +585,7 @@ void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         }
     }
     if (np) {
-        // FQZ5_HOT_MIN overrides the hot-model threshold (tests: 1 sends every
-        // eligible quality model through k_fqz_model_hot; 0 disables it)
-        static const uint32_t hot_min = [] {
-            const char *e = std::getenv("FQZ5_HOT_MIN");
-            return e ? uint32_t(std::strtoul(e, nullptr, 10)) : FQZ_HOT_MIN;
-        }();
+        const uint32_t hot_min = fqz_hot_min();
         uint32_t stride = 1;
         for (const FqzEvJob &J : jobs)
             stride = std::max(stride, 1u + std::min(FQZ_M_SEL, J.nev / std::max(hot_min, 1u) + 1));

@@ -29,6 +29,8 @@ struct FqzEncReq {
     struct Work;
     std::shared_ptr<Work> w;
 };
+uint32_t fqz_hot_min();
+uint32_t fqz_set_hot_min(uint32_t v);
 void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs);
 
 struct FqzDecReq {

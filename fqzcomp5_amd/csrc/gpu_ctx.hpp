@@ -181,7 +181,16 @@ struct GpuCtx {
     }
     void sync() { FQZ5_HIP(hipStreamSynchronize(stream)); }
 
-    template <class T> T *upload(const T *h, size_t n) {
+#ifdef FQZ5_COPY_STATS
+    static void copy_stat(const char *kind, const char *file, int line);
+#define FQZ5_CS_ARGS , const char *file_ = __builtin_FILE(), int line_ = __builtin_LINE()
+#define FQZ5_CS(kind) copy_stat(kind, file_, line_)
+#else
+#define FQZ5_CS_ARGS
+#define FQZ5_CS(kind)
+#endif
+    template <class T> T *upload(const T *h, size_t n FQZ5_CS_ARGS) {
+        FQZ5_CS("up");
         T *d = arena.alloc_n<T>(n ? n : 1);
         if (n) {
             uint8_t *st = staging.alloc(n * sizeof(T));
@@ -196,8 +205,15 @@ struct GpuCtx {
         arena.reset();
         staging.reset();
     }
-    template <class T> T *upload(const std::vector<T> &v) { return upload(v.data(), v.size()); }
-    template <class T> void download(T *h, const T *d, size_t n) {
+    template <class T> T *upload(const std::vector<T> &v FQZ5_CS_ARGS) {
+#ifdef FQZ5_COPY_STATS
+        return upload(v.data(), v.size(), file_, line_);
+#else
+        return upload(v.data(), v.size());
+#endif
+    }
+    template <class T> void download(T *h, const T *d, size_t n FQZ5_CS_ARGS) {
+        FQZ5_CS("down");
         if (n) FQZ5_HIP(hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, stream));
     }
     void memset0(void *d, size_t n) {

@@ -491,14 +491,28 @@ void Compressor::stage_encode() {
         return jobs_[a].n / jobs_[a].nx > jobs_[b].n / jobs_[b].nx;
     });
     uint32_t *d_lens = g_.arena.alloc_n<uint32_t>(jobs_.size());
+    // every job's symbol table and O1 remap in one upload each (a stripe
+    // candidate set is thousands of small jobs)
+    std::vector<size_t> tab_off(jobs_.size()), rm_off(jobs_.size());
+    std::vector<EncSym> all_syms;
+    std::vector<uint8_t> all_rm;
+    for (int i : order) {
+        const EJ &j = jobs_[i];
+        tab_off[i] = all_syms.size();
+        all_syms.insert(all_syms.end(), j.syms.begin(), j.syms.end());
+        rm_off[i] = all_rm.size();
+        if (j.o1) all_rm.insert(all_rm.end(), j.remap, j.remap + 256);
+    }
+    const EncSym *d_syms = g_.upload(all_syms);
+    const uint8_t *d_rms = all_rm.empty() ? nullptr : g_.upload(all_rm);
     for (int i : order) {
         EJ &j = jobs_[i];
         if (!j.h_in.empty()) j.d_in = g_.upload(j.h_in);
-        const EncSym *d_tab = g_.upload(j.syms);
+        const EncSym *d_tab = d_syms + tab_off[i];
         const size_t cap = 2 * size_t(j.n) + 16 * size_t(j.nx) + 1088;
         uint8_t *base = g_.arena.alloc_n<uint8_t>(cap);
         j.d_end = base + (cap & ~size_t(15));
-        const uint8_t *d_remap = j.o1 ? g_.upload(j.remap, 256) : nullptr;
+        const uint8_t *d_remap = j.o1 ? d_rms + rm_off[i] : nullptr;
         const uint32_t steps = j.o1 ? j.n - uint32_t(j.nx - 1) * (j.n / uint32_t(j.nx))
                                     : (j.n + uint32_t(j.nx) - 1) / uint32_t(j.nx);
         const uint32_t S = enc_chunk_steps(j.nx);

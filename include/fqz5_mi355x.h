@@ -182,6 +182,13 @@ const char *fqz5_last_error(void);
 void fqz5_profile(int on);
 void fqz5_profile_read(double *out6);
 
+/* fqz encoder: quality models with at least `min_events` events in a block
+ * are run one wavefront per model (the list in lanes); smaller ones one
+ * lane per model.  0 disables the per-model wavefronts; the default is
+ * 16384 (or $FQZ5_HOT_MIN).  Output bytes do not depend on it.  Returns the
+ * previous value. */
+unsigned fqz5_set_hot_min(unsigned min_events);
+
 /* Device check of the fqz decoder's division: floor(n / t) computed as
  * (u32)fma(n, recip(t), 2^-19) for every t < 2^16 and ~2000 n each.
  * Returns the number of mismatches (0), or -1 on a device error. */

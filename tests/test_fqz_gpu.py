@@ -125,3 +125,35 @@ def test_fqz_truncated_vs_oracle(golden):
             except RuntimeError:
                 got = None
             assert got == exp, (strat, at)
+
+
+@pytest.mark.parametrize("hot_min", [1, 0])
+def test_fqz_model_pass_paths(golden, hot_min):
+    """The encoder's model pass has two forms (fqz5_set_hot_min): one wave per
+    quality model with the list in lanes (runs of head hits coded in closed
+    form) and one lane per model.  hot_min=1 sends every eligible model
+    through the first, 0 none: both give the reference's bytes, including a
+    skewed block whose hottest models halve their lists many times."""
+    so = lib.load()
+    prev = so.fqz5_set_hot_min(hot_min)
+    try:
+        cs, vec, _ = golden
+        bad = []
+        for v in vec:
+            name, q, lens, flags, seq = cs[v["case"]]
+            out = lib.fqz_compress(q, lens.copy(), flags.copy(), v["strat"], seq)
+            if (len(out), hashlib.md5(out).hexdigest()) != (v["len"], v["md5"]):
+                bad.append((v["case"], v["strat"]))
+        assert not bad, bad
+        ora = binding.oracle()
+        rng = np.random.default_rng(5)
+        nrec = 3000
+        lens = np.full(nrec, 150, np.uint32)
+        p = np.array([.90, .06, .03, .01])
+        q = np.array([2, 12, 23, 37], np.uint8)[rng.choice(4, int(lens.sum()), p=p)].tobytes()
+        for strat in (1, 3):
+            exp = ora.fqz_compress(q, lens.copy(), np.zeros(nrec, np.uint32), strat)
+            got = lib.fqz_compress(q, lens.copy(), np.zeros(nrec, np.uint32), strat)
+            assert got == exp, strat
+    finally:
+        so.fqz5_set_hot_min(prev)

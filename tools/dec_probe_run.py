@@ -56,3 +56,30 @@ if len(sys.argv) > 2 and sys.argv[2] == "bench":
             print(f"  job {i:2d} n={n:9d} xcc={(k >> 24) & 15} cu={(k >> 16) & 15} se={(k >> 8) & 7} "
                   f"simd={k & 3} end {(b - t0) / 100:8.0f} us ns/step {(b - a) * 10 / max(n / 4, 1):.1f} "
                   f"cyc/step {cyc / max(n / 4, 1):.1f} loop {lc / max(ls, 1):.1f} clock {cyc / max((b - a) * 10, 1):.3f} GHz")
+
+if len(sys.argv) > 2 and sys.argv[2] == "same":
+    # one stream decoded by 20 / 80 waves of one launch: per-CU spread of a
+    # chain with identical data
+    data = r.seq.tobytes()
+    comp = lib.rans_compress(data, 0)
+    cin = torch.frombuffer(bytearray(comp), dtype=torch.uint8).cuda()
+    for nj in (20, 80):
+        outs = [torch.empty(len(data), dtype=torch.uint8, device="cuda") for _ in range(nj)]
+        jobs = [lib.RansJob(cin.data_ptr(), o.data_ptr(), len(comp), len(data), 0, 0, 0, 0) for o in outs]
+        lib.uncompress_batch_dev(jobs)
+        jt = (C.c_uint64 * (512 * 6))()
+        so.fqz5_chain_jobs_read(jt)
+        cyc = [jt[6 * i + 2] / (len(data) / 4) for i in range(nj)]
+        lp = [jt[6 * i + 4] / max(jt[6 * i + 5], 1) for i in range(nj)]
+        xcc = [(jt[6 * i + 3] >> 24) & 15 for i in range(nj)]
+        ok = all(bytes(o.cpu().numpy()) == data for o in outs[:2])
+        print(f"same stream x{nj}: ok={ok} cyc/step min {min(cyc):.1f} max {max(cyc):.1f}; "
+              f"loop min {min(lp):.1f} max {max(lp):.1f}", flush=True)
+        info = [jt[6 * i + 3] for i in range(nj)]
+        from collections import defaultdict
+        for name, f in (("simd", lambda k: k & 3), ("cu", lambda k: (k >> 16) & 15),
+                        ("se", lambda k: (k >> 8) & 7), ("xcc", lambda k: (k >> 24) & 15)):
+            d = defaultdict(list)
+            for k, c in zip(info, lp):
+                d[f(k)].append(c)
+            print(f"  by {name}:", {key: (len(v), round(sum(v) / len(v), 1)) for key, v in sorted(d.items())}, flush=True)
