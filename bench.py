@@ -57,12 +57,13 @@ def make_blocks(gb: float, seed: int, kind: str):
     return r, synth.split_blocks(r, BLK)
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, tag: str = ""):
     """HBM bytes per dispatch of `kernel` from the newest committed PMC
-    summary (profiles/rNN_pmc.json, written by tools/pmc_summary.py from
-    separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    summary of this workload (profiles/rNN_pmc{tag}.json, written by
+    tools/pmc_summary.py from separate rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes of this bench; tag "" = configs[1] -3, "_l5" = configs[2] -5)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_pmc{tag}.json")))
     if not files:
         return None, None
     ks = json.load(open(files[-1]))["kernels"]
@@ -133,7 +134,8 @@ def cpu_baseline(run, tried, meth, gpu_out, threads):
             "bytes_match_gpu": bool(same), "roundtrip": bool(rt)}
 
 
-def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local, dist):
+def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local, dist,
+            pmc_tag=""):
     """One workload: warmup + `steps` timed steps (barrier + synchronize on
     both sides, max over ranks) and the result fields of the JSON line."""
     import torch
@@ -205,7 +207,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
         name, ms, n, b = "k_rans_dec", dec_ms, dec_n, dec_b
     avg_ms = ms / max(n, 1)
     ach = (b / max(n, 1)) / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
-    traffic, tsrc = pmc_traffic(name)
+    traffic, tsrc = pmc_traffic(name, pmc_tag)
     # the decode launch is bound by its longest rANS chain: one step = one
     # symbol on each of the 4 interleaved states
     longest = max((e - s) for _, s, e, _, _ in run.spans)
@@ -259,7 +261,8 @@ def main():
         raise SystemExit("no GPU: " + lib.last_error())
 
     m = measure(args.level, args.kind, args.gb, args.steps, args.warmup, not args.no_cpu,
-                args.cpu_threads, world, rank, local, dist)
+                args.cpu_threads, world, rank, local, dist,
+                pmc_tag="_l5" if args.level == 5 else "")
     out = {"metric": "input MB/s encode+decode, 100MB blocks, -3 and -5; bit-exact vs CPU",
            "value": m["value"], "unit": "MB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": m["ms_per_step"], "higher_is_better": True,
@@ -272,7 +275,7 @@ def main():
     # line item with the same timing rules; `value` stays configs[1] (-3).
     if not args.no_level5 and args.level == 3:
         m5 = measure(5, "novaseq", 4.0, args.steps, args.warmup, not args.no_cpu,
-                     args.cpu_threads, world, rank, local, dist)
+                     args.cpu_threads, world, rank, local, dist, pmc_tag="_l5")
         out["level5"] = m5
     if rank == 0:
         print(json.dumps(out), flush=True)
