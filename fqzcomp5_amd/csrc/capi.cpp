@@ -41,6 +41,11 @@ void GpuCtx::copy_stat(const char *kind, const char *file, int line) {
 }
 #endif
 
+bool hedge_chains() {
+    static const bool on = std::getenv("FQZ5_NO_HEDGE") == nullptr;
+    return on;
+}
+
 // The calling thread's second context: its own streams and arenas, for
 // work the thread hands to a helper thread to run beside its own
 // (fqz5_sections_try: fqz candidates beside the rANS candidates).

@@ -602,7 +602,17 @@ void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         J.shifts = g.arena.alloc_n<uint32_t>(J.nev + 1);
         jobs[size_t(k)] = J;
     }
-    if (np) FQZ5_HIP(launch_fqz_rc(g.upload(jobs), np, g.stream));
+    if (np) {
+        // hedge: each range chain twice, on two CUs
+        std::vector<FqzEvJob> rj(jobs.begin(), jobs.end());
+        if (hedge_chains() && 2 * rj.size() <= size_t(g.cus)) {
+            uint32_t *d_done = g.arena.alloc_n<uint32_t>(rj.size());
+            g.memset0(d_done, rj.size() * 4);
+            for (size_t k = 0; k < rj.size(); k++) rj[k].done = d_done + k;
+            rj.insert(rj.end(), rj.begin(), rj.begin() + long(np));
+        }
+        FQZ5_HIP(launch_fqz_rc(g.upload(rj), int(rj.size()), g.stream));
+    }
     for (int k = 0; k < np; k++) {
         FqzEncReq::Work &W = *par[size_t(k)]->w;
         FqzEvJob &J = W.J;

@@ -621,6 +621,11 @@ __global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
     for (uint32_t base = 0; base < nev; base += RC_BLK) {
         const uint32_t cnt = min(RC_BLK, nev - base);
         if (base + RC_BLK < nev) fetch(base + RC_BLK);
+        // hedged launch (done != nullptr): two copies of the chain on two CUs
+        // write identical outputs; the flag loaded now is looked at after
+        // this block, and the copy that sees it raised leaves
+        const uint32_t hedge = J.done ? __hip_atomic_load(J.done, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #ifdef FQZ5_RC_PROBE
         const uint64_t c0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -665,7 +670,10 @@ __global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
         }
         if (base + RC_BLK < nev) stage();
         __syncthreads();
+        if (__builtin_amdgcn_readfirstlane(hedge)) return;
     }
+    if (J.done && l == 0)
+        __hip_atomic_store(J.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef FQZ5_RC_PROBE
     if (l == 0 && blockIdx.x == 0) {
         g_rcprobe[0] = __builtin_amdgcn_s_memtime() - p0;

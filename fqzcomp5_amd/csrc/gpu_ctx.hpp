@@ -221,6 +221,9 @@ struct GpuCtx {
     }
 };
 
+// Hedged chain launches (rANS decode): on unless $FQZ5_NO_HEDGE is set.
+bool hedge_chains();
+
 // The calling thread's context (created on first use).
 GpuCtx &gpu();
 // A second context of the calling thread, for work run by a helper thread

@@ -408,6 +408,22 @@ constexpr uint32_t DEC_OBUF_BYTES = DEC_OBUF + 2048 + 128;  // + idle-lane sink
 constexpr uint32_t DEC_LDS_BASE = DEC_RING_BYTES + DEC_OBUF_BYTES + 256;
 static_assert(DEC_LDS_BASE % 16 == 0, "table alignment");
 
+// Hedged chains (DecJob::done != nullptr): the host launches every stream
+// twice, on two CUs, because the same chain runs up to ~20 % slower on some
+// CUs than on others.  Both copies write identical
+// bytes; the first to finish raises done, and the other leaves at its next
+// group boundary.  The flag is loaded at a group's start and looked at its
+// end, so the chain never waits for it.
+static DEV uint32_t hedge_poll(const DecJob &J) {
+    if (!J.done) return 0u;
+    return __hip_atomic_load(J.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+static DEV bool hedge_lost(uint32_t v) { return __builtin_amdgcn_readfirstlane(v) != 0u; }
+static DEV void hedge_won(const DecJob &J) {
+    if (J.done && threadIdx.x == 0)
+        __hip_atomic_store(J.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct DecShared {
     uint16_t *ring;
     uint8_t *obuf;
@@ -605,6 +621,7 @@ static DEV void dec4_body(const DecJob &J) {
             pf = load_slab(wsrc, slabs, l);
         }
         __syncthreads();
+        const uint32_t hedge = hedge_poll(J);
         const uint32_t t1 = (T - t0 < G) ? T : t0 + G;
         const uint32_t tf = t1 < Tfull ? t1 : (t0 > Tfull ? t0 : Tfull);
         uint32_t t = t0;
@@ -650,8 +667,10 @@ static DEV void dec4_body(const DecJob &J) {
         __syncthreads();
         dec_flush<O1, NX, true>(J, sh, t0, t1 - t0, l);
         __syncthreads();
+        if (hedge_lost(hedge)) return;
     }
     if (l == 0) *J.status = (ptr <= nwords) ? 0 : -1;
+    hedge_won(J);
 }
 
 // NX = 32: lanes 0..31 are the states; each renormalising lane reads its
@@ -690,6 +709,7 @@ static DEV void dec32_body(const DecJob &J) {
             pf = load_slab(wsrc, slabs, l);
         }
         __syncthreads();
+        const uint32_t hedge = hedge_poll(J);
         const uint32_t t1 = (T - t0 < G) ? T : t0 + G;
         for (uint32_t t = t0; t < t1; t++) {
             const bool act = l < NX && (O1 ? t < lenz : uint32_t(NX) * t + z < n);
@@ -710,16 +730,21 @@ static DEV void dec32_body(const DecJob &J) {
         __syncthreads();
         dec_flush<O1, NX, false>(J, sh, t0, t1 - t0, l);
         __syncthreads();
+        if (hedge_lost(hedge)) return;
     }
     if (l == 0) *J.status = (ptr <= nwords) ? 0 : -1;
+    hedge_won(J);
 }
 
 // ---------------------------------------------------------------------------
 // O0, NX = 4: the lean chain.  The order-0 symbol does not feed the chain, so
 // the step carries only what the next state needs and the slot is emitted in
 // place of the symbol (mapped to the symbol at the group flush):
-//   LDS entry per slot   {f, slot - start} as two u32 (no symbol byte)
+//   LDS entry per slot   {f, slot - start, T, 0} (no symbol byte), with
+//                        T = ceil((2^15 - (slot - start)) / f)
 //   xd   = f * (x >> bits) + (slot - start)             (one mad24)
+//   renormalise  <=>  xd < 2^15  <=>  (x >> bits) < T, so the ballot does
+//        not wait for the mad24
 //   ptr  lives in a VGPR and advances with one v_bcnt of the renorm ballot;
 //        the ring is linear over a group (a mirrored head), so the window
 //        address is one shift-add of ptr.
@@ -732,9 +757,10 @@ constexpr uint32_t O0_MIRROR = 1040;                   // >= 4*G + 4, slab-unit 
 constexpr uint32_t O0_RING_BYTES = (RING_WORDS + O0_MIRROR) * 2;
 constexpr uint32_t O0_OBUF_BYTES = 4 * O0_G * 2;       // u16 slots, lane-major
 constexpr uint32_t O0_SYM_OFF = O0_RING_BYTES + O0_OBUF_BYTES;
-constexpr uint32_t O0_TAB_OFF = O0_SYM_OFF + 4096;     // u32 entries, 16-B aligned
+constexpr uint32_t O0_TAB_OFF = O0_SYM_OFF + 4096;     // 16-B entries, 16-B aligned
 static_assert(O0_TAB_OFF % 16 == 0, "O0 table alignment");
-constexpr uint32_t O0_LDS_BYTES = O0_TAB_OFF + 4096 * 8;
+constexpr uint32_t O0_LDS_BYTES = O0_TAB_OFF + 4096 * 16;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 static DEV void store_slab_o0(uint16_t *ring, uint32_t s, int z, uint4 v) {
     const uint32_t w0 = (s * SLAB_WORDS + uint32_t(z) * 8) & (RING_WORDS - 1);
@@ -765,7 +791,7 @@ static DEV void dec4_o0_body(const DecJob &J) {
     uint16_t *ring = reinterpret_cast<uint16_t *>(lds);
     uint16_t *obuf = reinterpret_cast<uint16_t *>(lds + O0_RING_BYTES);
     uint8_t *s2sym = lds + O0_SYM_OFF;
-    uint2 *tab = reinterpret_cast<uint2 *>(lds + O0_TAB_OFF);
+    uint4 *tab = reinterpret_cast<uint4 *>(lds + O0_TAB_OFF);
     const int l = int(threadIdx.x);
     const uint32_t n = J.n;
     const int bits = J.bits;
@@ -773,7 +799,8 @@ static DEV void dec4_o0_body(const DecJob &J) {
     // (f-1) << (bits+8) | (slot-start) << 8 | sym  ->  {f, slot-start}
     for (uint32_t i = l; i <= mask; i += 64) {
         const uint32_t e = J.tab[i];
-        tab[i] = make_uint2((e >> (bits + 8)) + 1, (e >> 8) & mask);
+        const uint32_t f = (e >> (bits + 8)) + 1, b = (e >> 8) & mask;
+        tab[i] = make_uint4(f, b, (RANS_LOW_D - b + f - 1) / f, 0);
         s2sym[i] = uint8_t(e);
     }
     uint32_t x = 1u << 16;
@@ -790,7 +817,7 @@ static DEV void dec4_o0_body(const DecJob &J) {
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(
         (__attribute__((address_space(3))) uint16_t *)(ring)));
     const uint32_t tab_lds = uint32_t(reinterpret_cast<uintptr_t>(
-        (__attribute__((address_space(3))) uint2 *)(tab)));
+        (__attribute__((address_space(3))) uint4 *)(tab)));
     uint16_t *myob = obuf + (l & 3) * G;
 #ifdef FQZ5_CHAIN_PROBE
     const uint64_t pr0 = __builtin_amdgcn_s_memtime(), rr0 = __builtin_amdgcn_s_memrealtime();
@@ -804,6 +831,7 @@ static DEV void dec4_o0_body(const DecJob &J) {
             pf = load_slab(wsrc, slabs, l);
         }
         __syncthreads();
+        const uint32_t hedge = hedge_poll(J);
         // word p of this group sits at byte wbase + 2p of the LDS (p - gp < 1028)
         const uint32_t gp = ptr;
         const uint32_t wbase = ring_lds + 2 * ((gp & (RING_WORDS - 1)) - gp);
@@ -819,13 +847,19 @@ static DEV void dec4_o0_body(const DecJob &J) {
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
                     a[u] = x & mask;
-                    const uint64_t e = *lds_ptr<uint64_t>(tab_lds + (a[u] << 3));
+                    const uint32_t xh = x >> bits;          // ready before the reads return
+                    // the window read (address known since the last step)
+                    // goes first so neither read waits for the other
                     const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
-                    const uint32_t xd = __umul24(uint32_t(e), x >> bits) + uint32_t(e >> 32);
-                    const uint64_t m = __ballot(xd < RANS_LOW_D);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const u32x4 e = *lds_ptr<u32x4>(tab_lds + (a[u] << 4));
+                    __builtin_amdgcn_sched_barrier(0);
+                    const bool c = xh < e.z;
+                    const uint32_t xd = __umul24(e.x, xh) + e.y;
+                    const uint64_t m = __ballot(c);
                     const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
                     const uint32_t w = uint32_t(win >> r16);
-                    x = (xd < RANS_LOW_D) ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
+                    x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
                     ptr = vbcnt(uint32_t(m), ptr, r16);
                 }
                 uint4 *o = reinterpret_cast<uint4 *>(myob + (t - t0));
@@ -843,7 +877,7 @@ static DEV void dec4_o0_body(const DecJob &J) {
             for (; t < t1; t++) {
                 const bool act = uint32_t(NX) * t + uint32_t(l) < n;
                 const uint32_t s = x & mask;
-                const uint2 e = tab[s];
+                const uint4 e = tab[s];
                 const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
                 const uint32_t xd = __umul24(e.x, x >> bits) + e.y;
                 const bool c = act && xd < RANS_LOW_D;
@@ -880,8 +914,10 @@ static DEV void dec4_o0_body(const DecJob &J) {
                 st8(out, NX * t0 + i, s2sym[obuf[(i & 3) * G + (i >> 2)]]);   // past n: dropped
         }
         __syncthreads();
+        if (hedge_lost(hedge)) return;
     }
     if (l == 0) *J.status = (ptr <= nwords) ? 0 : -1;
+    hedge_won(J);
 #ifdef FQZ5_CHAIN_PROBE
     if (l == 0 && blockIdx.x < 512) { g_jobt[blockIdx.x][4] = t_steps; g_jobt[blockIdx.x][5] = n_steps; }
     if (l == 0 && blockIdx.x == 0) {

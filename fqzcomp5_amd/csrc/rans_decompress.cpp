@@ -355,11 +355,20 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
         const uint32_t mode = dec_table_mode(j.o1, rows, j.bits);
         djs.push_back(DecJob{j.d + j.tab_len, d_tabs + offs[k].tab,
                              j.o1 ? d_alpha + offs[k].alpha : nullptr, j.d_out, d_status + k,
-                             j.len - j.tab_len, j.n, j.nx, j.bits, rows, mode});
+                             j.len - j.tab_len, j.n, j.nx, j.bits, rows, mode, nullptr});
         bytes += double(j.n) + (j.len - j.tab_len);
         lds = std::max(lds, dec_lds_bytes(rows, j.bits, int(mode)));
     }
     EventPair ev(g_.prof.on && !ord.empty(), g_.stream);
+    // hedge: every stream twice while two copies fit one per CU (the same
+    // chain runs up to ~20 % slower on some CUs)
+    if (hedge_chains() && !djs.empty() && 2 * djs.size() <= size_t(g_.cus)) {
+        uint32_t *d_done = g_.arena.alloc_n<uint32_t>(djs.size());
+        g_.memset0(d_done, djs.size() * 4);
+        const size_t nj = djs.size();
+        for (size_t k = 0; k < nj; k++) djs[k].done = d_done + k;
+        djs.insert(djs.end(), djs.begin(), djs.begin() + long(nj));
+    }
     lds = g_.chain_lds(lds, djs.size());
     if (!djs.empty()) FQZ5_HIP(launch_dec(g_.upload(djs), int(djs.size()), lds, g_.stream));
     ev.stop(g_.stream);
