@@ -1,4 +1,5 @@
 // capi.cpp — extern "C" entry points (include/fqz5_mi355x.h).
+#include <atomic>
 #include <climits>
 #include <cstdlib>
 #include <cstring>
@@ -41,9 +42,14 @@ void GpuCtx::copy_stat(const char *kind, const char *file, int line) {
 }
 #endif
 
+static std::atomic<int> g_hedge{-1};
 bool hedge_chains() {
-    static const bool on = std::getenv("FQZ5_NO_HEDGE") == nullptr;
-    return on;
+    int v = g_hedge.load();
+    if (v < 0) {
+        v = std::getenv("FQZ5_NO_HEDGE") == nullptr ? 1 : 0;
+        g_hedge.store(v);
+    }
+    return v != 0;
 }
 
 // The calling thread's second context: its own streams and arenas, for
@@ -297,6 +303,12 @@ int fqz5_device_ok(void) {
 const char *fqz5_last_error(void) { return g_err.c_str(); }
 
 unsigned fqz5_set_hot_min(unsigned min_events) { return fqz_set_hot_min(min_events); }
+
+int fqz5_set_hedge(int on) {
+    const int prev = hedge_chains() ? 1 : 0;
+    g_hedge.store(on ? 1 : 0);
+    return prev;
+}
 
 void fqz5_profile(int on) {
     try {

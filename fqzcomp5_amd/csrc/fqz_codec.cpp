@@ -605,11 +605,12 @@ void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
     if (np) {
         // hedge: each range chain twice, on two CUs
         std::vector<FqzEvJob> rj(jobs.begin(), jobs.end());
-        if (hedge_chains() && 2 * rj.size() <= size_t(g.cus)) {
+        const size_t copies = hedge_copies(rj.size(), size_t(g.cus));
+        if (copies > 1) {
             uint32_t *d_done = g.arena.alloc_n<uint32_t>(rj.size());
             g.memset0(d_done, rj.size() * 4);
             for (size_t k = 0; k < rj.size(); k++) rj[k].done = d_done + k;
-            rj.insert(rj.end(), rj.begin(), rj.begin() + long(np));
+            for (size_t c = 1; c < copies; c++) rj.insert(rj.end(), rj.begin(), rj.begin() + long(np));
         }
         FQZ5_HIP(launch_fqz_rc(g.upload(rj), int(rj.size()), g.stream));
     }

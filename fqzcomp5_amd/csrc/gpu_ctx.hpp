@@ -221,8 +221,15 @@ struct GpuCtx {
     }
 };
 
-// Hedged chain launches (rANS decode): on unless $FQZ5_NO_HEDGE is set.
+// Hedged chain launches (rANS decode, fqz range chain): on unless
+// $FQZ5_NO_HEDGE is set or fqz5_set_hedge(0).
 bool hedge_chains();
+// Copies of each of `jobs` chains: up to 4 while they fit one per CU.
+inline size_t hedge_copies(size_t jobs, size_t cus) {
+    if (!hedge_chains() || !jobs) return 1;
+    const size_t c = cus / jobs;
+    return c < 1 ? 1 : (c > 4 ? 4 : c);
+}
 
 // The calling thread's context (created on first use).
 GpuCtx &gpu();

@@ -408,11 +408,27 @@ constexpr uint32_t DEC_OBUF_BYTES = DEC_OBUF + 2048 + 128;  // + idle-lane sink
 constexpr uint32_t DEC_LDS_BASE = DEC_RING_BYTES + DEC_OBUF_BYTES + 256;
 static_assert(DEC_LDS_BASE % 16 == 0, "table alignment");
 
+// A 32-bit LDS byte address as a pointer (an unaligned 8-byte window is read
+// with one ds_read_b64: gfx950 LDS runs in unaligned mode).
+template <typename T>
+static DEV const __attribute__((address_space(3))) T *lds_ptr(uint32_t a) {
+    return reinterpret_cast<const __attribute__((address_space(3))) T *>(size_t(a));
+}
+
+// acc + popcount(m) in one VALU op.  `after` ties it behind the mbcnt of
+// the same ballot, which already waited out the VALU-writes-SGPR hazard
+// that the hazard recognizer does not see through inline asm.
+static DEV uint32_t vbcnt(uint32_t m, uint32_t acc, uint32_t after) {
+    uint32_t r;
+    asm volatile("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "s"(m), "v"(acc), "v"(after));
+    return r;
+}
+
 // Hedged chains (DecJob::done != nullptr): the host launches every stream
-// twice, on two CUs, because the same chain runs up to ~20 % slower on some
-// CUs than on others.  Both copies write identical
-// bytes; the first to finish raises done, and the other leaves at its next
-// group boundary.  The flag is loaded at a group's start and looked at its
+// 2-4 times, on different CUs, because the same chain runs up to ~20 %
+// slower on some CUs than on others.  All copies write
+// identical bytes; the first to finish raises done, and the others leave at
+// their next group boundary.  The flag is loaded at a group's start and looked at its
 // end, so the chain never waits for it.
 static DEV uint32_t hedge_poll(const DecJob &J) {
     if (!J.done) return 0u;
@@ -603,7 +619,7 @@ static DEV void dec4_body(const DecJob &J) {
         const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
         const uint32_t w = uint32_t(win >> r16);
         x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
-        ptr += uint32_t(__popcll(m & 15u));
+        ptr = vbcnt(uint32_t(m), ptr, r16);      // exec = the 4 state lanes
         // acc byte (u&3) <- sy byte 0, other bytes kept
         constexpr uint32_t SEL[4] = {0x07060500u, 0x07060004u, 0x07000504u, 0x00060504u};
         acc = __builtin_amdgcn_perm(acc, sy, SEL[u & 3]);
@@ -766,22 +782,6 @@ static DEV void store_slab_o0(uint16_t *ring, uint32_t s, int z, uint4 v) {
     const uint32_t w0 = (s * SLAB_WORDS + uint32_t(z) * 8) & (RING_WORDS - 1);
     *reinterpret_cast<uint4 *>(ring + w0) = v;
     if (w0 < O0_MIRROR) *reinterpret_cast<uint4 *>(ring + RING_WORDS + w0) = v;
-}
-
-// A 32-bit LDS byte address as a pointer (an unaligned 8-byte window is read
-// with one ds_read_b64: gfx950 LDS runs in unaligned mode).
-template <typename T>
-static DEV const __attribute__((address_space(3))) T *lds_ptr(uint32_t a) {
-    return reinterpret_cast<const __attribute__((address_space(3))) T *>(size_t(a));
-}
-
-// acc + popcount(m) in one VALU op.  `after` ties it behind the mbcnt of
-// the same ballot, which already waited out the VALU-writes-SGPR hazard
-// that the hazard recognizer does not see through inline asm.
-static DEV uint32_t vbcnt(uint32_t m, uint32_t acc, uint32_t after) {
-    uint32_t r;
-    asm volatile("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "s"(m), "v"(acc), "v"(after));
-    return r;
 }
 
 static DEV void dec4_o0_body(const DecJob &J) {

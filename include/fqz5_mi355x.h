@@ -189,6 +189,13 @@ void fqz5_profile_read(double *out6);
  * previous value. */
 unsigned fqz5_set_hot_min(unsigned min_events);
 
+/* Hedged chain launches: the rANS decoder and the fqz range chain run each
+ * dependent chain on 2-4 CUs at once while the copies fit one per CU, and
+ * the first copy to finish wins (the same chain runs up to ~20 % slower on
+ * some CUs).  Output bytes do not depend on it.  1 = on (default unless
+ * $FQZ5_NO_HEDGE is set), 0 = off; returns the previous setting. */
+int fqz5_set_hedge(int on);
+
 /* Device check of the fqz decoder's division: floor(n / t) computed as
  * (u32)fma(n, recip(t), 2^-19) for every t < 2^16 and ~2000 n each.
  * Returns the number of mismatches (0), or -1 on a device error. */

@@ -125,3 +125,40 @@ def test_large_q40_roundtrip():
         got = lib.rans_compress(q, o)
         assert got == ora.rans_compress(q, o), hex(o)
         assert lib.rans_uncompress(got) == q
+
+
+def test_hedged_launches_same_bytes():
+    """fqz5_set_hedge: the decode launch (and the fqz range chain) runs each
+    chain on several CUs and keeps the first copy to finish.  Off and on
+    give the same bytes, for several streams of several orders at once and
+    for a stream too short to reach a group boundary."""
+    import torch
+    from fqzcomp5_amd import synth
+    so = lib.load()
+    r = synth.illumina(20000, seed=9)
+    datas = [r.qual.tobytes(), r.seq.tobytes(), r.qual.tobytes()[:777]]
+    orders = [0, 1, 129, 193]
+    comps = [(d, lib.rans_compress(d, o)) for d in datas for o in orders]
+    prev = so.fqz5_set_hedge(1)
+    try:
+        outs = {}
+        for hedge in (0, 1):
+            so.fqz5_set_hedge(hedge)
+            cin = [torch.frombuffer(bytearray(c), dtype=torch.uint8).cuda() for _, c in comps]
+            cout = [torch.zeros(len(d), dtype=torch.uint8, device="cuda") for d, _ in comps]
+            jobs = [lib.RansJob(a.data_ptr(), b.data_ptr(), a.numel(), b.numel(), 0, 0, 0, 0)
+                    for a, b in zip(cin, cout)]
+            lib.uncompress_batch_dev(jobs)
+            assert all(j.status == 0 for j in jobs)
+            outs[hedge] = [bytes(b.cpu().numpy()) for b in cout]
+        assert outs[0] == outs[1]
+        assert outs[1] == [d for d, _ in comps]
+        q = r.qual.tobytes()
+        lens = r.lens.astype(np.uint32)
+        fq = {}
+        for hedge in (0, 1):
+            so.fqz5_set_hedge(hedge)
+            fq[hedge] = lib.fqz_compress(q, lens.copy(), np.zeros(len(lens), np.uint32), 1)
+        assert fq[0] == fq[1]
+    finally:
+        so.fqz5_set_hedge(prev)

@@ -73,6 +73,23 @@ __global__ void k(uint32_t *out, uint64_t *cyc, uint32_t a, uint32_t b) {
                 x = q * (y | 1u);
                 x <<= __builtin_clz(x | 1u) & 24u;
             }
+            if (T == 16) {                                                  // O0 step, LDS table (16 B entry)
+                const uint64_t e = lds[x & 4095];
+                const uint32_t xh = x >> 12;
+                x = __umul24(uint32_t(e) & 4095, xh) + uint32_t(e >> 32) + 0x8000;
+            }
+            if (T == 17) {                                                  // O0 step, register lookup (<= 4 boundaries)
+                const uint32_t sl = x & 4095;
+                const uint32_t s2 = sl | (sl << 16);
+                const uint32_t d1 = __builtin_amdgcn_perm(0, 0, 0) + (s2 - (a & 0x0fff0fffu)); // stand-in pk_sub
+                const uint32_t d2 = s2 - (b & 0x0fff0fffu);
+                const uint32_t n = __builtin_popcount(d1 & 0x80008000u) + __builtin_popcount(d2 & 0x80008000u);
+                const uint32_t sel = n * 0x0202u + 0x0100u;
+                const uint32_t f = __builtin_amdgcn_perm(a, b, sel) & 0xffffu;
+                const uint32_t st = __builtin_amdgcn_perm(b, a, sel) & 0xffffu;
+                const uint32_t xh = x >> 12;
+                x = __umul24(f | 1u, xh) + (sl - st) + 0x8000;
+            }
             if (T == 10) {                                                  // full renorm select chain
                 const uint64_t m = __ballot(x < y);
                 const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
@@ -93,14 +110,15 @@ int main() {
                            "cmp+mbcnt", "cmp+cndmask", "and,lshl_add,ds_read,mad", "same + never-taken branch",
                            "same + ~68%-taken branch", "renorm select (cmp,mbcnt,lshl,lshr64,perm,cndmask)",
                            "enc step cmp+cndmask", "enc step sign shift", "enc step sub borrow",
-                           "fqz range step f64", "fqz range step int magic"};
+                           "fqz range step f64", "fqz range step int magic",
+                           "O0 step LDS lookup + mad", "O0 step register lookup + mad"};
 #define RUN(T) hipLaunchKernelGGL(k<T>, dim3(1), dim3(64), 0, 0, out, cyc, 12345u, 99999u);
     for (int rep = 0; rep < 2; rep++) {
-        RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15)
+        RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15) RUN(16) RUN(17)
     }
     hipDeviceSynchronize();
     uint64_t h[32];
     hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
-    for (int t = 0; t <= 15; t++) printf("T%-2d %-55s %7.1f cyc/step\n", t, names[t], double(h[t]) / N);
+    for (int t = 0; t <= 17; t++) printf("T%-2d %-55s %7.1f cyc/step\n", t, names[t], double(h[t]) / N);
     return 0;
 }
