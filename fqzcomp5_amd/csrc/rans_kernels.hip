@@ -51,12 +51,28 @@ __global__ __launch_bounds__(256) void k_hist0(const HistItem *items,
     __syncthreads();
     const uint8_t *d = it.data;
     uint32_t *mine = h + (threadIdx.x % HIST0_C) * HIST0_ROW;
-    // e[c]: bytes equal to their predecessor (hist8e's run count)
-    for (uint32_t i = it.begin + threadIdx.x; i < it.end; i += blockDim.x) {
-        const uint32_t c = d[i];
-        const int prev = i ? int(d[i - 1]) : -1;
-        atomicAdd(&mine[c], 1u);
-        if (int(c) == prev) atomicAdd(&mine[256 + c], 1u);
+    // e[c]: bytes equal to their predecessor (hist8e's run count).  Each
+    // thread reads 16-byte aligned chunks (one load; the chunk's first byte
+    // takes its predecessor from one more byte load); bytes outside
+    // [begin, end) are skipped.  A chunk never leaves the 16-byte blocks
+    // that hold the slice's own bytes.
+    const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(d) & 15u);
+    const uint4 *al = reinterpret_cast<const uint4 *>(d - mis);
+    for (uint32_t c = (it.begin + mis) / 16 + threadIdx.x; 16 * c < it.end + mis; c += blockDim.x) {
+        const uint4 v = al[c];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        const int64_t p0 = int64_t(16 * c) - int64_t(mis);
+        int prev = p0 >= 1 ? int(d[p0 - 1]) : -1;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int b = int((w[k >> 2] >> (8 * (k & 3))) & 0xffu);
+            const int64_t p = p0 + k;
+            if (p >= int64_t(it.begin) && p < int64_t(it.end)) {
+                atomicAdd(&mine[b], 1u);
+                if (b == prev && p > 0) atomicAdd(&mine[256 + b], 1u);   // byte 0: none
+            }
+            prev = b;
+        }
     }
     __syncthreads();
     uint32_t *out = counts + size_t(it.seg) * 512;
@@ -94,12 +110,25 @@ __global__ __launch_bounds__(256) void k_hist1(const Hist1Item *items,
     uint32_t *gout = counts + it.out_off;
     uint32_t *mine = bins + (threadIdx.x & (C - 1)) * row;
     const uint8_t *d = it.data;
-    for (uint32_t i = it.begin + threadIdx.x; i < it.end; i += blockDim.x) {
-        uint32_t c = rm[d[i]];
-        uint32_t p = i ? rm[d[i - 1]] : rm[0];
-        uint32_t b = p * A + c;
-        if (BIG) atomicAdd(&bins[b >> 1], 1u << (16 * (b & 1)));
-        else atomicAdd(&mine[b], 1u);
+    // 16-byte aligned chunks per thread, as in k_hist0
+    const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(d) & 15u);
+    const uint4 *al = reinterpret_cast<const uint4 *>(d - mis);
+    for (uint32_t ch = (it.begin + mis) / 16 + threadIdx.x; 16 * ch < it.end + mis; ch += blockDim.x) {
+        const uint4 v = al[ch];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        const int64_t p0 = int64_t(16 * ch) - int64_t(mis);
+        uint32_t p = p0 >= 1 ? rm[d[p0 - 1]] : rm[0];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t c = rm[(w[k >> 2] >> (8 * (k & 3))) & 0xffu];
+            const int64_t q = p0 + k;
+            if (q >= int64_t(it.begin) && q < int64_t(it.end)) {
+                const uint32_t b = (q == 0 ? uint32_t(rm[0]) : p) * A + c;   // byte 0: context 0
+                if (BIG) atomicAdd(&bins[b >> 1], 1u << (16 * (b & 1)));
+                else atomicAdd(&mine[b], 1u);
+            }
+            p = c;
+        }
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
@@ -243,6 +272,28 @@ static DEV RleThr rle_thread_scan(const uint8_t *d, uint32_t a, uint32_t b,
     return r;
 }
 
+// The chunk's bytes [c0, c1) and the one before it, staged through LDS with
+// coalesced 16-byte loads (the scan then reads LDS): returns a pointer that
+// indexes like the input (dv[i] for i in [c0 - 1, c1)).
+static DEV const uint8_t *rle_stage(const uint8_t *in, uint32_t c0, uint32_t c1, uint8_t *stage) {
+    const uint8_t *src = in + c0;
+    const uint32_t mis = uint32_t(reinterpret_cast<uintptr_t>(src) & 15u);
+    const uint4 *al = reinterpret_cast<const uint4 *>(src - mis);
+    const uint32_t len = c1 - c0, nblk = (len + mis + 15) / 16;
+    for (uint32_t j = threadIdx.x; j < nblk; j += blockDim.x) {
+        const uint4 v = al[j];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int64_t o = int64_t(16 * j + k) - int64_t(mis);   // offset from c0
+            if (o >= 0 && o < int64_t(len)) stage[1 + o] = uint8_t(w[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+    if (threadIdx.x == 0) stage[0] = c0 ? in[c0 - 1] : 0;
+    __syncthreads();
+    return stage + 1 - int64_t(c0);
+}
+
 // Pass 1: per chunk {lit count, first lit, last lit, varint bytes excluding
 // the chunk's last literal, whether that literal is an RLE symbol}.
 __global__ __launch_bounds__(256) void k_rle_count(const RleItem *items,
@@ -253,18 +304,19 @@ __global__ __launch_bounds__(256) void k_rle_count(const RleItem *items,
     const uint32_t c = blockIdx.x;
     const RleItem it = items[chunk_item[2 * c]];
     const uint32_t lc = chunk_item[2 * c + 1];
+    __shared__ uint8_t stage[RLE_CH + 1];
     saved[threadIdx.x] = it.saved[threadIdx.x];
-    __syncthreads();
     const uint32_t c0 = lc * RLE_CH, c1 = min(it.n, c0 + RLE_CH);
+    const uint8_t *dv = rle_stage(it.in, c0, c1, stage);
     const uint32_t a = min(c1, c0 + threadIdx.x * RLE_PT), b = min(c1, a + RLE_PT);
-    RleThr r = rle_thread_scan(it.in, a, b, saved);
+    RleThr r = rle_thread_scan(dv, a, b, saved);
     // successor of my last literal inside the chunk = first literal of a later thread
     // suffix minimum of first-literal positions over the threads after me
     block_suffix_min(r.first, tmp);
     uint32_t later = (threadIdx.x < 255) ? tmp[threadIdx.x + 1] : NONE;
     __syncthreads();
     uint32_t vs = r.vsum;
-    if (r.last != NONE && later != NONE && saved[it.in[r.last]])
+    if (r.last != NONE && later != NONE && saved[dv[r.last]])
         vs += vlen32(later - r.last - 1);
     uint32_t tot_cnt, tot_vs;
     block_excl_sum(r.cnt, tmp, &tot_cnt);
@@ -279,7 +331,7 @@ __global__ __launch_bounds__(256) void k_rle_count(const RleItem *items,
     if (threadIdx.x == 0) {
         uint32_t *o = cstat + 5 * c;
         o[0] = tot_cnt; o[1] = cf; o[2] = cl1 ? cl1 - 1 : NONE; o[3] = tot_vs;
-        o[4] = cl1 ? saved[it.in[cl1 - 1]] : 0;
+        o[4] = cl1 ? saved[dv[cl1 - 1]] : 0;
     }
 }
 
@@ -293,20 +345,21 @@ __global__ __launch_bounds__(256) void k_rle_emit(const RleItem *items,
     const uint32_t c = blockIdx.x;
     const RleItem it = items[chunk_item[2 * c]];
     const uint32_t lc = chunk_item[2 * c + 1];
+    __shared__ uint8_t stage[RLE_CH + 1];
     saved[threadIdx.x] = it.saved[threadIdx.x];
-    __syncthreads();
     const uint32_t c0 = lc * RLE_CH, c1 = min(it.n, c0 + RLE_CH);
+    const uint8_t *dv = rle_stage(it.in, c0, c1, stage);
     const uint32_t a = min(c1, c0 + threadIdx.x * RLE_PT), b = min(c1, a + RLE_PT);
     const uint32_t lit_off = cmeta[3 * c], run_off = cmeta[3 * c + 1],
                    chunk_next = cmeta[3 * c + 2];
-    RleThr r = rle_thread_scan(it.in, a, b, saved);
+    RleThr r = rle_thread_scan(dv, a, b, saved);
     // successor of this thread's last literal
     block_suffix_min(r.first, tmp);
     uint32_t later = (threadIdx.x < 255) ? tmp[threadIdx.x + 1] : NONE;
     __syncthreads();
     if (later == NONE) later = chunk_next;
     uint32_t vs = r.vsum;
-    if (r.last != NONE && saved[it.in[r.last]]) vs += vlen32(later - r.last - 1);
+    if (r.last != NONE && saved[dv[r.last]]) vs += vlen32(later - r.last - 1);
     uint32_t lo = block_excl_sum(r.cnt, tmp, nullptr) + lit_off;
     uint32_t ro = block_excl_sum(vs, tmp, nullptr) + run_off;
     // sequential write of this thread's literals and run varints
@@ -317,12 +370,12 @@ __global__ __launch_bounds__(256) void k_rle_emit(const RleItem *items,
             it.runs[ro++] = uint8_t(((rl >> (7 * k)) & 0x7f) | (k ? 0x80 : 0));
     };
     for (uint32_t i = a; i < b; i++) {
-        if (!rle_is_lit(it.in, i, saved)) continue;
-        if (prev != NONE && saved[it.in[prev]]) put_run(i - prev - 1);
-        it.lits[lo++] = it.in[i];
+        if (!rle_is_lit(dv, i, saved)) continue;
+        if (prev != NONE && saved[dv[prev]]) put_run(i - prev - 1);
+        it.lits[lo++] = dv[i];
         prev = i;
     }
-    if (prev != NONE && saved[it.in[prev]]) put_run(later - prev - 1);
+    if (prev != NONE && saved[dv[prev]]) put_run(later - prev - 1);
 }
 
 // ---------------------------------------------------------------------------
