@@ -3,12 +3,47 @@
 // every stream in the batch is issued as one launch per stage, so the
 // per-stream dependent rANS chains of all streams run concurrently.
 #pragma once
+#include <algorithm>
+#include <thread>
+#include <mutex>
+#include <exception>
+#include <atomic>
 #include <cstdint>
 #include <vector>
 
 #include "gpu_ctx.hpp"
 
 namespace fqz5 {
+
+// Host-side table construction (encoder: normalise_freq, O1 shift choice,
+// serialised tables; decoder: slot tables) spread over up to 16 threads: a
+// -3/-5 batch has thousands of stripe jobs.  fn(i) must touch item i only.
+template <class F> inline void host_parallel(size_t n, F fn) {
+    const size_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < 64 || hw == 1) {
+        for (size_t i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    std::exception_ptr err;
+    std::mutex mu;
+    auto work = [&] {
+        try {
+            for (size_t i; (i = next.fetch_add(16)) < n;)
+                for (size_t k = i; k < std::min(n, i + 16); k++) fn(k);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err) err = std::current_exception();
+        }
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < hw; t++) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    if (err) std::rethrow_exception(err);
+}
+
+
 
 // A part of an output stream: host bytes or a device range.
 struct Piece {

@@ -19,6 +19,11 @@
 #include <algorithm>
 #include <climits>
 #include <cstring>
+#include <atomic>
+#include <exception>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "kernels.h"
 #include "rans_codec.hpp"
@@ -456,16 +461,15 @@ void Compressor::stage_tables() {
         EJ &j = jobs_[ji];
         for (int z = 1; z < j.nx; z++) j.seg_first[z] = pb[q++];
         j.last_byte = pb[q++];
-        build_o1(j, &h[j.f1_off]);
     }
+    host_parallel(o1jobs.size(), [&](size_t k) { build_o1(jobs_[o1jobs[k]], &h[jobs_[o1jobs[k]].f1_off]); });
 }
 
 // Stage 5: all rANS chains.  O1 tables above 1000 bytes get their own
 // O0-4x16 job (rANS_static16_int.h:397-412) in the same launch.
 void Compressor::stage_encode() {
     const size_t nmain = jobs_.size();
-    for (size_t i = 0; i < nmain; i++)
-        if (!jobs_[i].o1) build_o0(jobs_[i]);
+    host_parallel(nmain, [&](size_t i) { if (!jobs_[i].o1) build_o0(jobs_[i]); });
     for (size_t i = 0; i < nmain; i++) {
         if (!jobs_[i].o1 || jobs_[i].table.size() <= 1000) continue;
         EJ h;

@@ -291,15 +291,24 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
     struct Off { size_t tab, alpha; };
     std::vector<Off> offs;
     std::vector<int> used;
+    // table image offsets first, then every job's table in parallel
     for (int id : ids) {
         DJ &j = djs_[id];
         if (!j.ok || !j.n) continue;
-        const uint32_t M = 1u << j.bits;
         const size_t rows = j.o1 ? j.alpha.size() : 1;
         const uint32_t mode = dec_table_mode(j.o1, uint32_t(rows), j.bits);
         Off o{tabs.size(), alphas.size()};
         tabs.resize(tabs.size() + dec_tab_words(mode, uint32_t(rows), j.bits), 0);
-        uint32_t *t = &tabs[o.tab];
+        if (j.o1) alphas.insert(alphas.end(), j.alpha.begin(), j.alpha.end());
+        offs.push_back(o);
+        used.push_back(id);
+    }
+    host_parallel(used.size(), [&](size_t k) {
+        DJ &j = djs_[used[k]];
+        const uint32_t M = 1u << j.bits;
+        const size_t rows = j.o1 ? j.alpha.size() : 1;
+        const uint32_t mode = dec_table_mode(j.o1, uint32_t(rows), j.bits);
+        uint32_t *t = &tabs[offs[k].tab];
         // LDS/GLOBAL: [u32 per slot];  SPLIT: [u8 per slot][u32 fb]
         uint8_t *tsym = reinterpret_cast<uint8_t *>(t);
         uint32_t *tfb = t + rows * M / 4;
@@ -325,10 +334,7 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
                 x += F[s];
             }
         }
-        if (j.o1) alphas.insert(alphas.end(), j.alpha.begin(), j.alpha.end());
-        offs.push_back(o);
-        used.push_back(id);
-    }
+    });
     if (used.empty()) return;
     const uint32_t *d_tabs = g_.upload(tabs);
     const uint8_t *d_alpha = alphas.empty() ? nullptr : g_.upload(alphas);

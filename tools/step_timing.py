@@ -1,0 +1,28 @@
+"""Host-side phases of one bench step (-3 workload): where the wall time
+between GPU launches goes."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+torch.cuda.init()
+import bench  # noqa: E402
+from fqzcomp5_amd import sections as S  # noqa: E402
+
+reads, blocks = bench.make_blocks(1.0, seed=1, kind="illumina")
+run = S.Run(reads, blocks, torch.device("cuda", 0))
+enc = run.enc_secs()
+for rep in range(3):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = S.new_state()
+    res, meth, sizes, tried, off = S.encode_run(enc, S.masks(3), st)
+    t1 = time.perf_counter()
+    ds = run.dec_secs(res)
+    t2 = time.perf_counter()
+    dres = S.decode(ds)
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    print(f"encode_run {1e3*(t1-t0):.1f} ms  dec_secs {1e3*(t2-t1):.1f} ms  decode {1e3*(t3-t2):.1f} ms", flush=True)
