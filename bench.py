@@ -160,6 +160,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     for _ in range(warmup):
         step()
     so = lib.load()
+    fq0 = S.trial_counts()
     so.fqz5_profile(1)
     if world > 1:
         dist.barrier()
@@ -174,6 +175,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     prof = (C.c_double * 6)()
     so.fqz5_profile_read(prof)
     so.fqz5_profile(0)
+    fq1 = S.trial_counts()
     t_max = torch.tensor([dt], dtype=torch.float64, device=dev)
     tot_bytes = torch.tensor([float(in_bytes_local)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -197,7 +199,11 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                    "compressed_bytes_per_gpu": comp_bytes,
                    "methods": sorted({int(m) for m in meth_all}),
                    "roundtrip_ok": bool(ok),
-                   "parallelism": f"blocks sharded over {world} GPU(s)"},
+                   "parallelism": f"blocks sharded over {world} GPU(s)",
+                   # fqz trial candidates in the timed steps, and how many
+                   # were provably losing and skipped their range chain
+                   # (fqz5_set_trial_prune; output bytes unchanged)
+                   "fqz_trial": {"tried": fq1[0] - fq0[0], "pruned": fq1[1] - fq0[1]}},
     }
     # ---- roofline of the dominant kernel ---------------------------------
     enc_ms, enc_n, enc_b, dec_ms, dec_n, dec_b = list(prof)

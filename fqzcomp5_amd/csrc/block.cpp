@@ -10,6 +10,8 @@
 // side by side, so the extra candidates cost little wall time), then the
 // trial state machine is replayed on the host in block order, which gives
 // exactly the choices of a single-threaded (-t1) reference run.
+#include <atomic>
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -86,6 +88,7 @@ struct TrySession {
     std::vector<CompressReq> reqs;
     std::vector<std::vector<int>> req_of;
     std::vector<FqzEncReq> fqz;                   // FQZ candidates
+    std::vector<uint64_t> fqz_lb;                 // pruned candidates: size lower bound (else 0)
     std::vector<std::vector<int>> fqz_of;
     std::deque<std::vector<uint32_t>> recs;       // their (rewritable) lengths / flags
     bool open = false;
@@ -112,6 +115,65 @@ FqzEncReq fqz_req(const fqz5_section &S, int m, std::deque<std::vector<uint32_t>
 }
 thread_local TrySession t_sess;
 
+// Trial pruning (fqz5_set_trial_prune): an fqz candidate whose size is
+// provably not below the best rANS candidate's, in every trial section and
+// summed over the trial window, cannot be chosen (rANS methods come first,
+// so they win ties); its range chain and bytes are skipped and its lower
+// bound stands in for its size.  The caller enables it only when the
+// sections of this call that try fqz form one whole trial window.
+std::atomic<int> g_prune{0};
+std::atomic<uint64_t> g_fqz_tried{0}, g_fqz_pruned{0};
+
+// Which fqz requests to skip, from the exact rANS sizes and the fqz lower
+// bounds of this session (TrySession::req_of / fqz_of).
+std::vector<char> prune_plan(const std::vector<CompressReq> &reqs, std::vector<FqzEncReq> &fqz) {
+    std::vector<char> skip(fqz.size(), 0);
+    const int nsec = int(t_sess.fqz_of.size());
+    std::vector<int> F;                                 // sections trying fqz
+    for (int i = 0; i < nsec; i++)
+        for (int m = FQZ0; m <= FQZ4; m++)
+            if (t_sess.fqz_of[i][m] >= 0) { F.push_back(i); break; }
+    // one whole trial window: every method's usize is then the same, and the
+    // window's pick (min (csize + 1) / usize) compares plain sums
+    if (F.size() != size_t(FQZ5_METRICS_TRIAL)) return skip;
+    auto rsize = [&](int i, int m) -> int64_t {          // exact rANS size, -1 if none
+        const int ri = t_sess.req_of[i][m];
+        return ri >= 0 && reqs[size_t(ri)].ok ? int64_t(layout_size(reqs[size_t(ri)].out)) : -1;
+    };
+    std::vector<int64_t> best(F.size(), -1);            // per section: min rANS size
+    for (size_t k = 0; k < F.size(); k++)
+        for (int m = 1; m < FQZ0; m++) {
+            const int64_t z = rsize(F[k], m);
+            if (z >= 0 && (best[k] < 0 || z < best[k])) best[k] = z;
+        }
+    int64_t best_sum = -1;                              // min over rANS methods tried everywhere
+    for (int m = 1; m < FQZ0; m++) {
+        int64_t sum = 0;
+        bool all = true;
+        for (int i : F) {
+            const int64_t z = rsize(i, m);
+            if (z < 0) { all = false; break; }
+            sum += z;
+        }
+        if (all && (best_sum < 0 || sum < best_sum)) best_sum = sum;
+    }
+    for (int m = FQZ0; m <= FQZ4; m++) {
+        bool ok = true;
+        int64_t lbsum = 0;
+        for (size_t k = 0; k < F.size() && ok; k++) {
+            const int fi = t_sess.fqz_of[F[k]][m];
+            if (fi < 0) { ok = false; break; }            // must be tried in the whole window
+            const int64_t lb = int64_t(fqz_size_lower_bound(fqz[size_t(fi)]));
+            ok = lb > 0 && best[k] >= 0 && lb >= best[k];
+            lbsum += lb;
+        }
+        if (!ok || !(best_sum >= 0 && lbsum >= best_sum)) continue;
+        for (int i : F)
+            if (t_sess.fqz_of[i][m] >= 0) skip[size_t(t_sess.fqz_of[i][m])] = 1;
+    }
+    return skip;
+}
+
 }  // namespace fqz5
 
 using namespace fqz5;
@@ -119,6 +181,13 @@ using namespace fqz5;
 extern "C" {
 
 void fqz5_trial_init(fqz5_trial_state *st) { std::memset(st, 0, sizeof *st); }
+
+int fqz5_set_trial_prune(int on) { return g_prune.exchange(on ? 1 : 0); }
+
+void fqz5_trial_counts(uint64_t *out2) {
+    out2[0] = g_fqz_tried.load();
+    out2[1] = g_fqz_pruned.load();
+}
 
 void fqz5_trial_schedule(const int32_t *sec_ids, int nsec, const uint32_t *avail,
                          const fqz5_trial_state *st, uint32_t *masks_out) {
@@ -192,7 +261,7 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             std::thread th([&ga, &fq, &err] {
                 try {
                     FQZ5_HIP(hipSetDevice(ga.device));
-                    fqz_encode_batch(ga, fq);
+                    fqz_encode_prepare(ga, fq);
                 } catch (...) {
                     err = std::current_exception();
                 }
@@ -205,9 +274,17 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             }
             th.join();
             if (err) std::rethrow_exception(err);
+            std::vector<char> skip(fq.size(), 0);
+            if (g_prune.load()) skip = prune_plan(reqs, fq);
+            fqz_encode_finish(ga, fq, &skip);
+            for (size_t k = 0; k < fq.size(); k++) t_sess.fqz_lb.push_back(skip[k] ? fqz_size_lower_bound(fq[k]) : 0);
+            g_fqz_tried += fq.size();
+            for (char c : skip) g_fqz_pruned += c ? 1 : 0;
         } else {
             compress_batch(g, reqs);
             if (!t_sess.fqz.empty()) fqz_encode_batch(g, t_sess.fqz);
+            t_sess.fqz_lb.assign(t_sess.fqz.size(), 0);
+            g_fqz_tried += t_sess.fqz.size();
         }
         t_sess.open = true;
         // sizes as compress_with_methods sees them: UINT_MAX when not run,
@@ -217,7 +294,11 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 const int ri = t_sess.req_of[i][m], fi = t_sess.fqz_of[i][m];
                 uint32_t sz = UINT32_MAX;
                 if (ri >= 0) sz = reqs[ri].ok ? layout_size(reqs[ri].out) : 0;
-                if (fi >= 0) sz = t_sess.fqz[size_t(fi)].ok ? layout_size(t_sess.fqz[size_t(fi)].out) : 0;
+                if (fi >= 0) {
+                    const uint64_t lb = t_sess.fqz_lb[size_t(fi)];   // pruned: its lower bound
+                    sz = t_sess.fqz[size_t(fi)].ok ? layout_size(t_sess.fqz[size_t(fi)].out)
+                         : lb ? uint32_t(std::min<uint64_t>(lb, UINT32_MAX - 1)) : 0;
+                }
                 sizes[size_t(i) * FQZ5_M_LAST + m] = sz;
             }
         return 0;

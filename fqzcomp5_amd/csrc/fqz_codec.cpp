@@ -409,6 +409,7 @@ struct FqzEncReq::Work {
     size_t room = 0;
     uint32_t last[2] = {0, 0};          // last record's event offset and count
     uint32_t P = 0, clen = 0;
+    uint64_t lb = 0;                    // lower bound of the output size (0: unknown)
 };
 
 // Every block of the batch goes through each stage before the next one:
@@ -428,7 +429,7 @@ static std::atomic<uint32_t> &hot_min_var() {
 uint32_t fqz_hot_min() { return hot_min_var().load(); }
 uint32_t fqz_set_hot_min(uint32_t v) { return hot_min_var().exchange(v); }
 
-void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
+void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
     std::vector<FqzEncReq *> par;
     for (FqzEncReq &R : reqs) {
         R.ok = false;
@@ -592,7 +593,37 @@ void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         uint32_t *hot = g.arena.alloc_n<uint32_t>(size_t(stride) * size_t(np));
         g.memset0(hot, size_t(stride) * size_t(np) * 4);
         FQZ5_HIP(launch_fqz_model_pass(g.upload(jobs), np, hot, stride, hot_min, g.stream));
+        // the entropy of each block's events: a lower bound of its size
+        constexpr uint32_t EB = 1024;
+        double *part = g.arena.alloc_n<double>(size_t(EB) * size_t(np));
+        for (int k = 0; k < np; k++) FQZ5_HIP(launch_fqz_entropy(jobs[size_t(k)], part + size_t(k) * EB, EB, g.stream));
+        std::vector<double> hp(size_t(EB) * size_t(np));
+        g.download(hp.data(), part, hp.size());
+        g.sync();
+        for (int k = 0; k < np; k++) {
+            double bits = 0;
+            for (uint32_t b = 0; b < EB; b++) bits += hp[size_t(k) * EB + b];
+            // 8 P >= bits - 8 (log2 of the final over the initial range);
+            // a margin covers the rounding of the double sums
+            bits = bits * (1.0 - 1e-9) - 8.0 - 64.0;
+            const uint64_t P = bits > 0 ? uint64_t(bits / 8.0) : 0;
+            FqzEncReq::Work &W = *par[size_t(k)]->w;
+            W.lb = uint64_t(W.hdr.size()) + P + 5;
+        }
     }
+}
+
+// The range chain and the output bytes of every parallel request not in
+// `skip` (skip[i] != 0: request i is left without output), and the sizes.
+void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vector<char> *skip) {
+    std::vector<FqzEncReq *> par;
+    std::vector<FqzEvJob> jobs;
+    for (size_t i = 0; i < reqs.size(); i++)
+        if (reqs[i].w->parallel && !(skip && (*skip)[i])) {
+            par.push_back(&reqs[i]);
+            jobs.push_back(reqs[i].w->J);
+        }
+    const int np = int(par.size());
     // the range chain of every block (one wave each), then the output bytes
     for (int k = 0; k < np; k++) {
         FqzEvJob &J = par[size_t(k)]->w->J;
@@ -642,12 +673,17 @@ void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
     if (np) FQZ5_HIP(launch_fqz_carry(g.upload(jobs), np, g.stream));
     for (int k = 0; k < np; k++) FQZ5_HIP(launch_fqz_bytes(par[size_t(k)]->w->J, 2, g.stream));
 
-    for (FqzEncReq &R : reqs) g.download(&R.w->clen, R.w->E.out_len, 1);
+    for (size_t i = 0; i < reqs.size(); i++)
+        if (!(skip && (*skip)[i])) g.download(&reqs[i].w->clen, reqs[i].w->E.out_len, 1);
     g.sync();
-    for (FqzEncReq &R : reqs) {
+    for (size_t i = 0; i < reqs.size(); i++) {
+        FqzEncReq &R = reqs[i];
         FqzEncReq::Work &W = *R.w;
         for (int r = 0; r < R.nrec; r++) R.flags[r] &= 0xffff;
+        if (skip && (*skip)[i]) continue;
         if (W.clen > W.room) continue;   // (cannot happen: the bound covers the coder)
+        if (W.lb > uint64_t(W.hdr.size()) + W.clen)   // the entropy bound is a theorem
+            throw std::runtime_error("fqz: size below its entropy bound");
         Piece h;
         h.host = W.hdr;
         Piece d;
@@ -657,6 +693,13 @@ void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         R.out.push_back(d);
         R.ok = true;
     }
+}
+
+uint64_t fqz_size_lower_bound(const FqzEncReq &r) { return r.w ? r.w->lb : 0; }
+
+void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
+    fqz_encode_prepare(g, reqs);
+    fqz_encode_finish(g, reqs, nullptr);
 }
 
 uint8_t *fqz_encode_gpu(int vers, fqz_slice *s, const uint8_t *in, size_t n, size_t *out_size,

@@ -32,6 +32,14 @@ struct FqzEncReq {
 uint32_t fqz_hot_min();
 uint32_t fqz_set_hot_min(uint32_t v);
 void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs);
+// fqz_encode_batch in two halves: prepare runs every stage up to the model
+// pass and sets each parallel request's size lower bound (entropy of its
+// events; fqz_size_lower_bound, 0 if unknown); finish runs the range chain
+// and the bytes of the requests not marked in skip (skipped ones get no
+// output, ok = false).
+void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs);
+void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vector<char> *skip);
+uint64_t fqz_size_lower_bound(const FqzEncReq &r);
 
 struct FqzDecReq {
     const uint8_t *h_in = nullptr;      // host copy of the stream (parameters)

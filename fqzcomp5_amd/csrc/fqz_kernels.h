@@ -138,6 +138,8 @@ constexpr uint32_t FQZ_HOT_MIN = 16384;
 hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t *hot,
                                  uint32_t stride, uint32_t hot_min, hipStream_t s);
 hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
+// per workgroup: sum over its events of log2(total / freq) (after the model pass)
+hipError_t launch_fqz_entropy(const FqzEvJob &j, double *partial, uint32_t nblk, hipStream_t s);
 hipError_t launch_fqz_carry(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
 hipError_t launch_fqz_expand(const FqzEvJob &j, hipStream_t s);
 hipError_t launch_fqz_bytes(const FqzEvJob &j, int phase, hipStream_t s);

@@ -541,6 +541,33 @@ __global__ __launch_bounds__(64) void k_fqz_model_hot(const FqzEvJob *Js, const 
     }
 }
 
+// Entropy of a block's events under the adaptive models: sum of
+// log2(total / freq) over the codes the model pass wrote, one partial sum
+// per workgroup (the host adds them).  The coder's byte count P satisfies
+// 8 P >= this - 8, so it bounds the output size from
+// below before the range chain runs.
+__global__ __launch_bounds__(256) void k_fqz_entropy(FqzEvJob J, double *partial) {
+    __shared__ double red[256];
+    double acc = 0.0;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < J.nev; k += gridDim.x * blockDim.x) {
+        const uint64_t c = J.code[k];
+        const uint32_t f = uint32_t(c >> 16) & 0xffffu, t = uint32_t(c >> 32);
+        acc += log2(double(t)) - log2(double(f));
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (uint32_t o = 128; o; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+hipError_t launch_fqz_entropy(const FqzEvJob &j, double *partial, uint32_t nblk, hipStream_t s) {
+    if (nblk) hipLaunchKernelGGL(k_fqz_entropy, dim3(nblk), dim3(256), 0, s, j, partial);
+    return hipGetLastError();
+}
+
 // Phase 3b: per event (in stream order) the record the range chain reads:
 // {RN(1/total) as two words, freq, cum}.
 __global__ void k_fqz_expand(FqzEvJob J) {

@@ -72,11 +72,24 @@ class TrialState(C.Structure):
 _bound = False
 
 
+TRIAL_WINDOW = 3      # FQZ5_METRICS_TRIAL (fqzcomp5.c:152)
+
+
+def trial_counts() -> tuple[int, int]:
+    """(fqz candidates tried, of which pruned) since the library was loaded."""
+    out = (C.c_uint64 * 2)()
+    _load().fqz5_trial_counts(out)
+    return int(out[0]), int(out[1])
+
+
 def _load():
     global _bound
     so = _lib.load()
     if not _bound:
         so.fqz5_trial_init.argtypes = [C.POINTER(TrialState)]
+        so.fqz5_set_trial_prune.restype = C.c_int
+        so.fqz5_set_trial_prune.argtypes = [C.c_int]
+        so.fqz5_trial_counts.argtypes = [C.POINTER(C.c_uint64)]
         so.fqz5_trial_schedule.argtypes = [C.POINTER(C.c_int32), C.c_int,
                                            C.POINTER(C.c_uint32), C.POINTER(TrialState),
                                            C.POINTER(C.c_uint32)]
@@ -215,7 +228,7 @@ def exchange_sizes(local: np.ndarray, in_sizes: np.ndarray, sec_ids: np.ndarray,
 
 
 def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
-               group=None, speculate: bool = True):
+               group=None, speculate: bool = True, prune: bool = True):
     """try -> (exchange) -> replay -> commit for this rank's sections.
 
     speculate: every section tries every method in one GPU launch.  A launch
@@ -223,21 +236,35 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
     little, while encoding the non-trial sections after the replay would add
     a second chain-length launch.  speculate=False tries only the sections
     the schedule names (trial and re-trial blocks) and encodes the others
-    once at commit, for candidates that do cost in proportion to their work."""
+    once at commit, for candidates that do cost in proportion to their work.
+
+    prune: fqz candidates that provably cannot win the trial skip their range
+    chain (fqz5_set_trial_prune), when this rank holds every section the
+    schedule has try fqz and they form one whole trial window."""
     ins = np.array([s.in_size for s in secs], np.uint32)
     ids = np.array([s.sec for s in secs], np.int32)
     av = np.asarray(avail, np.uint32)
     if speculate and not (av & FQZ_MASK).any():
         masks = av[ids]
+        prune = False
     else:
         blank = np.zeros((len(secs), M_LAST), np.uint32)
         _, _, g_ids0, off = exchange_sizes(blank, ins, ids, group)
-        sched = trial_schedule(g_ids0, avail, state)[off:off + len(secs)]
+        sched_all = trial_schedule(g_ids0, avail, state)
+        sched = sched_all[off:off + len(secs)]
         # rANS candidates stay speculative (chain-bound, nearly free in one
         # launch); fqz candidates cost in proportion to their work, so only
         # the scheduled trial sections try them
         masks = (av[ids] & RANS_MASK) | (sched & FQZ_MASK) if speculate else sched
-    local = sections_try(secs, masks)
+        rows = np.nonzero(sched_all & FQZ_MASK)[0]
+        prune = prune and speculate and len(rows) == TRIAL_WINDOW and \
+            bool(((rows >= off) & (rows < off + len(secs))).all())
+    so = _load()
+    prev = so.fqz5_set_trial_prune(1 if prune else 0)
+    try:
+        local = sections_try(secs, masks)
+    finally:
+        so.fqz5_set_trial_prune(prev)
     g_sizes, g_ins, g_ids, off = exchange_sizes(local, ins, ids, group)
     tried = np.zeros(len(g_ids), np.uint32)
     meth_all = trial_replay(g_ids, g_ins, g_sizes, avail, state, tried)

@@ -95,6 +95,21 @@ void fqz5_trial_replay(const int32_t *sec_ids, const uint32_t *in_sizes,
 int fqz5_sections_commit(const fqz5_section *secs, int n, const int32_t *methods,
                          fqz5_section_result *res);
 
+/* Trial pruning (off by default).  When on, fqz5_sections_try skips the
+ * range chain and bytes of an fqz candidate whose size is provably not below
+ * the best rANS candidate: its lower bound 8 P >= sum log2(total/freq) - 8
+ * (from the model pass) is at least the smallest exact rANS size in each of
+ * the call's fqz sections and, summed over them, at least the smallest sum
+ * of one rANS method.  rANS methods precede fqz ones, so they win ties: the
+ * pruned candidate can never be chosen, and its reported size is the bound.
+ * The caller turns it on only when the sections of the call that try fqz
+ * are exactly one whole trial window (FQZ5_METRICS_TRIAL sections of one
+ * section kind); otherwise the call does not prune.  Returns the previous
+ * setting. */
+int fqz5_set_trial_prune(int on);
+/* {fqz candidates tried, of which pruned} since the library was loaded. */
+void fqz5_trial_counts(uint64_t *out2);
+
 /* Decode framed sections (strat 0 = rANS) into their outputs. */
 int fqz5_decode_sections(const fqz5_section *secs, int n, fqz5_section_result *res);
 

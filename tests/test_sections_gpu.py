@@ -35,7 +35,9 @@ def test_run_vs_reference(level, kind, nreads, blk):
     blocks = synth.split_blocks(reads, blk)
     assert len(blocks) >= 5
     run = S.Run(reads, blocks, torch.device("cuda", 0))
-    res, meth_all, _, tried, _ = S.encode_run(run.enc_secs(), S.masks(level), S.new_state())
+    t0, p0 = S.trial_counts()
+    res, meth_all, sizes, tried, _ = S.encode_run(run.enc_secs(), S.masks(level), S.new_state())
+    t1, p1 = S.trial_counts()
     assert all(r.status == 0 for r in res)
     offs = np.concatenate([[0], np.cumsum(reads.lens.astype(np.int64))])
     used = set()
@@ -53,6 +55,19 @@ def test_run_vs_reference(level, kind, nreads, blk):
             assert r.strat == 0
         assert run.chosen(res, i) == exp, (i, m)
     if level == 5:
+        # a reported fqz size is exact, or (pruned) a lower bound that is at
+        # least the section's best rANS size: never above the true size
+        for i, (sec, s, e, fl, k) in enumerate(run.spans):
+            for m in (S.FQZ1, S.FQZ3):
+                if sec != S.SEC_QUAL or int(sizes[i, m]) == 0xFFFFFFFF:
+                    continue                        # not a try-phase candidate
+                a, b = blocks[k]
+                true = len(codec.fqz_compress((reads.qual)[s:e].tobytes(), reads.lens[a:b].copy(),
+                                              np.zeros(b - a, np.uint32), m - S.FQZ0,
+                                              reads.seq[s:e].tobytes()))
+                assert int(sizes[i, m]) <= true, (i, m, int(sizes[i, m]), true)
+        if kind == "novaseq":                       # rANS wins by a margin: fqz pruned
+            assert p1 - p0 > 0 and t1 - t0 >= p1 - p0
         fqz_bits = (1 << S.FQZ1) | (1 << S.FQZ3)
         assert all(int(t) & fqz_bits for t, (sec, *_) in zip(tried[:6], run.spans)
                    if sec == S.SEC_QUAL)            # the trial blocks tried fqz
