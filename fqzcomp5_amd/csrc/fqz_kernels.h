@@ -126,7 +126,7 @@ struct FqzEvJob {
     uint32_t pad2;
     uint8_t *out;
     uint32_t *out_len;
-    uint32_t *done;             // hedged range chain: raised by the first copy to finish
+    uint32_t *done;             // hedged range chain: claim word (zeroed; ~0 = a copy finished)
 };
 
 hipError_t launch_fqz_events(const FqzEvJob &j, int phase, hipStream_t s);

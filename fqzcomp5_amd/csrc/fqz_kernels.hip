@@ -648,11 +648,16 @@ __global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
     for (uint32_t base = 0; base < nev; base += RC_BLK) {
         const uint32_t cnt = min(RC_BLK, nev - base);
         if (base + RC_BLK < nev) fetch(base + RC_BLK);
-        // hedged launch (done != nullptr): two copies of the chain on two CUs
-        // write identical outputs; the flag loaded now is looked at after
-        // this block, and the copy that sees it raised leaves
-        const uint32_t hedge = J.done ? __hip_atomic_load(J.done, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        // hedged launch (done != nullptr): 2-4 copies of the chain on
+        // different CUs compute identical outputs.  *done is a claim word
+        // (as in rans_chain.hip): the copy that starts this block first
+        // writes it; ~0 means a copy has finished, and the others leave
+        // after their current block.  The old value is looked at after it.
+        const uint32_t blk = base / RC_BLK;
+        uint32_t hedge = 0u;
+        if (J.done && l == 0)
+            hedge = __hip_atomic_fetch_max(J.done, blk + 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
 #ifdef FQZ5_RC_PROBE
         const uint64_t c0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -687,20 +692,23 @@ __global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
 #ifdef FQZ5_RC_PROBE
         pc += __builtin_amdgcn_s_memtime() - c0;
 #endif
+        hedge = __builtin_amdgcn_readlane(hedge, 0);
+        if (hedge <= blk) {
 #pragma unroll
-        for (uint32_t r = 0; r < RC_PER; r++) {
-            const uint32_t i = uint32_t(l) + 64u * r;   // q here; cum * q in k_fqz_accum
-            const uint32_t q = s_q[i];
-            const uint32_t k = (uint32_t(__builtin_clz((q * s_f[i]) | 1u)) & 24u) >> 3;
-            __builtin_amdgcn_raw_buffer_store_b32(q, radd, (base + i) * 4u, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(k, rsh, (base + i) * 4u, 0, 0);
+            for (uint32_t r = 0; r < RC_PER; r++) {
+                const uint32_t i = uint32_t(l) + 64u * r;   // q here; cum * q in k_fqz_accum
+                const uint32_t q = s_q[i];
+                const uint32_t k = (uint32_t(__builtin_clz((q * s_f[i]) | 1u)) & 24u) >> 3;
+                __builtin_amdgcn_raw_buffer_store_b32(q, radd, (base + i) * 4u, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(k, rsh, (base + i) * 4u, 0, 0);
+            }
         }
         if (base + RC_BLK < nev) stage();
         __syncthreads();
-        if (__builtin_amdgcn_readfirstlane(hedge)) return;
+        if (hedge == ~0u) return;
     }
     if (J.done && l == 0)
-        __hip_atomic_store(J.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(J.done, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef FQZ5_RC_PROBE
     if (l == 0 && blockIdx.x == 0) {
         g_rcprobe[0] = __builtin_amdgcn_s_memtime() - p0;

@@ -89,7 +89,7 @@ struct DecJob {
     int32_t bits;
     uint32_t rows;          // table rows (1 for O0)
     uint32_t mode;          // DEC_TAB_* (dec_table_mode)
-    uint32_t *done;         // hedged launch: raised by the first copy to finish (or nullptr)
+    uint32_t *done;         // hedged launch: claim word, zeroed; ~0 = a copy finished (or nullptr)
 };
 
 // Decoder table placement (rans_chain.hip).  Per slot of a row of 2^bits:

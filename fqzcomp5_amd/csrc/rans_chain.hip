@@ -426,18 +426,24 @@ static DEV uint32_t vbcnt(uint32_t m, uint32_t acc, uint32_t after) {
 
 // Hedged chains (DecJob::done != nullptr): the host launches every stream
 // 2-4 times, on different CUs, because the same chain runs up to ~20 %
-// slower on some CUs than on others.  All copies write
-// identical bytes; the first to finish raises done, and the others leave at
-// their next group boundary.  The flag is loaded at a group's start and looked at its
-// end, so the chain never waits for it.
-static DEV uint32_t hedge_poll(const DecJob &J) {
-    if (!J.done) return 0u;
-    return __hip_atomic_load(J.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// slower on some CUs than on others.  All copies
+// compute identical bytes.  *done is a claim word: a copy starting group g
+// raises it to g+1 (atomic max) and writes group g only if it was the first
+// to start it, so every group is written once; the first copy to finish sets
+// it to ~0 and the others leave after their current group.  The claim is
+// issued at a group's start and its old value looked at the group's end, so
+// the chain never waits for it.  Unhedged (done == nullptr): always write.
+static DEV uint32_t hedge_claim(const DecJob &J, uint32_t g) {
+    uint32_t v = 0u;
+    if (J.done && threadIdx.x == 0)
+        v = __hip_atomic_fetch_max(J.done, g + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
 }
-static DEV bool hedge_lost(uint32_t v) { return __builtin_amdgcn_readfirstlane(v) != 0u; }
+static DEV bool hedge_first(uint32_t v, uint32_t g) { return __builtin_amdgcn_readlane(v, 0) <= g; }
+static DEV bool hedge_lost(uint32_t v) { return __builtin_amdgcn_readlane(v, 0) == ~0u; }
 static DEV void hedge_won(const DecJob &J) {
     if (J.done && threadIdx.x == 0)
-        __hip_atomic_store(J.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(J.done, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 struct DecShared {
@@ -637,7 +643,7 @@ static DEV void dec4_body(const DecJob &J) {
             pf = load_slab(wsrc, slabs, l);
         }
         __syncthreads();
-        const uint32_t hedge = hedge_poll(J);
+        const uint32_t hedge = hedge_claim(J, t0 / G);
         const uint32_t t1 = (T - t0 < G) ? T : t0 + G;
         const uint32_t tf = t1 < Tfull ? t1 : (t0 > Tfull ? t0 : Tfull);
         uint32_t t = t0;
@@ -681,7 +687,7 @@ static DEV void dec4_body(const DecJob &J) {
             ptr += uint32_t(__popcll(m & 15u));
         }
         __syncthreads();
-        dec_flush<O1, NX, true>(J, sh, t0, t1 - t0, l);
+        if (hedge_first(hedge, t0 / G)) dec_flush<O1, NX, true>(J, sh, t0, t1 - t0, l);
         __syncthreads();
         if (hedge_lost(hedge)) return;
     }
@@ -725,7 +731,7 @@ static DEV void dec32_body(const DecJob &J) {
             pf = load_slab(wsrc, slabs, l);
         }
         __syncthreads();
-        const uint32_t hedge = hedge_poll(J);
+        const uint32_t hedge = hedge_claim(J, t0 / G);
         const uint32_t t1 = (T - t0 < G) ? T : t0 + G;
         for (uint32_t t = t0; t < t1; t++) {
             const bool act = l < NX && (O1 ? t < lenz : uint32_t(NX) * t + z < n);
@@ -744,7 +750,7 @@ static DEV void dec32_body(const DecJob &J) {
             ptr += uint32_t(__popcll(m & 0xffffffffull));
         }
         __syncthreads();
-        dec_flush<O1, NX, false>(J, sh, t0, t1 - t0, l);
+        if (hedge_first(hedge, t0 / G)) dec_flush<O1, NX, false>(J, sh, t0, t1 - t0, l);
         __syncthreads();
         if (hedge_lost(hedge)) return;
     }
@@ -831,7 +837,7 @@ static DEV void dec4_o0_body(const DecJob &J) {
             pf = load_slab(wsrc, slabs, l);
         }
         __syncthreads();
-        const uint32_t hedge = hedge_poll(J);
+        const uint32_t hedge = hedge_claim(J, t0 / G);
         // word p of this group sits at byte wbase + 2p of the LDS (p - gp < 1028)
         const uint32_t gp = ptr;
         const uint32_t wbase = ring_lds + 2 * ((gp & (RING_WORDS - 1)) - gp);
@@ -894,7 +900,10 @@ static DEV void dec4_o0_body(const DecJob &J) {
         ptr = __builtin_amdgcn_readfirstlane(ptr);
         __syncthreads();
         const uint32_t cnt = (t1 - t0) * NX;
-        if (cnt == NX * G && NX * t0 + NX * G <= n && (reinterpret_cast<uintptr_t>(J.out) & 15) == 0) {
+        if (!hedge_first(hedge, t0 / G)) {
+            // another copy started this group first and writes it
+        } else if (cnt == NX * G && NX * t0 + NX * G <= n &&
+                   (reinterpret_cast<uintptr_t>(J.out) & 15) == 0) {
             // a whole group: lane l writes output bytes [16l, 16l+16), i.e.
             // steps 4l..4l+3 of the 4 states, as one 16-byte store
             uint32_t v[4] = {0, 0, 0, 0};
