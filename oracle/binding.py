@@ -178,3 +178,55 @@ def ref() -> _Codec:
     if "ref" not in _cache:
         _cache["ref"] = _Codec(REF_SO, "")
     return _cache["ref"]
+
+
+# ---- sequence context model (fqzcomp5.c:1073-1406) -------------------------
+REF_CLI_SO = os.path.join(HERE, "_ref", "libfqz5ref.so")
+
+
+class SeqCM:
+    """encode_seq / decode_seq: ``ora_seq_*`` in liboracle.so, or the
+    reference's own functions in ``_ref/libfqz5ref.so``."""
+
+    def __init__(self, path: str, enc: str, dec: str):
+        self.lib = C.CDLL(path)
+        self._e = getattr(self.lib, enc)
+        self._e.restype = C.c_void_p
+        self._e.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint32), C.c_int,
+                            C.c_int, C.c_int, C.POINTER(C.c_uint)]
+        self._d = getattr(self.lib, dec)
+        self._d.restype = C.c_void_p
+        self._d.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint32), C.c_int,
+                            C.c_int, C.c_int, C.c_uint]
+
+    @staticmethod
+    def _lens(lens):
+        lens = list(lens) or [0]
+        return (C.c_uint32 * len(lens))(*lens), len(lens)
+
+    def encode(self, seq: bytes, lens, both: int, k: int):
+        la, nr = self._lens(lens)
+        n = C.c_uint(0)
+        p = self._e(seq, len(seq), la, nr, both, k, C.byref(n))
+        return _Codec._take(p, n.value)
+
+    def decode(self, comp: bytes, lens, both: int, k: int, out_size: int):
+        la, nr = self._lens(lens)
+        p = self._d(comp, len(comp), la, nr, both, k, out_size)
+        return _Codec._take(p, out_size)
+
+
+def seq_oracle() -> SeqCM:
+    if "seq_ora" not in _cache:
+        _cache["seq_ora"] = SeqCM(ORACLE_SO, "ora_seq_encode", "ora_seq_decode")
+    return _cache["seq_ora"]
+
+
+def have_seq_ref() -> bool:
+    return os.path.exists(REF_CLI_SO)
+
+
+def seq_ref() -> SeqCM:
+    if "seq_ref" not in _cache:
+        _cache["seq_ref"] = SeqCM(REF_CLI_SO, "encode_seq", "decode_seq")
+    return _cache["seq_ref"]

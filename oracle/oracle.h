@@ -44,4 +44,9 @@ uint8_t *ora_fqz_compress(int vers, ora_fqz_slice *s, uint8_t *in, size_t in_siz
                           size_t *out_size, int strat, void *gp);
 uint8_t *ora_fqz_decompress(uint8_t *in, size_t in_size, size_t *out_size,
                             int *lengths, int nlengths, ora_fqz_slice *s);
+/* sequence context model, fqzcomp5.c:1073-1406 (encode_seq / decode_seq) */
+uint8_t *ora_seq_encode(const uint8_t *in, uint32_t n, const uint32_t *len, int nrec,
+                        int both, int k, uint32_t *out_size);
+uint8_t *ora_seq_decode(const uint8_t *in, uint32_t in_size, const uint32_t *len, int nrec,
+                        int both, int k, uint32_t out_size);
 #endif
