@@ -613,41 +613,31 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
     }
 }
 
-// The range chain and the output bytes of every parallel request not in
-// `skip` (skip[i] != 0: request i is left without output), and the sizes.
-void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vector<char> *skip) {
-    std::vector<FqzEncReq *> par;
-    std::vector<FqzEvJob> jobs;
-    for (size_t i = 0; i < reqs.size(); i++)
-        if (reqs[i].w->parallel && !(skip && (*skip)[i])) {
-            par.push_back(&reqs[i]);
-            jobs.push_back(reqs[i].w->J);
-        }
-    const int np = int(par.size());
-    // the range chain of every block (one wave each), then the output bytes
-    for (int k = 0; k < np; k++) {
-        FqzEvJob &J = par[size_t(k)]->w->J;
-        J.rec = g.arena.alloc_n<uint4>(J.nev);
-        FQZ5_HIP(launch_fqz_expand(J, g.stream));
-        J.addend = g.arena.alloc_n<uint32_t>(J.nev);
-        J.shifts = g.arena.alloc_n<uint32_t>(J.nev + 1);
-        jobs[size_t(k)] = J;
+// The range coder back end for event jobs whose rec[] holds every event in
+// stream order: the range chain of every job (one wave each, hedged), the
+// scan of the byte shifts, and the big-number bytes into J.out / *J.out_len.
+void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
+    const int np = int(js.size());
+    if (!np) return;
+    std::vector<FqzEvJob> rj;
+    for (FqzEvJob *J : js) {
+        J->addend = g.arena.alloc_n<uint32_t>(J->nev);
+        J->shifts = g.arena.alloc_n<uint32_t>(J->nev + 1);
+        J->done = nullptr;
+        rj.push_back(*J);
     }
-    if (np) {
-        // hedge: each range chain twice, on two CUs
-        std::vector<FqzEvJob> rj(jobs.begin(), jobs.end());
-        const size_t copies = hedge_copies(rj.size(), size_t(g.cus));
-        if (copies > 1) {
-            uint32_t *d_done = g.arena.alloc_n<uint32_t>(rj.size());
-            g.memset0(d_done, rj.size() * 4);
-            for (size_t k = 0; k < rj.size(); k++) rj[k].done = d_done + k;
-            for (size_t c = 1; c < copies; c++) rj.insert(rj.end(), rj.begin(), rj.begin() + long(np));
-        }
-        FQZ5_HIP(launch_fqz_rc(g.upload(rj), int(rj.size()), g.stream));
+    // hedge: each range chain on 2-4 CUs
+    const size_t copies = hedge_copies(rj.size(), size_t(g.cus));
+    if (copies > 1) {
+        uint32_t *d_done = g.arena.alloc_n<uint32_t>(rj.size());
+        g.memset0(d_done, rj.size() * 4);
+        for (size_t k = 0; k < rj.size(); k++) rj[k].done = d_done + k;
+        for (size_t c = 1; c < copies; c++) rj.insert(rj.end(), rj.begin(), rj.begin() + long(np));
     }
+    FQZ5_HIP(launch_fqz_rc(g.upload(rj), int(rj.size()), g.stream));
+    std::vector<uint32_t> P(size_t(np), 0);
     for (int k = 0; k < np; k++) {
-        FqzEncReq::Work &W = *par[size_t(k)]->w;
-        FqzEvJob &J = W.J;
+        FqzEvJob &J = *js[size_t(k)];
         uint32_t *pos = g.arena.alloc_n<uint32_t>(J.nev + 1);
         g.memset0(J.shifts + J.nev, 4);
         size_t tb = 0;
@@ -656,22 +646,40 @@ void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vecto
         FQZ5_HIP(fqz_exclusive_scan(J.shifts, pos, int(J.nev + 1), tmp, tb, g.stream));
         J.pos = pos;
         J.nshift = pos + J.nev;
-        g.download(&W.P, pos + J.nev, 1);
+        g.download(&P[size_t(k)], pos + J.nev, 1);
     }
     g.sync();
+    std::vector<FqzEvJob> cj;
+    for (int k = 0; k < np; k++) {
+        FqzEvJob &J = *js[size_t(k)];
+        J.nwords = (P[size_t(k)] + 5 + 3) / 4 + 2;
+        J.acc = reinterpret_cast<unsigned long long *>(g.arena.alloc_n<uint64_t>(J.nwords));
+        g.memset0(J.acc, size_t(J.nwords) * 8);
+        FQZ5_HIP(launch_fqz_bytes(J, 0, g.stream));
+        cj.push_back(J);
+    }
+    FQZ5_HIP(launch_fqz_carry(g.upload(cj), np, g.stream));
+    for (int k = 0; k < np; k++) FQZ5_HIP(launch_fqz_bytes(*js[size_t(k)], 2, g.stream));
+}
+
+// The range chain and the output bytes of every parallel request not in
+// `skip` (skip[i] != 0: request i is left without output), and the sizes.
+void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vector<char> *skip) {
+    std::vector<FqzEncReq *> par;
+    for (size_t i = 0; i < reqs.size(); i++)
+        if (reqs[i].w->parallel && !(skip && (*skip)[i])) par.push_back(&reqs[i]);
+    const int np = int(par.size());
+    std::vector<FqzEvJob *> js;
     for (int k = 0; k < np; k++) {
         FqzEncReq::Work &W = *par[size_t(k)]->w;
         FqzEvJob &J = W.J;
-        J.nwords = (W.P + 5 + 3) / 4 + 2;
-        J.acc = reinterpret_cast<unsigned long long *>(g.arena.alloc_n<uint64_t>(J.nwords));
-        g.memset0(J.acc, size_t(J.nwords) * 8);
+        J.rec = g.arena.alloc_n<uint4>(J.nev);
+        FQZ5_HIP(launch_fqz_expand(J, g.stream));
         J.out = W.E.out;
         J.out_len = W.E.out_len;
-        FQZ5_HIP(launch_fqz_bytes(J, 0, g.stream));
-        jobs[size_t(k)] = J;
+        js.push_back(&J);
     }
-    if (np) FQZ5_HIP(launch_fqz_carry(g.upload(jobs), np, g.stream));
-    for (int k = 0; k < np; k++) FQZ5_HIP(launch_fqz_bytes(par[size_t(k)]->w->J, 2, g.stream));
+    rc_backend(g, js);
 
     for (size_t i = 0; i < reqs.size(); i++)
         if (!(skip && (*skip)[i])) g.download(&reqs[i].w->clen, reqs[i].w->E.out_len, 1);

@@ -40,6 +40,11 @@ void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs);
 void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs);
 void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vector<char> *skip);
 uint64_t fqz_size_lower_bound(const FqzEncReq &r);
+struct FqzEvJob;
+// The range coder back end shared by fqz and the sequence model: for jobs
+// whose rec[] (stream order), nev, out and out_len are set, the range
+// chain, the shift scan and the big-number bytes (*out_len = size).
+void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js);
 
 struct FqzDecReq {
     const uint8_t *h_in = nullptr;      // host copy of the stream (parameters)

@@ -1,0 +1,345 @@
+// seq_cm.hip — fqzcomp5's sequence context model (SEQ10 .. SEQ14B,
+// fqzcomp5.c:1073-1406) on the GPU.
+//
+// Encoder.  A k-mer context model (4 u8 counts per context,
+// c_small_model.h) plus run-length, literal and state models feed one range
+// coder.  A model's counts depend only on the events of that model, so, as
+// for fqzcomp_qual (fqz_kernels.hip), every context runs over its own events
+// in parallel after a stable sort by context, the side models run in one
+// pass over the runs, and the range coder back end (rc_backend,
+// fqz_codec.cpp) codes the events in stream order.
+//   heads / runs  the block's runs of one class (uppercase ACGT / lowercase
+//                 acgt / other bytes), their starts and event counts
+//   ctx           per record, the forward k-mer of every base and, in
+//                 both-strand mode, the reverse-complement k-mer whose model
+//                 counts the base that leaves it (fqzcomp5.c:1176-1199)
+//   model         per context, its events in stream order -> {1/total,
+//                 freq, cum} of the coded ones
+//   side          run-length digits, literal bytes and class switches
+// Decoder.  Each symbol selects the next context, so a block is one chain
+// (k_seq_dec).
+#include "fqz_model.hpp"
+#include "seq_cm.h"
+
+namespace fqz5 {
+
+// fqzcomp5.c:1107-1118
+DEV uint32_t seq_class(uint32_t c) {
+    switch (c) {
+    case 'A': case 'C': case 'G': case 'T': return 0u;
+    case 'a': case 'c': case 'g': case 't': return 1u;
+    default: return 2u;
+    }
+}
+
+DEV uint32_t seq_code(uint32_t c) {
+    switch (c | 0x20u) {
+    case 'a': return 0u;
+    case 'c': return 1u;
+    case 'g': return 2u;
+    default: return 3u;
+    }
+}
+
+// the stored bit of a class switch (fqzcomp5.c:1120-1124, :1243-1261)
+DEV uint32_t switch_bit(uint32_t from, uint32_t to) {
+    return to == 0u ? 0u : to == 1u ? uint32_t(from == 2u) : 1u;
+}
+
+DEV uint32_t switch_to(uint32_t from, uint32_t bit) {
+    if (from == 0u) return bit ? 2u : 1u;
+    if (from == 1u) return bit ? 2u : 0u;
+    return bit ? 1u : 0u;
+}
+
+// the context seeds of fqzcomp5.c:1103-1105
+DEV uint32_t seed_fw(uint32_t mask) { return 0x007616c7u & mask; }
+DEV uint32_t seed_rv(uint32_t k, uint32_t mask) { return (0x2c6b62ffu >> (32u - 2u * k)) & mask; }
+
+// 4 u8 counts in one word: total, cumulative count below `sym`, update
+DEV uint32_t sm4_total(uint32_t F) { return __builtin_amdgcn_sad_u8(F, 0u, 0u); }
+DEV uint32_t sm4_cum(uint32_t F, uint32_t sym) {
+    return sym ? __builtin_amdgcn_sad_u8(F & ((1u << (8u * sym)) - 1u), 0u, 0u) : 0u;
+}
+// c_small_model.h:104-131: +1, then halve every count if the total before
+// the update was >= 255 (counts stay <= 253, so bytes never carry)
+DEV uint32_t sm4_bump(uint32_t F, uint32_t sym, uint32_t tot) {
+    F += 1u << (8u * sym);
+    if (tot >= 255u) F -= (F >> 1) & 0x7F7F7F7Fu;
+    return F;
+}
+
+DEV uint4 rc_rec(uint32_t f, uint32_t cum, uint32_t tot) {
+    const uint64_t bits = uint64_t(__double_as_longlong(1.0 / double(tot)));
+    return make_uint4(uint32_t(bits), uint32_t(bits >> 32), f, cum);
+}
+
+// ---------------------------------------------------------------------------
+__global__ void k_seq_heads(SeqJob J) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= J.n) return;
+    J.flag[p] = p == 0 || seq_class(J.in[p]) != seq_class(J.in[p - 1]);
+}
+
+__global__ void k_seq_run_starts(SeqJob J) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < J.n && J.flag[p]) J.run_start[J.ex[p]] = p;
+}
+
+// per run: its digit count D = L/255 + 1 plus the switch after it
+__global__ void k_seq_run_cnt(SeqJob J) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r > J.nrun) return;
+    if (r == J.nrun) {
+        J.cnt[r] = 0;
+        return;
+    }
+    const uint32_t end = r + 1 < J.nrun ? J.run_start[r + 1] : J.n;
+    J.cnt[r] = (end - J.run_start[r]) / 255u + 2u;
+}
+
+// one thread per record segment (contexts restart at its start)
+__global__ void k_seq_ctx(SeqJob J) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= J.nseg) return;
+    const uint32_t mask = J.mask, inval = mask + 1u, top = 2u * J.k - 2u;
+    uint32_t fw = seed_fw(mask), rv = seed_rv(J.k, mask);
+    const uint32_t stride = J.both ? 2u : 1u;
+    for (uint32_t p = J.seg[s]; p < J.seg[s + 1]; p++) {
+        const uint32_t c = J.in[p];
+        const uint32_t i = stride * p;
+        if (seq_class(c) < 2u) {
+            const uint32_t b = seq_code(c);
+            J.key[i] = fw;
+            J.val[i] = (uint64_t(2u * p) << 8) | b;
+            fw = ((fw << 2) + b) & mask;
+            if (J.both) {
+                const uint32_t b2 = rv & 3u;
+                rv = (rv >> 2) + ((3u - b) << top);
+                J.key[i + 1] = rv;
+                J.val[i + 1] = (uint64_t(2u * p + 1u) << 8) | b2;
+            }
+        } else {
+            J.key[i] = inval;
+            if (J.both) J.key[i + 1] = inval;
+        }
+    }
+}
+
+// event index of the symbol at byte p (seq_cm.h)
+DEV uint32_t sym_event(const SeqJob &J, uint32_t p) {
+    const uint32_t r = J.ex[p] + J.flag[p] - 1u;
+    return p + J.lead + J.run_off[r] + J.cnt[r] - 1u;
+}
+
+// one thread per context: the head of its run in the sorted order walks it
+__global__ void k_seq_model(SeqJob J) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= J.nkeys) return;
+    const uint32_t key = J.skey[i];
+    if (key > J.mask || (i > 0 && J.skey[i - 1] == key)) return;
+    uint32_t F = 0x01010101u;
+    for (uint32_t j = i; j < J.nkeys && J.skey[j] == key; j++) {
+        const uint64_t v = J.sval[j];
+        const uint32_t sym = uint32_t(v) & 3u;
+        const uint32_t ord = uint32_t(v >> 8);
+        const uint32_t tot = sm4_total(F);
+        if (!(ord & 1u)) {
+            const uint32_t p = ord >> 1;
+            J.rec[sym_event(J, p)] = rc_rec((F >> (8u * sym)) & 255u, sm4_cum(F, sym), tot);
+        }
+        F = sm4_bump(F, sym, tot);
+    }
+}
+
+// the run-length, literal and state models over the runs in stream order
+__global__ __launch_bounds__(64) void k_seq_side(SeqJob J) {
+    __shared__ FList<256> run[3], lit;
+    if (threadIdx.x != 0 || J.n == 0) return;
+    for (int c = 0; c < 3; c++) fl_init(&run[c], 256);
+    fl_init(&lit, 256);
+    uint32_t st[3] = {0x0101u, 0x0101u, 0x0101u};   // 2 u8 counts each
+    auto put_fl = [&](FList<256> *m, uint32_t sym, uint32_t e) {
+        uint32_t acc = 0;
+        int k = 1;
+        while (m->sy[k] != sym) acc += m->fr[k++];
+        J.rec[e] = rc_rec(m->fr[k], acc, m->total);
+        fl_bump(m, k);
+    };
+    auto put_st = [&](uint32_t c, uint32_t bit, uint32_t e) {
+        const uint32_t F = st[c], tot = (F & 255u) + (F >> 8);
+        J.rec[e] = rc_rec(bit ? F >> 8 : F & 255u, bit ? F & 255u : 0u, tot);
+        st[c] = sm4_bump(F, bit, tot);
+    };
+    const uint32_t n = J.n;
+    if (J.lead) {
+        put_fl(&run[0], 0u, 0u);
+        put_st(0u, switch_bit(0u, seq_class(J.in[0])), 1u);
+    }
+    for (uint32_t r = 0; r < J.nrun; r++) {
+        const uint32_t s = J.run_start[r];
+        const uint32_t L = (r + 1 < J.nrun ? J.run_start[r + 1] : n) - s;
+        const uint32_t c = seq_class(J.in[s]);
+        const uint32_t D = J.cnt[r] - 1u;
+        const uint32_t base = s + J.lead + J.run_off[r];   // first digit
+        for (uint32_t d = 0; d < D; d++) put_fl(&run[c], d + 1 < D ? 255u : L - 255u * (D - 1u), base + d);
+        if (c == 2u)
+            for (uint32_t p = s; p < s + L; p++) put_fl(&lit, J.in[p], p + J.lead + J.run_off[r] + D);
+        if (r + 1 < J.nrun)
+            put_st(c, switch_bit(c, seq_class(J.in[s + L])), base + D + L);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Decoder: one lane per block runs the chain; models of the k-mer contexts
+// in HBM, the side models in LDS.
+__global__ void k_seq_models_init(uint32_t *m, size_t n) {
+    for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+        m[i] = 0x01010101u;
+}
+
+__global__ __launch_bounds__(64) void k_seq_dec(SeqDecJob J) {
+    __shared__ FList<256> run[3], lit;
+    if (threadIdx.x != 0) return;
+    for (int c = 0; c < 3; c++) fl_init(&run[c], 256);
+    fl_init(&lit, 256);
+    uint32_t st[3] = {0x0101u, 0x0101u, 0x0101u};
+    const uint8_t *in = J.in;
+    const uint32_t len = J.in_len, n = J.n, mask = J.mask, top = 2u * J.k - 2u;
+    // range decoder (c_range_coder.h); input past the end stops the chain
+    uint32_t code = 0, rng = 0xFFFFFFFFu, ip = 0;
+    bool bad = false;
+    if (len >= 5) {
+        for (int i = 0; i < 5; i++) code = (code << 8) | in[ip++];
+    } else {
+        bad = n > 0;
+    }
+    auto target = [&](uint32_t tot) -> uint32_t {
+        if (!tot || rng < tot) return 0u;
+        rng /= tot;
+        return code / rng;
+    };
+    auto take = [&](uint32_t cum, uint32_t f) {
+        code -= cum * rng;
+        rng *= f;
+        while (rng < (1u << 24)) {
+            if (ip >= len) {
+                bad = true;
+                return;
+            }
+            code = (code << 8) | in[ip++];
+            rng <<= 8;
+        }
+    };
+    auto get_fl = [&](FList<256> *m) -> uint32_t {
+        const uint32_t t = target(m->total);
+        if (t > FL_MAX) {
+            bad = true;
+            return 0u;
+        }
+        uint32_t acc = 0;
+        int k = 1;
+        while (acc + m->fr[k] <= t) acc += m->fr[k++];
+        if (k > 256) {
+            bad = true;
+            return 0u;
+        }
+        take(acc, m->fr[k]);
+        const uint32_t s = m->sy[k];
+        fl_bump(m, k);
+        return s;
+    };
+    auto get_st = [&](uint32_t c) -> uint32_t {
+        const uint32_t F = st[c], f0 = F & 255u, tot = f0 + (F >> 8);
+        const uint32_t bit = target(tot) >= f0;
+        take(bit ? f0 : 0u, bit ? F >> 8 : f0);
+        st[c] = sm4_bump(F, bit, tot);
+        return bit;
+    };
+
+    uint32_t fw = seed_fw(mask), rv = seed_rv(J.k, mask);
+    uint32_t si = 0, state = 0, p = 0, idle = 0;
+    while (p < n && !bad) {
+        uint32_t runlen = 0, d;
+        do {
+            d = get_fl(&run[state]);
+            runlen += d;
+        } while (d == 255u && !bad && runlen <= n);
+        if (bad) break;
+        if (runlen > n - p) runlen = n - p;
+        if (runlen == 0 && ++idle > 2) {   // only the first run can be empty
+            bad = true;
+            break;
+        }
+        const uint32_t end = p + runlen;
+        for (; p < end && !bad; p++) {
+            if (si + 1 < J.nseg && p == J.seg[si + 1]) {   // a record starts
+                si++;
+                fw = seed_fw(mask);
+                rv = seed_rv(J.k, mask);
+            }
+            if (state == 2u) {
+                J.out[p] = uint8_t(get_fl(&lit));
+                continue;
+            }
+            const uint32_t F = J.models[fw], tot = sm4_total(F);
+            const uint32_t t = target(tot);
+            const uint32_t c0 = F & 255u, c1 = c0 + ((F >> 8) & 255u), c2 = c1 + ((F >> 16) & 255u);
+            const uint32_t b = uint32_t(t >= c0) + uint32_t(t >= c1) + uint32_t(t >= c2);
+            take(sm4_cum(F, b), (F >> (8u * b)) & 255u);
+            J.models[fw] = sm4_bump(F, b, tot);
+            J.out[p] = uint8_t((state ? "acgt" : "ACGT")[b]);
+            fw = ((fw << 2) + b) & mask;
+            if (J.both) {
+                const uint32_t b2 = rv & 3u;
+                rv = (rv >> 2) + ((3u - b) << top);
+                const uint32_t G = J.models[rv];
+                J.models[rv] = sm4_bump(G, b2, sm4_total(G));
+            }
+        }
+        if (p >= n || bad) break;
+        state = switch_to(state, get_st(state));
+    }
+    *J.status = bad ? -1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+static dim3 grid_of(uint64_t n) { return dim3(unsigned((n + 255) / 256)); }
+
+hipError_t launch_seq_heads(const SeqJob &j, hipStream_t s) {
+    if (j.n) hipLaunchKernelGGL(k_seq_heads, grid_of(j.n), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_runs(const SeqJob &j, hipStream_t s) {
+    if (j.n) hipLaunchKernelGGL(k_seq_run_starts, grid_of(j.n), dim3(256), 0, s, j);
+    hipLaunchKernelGGL(k_seq_run_cnt, grid_of(uint64_t(j.nrun) + 1), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_ctx(const SeqJob &j, hipStream_t s) {
+    if (j.nseg && j.n) hipLaunchKernelGGL(k_seq_ctx, grid_of(j.nseg), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_model(const SeqJob &j, hipStream_t s) {
+    if (j.nkeys) hipLaunchKernelGGL(k_seq_model, grid_of(j.nkeys), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_side(const SeqJob &j, hipStream_t s) {
+    if (j.n) hipLaunchKernelGGL(k_seq_side, dim3(1), dim3(64), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_models_init(uint32_t *models, size_t nctx, hipStream_t s) {
+    hipLaunchKernelGGL(k_seq_models_init, dim3(1024), dim3(256), 0, s, models, nctx);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_dec(const SeqDecJob &j, hipStream_t s) {
+    hipLaunchKernelGGL(k_seq_dec, dim3(1), dim3(64), 0, s, j);
+    return hipGetLastError();
+}
+
+}  // namespace fqz5

@@ -98,6 +98,12 @@ def load() -> C.CDLL:
                                         C.POINTER(C.c_uint)]
     lib.arith_uncompress.restype = C.c_void_p
     lib.arith_uncompress.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint)]
+    lib.fqz5_seq_encode.restype = C.c_void_p
+    lib.fqz5_seq_encode.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint32), C.c_int,
+                                    C.c_int, C.c_int, C.POINTER(C.c_uint)]
+    lib.fqz5_seq_decode.restype = C.c_void_p
+    lib.fqz5_seq_decode.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint32), C.c_int,
+                                    C.c_int, C.c_int, C.c_uint]
     _lib = lib
     return lib
 
@@ -277,3 +283,31 @@ def fqz_decompress(comp: bytes, lens=None, flags=None, seq: bytes | None = None)
     out = C.string_at(p, n.value)
     _libc.free(p)
     return out, [L[i] for i in range(nl)]
+
+
+def _seq_lens(lens):
+    lens = [int(x) for x in lens] or [0]
+    return (C.c_uint32 * len(lens))(*lens), len(lens)
+
+
+def seq_encode(seq: bytes, lens, both: int, k: int) -> bytes:
+    """fqz5_seq_encode (encode_seq, fqzcomp5.c:1073) on the GPU."""
+    la, nr = _seq_lens(lens)
+    n = C.c_uint(0)
+    p = load().fqz5_seq_encode(bytes(seq), len(seq), la, nr, both, k, C.byref(n))
+    if not p:
+        raise NativeError("fqz5_seq_encode failed: " + last_error())
+    out = C.string_at(p, n.value)
+    _libc.free(p)
+    return out
+
+
+def seq_decode(comp: bytes, lens, both: int, k: int, out_size: int) -> bytes:
+    """fqz5_seq_decode (decode_seq, fqzcomp5.c:1272) on the GPU."""
+    la, nr = _seq_lens(lens)
+    p = load().fqz5_seq_decode(bytes(comp), len(comp), la, nr, both, k, out_size)
+    if not p:
+        raise NativeError("fqz5_seq_decode failed: " + last_error())
+    out = C.string_at(p, out_size)
+    _libc.free(p)
+    return out

@@ -122,6 +122,23 @@ char *fqz_compress(int vers, fqz_slice *s, char *in, size_t in_size,
 char *fqz_decompress(char *in, size_t in_size, size_t *out_size,
                      int *lengths, int nlengths, fqz_slice *s);
 
+/* ---- sequence context model (fqzcomp5.c:1073-1406) --------------------- */
+
+/* Replaces encode_seq (fqzcomp5.c:1073): the SEQ10 .. SEQ14B coder of a
+ * sequence section (ctx_size 10..14 in fqzcomp5; 1..14 here), len[] the
+ * record lengths whose starts reset the k-mer contexts.  Same bytes as the
+ * reference; NULL when the records run out before the data (as the
+ * reference) or on a device error.  malloc()ed result, caller frees. */
+char *fqz5_seq_encode(unsigned char *in, unsigned int in_size, unsigned int *len,
+                      int nrecords, int both_strands, int ctx_size,
+                      unsigned int *out_size);
+
+/* Replaces decode_seq (fqzcomp5.c:1272): out_size bytes from a stream of
+ * fqz5_seq_encode / encode_seq.  NULL on a damaged stream. */
+char *fqz5_seq_decode(unsigned char *in, unsigned int in_size, unsigned int *len,
+                      int nrecords, int both_strands, int ctx_size,
+                      unsigned int out_size);
+
 /* ---- arith_dynamic (arith_dynamic.h:41-54) ----------------------------- */
 
 /* Replaces arith_compress_bound (arith_dynamic.c:77). */
