@@ -22,6 +22,7 @@
 #include "../../include/fqz5_block.h"
 #include "rans_codec.hpp"
 #include "fqz_codec.hpp"
+#include "seq_codec.hpp"
 #include "rans_format.hpp"
 
 namespace fqz5 {
@@ -34,7 +35,8 @@ namespace {
 // fqzcomp5.c:185-208
 enum Method {
     RANS0 = 1, RANS1, RANS64, RANS65, RANS128, RANS129, RANS192, RANS193,
-    RANSXN1, LZP3, FQZ0 = 26, FQZ1, FQZ2, FQZ3, FQZ4, M_LAST = 31
+    RANSXN1, LZP3, SEQ10 = 20, SEQ12, SEQ12B, SEQ13B, SEQ14B, SEQ_CUSTOM,
+    FQZ0 = 26, FQZ1, FQZ2, FQZ3, FQZ4, M_LAST = 31
 };
 constexpr uint32_t RANS_MASK =
     (1u << RANS0) | (1u << RANS1) | (1u << RANS64) | (1u << RANS65) |
@@ -43,7 +45,29 @@ constexpr uint32_t RANS_MASK =
 constexpr uint32_t FQZ_MASK =
     (1u << FQZ0) | (1u << FQZ1) | (1u << FQZ2) | (1u << FQZ3) | (1u << FQZ4);
 
+constexpr uint32_t SEQ_MASK =
+    (1u << SEQ10) | (1u << SEQ12) | (1u << SEQ12B) | (1u << SEQ13B) | (1u << SEQ14B);
+
 bool is_fqz(int m) { return m >= FQZ0 && m <= FQZ4; }
+bool is_seqcm(int m) { return m >= SEQ10 && m <= SEQ14B; }
+
+// encode_seq's parameters per method and the section strat byte
+// (k << 4) | (both << 3) | 1 (fqzcomp5.c:2047-2062)
+SeqEncReq seq_req(const fqz5_section &S, int m) {
+    static const int slevel[] = {10, 12, 12, 13, 14}, both[] = {0, 0, 1, 1, 1};
+    SeqEncReq r;
+    r.d_in = S.in;
+    r.n = S.in_size;
+    r.lens = S.rec_len;
+    r.nrec = S.nrec;
+    r.k = slevel[m - SEQ10];
+    r.both = both[m - SEQ10];
+    return r;
+}
+int seq_strat(int m) {
+    static const int slevel[] = {10, 12, 12, 13, 14}, both[] = {0, 0, 1, 1, 1};
+    return (slevel[m - SEQ10] << 4) | (both[m - SEQ10] << 3) | 1;
+}
 
 // order word per rANS method (fqzcomp5.c:1992-2010)
 int method_order(int m, uint32_t fixed_len) {
@@ -90,6 +114,8 @@ struct TrySession {
     std::vector<FqzEncReq> fqz;                   // FQZ candidates
     std::vector<uint64_t> fqz_lb;                 // pruned candidates: size lower bound (else 0)
     std::vector<std::vector<int>> fqz_of;
+    std::vector<SeqEncReq> seq;                   // sequence CM candidates
+    std::vector<std::vector<int>> seq_of;
     std::deque<std::vector<uint32_t>> recs;       // their (rewritable) lengths / flags
     bool open = false;
 };
@@ -222,15 +248,18 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         }
         t_sess = TrySession();
         for (int i = 0; i < nsec; i++) {
-            if (masks[i] & ~(RANS_MASK | FQZ_MASK))
-                throw GpuError("fqz5_sections_try: method mask has LZP/tok3/seq-CM methods "
+            if (masks[i] & ~(RANS_MASK | FQZ_MASK | SEQ_MASK))
+                throw GpuError("fqz5_sections_try: method mask has LZP/tok3/SEQ_CUSTOM methods "
                                "(not in this build)");
+            if ((masks[i] & SEQ_MASK) && (secs[i].sec != FQZ5_SEC_SEQ || !secs[i].rec_len))
+                throw GpuError("fqz5_sections_try: SEQ methods need a sequence section with records");
             if ((masks[i] & FQZ_MASK) && (secs[i].sec != FQZ5_SEC_QUAL || !secs[i].rec_len))
                 throw GpuError("fqz5_sections_try: FQZ methods need a quality section with records");
         }
         std::vector<CompressReq> &reqs = t_sess.reqs;
         t_sess.req_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
         t_sess.fqz_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
+        t_sess.seq_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
         for (int i = 0; i < nsec; i++) {
             const fqz5_section &S = secs[i];
             for (int m = 1; m < FQZ5_M_LAST; m++) {
@@ -238,6 +267,11 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 if (is_fqz(m)) {
                     t_sess.fqz_of[i][m] = int(t_sess.fqz.size());
                     t_sess.fqz.push_back(fqz_req(S, m, t_sess.recs));
+                    continue;
+                }
+                if (is_seqcm(m)) {
+                    t_sess.seq_of[i][m] = int(t_sess.seq.size());
+                    t_sess.seq.push_back(seq_req(S, m));
                     continue;
                 }
                 if (m == RANSXN1 && !S.fixed_len) continue;   // out = NULL (:2004-2007)
@@ -286,14 +320,17 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             t_sess.fqz_lb.assign(t_sess.fqz.size(), 0);
             g_fqz_tried += t_sess.fqz.size();
         }
+        if (!t_sess.seq.empty()) seq_encode_batch(g, t_sess.seq);
         t_sess.open = true;
         // sizes as compress_with_methods sees them: UINT_MAX when not run,
         // 0 when the codec returned NULL (out_len = *out_size = 0)
         for (int i = 0; i < nsec; i++)
             for (int m = 0; m < FQZ5_M_LAST; m++) {
                 const int ri = t_sess.req_of[i][m], fi = t_sess.fqz_of[i][m];
+                const int si = t_sess.seq_of[i][m];
                 uint32_t sz = UINT32_MAX;
                 if (ri >= 0) sz = reqs[ri].ok ? layout_size(reqs[ri].out) : 0;
+                if (si >= 0) sz = t_sess.seq[size_t(si)].ok ? layout_size(t_sess.seq[size_t(si)].out) : 0;
                 if (fi >= 0) {
                     const uint64_t lb = t_sess.fqz_lb[size_t(fi)];   // pruned: its lower bound
                     sz = t_sess.fqz[size_t(fi)].ok ? layout_size(t_sess.fqz[size_t(fi)].out)
@@ -352,12 +389,19 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             throw GpuError("fqz5_sections_commit: no matching fqz5_sections_try");
         // sections outside the trial: their one method, encoded now
         std::vector<CompressReq> late;
-        std::vector<int> late_of(nsec, -1), late_fqz_of(nsec, -1);
+        std::vector<int> late_of(nsec, -1), late_fqz_of(nsec, -1), late_seq_of(nsec, -1);
         std::vector<FqzEncReq> late_fqz;
+        std::vector<SeqEncReq> late_seq;
         for (int i = 0; i < nsec; i++) {
             const int m = methods[i];
-            if (m <= 0 || m >= FQZ5_M_LAST || t_sess.req_of[i][m] >= 0 || t_sess.fqz_of[i][m] >= 0)
+            if (m <= 0 || m >= FQZ5_M_LAST || t_sess.req_of[i][m] >= 0 || t_sess.fqz_of[i][m] >= 0 ||
+                t_sess.seq_of[i][m] >= 0)
                 continue;
+            if (is_seqcm(m) && secs[i].sec == FQZ5_SEC_SEQ && secs[i].rec_len) {
+                late_seq_of[i] = int(late_seq.size());
+                late_seq.push_back(seq_req(secs[i], m));
+                continue;
+            }
             if (is_fqz(m) && secs[i].sec == FQZ5_SEC_QUAL && secs[i].rec_len) {
                 late_fqz_of[i] = int(late_fqz.size());
                 late_fqz.push_back(fqz_req(secs[i], m, t_sess.recs));
@@ -374,6 +418,7 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         }
         if (!late.empty()) compress_batch(g, late);
         if (!late_fqz.empty()) fqz_encode_batch(g, late_fqz);
+        if (!late_seq.empty()) seq_encode_batch(g, late_seq);
         std::vector<const Layout *> ls;
         std::vector<uint8_t *> dsts;
         std::vector<Layout> framed(nsec);
@@ -383,13 +428,16 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             const int m = methods[i];
             const int ri = (m > 0 && m < FQZ5_M_LAST) ? t_sess.req_of[i][m] : -1;
             const int fi = (m > 0 && m < FQZ5_M_LAST) ? t_sess.fqz_of[i][m] : -1;
+            const int si = (m > 0 && m < FQZ5_M_LAST) ? t_sess.seq_of[i][m] : -1;
             const Layout *lay = nullptr;
             if (ri >= 0 && t_sess.reqs[ri].ok) lay = &t_sess.reqs[ri].out;
             if (late_of[i] >= 0 && late[late_of[i]].ok) lay = &late[late_of[i]].out;
             if (fi >= 0 && t_sess.fqz[size_t(fi)].ok) lay = &t_sess.fqz[size_t(fi)].out;
             if (late_fqz_of[i] >= 0 && late_fqz[late_fqz_of[i]].ok) lay = &late_fqz[late_fqz_of[i]].out;
+            if (si >= 0 && t_sess.seq[size_t(si)].ok) lay = &t_sess.seq[size_t(si)].out;
+            if (late_seq_of[i] >= 0 && late_seq[late_seq_of[i]].ok) lay = &late_seq[late_seq_of[i]].out;
             R.method = m;
-            R.strat = is_fqz(m) ? 1 : 0;   // compress_with_methods' *strat
+            R.strat = is_fqz(m) ? 1 : is_seqcm(m) ? seq_strat(m) : 0;   // compress_with_methods' *strat
             R.status = -1;
             R.clen = 0;
             R.usize = S.in_size;
@@ -450,7 +498,8 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         g.sync();
         std::vector<DecompressReq> reqs;
         std::vector<FqzDecReq> fqz;
-        std::vector<int> who, who_fqz;
+        std::vector<SeqDecReq> seqd;
+        std::vector<int> who, who_fqz, who_seq;
         off = 0;
         for (int i = 0; i < nsec; i++) {
             const uint8_t *h = host.data() + off;
@@ -477,6 +526,20 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
                 who_fqz.push_back(i);
                 continue;
             }
+            if ((h[0] & 7) == 1 && secs[i].sec == FQZ5_SEC_SEQ) {   // decode_seq (:2421-2430)
+                SeqDecReq q;
+                q.d_in = secs[i].in + 9;
+                q.in_size = clen;
+                q.lens = secs[i].rec_len;
+                q.nrec = secs[i].nrec;
+                q.k = h[0] >> 4;
+                q.both = (h[0] >> 3) & 1;
+                q.d_out = secs[i].out;
+                q.n = ulen;
+                seqd.push_back(q);
+                who_seq.push_back(i);
+                continue;
+            }
             if (h[0] != 0) continue;
             DecompressReq r;
             r.h_in = h + 9;
@@ -488,13 +551,19 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             who.push_back(i);
         }
         decompress_batch(g, reqs);
-        // after the rANS sections: a quality section's sequence context may
+        if (!seqd.empty()) seq_decode_batch(g, seqd);
+        // after the rANS and sequence sections: a quality section's sequence context may
         // be the output of this call's sequence section
         if (!fqz.empty()) fqz_decode_batch(g, fqz);
         for (size_t k = 0; k < reqs.size(); k++) {
             fqz5_section_result &R = res[who[k]];
             R.status = reqs[k].ok ? 0 : -1;
             R.usize = reqs[k].out_size;
+        }
+        for (size_t k = 0; k < seqd.size(); k++) {
+            fqz5_section_result &R = res[who_seq[k]];
+            R.status = seqd[k].ok ? 0 : -1;
+            R.usize = seqd[k].n;
         }
         for (size_t k = 0; k < fqz.size(); k++) {
             fqz5_section_result &R = res[who_fqz[k]];

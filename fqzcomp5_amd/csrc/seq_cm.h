@@ -52,6 +52,7 @@ struct SeqDecJob {
     int32_t *status;                    // 0 ok, -1 damaged stream
 };
 hipError_t launch_seq_models_init(uint32_t *models, size_t nctx, hipStream_t s);
-hipError_t launch_seq_dec(const SeqDecJob &j, hipStream_t s);
+// one workgroup per job (device array)
+hipError_t launch_seq_dec(const SeqDecJob *d_jobs, int njobs, hipStream_t s);
 
 }  // namespace fqz5

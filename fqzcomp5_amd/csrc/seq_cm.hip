@@ -198,9 +198,10 @@ __global__ void k_seq_models_init(uint32_t *m, size_t n) {
         m[i] = 0x01010101u;
 }
 
-__global__ __launch_bounds__(64) void k_seq_dec(SeqDecJob J) {
+__global__ __launch_bounds__(64) void k_seq_dec(const SeqDecJob *Js) {
     __shared__ FList<256> run[3], lit;
     if (threadIdx.x != 0) return;
+    const SeqDecJob J = Js[blockIdx.x];   // one block per workgroup
     for (int c = 0; c < 3; c++) fl_init(&run[c], 256);
     fl_init(&lit, 256);
     uint32_t st[3] = {0x0101u, 0x0101u, 0x0101u};
@@ -337,8 +338,8 @@ hipError_t launch_seq_models_init(uint32_t *models, size_t nctx, hipStream_t s) 
     return hipGetLastError();
 }
 
-hipError_t launch_seq_dec(const SeqDecJob &j, hipStream_t s) {
-    hipLaunchKernelGGL(k_seq_dec, dim3(1), dim3(64), 0, s, j);
+hipError_t launch_seq_dec(const SeqDecJob *d_jobs, int njobs, hipStream_t s) {
+    if (njobs) hipLaunchKernelGGL(k_seq_dec, dim3(njobs), dim3(64), 0, s, d_jobs);
     return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 #include "fqz_codec.hpp"
 #include "fqz_kernels.h"
 #include "seq_cm.h"
+#include "seq_codec.hpp"
 
 namespace fqz5 {
 
@@ -48,7 +49,7 @@ bool seq_class_uc(uint8_t c) { return c == 'A' || c == 'C' || c == 'G' || c == '
 
 // One block: events, context and side models, then the range coder back end.
 // Returns the device output and its size.
-static uint8_t *seq_encode_dev(GpuCtx &g, const uint8_t *d_in, uint8_t first, uint32_t n,
+static uint8_t *seq_encode_dev(GpuCtx &g, const uint8_t *d_in, uint32_t n,
                                const std::vector<uint32_t> &seg, int both, int k,
                                uint32_t *out_len) {
     SeqJob J{};
@@ -57,7 +58,6 @@ static uint8_t *seq_encode_dev(GpuCtx &g, const uint8_t *d_in, uint8_t first, ui
     J.k = uint32_t(k);
     J.both = both ? 1u : 0u;
     J.mask = uint32_t((1ull << (2 * k)) - 1);
-    J.lead = (n && !seq_class_uc(first)) ? 2u : 0u;
     J.nseg = uint32_t(seg.size() - 1);
     J.seg = g.upload(seg);
     uint32_t nev = 0;
@@ -70,10 +70,13 @@ static uint8_t *seq_encode_dev(GpuCtx &g, const uint8_t *d_in, uint8_t first, ui
         void *tmp = g.arena.alloc_n<uint8_t>(tb);
         FQZ5_HIP(fqz_exclusive_scan(J.flag, J.ex, int(n), tmp, tb, g.stream));
         uint32_t last[2];
+        uint8_t first = 0;
         g.download(&last[0], J.ex + n - 1, 1);
         g.download(&last[1], J.flag + n - 1, 1);
+        g.download(&first, d_in, 1);
         g.sync();
         J.nrun = last[0] + last[1];
+        J.lead = seq_class_uc(first) ? 0u : 2u;
         J.run_start = g.arena.alloc_n<uint32_t>(J.nrun);
         J.cnt = g.arena.alloc_n<uint32_t>(J.nrun + 1);
         J.run_off = g.arena.alloc_n<uint32_t>(J.nrun + 1);
@@ -122,6 +125,56 @@ static uint8_t *seq_encode_dev(GpuCtx &g, const uint8_t *d_in, uint8_t first, ui
     return out;
 }
 
+void seq_encode_batch(GpuCtx &g, std::vector<SeqEncReq> &reqs) {
+    for (SeqEncReq &R : reqs) {
+        R.ok = false;
+        R.out.clear();
+        if (R.k < 1 || R.k > int(SEQ_K_MAX)) throw GpuError("seq: context size out of range (1..14)");
+        std::vector<uint32_t> seg;
+        if (!R.lens || !seq_segments(R.lens, R.nrec, R.n, seg)) continue;
+        uint32_t len = 0;
+        Piece p;
+        p.dev = seq_encode_dev(g, R.d_in, R.n, seg, R.both, R.k, &len);
+        p.len = len;
+        R.out.push_back(p);
+        R.ok = true;
+    }
+}
+
+void seq_decode_batch(GpuCtx &g, std::vector<SeqDecReq> &reqs) {
+    std::vector<SeqDecJob> js;
+    std::vector<size_t> who;
+    for (size_t i = 0; i < reqs.size(); i++) {
+        SeqDecReq &R = reqs[i];
+        R.ok = false;
+        if (R.k < 1 || R.k > int(SEQ_K_MAX)) continue;
+        std::vector<uint32_t> seg;
+        if (!R.lens || !seq_segments(R.lens, R.nrec, R.n, seg)) continue;
+        SeqDecJob J{};
+        J.in = R.d_in;
+        J.in_len = R.in_size;
+        J.n = R.n;
+        J.k = uint32_t(R.k);
+        J.both = R.both ? 1u : 0u;
+        J.mask = uint32_t((1ull << (2 * R.k)) - 1);
+        J.nseg = uint32_t(seg.size() - 1);
+        J.seg = g.upload(seg);
+        const size_t nctx = size_t(J.mask) + 1;
+        J.models = g.arena.alloc_n<uint32_t>(nctx);
+        FQZ5_HIP(launch_seq_models_init(J.models, nctx, g.stream));
+        J.out = R.d_out;
+        J.status = g.arena.alloc_n<int32_t>(1);
+        js.push_back(J);
+        who.push_back(i);
+    }
+    if (js.empty()) return;
+    FQZ5_HIP(launch_seq_dec(g.upload(js), int(js.size()), g.stream));
+    std::vector<int32_t> st(js.size(), -1);
+    for (size_t k = 0; k < js.size(); k++) g.download(&st[k], js[k].status, 1);
+    g.sync();
+    for (size_t k = 0; k < js.size(); k++) reqs[who[k]].ok = st[k] == 0;
+}
+
 }  // namespace fqz5
 
 using namespace fqz5;
@@ -142,8 +195,7 @@ char *fqz5_seq_encode(unsigned char *in, unsigned int in_size, unsigned int *len
         gp = &g;
         const uint8_t *d_in = g.upload(in, in_size);
         uint32_t n_out = 0;
-        uint8_t *d_out = seq_encode_dev(g, d_in, in_size ? in[0] : 0, in_size, seg, both_strands,
-                                        ctx_size, &n_out);
+        uint8_t *d_out = seq_encode_dev(g, d_in, in_size, seg, both_strands, ctx_size, &n_out);
         char *out = static_cast<char *>(std::malloc(n_out ? n_out : 1));
         if (!out) throw GpuError("fqz5_seq_encode: out of host memory");
         g.download(reinterpret_cast<uint8_t *>(out), d_out, n_out);
@@ -168,27 +220,21 @@ char *fqz5_seq_decode(unsigned char *in, unsigned int in_size, unsigned int *len
         if (!seq_segments(len, nrecords, out_size, seg)) return nullptr;
         GpuCtx &g = gpu();
         gp = &g;
-        SeqDecJob J{};
-        J.in = g.upload(in, in_size);
-        J.in_len = in_size;
-        J.n = out_size;
-        J.k = uint32_t(ctx_size);
-        J.both = both_strands ? 1u : 0u;
-        J.mask = uint32_t((1ull << (2 * ctx_size)) - 1);
-        J.nseg = uint32_t(seg.size() - 1);
-        J.seg = g.upload(seg);
-        const size_t nctx = size_t(J.mask) + 1;
-        J.models = g.arena.alloc_n<uint32_t>(nctx);
-        FQZ5_HIP(launch_seq_models_init(J.models, nctx, g.stream));
-        J.out = g.arena.alloc_n<uint8_t>(out_size ? out_size : 1);
-        J.status = g.arena.alloc_n<int32_t>(1);
-        FQZ5_HIP(launch_seq_dec(J, g.stream));
-        int32_t st = 0;
-        g.download(&st, J.status, 1);
+        std::vector<SeqDecReq> rq(1);
+        rq[0].d_in = g.upload(in, in_size);
+        rq[0].in_size = in_size;
+        rq[0].lens = len;
+        rq[0].nrec = nrecords;
+        rq[0].both = both_strands;
+        rq[0].k = ctx_size;
+        rq[0].n = out_size;
+        rq[0].d_out = g.arena.alloc_n<uint8_t>(out_size ? out_size : 1);
+        seq_decode_batch(g, rq);
         char *out = static_cast<char *>(std::malloc(out_size ? out_size : 1));
         if (!out) throw GpuError("fqz5_seq_decode: out of host memory");
-        g.download(reinterpret_cast<uint8_t *>(out), J.out, out_size);
+        g.download(reinterpret_cast<uint8_t *>(out), rq[0].d_out, out_size);
         g.reset();
+        const int32_t st = rq[0].ok ? 0 : -1;
         if (st != 0) {
             std::free(out);
             fqz5_set_error("fqz5_seq_decode: damaged stream");

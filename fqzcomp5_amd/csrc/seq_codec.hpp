@@ -1,0 +1,38 @@
+// seq_codec.hpp — the sequence context model (SEQ10 .. SEQ14B,
+// fqzcomp5.c:1073-1406) on device-resident blocks (seq_codec.cpp), for the
+// section coder (block.cpp) and fqz5_seq_encode / fqz5_seq_decode.
+#pragma once
+#include <vector>
+
+#include "gpu_ctx.hpp"
+#include "rans_codec.hpp"
+
+namespace fqz5 {
+
+struct SeqEncReq {
+    const uint8_t *d_in = nullptr;      // device bases
+    uint32_t n = 0;
+    const uint32_t *lens = nullptr;     // host record lengths
+    int nrec = 0;
+    int both = 0, k = 12;
+    // results
+    bool ok = false;                    // false: the records run out (encode_seq's NULL)
+    Layout out;                         // the coder bytes (device)
+};
+// one block after another (every phase is a parallel kernel)
+void seq_encode_batch(GpuCtx &g, std::vector<SeqEncReq> &reqs);
+
+struct SeqDecReq {
+    const uint8_t *d_in = nullptr;      // device stream
+    uint32_t in_size = 0;
+    const uint32_t *lens = nullptr;
+    int nrec = 0;
+    int both = 0, k = 12;
+    uint8_t *d_out = nullptr;           // device output of n bytes
+    uint32_t n = 0;
+    bool ok = false;
+};
+// every block's chain in one launch
+void seq_decode_batch(GpuCtx &g, std::vector<SeqDecReq> &reqs);
+
+}  // namespace fqz5

@@ -26,13 +26,20 @@ M_LAST = 31
 SEC_SEQ, SEC_QUAL = 2, 3
 RANS0, RANS1, RANS64, RANS65, RANS128, RANS129, RANS192, RANS193, RANSXN1 = range(1, 10)
 LZP3 = 10
+SEQ10, SEQ12, SEQ12B, SEQ13B, SEQ14B = range(20, 25)
 FQZ0, FQZ1, FQZ2, FQZ3, FQZ4 = range(26, 31)
 RANS_MASK = sum(1 << m for m in range(RANS0, RANSXN1 + 1))
 FQZ_MASK = sum(1 << m for m in range(FQZ0, FQZ4 + 1))
+SEQ_MASK = sum(1 << m for m in range(SEQ10, SEQ14B + 1))
+# candidates whose cost grows with their work: tried only where the trial
+# schedule names them (see encode_run)
+WORK_MASK = FQZ_MASK | SEQ_MASK
 
-# Method masks of the level presets (fqzcomp5.c:4886-4932) restricted to the
-# methods this build implements: rANS and fqzcomp_qual.  LZP3 and the
-# sequence context models (SEQ10/SEQ12B) are the next rows.
+# Method masks of the level presets (fqzcomp5.c:4886-4932) restricted to
+# rANS and fqzcomp_qual: the bench's workloads.  masks(level, seq_cm=True)
+# adds the sequence context models of the preset (SEQ10 / SEQ12B at -5),
+# which this build has (seq_cm.hip) but whose decoder is one serial chain
+# per block.  LZP3 is not in this build.
 LEVEL_MASKS = {
     1: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193],
         SEC_QUAL: [RANS0, RANS1, RANS129, RANS193]},
@@ -112,11 +119,17 @@ def _load():
     return so
 
 
-def masks(level: int) -> np.ndarray:
+SEQ_CM_MASKS = {5: [SEQ10, SEQ12B]}     # fqzcomp5.c:4905
+
+
+def masks(level: int, seq_cm: bool = False) -> np.ndarray:
     av = np.zeros(4, np.uint32)
     for sec, ms in LEVEL_MASKS[level].items():
         for m in ms:
             av[sec] |= np.uint32(1 << m)
+    if seq_cm:
+        for m in SEQ_CM_MASKS.get(level, []):
+            av[SEC_SEQ] |= np.uint32(1 << m)
     return av
 
 
@@ -244,7 +257,7 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
     ins = np.array([s.in_size for s in secs], np.uint32)
     ids = np.array([s.sec for s in secs], np.int32)
     av = np.asarray(avail, np.uint32)
-    if speculate and not (av & FQZ_MASK).any():
+    if speculate and not (av & WORK_MASK).any():
         masks = av[ids]
         prune = False
     else:
@@ -255,7 +268,7 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
         # rANS candidates stay speculative (chain-bound, nearly free in one
         # launch); fqz candidates cost in proportion to their work, so only
         # the scheduled trial sections try them
-        masks = (av[ids] & RANS_MASK) | (sched & FQZ_MASK) if speculate else sched
+        masks = (av[ids] & RANS_MASK) | (sched & WORK_MASK) if speculate else sched
         rows = np.nonzero(sched_all & FQZ_MASK)[0]
         prune = prune and speculate and len(rows) == TRIAL_WINDOW and \
             bool(((rows >= off) & (rows < off + len(secs))).all())

@@ -26,17 +26,18 @@ def _order(m, fl):
 
 # fqz beats rANS on the random-walk (Illumina) qualities from ~2 MB blocks
 # on; on i.i.d. NovaSeq qualities rANS O0 stays ahead at every size
-@pytest.mark.parametrize("level,kind,nreads,blk", [(3, "illumina", 6000, 200_000),
-                                                   (5, "novaseq", 6000, 200_000),
-                                                   (5, "illumina", 72000, 4_000_000)])
-def test_run_vs_reference(level, kind, nreads, blk):
+@pytest.mark.parametrize("level,kind,nreads,blk,cm", [(3, "illumina", 6000, 200_000, False),
+                                                      (5, "novaseq", 6000, 200_000, False),
+                                                      (5, "illumina", 72000, 4_000_000, False),
+                                                      (5, "novaseq", 6000, 200_000, True)])
+def test_run_vs_reference(level, kind, nreads, blk, cm):
     codec = binding.ref() if binding.have_ref() else binding.oracle()
     reads = (synth.novaseq if kind == "novaseq" else synth.illumina)(nreads, seed=11)
     blocks = synth.split_blocks(reads, blk)
     assert len(blocks) >= 5
     run = S.Run(reads, blocks, torch.device("cuda", 0))
     t0, p0 = S.trial_counts()
-    res, meth_all, sizes, tried, _ = S.encode_run(run.enc_secs(), S.masks(level), S.new_state())
+    res, meth_all, sizes, tried, _ = S.encode_run(run.enc_secs(), S.masks(level, cm), S.new_state())
     t1, p1 = S.trial_counts()
     assert all(r.status == 0 for r in res)
     offs = np.concatenate([[0], np.cumsum(reads.lens.astype(np.int64))])
@@ -50,6 +51,12 @@ def test_run_vs_reference(level, kind, nreads, blk):
             exp = codec.fqz_compress(data, reads.lens[a:b].copy(), np.zeros(b - a, np.uint32),
                                      m - S.FQZ0, reads.seq[s:e].tobytes())
             assert r.strat == 1
+        elif S.SEQ10 <= m <= S.SEQ14B:
+            a, b = blocks[k]
+            k_, both = {S.SEQ10: (10, 0), S.SEQ12B: (12, 1)}[m]
+            sc = binding.seq_ref() if binding.have_seq_ref() else binding.seq_oracle()
+            exp = sc.encode(data, [int(x) for x in reads.lens[a:b]], both, k_)
+            assert r.strat == (k_ << 4) | (both << 3) | 1
         else:
             exp = codec.rans_compress(data, _order(m, fl))
             assert r.strat == 0
@@ -66,13 +73,17 @@ def test_run_vs_reference(level, kind, nreads, blk):
                                               np.zeros(b - a, np.uint32), m - S.FQZ0,
                                               reads.seq[s:e].tobytes()))
                 assert int(sizes[i, m]) <= true, (i, m, int(sizes[i, m]), true)
-        if kind == "novaseq":                       # rANS wins by a margin: fqz pruned
+        if kind == "novaseq" and not cm:            # rANS wins by a margin: fqz pruned
             assert p1 - p0 > 0 and t1 - t0 >= p1 - p0
         fqz_bits = (1 << S.FQZ1) | (1 << S.FQZ3)
         assert all(int(t) & fqz_bits for t, (sec, *_) in zip(tried[:6], run.spans)
                    if sec == S.SEC_QUAL)            # the trial blocks tried fqz
         if kind == "illumina":                      # random-walk qualities: fqz wins
             assert used & {S.FQZ1, S.FQZ3}, used
+    if cm:                                          # trial blocks tried the CM
+        cm_bits = (1 << S.SEQ10) | (1 << S.SEQ12B)
+        assert all(int(t) & cm_bits for t, (sec, *_) in zip(tried[:6], run.spans)
+                   if sec == S.SEC_SEQ)
     dres = S.decode(run.dec_secs(res))
     assert all(r.status == 0 for r in dres)
     torch.cuda.synchronize()
