@@ -86,14 +86,6 @@ DEV uint32_t U(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 #endif
 DEV uint32_t RL(uint32_t v, uint32_t lane) { return __builtin_amdgcn_readlane(v, lane); }
 
-// RN(1/t) to within one ulp: hardware reciprocal plus one Newton step.
-DEV double recip(uint32_t t) {
-    const double d = double(t);
-    const double r = __builtin_amdgcn_rcp(d);
-    const double e = __fma_rn(-d, r, 1.0);
-    return __fma_rn(r, e, r);
-}
-DEV uint32_t quot(uint32_t rng, double rd) { return uint32_t(__fma_rn(double(rng), rd, 0x1p-19)); }
 
 // ---------------------------------------------------------------------------
 // input: a 4 KB LDS ring refilled 2 KB at a time, read through a 64-bit

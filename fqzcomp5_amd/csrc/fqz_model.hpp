@@ -76,6 +76,19 @@ template <int CAP> DEV void fl_bump(FList<CAP> *m, int k) {
     }
 }
 
+// floor(range / t) without a division (decoders): RN(1/t) to within one
+// ulp from the hardware reciprocal plus one Newton step, then
+// q = (u32)fma(range, RN(1/t), 2^-19), exact for range < 2^32 and t < 2^16
+// (fqz_div_selftest checks every t).
+// RN(1/t) to within one ulp: hardware reciprocal plus one Newton step.
+DEV double recip(uint32_t t) {
+    const double d = double(t);
+    const double r = __builtin_amdgcn_rcp(d);
+    const double e = __fma_rn(-d, r, 1.0);
+    return __fma_rn(r, e, r);
+}
+DEV uint32_t quot(uint32_t rng, double rd) { return uint32_t(__fma_rn(double(rng), rd, 0x1p-19)); }
+
 DEV uint32_t base2(uint8_t b) {
     switch (b) {
     case 'C': case 'c': return 1;

@@ -207,11 +207,43 @@ __global__ __launch_bounds__(64) void k_seq_dec(const SeqDecJob *Js) {
     uint32_t st[3] = {0x0101u, 0x0101u, 0x0101u};
     const uint8_t *in = J.in;
     const uint32_t len = J.in_len, n = J.n, mask = J.mask, top = 2u * J.k - 2u;
+    // input bytes through two 16-byte registers, the next one loaded a
+    // register ahead (buffer loads: zero past the end)
+    const uint32_t ia = uint32_t(reinterpret_cast<uintptr_t>(in) & 15u);
+    const auto rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(in - ia), 0,
+                                                       int(len + ia), 0x00020000);
+    const uint32_t iend = len + ia;
+    auto ld16 = [&](uint32_t off) {
+        if (off + 16u <= iend) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
+            return make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        // the chunk with the end in it: byte loads (a load that straddles
+        // the end of the range reads as zero)
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint32_t i = 0; i < 16u; i++)
+            w[i >> 2] |= uint32_t(__builtin_amdgcn_raw_buffer_load_b8(rin, off + i, 0, 0)) << (8u * (i & 3u));
+        return make_uint4(w[0], w[1], w[2], w[3]);
+    };
+    uint32_t cb = 0;                                    // cur = buffer bytes [cb, cb + 16)
+    uint4 cur = ld16(0), nxt = ld16(16);
+    uint32_t ip = 0;
+    auto next_byte = [&]() -> uint32_t {
+        const uint32_t o = ip++ + ia;
+        if (o - cb >= 16u) {                            // bytes are read in order
+            cb += 16u;
+            cur = nxt;
+            nxt = ld16(cb + 16u);
+        }
+        const uint32_t r = o - cb;
+        const uint32_t w = r < 8u ? (r < 4u ? cur.x : cur.y) : (r < 12u ? cur.z : cur.w);
+        return (w >> (8u * (r & 3u))) & 255u;
+    };
     // range decoder (c_range_coder.h); input past the end stops the chain
-    uint32_t code = 0, rng = 0xFFFFFFFFu, ip = 0;
+    uint32_t code = 0, rng = 0xFFFFFFFFu;
     bool bad = false;
     if (len >= 5) {
-        for (int i = 0; i < 5; i++) code = (code << 8) | in[ip++];
+        for (int i = 0; i < 5; i++) code = (code << 8) | next_byte();
     } else {
         bad = n > 0;
     }
@@ -220,15 +252,28 @@ __global__ __launch_bounds__(64) void k_seq_dec(const SeqDecJob *Js) {
         rng /= tot;
         return code / rng;
     };
+    // the next input bytes, MSB first: bb holds bn bits (whole bytes)
+    uint64_t bb = 0;
+    uint32_t bn = 0;
+    auto fill = [&]() {
+        while (bn <= 56u) {
+            bb |= uint64_t(next_byte()) << (56u - bn);
+            bn += 8u;
+        }
+    };
+    auto used = [&]() { return ip - (bn >> 3); };       // bytes the coder has taken
     auto take = [&](uint32_t cum, uint32_t f) {
         code -= cum * rng;
         rng *= f;
         while (rng < (1u << 24)) {
-            if (ip >= len) {
+            if (used() >= len) {
                 bad = true;
                 return;
             }
-            code = (code << 8) | in[ip++];
+            if (!bn) fill();
+            code = (code << 8) | uint32_t(bb >> 56);
+            bb <<= 8;
+            bn -= 8u;
             rng <<= 8;
         }
     };
@@ -260,6 +305,13 @@ __global__ __launch_bounds__(64) void k_seq_dec(const SeqDecJob *Js) {
 
     uint32_t fw = seed_fw(mask), rv = seed_rv(J.k, mask);
     uint32_t si = 0, state = 0, p = 0, idle = 0;
+    uint32_t F = 0;          // counts of context fw, when have
+    bool have = false;
+    // the next record start, kept in a register (a reload per symbol would
+    // wait for memory: the output stores may alias seg as far as the
+    // compiler knows)
+    uint32_t next_seg = J.nseg > 1 ? J.seg[1] : 0xFFFFFFFFu;
+    uint32_t *M = J.models;
     while (p < n && !bad) {
         uint32_t runlen = 0, d;
         do {
@@ -273,34 +325,71 @@ __global__ __launch_bounds__(64) void k_seq_dec(const SeqDecJob *Js) {
             break;
         }
         const uint32_t end = p + runlen;
+        have = false;
         for (; p < end && !bad; p++) {
-            if (si + 1 < J.nseg && p == J.seg[si + 1]) {   // a record starts
+            if (p == next_seg) {                           // a record starts
                 si++;
+                next_seg = si + 1 < J.nseg ? J.seg[si + 1] : 0xFFFFFFFFu;
                 fw = seed_fw(mask);
                 rv = seed_rv(J.k, mask);
+                have = false;
             }
             if (state == 2u) {
                 J.out[p] = uint8_t(get_fl(&lit));
                 continue;
             }
-            const uint32_t F = J.models[fw], tot = sm4_total(F);
-            const uint32_t t = target(tot);
+            // The counts of the 4 contexts that can follow fw (16 aligned
+            // bytes) and, both strands, of the 4 reverse contexts the base
+            // can lead to are loaded before this step's arithmetic; this
+            // step's own stores are patched in below.
+            if (bn < 8u) fill();                           // one byte is all a step takes
+            if (!have) F = M[fw];
+            // (u32 loads, the type of the stores, so that the compiler keeps
+            // them behind the previous step's stores)
+            const uint32_t *wp = M + ((fw << 2) & mask);
+            const uint4 win = make_uint4(wp[0], wp[1], wp[2], wp[3]);
+            uint32_t rc4[4] = {0, 0, 0, 0};
+            if (J.both)
+                for (uint32_t j = 0; j < 4; j++) rc4[j] = M[(rv >> 2) + (j << top)];
+            const uint32_t tot = sm4_total(F);
+            // symbol: the number of cumulative counts c with c * q <= code
+            // (q = range / total; c * q <= range, no overflow)
+            const uint32_t q = quot(rng, recip(tot));
             const uint32_t c0 = F & 255u, c1 = c0 + ((F >> 8) & 255u), c2 = c1 + ((F >> 16) & 255u);
-            const uint32_t b = uint32_t(t >= c0) + uint32_t(t >= c1) + uint32_t(t >= c2);
-            take(sm4_cum(F, b), (F >> (8u * b)) & 255u);
-            J.models[fw] = sm4_bump(F, b, tot);
-            J.out[p] = uint8_t((state ? "acgt" : "ACGT")[b]);
-            fw = ((fw << 2) + b) & mask;
+            const uint32_t b = uint32_t(c0 * q <= code) + uint32_t(c1 * q <= code) +
+                               uint32_t(c2 * q <= code);
+            // q >= 2^24 / 255, so q * freq >= 2^16: at most one byte in
+            code -= sm4_cum(F, b) * q;
+            rng = q * ((F >> (8u * b)) & 255u);
+            const bool sh = rng < (1u << 24);
+            code = sh ? (code << 8) | uint32_t(bb >> 56) : code;
+            rng = sh ? rng << 8 : rng;
+            bb = sh ? bb << 8 : bb;
+            bn -= sh ? 8u : 0u;
+            const uint32_t Fu = sm4_bump(F, b, tot);
+            M[fw] = Fu;
+            J.out[p] = uint8_t(((0x54474341u >> (8u * b)) & 255u) | (state << 5));   // ACGT / acgt
+            const uint32_t fn = ((fw << 2) + b) & mask;
+            uint32_t Fn = b == 0 ? win.x : b == 1 ? win.y : b == 2 ? win.z : win.w;
+            if (fn == fw) Fn = Fu;
             if (J.both) {
                 const uint32_t b2 = rv & 3u;
-                rv = (rv >> 2) + ((3u - b) << top);
-                const uint32_t G = J.models[rv];
-                J.models[rv] = sm4_bump(G, b2, sm4_total(G));
+                const uint32_t j = 3u - b;
+                rv = (rv >> 2) + (j << top);
+                uint32_t G = j == 0 ? rc4[0] : j == 1 ? rc4[1] : j == 2 ? rc4[2] : rc4[3];
+                if (rv == fw) G = Fu;
+                const uint32_t Gu = sm4_bump(G, b2, sm4_total(G));
+                M[rv] = Gu;
+                if (fn == rv) Fn = Gu;
             }
+            fw = fn;
+            F = Fn;
+            have = true;
         }
         if (p >= n || bad) break;
         state = switch_to(state, get_st(state));
     }
+    if (used() > len) bad = true;                      // took bytes past the end
     *J.status = bad ? -1 : 0;
 }
 
