@@ -98,6 +98,10 @@ def load() -> C.CDLL:
                                         C.POINTER(C.c_uint)]
     lib.arith_uncompress.restype = C.c_void_p
     lib.arith_uncompress.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint)]
+    lib.fqz5_crc32.restype = C.c_ulong
+    lib.fqz5_crc32.argtypes = [C.c_ulong, C.c_char_p, C.c_uint]
+    lib.fqz5_crc32_dev.restype = C.c_int
+    lib.fqz5_crc32_dev.argtypes = [C.c_uint32, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32)]
     lib.fqz5_seq_encode.restype = C.c_void_p
     lib.fqz5_seq_encode.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint32), C.c_int,
                                     C.c_int, C.c_int, C.POINTER(C.c_uint)]
@@ -311,3 +315,16 @@ def seq_decode(comp: bytes, lens, both: int, k: int, out_size: int) -> bytes:
     out = C.string_at(p, out_size)
     _libc.free(p)
     return out
+
+
+def crc32(data: bytes, crc: int = 0) -> int:
+    """zlib.crc32 computed on the GPU (fqz5_crc32, host buffer)."""
+    return int(load().fqz5_crc32(crc, bytes(data), len(data)))
+
+
+def crc32_dev(ptr: int, n: int, crc: int = 0) -> int:
+    """crc32 of n device bytes at ptr (fqz5_crc32_dev)."""
+    out = C.c_uint32(0)
+    if load().fqz5_crc32_dev(crc, C.c_void_p(ptr), n, C.byref(out)):
+        raise NativeError("fqz5_crc32_dev failed: " + last_error())
+    return int(out.value)

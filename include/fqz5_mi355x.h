@@ -139,6 +139,17 @@ char *fqz5_seq_decode(unsigned char *in, unsigned int in_size, unsigned int *len
                       int nrecords, int both_strands, int ctx_size,
                       unsigned int out_size);
 
+/* ---- CRC32 (zlib crc32, fqzcomp5.c:2268-2269, :2310-2311, :4443, :4670) --- */
+
+/* zlib's crc32(crc, buf, len) computed on the GPU (same value; buf == NULL
+ * returns 0, zlib's initial value).  On a device error it returns 0 with
+ * fqz5_last_error() set. */
+unsigned long fqz5_crc32(unsigned long crc, const unsigned char *buf, unsigned int len);
+
+/* The same over device memory of any length: *out = crc32(crc, d_buf, len).
+ * Returns 0, or -1 on a device error. */
+int fqz5_crc32_dev(uint32_t crc, const uint8_t *d_buf, uint64_t len, uint32_t *out);
+
 /* ---- arith_dynamic (arith_dynamic.h:41-54) ----------------------------- */
 
 /* Replaces arith_compress_bound (arith_dynamic.c:77). */
