@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 CPU = os.path.join(os.path.dirname(binding.REF_BIN), "fqzcomp5")
 GPU = os.path.join(os.path.dirname(binding.REF_BIN), "fqzcomp5_gpu")
+GPU_CRC = os.path.join(os.path.dirname(binding.REF_BIN), "fqzcomp5_gpu_crc")
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -66,3 +67,21 @@ def test_cli_threads(tmp_path):
     ref = open(src, "rb").read()
     assert open(ra, "rb").read() == ref
     assert open(rb, "rb").read() == ref
+
+
+def test_cli_crc_on_gpu(tmp_path):
+    """The CLI with its zlib crc32 calls mapped to fqz5_crc32 (block CRCs at
+    encode, their check at decode and --check) writes the same bytes."""
+    if not os.path.exists(GPU_CRC):
+        pytest.fail("oracle/_ref/fqzcomp5_gpu_crc not built (make -C oracle)")
+    for src in _inputs(str(tmp_path)):
+        a, b = str(tmp_path / "cpu.fqz5"), str(tmp_path / "gpu.fqz5")
+        back = str(tmp_path / "back.fastq")
+        subprocess.run([CPU, "-3", "-t1", src, a], check=True, capture_output=True)
+        subprocess.run([GPU_CRC, "-3", "-t1", src, b], check=True, capture_output=True,
+                       timeout=300)
+        assert open(a, "rb").read() == open(b, "rb").read(), src
+        subprocess.run([GPU_CRC, "--check", b], check=True, capture_output=True, timeout=300)
+        subprocess.run([GPU_CRC, "-d", "-t1", b, back], check=True, capture_output=True,
+                       timeout=300)
+        assert open(back, "rb").read() == open(src, "rb").read(), src
