@@ -11,6 +11,8 @@
 // trial state machine is replayed on the host in block order, which gives
 // exactly the choices of a single-threaded (-t1) reference run.
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -238,8 +240,18 @@ void fqz5_trial_schedule(const int32_t *sec_ids, int nsec, const uint32_t *avail
     }
 }
 
+static bool step_trace() {
+    static const bool on = std::getenv("FQZ5_STEP_TRACE") != nullptr;
+    return on;
+}
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                       uint32_t *sizes) {
+    const double t0 = step_trace() ? now_ms() : 0;
     try {
         GpuCtx &g = gpu();
         if (t_sess.open) {
@@ -300,13 +312,19 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                     err = std::current_exception();
                 }
             });
+            double tc = 0;
+            if (step_trace()) std::fprintf(stderr, "sections_try: before compress %.1f ms\n", now_ms() - t0);
             try {
                 compress_batch(g, reqs);
+                tc = step_trace() ? now_ms() : 0;
             } catch (...) {
                 th.join();
                 throw;
             }
             th.join();
+            if (step_trace())
+                std::fprintf(stderr, "sections_try: setup %.1f ms, rANS candidates %.1f ms, fqz prepare "
+                             "waited %.1f ms more\n", 0.0, tc - t0, now_ms() - tc);
             if (err) std::rethrow_exception(err);
             std::vector<char> skip(fq.size(), 0);
             if (g_prune.load()) skip = prune_plan(reqs, fq);
@@ -322,6 +340,7 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         }
         if (!t_sess.seq.empty()) seq_encode_batch(g, t_sess.seq);
         t_sess.open = true;
+        if (step_trace()) std::fprintf(stderr, "sections_try: %.1f ms\n", now_ms() - t0);
         // sizes as compress_with_methods sees them: UINT_MAX when not run,
         // 0 when the codec returned NULL (out_len = *out_size = 0)
         for (int i = 0; i < nsec; i++)
@@ -383,6 +402,7 @@ void fqz5_trial_replay(const int32_t *sec_ids, const uint32_t *in_sizes,
 
 int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *methods,
                          fqz5_section_result *res) {
+    const double t0 = step_trace() ? now_ms() : 0;
     try {
         GpuCtx &g = gpu();
         if (!t_sess.open || int(t_sess.req_of.size()) != nsec)
@@ -457,9 +477,13 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             dsts.push_back(S.out);
             R.status = 0;
         }
+        const double t1 = step_trace() ? now_ms() : 0;
         write_layouts_dev(g, ls, dsts);
         g.reset();
         t_sess = TrySession();
+        if (step_trace())
+            std::fprintf(stderr, "sections_commit: late encodes %.1f ms, write + sync %.1f ms\n",
+                         t1 - t0, now_ms() - t1);
         return 0;
     } catch (const std::exception &e) {
         fqz5_set_error(e.what());
@@ -486,13 +510,17 @@ int fqz5_encode_sections(const fqz5_section *secs, int nsec, const uint32_t *ava
 int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result *res) {
     try {
         GpuCtx &g = gpu();
+        static const bool trace = std::getenv("FQZ5_STEP_TRACE") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
         // section headers to the host, then the rANS payloads
         size_t tot = 0;
         for (int i = 0; i < nsec; i++) tot += secs[i].in_size;
-        std::vector<uint8_t> host(tot + 1);
+        // into the pinned staging arena (kept until g.reset() below): a
+        // pageable copy of a -5 run's 600 MB took 125 ms, this one ~5x less
+        uint8_t *host = g.staging.alloc(tot + 1);
         size_t off = 0;
         for (int i = 0; i < nsec; i++) {
-            g.download(host.data() + off, secs[i].in, secs[i].in_size);
+            g.download(host + off, secs[i].in, secs[i].in_size);
             off += secs[i].in_size;
         }
         g.sync();
@@ -502,7 +530,7 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         std::vector<int> who, who_fqz, who_seq;
         off = 0;
         for (int i = 0; i < nsec; i++) {
-            const uint8_t *h = host.data() + off;
+            const uint8_t *h = host + off;
             off += secs[i].in_size;
             res[i].status = -1;
             if (secs[i].in_size < 9) continue;
@@ -550,7 +578,12 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             reqs.push_back(r);
             who.push_back(i);
         }
+        const auto t1 = std::chrono::steady_clock::now();
         decompress_batch(g, reqs);
+        if (trace)
+            std::fprintf(stderr, "decode_sections: %zu bytes to host in %.1f ms, rANS %.1f ms\n", tot,
+                         std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
         if (!seqd.empty()) seq_decode_batch(g, seqd);
         // after the rANS and sequence sections: a quality section's sequence context may
         // be the output of this call's sequence section

@@ -17,10 +17,14 @@
 // capacity failures (NULL returns) are decided in stage 6 from sizes: they
 // never change the bytes of a successful call.
 #include <algorithm>
+#include <chrono>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <atomic>
 #include <exception>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -118,6 +122,7 @@ class Compressor {
   public:
     explicit Compressor(GpuCtx &g) : g_(g) {}
     void run(std::vector<CompressReq> &reqs);
+    size_t njobs() const { return jobs_.size(); }
 
   private:
     GpuCtx &g_;
@@ -722,6 +727,8 @@ bool Compressor::stripe_layout(const StripeReq &S, const CompressReq &r, Layout 
 
 // ---------------------------------------------------------------------------
 void Compressor::run(std::vector<CompressReq> &reqs) {
+    const double t_enter = std::chrono::duration<double, std::milli>(
+                               std::chrono::steady_clock::now().time_since_epoch()).count();
     std::vector<int> req_leaf(reqs.size(), -1), req_stripe(reqs.size(), -1);
     std::vector<StripeItem> sitems;
     uint32_t max_n = 0;
@@ -762,8 +769,17 @@ void Compressor::run(std::vector<CompressReq> &reqs) {
     }
     if (!sitems.empty())
         FQZ5_HIP(launch_stripe(g_.upload(sitems), int(sitems.size()), max_n, g_.stream));
+    static const bool trace = std::getenv("FQZ5_STEP_TRACE") != nullptr;
+    auto now = [] {
+        return std::chrono::duration<double, std::milli>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    const double t0 = trace ? now() : 0;
+    if (trace) std::fprintf(stderr, "compress: leaves %.1f ms\n", t0 - t_enter);
     stage_pack();
+    const double t1 = trace ? now() : 0;
     stage_rle();
+    const double t2 = trace ? now() : 0;
     for (auto &L : leaves_) {
         uint32_t n = L.n_cur;
         if (L.rle) {
@@ -782,8 +798,25 @@ void Compressor::run(std::vector<CompressReq> &reqs) {
             std::memcpy(jobs_[L.ej_main].F0, L.pack ? L.phist : L.hist, 1024);
         }
     }
+    const double t3 = trace ? now() : 0;
     stage_tables();
+    const double t4 = trace ? now() : 0;
     stage_encode();
+    const double t5 = trace ? now() : 0;
+    if (trace)
+        std::fprintf(stderr, "compress: pack %.1f ms, rle %.1f ms, jobs %.1f ms, tables %.1f ms, "
+                     "encode %.1f ms (%zu requests, %zu jobs)\n", t1 - t0, t2 - t1, t3 - t2,
+                     t4 - t3, t5 - t4, reqs.size(), jobs_.size());
+    struct Done {
+        bool on;
+        double t;
+        ~Done() {
+            if (on)
+                std::fprintf(stderr, "compress: layouts %.1f ms\n",
+                             std::chrono::duration<double, std::milli>(
+                                 std::chrono::steady_clock::now().time_since_epoch()).count() - t);
+        }
+    } done_{trace, t5};
     for (size_t i = 0; i < reqs.size(); i++) {
         CompressReq &r = reqs[i];
         if (r.n > uint32_t(INT_MAX)) continue;
@@ -811,8 +844,20 @@ void Compressor::run(std::vector<CompressReq> &reqs) {
 }  // namespace
 
 void compress_batch(GpuCtx &g, std::vector<CompressReq> &reqs) {
-    Compressor c(g);
-    c.run(reqs);
+    static const bool trace = std::getenv("FQZ5_STEP_TRACE") != nullptr;
+    auto now = [] {
+        return std::chrono::duration<double, std::milli>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    std::unique_ptr<Compressor> c(new Compressor(g));
+    c->run(reqs);
+    const double t0 = trace ? now() : 0;
+    // A batch of thousands of jobs frees ~100 MB of host tables and
+    // layouts (130 ms at -5, mostly munmap); the results no longer refer to
+    // them, so a detached thread frees them off the caller's critical path.
+    if (c->njobs() > 1000) std::thread([p = c.release()] { delete p; }).detach();
+    else c.reset();
+    if (trace) std::fprintf(stderr, "compress: teardown %.1f ms\n", now() - t0);
 }
 
 // ---------------------------------------------------------------------------

@@ -6,6 +6,9 @@
 //   A  O0 chains of compressed order-1 tables   (only when present)
 //   B  all O0 / O1 chains (main data and RLE meta-data)
 //   C  RLE expansion, D  un-packing, E  stripe interleave.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <climits>
 #include <cstring>
@@ -391,13 +394,25 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
         if (st[k]) djs_[used[k]].ok = false;
 }
 
+// $FQZ5_STEP_TRACE: host wall time of the decode phases on stderr
+static bool step_trace() {
+    static const bool on = std::getenv("FQZ5_STEP_TRACE") != nullptr;
+    return on;
+}
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 void Decompressor::run(std::vector<DecompressReq> &reqs) {
+    const double t0 = step_trace() ? now_ms() : 0;
     std::vector<int> roots;
     for (auto &r : reqs) {
         r.ok = false;
         r.out_size = 0;
         roots.push_back(parse(r.h_in, r.d_in, r.in_size, r.d_out, r.out_cap, 0));
     }
+    const double t1 = step_trace() ? now_ms() : 0;
     // A: compressed order-1 tables
     std::vector<int> hdr;
     for (size_t i = 0; i < djs_.size(); i++)
@@ -425,7 +440,9 @@ void Decompressor::run(std::vector<DecompressReq> &reqs) {
     for (int h : hdr) is_hdr[h] = 1;
     for (size_t i = 0; i < djs_.size(); i++)
         if (!is_hdr[i]) rest.push_back(int(i));
+    const double t2 = step_trace() ? now_ms() : 0;
     run_djs(rest);
+    const double t3 = step_trace() ? now_ms() : 0;
 
     // CAT payloads
     std::vector<CopyItem> cps;
@@ -604,6 +621,10 @@ void Decompressor::run(std::vector<DecompressReq> &reqs) {
     }
     if (!si.empty()) FQZ5_HIP(launch_stripe(g_.upload(si), int(si.size()), max_n, g_.stream));
     g_.sync();
+    if (step_trace())
+        std::fprintf(stderr, "decode: parse %.1f ms, o1 headers %.1f ms, chains %.1f ms, "
+                     "post %.1f ms (%zu streams, %zu chains)\n", t1 - t0, t2 - t1, t3 - t2,
+                     now_ms() - t3, reqs.size(), djs_.size());
     for (size_t i = 0; i < reqs.size(); i++) {
         Node &N = nodes_[roots[i]];
         reqs[i].ok = N.ok;

@@ -1,5 +1,6 @@
-"""Host-side phases of one bench step (-3 workload): where the wall time
-between GPU launches goes."""
+"""Host-side phases of one bench step: where the wall time between GPU
+launches goes.  Usage: step_timing.py [3|5]  (-3: 1 GB Illumina, -5: 4 GB
+NovaSeq, the bench's workloads)."""
 import os
 import sys
 import time
@@ -11,14 +12,16 @@ torch.cuda.init()
 import bench  # noqa: E402
 from fqzcomp5_amd import sections as S  # noqa: E402
 
-reads, blocks = bench.make_blocks(1.0, seed=1, kind="illumina")
+level = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+reads, blocks = (bench.make_blocks(1.0, seed=1, kind="illumina") if level == 3 else
+                 bench.make_blocks(4.0, seed=2, kind="novaseq"))
 run = S.Run(reads, blocks, torch.device("cuda", 0))
 enc = run.enc_secs()
 for rep in range(3):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     st = S.new_state()
-    res, meth, sizes, tried, off = S.encode_run(enc, S.masks(3), st)
+    res, meth, sizes, tried, off = S.encode_run(enc, S.masks(level), st)
     t1 = time.perf_counter()
     ds = run.dec_secs(res)
     t2 = time.perf_counter()
