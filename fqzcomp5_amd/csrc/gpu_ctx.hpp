@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -229,6 +230,34 @@ inline size_t hedge_copies(size_t jobs, size_t cus) {
     if (!hedge_chains() || !jobs) return 1;
     const size_t c = cus / jobs;
     return c < 1 ? 1 : (c > 4 ? 4 : c);
+}
+// Copies per chain of a launch, from the chains' step counts: one each,
+// then the CUs left over, one copy at a time in turn, to the chains of at
+// least half the longest length (they set the launch time; a shorter
+// chain finishes in time on any CU), up to 8 copies each.  The slowest CUs
+// run a chain ~40 % slower than the fastest, so the
+// long chains gain the most from more draws.  All ones when hedging is off.
+inline std::vector<int> hedge_plan(const std::vector<uint64_t> &steps, size_t cus) {
+    std::vector<int> c(steps.size(), 1);
+    static const size_t cap_waves = [] {   // experiments: $FQZ5_HEDGE_WAVES caps the launch
+        const char *e = std::getenv("FQZ5_HEDGE_WAVES");
+        return e ? size_t(std::strtoul(e, nullptr, 10)) : size_t(0);
+    }();
+    if (cap_waves && cap_waves < cus) cus = cap_waves;
+    if (!hedge_chains() || steps.empty() || steps.size() >= cus) return c;
+    uint64_t mx = 0;
+    for (uint64_t s : steps) mx = s > mx ? s : mx;
+    std::vector<size_t> longs;
+    for (size_t i = 0; i < steps.size(); i++)
+        if (2 * steps[i] >= mx) longs.push_back(i);
+    size_t spare = cus - steps.size();
+    for (int round = 1; round < 8 && spare; round++)
+        for (size_t i : longs) {
+            if (!spare) break;
+            c[i]++;
+            spare--;
+        }
+    return c;
 }
 
 // The calling thread's context (created on first use).

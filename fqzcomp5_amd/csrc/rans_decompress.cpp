@@ -369,15 +369,18 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
         lds = std::max(lds, dec_lds_bytes(rows, j.bits, int(mode)));
     }
     EventPair ev(g_.prof.on && !ord.empty(), g_.stream);
-    // hedge: every stream 2-4 times while the copies fit one per CU (the same
-    // chain runs up to ~20 % slower on some CUs)
-    const size_t copies = hedge_copies(djs.size(), size_t(g_.cus));
-    if (copies > 1) {
-        uint32_t *d_done = g_.arena.alloc_n<uint32_t>(djs.size());
-        g_.memset0(d_done, djs.size() * 4);
+    // hedge: the long streams several times on different CUs, while the
+    // copies fit one per CU (hedge_plan)
+    std::vector<uint64_t> steps;
+    for (const DecJob &d : djs) steps.push_back(uint64_t(d.n) / uint32_t(d.nx));
+    const std::vector<int> cp = hedge_plan(steps, size_t(g_.cus));
+    if (std::any_of(cp.begin(), cp.end(), [](int c) { return c > 1; })) {
         const size_t nj = djs.size();
+        uint32_t *d_done = g_.arena.alloc_n<uint32_t>(nj);
+        g_.memset0(d_done, nj * 4);
         for (size_t k = 0; k < nj; k++) djs[k].done = d_done + k;
-        for (size_t c = 1; c < copies; c++) djs.insert(djs.end(), djs.begin(), djs.begin() + long(nj));
+        for (size_t k = 0; k < nj; k++)
+            for (int c = 1; c < cp[k]; c++) djs.push_back(djs[k]);
     }
     lds = g_.chain_lds(lds, djs.size());
     if (!djs.empty()) FQZ5_HIP(launch_dec(g_.upload(djs), int(djs.size()), lds, g_.stream));
