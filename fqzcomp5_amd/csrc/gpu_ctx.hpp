@@ -234,9 +234,10 @@ inline size_t hedge_copies(size_t jobs, size_t cus) {
 // Copies per chain of a launch, from the chains' step counts: one each,
 // then the CUs left over, one copy at a time in turn, to the chains of at
 // least half the longest length (they set the launch time; a shorter
-// chain finishes in time on any CU), up to 8 copies each.  The slowest CUs
+// chain finishes in time on any CU), up to HEDGE_MAX copies each.  The slowest CUs
 // run a chain ~40 % slower than the fastest, so the
 // long chains gain the most from more draws.  All ones when hedging is off.
+constexpr int HEDGE_MAX = 24;   // copies of one chain at most
 inline std::vector<int> hedge_plan(const std::vector<uint64_t> &steps, size_t cus) {
     std::vector<int> c(steps.size(), 1);
     static const size_t cap_waves = [] {   // experiments: $FQZ5_HEDGE_WAVES caps the launch
@@ -251,7 +252,7 @@ inline std::vector<int> hedge_plan(const std::vector<uint64_t> &steps, size_t cu
     for (size_t i = 0; i < steps.size(); i++)
         if (2 * steps[i] >= mx) longs.push_back(i);
     size_t spare = cus - steps.size();
-    for (int round = 1; round < 8 && spare; round++)
+    for (int round = 1; round < HEDGE_MAX && spare; round++)
         for (size_t i : longs) {
             if (!spare) break;
             c[i]++;
