@@ -323,8 +323,8 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             }
             th.join();
             if (step_trace())
-                std::fprintf(stderr, "sections_try: setup %.1f ms, rANS candidates %.1f ms, fqz prepare "
-                             "waited %.1f ms more\n", 0.0, tc - t0, now_ms() - tc);
+                std::fprintf(stderr, "sections_try: rANS candidates %.1f ms, fqz prepare waited "
+                             "%.1f ms more\n", tc - t0, now_ms() - tc);
             if (err) std::rethrow_exception(err);
             std::vector<char> skip(fq.size(), 0);
             if (g_prune.load()) skip = prune_plan(reqs, fq);
