@@ -198,6 +198,16 @@ __global__ void k_seq_models_init(uint32_t *m, size_t n) {
         m[i] = 0x01010101u;
 }
 
+#ifdef FQZ5_SEQ_PROBE
+// shader cycles of the decoder's base steps (block 0): load + symbol,
+// renorm + stores, next counts + reverse update, from one step's end to the
+// next one's start, steps
+__device__ uint64_t g_seqprobe[8];
+extern "C" int fqz5_seq_probe_read(uint64_t *out) {
+    return int(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seqprobe), sizeof(g_seqprobe)));
+}
+#endif
+
 __global__ __launch_bounds__(64) void k_seq_dec(const SeqDecJob *Js) {
     __shared__ FList<256> run[3], lit;
     if (threadIdx.x != 0) return;
@@ -312,6 +322,9 @@ __global__ __launch_bounds__(64) void k_seq_dec(const SeqDecJob *Js) {
     // compiler knows)
     uint32_t next_seg = J.nseg > 1 ? J.seg[1] : 0xFFFFFFFFu;
     uint32_t *M = J.models;
+#ifdef FQZ5_SEQ_PROBE
+    uint64_t pr_ab = 0, pr_bc = 0, pr_cd = 0, pr_loop = 0, pr_last = 0, pr_n = 0;
+#endif
     while (p < n && !bad) {
         uint32_t runlen = 0, d;
         do {
@@ -326,7 +339,7 @@ __global__ __launch_bounds__(64) void k_seq_dec(const SeqDecJob *Js) {
         }
         const uint32_t end = p + runlen;
         have = false;
-        for (; p < end && !bad; p++) {
+        while (p < end && !bad) {
             if (p == next_seg) {                           // a record starts
                 si++;
                 next_seg = si + 1 < J.nseg ? J.seg[si + 1] : 0xFFFFFFFFu;
@@ -334,63 +347,98 @@ __global__ __launch_bounds__(64) void k_seq_dec(const SeqDecJob *Js) {
                 rv = seed_rv(J.k, mask);
                 have = false;
             }
+            // up to the run's end or the next record start, without
+            // per-base checks
+            const uint32_t stop = end < next_seg ? end : next_seg;
             if (state == 2u) {
-                J.out[p] = uint8_t(get_fl(&lit));
+                for (; p < stop && !bad; p++) J.out[p] = uint8_t(get_fl(&lit));
                 continue;
             }
-            // The counts of the 4 contexts that can follow fw (16 aligned
-            // bytes) and, both strands, of the 4 reverse contexts the base
-            // can lead to are loaded before this step's arithmetic; this
-            // step's own stores are patched in below.
-            if (bn < 8u) fill();                           // one byte is all a step takes
-            if (!have) F = M[fw];
-            // (u32 loads, the type of the stores, so that the compiler keeps
-            // them behind the previous step's stores)
-            const uint32_t *wp = M + ((fw << 2) & mask);
-            const uint4 win = make_uint4(wp[0], wp[1], wp[2], wp[3]);
-            uint32_t rc4[4] = {0, 0, 0, 0};
-            if (J.both)
-                for (uint32_t j = 0; j < 4; j++) rc4[j] = M[(rv >> 2) + (j << top)];
-            const uint32_t tot = sm4_total(F);
-            // symbol: the number of cumulative counts c with c * q <= code
-            // (q = range / total; c * q <= range, no overflow)
-            const uint32_t q = quot(rng, recip(tot));
-            const uint32_t c0 = F & 255u, c1 = c0 + ((F >> 8) & 255u), c2 = c1 + ((F >> 16) & 255u);
-            const uint32_t b = uint32_t(c0 * q <= code) + uint32_t(c1 * q <= code) +
-                               uint32_t(c2 * q <= code);
-            // q >= 2^24 / 255, so q * freq >= 2^16: at most one byte in
-            code -= sm4_cum(F, b) * q;
-            rng = q * ((F >> (8u * b)) & 255u);
-            const bool sh = rng < (1u << 24);
-            code = sh ? (code << 8) | uint32_t(bb >> 56) : code;
-            rng = sh ? rng << 8 : rng;
-            bb = sh ? bb << 8 : bb;
-            bn -= sh ? 8u : 0u;
-            const uint32_t Fu = sm4_bump(F, b, tot);
-            M[fw] = Fu;
-            J.out[p] = uint8_t(((0x54474341u >> (8u * b)) & 255u) | (state << 5));   // ACGT / acgt
-            const uint32_t fn = ((fw << 2) + b) & mask;
-            uint32_t Fn = b == 0 ? win.x : b == 1 ? win.y : b == 2 ? win.z : win.w;
-            if (fn == fw) Fn = Fu;
-            if (J.both) {
-                const uint32_t b2 = rv & 3u;
-                const uint32_t j = 3u - b;
-                rv = (rv >> 2) + (j << top);
-                uint32_t G = j == 0 ? rc4[0] : j == 1 ? rc4[1] : j == 2 ? rc4[2] : rc4[3];
-                if (rv == fw) G = Fu;
-                const uint32_t Gu = sm4_bump(G, b2, sm4_total(G));
-                M[rv] = Gu;
-                if (fn == rv) Fn = Gu;
+            for (; p < stop; p++) {
+                // The counts of the 4 contexts that can follow fw (16 aligned
+                // bytes) and, both strands, of the 4 reverse contexts the base
+                // can lead to are loaded before this step's arithmetic; this
+                // step's own stores are patched in below.
+#ifdef FQZ5_SEQ_PROBE
+                const uint64_t pa = __builtin_amdgcn_s_memtime();
+#endif
+                if (bn < 8u) fill();                           // one byte is all a step takes
+                if (!have) F = M[fw];
+                // (u32 loads, the type of the stores, so that the compiler keeps
+                // them behind the previous step's stores)
+                const uint32_t *wp = M + ((fw << 2) & mask);
+                const uint4 win = make_uint4(wp[0], wp[1], wp[2], wp[3]);
+                uint32_t rc4[4] = {0, 0, 0, 0};
+                if (J.both)
+                    for (uint32_t j = 0; j < 4; j++) rc4[j] = M[(rv >> 2) + (j << top)];
+                const uint32_t tot = sm4_total(F);
+                // symbol: the number of cumulative counts c with c * q <= code
+                // (q = range / total; c * q <= range, no overflow)
+                const uint32_t q = quot(rng, recip(tot));
+                const uint32_t c0 = F & 255u, c1 = c0 + ((F >> 8) & 255u), c2 = c1 + ((F >> 16) & 255u);
+                const uint32_t b = uint32_t(c0 * q <= code) + uint32_t(c1 * q <= code) +
+                                   uint32_t(c2 * q <= code);
+#ifdef FQZ5_SEQ_PROBE
+                asm volatile("" :: "v"(b));
+                const uint64_t pb = __builtin_amdgcn_s_memtime();
+#endif
+                // q >= 2^24 / 255, so q * freq >= 2^16: at most one byte in
+                code -= sm4_cum(F, b) * q;
+                rng = q * ((F >> (8u * b)) & 255u);
+                const bool sh = rng < (1u << 24);
+                code = sh ? (code << 8) | uint32_t(bb >> 56) : code;
+                rng = sh ? rng << 8 : rng;
+                bb = sh ? bb << 8 : bb;
+                bn -= sh ? 8u : 0u;
+                const uint32_t Fu = sm4_bump(F, b, tot);
+                M[fw] = Fu;
+                J.out[p] = uint8_t(((0x54474341u >> (8u * b)) & 255u) | (state << 5));   // ACGT / acgt
+#ifdef FQZ5_SEQ_PROBE
+                asm volatile("" :: "v"(code), "v"(rng));
+                const uint64_t pc = __builtin_amdgcn_s_memtime();
+#endif
+                const uint32_t fn = ((fw << 2) + b) & mask;
+                uint32_t Fn = b == 0 ? win.x : b == 1 ? win.y : b == 2 ? win.z : win.w;
+                if (fn == fw) Fn = Fu;
+                if (J.both) {
+                    const uint32_t b2 = rv & 3u;
+                    const uint32_t j = 3u - b;
+                    rv = (rv >> 2) + (j << top);
+                    uint32_t G = j == 0 ? rc4[0] : j == 1 ? rc4[1] : j == 2 ? rc4[2] : rc4[3];
+                    if (rv == fw) G = Fu;
+                    const uint32_t Gu = sm4_bump(G, b2, sm4_total(G));
+                    M[rv] = Gu;
+                    if (fn == rv) Fn = Gu;
+                }
+                fw = fn;
+                F = Fn;
+                have = true;
+#ifdef FQZ5_SEQ_PROBE
+                asm volatile("" :: "v"(F), "v"(rv));
+                const uint64_t pd = __builtin_amdgcn_s_memtime();
+                pr_ab += pb - pa;
+                pr_bc += pc - pb;
+                pr_cd += pd - pc;
+                if (pr_last) pr_loop += pa - pr_last;
+                pr_last = pd;
+                pr_n++;
+#endif
             }
-            fw = fn;
-            F = Fn;
-            have = true;
         }
         if (p >= n || bad) break;
         state = switch_to(state, get_st(state));
     }
     if (used() > len) bad = true;                      // took bytes past the end
     *J.status = bad ? -1 : 0;
+#ifdef FQZ5_SEQ_PROBE
+    if (blockIdx.x == 0) {
+        g_seqprobe[0] = pr_ab;
+        g_seqprobe[1] = pr_bc;
+        g_seqprobe[2] = pr_cd;
+        g_seqprobe[3] = pr_loop;
+        g_seqprobe[4] = pr_n;
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
