@@ -17,7 +17,11 @@ The default run adds configs[2] as the `level5` line item: a synthetic 4 GB
 NovaSeq FASTQ per GPU at -5 (fqzcomp_qual FQZ1/FQZ3 in the codec trial),
 timed with the same rules (`--no-level5` skips it).
 Names (tok3/LZP) and LZP3 for sequences are the next rows of SURVEY §8f
-and are not in the workload.  Multi-GPU: one process per GPU, weak scaling
+and are not in the workload; the sequence context models SEQ10/SEQ12B of
+the -5 preset are built (seq_cm.hip) but left out of the -5 masks while
+their decoder is one slow chain per block.  The `crc32` item
+times the block checksum (zlib crc32) over a 4 GiB device buffer.
+Multi-GPU: one process per GPU, weak scaling
 (each rank adds its own 1 GB file to the run); the only collective is the
 all-gather of candidate sizes that the trial state needs.
 
