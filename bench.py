@@ -1,34 +1,44 @@
 #!/usr/bin/env python3
-"""Benchmark: fqzcomp5 sequence+quality section coding on MI355X.
+"""Benchmark: fqzcomp5 per-block sequence + quality coding on MI355X.
 
 Metric (BASELINE.json): input MB/s encode+decode, 100 MB blocks, -3 and -5;
 bit-exact vs CPU.  Default workload (configs[1]): a synthetic 1 GB Illumina
 150 bp FASTQ with 8-level binned qualities at -3, split into 100 MB blocks
-by the reference's record rule (fqzcomp5.c:471-477).  `--level 5 --kind
-novaseq --gb 4` is configs[2] (the quality methods add FQZ1/FQZ3).  One step
-is one pass of the hot path over the whole workload, inputs resident in HBM:
+by the reference's record rule (fqzcomp5.c:471-477).  The default run adds
+configs[2] as the `level5` item: a synthetic 4 GB NovaSeq FASTQ per GPU at
+-5.  One step is one pass of the hot path over the whole workload, inputs
+resident in HBM:
 
     encode  every block's seq and qual section with the level's method sets
-            and the codec-trial state machine (fqzcomp5.c:1899-2144)
+            and the -t1 codec-trial state machine (fqzcomp5.c:1899-2144)
     decode  every chosen stream back to bytes.
 
-`value` = seq+qual section bytes of all ranks / step time (max over ranks).
-The default run adds configs[2] as the `level5` line item: a synthetic 4 GB
-NovaSeq FASTQ per GPU at -5 (fqzcomp_qual FQZ1/FQZ3 in the codec trial),
-timed with the same rules (`--no-level5` skips it).
-Names (tok3/LZP) and LZP3 for sequences are the next rows of SURVEY §8f
-and are not in the workload; the sequence context models SEQ10/SEQ12B of
-the -5 preset are built (seq_cm.hip) but left out of the -5 masks while
-their decoder is one slow chain per block.  The `crc32` item
-times the block checksum (zlib crc32) over a 4 GiB device buffer.
-Multi-GPU: one process per GPU, weak scaling
-(each rank adds its own 1 GB file to the run); the only collective is the
-all-gather of candidate sizes that the trial state needs.
+Encode and decode are timed separately inside each step (stream synchronised
+between them).  Reported per workload:
+    value     FASTQ input bytes of all ranks x steps / (t_enc + t_dec),
+              the max over ranks of each (the metric's combined figure)
+    enc_MBps, dec_MBps   the same bytes over t_enc and t_dec alone
+    section_MBps         the seq+qual section bytes over t_enc + t_dec
+The names and lengths sections of a block (tok3 / LZP names)
+are NOT coded by this build and not in the timed work; the FASTQ-byte rates
+divide by the whole FASTQ text, the section rate by the bytes coded.
+
+Methods: the level presets' sequence and quality masks (fqzcomp5.c:4886-4906)
+restricted to what this build codes; `config.methods_missing` names what
+the preset has that the run leaves out.
+
+Multi-GPU: `--gpus N` runs one process per GPU (it re-launches itself under
+torch.distributed.run when not started by it).  Weak scaling by default:
+each rank codes its own file of `--gb`, and the run's trial state covers the
+blocks of all ranks in rank order (the only collective: an all-gather of the
+candidate sizes, sections.exchange_sizes).  `--scaling strong` shards the
+blocks of one fixed file contiguously over the ranks.
 
 Also reported: the roofline of the dominant kernel from live HIP events on
-the library's stream, and the reference CPU path (oracle/_ref, compiled
-from the reference sources) timed on the host cores on the same bytes,
-whose output bytes are compared with the GPU's.
+the library's stream; the reference CPU path (oracle/_ref, compiled from the
+reference sources) on the host cores on the same sections, its chosen bytes
+compared with the GPU's; and the reference CLI relinked on this library
+(the drop-in) against the CLI as shipped on the same FASTQ file.
 """
 from __future__ import annotations
 
@@ -36,6 +46,7 @@ import argparse
 import ctypes as C
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -44,8 +55,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-FASTQ_REC = 346          # bytes per synthetic 150 bp FASTQ record (avg)
-BLK = 100_000_000        # -3 block size (fqzcomp5.c:4913)
+FASTQ_REC = 358          # bytes of FASTQ text per synthetic 150 bp record (avg)
+BLK = 100_000_000        # -3 / -5 block size (fqzcomp5.c:4896,4904)
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8 TB/s spec
 
 
@@ -54,11 +65,20 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def make_blocks(gb: float, seed: int, kind: str):
+def host_threads() -> int:
+    """The host cores this process may use: its CPU affinity, capped by the
+    box's per-GPU CPU share when one is set ($OMP_NUM_THREADS)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(n, 1)
+
+
+def make_reads(gb: float, seed: int, kind: str):
     from fqzcomp5_amd import synth
     n_reads = int(gb * 1e9 / FASTQ_REC)
-    r = (synth.novaseq if kind == "novaseq" else synth.illumina)(n_reads, seed=seed)
-    return r, synth.split_blocks(r, BLK)
+    return (synth.novaseq if kind == "novaseq" else synth.illumina)(n_reads, seed=seed)
 
 
 def pmc_traffic(kernel: str, tag: str = ""):
@@ -81,16 +101,17 @@ def method_order(m: int, fixed_len: int) -> int:
     return [0, 1, 64, 65, 128, 129, 192, 193][m - 1] if m <= 8 else (fixed_len << 8) + 9
 
 
-def cpu_baseline(run, tried, meth, gpu_out, threads):
-    """The reference (oracle/_ref) on the same sections and schedule: every
-    tried method of every section is compressed, the chosen stream is
-    checked against the GPU's bytes and decoded again."""
+def cpu_baseline(run, tried, meth, gpu_out, threads, fastq_bytes):
+    """The reference (oracle/_ref) on the same sections and schedule, one
+    section per host thread (hts_tpool-style): every tried method of every
+    section is compressed, the chosen stream is checked against the GPU's
+    bytes and decoded again."""
     from concurrent.futures import ThreadPoolExecutor
-    import numpy as np
     from oracle import binding
     from fqzcomp5_amd import sections as S
     kind = "reference" if binding.have_ref() else "port"
     codec = binding.ref() if kind == "reference" else binding.oracle()
+    seqc = None
     reads = run.reads
     secs = []
     for sec, s, e, fl, k in run.spans:
@@ -100,6 +121,7 @@ def cpu_baseline(run, tried, meth, gpu_out, threads):
                      reads.seq[s:e].tobytes()))
 
     def enc(i):
+        nonlocal seqc
         data, fixed, lens, seq = secs[i]
         best = None
         for m in range(1, S.M_LAST):
@@ -108,6 +130,13 @@ def cpu_baseline(run, tried, meth, gpu_out, threads):
             if m >= S.FQZ0:
                 out = codec.fqz_compress(data, lens.copy(), np.zeros(len(lens), np.uint32),
                                          m - S.FQZ0, seq)
+            elif S.SEQ10 <= m <= S.SEQ14B:
+                if seqc is None:
+                    seqc = binding.seq_ref() if binding.have_seq_ref() else binding.seq_oracle()
+                k_, both = S.SEQ_PARAMS[m]
+                out = seqc.encode(data, [int(x) for x in lens], both, k_)
+            elif m == S.LZP3:
+                out = codec.lzp3_compress(data)
             else:
                 out = codec.rans_compress(data, method_order(m, fixed))
             if m == meth[i]:
@@ -116,8 +145,14 @@ def cpu_baseline(run, tried, meth, gpu_out, threads):
 
     def dec(i):
         data, fixed, lens, seq = secs[i]
-        if meth[i] >= S.FQZ0:
+        m = meth[i]
+        if m >= S.FQZ0:
             return codec.fqz_decompress(chosen[i], lens.copy(), np.zeros(len(lens), np.uint32), seq)
+        if S.SEQ10 <= m <= S.SEQ14B:
+            k_, both = S.SEQ_PARAMS[m]
+            return seqc.decode(chosen[i], [int(x) for x in lens], both, k_, len(data))
+        if m == S.LZP3:
+            return codec.lzp3_uncompress(chosen[i], len(data))
         return codec.rans_uncompress(chosen[i])
 
     with ThreadPoolExecutor(threads) as ex:
@@ -129,49 +164,68 @@ def cpu_baseline(run, tried, meth, gpu_out, threads):
     same = all(c == g for c, g in zip(chosen, gpu_out))
     rt = all(b == h[0] for b, h in zip(back, secs))
     nbytes = sum(len(h[0]) for h in secs)
-    return {"value": round(nbytes / (t2 - t0) / 1e6, 2), "unit": "MB/s",
+    return {"value": round(fastq_bytes / (t2 - t0) / 1e6, 2), "unit": "MB/s",
             "cores": threads, "kind": kind,
-            "sample": f"all {len(secs)} seq+qual sections of the rank-0 "
-                      f"workload, the -t1 trial schedule (every tried "
-                      f"candidate encoded), {threads} host threads",
+            "sample": f"all {len(secs)} seq+qual sections of the rank-0 workload "
+                      f"({nbytes} section bytes of a {fastq_bytes} B FASTQ), the -t1 "
+                      f"trial schedule (every tried candidate encoded), one section "
+                      f"per host thread, {threads} threads",
+            "enc_MBps": round(fastq_bytes / (t1 - t0) / 1e6, 2),
+            "dec_MBps": round(fastq_bytes / (t2 - t1) / 1e6, 2),
+            "section_MBps": round(nbytes / (t2 - t0) / 1e6, 2),
             "enc_s": round(t1 - t0, 3), "dec_s": round(t2 - t1, 3),
             "bytes_match_gpu": bool(same), "roundtrip": bool(rt)}
 
 
 def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local, dist,
-            pmc_tag=""):
+            scaling="weak", pmc_tag=""):
     """One workload: warmup + `steps` timed steps (barrier + synchronize on
-    both sides, max over ranks) and the result fields of the JSON line."""
+    both sides, max over ranks) and the result fields of its JSON line."""
     import torch
-    from fqzcomp5_amd import lib, sections as S
+    from fqzcomp5_amd import lib, sections as S, synth
 
     t0 = time.time()
-    reads, blocks = make_blocks(gb, seed=(1 if level <= 3 else 2) + rank, kind=kind)
-    log(f"[bench] -{level} {kind} {gb:g} GB: generated {len(blocks)} blocks/rank in "
+    seed = (1 if level <= 3 else 2) + (rank if scaling == "weak" else 0)
+    reads = make_reads(gb, seed, kind)
+    blocks = synth.split_blocks(reads, BLK)
+    if scaling == "strong":                      # contiguous shard of one file
+        nb = len(blocks)
+        blocks = blocks[rank * nb // world:(rank + 1) * nb // world]
+    log(f"[bench] -{level} {kind} {gb:g} GB: {len(blocks)} blocks on rank 0, generated in "
         f"{time.time()-t0:.1f}s")
+    fq_local = sum(synth.fastq_size(reads, a, b) for a, b in blocks)
     dev = torch.device("cuda", local)
     run = S.Run(reads, blocks, dev)
     enc_secs = run.enc_secs()
-    avail = S.masks(level)
-    in_bytes_local = run.in_bytes
+    avail = S.masks(level, full=True)
 
-    def step():
-        state = S.new_state()
-        res, meth_all, sizes, tried, off = S.encode_run(enc_secs, avail, state)
-        dres = S.decode(run.dec_secs(res))
-        return res, dres, meth_all, tried, off
+    def encode():
+        res, meth_all, sizes, tried, off = S.encode_run(enc_secs, avail, S.new_state())
+        return res, meth_all, tried, off
+
+    def decode(res):
+        return S.decode(run.dec_secs(res))
 
     for _ in range(warmup):
-        step()
+        decode(encode()[0])
+    arena0 = lib.arena_bytes()
     so = lib.load()
     fq0 = S.trial_counts()
     so.fqz5_profile(1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    t_enc = t_dec = 0.0
     t0 = time.perf_counter()
     for _ in range(steps):
-        res, dres, meth_all, tried, off = step()
+        a = time.perf_counter()
+        res, meth_all, tried, off = encode()
+        torch.cuda.synchronize()
+        b = time.perf_counter()
+        dres = decode(res)
+        torch.cuda.synchronize()
+        t_enc += b - a
+        t_dec += time.perf_counter() - b
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -180,39 +234,54 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     so.fqz5_profile_read(prof)
     so.fqz5_profile(0)
     fq1 = S.trial_counts()
-    t_max = torch.tensor([dt], dtype=torch.float64, device=dev)
-    tot_bytes = torch.tensor([float(in_bytes_local)], dtype=torch.float64, device=dev)
+    arena1 = lib.arena_bytes()
+    tm = torch.tensor([dt, t_enc, t_dec], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(fq_local), float(run.in_bytes)], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot_bytes, op=dist.ReduceOp.SUM)
-    dt = float(t_max.item())
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    dt, t_enc, t_dec = (float(x) for x in tm.tolist())
+    fq_all, sec_all = (float(x) for x in tot.tolist())
 
     # ---- correctness: every decoded section equals its input -------------
     ok = all(r.status == 0 for r in res) and all(r.status == 0 for r in dres)
     ok = ok and run.roundtrip_ok()
     comp_bytes = sum(9 + r.clen for r in res)
     quals = "8-level binned quals" if kind == "illumina" else "NovaSeq 4-level i.i.d. quals"
+    full = set(S.preset_methods(level))
+    have = set(S.level_methods(level))
     out = {
-        "value": round(float(tot_bytes.item()) * steps / dt / 1e6, 2),
+        "value": round(fq_all * steps / (t_enc + t_dec) / 1e6, 2),
         "ms_per_step": round(dt / steps * 1e3, 2),
-        "data": f"synthetic (seeded {kind} 150 bp, {quals})",
+        "enc_MBps": round(fq_all * steps / t_enc / 1e6, 2),
+        "dec_MBps": round(fq_all * steps / t_dec / 1e6, 2),
+        "section_MBps": round(sec_all * steps / (t_enc + t_dec) / 1e6, 2),
+        "enc_ms_per_step": round(t_enc / steps * 1e3, 2),
+        "dec_ms_per_step": round(t_dec / steps * 1e3, 2),
+        "data": f"synthetic (seeded {kind} 150 bp, {quals}); inputs resident in HBM, "
+                f"no host<->device copies of section bytes in the timed region",
         "config": {"workload": f"fqzcomp5 -{level} seq+qual sections of a "
-                               f"{gb:g} GB FASTQ per GPU, 100 MB blocks",
-                   "blocks_per_gpu": len(blocks), "level": level,
-                   "section_bytes_per_gpu": in_bytes_local,
-                   "compressed_bytes_per_gpu": comp_bytes,
-                   "methods": sorted({int(m) for m in meth_all}),
+                               f"{gb:g} GB FASTQ {'per GPU' if scaling == 'weak' else 'in total'}, "
+                               f"100 MB blocks",
+                   "blocks_rank0": len(blocks), "level": level,
+                   "fastq_bytes_rank0": fq_local,
+                   "section_bytes_rank0": run.in_bytes,
+                   "compressed_bytes_rank0": comp_bytes,
+                   "not_coded": "names + lengths sections (SURVEY §8 f1)",
+                   "methods_tried": sorted(have),
+                   "methods_missing": sorted(full - have),
+                   "methods_chosen": sorted({int(m) for m in meth_all}),
                    "roundtrip_ok": bool(ok),
-                   "parallelism": f"blocks sharded over {world} GPU(s)",
-                   # fqz trial candidates in the timed steps, and how many
-                   # were provably losing and skipped their range chain
-                   # (fqz5_set_trial_prune; output bytes unchanged)
+                   "parallelism": f"blocks sharded over {world} GPU(s) ({scaling})",
+                   "arena_bytes": [int(arena0), int(arena1)],
+                   # candidates in the timed steps, and how many were provably
+                   # losing and skipped their range chain (output unchanged)
                    "fqz_trial": {"tried": fq1[0] - fq0[0], "pruned": fq1[1] - fq0[1]}},
     }
     # ---- roofline of the dominant kernel ---------------------------------
     enc_ms, enc_n, enc_b, dec_ms, dec_n, dec_b = list(prof)
     if enc_ms >= dec_ms:
-        name, ms, n, b = "k_rans_enc", enc_ms, enc_n, enc_b
+        name, ms, n, b = "k_enc_chain", enc_ms, enc_n, enc_b
     else:
         name, ms, n, b = "k_rans_dec", dec_ms, dec_n, dec_b
     avg_ms = ms / max(n, 1)
@@ -222,7 +291,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     # symbol on each of the 4 interleaved states
     longest = max((e - s) for _, s, e, _, _ in run.spans)
     out["roofline"] = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
-                       "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 6),
+                       "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 7),
                        "traffic": traffic, "traffic_source": tsrc, "kernel": name,
                        "avg_launch_ms": round(avg_ms, 3),
                        "bytes_per_launch": int(b / max(n, 1)),
@@ -235,9 +304,9 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     # ---- CPU baseline (rank 0, N=1) -----------------------------------------
     if rank == 0 and world == 1 and cpu:
         gpu_streams = [run.chosen(res, i) for i in range(len(res))]
-        threads = min(cpu_threads, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(run, tried[off:off + len(res)],
-                                           meth_all[off:off + len(res)], gpu_streams, threads)
+                                           meth_all[off:off + len(res)], gpu_streams,
+                                           cpu_threads, fq_local)
     del run, reads
     torch.cuda.empty_cache()
     return out
@@ -248,7 +317,6 @@ def crc_item(lib, torch, gib: int = 4, reps: int = 5):
     device-resident 4 GiB buffer: fqz5_crc32_dev wall time per call (best of
     `reps`, table upload + tile kernel + combine passes + sync), checked
     against zlib on a 1 MiB prefix.  HBM-bound: 1 B read per input byte."""
-    import time
     import zlib
     try:
         n = gib << 30
@@ -272,20 +340,88 @@ def crc_item(lib, torch, gib: int = 4, reps: int = 5):
         return {"error": str(e)}
 
 
+def dropin_item(gb: float, level: int, threads: int, timeout: int = 240):
+    """The reference CLI as shipped (oracle/_ref/fqzcomp5) against the same
+    CLI relinked on libfqz5_mi355x.so (oracle/_ref/fqzcomp5_gpu, the drop-in
+    of INTEGRATION.md) on the same synthetic FASTQ file: wall time of encode
+    and decode with -t<threads>, .fqz5 bytes compared.  Host buffers: every
+    codec call copies its block to the GPU and back (PCIe included)."""
+    import hashlib
+    import tempfile
+    from fqzcomp5_amd import synth
+    cpu = os.path.join(ROOT, "oracle", "_ref", "fqzcomp5")
+    gpu = os.path.join(ROOT, "oracle", "_ref", "fqzcomp5_gpu")
+    if not (os.path.exists(cpu) and os.path.exists(gpu)):
+        return {"error": "oracle/_ref CLIs not built"}
+    try:
+        with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+            src = os.path.join(td, "in.fastq")
+            r = synth.illumina(int(gb * 1e9 / FASTQ_REC), seed=1, with_names=True)
+            with open(src, "wb") as f:
+                f.write(r.to_fastq())
+            nbytes = os.path.getsize(src)
+            del r
+            res = {"fastq_bytes": nbytes, "level": level, "threads": threads}
+            md5 = {}
+            for tag, exe in (("cpu", cpu), ("gpu", gpu)):
+                out = os.path.join(td, tag + ".fqz5")
+                back = os.path.join(td, tag + ".fastq")
+                t0 = time.perf_counter()
+                subprocess.run([exe, f"-{level}", f"-t{threads}", src, out], check=True,
+                               capture_output=True, timeout=timeout)
+                t1 = time.perf_counter()
+                subprocess.run([exe, "-d", f"-t{threads}", out, back], check=True,
+                               capture_output=True, timeout=timeout)
+                t2 = time.perf_counter()
+                md5[tag] = hashlib.md5(open(out, "rb").read()).hexdigest()
+                with open(back, "rb") as fb, open(src, "rb") as fs:
+                    same = fb.read() == fs.read()
+                res[tag] = {"enc_MBps": round(nbytes / (t1 - t0) / 1e6, 2),
+                            "dec_MBps": round(nbytes / (t2 - t1) / 1e6, 2),
+                            "enc_s": round(t1 - t0, 3), "dec_s": round(t2 - t1, 3),
+                            "roundtrip": same}
+                os.unlink(back)
+            res["bytes_match"] = md5["cpu"] == md5["gpu"]
+            return res
+    except Exception as e:
+        return {"error": str(e)[-300:]}
+
+
+def relaunch(n: int) -> None:
+    """Start `n` ranks of this script under torch.distributed.run (one
+    process per GPU) and exit with its status.  Runs before anything has
+    touched the GPU."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    raise SystemExit(subprocess.call(cmd, env=env))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--gb", type=float, default=1.0)
-    ap.add_argument("--level", type=int, default=3, choices=[1, 3, 5])
+    ap.add_argument("--level", type=int, default=3, choices=[1, 3, 5, 7, 9])
     ap.add_argument("--kind", default="illumina", choices=["illumina", "novaseq"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-level5", action="store_true",
                     help="skip the configs[2] (-5 NovaSeq 4 GB) line item")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads of the CPU baseline (0: all this process may use)")
     ap.add_argument("--no-crc", action="store_true", help="skip the block-checksum item")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in CLI item")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        relaunch(args.gpus)
 
     import torch
     import torch.distributed as dist
@@ -294,31 +430,41 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        chk = torch.ones(1, device="cuda")
+        dist.all_reduce(chk)
+        assert int(chk.item()) == world, "RCCL does not see every rank"
     if not lib.device_ok():
         raise SystemExit("no GPU: " + lib.last_error())
+    threads = args.cpu_threads or host_threads()
 
     m = measure(args.level, args.kind, args.gb, args.steps, args.warmup, not args.no_cpu,
-                args.cpu_threads, world, rank, local, dist,
+                threads, world, rank, local, dist, scaling=args.scaling,
                 pmc_tag="_l5" if args.level == 5 else "")
     out = {"metric": "input MB/s encode+decode, 100MB blocks, -3 and -5; bit-exact vs CPU",
            "value": m["value"], "unit": "MB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": m["ms_per_step"], "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": m["data"],
-           "config": m["config"], "roofline": m["roofline"]}
+           "scaling": args.scaling, "vs_baseline": None, "dtype": "u8", "data": m["data"],
+           "config": m["config"], "enc_MBps": m["enc_MBps"], "dec_MBps": m["dec_MBps"],
+           "section_MBps": m["section_MBps"], "enc_ms_per_step": m["enc_ms_per_step"],
+           "dec_ms_per_step": m["dec_ms_per_step"], "roofline": m["roofline"]}
     if "cpu_baseline" in m:
         out["cpu_baseline"] = m["cpu_baseline"]
     # The metric covers -3 and -5: the default run adds configs[2] (-5,
-    # fqzcomp_qual candidates in the trial, 4 GB NovaSeq per GPU) as its own
-    # line item with the same timing rules; `value` stays configs[1] (-3).
+    # 4 GB NovaSeq per GPU) as its own item with the same timing rules;
+    # `value` stays configs[1] (-3).
     if not args.no_level5 and args.level == 3:
-        m5 = measure(5, "novaseq", 4.0, args.steps, args.warmup, not args.no_cpu,
-                     args.cpu_threads, world, rank, local, dist, pmc_tag="_l5")
-        out["level5"] = m5
-    if rank == 0 and not args.no_crc:
+        out["level5"] = measure(5, "novaseq", 4.0 if args.scaling == "weak" else 4.0 * world,
+                                args.steps, args.warmup, not args.no_cpu, threads, world,
+                                rank, local, dist, scaling=args.scaling, pmc_tag="_l5")
+    if rank == 0 and world == 1 and not args.no_crc:
         out["crc32"] = crc_item(lib, torch)
+    if rank == 0 and world == 1 and not args.no_dropin and args.level == 3:
+        out["dropin_cli"] = dropin_item(args.gb, 3, threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -480,6 +480,9 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         const double t1 = step_trace() ? now_ms() : 0;
         write_layouts_dev(g, ls, dsts);
         g.reset();
+        // the fqz candidates of the try live in the aux arena: rewind it too,
+        // or every step's trial buffers take fresh chunks (the r01 bench OOM)
+        if (!t_sess.fqz.empty()) gpu_aux().reset();
         t_sess = TrySession();
         if (step_trace())
             std::fprintf(stderr, "sections_commit: late encodes %.1f ms, write + sync %.1f ms\n",

@@ -60,6 +60,9 @@ GpuCtx &gpu_aux() {
     if (!g_aux) g_aux.reset(new GpuCtx());
     return *g_aux;
 }
+static uint64_t arena_bytes() {
+    return (g_ctx ? g_ctx->arena.bytes() : 0) + (g_aux ? g_aux->arena.bytes() : 0);
+}
 
 // Size a stream decodes to, from its header (needed when the caller did
 // not give an output buffer).  0 with ok=false if it cannot be known.
@@ -301,6 +304,8 @@ int fqz5_device_ok(void) {
 }
 
 const char *fqz5_last_error(void) { return g_err.c_str(); }
+
+uint64_t fqz5_arena_bytes(void) { return arena_bytes(); }
 
 unsigned fqz5_set_hot_min(unsigned min_events) { return fqz_set_hot_min(min_events); }
 

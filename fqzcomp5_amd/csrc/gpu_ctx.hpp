@@ -58,6 +58,12 @@ class DevArena {
         for (auto &c : chunks_) c.used = 0;
         cur_ = 0;
     }
+    // device bytes held (all chunks, used or not)
+    size_t bytes() const {
+        size_t t = 0;
+        for (auto &c : chunks_) t += c.size;
+        return t;
+    }
 
   private:
     struct Chunk { void *base; size_t size, used; };

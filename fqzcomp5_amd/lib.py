@@ -127,6 +127,13 @@ def device_ok() -> bool:
     return bool(load().fqz5_device_ok())
 
 
+def arena_bytes() -> int:
+    """Device bytes held by this thread's GPU arenas (fqz5_arena_bytes)."""
+    so = load()
+    so.fqz5_arena_bytes.restype = C.c_uint64
+    return int(so.fqz5_arena_bytes())
+
+
 def header_symbols() -> list[str]:
     """Function names declared in include/*.h."""
     import glob

@@ -35,19 +35,41 @@ SEQ_MASK = sum(1 << m for m in range(SEQ10, SEQ14B + 1))
 # schedule names them (see encode_run)
 WORK_MASK = FQZ_MASK | SEQ_MASK
 
-# Method masks of the level presets (fqzcomp5.c:4886-4932) restricted to
-# rANS and fqzcomp_qual: the bench's workloads.  masks(level, seq_cm=True)
-# adds the sequence context models of the preset (SEQ10 / SEQ12B at -5),
-# which this build has (seq_cm.hip) but whose decoder is one serial chain
-# per block.  LZP3 is not in this build.
-LEVEL_MASKS = {
-    1: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193],
+# Method masks of the level presets for the sequence and quality sections
+# (fqzcomp5.c:4886-4932; the names masks belong to SURVEY §8 f1) and their
+# block sizes.
+PRESET_MASKS = {
+    1: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3],
         SEC_QUAL: [RANS0, RANS1, RANS129, RANS193]},
-    3: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193],
+    3: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3],
         SEC_QUAL: [RANS0, RANS1, RANS129, RANS193, RANSXN1]},
-    5: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193],
+    5: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3, SEQ10, SEQ12B],
         SEC_QUAL: [RANS0, RANS1, RANS129, RANS193, RANSXN1, FQZ1, FQZ3]},
+    7: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3, RANS65, SEQ10, SEQ12B, SEQ13B],
+        SEC_QUAL: [RANS0, RANS1, RANS129, RANS193, RANS65, FQZ0, FQZ1, FQZ2, FQZ3, FQZ4]},
+    9: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, RANS64, RANS65, RANS128, LZP3,
+                  SEQ10, SEQ12, SEQ12B, SEQ13B, SEQ14B],
+        SEC_QUAL: [RANS0, RANS1, RANS129, RANS193, RANS64, RANS65, RANS128,
+                   FQZ0, FQZ1, FQZ2, FQZ3, FQZ4]},
 }
+BLOCK_SIZE = {1: 10_000_000, 3: 100_000_000, 5: 100_000_000, 7: 500_000_000,
+              9: 1_000_000_000}
+# encode_seq's (k, both strands) per method (fqzcomp5.c:2047-2062)
+SEQ_PARAMS = {SEQ10: (10, 0), SEQ12: (12, 0), SEQ12B: (12, 1), SEQ13B: (13, 1),
+              SEQ14B: (14, 1)}
+# methods this build codes (every rANS / fqz / sequence-CM method; LZP3 is
+# not built yet)
+BUILT = set(range(RANS0, RANSXN1 + 1)) | set(SEQ_PARAMS) | set(range(FQZ0, FQZ4 + 1))
+
+
+def preset_methods(level: int) -> list[int]:
+    """Every seq/qual method of the preset, (section, method) flattened."""
+    return sorted({m for ms in PRESET_MASKS[level].values() for m in ms})
+
+
+def level_methods(level: int) -> list[int]:
+    """The preset's seq/qual methods that this build codes."""
+    return [m for m in preset_methods(level) if m in BUILT]
 
 
 class Section(C.Structure):
@@ -119,17 +141,16 @@ def _load():
     return so
 
 
-SEQ_CM_MASKS = {5: [SEQ10, SEQ12B]}     # fqzcomp5.c:4905
-
-
-def masks(level: int, seq_cm: bool = False) -> np.ndarray:
+def masks(level: int, seq_cm: bool = False, full: bool = False) -> np.ndarray:
+    """Per-section method masks of a level preset, restricted to the built
+    methods.  Without `full` the sequence context models (SEQ*) are left out
+    unless `seq_cm` is set (the reduced trial of earlier tests)."""
     av = np.zeros(4, np.uint32)
-    for sec, ms in LEVEL_MASKS[level].items():
+    for sec, ms in PRESET_MASKS[level].items():
         for m in ms:
+            if m not in BUILT or (m in SEQ_PARAMS and not (seq_cm or full)):
+                continue
             av[sec] |= np.uint32(1 << m)
-    if seq_cm:
-        for m in SEQ_CM_MASKS.get(level, []):
-            av[SEC_SEQ] |= np.uint32(1 << m)
     return av
 
 

@@ -130,6 +130,17 @@ def novaseq(n_reads: int, seed: int = 2, read_len: int = 150,
     return Reads(seq, qual, lens, names, name_l)
 
 
+COMMENT = b" 1:N:0:ACGTACGT"      # the comment every synthetic name carries
+
+
+def fastq_size(r: Reads, a: int = 0, b: int | None = None) -> int:
+    """Bytes of the FASTQ text of records [a, b) as to_fastq writes it:
+    '@' name ' ' comment '\\n' seq '\\n' '+\\n' qual '\\n'."""
+    b = r.num_records if b is None else b
+    return int((r.name_l[a:b].astype(np.int64) + len(COMMENT) + 6).sum()
+               + 2 * r.lens[a:b].astype(np.int64).sum())
+
+
 def split_blocks(r: Reads, blk_size: int) -> list[tuple[int, int]]:
     """Record ranges [a, b) per block, by the load_seqs_kseq rule
     (fqzcomp5.c:471-477): ``record_size = name.l + 1 + seq.l + qual.l``."""

@@ -203,6 +203,11 @@ int fqz5_device_ok(void);
 /* Last error message of the calling thread ("" if none). */
 const char *fqz5_last_error(void);
 
+/* Device bytes held by the calling thread's arenas (its GPU context and
+ * the helper context of fqz5_sections_try).  Constant from step to step of
+ * a repeated workload once the first step has sized them. */
+uint64_t fqz5_arena_bytes(void);
+
 /* Kernel timing with HIP events on fqz5_stream() (benchmark roofline).
  * fqz5_profile(1) resets and enables; fqz5_profile_read fills
  * {enc_ms, enc_launches, enc_bytes, dec_ms, dec_launches, dec_bytes} for

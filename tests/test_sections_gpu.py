@@ -89,3 +89,21 @@ def test_run_vs_reference(level, kind, nreads, blk, cm):
     torch.cuda.synchronize()
     assert run.roundtrip_ok()
     del offs
+
+
+def test_arena_constant_over_steps():
+    """Repeated -5 encode + decode steps (fqz trial candidates on the helper
+    context) hold a constant amount of device arena memory: the r01 driver
+    bench died with hipMalloc out of memory because the helper arena was
+    never rewound after fqz5_sections_commit."""
+    reads = synth.illumina(20000, seed=5)
+    blocks = synth.split_blocks(reads, 1_000_000)
+    run = S.Run(reads, blocks, torch.device("cuda", 0))
+    sizes = []
+    for _ in range(8):
+        res, *_ = S.encode_run(run.enc_secs(), S.masks(5), S.new_state())
+        dres = S.decode(run.dec_secs(res))
+        assert all(r.status == 0 for r in res) and all(r.status == 0 for r in dres)
+        sizes.append(lib.arena_bytes())
+    assert run.roundtrip_ok()
+    assert sizes[1:] == sizes[1:2] * (len(sizes) - 1), sizes
