@@ -117,6 +117,7 @@ struct TrySession {
     std::vector<uint64_t> fqz_lb;                 // pruned candidates: size lower bound (else 0)
     std::vector<std::vector<int>> fqz_of;
     std::vector<SeqEncReq> seq;                   // sequence CM candidates
+    std::vector<uint64_t> seq_lb;                 // pruned candidates: size lower bound (else 0)
     std::vector<std::vector<int>> seq_of;
     std::deque<std::vector<uint32_t>> recs;       // their (rewritable) lengths / flags
     bool open = false;
@@ -143,24 +144,31 @@ FqzEncReq fqz_req(const fqz5_section &S, int m, std::deque<std::vector<uint32_t>
 }
 thread_local TrySession t_sess;
 
-// Trial pruning (fqz5_set_trial_prune): an fqz candidate whose size is
-// provably not below the best rANS candidate's, in every trial section and
-// summed over the trial window, cannot be chosen (rANS methods come first,
-// so they win ties); its range chain and bytes are skipped and its lower
-// bound stands in for its size.  The caller enables it only when the
-// sections of this call that try fqz form one whole trial window.
+// Trial pruning (fqz5_set_trial_prune): an fqz or sequence-model candidate
+// whose size is provably not below the best rANS candidate's, in every trial
+// section and summed over the trial window, cannot be chosen (rANS methods
+// come first, so they win ties); its range chain and bytes are skipped and
+// its lower bound stands in for its size.  The caller enables it only when
+// the sections of this call that try such methods form one whole trial
+// window per section kind.
 std::atomic<int> g_prune{0};
 std::atomic<uint64_t> g_fqz_tried{0}, g_fqz_pruned{0};
 
-// Which fqz requests to skip, from the exact rANS sizes and the fqz lower
-// bounds of this session (TrySession::req_of / fqz_of).
-std::vector<char> prune_plan(const std::vector<CompressReq> &reqs, std::vector<FqzEncReq> &fqz) {
-    std::vector<char> skip(fqz.size(), 0);
-    const int nsec = int(t_sess.fqz_of.size());
-    std::vector<int> F;                                 // sections trying fqz
+// Which requests of one family of work candidates (fqz methods FQZ0..FQZ4 on
+// quality sections, or the sequence models SEQ10..SEQ14B) to skip, from the
+// exact sizes of the earlier (rANS) methods and the family's lower bounds.
+// of[i][m]: the request index of method m in section i (-1 if none); lb(k):
+// request k's size lower bound (0 if unknown).
+template <class LB>
+std::vector<char> prune_plan(const std::vector<CompressReq> &reqs,
+                             const std::vector<std::vector<int>> &of, int mlo, int mhi,
+                             size_t nreq, LB lb) {
+    std::vector<char> skip(nreq, 0);
+    const int nsec = int(of.size());
+    std::vector<int> F;                                 // sections trying the family
     for (int i = 0; i < nsec; i++)
-        for (int m = FQZ0; m <= FQZ4; m++)
-            if (t_sess.fqz_of[i][m] >= 0) { F.push_back(i); break; }
+        for (int m = mlo; m <= mhi; m++)
+            if (of[i][m] >= 0) { F.push_back(i); break; }
     // one whole trial window: every method's usize is then the same, and the
     // window's pick (min (csize + 1) / usize) compares plain sums
     if (F.size() != size_t(FQZ5_METRICS_TRIAL)) return skip;
@@ -168,14 +176,14 @@ std::vector<char> prune_plan(const std::vector<CompressReq> &reqs, std::vector<F
         const int ri = t_sess.req_of[i][m];
         return ri >= 0 && reqs[size_t(ri)].ok ? int64_t(layout_size(reqs[size_t(ri)].out)) : -1;
     };
-    std::vector<int64_t> best(F.size(), -1);            // per section: min rANS size
+    std::vector<int64_t> best(F.size(), -1);            // per section: min earlier size
     for (size_t k = 0; k < F.size(); k++)
-        for (int m = 1; m < FQZ0; m++) {
+        for (int m = 1; m < mlo; m++) {
             const int64_t z = rsize(F[k], m);
             if (z >= 0 && (best[k] < 0 || z < best[k])) best[k] = z;
         }
-    int64_t best_sum = -1;                              // min over rANS methods tried everywhere
-    for (int m = 1; m < FQZ0; m++) {
+    int64_t best_sum = -1;                              // min over methods tried everywhere
+    for (int m = 1; m < mlo; m++) {
         int64_t sum = 0;
         bool all = true;
         for (int i : F) {
@@ -185,19 +193,19 @@ std::vector<char> prune_plan(const std::vector<CompressReq> &reqs, std::vector<F
         }
         if (all && (best_sum < 0 || sum < best_sum)) best_sum = sum;
     }
-    for (int m = FQZ0; m <= FQZ4; m++) {
+    for (int m = mlo; m <= mhi; m++) {
         bool ok = true;
         int64_t lbsum = 0;
         for (size_t k = 0; k < F.size() && ok; k++) {
-            const int fi = t_sess.fqz_of[F[k]][m];
+            const int fi = of[F[k]][m];
             if (fi < 0) { ok = false; break; }            // must be tried in the whole window
-            const int64_t lb = int64_t(fqz_size_lower_bound(fqz[size_t(fi)]));
-            ok = lb > 0 && best[k] >= 0 && lb >= best[k];
-            lbsum += lb;
+            const int64_t b = int64_t(lb(size_t(fi)));
+            ok = b > 0 && best[k] >= 0 && b >= best[k];
+            lbsum += b;
         }
         if (!ok || !(best_sum >= 0 && lbsum >= best_sum)) continue;
         for (int i : F)
-            if (t_sess.fqz_of[i][m] >= 0) skip[size_t(t_sess.fqz_of[i][m])] = 1;
+            if (of[i][m] >= 0) skip[size_t(of[i][m])] = 1;
     }
     return skip;
 }
@@ -296,18 +304,22 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 reqs.push_back(std::move(r));
             }
         }
-        // The fqz candidates (trial blocks) run on the thread's second
-        // context from a helper thread, beside the rANS candidates: both are
-        // a few long chains that leave most of the GPU idle.
+        // The fqz and sequence-model candidates (trial blocks) run on the
+        // thread's second context from a helper thread, beside the rANS
+        // candidates: both are a few long chains that leave most of the GPU
+        // idle.  Their model passes come first; then the candidates that
+        // provably lose the trial are pruned; then the range chains.
         static const bool no_aux = std::getenv("FQZ5_NO_AUX") != nullptr;
-        if (!t_sess.fqz.empty() && !no_aux) {
+        std::vector<FqzEncReq> &fq = t_sess.fqz;
+        std::vector<SeqEncReq> &sq = t_sess.seq;
+        if ((!fq.empty() || !sq.empty()) && !no_aux) {
             GpuCtx &ga = gpu_aux();
-            std::vector<FqzEncReq> &fq = t_sess.fqz;   // (t_sess is this thread's)
             std::exception_ptr err;
-            std::thread th([&ga, &fq, &err] {
+            std::thread th([&ga, &fq, &sq, &err] {
                 try {
                     FQZ5_HIP(hipSetDevice(ga.device));
-                    fqz_encode_prepare(ga, fq);
+                    if (!fq.empty()) fqz_encode_prepare(ga, fq);
+                    if (!sq.empty()) seq_encode_prepare(ga, sq);
                 } catch (...) {
                     err = std::current_exception();
                 }
@@ -323,22 +335,33 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             }
             th.join();
             if (step_trace())
-                std::fprintf(stderr, "sections_try: rANS candidates %.1f ms, fqz prepare waited "
+                std::fprintf(stderr, "sections_try: rANS candidates %.1f ms, model passes waited "
                              "%.1f ms more\n", tc - t0, now_ms() - tc);
             if (err) std::rethrow_exception(err);
-            std::vector<char> skip(fq.size(), 0);
-            if (g_prune.load()) skip = prune_plan(reqs, fq);
-            fqz_encode_finish(ga, fq, &skip);
-            for (size_t k = 0; k < fq.size(); k++) t_sess.fqz_lb.push_back(skip[k] ? fqz_size_lower_bound(fq[k]) : 0);
-            g_fqz_tried += fq.size();
-            for (char c : skip) g_fqz_pruned += c ? 1 : 0;
+            std::vector<char> skip_f(fq.size(), 0), skip_s(sq.size(), 0);
+            if (g_prune.load()) {
+                skip_f = prune_plan(reqs, t_sess.fqz_of, FQZ0, FQZ4, fq.size(),
+                                    [&](size_t k) { return fqz_size_lower_bound(fq[k]); });
+                skip_s = prune_plan(reqs, t_sess.seq_of, SEQ10, SEQ14B, sq.size(),
+                                    [&](size_t k) { return seq_size_lower_bound(sq[k]); });
+            }
+            if (!fq.empty()) fqz_encode_finish(ga, fq, &skip_f);
+            if (!sq.empty()) seq_encode_finish(ga, sq, &skip_s);
+            for (size_t k = 0; k < fq.size(); k++)
+                t_sess.fqz_lb.push_back(skip_f[k] ? fqz_size_lower_bound(fq[k]) : 0);
+            for (size_t k = 0; k < sq.size(); k++)
+                t_sess.seq_lb.push_back(skip_s[k] ? seq_size_lower_bound(sq[k]) : 0);
+            g_fqz_tried += fq.size() + sq.size();
+            for (char c : skip_f) g_fqz_pruned += c ? 1 : 0;
+            for (char c : skip_s) g_fqz_pruned += c ? 1 : 0;
         } else {
             compress_batch(g, reqs);
-            if (!t_sess.fqz.empty()) fqz_encode_batch(g, t_sess.fqz);
-            t_sess.fqz_lb.assign(t_sess.fqz.size(), 0);
-            g_fqz_tried += t_sess.fqz.size();
+            if (!fq.empty()) fqz_encode_batch(g, fq);
+            if (!sq.empty()) seq_encode_batch(g, sq);
+            t_sess.fqz_lb.assign(fq.size(), 0);
+            t_sess.seq_lb.assign(sq.size(), 0);
+            g_fqz_tried += fq.size() + sq.size();
         }
-        if (!t_sess.seq.empty()) seq_encode_batch(g, t_sess.seq);
         t_sess.open = true;
         if (step_trace()) std::fprintf(stderr, "sections_try: %.1f ms\n", now_ms() - t0);
         // sizes as compress_with_methods sees them: UINT_MAX when not run,
@@ -349,7 +372,11 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 const int si = t_sess.seq_of[i][m];
                 uint32_t sz = UINT32_MAX;
                 if (ri >= 0) sz = reqs[ri].ok ? layout_size(reqs[ri].out) : 0;
-                if (si >= 0) sz = t_sess.seq[size_t(si)].ok ? layout_size(t_sess.seq[size_t(si)].out) : 0;
+                if (si >= 0) {
+                    const uint64_t lb = t_sess.seq_lb[size_t(si)];   // pruned: its lower bound
+                    sz = t_sess.seq[size_t(si)].ok ? layout_size(t_sess.seq[size_t(si)].out)
+                         : lb ? uint32_t(std::min<uint64_t>(lb, UINT32_MAX - 1)) : 0;
+                }
                 if (fi >= 0) {
                     const uint64_t lb = t_sess.fqz_lb[size_t(fi)];   // pruned: its lower bound
                     sz = t_sess.fqz[size_t(fi)].ok ? layout_size(t_sess.fqz[size_t(fi)].out)
@@ -482,7 +509,7 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         g.reset();
         // the fqz candidates of the try live in the aux arena: rewind it too,
         // or every step's trial buffers take fresh chunks (the r01 bench OOM)
-        if (!t_sess.fqz.empty()) gpu_aux().reset();
+        if (!t_sess.fqz.empty() || !t_sess.seq.empty()) gpu_aux().reset();
         t_sess = TrySession();
         if (step_trace())
             std::fprintf(stderr, "sections_commit: late encodes %.1f ms, write + sync %.1f ms\n",

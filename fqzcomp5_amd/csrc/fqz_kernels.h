@@ -140,6 +140,8 @@ hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t *ho
 hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
 // per workgroup: sum over its events of log2(total / freq) (after the model pass)
 hipError_t launch_fqz_entropy(const FqzEvJob &j, double *partial, uint32_t nblk, hipStream_t s);
+hipError_t launch_rec_entropy(const uint4 *rec, uint32_t nev, double *partial, uint32_t nblk,
+                              hipStream_t s);
 hipError_t launch_fqz_carry(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
 hipError_t launch_fqz_expand(const FqzEvJob &j, hipStream_t s);
 hipError_t launch_fqz_bytes(const FqzEvJob &j, int phase, hipStream_t s);

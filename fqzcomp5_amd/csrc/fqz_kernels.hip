@@ -563,6 +563,32 @@ __global__ __launch_bounds__(256) void k_fqz_entropy(FqzEvJob J, double *partial
     if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
+// The same bound from coder records {RN(1/total) (2 words), freq, cum} in
+// stream order (the sequence model's events): log2(total) = -log2(RN(1/total))
+// to within 2^-52 relative, far inside the host's margin.
+__global__ __launch_bounds__(256) void k_rec_entropy(const uint4 *rec, uint32_t nev, double *partial) {
+    __shared__ double red[256];
+    double acc = 0.0;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nev; k += gridDim.x * blockDim.x) {
+        const uint4 r = rec[k];
+        const double rn = __longlong_as_double((long long)((uint64_t(r.y) << 32) | r.x));
+        acc += -log2(rn) - log2(double(r.z));
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (uint32_t o = 128; o; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+hipError_t launch_rec_entropy(const uint4 *rec, uint32_t nev, double *partial, uint32_t nblk,
+                              hipStream_t s) {
+    if (nblk) hipLaunchKernelGGL(k_rec_entropy, dim3(nblk), dim3(256), 0, s, rec, nev, partial);
+    return hipGetLastError();
+}
+
 hipError_t launch_fqz_entropy(const FqzEvJob &j, double *partial, uint32_t nblk, hipStream_t s) {
     if (nblk) hipLaunchKernelGGL(k_fqz_entropy, dim3(nblk), dim3(256), 0, s, j, partial);
     return hipGetLastError();

@@ -2,6 +2,7 @@
 // GPU, behind fqz5_seq_encode / fqz5_seq_decode: the drop-ins of fqzcomp5.c's
 // encode_seq (:1073-1270) and decode_seq (:1272-1406), same arguments, same
 // bytes, same NULL cases (include/fqz5_mi355x.h).
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -47,12 +48,21 @@ bool seq_class_uc(uint8_t c) { return c == 'A' || c == 'C' || c == 'G' || c == '
 
 }  // namespace
 
-// One block: events, context and side models, then the range coder back end.
-// Returns the device output and its size.
-static uint8_t *seq_encode_dev(GpuCtx &g, const uint8_t *d_in, uint32_t n,
-                               const std::vector<uint32_t> &seg, int both, int k,
-                               uint32_t *out_len) {
+struct SeqWork {
     SeqJob J{};
+    FqzEvJob E{};
+    uint32_t nev = 0;
+    uint64_t lb = 0;                    // output bytes >= lb
+    uint32_t clen = 0;
+    bool ready = false;                 // events built (records did not run out)
+};
+
+// One block: events, context and side models; the coder records J.rec in
+// stream order and the entropy partial sums into `part` (EB doubles).
+static void seq_prepare_dev(GpuCtx &g, SeqWork &W, const uint8_t *d_in, uint32_t n,
+                            const std::vector<uint32_t> &seg, int both, int k, double *part,
+                            uint32_t EB) {
+    SeqJob &J = W.J;
     J.in = d_in;
     J.n = n;
     J.k = uint32_t(k);
@@ -110,35 +120,75 @@ static uint8_t *seq_encode_dev(GpuCtx &g, const uint8_t *d_in, uint32_t n,
     J.rec = g.arena.alloc_n<uint4>(nev ? nev : 1);
     FQZ5_HIP(launch_seq_model(J, g.stream));
     FQZ5_HIP(launch_seq_side(J, g.stream));
-
-    FqzEvJob E{};
-    E.nev = nev;
-    E.rec = J.rec;
-    // each event shifts the coder at most twice (range >= 2^24 / 65519 >= 256 after it)
-    uint8_t *out = g.arena.alloc_n<uint8_t>(2 * size_t(nev) + 16);
-    E.out = out;
-    E.out_len = g.arena.alloc_n<uint32_t>(1);
-    std::vector<FqzEvJob *> js{&E};
-    rc_backend(g, js);
-    g.download(out_len, E.out_len, 1);
-    g.sync();
-    return out;
+    FQZ5_HIP(launch_rec_entropy(J.rec, nev, part, EB, g.stream));
+    W.nev = nev;
 }
 
-void seq_encode_batch(GpuCtx &g, std::vector<SeqEncReq> &reqs) {
-    for (SeqEncReq &R : reqs) {
+void seq_encode_prepare(GpuCtx &g, std::vector<SeqEncReq> &reqs) {
+    constexpr uint32_t EB = 256;
+    double *part = g.arena.alloc_n<double>(size_t(EB) * std::max<size_t>(reqs.size(), 1));
+    g.memset0(part, size_t(EB) * std::max<size_t>(reqs.size(), 1) * sizeof(double));
+    for (size_t i = 0; i < reqs.size(); i++) {
+        SeqEncReq &R = reqs[i];
         R.ok = false;
         R.out.clear();
+        R.w = std::make_shared<SeqWork>();
         if (R.k < 1 || R.k > int(SEQ_K_MAX)) throw GpuError("seq: context size out of range (1..14)");
         std::vector<uint32_t> seg;
         if (!R.lens || !seq_segments(R.lens, R.nrec, R.n, seg)) continue;
-        uint32_t len = 0;
-        Piece p;
-        p.dev = seq_encode_dev(g, R.d_in, R.n, seg, R.both, R.k, &len);
-        p.len = len;
-        R.out.push_back(p);
-        R.ok = true;
+        seq_prepare_dev(g, *R.w, R.d_in, R.n, seg, R.both, R.k, part + i * EB, EB);
+        R.w->ready = true;
     }
+    std::vector<double> hp(size_t(EB) * reqs.size());
+    g.download(hp.data(), part, hp.size());
+    g.sync();
+    for (size_t i = 0; i < reqs.size(); i++) {
+        SeqWork &W = *reqs[i].w;
+        if (!W.ready) continue;
+        double bits = 0;
+        for (uint32_t b = 0; b < EB; b++) bits += hp[i * EB + b];
+        // 8 P >= bits - 8, with a margin for the sums
+        bits = bits * (1.0 - 1e-9) - 8.0 - 64.0;
+        W.lb = bits > 0 ? uint64_t(bits / 8.0) : 0;
+    }
+}
+
+void seq_encode_finish(GpuCtx &g, std::vector<SeqEncReq> &reqs, const std::vector<char> *skip) {
+    std::vector<FqzEvJob *> js;
+    std::vector<SeqEncReq *> run;
+    for (size_t i = 0; i < reqs.size(); i++) {
+        SeqEncReq &R = reqs[i];
+        if (!R.w || !R.w->ready || (skip && (*skip)[i])) continue;
+        SeqWork &W = *R.w;
+        W.E = FqzEvJob{};
+        W.E.nev = W.nev;
+        W.E.rec = W.J.rec;
+        // each event shifts the coder at most twice (range >= 2^24 / 65519 >= 256 after it)
+        W.E.out = g.arena.alloc_n<uint8_t>(2 * size_t(W.nev) + 16);
+        W.E.out_len = g.arena.alloc_n<uint32_t>(1);
+        js.push_back(&W.E);
+        run.push_back(&R);
+    }
+    rc_backend(g, js);
+    for (SeqEncReq *R : run) g.download(&R->w->clen, R->w->E.out_len, 1);
+    g.sync();
+    for (SeqEncReq *R : run) {
+        SeqWork &W = *R->w;
+        if (W.lb > W.clen)   // the entropy bound is a theorem
+            throw GpuError("seq: size below its entropy bound");
+        Piece p;
+        p.dev = W.E.out;
+        p.len = W.clen;
+        R->out.push_back(p);
+        R->ok = true;
+    }
+}
+
+uint64_t seq_size_lower_bound(const SeqEncReq &r) { return r.w && r.w->ready ? r.w->lb : 0; }
+
+void seq_encode_batch(GpuCtx &g, std::vector<SeqEncReq> &reqs) {
+    seq_encode_prepare(g, reqs);
+    seq_encode_finish(g, reqs, nullptr);
 }
 
 void seq_decode_batch(GpuCtx &g, std::vector<SeqDecReq> &reqs) {
@@ -193,9 +243,17 @@ char *fqz5_seq_encode(unsigned char *in, unsigned int in_size, unsigned int *len
         if (!seq_segments(len, nrecords, in_size, seg)) return nullptr;
         GpuCtx &g = gpu();
         gp = &g;
-        const uint8_t *d_in = g.upload(in, in_size);
-        uint32_t n_out = 0;
-        uint8_t *d_out = seq_encode_dev(g, d_in, in_size, seg, both_strands, ctx_size, &n_out);
+        std::vector<SeqEncReq> rq(1);
+        rq[0].d_in = g.upload(in, in_size);
+        rq[0].n = in_size;
+        rq[0].lens = len;
+        rq[0].nrec = nrecords;
+        rq[0].both = both_strands;
+        rq[0].k = ctx_size;
+        seq_encode_batch(g, rq);
+        if (!rq[0].ok) { g.reset(); return nullptr; }
+        const uint32_t n_out = rq[0].out[0].len;
+        const uint8_t *d_out = rq[0].out[0].dev;
         char *out = static_cast<char *>(std::malloc(n_out ? n_out : 1));
         if (!out) throw GpuError("fqz5_seq_encode: out of host memory");
         g.download(reinterpret_cast<uint8_t *>(out), d_out, n_out);

@@ -2,6 +2,7 @@
 // fqzcomp5.c:1073-1406) on device-resident blocks (seq_codec.cpp), for the
 // section coder (block.cpp) and fqz5_seq_encode / fqz5_seq_decode.
 #pragma once
+#include <memory>
 #include <vector>
 
 #include "gpu_ctx.hpp"
@@ -18,8 +19,15 @@ struct SeqEncReq {
     // results
     bool ok = false;                    // false: the records run out (encode_seq's NULL)
     Layout out;                         // the coder bytes (device)
+    std::shared_ptr<struct SeqWork> w;  // between prepare and finish
 };
-// one block after another (every phase is a parallel kernel)
+// prepare: every block's events and model pass (one block after another,
+// every phase a parallel kernel) and its size lower bound; finish: the range
+// chains of the requests not in `skip` in one launch, and their bytes.
+void seq_encode_prepare(GpuCtx &g, std::vector<SeqEncReq> &reqs);
+void seq_encode_finish(GpuCtx &g, std::vector<SeqEncReq> &reqs, const std::vector<char> *skip);
+// Output size lower bound after prepare (entropy of the events), 0 if none.
+uint64_t seq_size_lower_bound(const SeqEncReq &r);
 void seq_encode_batch(GpuCtx &g, std::vector<SeqEncReq> &reqs);
 
 struct SeqDecReq {

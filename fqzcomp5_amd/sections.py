@@ -272,9 +272,10 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
     the schedule names (trial and re-trial blocks) and encodes the others
     once at commit, for candidates that do cost in proportion to their work.
 
-    prune: fqz candidates that provably cannot win the trial skip their range
-    chain (fqz5_set_trial_prune), when this rank holds every section the
-    schedule has try fqz and they form one whole trial window."""
+    prune: fqz and sequence-model candidates that provably cannot win the
+    trial skip their range chain (fqz5_set_trial_prune), when this rank holds
+    every section the schedule has try them and they form one whole trial
+    window per family."""
     ins = np.array([s.in_size for s in secs], np.uint32)
     ids = np.array([s.sec for s in secs], np.int32)
     av = np.asarray(avail, np.uint32)
@@ -290,9 +291,13 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
         # launch); fqz candidates cost in proportion to their work, so only
         # the scheduled trial sections try them
         masks = (av[ids] & RANS_MASK) | (sched & WORK_MASK) if speculate else sched
-        rows = np.nonzero(sched_all & FQZ_MASK)[0]
-        prune = prune and speculate and len(rows) == TRIAL_WINDOW and \
-            bool(((rows >= off) & (rows < off + len(secs))).all())
+        # pruning needs each family's trial window whole on this rank
+        for fam in (FQZ_MASK, SEQ_MASK):
+            rows = np.nonzero(sched_all & fam)[0]
+            if len(rows) == 0:
+                continue
+            prune = prune and speculate and len(rows) == TRIAL_WINDOW and \
+                bool(((rows >= off) & (rows < off + len(secs))).all())
     so = _load()
     prev = so.fqz5_set_trial_prune(1 if prune else 0)
     try:

@@ -159,6 +159,46 @@ class _Codec:
         return self._take(p, n.value)
 
 
+    # ---- LZP (lzp16e.c) and LZP3 (fqzcomp5.c:2013-2021, :2431-2445) -------
+    def _lzp_fns(self):
+        if getattr(self, "_lz", None) is None:
+            p = self._prefix
+            f = getattr(self.lib, p + "lzp")
+            f.restype = C.c_int
+            f.argtypes = [C.c_char_p, C.c_int, C.c_void_p]
+            g = getattr(self.lib, p + "unlzp")
+            g.restype = C.c_int
+            # the reference's unlzp has no capacity argument (extra args are
+            # harmless under the C calling convention)
+            g.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_int]
+            self._lz = (f, g)
+        return self._lz
+
+    def lzp(self, data: bytes) -> bytes:
+        f, _ = self._lzp_fns()
+        buf = C.create_string_buffer(3 * len(data) + 1000)
+        n = f(bytes(data), len(data), buf)
+        if n < 0:
+            raise RuntimeError("lzp failed")
+        return buf.raw[:n]
+
+    def unlzp(self, data: bytes, out_size: int) -> bytes:
+        """unlzp into a buffer of out_size bytes (the reference writes past
+        it on a stream that decodes longer: size it generously there)."""
+        _, g = self._lzp_fns()
+        buf = C.create_string_buffer(max(out_size, 1))
+        n = g(bytes(data), len(data), buf, out_size)
+        if n < 0:
+            raise RuntimeError("unlzp failed")
+        return buf.raw[:n]
+
+    def lzp3_compress(self, data: bytes) -> bytes:
+        return self.rans_compress(self.lzp(data), 5)
+
+    def lzp3_uncompress(self, comp: bytes, u_len: int) -> bytes:
+        return self.unlzp(self.rans_uncompress(comp), u_len)
+
+
 _cache: dict = {}
 
 

@@ -49,4 +49,10 @@ uint8_t *ora_seq_encode(const uint8_t *in, uint32_t n, const uint32_t *len, int 
                         int both, int k, uint32_t *out_size);
 uint8_t *ora_seq_decode(const uint8_t *in, uint32_t in_size, const uint32_t *len, int nrec,
                         int both, int k, uint32_t out_size);
+/* LZP pre-pass and the LZP3 sequence method (lzp16e.c, fqzcomp5.c:2013-2021) */
+int ora_lzp(const uint8_t *in, int in_len, uint8_t *out);
+int ora_unlzp(const uint8_t *in, int in_len, uint8_t *out, int out_cap);
+uint8_t *ora_lzp3_compress(uint8_t *in, unsigned int in_size, unsigned int *out_size);
+uint8_t *ora_lzp3_uncompress(uint8_t *in, unsigned int in_size, unsigned int u_len,
+                             unsigned int *out_size);
 #endif
