@@ -25,6 +25,7 @@
 #include "rans_codec.hpp"
 #include "fqz_codec.hpp"
 #include "seq_codec.hpp"
+#include "lzp_codec.hpp"
 #include "rans_format.hpp"
 
 namespace fqz5 {
@@ -210,6 +211,29 @@ std::vector<char> prune_plan(const std::vector<CompressReq> &reqs,
     return skip;
 }
 
+// LZP3 candidates of sections `which`: their lzp output (device, this
+// context's arena) joins `reqs` as an order-5 rANS request; of[i][LZP3]
+// gets its index.
+void add_lzp3(GpuCtx &g, const fqz5_section *secs, const std::vector<int> &which,
+              std::vector<CompressReq> &reqs, std::vector<std::vector<int>> &of) {
+    if (which.empty()) return;
+    std::vector<LzpEncReq> lz(which.size());
+    for (size_t k = 0; k < which.size(); k++) {
+        lz[k].d_in = secs[which[k]].in;
+        lz[k].n = secs[which[k]].in_size;
+    }
+    lzp_encode_batch(g, lz);
+    for (size_t k = 0; k < which.size(); k++) {
+        CompressReq r;
+        r.d_in = lz[k].d_out;
+        r.n = lz[k].out_len;
+        r.order = 5;
+        r.cap = compress_bound(r.n, r.order);
+        of[size_t(which[k])][LZP3] = int(reqs.size());
+        reqs.push_back(std::move(r));
+    }
+}
+
 }  // namespace fqz5
 
 using namespace fqz5;
@@ -268,8 +292,8 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         }
         t_sess = TrySession();
         for (int i = 0; i < nsec; i++) {
-            if (masks[i] & ~(RANS_MASK | FQZ_MASK | SEQ_MASK))
-                throw GpuError("fqz5_sections_try: method mask has LZP/tok3/SEQ_CUSTOM methods "
+            if (masks[i] & ~(RANS_MASK | FQZ_MASK | SEQ_MASK | (1u << LZP3)))
+                throw GpuError("fqz5_sections_try: method mask has name or SEQ_CUSTOM methods "
                                "(not in this build)");
             if ((masks[i] & SEQ_MASK) && (secs[i].sec != FQZ5_SEC_SEQ || !secs[i].rec_len))
                 throw GpuError("fqz5_sections_try: SEQ methods need a sequence section with records");
@@ -280,6 +304,7 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         t_sess.req_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
         t_sess.fqz_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
         t_sess.seq_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
+        std::vector<int> lzp_sec;                         // sections trying LZP3
         for (int i = 0; i < nsec; i++) {
             const fqz5_section &S = secs[i];
             for (int m = 1; m < FQZ5_M_LAST; m++) {
@@ -295,6 +320,10 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                     continue;
                 }
                 if (m == RANSXN1 && !S.fixed_len) continue;   // out = NULL (:2004-2007)
+                if (m == LZP3) {                               // after the lzp pass, below
+                    lzp_sec.push_back(i);
+                    continue;
+                }
                 CompressReq r;
                 r.d_in = S.in;
                 r.n = S.in_size;
@@ -304,6 +333,9 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 reqs.push_back(std::move(r));
             }
         }
+        // LZP3 (fqzcomp5.c:2013-2021): the lzp pass, then rANS order 5 of its
+        // output as one more request of the batch
+        add_lzp3(g, secs, lzp_sec, reqs, t_sess.req_of);
         // The fqz and sequence-model candidates (trial blocks) run on the
         // thread's second context from a helper thread, beside the rANS
         // candidates: both are a few long chains that leave most of the GPU
@@ -439,6 +471,8 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         std::vector<int> late_of(nsec, -1), late_fqz_of(nsec, -1), late_seq_of(nsec, -1);
         std::vector<FqzEncReq> late_fqz;
         std::vector<SeqEncReq> late_seq;
+        std::vector<int> late_lzp;
+        std::vector<std::vector<int>> late_lzp_of(nsec, std::vector<int>(FQZ5_M_LAST, -1));
         for (int i = 0; i < nsec; i++) {
             const int m = methods[i];
             if (m <= 0 || m >= FQZ5_M_LAST || t_sess.req_of[i][m] >= 0 || t_sess.fqz_of[i][m] >= 0 ||
@@ -454,6 +488,10 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
                 late_fqz.push_back(fqz_req(secs[i], m, t_sess.recs));
                 continue;
             }
+            if (m == LZP3 && secs[i].sec == FQZ5_SEC_SEQ) {
+                late_lzp.push_back(i);
+                continue;
+            }
             if (!(RANS_MASK & (1u << m)) || (m == RANSXN1 && !secs[i].fixed_len)) continue;
             CompressReq r;
             r.d_in = secs[i].in;
@@ -463,6 +501,8 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             late_of[i] = int(late.size());
             late.push_back(std::move(r));
         }
+        add_lzp3(g, secs, late_lzp, late, late_lzp_of);
+        for (int i : late_lzp) late_of[i] = late_lzp_of[size_t(i)][LZP3];
         if (!late.empty()) compress_batch(g, late);
         if (!late_fqz.empty()) fqz_encode_batch(g, late_fqz);
         if (!late_seq.empty()) seq_encode_batch(g, late_seq);
@@ -484,7 +524,8 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             if (si >= 0 && t_sess.seq[size_t(si)].ok) lay = &t_sess.seq[size_t(si)].out;
             if (late_seq_of[i] >= 0 && late_seq[late_seq_of[i]].ok) lay = &late_seq[late_seq_of[i]].out;
             R.method = m;
-            R.strat = is_fqz(m) ? 1 : is_seqcm(m) ? seq_strat(m) : 0;   // compress_with_methods' *strat
+            // compress_with_methods' *strat (fqzcomp5.c:1994-2069)
+            R.strat = is_fqz(m) ? 1 : is_seqcm(m) ? seq_strat(m) : m == LZP3 ? LZP3 : 0;
             R.status = -1;
             R.clen = 0;
             R.usize = S.in_size;
@@ -558,6 +599,9 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         std::vector<FqzDecReq> fqz;
         std::vector<SeqDecReq> seqd;
         std::vector<int> who, who_fqz, who_seq;
+        std::vector<LzpDecReq> lzd;
+        std::vector<int> who_lzp;                     // section of each lzd entry
+        std::vector<size_t> lzp_rans;                 // its rANS stage in reqs
         off = 0;
         for (int i = 0; i < nsec; i++) {
             const uint8_t *h = host + off;
@@ -598,6 +642,27 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
                 who_seq.push_back(i);
                 continue;
             }
+            if (h[0] == LZP3 && secs[i].sec == FQZ5_SEC_SEQ) {   // rANS, then unlzp (:2431-2445)
+                const uint8_t *hs = h + 9;
+                uint32_t rsz = 0;
+                if (clen < 2 || (hs[0] & ORD_NOSZ) || !varint_get(hs + 1, hs + clen, &rsz)) continue;
+                DecompressReq r;
+                r.h_in = hs;
+                r.d_in = secs[i].in + 9;
+                r.in_size = clen;
+                r.out_cap = rsz;
+                r.d_out = g.arena.alloc_n<uint8_t>(size_t(rsz) + 1);
+                LzpDecReq z;
+                z.d_in = r.d_out;
+                z.d_out = secs[i].out;
+                z.cap = ulen;
+                lzp_rans.push_back(reqs.size());
+                reqs.push_back(r);
+                who.push_back(-1);
+                lzd.push_back(z);
+                who_lzp.push_back(i);
+                continue;
+            }
             if (h[0] != 0) continue;
             DecompressReq r;
             r.h_in = h + 9;
@@ -614,11 +679,29 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             std::fprintf(stderr, "decode_sections: %zu bytes to host in %.1f ms, rANS %.1f ms\n", tot,
                          std::chrono::duration<double, std::milli>(t1 - t0).count(),
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
+        if (!lzd.empty()) {
+            std::vector<LzpDecReq> run;
+            std::vector<int> run_who;
+            for (size_t k = 0; k < lzd.size(); k++) {
+                const DecompressReq &r = reqs[lzp_rans[k]];
+                if (!r.ok) continue;
+                lzd[k].in_len = r.out_size;
+                run.push_back(lzd[k]);
+                run_who.push_back(who_lzp[k]);
+            }
+            lzp_decode_batch(g, run);
+            for (size_t k = 0; k < run.size(); k++) {
+                fqz5_section_result &R = res[run_who[k]];
+                R.status = run[k].ok ? 0 : -1;
+                R.usize = run[k].out_len;
+            }
+        }
         if (!seqd.empty()) seq_decode_batch(g, seqd);
         // after the rANS and sequence sections: a quality section's sequence context may
         // be the output of this call's sequence section
         if (!fqz.empty()) fqz_decode_batch(g, fqz);
         for (size_t k = 0; k < reqs.size(); k++) {
+            if (who[k] < 0) continue;                   // an LZP3 section's rANS stage
             fqz5_section_result &R = res[who[k]];
             R.status = reqs[k].ok ? 0 : -1;
             R.usize = reqs[k].out_size;

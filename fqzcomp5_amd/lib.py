@@ -324,6 +324,29 @@ def seq_decode(comp: bytes, lens, both: int, k: int, out_size: int) -> bytes:
     return out
 
 
+def lzp(data: bytes) -> bytes:
+    """fqz5_lzp (lzp16e.c:113 lzp) on the GPU."""
+    so = load()
+    so.fqz5_lzp.restype = C.c_int
+    so.fqz5_lzp.argtypes = [C.c_char_p, C.c_int, C.c_void_p]
+    buf = C.create_string_buffer(3 * len(data) + 16)
+    n = so.fqz5_lzp(bytes(data), len(data), buf)
+    if n < 0:
+        raise NativeError("fqz5_lzp failed: " + last_error())
+    return buf.raw[:n]
+
+
+def unlzp(data: bytes, out_cap: int) -> bytes | None:
+    """fqz5_unlzp (lzp16e.c:166 unlzp) on the GPU; None if the stream is
+    damaged or decodes to more than out_cap bytes."""
+    so = load()
+    so.fqz5_unlzp.restype = C.c_int
+    so.fqz5_unlzp.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_int]
+    buf = C.create_string_buffer(max(out_cap, 1))
+    n = so.fqz5_unlzp(bytes(data), len(data), buf, out_cap)
+    return None if n < 0 else buf.raw[:n]
+
+
 def crc32(data: bytes, crc: int = 0) -> int:
     """zlib.crc32 computed on the GPU (fqz5_crc32, host buffer)."""
     return int(load().fqz5_crc32(crc, bytes(data), len(data)))

@@ -33,7 +33,7 @@ FQZ_MASK = sum(1 << m for m in range(FQZ0, FQZ4 + 1))
 SEQ_MASK = sum(1 << m for m in range(SEQ10, SEQ14B + 1))
 # candidates whose cost grows with their work: tried only where the trial
 # schedule names them (see encode_run)
-WORK_MASK = FQZ_MASK | SEQ_MASK
+WORK_MASK = FQZ_MASK | SEQ_MASK | (1 << LZP3)
 
 # Method masks of the level presets for the sequence and quality sections
 # (fqzcomp5.c:4886-4932; the names masks belong to SURVEY §8 f1) and their
@@ -57,9 +57,9 @@ BLOCK_SIZE = {1: 10_000_000, 3: 100_000_000, 5: 100_000_000, 7: 500_000_000,
 # encode_seq's (k, both strands) per method (fqzcomp5.c:2047-2062)
 SEQ_PARAMS = {SEQ10: (10, 0), SEQ12: (12, 0), SEQ12B: (12, 1), SEQ13B: (13, 1),
               SEQ14B: (14, 1)}
-# methods this build codes (every rANS / fqz / sequence-CM method; LZP3 is
-# not built yet)
-BUILT = set(range(RANS0, RANSXN1 + 1)) | set(SEQ_PARAMS) | set(range(FQZ0, FQZ4 + 1))
+# methods this build codes: every sequence and quality method of the presets
+# (rANS, LZP3, the sequence context models, fqz)
+BUILT = set(range(RANS0, LZP3 + 1)) | set(SEQ_PARAMS) | set(range(FQZ0, FQZ4 + 1))
 
 
 def preset_methods(level: int) -> list[int]:

@@ -200,6 +200,21 @@ void *fqz5_stream(void);
 /* 1 if a HIP device is usable, else 0 (and fqz5_last_error() is set). */
 int fqz5_device_ok(void);
 
+/* LZP pre-pass of fqzcomp5's LZP3 sequence method and of its LZP name
+ * coding, on the GPU.
+ *   fqz5_lzp   replaces lzp()   (lzp16e.h; lzp16e.c:113): same bytes, returns
+ *              the output length (-1 on a device error).  `out` needs room for
+ *              3 bytes per input byte in the worst case (escaped markers); the
+ *              reference's callers allocate 2 * in_len + 1000, which the
+ *              output of their inputs fits.
+ *   fqz5_unlzp replaces unlzp() (lzp16e.c:166) with the output capacity the
+ *              call sites know (fqzcomp5.c:2444 u_len, :1602 and :1667 the
+ *              names buffers): returns the output length, or -1 if the
+ *              stream is damaged or would write past out_cap (the reference
+ *              would write past its buffer). */
+int fqz5_lzp(unsigned char *in, int in_len, unsigned char *out);
+int fqz5_unlzp(unsigned char *in, int in_len, unsigned char *out, int out_cap);
+
 /* Last error message of the calling thread ("" if none). */
 const char *fqz5_last_error(void);
 

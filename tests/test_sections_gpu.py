@@ -57,6 +57,9 @@ def test_run_vs_reference(level, kind, nreads, blk, cm):
             sc = binding.seq_ref() if binding.have_seq_ref() else binding.seq_oracle()
             exp = sc.encode(data, [int(x) for x in reads.lens[a:b]], both, k_)
             assert r.strat == (k_ << 4) | (both << 3) | 1
+        elif m == S.LZP3:
+            exp = codec.lzp3_compress(data)
+            assert r.strat == S.LZP3
         else:
             exp = codec.rans_compress(data, _order(m, fl))
             assert r.strat == 0
