@@ -122,6 +122,7 @@ struct TrySession {
     std::vector<std::vector<int>> seq_of;
     std::deque<std::vector<uint32_t>> recs;       // their (rewritable) lengths / flags
     bool open = false;
+    bool aux = false;                             // candidates live in the helper contexts
 };
 
 // fqz_compress(4, slice, in, size, &len, m - FQZ0, NULL) for a section
@@ -288,7 +289,7 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         GpuCtx &g = gpu();
         if (t_sess.open) {
             g.reset();
-            gpu_aux().reset();
+            gpu_aux_reset_all();
         }
         t_sess = TrySession();
         for (int i = 0; i < nsec; i++) {
@@ -333,43 +334,57 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 reqs.push_back(std::move(r));
             }
         }
-        // LZP3 (fqzcomp5.c:2013-2021): the lzp pass, then rANS order 5 of its
-        // output as one more request of the batch
-        add_lzp3(g, secs, lzp_sec, reqs, t_sess.req_of);
-        // The fqz and sequence-model candidates (trial blocks) run on the
-        // thread's second context from a helper thread, beside the rANS
-        // candidates: both are a few long chains that leave most of the GPU
-        // idle.  Their model passes come first; then the candidates that
-        // provably lose the trial are pruned; then the range chains.
+        // The candidates whose cost grows with their work (trial blocks only)
+        // run on the thread's helper contexts from helper threads, beside the
+        // rANS candidates (a few long chains that leave most of the GPU
+        // idle): LZP3 (the lzp pass, then rANS order 5 of its output,
+        // fqzcomp5.c:2013-2021), the fqz and the sequence-model model passes.
+        // Then the fqz / sequence-model candidates that provably lose the
+        // trial are pruned, and the others' range chains run.
         static const bool no_aux = std::getenv("FQZ5_NO_AUX") != nullptr;
         std::vector<FqzEncReq> &fq = t_sess.fqz;
         std::vector<SeqEncReq> &sq = t_sess.seq;
-        if ((!fq.empty() || !sq.empty()) && !no_aux) {
-            GpuCtx &ga = gpu_aux();
-            std::exception_ptr err;
-            std::thread th([&ga, &fq, &sq, &err] {
-                try {
-                    FQZ5_HIP(hipSetDevice(ga.device));
-                    if (!fq.empty()) fqz_encode_prepare(ga, fq);
-                    if (!sq.empty()) seq_encode_prepare(ga, sq);
-                } catch (...) {
-                    err = std::current_exception();
-                }
-            });
+        if ((!fq.empty() || !sq.empty() || !lzp_sec.empty()) && !no_aux) {
+            t_sess.aux = true;
+            GpuCtx &ga = gpu_aux(0), &gb = gpu_aux(1), &gc = gpu_aux(2);
+            std::vector<CompressReq> lzr;
+            std::vector<std::vector<int>> lzr_of(size_t(nsec), std::vector<int>(FQZ5_M_LAST, -1));
+            std::exception_ptr err[3];
+            auto on = [](GpuCtx &c, std::exception_ptr &e, auto &&fn) {
+                return std::thread([&c, &e, fn] {
+                    try {
+                        FQZ5_HIP(hipSetDevice(c.device));
+                        fn();
+                    } catch (...) {
+                        e = std::current_exception();
+                    }
+                });
+            };
+            std::thread th[3] = {
+                on(gc, err[0], [&] {
+                    add_lzp3(gc, secs, lzp_sec, lzr, lzr_of);
+                    if (!lzr.empty()) compress_batch(gc, lzr);
+                }),
+                on(ga, err[1], [&] { if (!fq.empty()) fqz_encode_prepare(ga, fq); }),
+                on(gb, err[2], [&] { if (!sq.empty()) seq_encode_prepare(gb, sq); })};
             double tc = 0;
-            if (step_trace()) std::fprintf(stderr, "sections_try: before compress %.1f ms\n", now_ms() - t0);
             try {
                 compress_batch(g, reqs);
                 tc = step_trace() ? now_ms() : 0;
             } catch (...) {
-                th.join();
+                for (auto &t : th) t.join();
                 throw;
             }
-            th.join();
+            for (auto &t : th) t.join();
             if (step_trace())
-                std::fprintf(stderr, "sections_try: rANS candidates %.1f ms, model passes waited "
+                std::fprintf(stderr, "sections_try: rANS candidates %.1f ms, helpers waited "
                              "%.1f ms more\n", tc - t0, now_ms() - tc);
-            if (err) std::rethrow_exception(err);
+            for (auto &e : err)
+                if (e) std::rethrow_exception(e);
+            for (int i : lzp_sec) {                     // the LZP3 streams join the batch
+                t_sess.req_of[size_t(i)][LZP3] = int(reqs.size());
+                reqs.push_back(std::move(lzr[size_t(lzr_of[size_t(i)][LZP3])]));
+            }
             std::vector<char> skip_f(fq.size(), 0), skip_s(sq.size(), 0);
             if (g_prune.load()) {
                 skip_f = prune_plan(reqs, t_sess.fqz_of, FQZ0, FQZ4, fq.size(),
@@ -377,8 +392,17 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 skip_s = prune_plan(reqs, t_sess.seq_of, SEQ10, SEQ14B, sq.size(),
                                     [&](size_t k) { return seq_size_lower_bound(sq[k]); });
             }
-            if (!fq.empty()) fqz_encode_finish(ga, fq, &skip_f);
-            if (!sq.empty()) seq_encode_finish(ga, sq, &skip_s);
+            std::exception_ptr ferr;
+            std::thread tf = on(ga, ferr, [&] { if (!fq.empty()) fqz_encode_finish(ga, fq, &skip_f); });
+            try {
+                FQZ5_HIP(hipSetDevice(gb.device));
+                if (!sq.empty()) seq_encode_finish(gb, sq, &skip_s);
+            } catch (...) {
+                tf.join();
+                throw;
+            }
+            tf.join();
+            if (ferr) std::rethrow_exception(ferr);
             for (size_t k = 0; k < fq.size(); k++)
                 t_sess.fqz_lb.push_back(skip_f[k] ? fqz_size_lower_bound(fq[k]) : 0);
             for (size_t k = 0; k < sq.size(); k++)
@@ -387,6 +411,7 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             for (char c : skip_f) g_fqz_pruned += c ? 1 : 0;
             for (char c : skip_s) g_fqz_pruned += c ? 1 : 0;
         } else {
+            add_lzp3(g, secs, lzp_sec, reqs, t_sess.req_of);
             compress_batch(g, reqs);
             if (!fq.empty()) fqz_encode_batch(g, fq);
             if (!sq.empty()) seq_encode_batch(g, sq);
@@ -421,7 +446,7 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         fqz5_set_error(e.what());
         t_sess = TrySession();
         try { gpu().reset(); } catch (...) {}
-        try { gpu_aux().reset(); } catch (...) {}
+        try { gpu_aux_reset_all(); } catch (...) {}
         return -1;
     }
 }
@@ -550,7 +575,7 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         g.reset();
         // the fqz candidates of the try live in the aux arena: rewind it too,
         // or every step's trial buffers take fresh chunks (the r01 bench OOM)
-        if (!t_sess.fqz.empty() || !t_sess.seq.empty()) gpu_aux().reset();
+        if (t_sess.aux) gpu_aux_reset_all();
         t_sess = TrySession();
         if (step_trace())
             std::fprintf(stderr, "sections_commit: late encodes %.1f ms, write + sync %.1f ms\n",

@@ -52,16 +52,23 @@ bool hedge_chains() {
     return v != 0;
 }
 
-// The calling thread's second context: its own streams and arenas, for
-// work the thread hands to a helper thread to run beside its own
-// (fqz5_sections_try: fqz candidates beside the rANS candidates).
-static thread_local std::unique_ptr<GpuCtx> g_aux;
-GpuCtx &gpu_aux() {
-    if (!g_aux) g_aux.reset(new GpuCtx());
-    return *g_aux;
+// The calling thread's helper contexts: their own streams and arenas, for
+// work the thread hands to helper threads to run beside its own
+// (fqz5_sections_try: LZP3, fqz and sequence-model candidates beside the
+// rANS candidates).
+static thread_local std::unique_ptr<GpuCtx> g_aux[AUX_CTXS];
+GpuCtx &gpu_aux(int k) {
+    if (!g_aux[k]) g_aux[k].reset(new GpuCtx());
+    return *g_aux[k];
+}
+void gpu_aux_reset_all() {
+    for (auto &a : g_aux)
+        if (a) a->reset();
 }
 static uint64_t arena_bytes() {
-    return (g_ctx ? g_ctx->arena.bytes() : 0) + (g_aux ? g_aux->arena.bytes() : 0);
+    uint64_t t = g_ctx ? g_ctx->arena.bytes() : 0;
+    for (auto &a : g_aux) t += a ? a->arena.bytes() : 0;
+    return t;
 }
 
 // Size a stream decodes to, from its header (needed when the caller did

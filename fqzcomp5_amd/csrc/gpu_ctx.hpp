@@ -269,8 +269,11 @@ inline std::vector<int> hedge_plan(const std::vector<uint64_t> &steps, size_t cu
 
 // The calling thread's context (created on first use).
 GpuCtx &gpu();
-// A second context of the calling thread, for work run by a helper thread
-// concurrently with the thread's own (created on first use).
-GpuCtx &gpu_aux();
+// Helper contexts of the calling thread (k < AUX_CTXS), for work run by
+// helper threads concurrently with the thread's own (created on first use),
+// and a rewind of every one that exists.
+constexpr int AUX_CTXS = 3;
+GpuCtx &gpu_aux(int k = 0);
+void gpu_aux_reset_all();
 
 }  // namespace fqz5
