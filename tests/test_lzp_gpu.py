@@ -66,12 +66,13 @@ def test_unlzp_damaged():
 
 
 def test_lzp3_wins_on_repeated_reads():
-    """Amplicon-like sequences (a few reads repeated): LZP3 wins the -3 trial;
+    """Amplicon sequences (3 reads repeated; with 40 distinct reads the 4-byte
+    LZP contexts mispredict and PACK|O1 wins): LZP3 wins the -3 trial;
     the section coder's stream equals the reference's LZP3 and decodes."""
     rng = np.random.default_rng(3)
     reads = synth.illumina(30000, seed=3)
-    pool = reads.seq[:150 * 40].reshape(40, 150)
-    reads.seq[:] = pool[rng.integers(0, 40, reads.num_records)].reshape(-1)
+    pool = reads.seq[:150 * 3].reshape(3, 150).copy()     # 3 amplicons
+    reads.seq[:] = pool[rng.integers(0, 3, reads.num_records)].reshape(-1)
     blocks = synth.split_blocks(reads, 2_000_000)
     run = S.Run(reads, blocks, torch.device("cuda", 0))
     res, meth_all, sizes, tried, _ = S.encode_run(run.enc_secs(), S.masks(3), S.new_state())
