@@ -346,10 +346,15 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         std::vector<SeqEncReq> &sq = t_sess.seq;
         if ((!fq.empty() || !sq.empty() || !lzp_sec.empty()) && !no_aux) {
             t_sess.aux = true;
-            GpuCtx &ga = gpu_aux(0), &gb = gpu_aux(1), &gc = gpu_aux(2);
+            GpuCtx &ga = gpu_aux(0), &gb = gpu_aux(2), &gc = gpu_aux(1);
+            // sequence-model candidates: one helper context each (their
+            // passes are latency-bound and overlap well), up to AUX_CTXS - 2
+            const size_t nsq = std::min<size_t>(sq.size(), size_t(AUX_CTXS - 2));
+            std::vector<std::vector<SeqEncReq>> sqg(nsq);
+            for (size_t k = 0; k < sq.size(); k++) sqg[k % std::max<size_t>(nsq, 1)].push_back(sq[k]);
             std::vector<CompressReq> lzr;
             std::vector<std::vector<int>> lzr_of(size_t(nsec), std::vector<int>(FQZ5_M_LAST, -1));
-            std::exception_ptr err[3];
+            std::vector<std::exception_ptr> err(2 + nsq);
             auto on = [](GpuCtx &c, std::exception_ptr &e, auto &&fn) {
                 return std::thread([&c, &e, fn] {
                     try {
@@ -360,13 +365,17 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                     }
                 });
             };
-            std::thread th[3] = {
-                on(gc, err[0], [&] {
-                    add_lzp3(gc, secs, lzp_sec, lzr, lzr_of);
-                    if (!lzr.empty()) compress_batch(gc, lzr);
-                }),
-                on(ga, err[1], [&] { if (!fq.empty()) fqz_encode_prepare(ga, fq); }),
-                on(gb, err[2], [&] { if (!sq.empty()) seq_encode_prepare(gb, sq); })};
+            std::vector<std::thread> th;
+            th.push_back(on(gc, err[0], [&] {
+                add_lzp3(gc, secs, lzp_sec, lzr, lzr_of);
+                if (!lzr.empty()) compress_batch(gc, lzr);
+            }));
+            th.push_back(on(ga, err[1], [&] { if (!fq.empty()) fqz_encode_prepare(ga, fq); }));
+            for (size_t k = 0; k < nsq; k++) {
+                GpuCtx &gk = gpu_aux(int(2 + k));
+                std::vector<SeqEncReq> &grp = sqg[k];
+                th.push_back(on(gk, err[2 + k], [&gk, &grp] { seq_encode_prepare(gk, grp); }));
+            }
             double tc = 0;
             try {
                 compress_batch(g, reqs);
@@ -381,6 +390,8 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                              "%.1f ms more\n", tc - t0, now_ms() - tc);
             for (auto &e : err)
                 if (e) std::rethrow_exception(e);
+            for (size_t k = 0; k < sq.size(); k++)          // their work back in request order
+                sq[k] = std::move(sqg[k % std::max<size_t>(nsq, 1)][k / std::max<size_t>(nsq, 1)]);
             for (int i : lzp_sec) {                     // the LZP3 streams join the batch
                 t_sess.req_of[size_t(i)][LZP3] = int(reqs.size());
                 reqs.push_back(std::move(lzr[size_t(lzr_of[size_t(i)][LZP3])]));

@@ -11,7 +11,7 @@ constexpr uint32_t LZP_HASH_BITS = 16;          // lzp16e.c:43-45
 constexpr uint32_t LZP_MIN_LEN = 3;             // lzp16e.c:50-52
 constexpr uint32_t LZP_MARK = 233;              // lzp16e.c:54
 constexpr uint32_t LZP_MAX_LEN = 65535;         // lzp16e.c:121
-constexpr uint32_t LZP_CHUNK = 65536;           // positions per speculative parse chunk
+constexpr uint32_t LZP_CHUNK = 8192;            // positions per speculative parse chunk
 
 // Encoder, one block: every position i gets its hash h_i (a function of the
 // 4 bytes before it), its prediction pred_i (the last j < i with h_j == h_i,

@@ -32,6 +32,7 @@ struct SeqJob {
     uint64_t *val;                      //   (2p + rv) << 8 | symbol
     const uint32_t *skey;               // the same, sorted by context
     const uint64_t *sval;
+    uint32_t *ev;                       // per byte: the event index of its symbol
     uint4 *rec;                         // per coding event: {RN(1/total) (2 words), freq, cum}
 };
 

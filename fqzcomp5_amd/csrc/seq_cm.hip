@@ -132,6 +132,14 @@ DEV uint32_t sym_event(const SeqJob &J, uint32_t p) {
     return p + J.lead + J.run_off[r] + J.cnt[r] - 1u;
 }
 
+// the event index of every byte (coalesced, so that the model pass below
+// does one random read per event instead of four)
+__global__ void k_seq_ev(SeqJob J) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= J.n) return;
+    J.ev[p] = sym_event(J, p);
+}
+
 // one thread per context: the head of its run in the sorted order walks it
 __global__ void k_seq_model(SeqJob J) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -146,7 +154,7 @@ __global__ void k_seq_model(SeqJob J) {
         const uint32_t tot = sm4_total(F);
         if (!(ord & 1u)) {
             const uint32_t p = ord >> 1;
-            J.rec[sym_event(J, p)] = rc_rec((F >> (8u * sym)) & 255u, sm4_cum(F, sym), tot);
+            J.rec[J.ev[p]] = rc_rec((F >> (8u * sym)) & 255u, sm4_cum(F, sym), tot);
         }
         F = sm4_bump(F, sym, tot);
     }
@@ -461,6 +469,7 @@ hipError_t launch_seq_ctx(const SeqJob &j, hipStream_t s) {
 }
 
 hipError_t launch_seq_model(const SeqJob &j, hipStream_t s) {
+    if (j.n) hipLaunchKernelGGL(k_seq_ev, grid_of(j.n), dim3(256), 0, s, j);
     if (j.nkeys) hipLaunchKernelGGL(k_seq_model, grid_of(j.nkeys), dim3(256), 0, s, j);
     return hipGetLastError();
 }

@@ -118,6 +118,7 @@ static void seq_prepare_dev(GpuCtx &g, SeqWork &W, const uint8_t *d_in, uint32_t
         J.sval = sval;
     }
     J.rec = g.arena.alloc_n<uint4>(nev ? nev : 1);
+    J.ev = g.arena.alloc_n<uint32_t>(n ? n : 1);
     FQZ5_HIP(launch_seq_model(J, g.stream));
     FQZ5_HIP(launch_seq_side(J, g.stream));
     FQZ5_HIP(launch_rec_entropy(J.rec, nev, part, EB, g.stream));
