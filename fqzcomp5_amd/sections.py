@@ -331,10 +331,12 @@ class Run:
         offs = np.concatenate([[0], np.cumsum(reads.lens.astype(np.int64))])
         self.seq_d = torch.from_numpy(reads.seq).to(device)
         self.qual_d = torch.from_numpy(reads.qual).to(device)
-        self.spans, self.lens = [], []
+        self.spans, self.lens, self.flags = [], [], []
         for a, b in blocks:
             s, e = int(offs[a]), int(offs[b])
             ln = np.ascontiguousarray(reads.lens[a:b], np.uint32)
+            self.flags.append(None if getattr(reads, "flags", None) is None else
+                              np.ascontiguousarray(reads.flags[a:b], np.uint32))
             fl = int(ln[0]) if len(ln) and bool(np.all(ln == ln[0])) else 0
             self.lens.append(ln)
             self.spans.append((SEC_SEQ, s, e, fl, len(self.lens) - 1))
@@ -361,13 +363,17 @@ class Run:
         ln = self.lens[k]
         return ln.ctypes.data_as(C.POINTER(C.c_uint32)), len(ln)
 
+    def _flags(self, k):
+        f = self.flags[k]
+        return None if f is None else f.ctypes.data_as(C.POINTER(C.c_uint32))
+
     def enc_secs(self) -> list[Section]:
         out = []
         for (sec, s, e, fl, k), (eo, cap) in zip(self.spans, self.enc):
             src = self.seq_d if sec == SEC_SEQ else self.qual_d
             rl, nr = self._rec(k)
             out.append(Section(src.data_ptr() + s, self.enc_buf.data_ptr() + eo, e - s, cap,
-                               fl, sec, rl, None, nr,
+                               fl, sec, rl, self._flags(k), nr,
                                self.seq_d.data_ptr() + s if sec == SEC_QUAL else None))
         return out
 
@@ -378,7 +384,7 @@ class Run:
             rl, nr = self._rec(k)
             seq = self.dec_buf.data_ptr() + self.dec[i - 1] if sec == SEC_QUAL else None
             out.append(Section(self.enc_buf.data_ptr() + eo, self.dec_buf.data_ptr() + do,
-                               9 + r.clen, e - s, 0, sec, rl, None, nr, seq))
+                               9 + r.clen, e - s, 0, sec, rl, self._flags(k), nr, seq))
         return out
 
     def chosen(self, res, i) -> bytes:

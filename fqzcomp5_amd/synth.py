@@ -9,6 +9,14 @@ case is generated here from a seed.  The shapes follow SURVEY.md §8(d) d2:
 * ``q40walk``   : as ``illumina`` but the walk is left un-binned (~40 levels).
 * ``novaseq``   (config C3): qualities i.i.d. from {2,12,23,37} with
   p = {.01,.04,.10,.85}.
+* ``ont``       (config C4): Oxford Nanopore-like long reads: log-normal
+  lengths with N50 ~ 20 kb, homopolymer-rich sequence, qualities Q3..Q30 as
+  an AR(1) walk around a per-read mean near Q12.
+* ``hifi``      (config C5): PacBio HiFi-like pairs, interleaved R1/R2 (names
+  ending /1 and /2, so the second of each pair carries FQZ_FREAD2 by the
+  reference's rule, fqzcomp5.c:518-526); lengths ~ N(15 kb, 3 kb); over half
+  of the qualities are '~' (Q93), so fqz's HiFi table applies
+  (fqzcomp_qual.c:919-938).
 
 Records are returned in the reference's in-memory SoA layout
 (``fastq`` struct, fqzcomp5.c:235-249): concatenated sequence bytes,
@@ -43,6 +51,8 @@ class Reads:
     lens: np.ndarray       # uint32 per record
     names: list | None     # list[bytes] without '@' (name + ' ' + comment)
     name_l: np.ndarray     # int32: kseq name.l (name part before the space)
+    flags: np.ndarray | None = None   # uint32 per record (FQZ_FREAD2), None = all 0
+    comment_l: int = 15    # bytes of ' ' + comment per name (0: no comment)
 
     @property
     def num_records(self) -> int:
@@ -135,9 +145,9 @@ COMMENT = b" 1:N:0:ACGTACGT"      # the comment every synthetic name carries
 
 def fastq_size(r: Reads, a: int = 0, b: int | None = None) -> int:
     """Bytes of the FASTQ text of records [a, b) as to_fastq writes it:
-    '@' name ' ' comment '\\n' seq '\\n' '+\\n' qual '\\n'."""
+    '@' name [' ' comment] '\\n' seq '\\n' '+\\n' qual '\\n'."""
     b = r.num_records if b is None else b
-    return int((r.name_l[a:b].astype(np.int64) + len(COMMENT) + 6).sum()
+    return int((r.name_l[a:b].astype(np.int64) + r.comment_l + 6).sum()
                + 2 * r.lens[a:b].astype(np.int64).sum())
 
 
@@ -164,4 +174,58 @@ def block(r: Reads, a: int, b: int) -> Reads:
     s, e = int(offs[a]), int(offs[b])
     return Reads(r.seq[s:e], r.qual[s:e], r.lens[a:b],
                  r.names[a:b] if r.names is not None else None,
-                 r.name_l[a:b])
+                 r.name_l[a:b], None if r.flags is None else r.flags[a:b], r.comment_l)
+
+
+def _homopolymer_seq(rng: np.random.Generator, n: int) -> np.ndarray:
+    """ACGT with geometric homopolymer runs (mean ~1.8 bases)."""
+    out = np.empty(0, np.uint8)
+    parts, got = [], 0
+    while got < n:
+        m = max(1024, (n - got) // 2 + 64)
+        runs = rng.geometric(0.55, m)
+        step = rng.integers(1, 4, m)                  # next base differs
+        base = np.cumsum(step) % 4
+        parts.append(np.repeat(base.astype(np.uint8), runs))
+        got += int(runs.sum())
+    out = np.concatenate(parts)[:n]
+    return np.frombuffer(b"ACGT", dtype=np.uint8)[out]
+
+
+def ont(n_reads: int, seed: int = 3, with_names: bool = False, median: float = 10500.0,
+        sigma: float = 0.8) -> Reads:
+    rng = np.random.default_rng(seed)
+    lens = np.clip(rng.lognormal(np.log(median), sigma, n_reads), 200, 400000).astype(np.uint32)
+    tot = int(lens.sum())
+    seq = _homopolymer_seq(rng, tot)
+    # qualities: an AR(1) walk (phi 0.8) around a per-read mean near Q12,
+    # clipped to Q3..Q30 (one filter over the whole run of records)
+    from scipy.signal import lfilter
+    mu = np.repeat(np.clip(rng.normal(12.0, 2.5, n_reads), 6, 20), lens)
+    d = lfilter([1.0], [1.0, -0.8], rng.normal(0.0, 2.8, tot))
+    q = np.clip(np.rint(mu + d), 3, 30).astype(np.uint8)
+    ids = rng.integers(0, 1 << 62, (n_reads, 2))
+    names = None
+    if with_names:                                # read ids, no comment
+        names = [b"%016x-%016x" % (int(a), int(b)) for a, b in ids.tolist()]
+    return Reads(seq, q, lens, names, np.full(n_reads, 33, np.int32), None, 0)
+
+
+def hifi(n_pairs: int, seed: int = 5, with_names: bool = False) -> Reads:
+    rng = np.random.default_rng(seed)
+    n = 2 * n_pairs
+    lens = np.clip(np.rint(rng.normal(15000.0, 3000.0, n)), 3000, 40000).astype(np.uint32)
+    tot = int(lens.sum())
+    seq = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, tot, dtype=np.uint8)].copy()
+    q = np.where(rng.random(tot) < 0.62, 93, rng.integers(10, 60, tot)).astype(np.uint8)
+    flags = np.tile(np.array([0, 128], np.uint32), n_pairs)        # FQZ_FREAD2 on /2
+    zmw = np.sort(rng.integers(1, 1 << 24, n_pairs))
+    if with_names:
+        names = [b"m84011_220902_175841_s1/%d/ccs/%d" % (int(z), k)
+                 for z in zmw.tolist() for k in (1, 2)]
+        name_l = np.array([len(nm) for nm in names], dtype=np.int32)
+    else:
+        names = None
+        name_l = np.repeat((len(b"m84011_220902_175841_s1//ccs/1")
+                            + np.floor(np.log10(zmw)).astype(np.int32) + 1), 2).astype(np.int32)
+    return Reads(seq, q, lens, names, name_l, flags, 0)

@@ -26,13 +26,21 @@ def _order(m, fl):
 
 # fqz beats rANS on the random-walk (Illumina) qualities from ~2 MB blocks
 # on; on i.i.d. NovaSeq qualities rANS O0 stays ahead at every size
+GEN = {"illumina": synth.illumina, "novaseq": synth.novaseq, "ont": synth.ont,
+       "hifi": lambda n, seed: synth.hifi(n // 2, seed=seed)}
+
+
+# -7 (ONT) and -9 (HiFi pairs) are BASELINE configs[3]/[4] at small block
+# sizes: every method of their presets (FQZ0..4, SEQ10..14B, RANS64/65/128)
 @pytest.mark.parametrize("level,kind,nreads,blk,cm", [(3, "illumina", 6000, 200_000, False),
                                                       (5, "novaseq", 6000, 200_000, False),
                                                       (5, "illumina", 72000, 4_000_000, False),
-                                                      (5, "novaseq", 6000, 200_000, True)])
+                                                      (5, "novaseq", 6000, 200_000, True),
+                                                      (7, "ont", 500, 1_500_000, True),
+                                                      (9, "hifi", 600, 1_500_000, True)])
 def test_run_vs_reference(level, kind, nreads, blk, cm):
     codec = binding.ref() if binding.have_ref() else binding.oracle()
-    reads = (synth.novaseq if kind == "novaseq" else synth.illumina)(nreads, seed=11)
+    reads = GEN[kind](nreads, seed=11)
     blocks = synth.split_blocks(reads, blk)
     assert len(blocks) >= 5
     run = S.Run(reads, blocks, torch.device("cuda", 0))
@@ -48,12 +56,13 @@ def test_run_vs_reference(level, kind, nreads, blk, cm):
         data = (reads.seq if sec == S.SEC_SEQ else reads.qual)[s:e].tobytes()
         if m >= S.FQZ0:
             a, b = blocks[k]
-            exp = codec.fqz_compress(data, reads.lens[a:b].copy(), np.zeros(b - a, np.uint32),
+            fl_ = np.zeros(b - a, np.uint32) if reads.flags is None else reads.flags[a:b].copy()
+            exp = codec.fqz_compress(data, reads.lens[a:b].copy(), fl_,
                                      m - S.FQZ0, reads.seq[s:e].tobytes())
             assert r.strat == 1
         elif S.SEQ10 <= m <= S.SEQ14B:
             a, b = blocks[k]
-            k_, both = {S.SEQ10: (10, 0), S.SEQ12B: (12, 1)}[m]
+            k_, both = S.SEQ_PARAMS[m]
             sc = binding.seq_ref() if binding.have_seq_ref() else binding.seq_oracle()
             exp = sc.encode(data, [int(x) for x in reads.lens[a:b]], both, k_)
             assert r.strat == (k_ << 4) | (both << 3) | 1
