@@ -54,6 +54,13 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# The library runs the trial's work candidates on helper contexts, each with
+# its own streams, beside the rANS batch; with HIP's default of 4 hardware
+# queues per process those streams share queues and serialise (measured:
+# the -3 encode waited 100 ms per step behind the LZP3 helper's chain).
+# Must be set before anything initialises HIP.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 FASTQ_REC = 358          # bytes of FASTQ text per synthetic 150 bp record (avg)
 BLK = 100_000_000        # -3 / -5 block size (fqzcomp5.c:4896,4904)
@@ -216,6 +223,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
         dist.barrier()
     torch.cuda.synchronize()
     t_enc = t_dec = 0.0
+    enc_steps, dec_steps = [], []
     t0 = time.perf_counter()
     for _ in range(steps):
         a = time.perf_counter()
@@ -224,8 +232,12 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
         b = time.perf_counter()
         dres = decode(res)
         torch.cuda.synchronize()
+        c = time.perf_counter()
         t_enc += b - a
-        t_dec += time.perf_counter() - b
+        t_dec += c - b
+        enc_steps.append(b - a)
+        dec_steps.append(c - b)
+        log(f"[bench] -{level} step: encode {1e3*(b-a):.1f} ms, decode {1e3*(c-b):.1f} ms")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -258,6 +270,9 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
         "section_MBps": round(sec_all * steps / (t_enc + t_dec) / 1e6, 2),
         "enc_ms_per_step": round(t_enc / steps * 1e3, 2),
         "dec_ms_per_step": round(t_dec / steps * 1e3, 2),
+        # rank 0's fastest / slowest step (spread between steps)
+        "enc_ms_min_max": [round(min(enc_steps) * 1e3, 1), round(max(enc_steps) * 1e3, 1)],
+        "dec_ms_min_max": [round(min(dec_steps) * 1e3, 1), round(max(dec_steps) * 1e3, 1)],
         "data": f"synthetic (seeded {kind} 150 bp, {quals}); inputs resident in HBM, "
                 f"no host<->device copies of section bytes in the timed region",
         "config": {"workload": f"fqzcomp5 -{level} seq+qual sections of a "
@@ -451,7 +466,8 @@ def main():
            "scaling": args.scaling, "vs_baseline": None, "dtype": "u8", "data": m["data"],
            "config": m["config"], "enc_MBps": m["enc_MBps"], "dec_MBps": m["dec_MBps"],
            "section_MBps": m["section_MBps"], "enc_ms_per_step": m["enc_ms_per_step"],
-           "dec_ms_per_step": m["dec_ms_per_step"], "roofline": m["roofline"]}
+           "dec_ms_per_step": m["dec_ms_per_step"], "enc_ms_min_max": m["enc_ms_min_max"],
+           "dec_ms_min_max": m["dec_ms_min_max"], "roofline": m["roofline"]}
     if "cpu_baseline" in m:
         out["cpu_baseline"] = m["cpu_baseline"]
     # The metric covers -3 and -5: the default run adds configs[2] (-5,

@@ -18,6 +18,15 @@
 
 namespace fqz5 {
 
+// The trial's helper contexts (gpu_aux) each own streams that must run
+// beside the calling thread's; HIP's default of 4 hardware queues per
+// process makes them share queues and serialise.  Raise it when the process
+// (e.g. the relinked CLI) loads this library before anything touched HIP.
+__attribute__((constructor)) static void hw_queues_default() {
+    const char *v = std::getenv("GPU_MAX_HW_QUEUES");
+    if (!v || std::atoi(v) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+}
+
 static thread_local std::string g_err;
 static thread_local std::unique_ptr<GpuCtx> g_ctx;
 

@@ -14,6 +14,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfqz5_mi355x.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
+# helper contexts' streams need queues of their own (bench.py); effective
+# only when nothing in the process has initialised HIP yet
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
 _libc = C.CDLL(None)
 _libc.free.argtypes = [C.c_void_p]
 

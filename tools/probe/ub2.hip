@@ -10,6 +10,8 @@ typedef __attribute__((address_space(3))) uint64_t lds64_t;
 template <int T>
 __global__ void k(uint32_t *out, uint64_t *cyc, uint32_t a, uint32_t b) {
     __shared__ uint64_t lds[4096];
+    uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds);
+    uint4 *lds128 = reinterpret_cast<uint4 *>(lds);
     const int l = threadIdx.x;
     for (int i = l; i < 4096; i += 64) lds[i] = (uint64_t((i * 40503u) & 4095) << 32) | ((i * 2654435761u) & 4095);
     __syncthreads();
@@ -90,6 +92,23 @@ __global__ void k(uint32_t *out, uint64_t *cyc, uint32_t a, uint32_t b) {
                 const uint32_t xh = x >> 12;
                 x = __umul24(f | 1u, xh) + (sl - st) + 0x8000;
             }
+            if (T == 18) x = lds32[x & 4095];                                   // LDS b32 chain
+            if (T == 19) { const uint4 v = lds128[x & 1023]; x = v.x ^ v.z; }  // LDS b128 chain
+            if (T == 20) {                                                  // renorm select via perm selector
+                const uint64_t m = __ballot(x < y);
+                const uint32_t sel = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0x0c0c0100u >> 0) * 0x0202u;
+                const uint32_t w = __builtin_amdgcn_perm(uint32_t(win >> 32), uint32_t(win), 0x0c0c0100u + sel);
+                x = (x < y) ? ((x << 16) | w) : x + 7;
+            }
+            if (T == 21) x = __umulhi(x, y);                                 // mul_hi chain
+            if (T == 22) {                                                  // enc q via f64
+                const double rd = __longlong_as_double((long long)(uint64_t(b) << 32 | a));
+                x = uint32_t(__fma_rn(double(x), rd, 1.0 / 1048576.0)) + y;
+            }
+            if (T == 23) {                                                  // cmp via VGPR sign, cndmask-free
+                const uint32_t s = ((y - x) >> 27) & 16u;
+                x = (x >> s) + 3;
+            }
             if (T == 10) {                                                  // full renorm select chain
                 const uint64_t m = __ballot(x < y);
                 const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
@@ -111,14 +130,16 @@ int main() {
                            "same + ~68%-taken branch", "renorm select (cmp,mbcnt,lshl,lshr64,perm,cndmask)",
                            "enc step cmp+cndmask", "enc step sign shift", "enc step sub borrow",
                            "fqz range step f64", "fqz range step int magic",
-                           "O0 step LDS lookup + mad", "O0 step register lookup + mad"};
+                           "O0 step LDS lookup + mad", "O0 step register lookup + mad",
+                           "ds_read_b32 chain", "ds_read_b128 chain", "renorm select via perm selector",
+                           "mul_hi chain", "enc q via f64 (cvt,fma,cvt,add)", "sign-shift (sub,lshr,and,lshr,add)"};
 #define RUN(T) hipLaunchKernelGGL(k<T>, dim3(1), dim3(64), 0, 0, out, cyc, 12345u, 99999u);
     for (int rep = 0; rep < 2; rep++) {
-        RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15) RUN(16) RUN(17)
+        RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15) RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23)
     }
     hipDeviceSynchronize();
     uint64_t h[32];
     hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
-    for (int t = 0; t <= 17; t++) printf("T%-2d %-55s %7.1f cyc/step\n", t, names[t], double(h[t]) / N);
+    for (int t = 0; t <= 23; t++) printf("T%-2d %-55s %7.1f cyc/step\n", t, names[t], double(h[t]) / N);
     return 0;
 }
