@@ -59,8 +59,8 @@ sys.path.insert(0, ROOT)
 # queues per process those streams share queues and serialise (measured:
 # the -3 encode waited 100 ms per step behind the LZP3 helper's chain).
 # Must be set before anything initialises HIP.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 FASTQ_REC = 358          # bytes of FASTQ text per synthetic 150 bp record (avg)
 BLK = 100_000_000        # -3 / -5 block size (fqzcomp5.c:4896,4904)

@@ -306,6 +306,8 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         t_sess.fqz_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
         t_sess.seq_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
         std::vector<int> lzp_sec;                         // sections trying LZP3
+        std::vector<CompressReq> sreq;                    // RANSXN1 (stripe) candidates
+        std::vector<int> sreq_sec;
         for (int i = 0; i < nsec; i++) {
             const fqz5_section &S = secs[i];
             for (int m = 1; m < FQZ5_M_LAST; m++) {
@@ -330,6 +332,11 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 r.n = S.in_size;
                 r.order = method_order(m, S.fixed_len);
                 r.cap = compress_bound(r.n, r.order);
+                if (m == RANSXN1) {          // thousands of short stripe chains
+                    sreq_sec.push_back(i);
+                    sreq.push_back(std::move(r));
+                    continue;
+                }
                 t_sess.req_of[i][m] = int(reqs.size());
                 reqs.push_back(std::move(r));
             }
@@ -344,12 +351,19 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         static const bool no_aux = std::getenv("FQZ5_NO_AUX") != nullptr;
         std::vector<FqzEncReq> &fq = t_sess.fqz;
         std::vector<SeqEncReq> &sq = t_sess.seq;
-        if ((!fq.empty() || !sq.empty() || !lzp_sec.empty()) && !no_aux) {
+        auto join_stripes = [&] {          // the stripe candidates join the batch
+            for (size_t k = 0; k < sreq.size(); k++) {
+                t_sess.req_of[size_t(sreq_sec[k])][RANSXN1] = int(reqs.size());
+                reqs.push_back(std::move(sreq[k]));
+            }
+            sreq.clear();
+        };
+        if ((!fq.empty() || !sq.empty() || !lzp_sec.empty() || !sreq.empty()) && !no_aux) {
             t_sess.aux = true;
             GpuCtx &ga = gpu_aux(0), &gb = gpu_aux(2), &gc = gpu_aux(1);
             // sequence-model candidates: one helper context each (their
-            // passes are latency-bound and overlap well), up to AUX_CTXS - 2
-            const size_t nsq = std::min<size_t>(sq.size(), size_t(AUX_CTXS - 2));
+            // passes are latency-bound and overlap well), up to AUX_CTXS - 3
+            const size_t nsq = std::min<size_t>(sq.size(), size_t(AUX_CTXS - 3));
             std::vector<std::vector<SeqEncReq>> sqg(nsq);
             for (size_t k = 0; k < sq.size(); k++) sqg[k % std::max<size_t>(nsq, 1)].push_back(sq[k]);
             std::vector<CompressReq> lzr;
@@ -371,6 +385,14 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 if (!lzr.empty()) compress_batch(gc, lzr);
             }));
             th.push_back(on(ga, err[1], [&] { if (!fq.empty()) fqz_encode_prepare(ga, fq); }));
+            // The RANSXN1 candidates (150 stripes x 4 orders per quality
+            // section: most of a batch's jobs, and most of its host work on
+            // tables) run as their own batch on a helper context, so that
+            // their host work overlaps the long chains of the other rANS
+            // candidates on the GPU.
+            GpuCtx &gs = gpu_aux(AUX_CTXS - 1);
+            std::exception_ptr serr;
+            std::thread ts = on(gs, serr, [&] { if (!sreq.empty()) compress_batch(gs, sreq); });
             for (size_t k = 0; k < nsq; k++) {
                 GpuCtx &gk = gpu_aux(int(2 + k));
                 std::vector<SeqEncReq> &grp = sqg[k];
@@ -382,9 +404,13 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 tc = step_trace() ? now_ms() : 0;
             } catch (...) {
                 for (auto &t : th) t.join();
+                ts.join();
                 throw;
             }
             for (auto &t : th) t.join();
+            ts.join();
+            if (serr) std::rethrow_exception(serr);
+            join_stripes();
             if (step_trace())
                 std::fprintf(stderr, "sections_try: rANS candidates %.1f ms, helpers waited "
                              "%.1f ms more\n", tc - t0, now_ms() - tc);
@@ -422,6 +448,7 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             for (char c : skip_f) g_fqz_pruned += c ? 1 : 0;
             for (char c : skip_s) g_fqz_pruned += c ? 1 : 0;
         } else {
+            join_stripes();
             add_lzp3(g, secs, lzp_sec, reqs, t_sess.req_of);
             compress_batch(g, reqs);
             if (!fq.empty()) fqz_encode_batch(g, fq);

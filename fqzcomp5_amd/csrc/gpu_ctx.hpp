@@ -272,7 +272,7 @@ GpuCtx &gpu();
 // Helper contexts of the calling thread (k < AUX_CTXS), for work run by
 // helper threads concurrently with the thread's own (created on first use),
 // and a rewind of every one that exists.
-constexpr int AUX_CTXS = 8;
+constexpr int AUX_CTXS = 9;   // 0 fqz, 1 LZP3, 2..7 sequence models, 8 stripes
 GpuCtx &gpu_aux(int k = 0);
 void gpu_aux_reset_all();
 

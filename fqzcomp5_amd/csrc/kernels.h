@@ -110,6 +110,13 @@ __host__ __device__ inline uint32_t dec_tab_words(uint32_t mode, uint32_t rows, 
     if (mode == DEC_TAB_SPLIT) return slots / 4 + (rows << dec_rp_log(rows));
     return slots;
 }
+// NX=4 streams whose table fits the lean decoder's 16-byte entries in LDS
+// (rans_chain.hip dec4_lean_body): O0, and O1 with rows x 2^bits <= 8192.
+constexpr uint32_t DEC_LEAN_ENTRIES = 8192;
+__host__ __device__ inline bool dec_lean(uint32_t rows, int bits) {
+    return (uint64_t(rows) << bits) <= DEC_LEAN_ENTRIES;
+}
+
 inline uint32_t dec_table_mode(bool o1, uint32_t rows, int bits) {
     if (dec_tab_words(DEC_TAB_LDS, rows, bits) * 4u <= DEC_TAB_LDS_MAX) return DEC_TAB_LDS;
     if (o1 && dec_tab_words(DEC_TAB_SPLIT, rows, bits) * 4u <= DEC_TAB_LDS_MAX)

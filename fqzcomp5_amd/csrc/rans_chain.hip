@@ -37,7 +37,7 @@ namespace fqz5 {
 extern __shared__ uint4 chain_lds[];
 #ifdef FQZ5_CHAIN_PROBE
 __device__ uint64_t g_probe[8];
-__device__ uint64_t g_jobt[512][6];   // per decode job: start, end (100 MHz), cycles, info, loop cycles, loop steps
+__device__ uint64_t g_jobt[512][8];   // per decode job: start, end (100 MHz), cycles, info, loop cycles, loop steps, rows|nx<<16|mode<<24, in_len
 #endif
 
 // Raw buffer over [p, p+n): loads past n return 0, stores past n are dropped.
@@ -759,17 +759,24 @@ static DEV void dec32_body(const DecJob &J) {
 }
 
 // ---------------------------------------------------------------------------
-// O0, NX = 4: the lean chain.  The order-0 symbol does not feed the chain, so
-// the step carries only what the next state needs and the slot is emitted in
-// place of the symbol (mapped to the symbol at the group flush):
-//   LDS entry per slot   {f, slot - start, T, 0} (no symbol byte), with
-//                        T = ceil((2^15 - (slot - start)) / f)
+// NX = 4, O0 and small-table O1: the lean chain.  The step carries only what
+// the next state needs and a table index is emitted in place of the symbol
+// (mapped to the symbol at the group flush):
+//   LDS entry per (row, slot)   {f, slot - start, T, next} (16 B), with
+//                        T = ceil((2^15 - (slot - start)) / f) and next the
+//                        LDS address of the row the decoded symbol selects
+//                        (O1: the next step's context; O0: the one row)
+//   entry address = row + slot * 16      (one shift-add; row = last entry's next)
 //   xd   = f * (x >> bits) + (slot - start)             (one mad24)
 //   renormalise  <=>  xd < 2^15  <=>  (x >> bits) < T, so the ballot does
 //        not wait for the mad24
 //   ptr  lives in a VGPR and advances with one v_bcnt of the renorm ballot;
 //        the ring is linear over a group (a mirrored head), so the window
 //        address is one shift-add of ptr.
+// O1 thus costs what O0 does: the context is a field of the entry read on
+// the chain anyway.  It applies while the table's rows x 2^bits entries
+// fit (dec_lean: at most 8192, i.e. up to 8 contexts at TF_SHIFT 10 — the
+// quality and sequence alphabets of the bench's data).
 // Per step: 2 VALU for the table address, the table and window reads, 2 for
 // xd, the ballot, 6 for the renorm select and ptr (slots stay in VGPRs): no
 // SALU on the chain (a wave issues one instruction per ~4 cycles whatever the
@@ -777,11 +784,12 @@ static DEV void dec32_body(const DecJob &J) {
 constexpr uint32_t O0_G = 256;                         // steps per group
 constexpr uint32_t O0_MIRROR = 1040;                   // >= 4*G + 4, slab-unit multiple of 8
 constexpr uint32_t O0_RING_BYTES = (RING_WORDS + O0_MIRROR) * 2;
-constexpr uint32_t O0_OBUF_BYTES = 4 * O0_G * 2;       // u16 slots, lane-major
+constexpr uint32_t O0_OBUF_BYTES = 4 * O0_G * 2;       // u16 table indices, lane-major
 constexpr uint32_t O0_SYM_OFF = O0_RING_BYTES + O0_OBUF_BYTES;
-constexpr uint32_t O0_TAB_OFF = O0_SYM_OFF + 4096;     // 16-B entries, 16-B aligned
-static_assert(O0_TAB_OFF % 16 == 0, "O0 table alignment");
-constexpr uint32_t O0_LDS_BYTES = O0_TAB_OFF + 4096 * 16;
+constexpr uint32_t O0_TAB_OFF = O0_SYM_OFF + DEC_LEAN_ENTRIES;   // 16-B entries, 16-B aligned
+static_assert(O0_TAB_OFF % 16 == 0, "lean table alignment");
+constexpr uint32_t O0_LDS_BYTES = O0_TAB_OFF + DEC_LEAN_ENTRIES * 16;
+static_assert(O0_LDS_BYTES <= 160 * 1024, "lean decoder LDS");
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 static DEV void store_slab_o0(uint16_t *ring, uint32_t s, int z, uint4 v) {
@@ -790,7 +798,8 @@ static DEV void store_slab_o0(uint16_t *ring, uint32_t s, int z, uint4 v) {
     if (w0 < O0_MIRROR) *reinterpret_cast<uint4 *>(ring + RING_WORDS + w0) = v;
 }
 
-static DEV void dec4_o0_body(const DecJob &J) {
+template <bool O1>
+static DEV void dec4_lean_body(const DecJob &J) {
     constexpr int NX = 4;
     constexpr uint32_t G = O0_G;
     uint8_t *lds = reinterpret_cast<uint8_t *>(chain_lds);
@@ -802,12 +811,17 @@ static DEV void dec4_o0_body(const DecJob &J) {
     const uint32_t n = J.n;
     const int bits = J.bits;
     const uint32_t mask = (1u << bits) - 1;
-    // (f-1) << (bits+8) | (slot-start) << 8 | sym  ->  {f, slot-start}
-    for (uint32_t i = l; i <= mask; i += 64) {
+    const uint32_t tab_lds = uint32_t(reinterpret_cast<uintptr_t>(
+        (__attribute__((address_space(3))) uint4 *)(tab)));
+    const uint32_t rows = O1 ? J.rows : 1u;
+    const uint32_t idx0 = tab_lds >> 4;                // emitted index = entry address / 16
+    // (f-1) << (bits+8) | (slot-start) << 8 | sym  ->  {f, slot-start, T, row of sym}
+    for (uint32_t i = l; i < (rows << bits); i += 64) {
         const uint32_t e = J.tab[i];
-        const uint32_t f = (e >> (bits + 8)) + 1, b = (e >> 8) & mask;
-        tab[i] = make_uint4(f, b, (RANS_LOW_D - b + f - 1) / f, 0);
-        s2sym[i] = uint8_t(e);
+        const uint32_t f = (e >> (bits + 8)) + 1, b = (e >> 8) & mask, sy = e & 0xffu;
+        tab[i] = make_uint4(f, b, (RANS_LOW_D - b + f - 1) / f,
+                            O1 ? tab_lds + ((sy << bits) << 4) : tab_lds);
+        s2sym[i] = O1 ? J.alpha[sy] : uint8_t(sy);
     }
     uint32_t x = 1u << 16;
     if (l < NX) {
@@ -818,12 +832,16 @@ static DEV void dec4_o0_body(const DecJob &J) {
     const auto wsrc = buf(J.in + 4 * NX, nwords * 2);
     uint32_t slabs = 0;
     uint4 pf = load_slab(wsrc, 0, l);
-    const uint32_t T = (n + NX - 1) / NX, Tfull = n / NX;
+    // O0: step t, lane z -> byte 4t + z.  O1: lane z owns the bytes
+    // [z*isz, z*isz + lenz), the last lane the tail (rANS_static4x16pr.c:464-481)
+    const uint32_t isz = n / NX;
+    const uint32_t lenz = O1 ? ((l & 3) == NX - 1 ? n - uint32_t(NX - 1) * isz : isz) : 0;
+    const uint32_t T = O1 ? n - uint32_t(NX - 1) * isz : (n + NX - 1) / NX;
+    const uint32_t Tfull = O1 ? isz : n / NX;          // steps with all lanes active
     uint32_t ptr = 0;                                  // words consumed (uniform)
+    uint32_t row = tab_lds;                            // O1: context 0 at a segment start
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(
         (__attribute__((address_space(3))) uint16_t *)(ring)));
-    const uint32_t tab_lds = uint32_t(reinterpret_cast<uintptr_t>(
-        (__attribute__((address_space(3))) uint4 *)(tab)));
     uint16_t *myob = obuf + (l & 3) * G;
 #ifdef FQZ5_CHAIN_PROBE
     const uint64_t pr0 = __builtin_amdgcn_s_memtime(), rr0 = __builtin_amdgcn_s_memrealtime();
@@ -852,13 +870,14 @@ static DEV void dec4_o0_body(const DecJob &J) {
                 uint32_t a[16];
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
-                    a[u] = x & mask;
+                    const uint32_t ea = O1 ? row + ((x & mask) << 4) : tab_lds + ((x & mask) << 4);
+                    a[u] = O1 ? (ea >> 4) - idx0 : x & mask;
                     const uint32_t xh = x >> bits;          // ready before the reads return
                     // the window read (address known since the last step)
                     // goes first so neither read waits for the other
                     const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
                     __builtin_amdgcn_sched_barrier(0);
-                    const u32x4 e = *lds_ptr<u32x4>(tab_lds + (a[u] << 4));
+                    const u32x4 e = *lds_ptr<u32x4>(ea);
                     __builtin_amdgcn_sched_barrier(0);
                     const bool c = xh < e.z;
                     const uint32_t xd = __umul24(e.x, xh) + e.y;
@@ -867,6 +886,7 @@ static DEV void dec4_o0_body(const DecJob &J) {
                     const uint32_t w = uint32_t(win >> r16);
                     x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
                     ptr = vbcnt(uint32_t(m), ptr, r16);
+                    if (O1) row = e.w;
                 }
                 uint4 *o = reinterpret_cast<uint4 *>(myob + (t - t0));
                 o[0] = make_uint4(a[0] | a[1] << 16, a[2] | a[3] << 16, a[4] | a[5] << 16,
@@ -878,12 +898,14 @@ static DEV void dec4_o0_body(const DecJob &J) {
             t_steps += __builtin_amdgcn_s_memtime() - ps0;
             n_steps += t - t0;
 #endif
-            // rest of the group: single steps; in the last step only lanes
-            // z < n % 4 are active
+            // rest of the group: single steps; where lanes run out of
+            // bytes (O0: the last step's lanes z >= n % 4, O1: all but the
+            // last lane's tail) they are inactive
             for (; t < t1; t++) {
-                const bool act = uint32_t(NX) * t + uint32_t(l) < n;
-                const uint32_t s = x & mask;
-                const uint4 e = tab[s];
+                const bool act = O1 ? t < lenz : uint32_t(NX) * t + uint32_t(l) < n;
+                const uint32_t ea = (O1 ? row : tab_lds) + ((x & mask) << 4);
+                const uint4 e = *reinterpret_cast<const uint4 *>(
+                    lds + O0_TAB_OFF + (ea - tab_lds));
                 const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
                 const uint32_t xd = __umul24(e.x, x >> bits) + e.y;
                 const bool c = act && xd < RANS_LOW_D;
@@ -892,7 +914,8 @@ static DEV void dec4_o0_body(const DecJob &J) {
                 const uint32_t w = uint32_t(win >> r16);
                 if (act) {
                     x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
-                    myob[t - t0] = uint16_t(s);
+                    myob[t - t0] = uint16_t((ea >> 4) - idx0);
+                    if (O1) row = e.w;
                 }
                 ptr += uint32_t(__popcll(m));
             }
@@ -902,6 +925,15 @@ static DEV void dec4_o0_body(const DecJob &J) {
         const uint32_t cnt = (t1 - t0) * NX;
         if (!hedge_first(hedge, t0 / G)) {
             // another copy started this group first and writes it
+        } else if (O1) {
+            // lane-major: byte (t, z) at z*isz + t; lanes past their length
+            // (the tail of the last) hold nothing
+            const auto out = buf(J.out, n);
+            for (uint32_t i = l; i < cnt; i += 64) {
+                const uint32_t zc = i / (t1 - t0), tt = i % (t1 - t0);
+                const uint32_t lz = (zc == NX - 1) ? n - uint32_t(NX - 1) * isz : isz;
+                if (t0 + tt < lz) st8(out, zc * isz + t0 + tt, s2sym[obuf[zc * G + tt]]);
+            }
         } else if (cnt == NX * G && NX * t0 + NX * G <= n &&
                    (reinterpret_cast<uintptr_t>(J.out) & 15) == 0) {
             // a whole group: lane l writes output bytes [16l, 16l+16), i.e.
@@ -942,7 +974,8 @@ static DEV void dec4_o0_body(const DecJob &J) {
 template <bool O1, int TM>
 static DEV void dec_any(const DecJob &J) {
     if (J.nx == 32) dec32_body<O1, TM>(J);
-    else if (!O1)   dec4_o0_body(J);
+    else if (!O1)   dec4_lean_body<false>(J);
+    else if (TM == DEC_TAB_LDS && dec_lean(J.rows, J.bits)) dec4_lean_body<true>(J);
     else            dec4_body<O1, TM>(J);
 }
 
@@ -961,6 +994,8 @@ __global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
                 g_jobt[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
                 g_jobt[blockIdx.x][2] = __builtin_amdgcn_s_memtime() - c0;
                 g_jobt[blockIdx.x][3] = uint64_t(J.n) << 32 | (xcc & 0xf) << 24 | ((hw >> 8) & 0xf) << 16 | ((hw >> 13) & 0x7) << 8 | ((hw >> 4) & 3);
+                g_jobt[blockIdx.x][6] = uint64_t(J.alpha ? J.rows : 0u) | uint64_t(J.nx) << 16 | uint64_t(J.mode) << 24;
+                g_jobt[blockIdx.x][7] = J.in_len;
             }
         }
     } end_{jt0, jc0, J};
@@ -978,7 +1013,7 @@ __global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
 uint32_t dec_lds_bytes(uint32_t rows, int bits, int mode) {
     if (mode == DEC_TAB_GLOBAL) return DEC_LDS_BASE;
     const uint32_t b = DEC_LDS_BASE + dec_tab_words(uint32_t(mode), rows, bits) * 4u;
-    return rows == 1 && b < O0_LDS_BYTES ? O0_LDS_BYTES : b;   // O0 (dec4_o0_body)
+    return dec_lean(rows, bits) && b < O0_LDS_BYTES ? O0_LDS_BYTES : b;   // dec4_lean_body
 }
 
 static void lds_attr(const void *f) {

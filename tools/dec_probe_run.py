@@ -47,11 +47,11 @@ if len(sys.argv) > 2 and sys.argv[2] == "bench":
         print(f"bench launch: dec {pr[3]:.1f} ms; job0 steps={T} {tot/max(T,1):.1f} cyc/step "
               f"loop {ts/max(ns,1):.1f}/step clock {tot/(real*10.0):.3f} GHz wall {real/100:.0f} us",
               flush=True)
-        jt = (C.c_uint64 * (512 * 6))()
+        jt = (C.c_uint64 * (512 * 8))()
         so.fqz5_chain_jobs_read(jt)
-        t0 = min(jt[6 * i] for i in range(len(dres)) if jt[6 * i])
+        t0 = min(jt[8 * i] for i in range(len(dres)) if jt[8 * i])
         for i in range(len(dres)):
-            a, b, cyc, k, lc, ls = jt[6 * i:6 * i + 6]
+            a, b, cyc, k, lc, ls = jt[8 * i:8 * i + 6]
             n = k >> 32
             print(f"  job {i:2d} n={n:9d} xcc={(k >> 24) & 15} cu={(k >> 16) & 15} se={(k >> 8) & 7} "
                   f"simd={k & 3} end {(b - t0) / 100:8.0f} us ns/step {(b - a) * 10 / max(n / 4, 1):.1f} "
@@ -67,15 +67,15 @@ if len(sys.argv) > 2 and sys.argv[2] == "same":
         outs = [torch.empty(len(data), dtype=torch.uint8, device="cuda") for _ in range(nj)]
         jobs = [lib.RansJob(cin.data_ptr(), o.data_ptr(), len(comp), len(data), 0, 0, 0, 0) for o in outs]
         lib.uncompress_batch_dev(jobs)
-        jt = (C.c_uint64 * (512 * 6))()
+        jt = (C.c_uint64 * (512 * 8))()
         so.fqz5_chain_jobs_read(jt)
-        cyc = [jt[6 * i + 2] / (len(data) / 4) for i in range(nj)]
-        lp = [jt[6 * i + 4] / max(jt[6 * i + 5], 1) for i in range(nj)]
-        xcc = [(jt[6 * i + 3] >> 24) & 15 for i in range(nj)]
+        cyc = [jt[8 * i + 2] / (len(data) / 4) for i in range(nj)]
+        lp = [jt[8 * i + 4] / max(jt[8 * i + 5], 1) for i in range(nj)]
+        xcc = [(jt[8 * i + 3] >> 24) & 15 for i in range(nj)]
         ok = all(bytes(o.cpu().numpy()) == data for o in outs[:2])
         print(f"same stream x{nj}: ok={ok} cyc/step min {min(cyc):.1f} max {max(cyc):.1f}; "
               f"loop min {min(lp):.1f} max {max(lp):.1f}", flush=True)
-        info = [jt[6 * i + 3] for i in range(nj)]
+        info = [jt[8 * i + 3] for i in range(nj)]
         from collections import defaultdict
         for name, f in (("simd", lambda k: k & 3), ("cu", lambda k: (k >> 16) & 15),
                         ("se", lambda k: (k >> 8) & 7), ("xcc", lambda k: (k >> 24) & 15)):

@@ -7,7 +7,7 @@
 #define N 4096
 typedef __attribute__((address_space(3))) uint64_t lds64_t;
 
-template <int T>
+template <int T, int L = 4>
 __global__ void k(uint32_t *out, uint64_t *cyc, uint32_t a, uint32_t b) {
     __shared__ uint64_t lds[4096];
     uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds);
@@ -18,7 +18,7 @@ __global__ void k(uint32_t *out, uint64_t *cyc, uint32_t a, uint32_t b) {
     uint32_t x = a + l, y = b, p = 0;
     uint64_t win = (uint64_t(b) << 32) | a;
     uint64_t t0 = 0, t1 = 0;
-    if (l < 4) {
+    if (l < L) {
         __builtin_amdgcn_s_waitcnt(0);
         t0 = __builtin_amdgcn_s_memtime();
 #pragma unroll 16
@@ -109,6 +109,24 @@ __global__ void k(uint32_t *out, uint64_t *cyc, uint32_t a, uint32_t b) {
                 const uint32_t s = ((y - x) >> 27) & 16u;
                 x = (x >> s) + 3;
             }
+            if (T == 24) {                                                  // enc step asm, cndmask sdwa
+                uint32_t q;
+                asm volatile(
+                    "v_cmp_gt_u32_e32 vcc, %0, %3\n\t"
+                    "s_nop 1\n\t"
+                    "v_cndmask_b32_sdwa %0, %0, %0, vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+                    "v_mul_hi_u32 %1, %0, %2\n\t"
+                    "v_lshrrev_b32_sdwa %1, %5, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"
+                    "v_mul_u32_u24_sdwa %1, %1, %5 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+                    "v_add3_u32 %0, %0, %4, %1"
+                    : "+v"(x), "=&v"(q) : "v"(0x9e3779b1u), "v"(y), "v"(12345u), "v"(0x00030003u | (a & 7) << 16) : "vcc");
+            }
+            if (T == 25) {                                                  // enc step C (cmp+cndmask), ref for T24
+                const uint32_t w = 0x00030003u | (a & 7) << 16;
+                const uint32_t xr = (x > y) ? (x >> 16) : x;
+                const uint32_t q = __umulhi(xr, 0x9e3779b1u) >> (w >> 16);
+                x = __umul24(q, w & 0xffffu) + (xr + 12345u);
+            }
             if (T == 10) {                                                  // full renorm select chain
                 const uint64_t m = __ballot(x < y);
                 const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
@@ -119,12 +137,12 @@ __global__ void k(uint32_t *out, uint64_t *cyc, uint32_t a, uint32_t b) {
         t1 = __builtin_amdgcn_s_memtime();
     }
     out[l] = x + p + y;
-    if (l == 0) cyc[T] = t1 - t0;
+    if (l == 0) cyc[L == 4 ? T : 32 + T] = t1 - t0;
 }
 
 int main() {
     uint32_t *out; uint64_t *cyc;
-    hipMalloc(&out, 64 * 4); hipMalloc(&cyc, 32 * 8);
+    hipMalloc(&out, 64 * 4); hipMalloc(&cyc, 64 * 8);
     const char *names[] = {"ds_read_b64 chain", "v_add", "mad24", "lshr_b64+add", "perm+add",
                            "cmp+mbcnt", "cmp+cndmask", "and,lshl_add,ds_read,mad", "same + never-taken branch",
                            "same + ~68%-taken branch", "renorm select (cmp,mbcnt,lshl,lshr64,perm,cndmask)",
@@ -132,14 +150,17 @@ int main() {
                            "fqz range step f64", "fqz range step int magic",
                            "O0 step LDS lookup + mad", "O0 step register lookup + mad",
                            "ds_read_b32 chain", "ds_read_b128 chain", "renorm select via perm selector",
-                           "mul_hi chain", "enc q via f64 (cvt,fma,cvt,add)", "sign-shift (sub,lshr,and,lshr,add)"};
+                           "mul_hi chain", "enc q via f64 (cvt,fma,cvt,add)", "sign-shift (sub,lshr,and,lshr,add)",
+                           "enc step asm cndmask_sdwa", "enc step C, packed cmpl|shift"};
 #define RUN(T) hipLaunchKernelGGL(k<T>, dim3(1), dim3(64), 0, 0, out, cyc, 12345u, 99999u);
+#define RUN64(T) hipLaunchKernelGGL((k<T, 64>), dim3(1), dim3(64), 0, 0, out, cyc, 12345u, 99999u);
     for (int rep = 0; rep < 2; rep++) {
-        RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15) RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23)
+        RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15) RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23) RUN(24) RUN(25) RUN64(11) RUN64(21) RUN64(24) RUN64(25) RUN64(16)
     }
     hipDeviceSynchronize();
-    uint64_t h[32];
+    uint64_t h[64];
     hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
-    for (int t = 0; t <= 23; t++) printf("T%-2d %-55s %7.1f cyc/step\n", t, names[t], double(h[t]) / N);
+    for (int t = 0; t <= 25; t++) printf("T%-2d %-55s %7.1f cyc/step\n", t, names[t], double(h[t]) / N);
+    for (int t : {11, 21, 24, 25, 16}) printf("T%-2d %-55s %7.1f cyc/step (64 lanes)\n", t, names[t], double(h[32 + t]) / N);
     return 0;
 }
