@@ -67,7 +67,7 @@ bool hedge_chains() {
 // rANS candidates).
 static thread_local std::unique_ptr<GpuCtx> g_aux[AUX_CTXS];
 GpuCtx &gpu_aux(int k) {
-    if (!g_aux[k]) g_aux[k].reset(new GpuCtx());
+    if (!g_aux[k]) g_aux[k].reset(new GpuCtx(std::getenv("FQZ5_AUX_NORMAL_PRIO") == nullptr));
     return *g_aux[k];
 }
 void gpu_aux_reset_all() {

@@ -159,14 +159,20 @@ struct GpuCtx {
         return jobs <= size_t(cus) && lds < HALF_CU ? HALF_CU : lds;
     }
 
-    GpuCtx() {
+    // high_prio: the streams of a helper context (gpu_aux) get the device's
+    // highest priority, so that the short kernels of the trial's work
+    // candidates are dispatched ahead of the rANS batch's long chains.
+    explicit GpuCtx(bool high_prio = false) {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
             throw GpuError("fqz5: no HIP device visible (this library has no CPU path)");
         FQZ5_HIP(hipGetDevice(&device));
         FQZ5_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        FQZ5_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        FQZ5_HIP(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+        int lo = 0, hi = 0;
+        FQZ5_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        const int prio = high_prio ? hi : lo;
+        FQZ5_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio));
+        FQZ5_HIP(hipStreamCreateWithPriority(&stream2, hipStreamNonBlocking, prio));
         FQZ5_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
         FQZ5_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
     }

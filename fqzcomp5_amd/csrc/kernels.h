@@ -159,6 +159,16 @@ hipError_t launch_unrle_expand(const UnRleItem *items, const uint32_t *chunk_ite
                                int what, hipStream_t s);
 
 hipError_t launch_gather(const GatherItem *items, int n, uint8_t *out, hipStream_t s);
+// Order-1 encoder table of one job, built on the GPU: f[A*A] the normalised
+// frequencies over the compacted alphabet (row = context), out[A*A] the
+// EncSym of every (context, symbol) (rans_compress.cpp build_o1).
+struct EncTabItem {
+    const uint16_t *f;
+    EncSym *out;
+    uint32_t A;
+    uint32_t bits;
+};
+hipError_t launch_enc_tab(const EncTabItem *d_items, int nitems, hipStream_t s);
 hipError_t launch_hist0(const HistItem *d_items, int nitems, uint32_t *d_counts,
                         hipStream_t s);
 // big: items with A*A >= 16384 (16-bit LDS counters; slices < 65536 bytes)

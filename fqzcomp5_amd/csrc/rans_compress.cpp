@@ -58,7 +58,8 @@ struct EJ {                       // one rANS entropy stream to encode
     // tables
     int bits = 12;
     std::vector<uint8_t> table;   // serialised frequency table
-    std::vector<EncSym> syms;
+    std::vector<EncSym> syms;     // O0 (host-built)
+    std::vector<uint16_t> f1;     // O1: normalised frequencies [A*A], the table is built on the GPU
     int hdr_job = -1;             // O1: job compressing table[1..]
     // kernel output
     uint8_t *d_end = nullptr;
@@ -393,7 +394,11 @@ void Compressor::build_o1(EJ &j, const uint32_t *cnt) {
     uint32_t rowmax[256] = {0};
     const int shift = o1_pick_shift(T, F, rowmax);
     j.bits = shift;
-    j.syms.assign(size_t(j.A) * j.A, EncSym{0, 0, 0, 0});
+    // Per context, the normalised frequencies over the compacted alphabet;
+    // k_enc_tab turns them into the EncSym table (start = the running sum
+    // in byte order).  Every symbol with a frequency is in the alphabet (it
+    // occurs in the input, or is 0).
+    j.f1.assign(size_t(j.A) * j.A, 0);
     for (int i = 0; i < 256; i++) {
         if (!T[i]) continue;
         uint32_t mv = rowmax[i];
@@ -402,10 +407,11 @@ void Compressor::build_o1(EJ &j, const uint32_t *cnt) {
         p += put_freq_row(&h[p], T, F[i]);
         scale_pow2(F[i], mv, 1u << shift);
         const size_t row = size_t(j.remap[i]) * j.A;
-        for (uint32_t s = 0, x = 0; s < 256; s++) {
+        for (uint32_t s = 0; s < 256; s++) {
             if (!F[i][s]) continue;
-            if (s == 0 || j.F0[s]) j.syms[row + j.remap[s]] = make_encsym(x, F[i][s], shift);
-            x += F[i][s];
+            if (s != 0 && !j.F0[s])
+                throw GpuError("rANS O1: a frequency outside the alphabet");
+            j.f1[row + j.remap[s]] = uint16_t(F[i][s]);
         }
     }
     h.resize(p);
@@ -413,6 +419,12 @@ void Compressor::build_o1(EJ &j, const uint32_t *cnt) {
 }
 
 void Compressor::stage_tables() {
+    static const bool trace = std::getenv("FQZ5_STEP_TRACE") != nullptr;
+    auto now = [] {
+        return std::chrono::duration<double, std::milli>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    const double ta = trace ? now() : 0;
     // byte histograms of job inputs made in stage 4 (RLE literals, meta)
     std::vector<std::pair<const uint8_t *, uint32_t>> segs;
     std::vector<int> who;
@@ -467,12 +479,22 @@ void Compressor::stage_tables() {
         for (int z = 1; z < j.nx; z++) j.seg_first[z] = pb[q++];
         j.last_byte = pb[q++];
     }
+    const double tb = trace ? now() : 0;
     host_parallel(o1jobs.size(), [&](size_t k) { build_o1(jobs_[o1jobs[k]], &h[jobs_[o1jobs[k]].f1_off]); });
+    if (trace)
+        std::fprintf(stderr, "tables: o1 hist %.1f ms, build_o1 %.1f ms (%zu jobs, %u pairs)\n",
+                     tb - ta, now() - tb, o1jobs.size(), total);
 }
 
 // Stage 5: all rANS chains.  O1 tables above 1000 bytes get their own
 // O0-4x16 job (rANS_static16_int.h:397-412) in the same launch.
 void Compressor::stage_encode() {
+    static const bool trace = std::getenv("FQZ5_STEP_TRACE") != nullptr;
+    auto now = [] {
+        return std::chrono::duration<double, std::milli>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    const double ta = trace ? now() : 0;
     const size_t nmain = jobs_.size();
     host_parallel(nmain, [&](size_t i) { if (!jobs_[i].o1) build_o0(jobs_[i]); });
     for (size_t i = 0; i < nmain; i++) {
@@ -502,17 +524,47 @@ void Compressor::stage_encode() {
     uint32_t *d_lens = g_.arena.alloc_n<uint32_t>(jobs_.size());
     // every job's symbol table and O1 remap in one upload each (a stripe
     // candidate set is thousands of small jobs)
-    std::vector<size_t> tab_off(jobs_.size()), rm_off(jobs_.size());
+    // O0 tables from the host; O1 tables built on the GPU from their
+    // frequencies (k_enc_tab), into one device array
+    std::vector<size_t> tab_off(jobs_.size()), rm_off(jobs_.size()), f1_off(jobs_.size());
     std::vector<EncSym> all_syms;
+    std::vector<uint16_t> all_f1;
     std::vector<uint8_t> all_rm;
+    size_t nsyms = 0;
     for (int i : order) {
         const EJ &j = jobs_[i];
-        tab_off[i] = all_syms.size();
-        all_syms.insert(all_syms.end(), j.syms.begin(), j.syms.end());
+        if (j.o1) {
+            tab_off[i] = nsyms;
+            nsyms += j.f1.size();
+            f1_off[i] = all_f1.size();
+            all_f1.insert(all_f1.end(), j.f1.begin(), j.f1.end());
+        }
         rm_off[i] = all_rm.size();
         if (j.o1) all_rm.insert(all_rm.end(), j.remap, j.remap + 256);
     }
-    const EncSym *d_syms = g_.upload(all_syms);
+    for (int i : order) {
+        const EJ &j = jobs_[i];
+        if (j.o1) continue;
+        tab_off[i] = nsyms + all_syms.size();
+        all_syms.insert(all_syms.end(), j.syms.begin(), j.syms.end());
+    }
+    const double tb = trace ? now() : 0;
+    EncSym *d_syms = g_.arena.alloc_n<EncSym>(std::max<size_t>(nsyms + all_syms.size(), 1));
+    if (!all_syms.empty()) {
+        uint8_t *st = g_.staging.alloc(all_syms.size() * sizeof(EncSym));
+        std::memcpy(st, all_syms.data(), all_syms.size() * sizeof(EncSym));
+        FQZ5_HIP(hipMemcpyAsync(d_syms + nsyms, st, all_syms.size() * sizeof(EncSym),
+                                hipMemcpyHostToDevice, g_.stream));
+    }
+    if (!all_f1.empty()) {
+        const uint16_t *d_f1 = g_.upload(all_f1);
+        std::vector<EncTabItem> ti;
+        for (int i : order)
+            if (jobs_[i].o1)
+                ti.push_back({d_f1 + f1_off[i], d_syms + tab_off[i], uint32_t(jobs_[i].A),
+                              uint32_t(jobs_[i].bits)});
+        FQZ5_HIP(launch_enc_tab(g_.upload(ti), int(ti.size()), g_.stream));
+    }
     const uint8_t *d_rms = all_rm.empty() ? nullptr : g_.upload(all_rm);
     for (int i : order) {
         EJ &j = jobs_[i];
@@ -563,9 +615,11 @@ void Compressor::stage_encode() {
         FQZ5_HIP(launch_enc_replay(d_all, d_items, nit, true, lds_r, g_.stream));
     }
     ev.stop(g_.stream);
+    const double tc = trace ? now() : 0;
     std::vector<uint32_t> lens(jobs_.size(), 0);
     g_.download(lens.data(), d_lens, jobs_.size());
     g_.sync();
+    const double td = trace ? now() : 0;
     if (ev.on) {
         g_.prof.enc_ms += ev.ms();
         g_.prof.enc_launches += 1;
@@ -574,6 +628,10 @@ void Compressor::stage_encode() {
     for (size_t i = 0; i < jobs_.size(); i++) jobs_[i].payload = jobs_[i].n ? lens[i] : 0;
     for (size_t i = nmain; i < jobs_.size(); i++) finish_job(jobs_[i]);
     for (size_t i = 0; i < nmain; i++) finish_job(jobs_[i]);
+    if (trace)
+        std::fprintf(stderr, "encode: tables %.1f ms (%zu syms), uploads+launch %.1f ms, "
+                     "wait %.1f ms, finish %.1f ms\n", tb - ta, nsyms + all_syms.size(), tc - tb,
+                     td - tc, now() - td);
 }
 
 void Compressor::finish_job(EJ &j) {

@@ -567,4 +567,54 @@ hipError_t launch_unrle_expand(const UnRleItem *items, const uint32_t *chunk_ite
     return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------
+// Order-1 encoder tables (build_o1's last loop, rANS_static4x16pr.c:423-518
+// with RansEncSymbolInit, rANS_word.h:201-272): workgroup (row, job) scans
+// the row's frequencies into starts and writes one EncSym per symbol — the
+// host sends 2 bytes per (context, symbol) instead of 16 (a -5 trial batch
+// has ~150 jobs of 256 x 256 entries).
+__global__ __launch_bounds__(256) void k_enc_tab(const EncTabItem *items) {
+    const EncTabItem it = items[blockIdx.y];
+    const uint32_t r = blockIdx.x, t = threadIdx.x, A = it.A;
+    if (r >= A) return;
+    __shared__ uint32_t sc[256];
+    const uint32_t f = t < A ? it.f[r * A + t] : 0u;
+    sc[t] = f;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1) {          // inclusive scan
+        const uint32_t v = t >= d ? sc[t - d] : 0u;
+        __syncthreads();
+        sc[t] += v;
+        __syncthreads();
+    }
+    if (t >= A) return;
+    const uint32_t start = sc[t] - f;
+    const int bits = int(it.bits);
+    EncSym e{0, 0, 0, 0};
+    if (f) {                                          // = make_encsym(start, f, bits)
+        uint32_t sh;
+        e.xmax = ((RANS_LOW >> bits) << 16) * f - 1;
+        if (f < 2) {
+            e.rcp = ~0u;
+            sh = 0;
+            e.bias = start + (1u << bits) - 1;
+        } else {
+            uint32_t sbits = 0;
+            while (f > (1u << sbits)) sbits++;
+            e.rcp = uint32_t(((1ull << (sbits + 31)) + f - 1) / f);
+            sh = sbits - 1;
+            e.bias = start;
+        }
+        e.cmpl_sh = (((1u << bits) - f) & 0xffff) | (sh << 16);
+    }
+    it.out[r * A + t] = e;
+}
+
+hipError_t launch_enc_tab(const EncTabItem *d_items, int nitems, hipStream_t s) {
+    if (!nitems) return hipSuccess;
+    hipLaunchKernelGGL(k_enc_tab, dim3(256, nitems), dim3(256), 0, s, d_items);
+    return hipGetLastError();
+}
+
 }  // namespace fqz5
