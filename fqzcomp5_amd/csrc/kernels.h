@@ -184,6 +184,9 @@ hipError_t launch_copy(const CopyItem *d_items, int nitems, hipStream_t s);
 // over the launch's jobs.
 uint32_t enc_lds_bytes(int o1, uint32_t A);
 uint32_t enc_replay_lds_bytes(int o1, uint32_t A);
+bool enc_chain_2w(int o1, int nx, uint32_t A);       // runs k_enc_chain2w
+uint32_t enc_2w_lds_bytes(int o1, uint32_t A);
+hipError_t launch_enc_chain2w(const EncJob *d_jobs, int njobs, uint32_t lds, hipStream_t s);
 uint32_t dec_lds_bytes(uint32_t rows, int bits, int mode);
 hipError_t launch_enc_chain(const EncJob *d_jobs, int njobs, uint32_t lds, hipStream_t s);
 // d_items: uint32 pairs {job index, first chunk}

@@ -226,6 +226,141 @@ static DEV void chain_body(const EncJob &J) {
 #endif
 }
 
+// NX = 4 with the table in LDS (the long chains): a workgroup of two waves.
+// Wave 0 runs the chain over one entry buffer while wave 1 loads the next
+// chunk's symbols and stages its entries into the other; they meet at one
+// barrier per chunk.  The staging (~7 cycles per step when the chain wave
+// did it between chunks) then costs the chain nothing: the waves sit on
+// different SIMDs and the staging finishes well within the chain's time.
+constexpr uint32_t ENC_BUF_ENT = ENC_ENT + 512;                // entries per buffer, + chain over-read
+constexpr uint32_t ENC_2W_BASE = 2 * ENC_BUF_ENT * 16 + 256;   // 2 buffers + remap
+
+template <bool O1>
+static DEV void chain_body_2w(const EncJob &J) {
+    constexpr int NX = 4;
+    constexpr uint32_t S = enc_chunk<NX>();               // 256 steps per chunk
+    constexpr int R = int(ENC_ENT / 64);                  // 16 entries staged per lane
+    constexpr int CB = 8;
+    uint8_t *lds = reinterpret_cast<uint8_t *>(chain_lds);
+    uint4 *entb = reinterpret_cast<uint4 *>(lds);
+    uint8_t *rm = lds + 2 * ENC_BUF_ENT * 16;
+    uint4 *ltab = reinterpret_cast<uint4 *>(lds + ENC_2W_BASE);
+
+    const int tid = int(threadIdx.x);
+    const int wave = tid >> 6, l = tid & 63;
+    const uint32_t n = J.n;
+    const uint32_t A = uint32_t(J.A);
+    {
+        const uint4 *gtab = reinterpret_cast<const uint4 *>(J.tab);
+        const uint32_t ntab = O1 ? A * A : 256u;
+        for (uint32_t i = tid; i < ntab; i += 128) ltab[i] = gtab[i];
+    }
+    if (O1)
+        for (int i = tid; i < 256; i += 128) rm[i] = J.remap[i];
+    __syncthreads();
+
+    const uint32_t isz = n / NX;
+    const uint32_t T = enc_steps<O1, NX>(n);
+    const uint32_t jtop = (T - 1) / S;
+    const auto in = buf(J.in, n);
+
+    // wave 1: chunk j's entries into dst (as chain_body's issue + stage)
+    auto stage = [&](uint32_t j, uint4 *dst) {
+        uint32_t sb[R], cb[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const uint32_t i = uint32_t(l) + 64u * r;
+            if (O1) {
+                const uint32_t z = i / S, k = j * S + i % S;
+                sb[r] = ld8(in, z * isz + k);
+                cb[r] = ld8(in, z * isz + k - 1u);
+            } else {
+                sb[r] = ld8(in, NX * S * j + i);
+            }
+        }
+        const uint4 ID = make_uint4(0, 0xffffffffu, 0, 0);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const uint32_t i = uint32_t(l) + 64u * r;
+            uint32_t z, kk, idx;
+            bool ok;
+            if (O1) {
+                z = i / S;
+                kk = i % S;
+                const uint32_t k = j * S + kk;
+                ok = k < ((z == NX - 1) ? T : isz);
+                idx = uint32_t(rm[k ? cb[r] : 0u]) * A + rm[sb[r]];
+            } else {
+                z = i % NX;
+                kk = i / NX;
+                ok = NX * S * j + i < n;
+                idx = sb[r];
+            }
+            uint4 e = ltab[ok ? idx : 0u];
+            if (!ok) e = ID;
+            dst[(S - 1 - kk) * NX + z] = e;
+        }
+    };
+
+    if (wave == 1) stage(jtop, entb);
+    __syncthreads();
+
+    const int zl = l & (NX - 1);
+    const bool writer = wave == 0 && l < NX;
+    uint32_t x = RANS_LOW_D;
+    uint32_t *ck = J.ck + zl;
+    auto step = [&](const uint4 e) {
+        const bool c = x > e.y;
+        const uint32_t xr = c ? (x >> 16) : x;
+        const uint32_t q = __umulhi(xr, e.x) >> (e.w >> 16);
+        x = __umul24(q, e.w & 0xffffu) + (xr + e.z);
+    };
+#ifdef FQZ5_CHAIN_PROBE
+    uint64_t t_chain = 0;
+#endif
+    for (int32_t j = int32_t(jtop); j >= 0; j--) {
+        const uint32_t cur = (jtop - uint32_t(j)) & 1u;
+        if (wave == 0) {
+#ifdef FQZ5_CHAIN_PROBE
+            const uint64_t tp0 = __builtin_amdgcn_s_memtime();
+#endif
+            if (writer) *ck = x;
+            ck += NX;
+            const uint4 *ep = entb + cur * ENC_BUF_ENT + zl;
+            uint4 E[2][CB];
+#pragma unroll
+            for (int i = 0; i < CB; i++) E[0][i] = ep[i * NX];
+#pragma unroll
+            for (uint32_t b = 0; b < S / CB; b++) {
+                step(E[b & 1][0]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < CB; i++) E[(b + 1) & 1][i] = ep[(CB * (b + 1) + i) * NX];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 1; i < CB; i++) step(E[b & 1][i]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#ifdef FQZ5_CHAIN_PROBE
+            t_chain += __builtin_amdgcn_s_memtime() - tp0;
+#endif
+        } else if (j > 0) {
+            stage(uint32_t(j) - 1u, entb + (cur ^ 1u) * ENC_BUF_ENT);
+        }
+        __syncthreads();
+    }
+    if (writer) *ck = x;                              // checkpoint nchunks
+#ifdef FQZ5_CHAIN_PROBE
+    if (tid == 0) g_probe[1] += t_chain;
+#endif
+}
+
+__global__ __launch_bounds__(128) void k_enc_chain2w(const EncJob *jobs) {
+    const EncJob J = jobs[blockIdx.x];
+    if (J.remap != nullptr) chain_body_2w<true>(J);
+    else                    chain_body_2w<false>(J);
+}
+
 __global__ __launch_bounds__(64) void k_enc_chain(const EncJob *jobs) {
     const EncJob J = jobs[blockIdx.x];
     const bool o1 = J.remap != nullptr;
@@ -376,6 +511,15 @@ __global__ __launch_bounds__(1024) void k_enc_scan(const EncJob *jobs) {
 uint32_t enc_lds_bytes(int o1, uint32_t A) {
     const uint32_t ntab = o1 ? A * A : 256u;
     return ENC_LDS_BASE + (ntab * 16u <= ENC_TAB_LDS_MAX ? ntab * 16u : 0u);
+}
+
+// Jobs that run k_enc_chain2w (NX=4, table in LDS) and their LDS.
+bool enc_chain_2w(int o1, int nx, uint32_t A) {
+    const uint32_t ntab = o1 ? A * A : 256u;
+    return nx == 4 && ntab * 16u <= ENC_TAB_LDS_MAX;
+}
+uint32_t enc_2w_lds_bytes(int o1, uint32_t A) {
+    return ENC_2W_BASE + (o1 ? A * A : 256u) * 16u;
 }
 
 uint32_t enc_replay_lds_bytes(int o1, uint32_t A) {
@@ -1025,6 +1169,14 @@ hipError_t launch_enc_chain(const EncJob *d_jobs, int njobs, uint32_t lds, hipSt
     static bool attr = false;
     if (!attr) { lds_attr(reinterpret_cast<const void *>(k_enc_chain)); attr = true; }
     hipLaunchKernelGGL(k_enc_chain, dim3(njobs), dim3(64), lds, s, d_jobs);
+    return hipGetLastError();
+}
+
+hipError_t launch_enc_chain2w(const EncJob *d_jobs, int njobs, uint32_t lds, hipStream_t s) {
+    if (!njobs) return hipSuccess;
+    static bool attr = false;
+    if (!attr) { lds_attr(reinterpret_cast<const void *>(k_enc_chain2w)); attr = true; }
+    hipLaunchKernelGGL(k_enc_chain2w, dim3(njobs), dim3(128), lds, s, d_jobs);
     return hipGetLastError();
 }
 

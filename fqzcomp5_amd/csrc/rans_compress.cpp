@@ -582,9 +582,15 @@ void Compressor::stage_encode() {
         uint32_t *d_cnt = g_.arena.alloc_n<uint32_t>(nch);
         const EncJob e{j.d_in, d_tab, d_remap, j.d_end, d_lens + i, d_ck, d_cnt,
                        j.n, j.nx, j.bits, j.A, nch};
-        const uint32_t lds = enc_lds_bytes(j.o1, uint32_t(j.A));
-        if (lds <= 24 * 1024) { ejs.push_back(e); lds_s = std::max(lds_s, lds); }
-        else { ejb.push_back(e); lds_b = std::max(lds_b, lds); }
+        // ejs: two-wave chains (NX=4, table in LDS: the long ones);
+        // ejb: the rest (X32, O1 tables too big for LDS)
+        if (enc_chain_2w(j.o1, j.nx, uint32_t(j.A))) {
+            ejs.push_back(e);
+            lds_s = std::max(lds_s, enc_2w_lds_bytes(j.o1, uint32_t(j.A)));
+        } else {
+            ejb.push_back(e);
+            lds_b = std::max(lds_b, enc_lds_bytes(j.o1, uint32_t(j.A)));
+        }
         const uint32_t per = enc_replay_chunks(j.nx);
         for (uint32_t c0 = 0; c0 < nch; c0 += per) {
             items.push_back(uint32_t(eall.size()));
@@ -600,7 +606,7 @@ void Compressor::stage_encode() {
         const EncJob *d = g_.upload(ejs);
         const EncJob *db = ejb.empty() ? nullptr : g_.upload(ejb);
         g_.fork();
-        FQZ5_HIP(launch_enc_chain(d, int(ejs.size()), lds_s, g_.stream2));
+        FQZ5_HIP(launch_enc_chain2w(d, int(ejs.size()), lds_s, g_.stream2));
         if (db) FQZ5_HIP(launch_enc_chain(db, int(ejb.size()), lds_b, g_.stream));
         g_.join();
     } else if (!ejb.empty()) {
