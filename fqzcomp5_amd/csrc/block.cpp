@@ -369,11 +369,14 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             std::vector<CompressReq> lzr;
             std::vector<std::vector<int>> lzr_of(size_t(nsec), std::vector<int>(FQZ5_M_LAST, -1));
             std::vector<std::exception_ptr> err(2 + nsq);
-            auto on = [](GpuCtx &c, std::exception_ptr &e, auto &&fn) {
-                return std::thread([&c, &e, fn] {
+            auto on = [t0](GpuCtx &c, std::exception_ptr &e, auto &&fn) {
+                return std::thread([&c, &e, fn, t0] {
                     try {
                         FQZ5_HIP(hipSetDevice(c.device));
                         fn();
+                        if (step_trace())
+                            std::fprintf(stderr, "sections_try: helper context %p done at %.1f ms\n",
+                                         static_cast<void *>(&c), now_ms() - t0);
                     } catch (...) {
                         e = std::current_exception();
                     }

@@ -925,8 +925,8 @@ static DEV void dec32_body(const DecJob &J) {
 // xd, the ballot, 6 for the renorm select and ptr (slots stay in VGPRs): no
 // SALU on the chain (a wave issues one instruction per ~4 cycles whatever the
 // unit, so SALU round trips cost as much as VALU ones).
-constexpr uint32_t O0_G = 256;                         // steps per group
-constexpr uint32_t O0_MIRROR = 1040;                   // >= 4*G + 4, slab-unit multiple of 8
+constexpr uint32_t O0_G = 512;                         // steps per group (per-group work: ~2 %)
+constexpr uint32_t O0_MIRROR = 2056;                   // >= 4*G + 4, slab-unit multiple of 8
 constexpr uint32_t O0_RING_BYTES = (RING_WORDS + O0_MIRROR) * 2;
 constexpr uint32_t O0_OBUF_BYTES = 4 * O0_G * 2;       // u16 table indices, lane-major
 constexpr uint32_t O0_SYM_OFF = O0_RING_BYTES + O0_OBUF_BYTES;
@@ -1080,19 +1080,23 @@ static DEV void dec4_lean_body(const DecJob &J) {
             }
         } else if (cnt == NX * G && NX * t0 + NX * G <= n &&
                    (reinterpret_cast<uintptr_t>(J.out) & 15) == 0) {
-            // a whole group: lane l writes output bytes [16l, 16l+16), i.e.
-            // steps 4l..4l+3 of the 4 states, as one 16-byte store
-            uint32_t v[4] = {0, 0, 0, 0};
+            // a whole group: lane l writes output bytes [16l, 16l+16) of each
+            // 1 KB, i.e. steps 4l..4l+3 of the 4 states, as one 16-byte store
 #pragma unroll
-            for (int z = 0; z < NX; z++) {
-                const uint2 q = *reinterpret_cast<const uint2 *>(obuf + z * G + 4 * l);
+            for (uint32_t h = 0; h < G / 256; h++) {
+                uint32_t v[4] = {0, 0, 0, 0};
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t sl = (k & 2 ? q.y : q.x) >> (16 * (k & 1)) & 0xffffu;
-                    v[k] |= uint32_t(s2sym[sl]) << (8 * z);
+                for (int z = 0; z < NX; z++) {
+                    const uint2 q = *reinterpret_cast<const uint2 *>(obuf + z * G + 256 * h + 4 * l);
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t sl = (k & 2 ? q.y : q.x) >> (16 * (k & 1)) & 0xffffu;
+                        v[k] |= uint32_t(s2sym[sl]) << (8 * z);
+                    }
                 }
+                *reinterpret_cast<uint4 *>(J.out + NX * t0 + 1024 * h + 16 * l) =
+                    make_uint4(v[0], v[1], v[2], v[3]);
             }
-            *reinterpret_cast<uint4 *>(J.out + NX * t0 + 16 * l) = make_uint4(v[0], v[1], v[2], v[3]);
         } else {
             const auto out = buf(J.out, n);
             for (uint32_t i = l; i < cnt; i += 64)

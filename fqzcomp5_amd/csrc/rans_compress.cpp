@@ -17,6 +17,7 @@
 // capacity failures (NULL returns) are decided in stage 6 from sizes: they
 // never change the bytes of a successful call.
 #include <algorithm>
+#include <map>
 #include <chrono>
 #include <climits>
 #include <cstdio>
@@ -168,16 +169,27 @@ void Compressor::hist0(const std::vector<std::pair<const uint8_t *, uint32_t>> &
                        std::vector<uint32_t> &counts) {
     counts.assign(segs.size() * 512, 0);
     if (segs.empty()) return;
+    // the candidates of one section share their input: count each distinct
+    // (pointer, length) once
+    std::map<std::pair<const uint8_t *, uint32_t>, uint32_t> uniq;
+    std::vector<uint32_t> of(segs.size());
     std::vector<HistItem> items;
-    for (uint32_t s = 0; s < segs.size(); s++)
+    for (uint32_t s = 0; s < segs.size(); s++) {
+        auto ins = uniq.emplace(segs[s], uint32_t(uniq.size()));
+        of[s] = ins.first->second;
+        if (!ins.second) continue;
         for (uint32_t b = 0; b < segs[s].second; b += HIST_SLICE)
-            items.push_back({segs[s].first, b, std::min(segs[s].second, b + HIST_SLICE), s, 0});
-    uint32_t *d_counts = g_.arena.alloc_n<uint32_t>(counts.size());
-    g_.memset0(d_counts, counts.size() * 4);
+            items.push_back({segs[s].first, b, std::min(segs[s].second, b + HIST_SLICE), of[s], 0});
+    }
+    std::vector<uint32_t> u(uniq.size() * 512);
+    uint32_t *d_counts = g_.arena.alloc_n<uint32_t>(u.size());
+    g_.memset0(d_counts, u.size() * 4);
     if (!items.empty())
         FQZ5_HIP(launch_hist0(g_.upload(items), int(items.size()), d_counts, g_.stream));
-    g_.download(counts.data(), d_counts, counts.size());
+    g_.download(u.data(), d_counts, u.size());
     g_.sync();
+    for (uint32_t s = 0; s < segs.size(); s++)
+        std::memcpy(&counts[size_t(s) * 512], &u[size_t(of[s]) * 512], 2048);
 }
 
 void Compressor::gather(const std::vector<const uint8_t *> &ptrs, std::vector<uint8_t> &out) {
@@ -201,6 +213,9 @@ void Compressor::stage_pack() {
     std::vector<PackItem> items;
     std::vector<uint8_t> codes;
     uint32_t max_out = 0;
+    // leaves packing the same input (e.g. RANS129 and RANS193 of a section)
+    // share one packed copy: same histogram, same codes
+    std::map<std::pair<const uint8_t *, uint32_t>, uint8_t *> packed;
     for (size_t i = 0; i < leaves_.size(); i++) {
         Leaf &L = leaves_[i];
         std::memcpy(L.hist, &cnt[i * 512], 1024);
@@ -218,7 +233,12 @@ void Compressor::stage_pack() {
         L.pmeta_len = ns + 1;
         L.per = ns > 4 ? 2 : ns > 2 ? 4 : ns > 1 ? 8 : 0;
         L.plen = L.per ? (L.n + L.per - 1) / L.per : 0;
-        L.d_packed = g_.arena.alloc_n<uint8_t>(L.plen + 1);
+        auto ins = packed.emplace(std::make_pair(L.d_in, L.n), nullptr);
+        if (!ins.second) {
+            L.d_packed = ins.first->second;
+            continue;
+        }
+        L.d_packed = ins.first->second = g_.arena.alloc_n<uint8_t>(L.plen + 1);
         if (L.per) {
             codes.insert(codes.end(), L.code, L.code + 256);
             items.push_back({L.d_in, L.d_packed, nullptr, L.n, L.per});

@@ -38,10 +38,10 @@ for i in range(512):
     n = k >> 32
     o1rows, nx, mode = ext & 0xffff, (ext >> 16) & 0xff, ext >> 24
     steps = (n - (nx - 1) * (n // nx)) if o1rows else (n + nx - 1) // nx
-    rows.append((b, i, n, o1rows, nx, mode, steps, (b - a) * 10 / max(steps, 1), cyc / max(steps, 1), inl))
+    rows.append((b, i, n, o1rows, nx, mode, steps, lc / max(ls, 1), cyc / max(steps, 1), inl))
 t0 = min(r[0] for r in rows)
 print(f"launch {pr[3]:.1f} ms, {len(rows)} workgroups")
 for r in sorted(rows)[-40:]:
-    b, i, n, o1rows, nx, mode, steps, nsps, cps, inl = r
+    b, i, n, o1rows, nx, mode, steps, loopc, cps, inl = r
     print(f"wg {i:3d} n={n:9d} in={inl:9d} {'O1 rows=' + str(o1rows) if o1rows else 'O0'} nx={nx} mode={mode} "
-          f"steps={steps:9d} end {(b - t0) / 100:8.0f} us  {nsps:6.1f} ns/step {cps:6.1f} cyc/step")
+          f"steps={steps:9d} {cps:6.1f} cyc/step (fast loop {loopc:6.1f})")
