@@ -108,7 +108,7 @@ def method_order(m: int, fixed_len: int) -> int:
     return [0, 1, 64, 65, 128, 129, 192, 193][m - 1] if m <= 8 else (fixed_len << 8) + 9
 
 
-def cpu_baseline(run, tried, meth, gpu_out, threads, fastq_bytes):
+def cpu_baseline(run, tried, meth, gpu_out, threads, fastq_bytes, simd=False):
     """The reference (oracle/_ref) on the same sections and schedule, one
     section per host thread (hts_tpool-style): every tried method of every
     section is compressed, the chosen stream is checked against the GPU's
@@ -118,6 +118,8 @@ def cpu_baseline(run, tried, meth, gpu_out, threads, fastq_bytes):
     from fqzcomp5_amd import sections as S
     kind = "reference" if binding.have_ref() else "port"
     codec = binding.ref() if kind == "reference" else binding.oracle()
+    if simd:   # the reference with its x86 SIMD 32x16 dispatch compiled in
+        codec = binding.ref_simd()
     seqc = None
     reads = run.reads
     secs = []
@@ -322,6 +324,15 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
         out["cpu_baseline"] = cpu_baseline(run, tried[off:off + len(res)],
                                            meth_all[off:off + len(res)], gpu_streams,
                                            cpu_threads, fq_local)
+        # the as-shipped build runs the scalar 32x16 code (its
+        # config.h compiles the CPU dispatcher out); the same workload with
+        # the SSE4/AVX2/AVX-512 dispatch compiled in (oracle/Makefile)
+        from oracle import binding
+        if binding.have_ref_simd():
+            sb = cpu_baseline(run, tried[off:off + len(res)], meth_all[off:off + len(res)],
+                              gpu_streams, cpu_threads, fq_local, simd=True)
+            out["cpu_baseline"]["simd_build"] = {
+                k: sb[k] for k in ("value", "enc_MBps", "dec_MBps", "bytes_match_gpu")}
     del run, reads
     torch.cuda.empty_cache()
     return out

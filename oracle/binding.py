@@ -220,6 +220,22 @@ def ref() -> _Codec:
     return _cache["ref"]
 
 
+REF_SIMD_SO = os.path.join(HERE, "_ref", "libhtsref_simd.so")
+
+
+def have_ref_simd() -> bool:
+    return os.path.exists(REF_SIMD_SO)
+
+
+def ref_simd() -> _Codec:
+    """The reference with its x86 SIMD 32x16 codecs dispatched at run time
+    (oracle/Makefile libhtsref_simd.so; the shipped config.h compiles the
+    dispatcher out)."""
+    if "ref_simd" not in _cache:
+        _cache["ref_simd"] = _Codec(REF_SIMD_SO, "")
+    return _cache["ref_simd"]
+
+
 # ---- sequence context model (fqzcomp5.c:1073-1406) -------------------------
 REF_CLI_SO = os.path.join(HERE, "_ref", "libfqz5ref.so")
 
