@@ -1,4 +1,5 @@
 // capi.cpp — extern "C" entry points (include/fqz5_mi355x.h).
+#include <algorithm>
 #include <atomic>
 #include <climits>
 #include <cstdlib>
@@ -52,6 +53,13 @@ void GpuCtx::copy_stat(const char *kind, const char *file, int line) {
 #endif
 
 static std::atomic<int> g_hedge{-1};
+static std::atomic<int> g_hedging{0};
+HedgeShare::HedgeShare(size_t all) {
+    const int k = g_hedging.fetch_add(1) + 1;
+    cus = std::max<size_t>(1, all / size_t(k));
+}
+HedgeShare::~HedgeShare() { g_hedging.fetch_sub(1); }
+
 bool hedge_chains() {
     int v = g_hedge.load();
     if (v < 0) {

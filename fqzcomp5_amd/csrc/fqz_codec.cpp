@@ -627,7 +627,8 @@ void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
         rj.push_back(*J);
     }
     // hedge: each range chain on 2-4 CUs
-    const size_t copies = hedge_copies(rj.size(), size_t(g.cus));
+    HedgeShare share(size_t(g.cus));
+    const size_t copies = hedge_copies(rj.size(), share.cus);
     if (copies > 1) {
         uint32_t *d_done = g.arena.alloc_n<uint32_t>(rj.size());
         g.memset0(d_done, rj.size() * 4);

@@ -273,6 +273,15 @@ inline std::vector<int> hedge_plan(const std::vector<uint64_t> &steps, size_t cu
     return c;
 }
 
+// Hedged launches in flight in this process (decode chains, fqz range
+// chains).  Concurrent callers (the drop-in CLI's thread pool, several host
+// threads) share the spare CUs: each plans its copies for cus / active.
+struct HedgeShare {
+    size_t cus;
+    explicit HedgeShare(size_t all);
+    ~HedgeShare();
+};
+
 // The calling thread's context (created on first use).
 GpuCtx &gpu();
 // Helper contexts of the calling thread (k < AUX_CTXS), for work run by

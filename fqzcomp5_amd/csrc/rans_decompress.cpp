@@ -373,7 +373,8 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
     // copies fit one per CU (hedge_plan)
     std::vector<uint64_t> steps;
     for (const DecJob &d : djs) steps.push_back(uint64_t(d.n) / uint32_t(d.nx));
-    const std::vector<int> cp = hedge_plan(steps, size_t(g_.cus));
+    HedgeShare share(size_t(g_.cus));          // held until the launch is synchronised
+    const std::vector<int> cp = hedge_plan(steps, share.cus);
     if (std::any_of(cp.begin(), cp.end(), [](int c) { return c > 1; })) {
         const size_t nj = djs.size();
         uint32_t *d_done = g_.arena.alloc_n<uint32_t>(nj);
