@@ -1,0 +1,820 @@
+// tok3.cpp — the read-name tokeniser (htscodecs tokenise_name3.c, the
+// TOK3 name methods of fqzcomp5) behind its own C-ABI:
+// tok3_encode_names / tok3_decode_names, byte-identical to the reference.
+//
+// A block of names becomes up to 128 x 16 byte streams ("descriptors"): per
+// token position, the token types and one stream per type's values, each
+// name tokenised against an earlier name found through a trie of all names
+// (search_trie, tokenise_name3.c:591-695).  The tokenising is a short serial
+// pass over the names on the host (a name's tokens depend on the earlier
+// name and on per-column running counts); the descriptors are then entropy
+// coded as one batch of rANS 4x16 candidates on the GPU (compress():
+// every method the level lists for the stream's type, smallest kept, first
+// on ties, tokenise_name3.c:1268-1417), and decoded as one batch of rANS
+// streams before the names are rebuilt.  use_arith (never set by fqzcomp5,
+// fqzcomp5.c:1433,1490) codes them with arith_dynamic, also on the GPU.
+#include <algorithm>
+#include <cctype>
+#include <climits>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/fqz5_mi355x.h"
+#include "rans_codec.hpp"
+#include "rans_format.hpp"
+
+namespace fqz5 {
+void fqz5_set_error(const char *msg);   // capi.cpp
+namespace {
+
+constexpr int MAX_TOKENS = 128;                 // tokenise_name3.c:75-76
+constexpr int MAX_TBLOCKS = MAX_TOKENS << 4;
+
+enum NameType : int {                           // :81-82
+    N_TYPE = 0, N_ALPHA, N_CHAR, N_DIGITS0, N_DZLEN, N_DUP, N_DIFF,
+    N_DIGITS, N_DDELTA, N_DDELTA0, N_MATCH, N_NOP, N_END, N_ALL
+};
+
+struct Tok { int type = 0, ival = 0, sval = 0; };    // last_context_tok
+struct Last {                                         // last_context
+    const char *name = nullptr;
+    int ntok = 0;
+    std::vector<Tok> tok;
+};
+
+// ---------------------------------------------------------------------------
+// Trie over all names of the block (build_trie / search_trie, :477-695): a
+// node keeps the index of the last name that walked through it (24 bits, as
+// the reference's bitfield), initially the one that created it.
+struct Trie {
+    struct Node { int next = -1, sib = -1; uint8_t c = 0; uint32_t n = 0; };
+    std::vector<Node> nodes{Node()};                   // node 0: the root
+
+    bool build(const char *d, size_t len, uint32_t n) {
+        int t = 0;
+        for (size_t i = 0; i < len && uint8_t(d[i]) > '\n'; i++) {
+            const uint8_t c0 = uint8_t(d[i]);
+            if (c0 & 0x80) return false;               // :498-500
+            const uint8_t c = c0 & 127;
+            int x = nodes[size_t(t)].next, l = -1;
+            while (x >= 0 && nodes[size_t(x)].c != c) { l = x; x = nodes[size_t(x)].sib; }
+            if (x < 0) {
+                Node nn;
+                nn.c = c;
+                nn.n = n & 0xffffffu;
+                nodes.push_back(nn);
+                x = int(nodes.size()) - 1;
+                if (l < 0) nodes[size_t(t)].next = x;
+                else nodes[size_t(l)].sib = x;
+            }
+            t = x;
+        }
+        return true;
+    }
+
+    // -> the name to tokenise against, or -1 (:591-695)
+    int search(const char *data, size_t len, uint32_t n, int *exact, int *is_fixed,
+               int *fixed_len) {
+        int from = -1, p3 = -1;
+        *exact = 0;
+        *fixed_len = 0;
+        *is_fixed = 0;
+        int prefix_len;
+        const char *d = *data == '@' ? data + 1 : data;
+        const int l = *data == '@' ? int(len) - 1 : int(len);
+        const int f = (*data == '>') ? 1 : 0;
+        auto xd = [](char c) { return std::isxdigit(uint8_t(c)) != 0; };
+        if (l > 70 && d[f + 0] == 'm' && d[7] == '_' && d[f + 14] == '_' && d[f + 61] == '/') {
+            prefix_len = 60;                           // PacBio
+            *is_fixed = 0;
+        } else if (l == 17 && d[f + 5] == ':' && d[f + 11] == ':') {
+            prefix_len = 6;                            // IonTorrent
+            *fixed_len = 6;
+            *is_fixed = 1;
+        } else if (l >= 36 && d[f + 8] == '-' && d[f + 13] == '-' && d[f + 18] == '-' &&
+                   d[f + 23] == '-' && xd(d[f + 0]) && xd(d[f + 7]) && xd(d[f + 9]) &&
+                   xd(d[f + 12]) && xd(d[f + 14]) && xd(d[f + 17]) && xd(d[f + 19]) &&
+                   xd(d[f + 22]) && xd(d[f + 24]) && xd(d[f + 35])) {
+            prefix_len = 36;                           // ONT uuid
+            *fixed_len = 36;
+            *is_fixed = 1;
+        } else {                                       // Illumina: lane:tile:x:y
+            int colons = 0;
+            size_t i = 0;
+            for (i = 0; i < len && data[i] > ' '; i++) {}
+            while (i > 0 && colons < 4)
+                if (data[--i] == ':') colons++;
+            if (colons == 4) {
+                *fixed_len = int(i) + 1;
+                prefix_len = int(i) + 1;
+                *is_fixed = 1;
+            } else {
+                prefix_len = INT_MAX;
+                *is_fixed = 0;
+            }
+        }
+        int from_punct = from;
+        int t = 0;
+        for (size_t i = 0; i < len && uint8_t(data[i]) > '\n';) {
+            const uint8_t c0 = uint8_t(data[i++]);
+            if (c0 & 0x80) return -1;
+            const uint8_t c = c0 & 127;
+            int x = nodes[size_t(t)].next;
+            while (x >= 0 && nodes[size_t(x)].c != c) x = nodes[size_t(x)].sib;
+            t = x;                                     // present: built from every name
+            Node &T = nodes[size_t(t)];
+            from = int(T.n);
+            if ((std::ispunct(c) || std::isspace(c)) && T.n != (n & 0xffffffu))
+                from_punct = int(T.n);
+            if (int(i) == prefix_len) p3 = int(T.n);
+            T.n = n & 0xffffffu;
+        }
+        *exact = (int(n & 0xffffffu) != from) && len;
+        return *exact ? from : (p3 != -1 ? p3 : from_punct);
+    }
+};
+
+// ---------------------------------------------------------------------------
+struct Encoder {
+    std::vector<std::vector<uint8_t>> desc = std::vector<std::vector<uint8_t>>(MAX_TBLOCKS);
+    int dcount[MAX_TOKENS] = {0}, icount[MAX_TOKENS] = {0};
+    int max_tok = 1;                                 // create_context (:204)
+    int counter = 0;
+    std::vector<Last> lc;
+    Trie trie;
+
+    void grow_tok(int ntok) {                          // the reference's max_tok resets
+        for (int t = max_tok; t <= ntok; t++) {
+            for (int k = 0; k < 16; k++) desc[size_t(t << 4 | k)].clear();
+            dcount[t] = icount[t] = 0;
+        }
+        max_tok = ntok + 1;
+    }
+    void type(int ntok, int ty) { desc[size_t(ntok << 4)].push_back(uint8_t(ty)); }
+    void tint(int ntok, int ty, uint32_t v) {          // encode_token_int
+        type(ntok, ty);
+        auto &b = desc[size_t(ntok << 4 | ty)];
+        for (int k = 0; k < 4; k++) b.push_back(uint8_t(v >> (8 * k)));
+    }
+    void tint1(int ntok, int ty, uint32_t v) {         // encode_token_int1
+        type(ntok, ty);
+        desc[size_t(ntok << 4 | ty)].push_back(uint8_t(v));
+    }
+    void tint1_(int ntok, int ty, uint32_t v) {        // encode_token_int1_ (no type)
+        desc[size_t(ntok << 4 | ty)].push_back(uint8_t(v));
+    }
+    void alpha(int ntok, const char *s, int len) {
+        type(ntok, N_ALPHA);
+        auto &b = desc[size_t(ntok << 4 | N_ALPHA)];
+        b.insert(b.end(), s, s + len);
+        b.push_back(0);
+    }
+    void chr(int ntok, char c) {
+        type(ntok, N_CHAR);
+        desc[size_t(ntok << 4 | N_CHAR)].push_back(uint8_t(c));
+    }
+
+    // encode_name (:697-1020), mode 1
+    bool name(char *nm, int len) {
+        int is_fixed, fixed_len, exact;
+        const int cnum = counter++;
+        int pnum = trie.search(nm, size_t(len), uint32_t(cnum), &exact, &is_fixed, &fixed_len);
+        if (pnum < 0) pnum = cnum ? cnum - 1 : 0;
+        Last &C = lc[size_t(cnum)];
+        const Last &P = lc[size_t(pnum)];
+        if (exact && size_t(len) == std::strlen(P.name)) {
+            tint(0, N_DUP, uint32_t(cnum - pnum));
+            C.name = nm;
+            C.ntok = P.ntok;
+            C.tok.assign(P.tok.begin(), P.tok.begin() + std::min<size_t>(P.tok.size(), size_t(P.ntok)));
+            C.tok.resize(size_t(std::max(P.ntok, 1)));
+            return true;
+        }
+        C.tok.assign(MAX_TOKENS, Tok());
+        tint(0, N_DIFF, uint32_t(cnum - pnum));
+        int ntok = 1, i;
+        auto ptok = [&](int t) -> const Tok * {
+            return (pnum < cnum && t < P.ntok) ? &P.tok[size_t(t)] : nullptr;
+        };
+        if (fixed_len == 36) {                         // ONT uuid (:735-752)
+            if (37 >= max_tok) grow_tok(37);
+            for (i = 0; i < 36; i++, ntok++) {
+                chr(ntok, nm[i]);
+                C.tok[size_t(ntok)] = {N_CHAR, nm[i], 0};
+            }
+            is_fixed = 0;
+            i = 36;
+        } else if (is_fixed) {                         // :753-773
+            if (ntok >= max_tok) grow_tok(ntok);
+            const Tok *pt = ptok(ntok);
+            if (pt && pt->type == N_ALPHA && pt->ival == fixed_len &&
+                std::memcmp(nm, P.name, size_t(fixed_len)) == 0)
+                type(ntok, N_MATCH);
+            else
+                alpha(ntok, nm, fixed_len);
+            C.tok[size_t(ntok++)] = {N_ALPHA, fixed_len, 0};
+            i = fixed_len;
+        } else {
+            i = 0;
+        }
+        for (; i < len; i++) {
+            if (ntok >= max_tok) {
+                if (max_tok >= MAX_TOKENS) return false;
+                grow_tok(ntok);
+            }
+            const uint8_t ci = uint8_t(nm[i]);
+            bool as_char = false;
+            if (std::isalpha(ci)) {                    // :791-838
+                int s = i + 1;
+                while (s < len && (std::isalpha(uint8_t(nm[s])) || std::ispunct(uint8_t(nm[s])))) s++;
+                if (s - i == 1) {
+                    as_char = true;
+                } else {
+                    const Tok *pt = ptok(ntok);
+                    if (pt && pt->type == N_ALPHA && s - i == pt->ival &&
+                        std::memcmp(&nm[i], &P.name[pt->sval], size_t(s - i)) == 0)
+                        type(ntok, N_MATCH);
+                    else
+                        alpha(ntok, &nm[i], s - i);
+                    C.tok[size_t(ntok)] = {N_ALPHA, s - i, i};
+                    i = s - 1;
+                }
+            } else if (std::isdigit(ci)) {
+                // digits (:839-943); a leading 0, or the previous name's
+                // token being DIGITS0 of the same length, codes DIGITS0
+                uint32_t s = uint32_t(i), v = 0;
+                while (s < uint32_t(len) && std::isdigit(uint8_t(nm[s])) && s - uint32_t(i) < 9) {
+                    v = v * 10 + uint32_t(nm[s] - '0');
+                    s++;
+                }
+                const uint32_t dl = s - uint32_t(i);
+                const Tok *pt = ptok(ntok);
+                const bool zero = ci == '0' || (pt && pt->type == N_DIGITS0 && uint32_t(pt->sval) == dl);
+                if (zero) {
+                    if (pt && pt->type == N_DIGITS0) {
+                        const int d = int(v - uint32_t(pt->ival));
+                        if (d == 0 && uint32_t(pt->sval) == dl) {
+                            type(ntok, N_MATCH);
+                        } else if (d < 256 && d >= 0 && uint32_t(pt->sval) == dl) {
+                            tint1(ntok, N_DDELTA0, uint32_t(d));
+                        } else {
+                            tint1_(ntok, N_DZLEN, dl);
+                            tint(ntok, N_DIGITS0, v);
+                        }
+                    } else {
+                        tint1_(ntok, N_DZLEN, dl);
+                        tint(ntok, N_DIGITS0, v);
+                    }
+                    C.tok[size_t(ntok)] = {N_DIGITS0, int(v), int(dl)};
+                } else {
+                    if (pt && pt->type == N_DIGITS) {
+                        const int d = int(v - uint32_t(pt->ival));
+                        if (d == 0) {
+                            type(ntok, N_MATCH);
+                        } else if (d < 256 && d >= 0 && (5 + dcount[ntok]) > icount[ntok]) {
+                            tint1(ntok, N_DDELTA, uint32_t(d));
+                            dcount[ntok]++;
+                        } else {
+                            tint(ntok, N_DIGITS, v);
+                            icount[ntok]++;
+                        }
+                    } else {
+                        tint(ntok, N_DIGITS, v);
+                    }
+                    // token_str keeps whatever this slot held (:939-941)
+                    C.tok[size_t(ntok)].type = N_DIGITS;
+                    C.tok[size_t(ntok)].ival = int(v);
+                }
+                i = int(s) - 1;
+            } else {
+                as_char = true;
+            }
+            if (as_char) {                             // n_char (:944-967)
+                const Tok *pt = ptok(ntok);
+                if (pt && pt->type == N_CHAR && nm[i] == char(pt->ival))
+                    type(ntok, N_MATCH);
+                else
+                    chr(ntok, nm[i]);
+                C.tok[size_t(ntok)].type = N_CHAR;
+                C.tok[size_t(ntok)].ival = nm[i];
+            }
+            ntok++;
+        }
+        if (ntok >= max_tok) {
+            if (max_tok >= MAX_TOKENS) return false;
+            grow_tok(ntok);
+        }
+        type(ntok, N_END);
+        C.name = nm;
+        C.ntok = ntok;
+        C.tok.resize(size_t(ntok + 1));
+        return true;
+    }
+};
+
+// compress()'s method lists (:1281-1358), by level (1-9 -> 0-4) and type
+const int METH[5][N_ALL][7] = {
+    {{1, 128}, {1, 129}, {1, 0}, {1, 8}, {1, 0}, {1, 8}, {1, 8}, {1, 8}, {1, 0}, {1, 128},
+     {1, 0}, {1, 0}, {1, 0}},
+    {{2, 192, 0}, {2, 129, 1}, {1, 0}, {2, 128 + 8, 0}, {1, 0}, {1, 192 + 8}, {1, 128 + 8},
+     {1, 192 + 8}, {1, 0}, {1, 128}, {1, 0}, {1, 0}, {1, 0}},
+    {{2, 192, 0}, {4, 1, 128, 0, 129}, {1, 0}, {2, 200, 0}, {1, 0}, {1, 200}, {2, 192, 200},
+     {2, 132, 201}, {1, 0}, {1, 128}, {1, 0}, {1, 0}, {1, 0}},
+    {{3, 193, 0, 1}, {5, 128, 1, 128, 0, 129}, {2, 1, 0}, {2, 200, 0}, {1, 0}, {1, 201},
+     {2, 192, 200}, {2, 132, 201}, {1, 0}, {1, 128}, {1, 0}, {1, 0}, {1, 0}},
+    {{6, 192, 0, 1, 65, 193, 132}, {4, 132, 1, 0, 129}, {3, 1, 0, 192}, {4, 201, 0, 192, 64},
+     {3, 0, 128, 1}, {1, 201}, {3, 192, 201, 65}, {6, 132, 201, 1, 192, 129, 193},
+     {3, 1, 0, 192}, {3, 192, 1, 0}, {1, 0}, {1, 0}, {1, 0}},
+};
+
+#define GUARD_BEGIN try {
+#define GUARD_END(failret)                                                    \
+    }                                                                         \
+    catch (const std::exception &e) {                                         \
+        fqz5_set_error(e.what());                                             \
+        return failret;                                                       \
+    }
+
+int put_varint(uint8_t *out, uint32_t v) {
+    uint8_t tmp[8];
+    const int k = varint_put(tmp, nullptr, v);
+    std::memcpy(out, tmp, size_t(k));
+    return k;
+}
+
+}  // namespace
+}  // namespace fqz5
+
+using namespace fqz5;
+
+extern "C" {
+
+uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *out_len,
+                           int *last_start_p) {
+    if (len < 0) {
+        *out_len = 0;
+        return nullptr;
+    }
+    GUARD_BEGIN
+    int nreads = 0, last_start = 0, i, j;
+    for (i = 0; i < len; i++)
+        if (blk[i] <= '\n') nreads++;
+    if (nreads <= 0 || nreads > 10000000) return nullptr;   // create_context (:172-187)
+    Encoder E;
+    E.lc.resize(size_t(nreads) + 1);
+    int ctr = 0;                                       // the trie of all names (:1469-1482)
+    for (i = j = 0; i < len; j = ++i) {
+        while (i < len && blk[i] > '\n') i++;
+        if (i >= len) break;
+        last_start = i + 1;
+        if (!E.trie.build(&blk[j], size_t(i - j), uint32_t(ctr++))) return nullptr;
+    }
+    if (last_start_p) *last_start_p = last_start;
+    for (i = j = 0; i < len; j = ++i) {                // names (:1487-1505)
+        while (i < len && static_cast<signed char>(blk[i]) >= ' ') i++;
+        if (i >= len) break;
+        if (blk[i] != '\0' && blk[i] != '\n') return nullptr;
+        blk[i] = '\0';
+        if (!E.name(&blk[j], i - j)) return nullptr;
+    }
+    // drop the type stream of a column that is all MATCH bar its first
+    // entry while the column has other streams (:1531-1553)
+    for (i = 0; i < E.max_tok * 16; i += 16) {
+        std::vector<uint8_t> &b = E.desc[size_t(i)];
+        if (b.empty()) continue;
+        size_t z = 1;
+        while (z < b.size() && b[z] == N_MATCH) z++;
+        if (z == b.size()) {
+            int k = 1;
+            while (k < 16 && E.desc[size_t(i + k)].empty()) k++;
+            if (k < 16) b.clear();
+        }
+    }
+    // every stream's candidate methods, one GPU batch (compress(), :1268-1417)
+    const int lv = std::min(std::max((level - 1) / 2, 0), 4);
+    GpuCtx &g = gpu();
+    std::vector<int> sid;                             // descriptor per stream
+    std::vector<uint32_t> cap;
+    std::vector<std::vector<std::pair<int, int>>> cand(size_t(E.max_tok * 16));   // (method, request)
+    std::vector<CompressReq> reqs;
+    std::vector<int> arith_m;
+    for (i = 0; i < E.max_tok * 16; i++) {
+        const std::vector<uint8_t> &b = E.desc[size_t(i)];
+        if (b.empty()) continue;
+        int meth[7];
+        std::memcpy(meth, METH[lv][i & 15], sizeof(meth));
+        if (use_arith && lv == 1 && (i & 15) == N_DIGITS) meth[1] = 201;   // :1364
+        const uint32_t ocap = uint32_t(1.5 * arith_compress_bound(unsigned(b.size()), 1));
+        const uint8_t *d_in = g.upload(b.data(), b.size());
+        for (int m = 1; m <= meth[0]; m++) {
+            int mm = meth[m];
+            if (!use_arith && (mm & 4)) mm &= ~4;
+            if (b.size() % 4 != 0 && (mm & 8)) continue;
+            CompressReq r;
+            r.d_in = d_in;
+            r.n = uint32_t(b.size());
+            r.order = mm;
+            r.cap = ocap > 6 ? ocap - 6 : 0;
+            cand[size_t(i)].push_back({mm, int(reqs.size())});
+            reqs.push_back(std::move(r));
+        }
+    }
+    std::vector<std::vector<uint8_t>> comp(size_t(E.max_tok * 16));
+    if (!use_arith) {
+        compress_batch(g, reqs);
+        for (i = 0; i < E.max_tok * 16; i++) {
+            if (E.desc[size_t(i)].empty()) continue;
+            int best = -1;
+            uint64_t best_sz = UINT64_MAX;
+            for (auto &c : cand[size_t(i)]) {
+                CompressReq &r = reqs[size_t(c.second)];
+                if (!r.ok) {                            // rans_encode failed (:1383-1386)
+                    g.reset();
+                    return nullptr;
+                }
+                uint8_t v[8];
+                const uint64_t sz = uint64_t(layout_size(r.out)) + uint64_t(put_varint(v, layout_size(r.out)));
+                if (best_sz > sz) { best_sz = sz; best = c.second; }
+            }
+            CompressReq &r = reqs[size_t(best)];
+            const uint32_t olen = layout_size(r.out);
+            std::vector<uint8_t> &o = comp[size_t(i)];
+            o.resize(8 + olen);
+            const int nb = put_varint(o.data(), olen);
+            write_layout_host(g, r.out, o.data() + nb);
+            o.resize(size_t(nb) + olen);
+        }
+        g.reset();
+    } else {
+        g.reset();
+        for (i = 0; i < E.max_tok * 16; i++) {
+            std::vector<uint8_t> &b = E.desc[size_t(i)];
+            if (b.empty()) continue;
+            uint64_t best_sz = UINT64_MAX;
+            const uint32_t ocap = uint32_t(1.5 * arith_compress_bound(unsigned(b.size()), 1));
+            std::vector<uint8_t> out(ocap + 8);
+            for (auto &c : cand[size_t(i)]) {          // arith_encode (:1214-1224)
+                unsigned olen = ocap - 6;
+                if (!arith_compress_to(b.data(), unsigned(b.size()), out.data() + 6, &olen, c.first))
+                    return nullptr;
+                uint8_t v[8];
+                const int nb = put_varint(v, olen);
+                if (best_sz > uint64_t(olen) + uint64_t(nb)) {
+                    best_sz = uint64_t(olen) + uint64_t(nb);
+                    comp[size_t(i)].assign(v, v + nb);
+                    comp[size_t(i)].insert(comp[size_t(i)].end(), out.data() + 6, out.data() + 6 + olen);
+                }
+            }
+        }
+    }
+    // serialise, with streams equal to an earlier one as references (:1559-1657)
+    uint32_t tot = 9;
+    std::vector<int> dup(size_t(E.max_tok * 16), -1);
+    for (i = 0; i < E.max_tok * 16; i++) {
+        if (E.desc[size_t(i)].empty()) continue;
+        const std::vector<uint8_t> &ci = comp[size_t(i)];
+        for (j = 0; j < i; j++) {
+            const std::vector<uint8_t> &cj = comp[size_t(j)];
+            if (E.desc[size_t(j)].empty() || ci.size() != cj.size() || ci.size() <= 4) continue;
+            if (std::memcmp(ci.data(), cj.data(), ci.size()) == 0) break;
+        }
+        if (j < i) { dup[size_t(i)] = j; tot += 3; }
+        else tot += uint32_t(ci.size()) + 1;
+    }
+    uint8_t *out = static_cast<uint8_t *>(malloc(size_t(tot) + 13));
+    if (!out) return nullptr;
+    uint8_t *cp = out;
+    for (int k = 0; k < 4; k++) *cp++ = uint8_t(uint32_t(last_start) >> (8 * k));
+    for (int k = 0; k < 4; k++) *cp++ = uint8_t(uint32_t(nreads) >> (8 * k));
+    *cp++ = uint8_t(use_arith);
+    int last_tnum = -1;
+    for (i = 0; i < E.max_tok * 16; i++) {
+        if (E.desc[size_t(i)].empty()) continue;
+        uint8_t t8 = uint8_t(i & 15);
+        if ((i >> 4) != last_tnum) { t8 |= 128; last_tnum = i >> 4; }
+        if (dup[size_t(i)] >= 0) {
+            *cp++ = t8 | 64;
+            *cp++ = uint8_t(dup[size_t(i)] >> 4);
+            *cp++ = uint8_t(dup[size_t(i)] & 15);
+        } else {
+            *cp++ = t8;
+            std::memcpy(cp, comp[size_t(i)].data(), comp[size_t(i)].size());
+            cp += comp[size_t(i)].size();
+        }
+    }
+    *out_len = int(tot);
+    return out;
+    GUARD_END(nullptr)
+}
+
+uint8_t *tok3_decode_names(uint8_t *in, uint32_t sz, uint32_t *out_len) {
+    if (sz < 9) return nullptr;
+    GUARD_BEGIN
+    const int ulen0 = int(uint32_t(in[0]) | uint32_t(in[1]) << 8 | uint32_t(in[2]) << 16 |
+                          uint32_t(in[3]) << 24);
+    if (ulen0 < 0 || ulen0 >= INT_MAX - 1024) return nullptr;
+    const int nreads = int(uint32_t(in[4]) | uint32_t(in[5]) << 8 | uint32_t(in[6]) << 16 |
+                           uint32_t(in[7]) << 24);
+    const int use_arith = in[8];
+    if (nreads <= 0 || nreads > 10000000) return nullptr;   // create_context (:172-187)
+    // streams: raw bytes, the descriptor they fill and (for coded ones)
+    // their compressed position (:1696-1807)
+    struct D { std::vector<uint8_t> buf; size_t l = 0; bool have = false; };
+    std::vector<D> desc(MAX_TBLOCKS);
+    struct Coded { int i; uint32_t off, clen, ulen; };
+    std::vector<Coded> coded;
+    struct Copy { int i, j; bool col0; };
+    std::vector<std::pair<int, int>> order;            // (kind 0 coded / 1 copy / 2 col0, index)
+    std::vector<Copy> copies;
+    int tnum = -1, max_tok = 1;
+    uint32_t o = 9;
+    auto col0 = [&](int t, int ty) {                   // an elided type stream: ty then MATCH
+        D &c = desc[size_t(t << 4)];
+        c.buf.assign(size_t(std::max(nreads, 1)), uint8_t(N_MATCH));
+        if (nreads > 0) c.buf[0] = uint8_t(ty);
+        c.buf.resize(size_t(nreads));
+        c.have = true;
+    };
+    while (o < sz) {
+        const uint8_t tt = in[o++];
+        if (tt & 64) {
+            if (o + 2 > sz) return nullptr;
+            int j = in[o++] << 4;
+            j += in[o++];
+            if (tt & 128) {
+                if (++tnum >= MAX_TOKENS) return nullptr;
+                max_tok = tnum + 1;
+                for (int k = 0; k < 16; k++) desc[size_t(tnum << 4 | k)] = D();
+            }
+            if ((tt & 15) != 0 && (tt & 128)) {
+                if (tnum < 0) return nullptr;
+                order.push_back({2, tnum << 4 | (tt & 15)});
+            }
+            if (tnum < 0) return nullptr;
+            const int i = (tnum << 4) | (tt & 15);
+            if (j >= i) return nullptr;
+            copies.push_back({i, j, false});
+            order.push_back({1, int(copies.size()) - 1});
+            continue;
+        }
+        if (tt & 128) {
+            if (++tnum >= MAX_TOKENS) return nullptr;
+            max_tok = tnum + 1;
+            for (int k = 0; k < 16; k++) desc[size_t(tnum << 4 | k)] = D();
+        }
+        if ((tt & 15) != 0 && (tt & 128)) {
+            if (tnum < 0) return nullptr;
+            order.push_back({2, tnum << 4 | (tt & 15)});
+        }
+        // uncompressed_size (:1419-1429): varint clen, then the codec's order
+        // byte and its varint size
+        uint32_t clen = 0, ul = 0;
+        const int nb = varint_get(in + o, in + sz, &clen);
+        if (!nb || o + uint32_t(nb) + 1 > sz) return nullptr;
+        if (!varint_get(in + o + nb + 1, in + sz, &ul)) return nullptr;
+        if (tnum < 0 || ul >= uint32_t(INT_MAX)) return nullptr;
+        const int i = (tnum << 4) | (tt & 15);
+        // the codec sees the rest of the block (:1792); clen only advances
+        coded.push_back({i, o + uint32_t(nb), sz - o - uint32_t(nb), ul});
+        order.push_back({0, int(coded.size()) - 1});
+        if (uint64_t(o) + uint64_t(nb) + clen >= sz) break;
+        o += uint32_t(nb) + clen;
+    }
+    // decode every coded stream in one batch
+    std::vector<std::vector<uint8_t>> dec(coded.size());
+    if (!use_arith) {
+        GpuCtx &g = gpu();
+        std::vector<DecompressReq> reqs;
+        const uint8_t *d_all = g.upload(in, sz);
+        for (const Coded &c : coded) {
+            DecompressReq r;
+            r.h_in = in + c.off;
+            r.d_in = d_all + c.off;
+            r.in_size = c.clen;
+            r.out_cap = c.ulen;
+            r.d_out = g.arena.alloc_n<uint8_t>(size_t(c.ulen) + 1);
+            reqs.push_back(r);
+        }
+        decompress_batch(g, reqs);
+        for (size_t k = 0; k < coded.size(); k++) {
+            if (!reqs[k].ok || reqs[k].out_size != coded[k].ulen) { g.reset(); return nullptr; }
+            dec[k].resize(coded[k].ulen);
+            g.download(dec[k].data(), reqs[k].d_out, coded[k].ulen);
+        }
+        g.sync();
+        g.reset();
+    } else {
+        for (size_t k = 0; k < coded.size(); k++) {
+            unsigned ol = coded[k].ulen;
+            dec[k].resize(size_t(ol) + 1);
+            if (!arith_uncompress_to(in + coded[k].off, coded[k].clen, dec[k].data(), &ol) ||
+                ol != coded[k].ulen)
+                return nullptr;
+            dec[k].resize(ol);
+        }
+    }
+    for (auto &e : order) {                            // in stream order, as the reference
+        if (e.first == 2) {
+            col0(e.second >> 4, e.second & 15);
+        } else if (e.first == 1) {
+            const Copy &c = copies[size_t(e.second)];
+            if (!desc[size_t(c.j)].have) return nullptr;
+            desc[size_t(c.i)].buf = desc[size_t(c.j)].buf;
+            desc[size_t(c.i)].have = true;
+            desc[size_t(c.i)].l = 0;
+        } else {
+            const Coded &c = coded[size_t(e.second)];
+            desc[size_t(c.i)].buf = std::move(dec[size_t(e.second)]);
+            desc[size_t(c.i)].have = true;
+            desc[size_t(c.i)].l = 0;
+        }
+    }
+    // decode_name per name (:1023-1212)
+    auto dtype = [&](int ntok) -> int {
+        D &d = desc[size_t(ntok << 4)];
+        if (d.l >= d.buf.size()) return -1;
+        return d.buf[d.l++];
+    };
+    auto dint = [&](int ntok, int ty, uint32_t *v) -> bool {
+        D &d = desc[size_t(ntok << 4 | ty)];
+        if (d.l + 4 > d.buf.size()) return false;
+        const uint8_t *p = d.buf.data() + d.l;
+        *v = uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+        d.l += 4;
+        return true;
+    };
+    auto dint1 = [&](int ntok, int ty, uint32_t *v) -> bool {
+        D &d = desc[size_t(ntok << 4 | ty)];
+        if (d.l >= d.buf.size()) return false;
+        *v = d.buf[d.l++];
+        return true;
+    };
+    auto fixed = [](char *cp, uint32_t v, uint8_t l) -> int {   // append_uint32_fixed (:233)
+        if (l <= 9) {
+            uint32_t p = 1;
+            for (int k = 1; k < l; k++) p *= 10;
+            for (; p; p /= 10) { *cp++ = char(v / p + '0'); v %= p; }
+        }
+        return l;
+    };
+    auto var = [](char *cp, uint32_t v) {              // append_uint32_var (v = 0 writes nothing)
+        char t[12];
+        int n = 0;
+        while (v) { t[n++] = char('0' + v % 10); v /= 10; }
+        for (int k = 0; k < n; k++) cp[k] = t[n - 1 - k];
+        return n;
+    };
+    int64_t ulen = int64_t(ulen0) + 1024;
+    std::vector<char> outb(static_cast<size_t>(ulen));
+    std::vector<Last> lc(size_t(nreads) + 1);          // max_names = nreads + 1 (:190)
+    size_t osz = 0;
+    int counter = 0, ret = 0;
+    for (;;) {
+        char *nm = outb.data() + osz;
+        const int64_t nlen = ulen;
+        ret = -1;
+        const int cnum = counter++;
+        if (cnum > nreads) { ret = -1; break; }
+        const int t0 = dtype(0);
+        if (t0 < 0 || t0 >= max_tok * 16) { ret = 0; break; }
+        uint32_t dist;
+        if (!dint(0, t0, &dist) || int64_t(dist) > cnum) break;
+        int pnum = cnum - int(dist);
+        if (pnum < 0) pnum = 0;
+        Last &C = lc[size_t(cnum)];
+        const Last &P = lc[size_t(pnum)];
+        if (t0 == N_DUP) {
+            if (pnum == cnum) break;
+            const size_t pl = std::strlen(P.name);
+            if (int64_t(pl) + 1 >= nlen) break;
+            std::memcpy(nm, P.name, pl + 1);
+            C.name = nm;
+            C.ntok = P.ntok;
+            C.tok = P.tok;
+            ret = int(pl) + 1;
+        } else {
+            *nm = 0;
+            int64_t len = 0;
+            C.tok.assign(MAX_TOKENS, Tok());
+            int ntok;
+            bool done = false, bad = false;
+            for (ntok = 1; ntok < MAX_TOKENS && ntok < max_tok && !done && !bad; ntok++) {
+                uint32_t v, vl;
+                const int tok = dtype(ntok);
+                C.ntok = 0;
+                Tok &T = C.tok[size_t(ntok)];
+                const Tok *pt = ntok < P.ntok ? &P.tok[size_t(ntok)] : nullptr;
+                switch (tok) {
+                case N_CHAR:
+                    if (len + 1 >= nlen || !dint1(ntok, N_CHAR, &v)) { bad = true; break; }
+                    nm[len] = char(v);
+                    T.type = N_CHAR;
+                    T.ival = nm[len++];
+                    break;
+                case N_ALPHA: {
+                    D &d = desc[size_t(ntok << 4 | N_ALPHA)];
+                    if (d.l >= d.buf.size()) { bad = true; break; }
+                    int64_t l2 = 0;
+                    char c;
+                    const int64_t maxl = nlen - len;
+                    do {
+                        c = char(d.buf[d.l++]);
+                        nm[len + l2++] = c;
+                    } while (c && l2 < maxl && d.l < d.buf.size());
+                    T.type = N_ALPHA;
+                    T.sval = int(len);
+                    T.ival = int(l2 - 1);
+                    len += l2 - 1;
+                    break;
+                }
+                case N_DIGITS0:
+                    if (!dint1(ntok, N_DZLEN, &vl) || !dint(ntok, N_DIGITS0, &v)) { bad = true; break; }
+                    if (len + 20 + int64_t(vl) >= nlen) { bad = true; break; }
+                    len += fixed(nm + len, v, uint8_t(vl));
+                    T = {N_DIGITS0, int(v), int(vl)};
+                    break;
+                case N_DDELTA0:
+                    if (!pt || !dint1(ntok, N_DDELTA0, &v)) { bad = true; break; }
+                    v += uint32_t(pt->ival);
+                    if (len + pt->sval + 1 >= nlen) { bad = true; break; }
+                    len += fixed(nm + len, v, uint8_t(pt->sval));
+                    T = {N_DIGITS0, int(v), pt->sval};
+                    break;
+                case N_DIGITS:
+                    if (!dint(ntok, N_DIGITS, &v) || len + 20 >= nlen) { bad = true; break; }
+                    len += var(nm + len, v);
+                    T.type = N_DIGITS;
+                    T.ival = int(v);
+                    break;
+                case N_DDELTA:
+                    if (!pt || !dint1(ntok, N_DDELTA, &v)) { bad = true; break; }
+                    v += uint32_t(pt->ival);
+                    if (len + 20 >= nlen) { bad = true; break; }
+                    len += var(nm + len, v);
+                    T.type = N_DIGITS;
+                    T.ival = int(v);
+                    break;
+                case N_NOP:
+                    T.type = N_NOP;
+                    break;
+                case N_MATCH:
+                    if (!pt) { bad = true; break; }
+                    switch (pt->type) {
+                    case N_CHAR:
+                        if (len + 1 >= nlen) { bad = true; break; }
+                        nm[len++] = char(pt->ival);
+                        T.type = N_CHAR;
+                        T.ival = pt->ival;
+                        break;
+                    case N_ALPHA:
+                        if (pt->ival < 0 || len + pt->ival >= nlen) { bad = true; break; }
+                        std::memcpy(nm + len, P.name + pt->sval, size_t(pt->ival));
+                        T = {N_ALPHA, pt->ival, int(len)};
+                        len += pt->ival;
+                        break;
+                    case N_DIGITS:
+                        if (len + 20 >= nlen) { bad = true; break; }
+                        len += var(nm + len, uint32_t(pt->ival));
+                        T.type = N_DIGITS;
+                        T.ival = pt->ival;
+                        break;
+                    case N_DIGITS0:
+                        if (len + pt->sval >= nlen) { bad = true; break; }
+                        len += fixed(nm + len, uint32_t(pt->ival), uint8_t(pt->sval));
+                        T = {N_DIGITS0, pt->ival, pt->sval};
+                        break;
+                    default:
+                        bad = true;
+                    }
+                    break;
+                default:                                // an elided N_END
+                case N_END:
+                    if (len + 1 >= nlen) { bad = true; break; }
+                    nm[len++] = 0;
+                    T.type = N_END;
+                    C.name = nm;
+                    C.ntok = ntok;
+                    C.tok.resize(size_t(ntok + 1));
+                    done = true;
+                    ret = int(len);
+                    break;
+                }
+            }
+            if (!done) ret = -1;
+        }
+        if (ret <= 0) break;
+        osz += size_t(ret);
+        ulen -= ret;
+    }
+    if (ret < 0) return nullptr;
+    uint8_t *out = static_cast<uint8_t *>(malloc(std::max<size_t>(osz, 1)));
+    if (!out) return nullptr;
+    std::memcpy(out, outb.data(), osz);
+    *out_len = uint32_t(osz);
+    return out;
+    GUARD_END(nullptr)
+}
+
+}  // extern "C"

@@ -363,3 +363,39 @@ def crc32_dev(ptr: int, n: int, crc: int = 0) -> int:
     if load().fqz5_crc32_dev(crc, C.c_void_p(ptr), n, C.byref(out)):
         raise NativeError("fqz5_crc32_dev failed: " + last_error())
     return int(out.value)
+
+
+def tok3_encode(names: bytes, level: int, use_arith: int = 0):
+    """tok3_encode_names (tokenise_name3.c:1451): tokenised on the host, the
+    token streams entropy coded as one GPU batch.  Works on a private copy
+    of `names` (the codec rewrites terminators): (stream, last_start), or
+    None where the reference returns NULL."""
+    so = load()
+    f = so.tok3_encode_names
+    f.restype = C.c_void_p
+    f.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
+                  C.POINTER(C.c_int)]
+    buf = C.create_string_buffer(bytes(names), max(len(names), 1))
+    n, ls = C.c_int(0), C.c_int(-1)
+    p = f(buf, len(names), level, use_arith, C.byref(n), C.byref(ls))
+    if not p:
+        return None
+    out = C.string_at(p, n.value)
+    _libc.free(p)
+    return out, ls.value
+
+
+def tok3_decode(comp: bytes) -> bytes | None:
+    """tok3_decode_names (tokenise_name3.c:1679): the '\\0'-terminated
+    names, or None on a malformed stream."""
+    so = load()
+    f = so.tok3_decode_names
+    f.restype = C.c_void_p
+    f.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_uint32)]
+    n = C.c_uint32(0)
+    p = f(bytes(comp), len(comp), C.byref(n))
+    if not p:
+        return None
+    out = C.string_at(p, n.value)
+    _libc.free(p)
+    return out

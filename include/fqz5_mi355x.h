@@ -175,6 +175,23 @@ unsigned char *arith_uncompress_to(unsigned char *in, unsigned int in_size,
 unsigned char *arith_uncompress(unsigned char *in, unsigned int in_size,
                                 unsigned int *out_size);
 
+/* ---- tok3 read-name tokeniser (tokenise_name3.h:43-75) ----------------- */
+
+/* Replaces tok3_encode_names (tokenise_name3.c:1451).  `blk` holds names
+ * terminated by '\n' or '\0' (rewritten to '\0' in place).  level 1-9
+ * selects the per-type rANS / arith method lists of compress()
+ * (tokenise_name3.c:1281-1358); use_arith codes the streams with
+ * arith_dynamic.  Returns a malloc()ed buffer of *out_len bytes, or NULL
+ * (more than 128 tokens, a byte >= 0x80, a codec failure).  *last_start_p
+ * (when not NULL) receives the offset after the last terminator. */
+uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith,
+                           int *out_len, int *last_start_p);
+
+/* Replaces tok3_decode_names (tokenise_name3.c:1675).  Returns the
+ * '\0'-terminated names, malloc()ed, *out_len bytes; NULL on a malformed
+ * stream. */
+uint8_t *tok3_decode_names(uint8_t *in, uint32_t sz, uint32_t *out_len);
+
 /* ---- Part 2: batched device API --------------------------------------- */
 
 /* One stream.  `in`/`out` are device pointers. */

@@ -123,6 +123,28 @@ class _Codec:
         p = self._ru(bytes(comp), len(comp), C.byref(n))
         return self._take(p, n.value)
 
+    def tok3_encode(self, names: bytes, level: int, use_arith: int = 0):
+        """tok3_encode_names (tokenise_name3.c:1451) on a private copy of
+        `names`: (stream, last_start), or None where it returns NULL."""
+        f = getattr(self.lib, self._prefix + "tok3_encode_names")
+        f.restype = C.c_void_p
+        f.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
+                      C.POINTER(C.c_int)]
+        buf = C.create_string_buffer(bytes(names), max(len(names), 1))
+        n, ls = C.c_int(0), C.c_int(-1)
+        p = f(buf, len(names), level, use_arith, C.byref(n), C.byref(ls))
+        return None if not p else (self._take(p, n.value), ls.value)
+
+    def tok3_decode(self, comp: bytes):
+        """tok3_decode_names (tokenise_name3.c:1679): the '\\0'-terminated
+        names, or None."""
+        f = getattr(self.lib, self._prefix + "tok3_decode_names")
+        f.restype = C.c_void_p
+        f.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_uint32)]
+        n = C.c_uint32(0)
+        p = f(bytes(comp), len(comp), C.byref(n))
+        return None if not p else self._take(p, n.value)
+
     def _slice(self, lens, flags, seq: bytes | None):
         import numpy as np
         nr = len(lens)
