@@ -1,10 +1,12 @@
 """Drop-in integration on the GPU: the reference fqzcomp5 CLI relinked with
-libfqz5_mi355x.so in place of its rANS 4x16/32x16 and fqzcomp_qual objects
-(oracle/Makefile target _ref/fqzcomp5_gpu) must write the
-same .fqz5 bytes as the CLI built as shipped, and decode them back to the
-input.  Every rANS call fqzcomp5 makes (sequence, quality, lengths, tok3
-name columns, compressed O1 headers) and every fqz_compress /
-fqz_decompress (-5 quality methods) then runs on the GPU."""
+libfqz5_mi355x.so in place of its rANS 4x16/32x16, fqzcomp_qual,
+arith_dynamic and tokenise_name3 objects (oracle/Makefile target
+_ref/fqzcomp5_gpu) must write the same .fqz5 bytes as the
+CLI built as shipped, and decode them back to the input.  Every rANS call
+fqzcomp5 makes (sequence, quality, lengths, compressed O1 headers), every
+tok3_encode_names / tok3_decode_names (TOK3 name methods, -3 up) and every
+fqz_compress / fqz_decompress (-5 up quality methods) then runs through
+the GPU library."""
 import os
 import subprocess
 
@@ -37,7 +39,7 @@ def _inputs(tmp):
     return ins + [syn]
 
 
-@pytest.mark.parametrize("level", ["-1", "-3", "-5"])
+@pytest.mark.parametrize("level", ["-1", "-3", "-5", "-7", "-9"])
 def test_cli_bytes_match(tmp_path, level):
     for src in _inputs(str(tmp_path)):
         a, b = str(tmp_path / "cpu.fqz5"), str(tmp_path / "gpu.fqz5")
