@@ -26,6 +26,7 @@
 #include "fqz_codec.hpp"
 #include "seq_codec.hpp"
 #include "lzp_codec.hpp"
+#include "names.hpp"
 #include "rans_format.hpp"
 
 namespace fqz5 {
@@ -50,6 +51,7 @@ constexpr uint32_t FQZ_MASK =
 
 constexpr uint32_t SEQ_MASK =
     (1u << SEQ10) | (1u << SEQ12) | (1u << SEQ12B) | (1u << SEQ13B) | (1u << SEQ14B);
+constexpr uint32_t NAME_MASK = ((1u << (M_TOK3_9_LZP + 1)) - 1) & ~((1u << M_TLZP3) - 1);
 
 bool is_fqz(int m) { return m >= FQZ0 && m <= FQZ4; }
 bool is_seqcm(int m) { return m >= SEQ10 && m <= SEQ14B; }
@@ -121,6 +123,8 @@ struct TrySession {
     std::vector<uint64_t> seq_lb;                 // pruned candidates: size lower bound (else 0)
     std::vector<std::vector<int>> seq_of;
     std::deque<std::vector<uint32_t>> recs;       // their (rewritable) lengths / flags
+    std::vector<NameEnc> names;                   // name-section candidates (host bytes)
+    std::vector<std::vector<int>> name_of;
     bool open = false;
     bool aux = false;                             // candidates live in the helper contexts
 };
@@ -145,6 +149,37 @@ FqzEncReq fqz_req(const fqz5_section &S, int m, std::deque<std::vector<uint32_t>
     return r;
 }
 thread_local TrySession t_sess;
+
+// Name-section candidates (encode_names, fqzcomp5.c:1408-1586) of sections
+// `which` x methods `meth`, on context g: the names come down once per
+// section, are split / tokenised on host threads, and every lzp pass and
+// rANS stream of all candidates runs as one batch each.
+void encode_name_jobs(GpuCtx &g, const fqz5_section *secs, const std::vector<int> &which,
+                      const std::vector<int> &meth, std::vector<NameEnc> &out) {
+    out.assign(which.size(), NameEnc());
+    if (which.empty()) return;
+    std::vector<std::vector<uint8_t>> host;
+    std::vector<int> host_of(which.size());
+    std::vector<int> seen;
+    for (size_t k = 0; k < which.size(); k++) {
+        auto it = std::find(seen.begin(), seen.end(), which[k]);
+        if (it != seen.end()) { host_of[k] = int(it - seen.begin()); continue; }
+        host_of[k] = int(seen.size());
+        seen.push_back(which[k]);
+        const fqz5_section &S = secs[which[k]];
+        host.emplace_back(S.in_size);
+        g.download(host.back().data(), S.in, S.in_size);
+    }
+    g.sync();
+    std::vector<const uint8_t *> h(which.size()), d(which.size());
+    std::vector<uint32_t> lens(which.size());
+    for (size_t k = 0; k < which.size(); k++) {
+        h[k] = host[size_t(host_of[k])].data();
+        d[k] = secs[which[k]].in;
+        lens[k] = secs[which[k]].in_size;
+    }
+    names_encode_batch(g, out, h, d, lens, meth);
+}
 
 // Trial pruning (fqz5_set_trial_prune): an fqz or sequence-model candidate
 // whose size is provably not below the best rANS candidate's, in every trial
@@ -293,9 +328,12 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         }
         t_sess = TrySession();
         for (int i = 0; i < nsec; i++) {
-            if (masks[i] & ~(RANS_MASK | FQZ_MASK | SEQ_MASK | (1u << LZP3)))
-                throw GpuError("fqz5_sections_try: method mask has name or SEQ_CUSTOM methods "
-                               "(not in this build)");
+            if (masks[i] & ~(RANS_MASK | FQZ_MASK | SEQ_MASK | NAME_MASK | (1u << LZP3)))
+                throw GpuError("fqz5_sections_try: method mask has SEQ_CUSTOM (not in this build)");
+            if ((masks[i] & NAME_MASK) && secs[i].sec != FQZ5_SEC_NAME)
+                throw GpuError("fqz5_sections_try: name methods need a name section");
+            if (secs[i].sec == FQZ5_SEC_NAME && (masks[i] & ~NAME_MASK))
+                throw GpuError("fqz5_sections_try: a name section takes name methods only");
             if ((masks[i] & SEQ_MASK) && (secs[i].sec != FQZ5_SEC_SEQ || !secs[i].rec_len))
                 throw GpuError("fqz5_sections_try: SEQ methods need a sequence section with records");
             if ((masks[i] & FQZ_MASK) && (secs[i].sec != FQZ5_SEC_QUAL || !secs[i].rec_len))
@@ -305,6 +343,8 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         t_sess.req_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
         t_sess.fqz_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
         t_sess.seq_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
+        t_sess.name_of.assign(nsec, std::vector<int>(FQZ5_M_LAST, -1));
+        std::vector<int> name_sec, name_meth;             // name candidates
         std::vector<int> lzp_sec;                         // sections trying LZP3
         std::vector<CompressReq> sreq;                    // RANSXN1 (stripe) candidates
         std::vector<int> sreq_sec;
@@ -320,6 +360,12 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 if (is_seqcm(m)) {
                     t_sess.seq_of[i][m] = int(t_sess.seq.size());
                     t_sess.seq.push_back(seq_req(S, m));
+                    continue;
+                }
+                if (is_name_method(m)) {
+                    t_sess.name_of[i][m] = int(name_sec.size());
+                    name_sec.push_back(i);
+                    name_meth.push_back(m);
                     continue;
                 }
                 if (m == RANSXN1 && !S.fixed_len) continue;   // out = NULL (:2004-2007)
@@ -358,12 +404,13 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             }
             sreq.clear();
         };
-        if ((!fq.empty() || !sq.empty() || !lzp_sec.empty() || !sreq.empty()) && !no_aux) {
+        if ((!fq.empty() || !sq.empty() || !lzp_sec.empty() || !sreq.empty() || !name_sec.empty()) &&
+            !no_aux) {
             t_sess.aux = true;
             GpuCtx &ga = gpu_aux(0), &gb = gpu_aux(2), &gc = gpu_aux(1);
             // sequence-model candidates: one helper context each (their
-            // passes are latency-bound and overlap well), up to AUX_CTXS - 3
-            const size_t nsq = std::min<size_t>(sq.size(), size_t(AUX_CTXS - 3));
+            // passes are latency-bound and overlap well), up to AUX_NSEQ
+            const size_t nsq = std::min<size_t>(sq.size(), size_t(AUX_NSEQ));
             std::vector<std::vector<SeqEncReq>> sqg(nsq);
             for (size_t k = 0; k < sq.size(); k++) sqg[k % std::max<size_t>(nsq, 1)].push_back(sq[k]);
             std::vector<CompressReq> lzr;
@@ -393,11 +440,20 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             // tables) run as their own batch on a helper context, so that
             // their host work overlaps the long chains of the other rANS
             // candidates on the GPU.
-            GpuCtx &gs = gpu_aux(AUX_CTXS - 1);
+            GpuCtx &gs = gpu_aux(AUX_STRIPES);
             std::exception_ptr serr;
             std::thread ts = on(gs, serr, [&] { if (!sreq.empty()) compress_batch(gs, sreq); });
+            // the name candidates: host tokenising, then their own batches
+            // (t_sess is thread_local: the helper thread gets the caller's
+            // vector by reference)
+            GpuCtx &gn = gpu_aux(AUX_NAMES);
+            std::exception_ptr nerr;
+            std::vector<NameEnc> &nres = t_sess.names;
+            std::thread tn = on(gn, nerr, [&] {
+                encode_name_jobs(gn, secs, name_sec, name_meth, nres);
+            });
             for (size_t k = 0; k < nsq; k++) {
-                GpuCtx &gk = gpu_aux(int(2 + k));
+                GpuCtx &gk = gpu_aux(int(AUX_SEQ0 + k));
                 std::vector<SeqEncReq> &grp = sqg[k];
                 th.push_back(on(gk, err[2 + k], [&gk, &grp] { seq_encode_prepare(gk, grp); }));
             }
@@ -408,11 +464,14 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             } catch (...) {
                 for (auto &t : th) t.join();
                 ts.join();
+                tn.join();
                 throw;
             }
             for (auto &t : th) t.join();
             ts.join();
+            tn.join();
             if (serr) std::rethrow_exception(serr);
+            if (nerr) std::rethrow_exception(nerr);
             join_stripes();
             if (step_trace())
                 std::fprintf(stderr, "sections_try: rANS candidates %.1f ms, helpers waited "
@@ -454,6 +513,7 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             join_stripes();
             add_lzp3(g, secs, lzp_sec, reqs, t_sess.req_of);
             compress_batch(g, reqs);
+            encode_name_jobs(g, secs, name_sec, name_meth, t_sess.names);
             if (!fq.empty()) fqz_encode_batch(g, fq);
             if (!sq.empty()) seq_encode_batch(g, sq);
             t_sess.fqz_lb.assign(fq.size(), 0);
@@ -467,9 +527,13 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         for (int i = 0; i < nsec; i++)
             for (int m = 0; m < FQZ5_M_LAST; m++) {
                 const int ri = t_sess.req_of[i][m], fi = t_sess.fqz_of[i][m];
-                const int si = t_sess.seq_of[i][m];
+                const int si = t_sess.seq_of[i][m], ni = t_sess.name_of[i][m];
                 uint32_t sz = UINT32_MAX;
                 if (ri >= 0) sz = reqs[ri].ok ? layout_size(reqs[ri].out) : 0;
+                // a name candidate's size is its whole section (encode_names'
+                // *out_size); one that fails (encode_names NULL) is never chosen
+                if (ni >= 0 && t_sess.names[size_t(ni)].ok)
+                    sz = uint32_t(t_sess.names[size_t(ni)].out.size());
                 if (si >= 0) {
                     const uint64_t lb = t_sess.seq_lb[size_t(si)];   // pruned: its lower bound
                     sz = t_sess.seq[size_t(si)].ok ? layout_size(t_sess.seq[size_t(si)].out)
@@ -539,11 +603,18 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         std::vector<SeqEncReq> late_seq;
         std::vector<int> late_lzp;
         std::vector<std::vector<int>> late_lzp_of(nsec, std::vector<int>(FQZ5_M_LAST, -1));
+        std::vector<int> late_name_sec, late_name_meth, late_name_of(nsec, -1);
         for (int i = 0; i < nsec; i++) {
             const int m = methods[i];
             if (m <= 0 || m >= FQZ5_M_LAST || t_sess.req_of[i][m] >= 0 || t_sess.fqz_of[i][m] >= 0 ||
-                t_sess.seq_of[i][m] >= 0)
+                t_sess.seq_of[i][m] >= 0 || t_sess.name_of[i][m] >= 0)
                 continue;
+            if (is_name_method(m) && secs[i].sec == FQZ5_SEC_NAME) {
+                late_name_of[i] = int(late_name_sec.size());
+                late_name_sec.push_back(i);
+                late_name_meth.push_back(m);
+                continue;
+            }
             if (is_seqcm(m) && secs[i].sec == FQZ5_SEC_SEQ && secs[i].rec_len) {
                 late_seq_of[i] = int(late_seq.size());
                 late_seq.push_back(seq_req(secs[i], m));
@@ -572,6 +643,8 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         if (!late.empty()) compress_batch(g, late);
         if (!late_fqz.empty()) fqz_encode_batch(g, late_fqz);
         if (!late_seq.empty()) seq_encode_batch(g, late_seq);
+        std::vector<NameEnc> late_names;
+        encode_name_jobs(g, secs, late_name_sec, late_name_meth, late_names);
         std::vector<const Layout *> ls;
         std::vector<uint8_t *> dsts;
         std::vector<Layout> framed(nsec);
@@ -582,6 +655,27 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             const int ri = (m > 0 && m < FQZ5_M_LAST) ? t_sess.req_of[i][m] : -1;
             const int fi = (m > 0 && m < FQZ5_M_LAST) ? t_sess.fqz_of[i][m] : -1;
             const int si = (m > 0 && m < FQZ5_M_LAST) ? t_sess.seq_of[i][m] : -1;
+            const int ni = (m > 0 && m < FQZ5_M_LAST) ? t_sess.name_of[i][m] : -1;
+            if (S.sec == FQZ5_SEC_NAME) {             // encode_names' bytes, unframed
+                const NameEnc *E = ni >= 0 ? &t_sess.names[size_t(ni)]
+                                   : late_name_of[i] >= 0 ? &late_names[size_t(late_name_of[i])]
+                                                          : nullptr;
+                R.method = m;
+                R.strat = is_name_method(m) ? name_strat(m) : 0;
+                R.status = -1;
+                R.clen = 0;
+                R.usize = S.in_size;
+                if (!E || !E->ok) continue;
+                R.clen = uint32_t(E->out.size());
+                if (E->out.size() > S.out_cap) continue;
+                Piece p;
+                p.host = E->out;
+                framed[i].push_back(std::move(p));
+                ls.push_back(&framed[i]);
+                dsts.push_back(S.out);
+                R.status = 0;
+                continue;
+            }
             const Layout *lay = nullptr;
             if (ri >= 0 && t_sess.reqs[ri].ok) lay = &t_sess.reqs[ri].out;
             if (late_of[i] >= 0 && late[late_of[i]].ok) lay = &late[late_of[i]].out;
@@ -668,12 +762,28 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         std::vector<LzpDecReq> lzd;
         std::vector<int> who_lzp;                     // section of each lzd entry
         std::vector<size_t> lzp_rans;                 // its rANS stage in reqs
+        std::vector<NameDec> nd;                      // name sections (decode_names)
+        std::vector<int> who_name;
         off = 0;
         for (int i = 0; i < nsec; i++) {
             const uint8_t *h = host + off;
             off += secs[i].in_size;
             res[i].status = -1;
             if (secs[i].in_size < 9) continue;
+            if (secs[i].sec == FQZ5_SEC_NAME) {       // [u32 u_len][u8 strat][u32 c_len] (:2325-2327)
+                NameDec D;
+                std::memcpy(&D.u_len, h, 4);
+                D.strat = h[4];
+                std::memcpy(&D.c_len, h + 5, 4);
+                res[i].strat = D.strat;
+                res[i].clen = D.c_len;
+                if (9ull + D.c_len > secs[i].in_size || D.u_len > secs[i].out_cap) continue;
+                D.comp = h + 9;
+                D.d_comp = secs[i].in + 9;
+                nd.push_back(D);
+                who_name.push_back(i);
+                continue;
+            }
             uint32_t ulen, clen;
             std::memcpy(&ulen, h + 1, 4);
             std::memcpy(&clen, h + 5, 4);
@@ -766,6 +876,16 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         // after the rANS and sequence sections: a quality section's sequence context may
         // be the output of this call's sequence section
         if (!fqz.empty()) fqz_decode_batch(g, fqz);
+        if (!nd.empty()) names_decode_batch(g, nd);
+        for (size_t k = 0; k < nd.size(); k++) {
+            fqz5_section_result &R = res[who_name[k]];
+            if (!nd[k].ok) continue;
+            if (nd[k].u_len)
+                FQZ5_HIP(hipMemcpyAsync(secs[who_name[k]].out, nd[k].names.data(), nd[k].u_len,
+                                        hipMemcpyHostToDevice, g.stream));
+            R.status = 0;
+            R.usize = nd[k].u_len;
+        }
         for (size_t k = 0; k < reqs.size(); k++) {
             if (who[k] < 0) continue;                   // an LZP3 section's rANS stage
             fqz5_section_result &R = res[who[k]];

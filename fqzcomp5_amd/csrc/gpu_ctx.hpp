@@ -287,7 +287,8 @@ GpuCtx &gpu();
 // Helper contexts of the calling thread (k < AUX_CTXS), for work run by
 // helper threads concurrently with the thread's own (created on first use),
 // and a rewind of every one that exists.
-constexpr int AUX_CTXS = 9;   // 0 fqz, 1 LZP3, 2..7 sequence models, 8 stripes
+constexpr int AUX_CTXS = 10;  // 0 fqz, 1 LZP3, 2..7 sequence models, 8 stripes, 9 names
+constexpr int AUX_SEQ0 = 2, AUX_NSEQ = 6, AUX_STRIPES = 8, AUX_NAMES = 9;
 GpuCtx &gpu_aux(int k = 0);
 void gpu_aux_reset_all();
 

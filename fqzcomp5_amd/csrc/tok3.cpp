@@ -24,6 +24,7 @@
 #include "../../include/fqz5_mi355x.h"
 #include "rans_codec.hpp"
 #include "rans_format.hpp"
+#include "tok3.hpp"
 
 namespace fqz5 {
 void fqz5_set_error(const char *msg);   // capi.cpp
@@ -345,23 +346,17 @@ int put_varint(uint8_t *out, uint32_t v) {
 }
 
 }  // namespace
-}  // namespace fqz5
 
-using namespace fqz5;
-
-extern "C" {
-
-uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *out_len,
-                           int *last_start_p) {
-    if (len < 0) {
-        *out_len = 0;
-        return nullptr;
-    }
-    GUARD_BEGIN
+bool tok3_tokenise(char *blk, int len, int level, int use_arith, Tok3Enc &T) {
+    T = Tok3Enc();
+    T.level = level;
+    T.use_arith = use_arith;
+    T.last_start = -1;
+    if (len < 0) return false;
     int nreads = 0, last_start = 0, i, j;
     for (i = 0; i < len; i++)
         if (blk[i] <= '\n') nreads++;
-    if (nreads <= 0 || nreads > 10000000) return nullptr;   // create_context (:172-187)
+    if (nreads <= 0 || nreads > 10000000) return false;     // create_context (:172-187)
     Encoder E;
     E.lc.resize(size_t(nreads) + 1);
     int ctr = 0;                                       // the trie of all names (:1469-1482)
@@ -369,15 +364,15 @@ uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *ou
         while (i < len && blk[i] > '\n') i++;
         if (i >= len) break;
         last_start = i + 1;
-        if (!E.trie.build(&blk[j], size_t(i - j), uint32_t(ctr++))) return nullptr;
+        if (!E.trie.build(&blk[j], size_t(i - j), uint32_t(ctr++))) return false;
     }
-    if (last_start_p) *last_start_p = last_start;
+    T.last_start = last_start;
     for (i = j = 0; i < len; j = ++i) {                // names (:1487-1505)
         while (i < len && static_cast<signed char>(blk[i]) >= ' ') i++;
         if (i >= len) break;
-        if (blk[i] != '\0' && blk[i] != '\n') return nullptr;
+        if (blk[i] != '\0' && blk[i] != '\n') return false;
         blk[i] = '\0';
-        if (!E.name(&blk[j], i - j)) return nullptr;
+        if (!E.name(&blk[j], i - j)) return false;
     }
     // drop the type stream of a column that is all MATCH bar its first
     // entry while the column has other streams (:1531-1553)
@@ -392,106 +387,136 @@ uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *ou
             if (k < 16) b.clear();
         }
     }
-    // every stream's candidate methods, one GPU batch (compress(), :1268-1417)
-    const int lv = std::min(std::max((level - 1) / 2, 0), 4);
-    GpuCtx &g = gpu();
-    std::vector<int> sid;                             // descriptor per stream
-    std::vector<uint32_t> cap;
-    std::vector<std::vector<std::pair<int, int>>> cand(size_t(E.max_tok * 16));   // (method, request)
-    std::vector<CompressReq> reqs;
-    std::vector<int> arith_m;
-    for (i = 0; i < E.max_tok * 16; i++) {
-        const std::vector<uint8_t> &b = E.desc[size_t(i)];
+    T.nreads = nreads;
+    T.max_tok = E.max_tok;
+    T.desc = std::move(E.desc);
+    return true;
+}
+
+void tok3_add_requests(GpuCtx &g, Tok3Enc &T, std::vector<CompressReq> &reqs) {
+    const int lv = std::min(std::max((T.level - 1) / 2, 0), 4);
+    T.cand.assign(size_t(T.max_tok * 16), {});
+    for (int i = 0; i < T.max_tok * 16; i++) {
+        const std::vector<uint8_t> &b = T.desc[size_t(i)];
         if (b.empty()) continue;
         int meth[7];
         std::memcpy(meth, METH[lv][i & 15], sizeof(meth));
-        if (use_arith && lv == 1 && (i & 15) == N_DIGITS) meth[1] = 201;   // :1364
+        if (T.use_arith && lv == 1 && (i & 15) == N_DIGITS) meth[1] = 201;   // :1364
         const uint32_t ocap = uint32_t(1.5 * arith_compress_bound(unsigned(b.size()), 1));
-        const uint8_t *d_in = g.upload(b.data(), b.size());
+        const uint8_t *d_in = T.use_arith ? nullptr : g.upload(b.data(), b.size());
         for (int m = 1; m <= meth[0]; m++) {
             int mm = meth[m];
-            if (!use_arith && (mm & 4)) mm &= ~4;
+            if (!T.use_arith && (mm & 4)) mm &= ~4;
             if (b.size() % 4 != 0 && (mm & 8)) continue;
+            if (T.use_arith) {                          // coded in tok3_assemble
+                T.cand[size_t(i)].push_back({mm, -1});
+                continue;
+            }
             CompressReq r;
             r.d_in = d_in;
             r.n = uint32_t(b.size());
             r.order = mm;
-            r.cap = ocap > 6 ? ocap - 6 : 0;
-            cand[size_t(i)].push_back({mm, int(reqs.size())});
+            r.cap = ocap > 6 ? ocap - 6 : 0;           // rans_encode's *out_len - 6 (:1242)
+            T.cand[size_t(i)].push_back({mm, int(reqs.size())});
             reqs.push_back(std::move(r));
         }
     }
-    std::vector<std::vector<uint8_t>> comp(size_t(E.max_tok * 16));
-    if (!use_arith) {
-        compress_batch(g, reqs);
-        for (i = 0; i < E.max_tok * 16; i++) {
-            if (E.desc[size_t(i)].empty()) continue;
+}
+
+void download_layouts(GpuCtx &g, const std::vector<const Layout *> &ls,
+                      const std::vector<uint8_t *> &dsts) {
+    size_t tot = 0;
+    std::vector<size_t> off(ls.size());
+    for (size_t k = 0; k < ls.size(); k++) {
+        off[k] = tot;
+        tot += layout_size(*ls[k]);
+    }
+    if (!tot) return;
+    uint8_t *d = g.arena.alloc_n<uint8_t>(tot);
+    std::vector<uint8_t *> dd(ls.size());
+    for (size_t k = 0; k < ls.size(); k++) dd[k] = d + off[k];
+    write_layouts_dev(g, ls, dd);
+    uint8_t *h = g.staging.alloc(tot);
+    g.download(h, d, tot);
+    g.sync();
+    for (size_t k = 0; k < ls.size(); k++)
+        std::memcpy(dsts[k], h + off[k], layout_size(*ls[k]));
+}
+
+bool tok3_assemble(GpuCtx &g, const Tok3Enc &T, const std::vector<CompressReq> &reqs,
+                   std::vector<uint8_t> &out) {
+    const int nd = T.max_tok * 16;
+    int i, j;
+    std::vector<std::vector<uint8_t>> comp(static_cast<size_t>(nd));
+    if (!T.use_arith) {
+        std::vector<const Layout *> ls;
+        std::vector<uint8_t *> dst;
+        for (i = 0; i < nd; i++) {
+            if (T.desc[size_t(i)].empty()) continue;
             int best = -1;
             uint64_t best_sz = UINT64_MAX;
-            for (auto &c : cand[size_t(i)]) {
-                CompressReq &r = reqs[size_t(c.second)];
-                if (!r.ok) {                            // rans_encode failed (:1383-1386)
-                    g.reset();
-                    return nullptr;
-                }
+            for (auto &c : T.cand[size_t(i)]) {
+                const CompressReq &r = reqs[size_t(c.second)];
+                if (!r.ok) return false;                // rans_encode failed (:1383-1386)
                 uint8_t v[8];
-                const uint64_t sz = uint64_t(layout_size(r.out)) + uint64_t(put_varint(v, layout_size(r.out)));
+                const uint32_t olen = layout_size(r.out);
+                const uint64_t sz = uint64_t(olen) + uint64_t(put_varint(v, olen));
                 if (best_sz > sz) { best_sz = sz; best = c.second; }
             }
-            CompressReq &r = reqs[size_t(best)];
-            const uint32_t olen = layout_size(r.out);
+            if (best < 0) return false;
+            const uint32_t olen = layout_size(reqs[size_t(best)].out);
             std::vector<uint8_t> &o = comp[size_t(i)];
-            o.resize(8 + olen);
+            o.resize(8 + size_t(olen));
             const int nb = put_varint(o.data(), olen);
-            write_layout_host(g, r.out, o.data() + nb);
             o.resize(size_t(nb) + olen);
+            ls.push_back(&reqs[size_t(best)].out);
+            dst.push_back(o.data() + nb);
         }
-        g.reset();
+        download_layouts(g, ls, dst);
     } else {
-        g.reset();
-        for (i = 0; i < E.max_tok * 16; i++) {
-            std::vector<uint8_t> &b = E.desc[size_t(i)];
+        for (i = 0; i < nd; i++) {
+            const std::vector<uint8_t> &b = T.desc[size_t(i)];
             if (b.empty()) continue;
             uint64_t best_sz = UINT64_MAX;
             const uint32_t ocap = uint32_t(1.5 * arith_compress_bound(unsigned(b.size()), 1));
-            std::vector<uint8_t> out(ocap + 8);
-            for (auto &c : cand[size_t(i)]) {          // arith_encode (:1214-1224)
+            std::vector<uint8_t> o(ocap + 8);
+            std::vector<uint8_t> in(b);
+            for (auto &c : T.cand[size_t(i)]) {          // arith_encode (:1214-1224)
                 unsigned olen = ocap - 6;
-                if (!arith_compress_to(b.data(), unsigned(b.size()), out.data() + 6, &olen, c.first))
-                    return nullptr;
+                if (!arith_compress_to(in.data(), unsigned(in.size()), o.data() + 6, &olen, c.first))
+                    return false;
                 uint8_t v[8];
                 const int nb = put_varint(v, olen);
                 if (best_sz > uint64_t(olen) + uint64_t(nb)) {
                     best_sz = uint64_t(olen) + uint64_t(nb);
                     comp[size_t(i)].assign(v, v + nb);
-                    comp[size_t(i)].insert(comp[size_t(i)].end(), out.data() + 6, out.data() + 6 + olen);
+                    comp[size_t(i)].insert(comp[size_t(i)].end(), o.data() + 6, o.data() + 6 + olen);
                 }
             }
         }
     }
     // serialise, with streams equal to an earlier one as references (:1559-1657)
     uint32_t tot = 9;
-    std::vector<int> dup(size_t(E.max_tok * 16), -1);
-    for (i = 0; i < E.max_tok * 16; i++) {
-        if (E.desc[size_t(i)].empty()) continue;
+    std::vector<int> dup(size_t(nd), -1);
+    for (i = 0; i < nd; i++) {
+        if (T.desc[size_t(i)].empty()) continue;
         const std::vector<uint8_t> &ci = comp[size_t(i)];
         for (j = 0; j < i; j++) {
             const std::vector<uint8_t> &cj = comp[size_t(j)];
-            if (E.desc[size_t(j)].empty() || ci.size() != cj.size() || ci.size() <= 4) continue;
+            if (T.desc[size_t(j)].empty() || ci.size() != cj.size() || ci.size() <= 4) continue;
             if (std::memcmp(ci.data(), cj.data(), ci.size()) == 0) break;
         }
         if (j < i) { dup[size_t(i)] = j; tot += 3; }
         else tot += uint32_t(ci.size()) + 1;
     }
-    uint8_t *out = static_cast<uint8_t *>(malloc(size_t(tot) + 13));
-    if (!out) return nullptr;
-    uint8_t *cp = out;
-    for (int k = 0; k < 4; k++) *cp++ = uint8_t(uint32_t(last_start) >> (8 * k));
-    for (int k = 0; k < 4; k++) *cp++ = uint8_t(uint32_t(nreads) >> (8 * k));
-    *cp++ = uint8_t(use_arith);
+    out.resize(tot);
+    uint8_t *cp = out.data();
+    for (int k = 0; k < 4; k++) *cp++ = uint8_t(uint32_t(T.last_start) >> (8 * k));
+    for (int k = 0; k < 4; k++) *cp++ = uint8_t(uint32_t(T.nreads) >> (8 * k));
+    *cp++ = uint8_t(T.use_arith);
     int last_tnum = -1;
-    for (i = 0; i < E.max_tok * 16; i++) {
-        if (E.desc[size_t(i)].empty()) continue;
+    for (i = 0; i < nd; i++) {
+        if (T.desc[size_t(i)].empty()) continue;
         uint8_t t8 = uint8_t(i & 15);
         if ((i >> 4) != last_tnum) { t8 |= 128; last_tnum = i >> 4; }
         if (dup[size_t(i)] >= 0) {
@@ -504,141 +529,153 @@ uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *ou
             cp += comp[size_t(i)].size();
         }
     }
-    *out_len = int(tot);
-    return out;
-    GUARD_END(nullptr)
+    return true;
 }
 
-uint8_t *tok3_decode_names(uint8_t *in, uint32_t sz, uint32_t *out_len) {
-    if (sz < 9) return nullptr;
-    GUARD_BEGIN
-    const int ulen0 = int(uint32_t(in[0]) | uint32_t(in[1]) << 8 | uint32_t(in[2]) << 16 |
-                          uint32_t(in[3]) << 24);
-    if (ulen0 < 0 || ulen0 >= INT_MAX - 1024) return nullptr;
-    const int nreads = int(uint32_t(in[4]) | uint32_t(in[5]) << 8 | uint32_t(in[6]) << 16 |
-                           uint32_t(in[7]) << 24);
-    const int use_arith = in[8];
-    if (nreads <= 0 || nreads > 10000000) return nullptr;   // create_context (:172-187)
-    // streams: raw bytes, the descriptor they fill and (for coded ones)
-    // their compressed position (:1696-1807)
-    struct D { std::vector<uint8_t> buf; size_t l = 0; bool have = false; };
-    std::vector<D> desc(MAX_TBLOCKS);
-    struct Coded { int i; uint32_t off, clen, ulen; };
-    std::vector<Coded> coded;
-    struct Copy { int i, j; bool col0; };
-    std::vector<std::pair<int, int>> order;            // (kind 0 coded / 1 copy / 2 col0, index)
-    std::vector<Copy> copies;
-    int tnum = -1, max_tok = 1;
+bool tok3_dec_parse(const uint8_t *in, uint32_t sz, Tok3Dec &D) {
+    D = Tok3Dec();
+    if (sz < 9) return false;
+    D.in = in;
+    D.sz = sz;
+    D.ulen0 = int(uint32_t(in[0]) | uint32_t(in[1]) << 8 | uint32_t(in[2]) << 16 |
+                  uint32_t(in[3]) << 24);
+    if (D.ulen0 < 0 || D.ulen0 >= INT_MAX - 1024) return false;
+    D.nreads = int(uint32_t(in[4]) | uint32_t(in[5]) << 8 | uint32_t(in[6]) << 16 |
+                   uint32_t(in[7]) << 24);
+    D.use_arith = in[8];
+    if (D.nreads <= 0 || D.nreads > 10000000) return false;   // create_context (:172-187)
+    // the streams in order: coded, copies of earlier ones, and elided type
+    // streams regenerated from the first type of the column (:1704-1809)
+    int tnum = -1;
     uint32_t o = 9;
-    auto col0 = [&](int t, int ty) {                   // an elided type stream: ty then MATCH
-        D &c = desc[size_t(t << 4)];
-        c.buf.assign(size_t(std::max(nreads, 1)), uint8_t(N_MATCH));
-        if (nreads > 0) c.buf[0] = uint8_t(ty);
-        c.buf.resize(size_t(nreads));
-        c.have = true;
-    };
     while (o < sz) {
         const uint8_t tt = in[o++];
         if (tt & 64) {
-            if (o + 2 > sz) return nullptr;
+            if (o + 2 > sz) return false;
             int j = in[o++] << 4;
             j += in[o++];
             if (tt & 128) {
-                if (++tnum >= MAX_TOKENS) return nullptr;
-                max_tok = tnum + 1;
-                for (int k = 0; k < 16; k++) desc[size_t(tnum << 4 | k)] = D();
+                if (++tnum >= MAX_TOKENS) return false;
+                D.max_tok = tnum + 1;
             }
             if ((tt & 15) != 0 && (tt & 128)) {
-                if (tnum < 0) return nullptr;
-                order.push_back({2, tnum << 4 | (tt & 15)});
+                if (tnum < 0) return false;
+                D.order.push_back({2, tnum << 4 | (tt & 15)});
             }
-            if (tnum < 0) return nullptr;
+            if (tnum < 0) return false;
             const int i = (tnum << 4) | (tt & 15);
-            if (j >= i) return nullptr;
-            copies.push_back({i, j, false});
-            order.push_back({1, int(copies.size()) - 1});
+            if (j >= i) return false;
+            D.copies.push_back({i, j});
+            D.order.push_back({1, int(D.copies.size()) - 1});
             continue;
         }
         if (tt & 128) {
-            if (++tnum >= MAX_TOKENS) return nullptr;
-            max_tok = tnum + 1;
-            for (int k = 0; k < 16; k++) desc[size_t(tnum << 4 | k)] = D();
+            if (++tnum >= MAX_TOKENS) return false;
+            D.max_tok = tnum + 1;
         }
         if ((tt & 15) != 0 && (tt & 128)) {
-            if (tnum < 0) return nullptr;
-            order.push_back({2, tnum << 4 | (tt & 15)});
+            if (tnum < 0) return false;
+            D.order.push_back({2, tnum << 4 | (tt & 15)});
         }
         // uncompressed_size (:1419-1429): varint clen, then the codec's order
         // byte and its varint size
         uint32_t clen = 0, ul = 0;
         const int nb = varint_get(in + o, in + sz, &clen);
-        if (!nb || o + uint32_t(nb) + 1 > sz) return nullptr;
-        if (!varint_get(in + o + nb + 1, in + sz, &ul)) return nullptr;
-        if (tnum < 0 || ul >= uint32_t(INT_MAX)) return nullptr;
+        if (!nb || o + uint32_t(nb) + 1 > sz) return false;
+        if (!varint_get(in + o + nb + 1, in + sz, &ul)) return false;
+        if (tnum < 0 || ul >= uint32_t(INT_MAX)) return false;
         const int i = (tnum << 4) | (tt & 15);
         // the codec sees the rest of the block (:1792); clen only advances
-        coded.push_back({i, o + uint32_t(nb), sz - o - uint32_t(nb), ul});
-        order.push_back({0, int(coded.size()) - 1});
+        D.coded.push_back({i, o + uint32_t(nb), sz - o - uint32_t(nb), ul});
+        D.order.push_back({0, int(D.coded.size()) - 1});
         if (uint64_t(o) + uint64_t(nb) + clen >= sz) break;
         o += uint32_t(nb) + clen;
     }
-    // decode every coded stream in one batch
-    std::vector<std::vector<uint8_t>> dec(coded.size());
-    if (!use_arith) {
-        GpuCtx &g = gpu();
-        std::vector<DecompressReq> reqs;
-        const uint8_t *d_all = g.upload(in, sz);
-        for (const Coded &c : coded) {
-            DecompressReq r;
-            r.h_in = in + c.off;
-            r.d_in = d_all + c.off;
-            r.in_size = c.clen;
-            r.out_cap = c.ulen;
-            r.d_out = g.arena.alloc_n<uint8_t>(size_t(c.ulen) + 1);
-            reqs.push_back(r);
+    return true;
+}
+
+void tok3_dec_add_requests(GpuCtx &g, Tok3Dec &D, const uint8_t *d_in,
+                           std::vector<DecompressReq> &reqs) {
+    D.req0 = reqs.size();
+    if (D.use_arith || D.coded.empty()) return;
+    if (!d_in) d_in = g.upload(D.in, D.sz);
+    D.out_off.resize(D.coded.size());
+    D.out_tot = 0;
+    for (size_t k = 0; k < D.coded.size(); k++) {
+        D.out_off[k] = D.out_tot;
+        D.out_tot += size_t(D.coded[k].ulen) + 1;
+    }
+    D.d_out = g.arena.alloc_n<uint8_t>(D.out_tot);
+    for (size_t k = 0; k < D.coded.size(); k++) {
+        const Tok3Dec::Coded &c = D.coded[k];
+        DecompressReq r;
+        r.h_in = D.in + c.off;
+        r.d_in = d_in + c.off;
+        r.in_size = c.clen;
+        r.out_cap = c.ulen;
+        r.d_out = D.d_out + D.out_off[k];
+        reqs.push_back(r);
+    }
+}
+
+bool tok3_dec_finish(GpuCtx &g, const Tok3Dec &D, const std::vector<DecompressReq> &reqs,
+                     std::vector<uint8_t> &out) {
+    struct Desc { std::vector<uint8_t> buf; size_t l = 0; bool have = false; };
+    std::vector<Desc> desc(MAX_TBLOCKS);
+    const int nreads = D.nreads, max_tok = D.max_tok;
+    std::vector<std::vector<uint8_t>> dec(D.coded.size());
+    if (!D.use_arith) {
+        for (size_t k = 0; k < D.coded.size(); k++) {
+            const DecompressReq &r = reqs[D.req0 + k];
+            if (!r.ok || r.out_size != D.coded[k].ulen) return false;
         }
-        decompress_batch(g, reqs);
-        for (size_t k = 0; k < coded.size(); k++) {
-            if (!reqs[k].ok || reqs[k].out_size != coded[k].ulen) { g.reset(); return nullptr; }
-            dec[k].resize(coded[k].ulen);
-            g.download(dec[k].data(), reqs[k].d_out, coded[k].ulen);
+        if (D.out_tot) {
+            uint8_t *h = g.staging.alloc(D.out_tot);
+            g.download(h, D.d_out, D.out_tot);
+            g.sync();
+            for (size_t k = 0; k < D.coded.size(); k++)
+                dec[k].assign(h + D.out_off[k], h + D.out_off[k] + D.coded[k].ulen);
         }
-        g.sync();
-        g.reset();
     } else {
-        for (size_t k = 0; k < coded.size(); k++) {
-            unsigned ol = coded[k].ulen;
+        for (size_t k = 0; k < D.coded.size(); k++) {
+            unsigned ol = D.coded[k].ulen;
             dec[k].resize(size_t(ol) + 1);
-            if (!arith_uncompress_to(in + coded[k].off, coded[k].clen, dec[k].data(), &ol) ||
-                ol != coded[k].ulen)
-                return nullptr;
+            if (!arith_uncompress_to(const_cast<uint8_t *>(D.in) + D.coded[k].off, D.coded[k].clen,
+                                     dec[k].data(), &ol) ||
+                ol != D.coded[k].ulen)
+                return false;
             dec[k].resize(ol);
         }
     }
-    for (auto &e : order) {                            // in stream order, as the reference
-        if (e.first == 2) {
-            col0(e.second >> 4, e.second & 15);
+    for (auto &e : D.order) {                          // in stream order, as the reference
+        if (e.first == 2) {                            // an elided type stream: ty then MATCH
+            Desc &c = desc[size_t(e.second & ~15)];
+            c.buf.assign(size_t(nreads), uint8_t(N_MATCH));
+            c.buf[0] = uint8_t(e.second & 15);
+            c.have = true;
+            c.l = 0;
         } else if (e.first == 1) {
-            const Copy &c = copies[size_t(e.second)];
-            if (!desc[size_t(c.j)].have) return nullptr;
-            desc[size_t(c.i)].buf = desc[size_t(c.j)].buf;
-            desc[size_t(c.i)].have = true;
-            desc[size_t(c.i)].l = 0;
+            const auto &c = D.copies[size_t(e.second)];
+            if (!desc[size_t(c.second)].have) return false;
+            desc[size_t(c.first)].buf = desc[size_t(c.second)].buf;
+            desc[size_t(c.first)].have = true;
+            desc[size_t(c.first)].l = 0;
         } else {
-            const Coded &c = coded[size_t(e.second)];
+            const Tok3Dec::Coded &c = D.coded[size_t(e.second)];
             desc[size_t(c.i)].buf = std::move(dec[size_t(e.second)]);
             desc[size_t(c.i)].have = true;
             desc[size_t(c.i)].l = 0;
         }
     }
+    using D_ = Desc;
     // decode_name per name (:1023-1212)
     auto dtype = [&](int ntok) -> int {
-        D &d = desc[size_t(ntok << 4)];
+        D_ &d = desc[size_t(ntok << 4)];
         if (d.l >= d.buf.size()) return -1;
         return d.buf[d.l++];
     };
     auto dint = [&](int ntok, int ty, uint32_t *v) -> bool {
-        D &d = desc[size_t(ntok << 4 | ty)];
+        D_ &d = desc[size_t(ntok << 4 | ty)];
         if (d.l + 4 > d.buf.size()) return false;
         const uint8_t *p = d.buf.data() + d.l;
         *v = uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
@@ -646,7 +683,7 @@ uint8_t *tok3_decode_names(uint8_t *in, uint32_t sz, uint32_t *out_len) {
         return true;
     };
     auto dint1 = [&](int ntok, int ty, uint32_t *v) -> bool {
-        D &d = desc[size_t(ntok << 4 | ty)];
+        D_ &d = desc[size_t(ntok << 4 | ty)];
         if (d.l >= d.buf.size()) return false;
         *v = d.buf[d.l++];
         return true;
@@ -666,7 +703,7 @@ uint8_t *tok3_decode_names(uint8_t *in, uint32_t sz, uint32_t *out_len) {
         for (int k = 0; k < n; k++) cp[k] = t[n - 1 - k];
         return n;
     };
-    int64_t ulen = int64_t(ulen0) + 1024;
+    int64_t ulen = int64_t(D.ulen0) + 1024;
     std::vector<char> outb(static_cast<size_t>(ulen));
     std::vector<Last> lc(size_t(nreads) + 1);          // max_names = nreads + 1 (:190)
     size_t osz = 0;
@@ -714,7 +751,7 @@ uint8_t *tok3_decode_names(uint8_t *in, uint32_t sz, uint32_t *out_len) {
                     T.ival = nm[len++];
                     break;
                 case N_ALPHA: {
-                    D &d = desc[size_t(ntok << 4 | N_ALPHA)];
+                    D_ &d = desc[size_t(ntok << 4 | N_ALPHA)];
                     if (d.l >= d.buf.size()) { bad = true; break; }
                     int64_t l2 = 0;
                     char c;
@@ -808,13 +845,66 @@ uint8_t *tok3_decode_names(uint8_t *in, uint32_t sz, uint32_t *out_len) {
         osz += size_t(ret);
         ulen -= ret;
     }
-    if (ret < 0) return nullptr;
-    uint8_t *out = static_cast<uint8_t *>(malloc(std::max<size_t>(osz, 1)));
+    if (ret < 0) return false;
+    out.assign(outb.begin(), outb.begin() + ptrdiff_t(osz));
+    return true;
+}
+
+}  // namespace fqz5
+
+using namespace fqz5;
+
+extern "C" {
+
+uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *out_len,
+                           int *last_start_p) {
+    if (len < 0) {
+        *out_len = 0;
+        return nullptr;
+    }
+    GpuCtx *gp = nullptr;
+    GUARD_BEGIN
+    Tok3Enc T;
+    const bool ok = tok3_tokenise(blk, len, level, use_arith, T);
+    if (last_start_p && T.last_start >= 0) *last_start_p = T.last_start;
+    if (!ok) return nullptr;
+    GpuCtx &g = gpu();
+    gp = &g;
+    std::vector<CompressReq> reqs;
+    tok3_add_requests(g, T, reqs);
+    if (!reqs.empty()) compress_batch(g, reqs);
+    std::vector<uint8_t> o;
+    const bool good = tok3_assemble(g, T, reqs, o);
+    g.reset();
+    if (!good) return nullptr;
+    uint8_t *out = static_cast<uint8_t *>(malloc(o.size() + 13));
     if (!out) return nullptr;
-    std::memcpy(out, outb.data(), osz);
-    *out_len = uint32_t(osz);
+    std::memcpy(out, o.data(), o.size());
+    *out_len = int(o.size());
     return out;
-    GUARD_END(nullptr)
+    GUARD_END((gp ? (void)gp->reset() : (void)0, nullptr))
+}
+
+uint8_t *tok3_decode_names(uint8_t *in, uint32_t sz, uint32_t *out_len) {
+    GpuCtx *gp = nullptr;
+    GUARD_BEGIN
+    Tok3Dec D;
+    if (!tok3_dec_parse(in, sz, D)) return nullptr;
+    GpuCtx &g = gpu();
+    gp = &g;
+    std::vector<DecompressReq> reqs;
+    tok3_dec_add_requests(g, D, nullptr, reqs);
+    if (!reqs.empty()) decompress_batch(g, reqs);
+    std::vector<uint8_t> o;
+    const bool good = tok3_dec_finish(g, D, reqs, o);
+    g.reset();
+    if (!good) return nullptr;
+    uint8_t *out = static_cast<uint8_t *>(malloc(std::max<size_t>(o.size(), 1)));
+    if (!out) return nullptr;
+    std::memcpy(out, o.data(), o.size());
+    *out_len = uint32_t(o.size());
+    return out;
+    GUARD_END((gp ? (void)gp->reset() : (void)0, nullptr))
 }
 
 }  // extern "C"

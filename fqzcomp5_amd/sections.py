@@ -1,7 +1,7 @@
 """Block-section coding on the GPU (include/fqz5_block.h) from Python.
 
-A "run" is a list of blocks in file order; each block has a sequence and a
-quality section (fqzcomp5.c:2217-2257).  Encoding follows fqzcomp5's codec
+A "run" is a list of blocks in file order; each block has a name, a
+sequence and a quality section (fqzcomp5.c:2167-2257).  Encoding follows fqzcomp5's codec
 trial (metrics_method / compress_with_methods, fqzcomp5.c:1899-2144):
 
     ids    = exchange(section ids)          # multi-GPU: all_gather (RCCL)
@@ -23,9 +23,13 @@ import numpy as np
 from . import lib as _lib
 
 M_LAST = 31
-SEC_SEQ, SEC_QUAL = 2, 3
+SEC_NAME, SEC_SEQ, SEC_QUAL = 0, 2, 3
 RANS0, RANS1, RANS64, RANS65, RANS128, RANS129, RANS192, RANS193, RANSXN1 = range(1, 10)
 LZP3 = 10
+TLZP3 = 11
+TOK3_3, TOK3_5, TOK3_7, TOK3_9 = range(12, 16)
+TOK3_3_LZP, TOK3_5_LZP, TOK3_7_LZP, TOK3_9_LZP = range(16, 20)
+NAME_MASK = sum(1 << m for m in range(TLZP3, TOK3_9_LZP + 1))
 SEQ10, SEQ12, SEQ12B, SEQ13B, SEQ14B = range(20, 25)
 FQZ0, FQZ1, FQZ2, FQZ3, FQZ4 = range(26, 31)
 RANS_MASK = sum(1 << m for m in range(RANS0, RANSXN1 + 1))
@@ -35,19 +39,23 @@ SEQ_MASK = sum(1 << m for m in range(SEQ10, SEQ14B + 1))
 # schedule names them (see encode_run)
 WORK_MASK = FQZ_MASK | SEQ_MASK | (1 << LZP3)
 
-# Method masks of the level presets for the sequence and quality sections
-# (fqzcomp5.c:4886-4932; the names masks belong to SURVEY §8 f1) and their
-# block sizes.
+# Method masks of the level presets (name: arg.nauto, sequence, quality;
+# fqzcomp5.c:4886-4932, :2750-2793) and their block sizes.
 PRESET_MASKS = {
-    1: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3],
+    1: {SEC_NAME: [TLZP3],
+        SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3],
         SEC_QUAL: [RANS0, RANS1, RANS129, RANS193]},
-    3: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3],
+    3: {SEC_NAME: [TLZP3, TOK3_3_LZP],
+        SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3],
         SEC_QUAL: [RANS0, RANS1, RANS129, RANS193, RANSXN1]},
-    5: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3, SEQ10, SEQ12B],
+    5: {SEC_NAME: [TLZP3, TOK3_5_LZP],
+        SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3, SEQ10, SEQ12B],
         SEC_QUAL: [RANS0, RANS1, RANS129, RANS193, RANSXN1, FQZ1, FQZ3]},
-    7: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3, RANS65, SEQ10, SEQ12B, SEQ13B],
+    7: {SEC_NAME: [TLZP3, TOK3_7_LZP, TOK3_7],
+        SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, LZP3, RANS65, SEQ10, SEQ12B, SEQ13B],
         SEC_QUAL: [RANS0, RANS1, RANS129, RANS193, RANS65, FQZ0, FQZ1, FQZ2, FQZ3, FQZ4]},
-    9: {SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, RANS64, RANS65, RANS128, LZP3,
+    9: {SEC_NAME: [TLZP3, TOK3_9_LZP, TOK3_9],
+        SEC_SEQ: [RANS0, RANS1, RANS129, RANS193, RANS64, RANS65, RANS128, LZP3,
                   SEQ10, SEQ12, SEQ12B, SEQ13B, SEQ14B],
         SEC_QUAL: [RANS0, RANS1, RANS129, RANS193, RANS64, RANS65, RANS128,
                    FQZ0, FQZ1, FQZ2, FQZ3, FQZ4]},
@@ -57,19 +65,20 @@ BLOCK_SIZE = {1: 10_000_000, 3: 100_000_000, 5: 100_000_000, 7: 500_000_000,
 # encode_seq's (k, both strands) per method (fqzcomp5.c:2047-2062)
 SEQ_PARAMS = {SEQ10: (10, 0), SEQ12: (12, 0), SEQ12B: (12, 1), SEQ13B: (13, 1),
               SEQ14B: (14, 1)}
-# methods this build codes: every sequence and quality method of the presets
-# (rANS, LZP3, the sequence context models, fqz)
-BUILT = set(range(RANS0, LZP3 + 1)) | set(SEQ_PARAMS) | set(range(FQZ0, FQZ4 + 1))
+# methods this build codes: every method of the presets (rANS, LZP3, the
+# name methods, the sequence context models, fqz)
+BUILT = set(range(RANS0, TOK3_9_LZP + 1)) | set(SEQ_PARAMS) | set(range(FQZ0, FQZ4 + 1))
 
 
-def preset_methods(level: int) -> list[int]:
-    """Every seq/qual method of the preset, (section, method) flattened."""
-    return sorted({m for ms in PRESET_MASKS[level].values() for m in ms})
+def preset_methods(level: int, names: bool = True) -> list[int]:
+    """Every method of the preset, (section, method) flattened."""
+    return sorted({m for sec, ms in PRESET_MASKS[level].items()
+                   for m in ms if names or sec != SEC_NAME})
 
 
-def level_methods(level: int) -> list[int]:
-    """The preset's seq/qual methods that this build codes."""
-    return [m for m in preset_methods(level) if m in BUILT]
+def level_methods(level: int, names: bool = True) -> list[int]:
+    """The preset's methods that this build codes."""
+    return [m for m in preset_methods(level, names) if m in BUILT]
 
 
 class Section(C.Structure):
@@ -279,6 +288,9 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
     ins = np.array([s.in_size for s in secs], np.uint32)
     ids = np.array([s.sec for s in secs], np.int32)
     av = np.asarray(avail, np.uint32)
+    # name candidates are speculative too: their host tokenising runs on a
+    # helper thread beside the rANS batch, and none is left for commit
+    SPEC = RANS_MASK | NAME_MASK
     if speculate and not (av & WORK_MASK).any():
         masks = av[ids]
         prune = False
@@ -290,7 +302,7 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
         # rANS candidates stay speculative (chain-bound, nearly free in one
         # launch); fqz candidates cost in proportion to their work, so only
         # the scheduled trial sections try them
-        masks = (av[ids] & RANS_MASK) | (sched & WORK_MASK) if speculate else sched
+        masks = (av[ids] & SPEC) | (sched & WORK_MASK) if speculate else sched
         # pruning needs each family's trial window whole on this rank
         for fam in (FQZ_MASK, SEQ_MASK):
             rows = np.nonzero(sched_all & fam)[0]
@@ -318,32 +330,113 @@ def fqz_bound(n: int) -> int:
     return int(n * 1.1) + 100000 + 16384
 
 
+class BlockParts(C.Structure):
+    """fqz5_block_parts"""
+    _fields_ = [("nrec", C.c_int32), ("name", C.c_void_p), ("name_size", C.c_uint32),
+                ("lengths", C.c_void_p), ("lengths_size", C.c_uint32),
+                ("seq", C.c_void_p), ("seq_size", C.c_uint32),
+                ("qual", C.c_void_p), ("qual_size", C.c_uint32)]
+
+
+class BlockView(C.Structure):
+    """fqz5_block_view"""
+    _fields_ = [("block_size", C.c_uint32), ("nrec", C.c_uint32), ("crc_ok", C.c_int32),
+                ("name_off", C.c_uint32), ("name_size", C.c_uint32), ("name_ulen", C.c_uint32),
+                ("fixed_len", C.c_int32), ("seq_off", C.c_uint32), ("seq_size", C.c_uint32),
+                ("seq_ulen", C.c_uint32), ("qual_off", C.c_uint32), ("qual_size", C.c_uint32),
+                ("qual_ulen", C.c_uint32)]
+
+
+_bound_blk = False
+
+
+def _load_blk():
+    global _bound_blk
+    so = _load()
+    if not _bound_blk:
+        so.fqz5_name_flags.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.POINTER(C.c_uint32)]
+        so.fqz5_block_lengths.restype = C.c_int
+        so.fqz5_block_lengths.argtypes = [C.POINTER(C.c_uint32), C.c_int, C.c_int32,
+                                          C.c_void_p, C.c_uint32]
+        so.fqz5_block_size.restype = C.c_uint64
+        so.fqz5_block_size.argtypes = [C.POINTER(BlockParts)]
+        so.fqz5_blocks_assemble.restype = C.c_int
+        so.fqz5_blocks_assemble.argtypes = [C.POINTER(BlockParts), C.c_int, C.c_void_p,
+                                            C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+        so.fqz5_block_parse.restype = C.c_int
+        so.fqz5_block_parse.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(BlockView),
+                                        C.POINTER(C.c_uint32), C.c_uint32]
+        _bound_blk = True
+    return so
+
+
+def name_flags(names: np.ndarray, nrec: int) -> np.ndarray:
+    """load_seqs_kseq's per-record flags from the names (fqz5_name_flags)."""
+    out = np.zeros(nrec, np.uint32)
+    nb = np.ascontiguousarray(names, np.uint8)
+    _load_blk().fqz5_name_flags(nb.ctypes.data, len(nb), nrec,
+                                out.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return out
+
+
+def block_lengths(lens: np.ndarray, fixed_len: int) -> bytes:
+    ln = np.ascontiguousarray(lens, np.uint32)
+    buf = C.create_string_buffer(5 * len(ln) + 16)
+    n = _load_blk().fqz5_block_lengths(ln.ctypes.data_as(C.POINTER(C.c_uint32)), len(ln),
+                                       fixed_len, buf, len(buf))
+    if n < 0:
+        raise _lib.NativeError("fqz5_block_lengths")
+    return buf.raw[:n]
+
+
 class Run:
     """Device buffers and sections of a run of blocks in file order, each
-    block a sequence then a quality section (encode_block order).  The
-    quality sections carry the records (FQZ methods) and point at their
-    block's sequence bytes: the input when encoding, the decoded sequence
-    section when decoding."""
+    block a name (when the reads carry names), a sequence and a quality
+    section (encode_block order).  The quality sections carry the records
+    (FQZ methods) and point at their block's sequence bytes: the input when
+    encoding, the decoded sequence section when decoding.
 
-    def __init__(self, reads, blocks, device):
+    With names, `assemble` writes whole .fqz5 blocks (fqz5_blocks_assemble:
+    header, CRC32, lengths) and `parse` reads them back (fqz5_block_parse)."""
+
+    def __init__(self, reads, blocks, device, names: bool | None = None):
         import torch
+        from . import synth
         self.reads, self.blocks = reads, blocks
+        self.names = reads.has_names() if names is None else names
         offs = np.concatenate([[0], np.cumsum(reads.lens.astype(np.int64))])
         self.seq_d = torch.from_numpy(reads.seq).to(device)
         self.qual_d = torch.from_numpy(reads.qual).to(device)
-        self.spans, self.lens, self.flags = [], [], []
+        self.name_h = self.name_off = self.name_d = None
+        if self.names:
+            self.name_h, self.name_off = synth.all_names(reads)
+            self.name_d = torch.from_numpy(self.name_h).to(device)
+        self.spans, self.lens, self.flags, self.fixed, self.lengths = [], [], [], [], []
         for a, b in blocks:
             s, e = int(offs[a]), int(offs[b])
             ln = np.ascontiguousarray(reads.lens[a:b], np.uint32)
-            self.flags.append(None if getattr(reads, "flags", None) is None else
-                              np.ascontiguousarray(reads.flags[a:b], np.uint32))
             fl = int(ln[0]) if len(ln) and bool(np.all(ln == ln[0])) else 0
+            k = len(self.lens)
             self.lens.append(ln)
-            self.spans.append((SEC_SEQ, s, e, fl, len(self.lens) - 1))
-            self.spans.append((SEC_QUAL, s, e, fl, len(self.lens) - 1))
+            if self.names:          # load_seqs_kseq derives them from the names
+                ns, ne = int(self.name_off[a]), int(self.name_off[b])
+                self.flags.append(name_flags(self.name_h[ns:ne], b - a))
+            elif getattr(reads, "flags", None) is not None:
+                self.flags.append(np.ascontiguousarray(reads.flags[a:b], np.uint32))
+            else:
+                self.flags.append(None)
+            self.fixed.append(fl)
+            if self.names:
+                self.lengths.append(block_lengths(ln, fl if len(ln) else -1))
+                self.spans.append((SEC_NAME, int(self.name_off[a]), int(self.name_off[b]), 0, k))
+            self.spans.append((SEC_SEQ, s, e, fl, k))
+            self.spans.append((SEC_QUAL, s, e, fl, k))
         caps = []
         for sec, s, e, fl, _ in self.spans:
             n = e - s
+            if sec == SEC_NAME:    # encode_names' buffer (fqzcomp5.c:1412) and then some
+                caps.append(2 * n + 1000 + 65536)
+                continue
             caps.append(9 + max(max(_lib.compress_bound(n, o) for o in
                                     (0, 1, 64, 65, 128, 129, 192, 193, (fl << 8) + 9)),
                                 fqz_bound(n)))
@@ -358,6 +451,11 @@ class Run:
             eo += cap
             do += e - s
         self.in_bytes = sum(e - s for _, s, e, _, _ in self.spans)
+        self.blk_buf = None
+        self.blk_off = None
+
+    def _src(self, sec):
+        return {SEC_NAME: self.name_d, SEC_SEQ: self.seq_d, SEC_QUAL: self.qual_d}[sec]
 
     def _rec(self, k):
         ln = self.lens[k]
@@ -370,32 +468,117 @@ class Run:
     def enc_secs(self) -> list[Section]:
         out = []
         for (sec, s, e, fl, k), (eo, cap) in zip(self.spans, self.enc):
-            src = self.seq_d if sec == SEC_SEQ else self.qual_d
+            src = self._src(sec)
             rl, nr = self._rec(k)
             out.append(Section(src.data_ptr() + s, self.enc_buf.data_ptr() + eo, e - s, cap,
                                fl, sec, rl, self._flags(k), nr,
                                self.seq_d.data_ptr() + s if sec == SEC_QUAL else None))
         return out
 
+    def _seq_dec(self, i):
+        """The decoded sequence section of the block of section i."""
+        j = i - 1
+        while self.spans[j][0] != SEC_SEQ:
+            j -= 1
+        return self.dec_buf.data_ptr() + self.dec[j]
+
     def dec_secs(self, res) -> list[Section]:
         out = []
         for i, ((sec, s, e, fl, k), (eo, cap), do, r) in enumerate(
                 zip(self.spans, self.enc, self.dec, res)):
             rl, nr = self._rec(k)
-            seq = self.dec_buf.data_ptr() + self.dec[i - 1] if sec == SEC_QUAL else None
+            seq = self._seq_dec(i) if sec == SEC_QUAL else None
+            size = r.clen if sec == SEC_NAME else 9 + r.clen
             out.append(Section(self.enc_buf.data_ptr() + eo, self.dec_buf.data_ptr() + do,
-                               9 + r.clen, e - s, 0, sec, rl, self._flags(k), nr, seq))
+                               size, e - s, 0, sec, rl, self._flags(k), nr, seq))
         return out
 
     def chosen(self, res, i) -> bytes:
-        """The i-th section's chosen stream (without the 9-byte frame)."""
+        """The i-th section's chosen stream (without the 9-byte frame; a name
+        section whole)."""
         eo, _ = self.enc[i]
-        return self.enc_buf[eo + 9:eo + 9 + res[i].clen].cpu().numpy().tobytes()
+        skip = 0 if self.spans[i][0] == SEC_NAME else 9
+        return self.enc_buf[eo + skip:eo + 9 + res[i].clen].cpu().numpy().tobytes() \
+            if skip else self.enc_buf[eo:eo + res[i].clen].cpu().numpy().tobytes()
 
     def roundtrip_ok(self) -> bool:
         import torch
         ok = True
         for (sec, s, e, _, _), do in zip(self.spans, self.dec):
-            src = self.seq_d if sec == SEC_SEQ else self.qual_d
+            src = self._src(sec)
             ok = ok and bool(torch.equal(self.dec_buf[do:do + e - s], src[s:e]))
         return ok
+
+    # ---- whole blocks (encode_block / decode_block) -----------------------
+    def _parts(self, res) -> list[BlockParts]:
+        assert self.names, "blocks need the name sections"
+        parts = []
+        base = self.enc_buf.data_ptr()
+        for b in range(len(self.blocks)):
+            i = 3 * b
+            (eo_n, _), (eo_s, _), (eo_q, _) = self.enc[i], self.enc[i + 1], self.enc[i + 2]
+            ln = self.lengths[b]
+            parts.append(BlockParts(len(self.lens[b]), base + eo_n, res[i].clen,
+                                    C.cast(C.c_char_p(ln), C.c_void_p), len(ln),
+                                    base + eo_s, 9 + res[i + 1].clen,
+                                    base + eo_q, 9 + res[i + 2].clen))
+        return parts
+
+    def assemble(self, res):
+        """Write every block (fqz5_blocks_assemble) into self.blk_buf at
+        self.blk_off; returns the block sizes."""
+        import torch
+        so = _load_blk()
+        parts = self._parts(res)
+        sizes = [int(so.fqz5_block_size(C.byref(p))) for p in parts]
+        off = np.zeros(len(parts) + 1, np.uint64)
+        np.cumsum(sizes, out=off[1:])
+        if self.blk_buf is None or self.blk_buf.numel() < int(off[-1]):
+            self.blk_buf = torch.empty(int(off[-1]) + 64, dtype=torch.uint8,
+                                       device=self.seq_d.device)
+        self.blk_off = off
+        out = np.zeros(len(parts), np.uint32)
+        rc = so.fqz5_blocks_assemble(_arr(BlockParts, parts), len(parts), self.blk_buf.data_ptr(),
+                                     off.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                     out.ctypes.data_as(C.POINTER(C.c_uint32)))
+        if rc:
+            raise _lib.NativeError("fqz5_blocks_assemble: " + _lib.last_error())
+        return out
+
+    def block_bytes(self, b: int) -> bytes:
+        s, e = int(self.blk_off[b]), int(self.blk_off[b + 1])
+        return self.blk_buf[s:e].cpu().numpy().tobytes()
+
+    def parse(self, b: int) -> tuple[BlockView, np.ndarray]:
+        """fqz5_block_parse of block b of blk_buf: its view and lengths."""
+        so = _load_blk()
+        v = BlockView()
+        s, e = int(self.blk_off[b]), int(self.blk_off[b + 1])
+        nrec = len(self.lens[b])
+        lens = np.zeros(max(nrec, 1), np.uint32)
+        if so.fqz5_block_parse(self.blk_buf.data_ptr() + s, e - s, C.byref(v),
+                               lens.ctypes.data_as(C.POINTER(C.c_uint32)), len(lens)):
+            raise _lib.NativeError("fqz5_block_parse: " + _lib.last_error())
+        return v, lens[:v.nrec]
+
+    def block_dec_secs(self) -> list[Section]:
+        """Decode sections that read the assembled blocks (after parse)."""
+        out = []
+        base = self.blk_buf.data_ptr()
+        for b in range(len(self.blocks)):
+            v, lens = self.parse(b)
+            if not v.crc_ok:
+                raise _lib.NativeError(f"block {b}: CRC mismatch")
+            if not np.array_equal(lens, self.lens[b]):
+                raise _lib.NativeError(f"block {b}: lengths differ")
+            bo = int(self.blk_off[b])
+            for j, (off, size) in enumerate(((v.name_off, v.name_size),
+                                             (v.seq_off, v.seq_size),
+                                             (v.qual_off, v.qual_size))):
+                i = 3 * b + j
+                sec, s, e, fl, k = self.spans[i]
+                rl, nr = self._rec(k)
+                seq = self._seq_dec(i) if sec == SEC_QUAL else None
+                out.append(Section(base + bo + off, self.dec_buf.data_ptr() + self.dec[i],
+                                   size, e - s, 0, sec, rl, self._flags(k), nr, seq))
+        return out

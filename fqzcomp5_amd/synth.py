@@ -35,6 +35,9 @@ import numpy as np
 ILLUMINA_BINS = np.array([2, 6, 15, 22, 27, 33, 37, 40], dtype=np.uint8)
 
 
+COMMENT = b" 1:N:0:ACGTACGT"      # the comment every synthetic name carries
+
+
 def _illumina_bin(q: np.ndarray) -> np.ndarray:
     # Illumina 8-level binning: 2-9 -> 6, 10-19 -> 15, 20-24 -> 22,
     # 25-29 -> 27, 30-34 -> 33, 35-39 -> 37, >=40 -> 40; <2 -> 2.
@@ -53,6 +56,8 @@ class Reads:
     name_l: np.ndarray     # int32: kseq name.l (name part before the space)
     flags: np.ndarray | None = None   # uint32 per record (FQZ_FREAD2), None = all 0
     comment_l: int = 15    # bytes of ' ' + comment per name (0: no comment)
+    name_buf: np.ndarray | None = None   # uint8: every name, '\0' after each
+    name_off: np.ndarray | None = None   # int64 [n + 1]: offsets into name_buf
 
     @property
     def num_records(self) -> int:
@@ -65,38 +70,77 @@ class Reads:
         l0 = int(self.lens[0])
         return l0 if bool(np.all(self.lens == l0)) else 0
 
+    def has_names(self) -> bool:
+        return self.names is not None or self.name_buf is not None
+
+    def name(self, i: int) -> bytes:
+        if self.names is not None:
+            return self.names[i]
+        return self.name_buf[self.name_off[i]:self.name_off[i + 1] - 1].tobytes()
+
     def to_fastq(self) -> bytes:
-        assert self.names is not None
+        assert self.has_names()
         out = []
         off = 0
         for i, ln in enumerate(self.lens.tolist()):
             s = self.seq[off:off + ln].tobytes()
             q = (self.qual[off:off + ln] + 33).astype(np.uint8).tobytes()
-            out.append(b"@" + self.names[i] + b"\n" + s + b"\n+\n" + q + b"\n")
+            out.append(b"@" + self.name(i) + b"\n" + s + b"\n+\n" + q + b"\n")
             off += ln
         return b"".join(out)
 
 
-def _names(rng: np.random.Generator, n: int) -> tuple[list, np.ndarray]:
+def _digits(v: np.ndarray, width: int) -> tuple[np.ndarray, np.ndarray]:
+    """Decimal digits of v (< 10**width) right-aligned in `width` columns,
+    and the mask of the significant ones."""
+    cols = np.empty((v.shape[0], width), np.uint8)
+    t = v.astype(np.int64).copy()
+    for c in range(width - 1, -1, -1):
+        cols[:, c] = (t % 10 + 48).astype(np.uint8)
+        t //= 10
+    nd = np.floor(np.log10(np.maximum(v, 1))).astype(np.int64) + 1
+    mask = np.arange(width)[None, :] >= (width - nd)[:, None]
+    return cols, mask
+
+
+def _names_buf(lane, tile, x, y) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """The names 'A00123:45:HXXXXXXX:lane:tile:x:y 1:N:0:ACGTACGT', '\0'
+    after each, built column-wise: (buffer, offsets [n + 1], name.l)."""
+    n = lane.shape[0]
+    parts, masks = [], []
+
+    def lit(b):
+        parts.append(np.broadcast_to(np.frombuffer(b, np.uint8), (n, len(b))))
+        masks.append(np.ones((n, len(b)), bool))
+    lit(b"A00123:45:HXXXXXXX:")
+    for i, (v, w) in enumerate(((lane, 1), (tile, 4), (x, 5), (y, 5))):
+        c, m = _digits(v, w)
+        parts.append(c)
+        masks.append(m)
+        if i < 3:
+            lit(b":")
+    lit(COMMENT + b"\0")
+    rows = np.concatenate(parts, 1)
+    mask = np.concatenate(masks, 1)
+    buf = rows[mask]
+    per = mask.sum(1).astype(np.int64)
+    off = np.zeros(n + 1, np.int64)
+    np.cumsum(per, out=off[1:])
+    name_l = (per - 1 - len(COMMENT)).astype(np.int32)
+    return np.ascontiguousarray(buf), off, name_l
+
+
+def _names(rng: np.random.Generator, n: int, as_list: bool):
     lane = rng.integers(1, 5, n)
     tile = rng.integers(1101, 2679, n)
     x = np.sort(rng.integers(1000, 32000, n))
     y = rng.integers(1000, 40000, n)
-    names = [b"A00123:45:HXXXXXXX:%d:%d:%d:%d 1:N:0:ACGTACGT" % t
-             for t in zip(lane.tolist(), tile.tolist(), x.tolist(), y.tolist())]
-    name_l = np.array([nm.index(b" ") for nm in names], dtype=np.int32)
-    return names, name_l
-
-
-def _name_lengths(rng: np.random.Generator, n: int) -> np.ndarray:
-    # Same digit-count distribution as _names() without building strings.
-    lane = rng.integers(1, 5, n)
-    tile = rng.integers(1101, 2679, n)
-    x = rng.integers(1000, 32000, n)
-    y = rng.integers(1000, 40000, n)
-    nd = lambda v: np.floor(np.log10(v)).astype(np.int32) + 1  # noqa: E731
-    return (len(b"A00123:45:HXXXXXXX") + 4 + nd(lane) + nd(tile) + nd(x)
-            + nd(y)).astype(np.int32)
+    buf, off, name_l = _names_buf(lane, tile, x, y)
+    names = None
+    if as_list:
+        names = [b"A00123:45:HXXXXXXX:%d:%d:%d:%d 1:N:0:ACGTACGT" % t
+                 for t in zip(lane.tolist(), tile.tolist(), x.tolist(), y.tolist())]
+    return names, name_l, buf, off
 
 
 def illumina(n_reads: int, seed: int = 1, read_len: int = 150,
@@ -117,11 +161,8 @@ def illumina(n_reads: int, seed: int = 1, read_len: int = 150,
     q = q.reshape(-1)
     qual = _illumina_bin(q) if binned else q.astype(np.uint8)
     lens = np.full(n_reads, read_len, dtype=np.uint32)
-    if with_names:
-        names, name_l = _names(rng, n_reads)
-    else:
-        names, name_l = None, _name_lengths(rng, n_reads)
-    return Reads(seq, qual.astype(np.uint8), lens, names, name_l)
+    names, name_l, nbuf, noff = _names(rng, n_reads, with_names)
+    return Reads(seq, qual.astype(np.uint8), lens, names, name_l, name_buf=nbuf, name_off=noff)
 
 
 def novaseq(n_reads: int, seed: int = 2, read_len: int = 150,
@@ -133,14 +174,10 @@ def novaseq(n_reads: int, seed: int = 2, read_len: int = 150,
     qual = levels[rng.choice(4, size=n_reads * read_len,
                              p=[.01, .04, .10, .85])]
     lens = np.full(n_reads, read_len, dtype=np.uint32)
-    if with_names:
-        names, name_l = _names(rng, n_reads)
-    else:
-        names, name_l = None, _name_lengths(rng, n_reads)
-    return Reads(seq, qual, lens, names, name_l)
+    names, name_l, nbuf, noff = _names(rng, n_reads, with_names)
+    return Reads(seq, qual, lens, names, name_l, name_buf=nbuf, name_off=noff)
 
 
-COMMENT = b" 1:N:0:ACGTACGT"      # the comment every synthetic name carries
 
 
 def fastq_size(r: Reads, a: int = 0, b: int | None = None) -> int:
@@ -172,9 +209,26 @@ def split_blocks(r: Reads, blk_size: int) -> list[tuple[int, int]]:
 def block(r: Reads, a: int, b: int) -> Reads:
     offs = np.concatenate([[0], np.cumsum(r.lens.astype(np.int64))])
     s, e = int(offs[a]), int(offs[b])
+    nb = no = None
+    if r.name_buf is not None:
+        nb = r.name_buf[r.name_off[a]:r.name_off[b]]
+        no = r.name_off[a:b + 1] - r.name_off[a]
     return Reads(r.seq[s:e], r.qual[s:e], r.lens[a:b],
                  r.names[a:b] if r.names is not None else None,
-                 r.name_l[a:b], None if r.flags is None else r.flags[a:b], r.comment_l)
+                 r.name_l[a:b], None if r.flags is None else r.flags[a:b], r.comment_l,
+                 nb, no)
+
+
+def all_names(r: Reads) -> tuple[np.ndarray, np.ndarray]:
+    """(buffer, offsets [n + 1]) of every name, '\0' after each: the name
+    section input of load_seqs_kseq (name [' ' comment] '\0')."""
+    if r.name_buf is not None:
+        return r.name_buf, r.name_off
+    assert r.names is not None
+    buf = np.frombuffer(b"".join(nm + b"\0" for nm in r.names), np.uint8).copy()
+    off = np.zeros(r.num_records + 1, np.int64)
+    np.cumsum([len(nm) + 1 for nm in r.names], out=off[1:])
+    return buf, off
 
 
 def _homopolymer_seq(rng: np.random.Generator, n: int) -> np.ndarray:

@@ -9,9 +9,18 @@
  * [strat u8][u32 usize][u32 csize][stream] (fqzcomp5.c:2217-2257).
  * A caller hands over a run of blocks at once; the choices equal those of a
  * single-threaded reference run over the same blocks in the same order.
- * This build implements the rANS methods (RANS0..RANS193, RANSXN1) and the
- * fqzcomp_qual methods FQZ0..FQZ4 (quality sections, strat byte 1); masks
- * with LZP/tok3/seq-CM bits are rejected.
+ * This build implements every method of the level presets: rANS (RANS0..
+ * RANS193, RANSXN1), LZP3, the sequence context models SEQ10..SEQ14B, the
+ * fqzcomp_qual methods FQZ0..FQZ4, and for name sections (FQZ5_SEC_NAME)
+ * TLZP3, TOK3_3..9 and TOK3_3..9_LZP (encode_names, fqzcomp5.c:1408-1586).
+ * A name section's output is encode_names' bytes [u32 name_len][u8 strat]
+ * [u32 clen][payload] (no extra frame); its input is the block's names,
+ * '\0' after each.  SEQ_CUSTOM is rejected.
+ *
+ * Blocks (encode_block / decode_block, fqzcomp5.c:2147-2547): the caller
+ * codes the name, sequence and quality sections with the calls above, then
+ * fqz5_blocks_assemble writes [u32 block_size][u32 nrec][u32 crc32] + names
+ * + lengths + sequence + quality per block; fqz5_block_parse reads one back.
  */
 #ifndef FQZ5_BLOCK_H
 #define FQZ5_BLOCK_H
@@ -112,6 +121,60 @@ void fqz5_trial_counts(uint64_t *out2);
 
 /* Decode framed sections (strat 0 = rANS) into their outputs. */
 int fqz5_decode_sections(const fqz5_section *secs, int n, fqz5_section_result *res);
+
+/* ---- blocks (fqzcomp5.c:2147-2547) ------------------------------------ */
+
+#define FQZ5_FREAD2 128           /* fqzcomp_qual.h:45 */
+
+/* Per-record flags the way load_seqs_kseq sets them (fqzcomp5.c:518-527):
+ * FQZ5_FREAD2 when the name (with its comment) ends in "/2" or equals the
+ * previous name of the block.  names: host, '\0' after each. */
+void fqz5_name_flags(const char *names, uint32_t name_len, int nrec, uint32_t *flags);
+
+/* The lengths section (fqzcomp5.c:2189-2214): [nb][varint fixed_len] when
+ * fixed_len != 0 (fq->fixed_len: -1 for a block without records), else
+ * [0][u32 size][varint per record].  Returns its size (<= 5 + 5 nrec), or
+ * -1 if cap is too small. */
+int fqz5_block_lengths(const uint32_t *len, int nrec, int32_t fixed_len, uint8_t *out,
+                       uint32_t cap);
+
+typedef struct {                  /* one block's coded parts */
+    int32_t nrec;
+    const uint8_t *name;          /* device: encode_names' bytes */
+    uint32_t name_size;
+    const uint8_t *lengths;       /* host: fqz5_block_lengths' bytes */
+    uint32_t lengths_size;
+    const uint8_t *seq;           /* device: framed sequence section */
+    uint32_t seq_size;
+    const uint8_t *qual;          /* device: framed quality section; NULL for */
+    uint32_t qual_size;           /*   FASTA (9 zero bytes are written) */
+} fqz5_block_parts;
+
+/* Write n blocks, block i at d_out + off[i] (device); size[i] receives its
+ * bytes (12 + parts; the caller sizes off[] with fqz5_block_size).  The
+ * CRC32 of bytes 12.. is computed on the device.  Returns 0 or -1. */
+uint64_t fqz5_block_size(const fqz5_block_parts *p);
+int fqz5_blocks_assemble(const fqz5_block_parts *parts, int n, uint8_t *d_out,
+                         const uint64_t *off, uint32_t *size);
+
+typedef struct {                  /* one block read back (decode_block) */
+    uint32_t block_size;          /* bytes after the block_size field */
+    uint32_t nrec;
+    int32_t crc_ok;               /* stored CRC equals the CRC of the block */
+    uint32_t name_off, name_size; /* encode_names' bytes, offsets in the block */
+    uint32_t name_ulen;           /* names' decoded size */
+    int32_t fixed_len;            /* 0: variable lengths */
+    uint32_t seq_off, seq_size;   /* framed sections */
+    uint32_t seq_ulen;
+    uint32_t qual_off, qual_size; /* qual_size 9 with qual_ulen 0: FASTA */
+    uint32_t qual_ulen;
+} fqz5_block_view;
+
+/* Parse the block at d_block (device, `avail` bytes readable): the layout,
+ * the CRC check and, when lens != NULL (nrec entries), the record lengths.
+ * Returns 0, or -1 on a malformed block. */
+int fqz5_block_parse(const uint8_t *d_block, uint64_t avail, fqz5_block_view *v,
+                     uint32_t *lens, uint32_t lens_cap);
 
 #ifdef __cplusplus
 }

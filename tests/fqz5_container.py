@@ -39,6 +39,19 @@ def _sec(buf, p):
     return Section(strat, u, bytes(buf[p + 9:p + 9 + c])), p + 9 + c
 
 
+def raw_blocks(path):
+    """Each block's bytes as the file holds them (block_size field first)."""
+    buf = open(path, "rb").read()
+    (idx,) = struct.unpack_from("<Q", buf, 8)
+    end = idx if idx else len(buf)
+    p, out = 16, []
+    while p < end:
+        (bsz,) = struct.unpack_from("<I", buf, p)
+        out.append(bytes(buf[p:p + 4 + bsz]))
+        p += 4 + bsz
+    return out
+
+
 def read(path):
     buf = open(path, "rb").read()
     assert buf[:8] == MAGIC, buf[:8]

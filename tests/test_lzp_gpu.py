@@ -74,7 +74,7 @@ def test_lzp3_wins_on_repeated_reads():
     pool = reads.seq[:150 * 3].reshape(3, 150).copy()     # 3 amplicons
     reads.seq[:] = pool[rng.integers(0, 3, reads.num_records)].reshape(-1)
     blocks = synth.split_blocks(reads, 2_000_000)
-    run = S.Run(reads, blocks, torch.device("cuda", 0))
+    run = S.Run(reads, blocks, torch.device("cuda", 0), names=False)
     res, meth_all, sizes, tried, _ = S.encode_run(run.enc_secs(), S.masks(3), S.new_state())
     codec = binding.ref() if binding.have_ref() else binding.oracle()
     seen = False

@@ -43,7 +43,7 @@ def test_run_vs_reference(level, kind, nreads, blk, cm):
     reads = GEN[kind](nreads, seed=11)
     blocks = synth.split_blocks(reads, blk)
     assert len(blocks) >= 5
-    run = S.Run(reads, blocks, torch.device("cuda", 0))
+    run = S.Run(reads, blocks, torch.device("cuda", 0), names=False)
     t0, p0 = S.trial_counts()
     res, meth_all, sizes, tried, _ = S.encode_run(run.enc_secs(), S.masks(level, cm), S.new_state())
     t1, p1 = S.trial_counts()
@@ -110,7 +110,7 @@ def test_arena_constant_over_steps():
     never rewound after fqz5_sections_commit."""
     reads = synth.illumina(20000, seed=5)
     blocks = synth.split_blocks(reads, 1_000_000)
-    run = S.Run(reads, blocks, torch.device("cuda", 0))
+    run = S.Run(reads, blocks, torch.device("cuda", 0), names=False)
     sizes = []
     for _ in range(8):
         res, *_ = S.encode_run(run.enc_secs(), S.masks(5), S.new_state())

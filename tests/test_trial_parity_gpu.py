@@ -1,14 +1,17 @@
 """Trial-choice parity with the reference: the reference
 CLI run single-threaded (-t1, the deterministic trial order) over a
-109-block file (-b 1M) picks, per block, the sequence and quality method by
-its codec trial (metrics_method / compress_with_methods,
+109-block file (-b 1M) picks, per block, the name, sequence and quality
+method by its codec trial (metrics_method / compress_with_methods,
 fqzcomp5.c:1899-1958, :2106; the first 3 blocks try every method, block 4
 fixes the winner, blocks 5-104 reuse it and block 105 re-trials,
 METRICS_REVIEW = 100, :151-152).  The GPU section coder over the same
 records must write, block for block, the same strat byte, the same sizes
-and the same bytes for both sections."""
+and the same bytes for all three sections, and the assembled blocks
+(header, CRC32, lengths: fqz5_blocks_assemble) must equal the file's
+blocks byte for byte and decode back to the records."""
 import hashlib
 import os
+import struct
 import subprocess
 
 import pytest
@@ -55,13 +58,29 @@ def test_trial_choices_match_reference(tmp_path, level, kind):
                                                   S.new_state())
     assert all(r.status == 0 for r in res)
     for i, (sec, s, e, fl, k) in enumerate(run.spans):
+        if sec == S.SEC_NAME:                       # encode_names' bytes, whole
+            want = ref[k].names
+            exp = struct.pack("<IBI", want.u_len, want.strat, len(want.data)) + want.data
+            assert (res[i].strat, res[i].clen) == (want.strat, len(exp)), (k, int(meth_all[i]))
+            assert run.chosen(res, i) == exp, (k, sec)
+            continue
         want = ref[k].seq if sec == S.SEC_SEQ else ref[k].qual
         assert (res[i].strat, res[i].usize, res[i].clen) == \
             (want.strat, want.u_len, len(want.data)), (k, sec, int(meth_all[i]))
         assert run.chosen(res, i) == want.data, (k, sec)
     # the run exercised a trial: blocks 1-3 and 105-107 tried every method
     for k in ((0, 1, 2, 104, 105, 106) if level <= 5 else (0, 1, 2)):
-        assert bin(int(tried[2 * k])).count("1") > 1 and bin(int(tried[2 * k + 1])).count("1") > 1
+        assert all(bin(int(tried[3 * k + j])).count("1") > 1 for j in (1, 2))
+    # whole blocks: header, CRC, lengths and sections as the file has them
+    run.assemble(res)
+    raw = F.raw_blocks(out)
+    for k in range(len(blocks)):
+        assert run.block_bytes(k) == raw[k], k
+    # and back: parse every block, decode its sections
+    dres = S.decode(run.block_dec_secs())
+    assert all(r.status == 0 for r in dres)
+    torch.cuda.synchronize()
+    assert run.roundtrip_ok()
 
 
 def test_sample_fastq_dropin_plumbing(tmp_path):
