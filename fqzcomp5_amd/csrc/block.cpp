@@ -18,7 +18,9 @@
 #include <cstring>
 #include <exception>
 #include <thread>
+#include <condition_variable>
 #include <deque>
+#include <mutex>
 #include <vector>
 
 #include "../../include/fqz5_block.h"
@@ -850,6 +852,43 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             who.push_back(i);
         }
         const auto t1 = std::chrono::steady_clock::now();
+        // the name sections on their helper context, beside the chains: their
+        // host rebuild overlaps the GPU's rANS / fqz / sequence decoding
+        // The long chains of the main batch take every CU they can (hedged
+        // copies), so the names' short GPU stages go first (~45 ms) and the
+        // chains start once they are done, while the names' host rebuild runs
+        // beside the chains.
+        std::exception_ptr nerr;
+        std::thread tn;
+        GpuCtx *gn = nullptr;
+        std::mutex nmu;
+        std::condition_variable ncv;
+        bool ngpu_done = nd.empty();
+        if (!nd.empty()) {
+            gn = &gpu_aux(AUX_NAMES);
+            tn = std::thread([&] {
+                auto release = [&] {
+                    std::lock_guard<std::mutex> lk(nmu);
+                    ngpu_done = true;
+                    ncv.notify_all();
+                };
+                try {
+                    FQZ5_HIP(hipSetDevice(gn->device));
+                    names_decode_batch(*gn, nd, release);
+                } catch (...) {
+                    nerr = std::current_exception();
+                }
+                release();
+            });
+        }
+        struct Join {                                 // joined on every exit
+            std::thread &t;
+            ~Join() { if (t.joinable()) t.join(); }
+        } join_names{tn};
+        {
+            std::unique_lock<std::mutex> lk(nmu);
+            ncv.wait(lk, [&] { return ngpu_done; });
+        }
         decompress_batch(g, reqs);
         if (trace)
             std::fprintf(stderr, "decode_sections: %zu bytes to host in %.1f ms, rANS %.1f ms\n", tot,
@@ -876,7 +915,8 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         // after the rANS and sequence sections: a quality section's sequence context may
         // be the output of this call's sequence section
         if (!fqz.empty()) fqz_decode_batch(g, fqz);
-        if (!nd.empty()) names_decode_batch(g, nd);
+        if (tn.joinable()) tn.join();
+        if (nerr) std::rethrow_exception(nerr);
         for (size_t k = 0; k < nd.size(); k++) {
             fqz5_section_result &R = res[who_name[k]];
             if (!nd[k].ok) continue;
@@ -903,10 +943,12 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             R.usize = uint32_t(fqz[k].out_size);
         }
         g.reset();
+        if (gn) gn->reset();
         return 0;
     } catch (const std::exception &e) {
         fqz5_set_error(e.what());
         try { gpu().reset(); } catch (...) {}
+        try { gpu_aux_reset_all(); } catch (...) {}
         return -1;
     }
 }

@@ -39,6 +39,8 @@ struct LzpEncJob {
 hipError_t launch_lzp_hash(const LzpEncJob &j, hipStream_t s);
 hipError_t launch_lzp_pred(const LzpEncJob &j, hipStream_t s);
 hipError_t launch_lzp_stops(const LzpEncJob &j, hipStream_t s);
+hipError_t launch_lzp_endscan(const LzpEncJob &j, hipStream_t s);
+hipError_t launch_lzp_resolve(const LzpEncJob &j, hipStream_t s);
 hipError_t launch_lzp_lengths(const LzpEncJob &j, hipStream_t s);
 hipError_t launch_lzp_parse(const LzpEncJob &j, hipStream_t s);      // chunks + walk
 hipError_t launch_lzp_sizes(const LzpEncJob &j, hipStream_t s);
@@ -47,6 +49,8 @@ hipError_t launch_lzp_emit(const LzpEncJob &j, hipStream_t s);
 hipError_t lzp_sort(const LzpEncJob &j, void *tmp, size_t &bytes, hipStream_t s);
 hipError_t lzp_min_scan(const LzpEncJob &j, void *tmp, size_t &bytes, hipStream_t s);
 hipError_t lzp_size_scan(const LzpEncJob &j, void *tmp, size_t &bytes, hipStream_t s);
+hipError_t lzp_sort_ends(const LzpEncJob &j, void *tmp, size_t &bytes, hipStream_t s);  // key/val by distance
+hipError_t lzp_end_scan(const LzpEncJob &j, void *tmp, size_t &bytes, hipStream_t s);   // val -> off
 
 // Decoder: one wave per block.  Literal runs go 64 bytes per step; each
 // marker byte looks up the hash table (65536 u32, zeroed) of its position.

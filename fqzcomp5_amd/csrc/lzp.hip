@@ -14,7 +14,13 @@
 //   L_i      the common prefix of in[i..] and in[pred_i..] (capped 65535):
 //            L_i = 1 + L_{i+1} when in[i] == in[pred_i] and pred_{i+1} ==
 //            pred_i + 1, so L is a backward segmented scan whose segment
-//            ends compare directly
+//            ends are computed directly.  An end i has distance d = i -
+//            pred_i; its common prefix is the run of in[k] == in[k - d] from
+//            i.  Ends sorted by (d, i): each compares bytes only up to the
+//            next end of the same distance, and when it gets there its run
+//            continues that end's (a second segmented scan).  Periodic input
+//            (the comments of a name block) thus costs a few bytes per end
+//            instead of up to 65535.
 //   tokens   a match of L_i >= 3 at i jumps to i + L_i, else i + 1.  Each
 //            64 KiB chunk parses from its own start speculatively; one walk
 //            joins them (the true path runs serially only until it meets a
@@ -57,7 +63,9 @@ __global__ void k_lzp_pred(LzpEncJob J) {
 
 // Segment ends of the backward length scan: position i links to i+1 when
 // in[i] == in[p] and pred[i+1] == p+1 (p = pred[i] > 0).  rev[n-1-i] = i at
-// an end, UINT32_MAX where linked; base[i] = the length at an end.
+// an end, UINT32_MAX where linked.  An end with in[i] != in[p] has length 0
+// (base[i]); the others get key = their distance i - p for the sort by
+// (distance, position), every other position the key n (last).
 __global__ void k_lzp_stops(LzpEncJob J) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = J.n;
@@ -65,18 +73,55 @@ __global__ void k_lzp_stops(LzpEncJob J) {
     const uint32_t p = J.pred[i];
     const bool eq = p > 0 && J.in[i] == J.in[p];
     const bool link = eq && i + 1 < n && J.pred[i + 1] == p + 1;
+    J.val[i] = i;
+    J.key[i] = (!link && eq) ? i - p : n;
     if (link) {
         J.rev[n - 1 - i] = 0xffffffffu;
         return;
     }
     J.rev[n - 1 - i] = i;
-    uint32_t L = 0;
-    if (eq) {
-        const uint32_t left = n - i;
-        const uint32_t lim = left < LZP_MAX_LEN ? left : LZP_MAX_LEN;
-        while (L < lim && J.in[i + L] == J.in[p + L]) L++;
+    if (!eq) J.base[i] = 0;
+}
+
+// Ends in (distance, position) order, k-th: compare from i = sval[k] at
+// distance d up to the next end of the same distance (or the cap / the
+// block end).  Reaching it links k to k+1 (rev2[n-1-k] = UINT32_MAX);
+// otherwise the run length is direct (dl[k]).  dl aliases key, rev2 val.
+__global__ void k_lzp_endscan(LzpEncJob J) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = J.n;
+    if (k >= n) return;
+    const uint32_t d = J.skey[k];
+    uint32_t *dl = J.key, *rev2 = J.val;
+    if (d >= n) {                                  // not an end to measure
+        rev2[n - 1 - k] = k;
+        dl[k] = 0;
+        return;
     }
-    J.base[i] = L;
+    const uint32_t i = J.sval[k];
+    const bool has_next = k + 1 < n && J.skey[k + 1] == d;
+    const uint32_t left = n - i;
+    const uint32_t lim = left < LZP_MAX_LEN ? left : LZP_MAX_LEN;
+    const uint32_t gap = has_next ? J.sval[k + 1] - i : 0xffffffffu;
+    const uint32_t stop = gap < lim ? gap : lim;
+    const uint8_t *a = J.in + i, *b = J.in + (i - d);
+    uint32_t L = 0;
+    while (L < stop && a[L] == b[L]) L++;
+    const bool linked = has_next && gap < lim && L == gap;
+    rev2[n - 1 - k] = linked ? 0xffffffffu : k;
+    dl[k] = L;
+}
+
+// After the min-scan of rev2 (into off): the first unlinked end k2 >= k of
+// the same distance; the run from i is (i2 - i) + dl[k2], capped.
+__global__ void k_lzp_resolve(LzpEncJob J) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = J.n;
+    if (k >= n || J.skey[k] >= n) return;
+    const uint32_t i = J.sval[k];
+    const uint32_t k2 = J.off[n - 1 - k];
+    const uint64_t L = uint64_t(J.sval[k2] - i) + J.key[k2];
+    J.base[i] = L > LZP_MAX_LEN ? LZP_MAX_LEN : uint32_t(L);
 }
 
 // match length per position: the next segment end e >= i gives
@@ -187,6 +232,14 @@ hipError_t launch_lzp_stops(const LzpEncJob &j, hipStream_t s) {
     if (j.n) hipLaunchKernelGGL(k_lzp_stops, grid_of(j.n), dim3(256), 0, s, j);
     return hipGetLastError();
 }
+hipError_t launch_lzp_endscan(const LzpEncJob &j, hipStream_t s) {
+    if (j.n) hipLaunchKernelGGL(k_lzp_endscan, grid_of(j.n), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+hipError_t launch_lzp_resolve(const LzpEncJob &j, hipStream_t s) {
+    if (j.n) hipLaunchKernelGGL(k_lzp_resolve, grid_of(j.n), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
 hipError_t launch_lzp_lengths(const LzpEncJob &j, hipStream_t s) {
     if (j.n) hipLaunchKernelGGL(k_lzp_lengths, grid_of(j.n), dim3(256), 0, s, j);
     return hipGetLastError();
@@ -212,6 +265,14 @@ hipError_t lzp_sort(const LzpEncJob &j, void *tmp, size_t &bytes, hipStream_t s)
 }
 hipError_t lzp_min_scan(const LzpEncJob &j, void *tmp, size_t &bytes, hipStream_t s) {
     return hipcub::DeviceScan::InclusiveScan(tmp, bytes, j.rev, j.nxt, hipcub::Min(), int(j.n), s);
+}
+static int bits_of(uint32_t n) { return n ? 32 - __builtin_clz(n) : 1; }
+hipError_t lzp_sort_ends(const LzpEncJob &j, void *tmp, size_t &bytes, hipStream_t s) {
+    return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, j.key, j.skey, j.val, j.sval, int(j.n),
+                                              0, bits_of(j.n), s);
+}
+hipError_t lzp_end_scan(const LzpEncJob &j, void *tmp, size_t &bytes, hipStream_t s) {
+    return hipcub::DeviceScan::InclusiveScan(tmp, bytes, j.val, j.off, hipcub::Min(), int(j.n), s);
 }
 hipError_t lzp_size_scan(const LzpEncJob &j, void *tmp, size_t &bytes, hipStream_t s) {
     return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, j.size, j.off, int(j.n), s);

@@ -53,16 +53,24 @@ void lzp_encode_batch(GpuCtx &g, std::vector<LzpEncReq> &reqs) {
         g.memset0(J.walk, n);
         FQZ5_HIP(hipMemsetAsync(J.conv, 0xff, size_t(J.nchunk) * 4, g.stream));
         FQZ5_HIP(launch_lzp_hash(J, g.stream));
-        size_t tb = 0, t2 = 0, t3 = 0;
+        size_t tb = 0, t2 = 0, t3 = 0, t4 = 0, t5 = 0;
         FQZ5_HIP(lzp_sort(J, nullptr, tb, g.stream));
         FQZ5_HIP(lzp_min_scan(J, nullptr, t2, g.stream));
         FQZ5_HIP(lzp_size_scan(J, nullptr, t3, g.stream));
-        const size_t tmax = std::max(tb, std::max(t2, t3));
+        FQZ5_HIP(lzp_sort_ends(J, nullptr, t4, g.stream));
+        FQZ5_HIP(lzp_end_scan(J, nullptr, t5, g.stream));
+        const size_t tmax = std::max({tb, t2, t3, t4, t5});
         void *tmp = g.arena.alloc_n<uint8_t>(tmax);
-        tb = t2 = t3 = tmax;
+        tb = t2 = t3 = t4 = t5 = tmax;
         FQZ5_HIP(lzp_sort(J, tmp, tb, g.stream));
         FQZ5_HIP(launch_lzp_pred(J, g.stream));
         FQZ5_HIP(launch_lzp_stops(J, g.stream));
+        // segment-end lengths: ends sorted by (distance, position), each run
+        // measured up to the next end of its distance, then linked
+        FQZ5_HIP(lzp_sort_ends(J, tmp, t4, g.stream));
+        FQZ5_HIP(launch_lzp_endscan(J, g.stream));
+        FQZ5_HIP(lzp_end_scan(J, tmp, t5, g.stream));
+        FQZ5_HIP(launch_lzp_resolve(J, g.stream));
         FQZ5_HIP(lzp_min_scan(J, tmp, t2, g.stream));
         FQZ5_HIP(launch_lzp_lengths(J, g.stream));
         FQZ5_HIP(launch_lzp_parse(J, g.stream));

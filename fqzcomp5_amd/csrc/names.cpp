@@ -4,6 +4,9 @@
 // columns, lzp outputs, flag bytes) and every decode as one batch each.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <mutex>
@@ -41,6 +44,14 @@ template <class F> void on_threads(size_t n, F fn) {
     work();
     for (auto &t : th) t.join();
     if (err) std::rethrow_exception(err);
+}
+bool trace() {
+    static const bool on = std::getenv("FQZ5_STEP_TRACE") != nullptr;
+    return on;
+}
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 }  // namespace
 
@@ -192,16 +203,24 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
                         const std::vector<const uint8_t *> &h_names,
                         const std::vector<const uint8_t *> &d_names,
                         const std::vector<uint32_t> &lens, const std::vector<int> &methods) {
+    const double t0 = trace() ? now_ms() : 0;
     on_threads(jobs.size(), [&](size_t k) {
         name_prepare(h_names[k], lens[k], name_strat(methods[k]), name_level(methods[k]), jobs[k]);
     });
+    const double t1 = trace() ? now_ms() : 0;
     std::vector<LzpEncReq> lz;
     for (size_t k = 0; k < jobs.size(); k++) name_add_lzp(g, jobs[k], d_names[k], lz);
     if (!lz.empty()) lzp_encode_batch(g, lz);
+    const double t2 = trace() ? now_ms() : 0;
     std::vector<CompressReq> reqs;
     for (auto &E : jobs) name_add_requests(g, E, lz, reqs);
     if (!reqs.empty()) compress_batch(g, reqs);
+    const double t3 = trace() ? now_ms() : 0;
     for (auto &E : jobs) name_assemble(g, E, reqs);
+    if (trace())
+        std::fprintf(stderr, "names encode: %zu candidates, tokenise %.1f ms, lzp %.1f ms, "
+                     "%zu rANS streams %.1f ms, assemble %.1f ms\n", jobs.size(), t1 - t0, t2 - t1,
+                     reqs.size(), t3 - t2, now_ms() - t3);
 }
 
 // ---------------------------------------------------------------------------
@@ -265,8 +284,9 @@ void name_dec_add_lzp(GpuCtx &g, NameDec &D, const std::vector<DecompressReq> &r
     lz.push_back(z);
 }
 
-void name_dec_finish(GpuCtx &g, NameDec &D, const std::vector<DecompressReq> &reqs,
-                     const std::vector<LzpDecReq> &lz) {
+void name_dec_fetch(GpuCtx &g, NameDec &D, const std::vector<DecompressReq> &reqs,
+                    const std::vector<LzpDecReq> &lz) {
+    D.fetched = false;
     D.ok = false;
     D.names.assign(D.u_len, 0);
     if (D.strat == 0) {
@@ -274,32 +294,46 @@ void name_dec_finish(GpuCtx &g, NameDec &D, const std::vector<DecompressReq> &re
         const uint32_t n = std::min(lz[size_t(D.lzp)].out_len, D.u_len);
         g.download(D.names.data(), D.d_lout, n);
         g.sync();
+        D.fetched = true;
+        return;
+    }
+    if (!tok3_dec_fetch(g, D.tok, reqs)) return;
+    if (D.strat == 2) {
+        if (D.req_flag < 0 || !reqs[size_t(D.req_flag)].ok) return;
+        if (D.clen2 && (D.lzp < 0 || !lz[size_t(D.lzp)].ok)) return;
+        D.fl.resize(reqs[size_t(D.req_flag)].out_size);
+        g.download(D.fl.data(), D.d_flag, D.fl.size());
+        if (D.clen2) {
+            D.out2.resize(lz[size_t(D.lzp)].out_len);
+            g.download(D.out2.data(), D.d_lout, D.out2.size());
+        }
+        g.sync();
+    }
+    D.fetched = true;
+}
+
+void name_dec_rebuild(NameDec &D) {
+    D.ok = false;
+    if (!D.fetched) return;
+    if (D.strat == 0) {
         D.ok = true;
         return;
     }
     std::vector<uint8_t> out1;
-    if (!tok3_dec_finish(g, D.tok, reqs, out1)) return;
+    if (!tok3_dec_rebuild(D.tok, out1)) return;
     if (D.strat == 1) {
         std::memcpy(D.names.data(), out1.data(), std::min<size_t>(out1.size(), D.u_len));
         D.ok = true;
         return;
     }
-    if (D.req_flag < 0 || !reqs[size_t(D.req_flag)].ok) return;
-    if (D.clen2 && (D.lzp < 0 || !lz[size_t(D.lzp)].ok)) return;
-    const uint32_t u_lenf = reqs[size_t(D.req_flag)].out_size;
-    std::vector<uint8_t> fl(u_lenf), out2;
-    g.download(fl.data(), D.d_flag, u_lenf);
-    if (D.clen2) {
-        out2.resize(lz[size_t(D.lzp)].out_len);
-        g.download(out2.data(), D.d_lout, out2.size());
-    }
-    g.sync();
     // stitch id + flag + comment (fqzcomp5.c:1683-1777)
+    const uint32_t u_lenf = uint32_t(D.fl.size());
     const size_t out_size = size_t(D.u_len) + size_t(u_lenf) * 2;
     std::vector<uint8_t> out(out_size, 0);
     const uint8_t *cp1 = out1.data(), *cp1_end = cp1 + out1.size();
-    const uint8_t *cpf = fl.data(), *cpf_end = cpf + fl.size();
-    const uint8_t *cp2 = D.clen2 ? out2.data() : nullptr, *cp2_end = cp2 + (cp2 ? out2.size() : 0);
+    const uint8_t *cpf = D.fl.data(), *cpf_end = cpf + D.fl.size();
+    const uint8_t *cp2 = D.clen2 ? D.out2.data() : nullptr;
+    const uint8_t *cp2_end = cp2 + (cp2 ? D.out2.size() : 0);
     uint8_t *cp = out.data(), *cp_end = cp + out_size, *last_cp = nullptr;
     int rec = 0;
     D.flags.assign(u_lenf, 0);
@@ -329,7 +363,15 @@ void name_dec_finish(GpuCtx &g, NameDec &D, const std::vector<DecompressReq> &re
     D.ok = true;
 }
 
-void names_decode_batch(GpuCtx &g, std::vector<NameDec> &jobs) {
+void name_dec_finish(GpuCtx &g, NameDec &D, const std::vector<DecompressReq> &reqs,
+                     const std::vector<LzpDecReq> &lz) {
+    name_dec_fetch(g, D, reqs, lz);
+    name_dec_rebuild(D);
+}
+
+void names_decode_batch(GpuCtx &g, std::vector<NameDec> &jobs,
+                        const std::function<void()> &fetched) {
+    const double t0 = trace() ? now_ms() : 0;
     std::vector<DecompressReq> reqs;
     std::vector<char> good(jobs.size());
     for (size_t k = 0; k < jobs.size(); k++) {
@@ -341,9 +383,17 @@ void names_decode_batch(GpuCtx &g, std::vector<NameDec> &jobs) {
     for (size_t k = 0; k < jobs.size(); k++)
         if (good[k]) name_dec_add_lzp(g, jobs[k], reqs, lz);
     if (!lz.empty()) lzp_decode_batch(g, lz);
+    const double t1 = trace() ? now_ms() : 0;
     for (size_t k = 0; k < jobs.size(); k++)
-        if (good[k]) name_dec_finish(g, jobs[k], reqs, lz);
-        else jobs[k].ok = false;
+        if (good[k]) name_dec_fetch(g, jobs[k], reqs, lz);
+        else jobs[k].fetched = false;
+    const double t2 = trace() ? now_ms() : 0;
+    if (fetched) fetched();
+    on_threads(jobs.size(), [&](size_t k) { name_dec_rebuild(jobs[k]); });
+    if (trace())
+        std::fprintf(stderr, "names decode: %zu sections, %zu rANS streams + lzp %.1f ms, "
+                     "fetch %.1f ms, rebuild %.1f ms\n", jobs.size(), reqs.size(), t1 - t0,
+                     t2 - t1, now_ms() - t2);
 }
 
 }  // namespace fqz5

@@ -12,6 +12,7 @@
 // payload [u32 clen1][u32 clenf][tok3][flags][comments].
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "lzp_codec.hpp"
@@ -79,6 +80,8 @@ struct NameDec {
     std::vector<uint8_t> names;      // u_len bytes
     std::vector<uint32_t> flags;     // strat 2: FQZ_FREAD2 per decoded record
     int nrec = 0;                    // strat 2: decode_names' *out_num_records
+    bool fetched = false;            // name_dec_fetch: the device outputs on the host
+    std::vector<uint8_t> fl, out2;   // strat 2: flag bytes, comments
 };
 
 // decode_names (fqzcomp5.c:1588-1794) in stages over a batch.
@@ -86,8 +89,15 @@ bool name_dec_parse(NameDec &D);
 void name_dec_add_requests(GpuCtx &g, NameDec &D, std::vector<DecompressReq> &reqs);
 void name_dec_add_lzp(GpuCtx &g, NameDec &D, const std::vector<DecompressReq> &reqs,
                       std::vector<LzpDecReq> &lz);
+// = name_dec_fetch (downloads; serial per context) + name_dec_rebuild
+// (host only: any thread).
 void name_dec_finish(GpuCtx &g, NameDec &D, const std::vector<DecompressReq> &reqs,
                      const std::vector<LzpDecReq> &lz);
-void names_decode_batch(GpuCtx &g, std::vector<NameDec> &jobs);
+void name_dec_fetch(GpuCtx &g, NameDec &D, const std::vector<DecompressReq> &reqs,
+                    const std::vector<LzpDecReq> &lz);
+void name_dec_rebuild(NameDec &D);
+// fetched (optional) runs once the GPU work is done, before the host rebuild
+void names_decode_batch(GpuCtx &g, std::vector<NameDec> &jobs,
+                        const std::function<void()> &fetched = {});
 
 }  // namespace fqz5

@@ -38,11 +38,20 @@ enum NameType : int {                           // :81-82
     N_DIGITS, N_DDELTA, N_DDELTA0, N_MATCH, N_NOP, N_END, N_ALL
 };
 
+// <ctype.h> classes of the C locale, for 7-bit bytes (the names are 7-bit)
+inline bool c_alpha(uint8_t c) { return uint8_t((c | 32) - 'a') < 26; }
+inline bool c_digit(uint8_t c) { return uint8_t(c - '0') < 10; }
+inline bool c_space(uint8_t c) { return c == ' ' || uint8_t(c - 9) < 5; }
+inline bool c_punct(uint8_t c) { return c > 32 && c < 127 && !c_alpha(c) && !c_digit(c); }
+inline bool c_xdigit(uint8_t c) { return c_digit(c) || uint8_t((c | 32) - 'a') < 6; }
+
 struct Tok { int type = 0, ival = 0, sval = 0; };    // last_context_tok
-struct Last {                                         // last_context
+// last_context: a name's tokens live in one arena per block (a finished
+// name's tokens never change, so a duplicate shares its original's)
+struct Last {
     const char *name = nullptr;
     int ntok = 0;
-    std::vector<Tok> tok;
+    uint32_t off = 0;                                  // first token in the arena
 };
 
 // ---------------------------------------------------------------------------
@@ -53,29 +62,12 @@ struct Trie {
     struct Node { int next = -1, sib = -1; uint8_t c = 0; uint32_t n = 0; };
     std::vector<Node> nodes{Node()};                   // node 0: the root
 
-    bool build(const char *d, size_t len, uint32_t n) {
-        int t = 0;
-        for (size_t i = 0; i < len && uint8_t(d[i]) > '\n'; i++) {
-            const uint8_t c0 = uint8_t(d[i]);
-            if (c0 & 0x80) return false;               // :498-500
-            const uint8_t c = c0 & 127;
-            int x = nodes[size_t(t)].next, l = -1;
-            while (x >= 0 && nodes[size_t(x)].c != c) { l = x; x = nodes[size_t(x)].sib; }
-            if (x < 0) {
-                Node nn;
-                nn.c = c;
-                nn.n = n & 0xffffffu;
-                nodes.push_back(nn);
-                x = int(nodes.size()) - 1;
-                if (l < 0) nodes[size_t(t)].next = x;
-                else nodes[size_t(l)].sib = x;
-            }
-            t = x;
-        }
-        return true;
-    }
-
-    // -> the name to tokenise against, or -1 (:591-695)
+    // -> the name to tokenise against, or -1 (:591-695).  Fused with
+    // build_trie: the reference builds the trie of every name first (a node
+    // holding its first name) and then searches name by name (each visit
+    // leaving the visitor's number), so at name n's visit a node holds the
+    // last earlier name through it, or n itself when n is the first.  A node
+    // created here on first sight holds n: the same values in one pass.
     int search(const char *data, size_t len, uint32_t n, int *exact, int *is_fixed,
                int *fixed_len) {
         int from = -1, p3 = -1;
@@ -86,7 +78,7 @@ struct Trie {
         const char *d = *data == '@' ? data + 1 : data;
         const int l = *data == '@' ? int(len) - 1 : int(len);
         const int f = (*data == '>') ? 1 : 0;
-        auto xd = [](char c) { return std::isxdigit(uint8_t(c)) != 0; };
+        auto xd = [](char c) { return c_xdigit(uint8_t(c)); };
         if (l > 70 && d[f + 0] == 'm' && d[7] == '_' && d[f + 14] == '_' && d[f + 61] == '/') {
             prefix_len = 60;                           // PacBio
             *is_fixed = 0;
@@ -122,12 +114,21 @@ struct Trie {
             const uint8_t c0 = uint8_t(data[i++]);
             if (c0 & 0x80) return -1;
             const uint8_t c = c0 & 127;
-            int x = nodes[size_t(t)].next;
-            while (x >= 0 && nodes[size_t(x)].c != c) x = nodes[size_t(x)].sib;
-            t = x;                                     // present: built from every name
+            int x = nodes[size_t(t)].next, l = -1;
+            while (x >= 0 && nodes[size_t(x)].c != c) { l = x; x = nodes[size_t(x)].sib; }
+            if (x < 0) {                               // build_trie's node, made by n
+                Node nn;
+                nn.c = c;
+                nn.n = n & 0xffffffu;
+                nodes.push_back(nn);
+                x = int(nodes.size()) - 1;
+                if (l < 0) nodes[size_t(t)].next = x;
+                else nodes[size_t(l)].sib = x;
+            }
+            t = x;
             Node &T = nodes[size_t(t)];
             from = int(T.n);
-            if ((std::ispunct(c) || std::isspace(c)) && T.n != (n & 0xffffffu))
+            if ((c_punct(c) || c_space(c)) && T.n != (n & 0xffffffu))
                 from_punct = int(T.n);
             if (int(i) == prefix_len) p3 = int(T.n);
             T.n = n & 0xffffffu;
@@ -144,6 +145,7 @@ struct Encoder {
     int max_tok = 1;                                 // create_context (:204)
     int counter = 0;
     std::vector<Last> lc;
+    std::vector<Tok> toks;                             // every name's tokens
     Trie trie;
 
     void grow_tok(int ntok) {                          // the reference's max_tok resets
@@ -189,33 +191,40 @@ struct Encoder {
             tint(0, N_DUP, uint32_t(cnum - pnum));
             C.name = nm;
             C.ntok = P.ntok;
-            C.tok.assign(P.tok.begin(), P.tok.begin() + std::min<size_t>(P.tok.size(), size_t(P.ntok)));
-            C.tok.resize(size_t(std::max(P.ntok, 1)));
+            C.off = P.off;
             return true;
         }
-        C.tok.assign(MAX_TOKENS, Tok());
+        C.off = uint32_t(toks.size());
+        // slot t of this name exists before any pointer into the arena is
+        // taken for step t (growing it moves the arena)
+        auto ensure = [&](int t) {
+            if (toks.size() < size_t(C.off) + size_t(t) + 1) toks.resize(size_t(C.off) + size_t(t) + 1);
+        };
+        auto ct = [&](int t) -> Tok & { return toks[size_t(C.off) + size_t(t)]; };
         tint(0, N_DIFF, uint32_t(cnum - pnum));
         int ntok = 1, i;
         auto ptok = [&](int t) -> const Tok * {
-            return (pnum < cnum && t < P.ntok) ? &P.tok[size_t(t)] : nullptr;
+            return (pnum < cnum && t < P.ntok) ? &toks[size_t(P.off) + size_t(t)] : nullptr;
         };
         if (fixed_len == 36) {                         // ONT uuid (:735-752)
             if (37 >= max_tok) grow_tok(37);
             for (i = 0; i < 36; i++, ntok++) {
                 chr(ntok, nm[i]);
-                C.tok[size_t(ntok)] = {N_CHAR, nm[i], 0};
+                ensure(ntok);
+                ct(ntok) = {N_CHAR, nm[i], 0};
             }
             is_fixed = 0;
             i = 36;
         } else if (is_fixed) {                         // :753-773
             if (ntok >= max_tok) grow_tok(ntok);
+            ensure(ntok);
             const Tok *pt = ptok(ntok);
             if (pt && pt->type == N_ALPHA && pt->ival == fixed_len &&
                 std::memcmp(nm, P.name, size_t(fixed_len)) == 0)
                 type(ntok, N_MATCH);
             else
                 alpha(ntok, nm, fixed_len);
-            C.tok[size_t(ntok++)] = {N_ALPHA, fixed_len, 0};
+            ct(ntok++) = {N_ALPHA, fixed_len, 0};
             i = fixed_len;
         } else {
             i = 0;
@@ -225,11 +234,12 @@ struct Encoder {
                 if (max_tok >= MAX_TOKENS) return false;
                 grow_tok(ntok);
             }
+            ensure(ntok);
             const uint8_t ci = uint8_t(nm[i]);
             bool as_char = false;
-            if (std::isalpha(ci)) {                    // :791-838
+            if (c_alpha(ci)) {                         // :791-838
                 int s = i + 1;
-                while (s < len && (std::isalpha(uint8_t(nm[s])) || std::ispunct(uint8_t(nm[s])))) s++;
+                while (s < len && (c_alpha(uint8_t(nm[s])) || c_punct(uint8_t(nm[s])))) s++;
                 if (s - i == 1) {
                     as_char = true;
                 } else {
@@ -239,14 +249,14 @@ struct Encoder {
                         type(ntok, N_MATCH);
                     else
                         alpha(ntok, &nm[i], s - i);
-                    C.tok[size_t(ntok)] = {N_ALPHA, s - i, i};
+                    ct(ntok) = {N_ALPHA, s - i, i};
                     i = s - 1;
                 }
-            } else if (std::isdigit(ci)) {
+            } else if (c_digit(ci)) {
                 // digits (:839-943); a leading 0, or the previous name's
                 // token being DIGITS0 of the same length, codes DIGITS0
                 uint32_t s = uint32_t(i), v = 0;
-                while (s < uint32_t(len) && std::isdigit(uint8_t(nm[s])) && s - uint32_t(i) < 9) {
+                while (s < uint32_t(len) && c_digit(uint8_t(nm[s])) && s - uint32_t(i) < 9) {
                     v = v * 10 + uint32_t(nm[s] - '0');
                     s++;
                 }
@@ -268,7 +278,7 @@ struct Encoder {
                         tint1_(ntok, N_DZLEN, dl);
                         tint(ntok, N_DIGITS0, v);
                     }
-                    C.tok[size_t(ntok)] = {N_DIGITS0, int(v), int(dl)};
+                    ct(ntok) = {N_DIGITS0, int(v), int(dl)};
                 } else {
                     if (pt && pt->type == N_DIGITS) {
                         const int d = int(v - uint32_t(pt->ival));
@@ -285,8 +295,8 @@ struct Encoder {
                         tint(ntok, N_DIGITS, v);
                     }
                     // token_str keeps whatever this slot held (:939-941)
-                    C.tok[size_t(ntok)].type = N_DIGITS;
-                    C.tok[size_t(ntok)].ival = int(v);
+                    ct(ntok).type = N_DIGITS;
+                    ct(ntok).ival = int(v);
                 }
                 i = int(s) - 1;
             } else {
@@ -298,8 +308,8 @@ struct Encoder {
                     type(ntok, N_MATCH);
                 else
                     chr(ntok, nm[i]);
-                C.tok[size_t(ntok)].type = N_CHAR;
-                C.tok[size_t(ntok)].ival = nm[i];
+                ct(ntok).type = N_CHAR;
+                ct(ntok).ival = nm[i];
             }
             ntok++;
         }
@@ -308,9 +318,9 @@ struct Encoder {
             grow_tok(ntok);
         }
         type(ntok, N_END);
+        ensure(ntok);
         C.name = nm;
         C.ntok = ntok;
-        C.tok.resize(size_t(ntok + 1));
         return true;
     }
 };
@@ -359,13 +369,12 @@ bool tok3_tokenise(char *blk, int len, int level, int use_arith, Tok3Enc &T) {
     if (nreads <= 0 || nreads > 10000000) return false;     // create_context (:172-187)
     Encoder E;
     E.lc.resize(size_t(nreads) + 1);
-    int ctr = 0;                                       // the trie of all names (:1469-1482)
-    for (i = j = 0; i < len; j = ++i) {
-        while (i < len && blk[i] > '\n') i++;
-        if (i >= len) break;
-        last_start = i + 1;
-        if (!E.trie.build(&blk[j], size_t(i - j), uint32_t(ctr++))) return false;
-    }
+    E.trie.nodes.reserve(size_t(len) / 4 + 16);
+    // the trie of all names (:1469-1482) is built inside the search (Trie::
+    // search); its loop's line ends give last_start (it cannot fail: its
+    // lines hold no byte >= 0x80)
+    for (i = len - 1; i >= 0; i--)
+        if (blk[i] <= '\n') { last_start = i + 1; break; }
     T.last_start = last_start;
     for (i = j = 0; i < len; j = ++i) {                // names (:1487-1505)
         while (i < len && static_cast<signed char>(blk[i]) >= ' ') i++;
@@ -618,12 +627,10 @@ void tok3_dec_add_requests(GpuCtx &g, Tok3Dec &D, const uint8_t *d_in,
     }
 }
 
-bool tok3_dec_finish(GpuCtx &g, const Tok3Dec &D, const std::vector<DecompressReq> &reqs,
-                     std::vector<uint8_t> &out) {
-    struct Desc { std::vector<uint8_t> buf; size_t l = 0; bool have = false; };
-    std::vector<Desc> desc(MAX_TBLOCKS);
-    const int nreads = D.nreads, max_tok = D.max_tok;
-    std::vector<std::vector<uint8_t>> dec(D.coded.size());
+bool tok3_dec_fetch(GpuCtx &g, Tok3Dec &D, const std::vector<DecompressReq> &reqs) {
+    D.fetched = false;
+    D.dec.assign(D.coded.size(), {});
+    std::vector<std::vector<uint8_t>> &dec = D.dec;
     if (!D.use_arith) {
         for (size_t k = 0; k < D.coded.size(); k++) {
             const DecompressReq &r = reqs[D.req0 + k];
@@ -647,6 +654,21 @@ bool tok3_dec_finish(GpuCtx &g, const Tok3Dec &D, const std::vector<DecompressRe
             dec[k].resize(ol);
         }
     }
+    D.fetched = true;
+    return true;
+}
+
+bool tok3_dec_finish(GpuCtx &g, Tok3Dec &D, const std::vector<DecompressReq> &reqs,
+                     std::vector<uint8_t> &out) {
+    return tok3_dec_fetch(g, D, reqs) && tok3_dec_rebuild(D, out);
+}
+
+bool tok3_dec_rebuild(Tok3Dec &D, std::vector<uint8_t> &out) {
+    if (!D.fetched) return false;
+    struct Desc { std::vector<uint8_t> buf; size_t l = 0; bool have = false; };
+    std::vector<Desc> desc(MAX_TBLOCKS);
+    const int nreads = D.nreads, max_tok = D.max_tok;
+    std::vector<std::vector<uint8_t>> &dec = D.dec;
     for (auto &e : D.order) {                          // in stream order, as the reference
         if (e.first == 2) {                            // an elided type stream: ty then MATCH
             Desc &c = desc[size_t(e.second & ~15)];
@@ -706,6 +728,7 @@ bool tok3_dec_finish(GpuCtx &g, const Tok3Dec &D, const std::vector<DecompressRe
     int64_t ulen = int64_t(D.ulen0) + 1024;
     std::vector<char> outb(static_cast<size_t>(ulen));
     std::vector<Last> lc(size_t(nreads) + 1);          // max_names = nreads + 1 (:190)
+    std::vector<Tok> toks;
     size_t osz = 0;
     int counter = 0, ret = 0;
     for (;;) {
@@ -729,20 +752,22 @@ bool tok3_dec_finish(GpuCtx &g, const Tok3Dec &D, const std::vector<DecompressRe
             std::memcpy(nm, P.name, pl + 1);
             C.name = nm;
             C.ntok = P.ntok;
-            C.tok = P.tok;
+            C.off = P.off;
             ret = int(pl) + 1;
         } else {
             *nm = 0;
             int64_t len = 0;
-            C.tok.assign(MAX_TOKENS, Tok());
+            C.off = uint32_t(toks.size());
             int ntok;
             bool done = false, bad = false;
             for (ntok = 1; ntok < MAX_TOKENS && ntok < max_tok && !done && !bad; ntok++) {
                 uint32_t v, vl;
                 const int tok = dtype(ntok);
                 C.ntok = 0;
-                Tok &T = C.tok[size_t(ntok)];
-                const Tok *pt = ntok < P.ntok ? &P.tok[size_t(ntok)] : nullptr;
+                if (toks.size() < size_t(C.off) + size_t(ntok) + 1)
+                    toks.resize(size_t(C.off) + size_t(ntok) + 1);
+                Tok &T = toks[size_t(C.off) + size_t(ntok)];
+                const Tok *pt = ntok < P.ntok ? &toks[size_t(P.off) + size_t(ntok)] : nullptr;
                 switch (tok) {
                 case N_CHAR:
                     if (len + 1 >= nlen || !dint1(ntok, N_CHAR, &v)) { bad = true; break; }
@@ -833,7 +858,6 @@ bool tok3_dec_finish(GpuCtx &g, const Tok3Dec &D, const std::vector<DecompressRe
                     T.type = N_END;
                     C.name = nm;
                     C.ntok = ntok;
-                    C.tok.resize(size_t(ntok + 1));
                     done = true;
                     ret = int(len);
                     break;

@@ -51,6 +51,8 @@ struct Tok3Dec {
     uint8_t *d_out = nullptr;                                // the decoded streams, back to back
     std::vector<size_t> out_off;
     size_t out_tot = 0;
+    std::vector<std::vector<uint8_t>> dec;                   // tok3_dec_fetch: host copies
+    bool fetched = false;
 };
 
 // Parse the stream layout (tokenise_name3.c:1679-1809); false = NULL.
@@ -60,8 +62,12 @@ bool tok3_dec_parse(const uint8_t *in, uint32_t sz, Tok3Dec &D);
 void tok3_dec_add_requests(GpuCtx &g, Tok3Dec &D, const uint8_t *d_in,
                            std::vector<DecompressReq> &reqs);
 // After decompress_batch: the names, '\0' after each; false = NULL.
-bool tok3_dec_finish(GpuCtx &g, const Tok3Dec &D, const std::vector<DecompressReq> &reqs,
+// = tok3_dec_fetch (the decoded streams to the host; arith streams decoded)
+// + tok3_dec_rebuild (host only: any thread).
+bool tok3_dec_finish(GpuCtx &g, Tok3Dec &D, const std::vector<DecompressReq> &reqs,
                      std::vector<uint8_t> &out);
+bool tok3_dec_fetch(GpuCtx &g, Tok3Dec &D, const std::vector<DecompressReq> &reqs);
+bool tok3_dec_rebuild(Tok3Dec &D, std::vector<uint8_t> &out);
 
 // Host copies of device layouts: one gather on the device, one copy down.
 void download_layouts(GpuCtx &g, const std::vector<const Layout *> &ls,

@@ -219,6 +219,57 @@ def block(r: Reads, a: int, b: int) -> Reads:
                  nb, no)
 
 
+def fastq_chunk(r: Reads, a: int, b: int, names=None) -> np.ndarray:
+    """FASTQ text of records [a, b) as to_fastq writes it, built with
+    vectorised scatters: '@' name '\\n' seq '\\n+\\n' qual+33 '\\n'."""
+    buf, off = names if names is not None else all_names(r)
+    n = b - a
+    nl = (off[a + 1:b + 1] - off[a:b] - 1).astype(np.int64)
+    L = r.lens[a:b].astype(np.int64)
+    rec = nl + 2 * L + 6
+    start = np.zeros(n + 1, np.int64)
+    np.cumsum(rec, out=start[1:])
+    out = np.empty(int(start[-1]), np.uint8)
+    st = start[:-1]
+    out[st] = ord("@")
+
+    def scatter(src, lengths, base):
+        tot = int(lengths.sum())
+        if not tot:
+            return
+        ri = np.repeat(np.arange(n), lengths)
+        first = np.zeros(n, np.int64)
+        np.cumsum(lengths[:-1], out=first[1:])
+        within = np.arange(tot, dtype=np.int64) - first[ri]
+        out[base[ri] + within] = src
+    nb = buf[off[a]:off[b]]
+    scatter(nb[nb != 0], nl, st + 1)
+    out[st + 1 + nl] = ord("\n")
+    boff = np.concatenate([[0], np.cumsum(r.lens.astype(np.int64))])
+    s, e = int(boff[a]), int(boff[b])
+    scatter(r.seq[s:e], L, st + nl + 2)
+    q0 = st + nl + 2 + L
+    out[q0] = ord("\n")
+    out[q0 + 1] = ord("+")
+    out[q0 + 2] = ord("\n")
+    scatter((r.qual[s:e] + 33).astype(np.uint8), L, q0 + 3)
+    out[st + rec - 1] = ord("\n")
+    return out
+
+
+def write_fastq(r: Reads, path: str, chunk: int = 200_000) -> int:
+    """Write the reads as FASTQ text (to_fastq's bytes) in chunks; returns
+    the bytes written."""
+    names = all_names(r)
+    tot = 0
+    with open(path, "wb") as f:
+        for a in range(0, r.num_records, chunk):
+            c = fastq_chunk(r, a, min(a + chunk, r.num_records), names)
+            f.write(c.tobytes())
+            tot += c.shape[0]
+    return tot
+
+
 def all_names(r: Reads) -> tuple[np.ndarray, np.ndarray]:
     """(buffer, offsets [n + 1]) of every name, '\0' after each: the name
     section input of load_seqs_kseq (name [' ' comment] '\0')."""
