@@ -1,0 +1,433 @@
+// fastq.hip — FASTQ text in HBM to fqzcomp5 blocks and back:
+// the record parse of load_seqs_kseq (fqzcomp5.c:423-623, kseq.h:178-218)
+// for 4-line FASTQ, its block split rule (fqzcomp5.c:471-477), the gather of
+// a block's name / sequence / quality sections with the records' lengths and
+// READ2 flags, and output_fastq (fqzcomp5.c:3441-3480) on decoded blocks.
+//
+// Lines: every '\n' of the text is found by 64 KiB tiles (counts, a scan,
+// then ordered writes), so record r is lines 4r..4r+3.  Records are parsed
+// one per thread; the section bytes are gathered one wave per record at the
+// scanned offsets.  Text that is not 4-line FASTQ (multi-line sequences,
+// FASTA) is refused with an error, never parsed on the host.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/fqz5_fastq.h"
+#include "gpu_ctx.hpp"
+
+namespace fqz5 {
+GpuCtx &gpu();
+void fqz5_set_error(const char *msg);
+
+namespace {
+
+constexpr int FQ_TPB = 256;
+constexpr uint32_t FQ_STEP = FQ_TPB * 16;          // bytes per workgroup iteration
+constexpr uint32_t FQ_ITERS = 16;
+constexpr uint64_t FQ_TILE = uint64_t(FQ_STEP) * FQ_ITERS;   // 64 KiB
+
+__device__ __forceinline__ uint32_t count_in16(const uint8_t *t, uint64_t at, uint64_t len,
+                                               uint8_t ch) {
+    uint32_t c = 0;
+    if (at + 16 <= len && !(reinterpret_cast<uintptr_t>(t + at) & 15)) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(t + at);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) c += ((w[k] >> (8 * b)) & 0xffu) == ch;
+    } else {
+        const uint64_t e = at + 16 < len ? at + 16 : len;
+        for (uint64_t p = at; p < e; p++) c += t[p] == ch;
+    }
+    return c;
+}
+
+// per 64 KiB tile: the number of `ch` bytes
+__global__ void k_delim_count(const uint8_t *t, uint64_t len, uint8_t ch, uint32_t *tile_cnt) {
+    using BR = hipcub::BlockReduce<uint32_t, FQ_TPB>;
+    __shared__ typename BR::TempStorage tmp;
+    const uint64_t base = uint64_t(blockIdx.x) * FQ_TILE;
+    uint32_t c = 0;
+    for (uint32_t it = 0; it < FQ_ITERS; it++) {
+        const uint64_t at = base + uint64_t(it) * FQ_STEP + uint64_t(threadIdx.x) * 16;
+        if (at < len) c += count_in16(t, at, len, ch);
+    }
+    const uint32_t s = BR(tmp).Sum(c);
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = s;
+}
+
+// positions of every `ch` byte, in text order, from the tiles' scanned counts
+__global__ void k_delim_write(const uint8_t *t, uint64_t len, uint8_t ch, const uint32_t *tile_off,
+                              uint64_t *pos) {
+    using BS = hipcub::BlockScan<uint32_t, FQ_TPB>;
+    __shared__ typename BS::TempStorage tmp;
+    const uint64_t base = uint64_t(blockIdx.x) * FQ_TILE;
+    uint64_t o = tile_off[blockIdx.x];
+    for (uint32_t it = 0; it < FQ_ITERS; it++) {
+        const uint64_t at = base + uint64_t(it) * FQ_STEP + uint64_t(threadIdx.x) * 16;
+        const uint32_t c = at < len ? count_in16(t, at, len, ch) : 0u;
+        uint32_t ex, tot;
+        BS(tmp).ExclusiveSum(c, ex, tot);
+        __syncthreads();
+        if (c) {
+            uint64_t w = o + ex;
+            const uint64_t e = at + 16 < len ? at + 16 : len;   // (count_in16's bytes)
+            for (uint64_t p = at; p < e; p++)
+                if (t[p] == ch) pos[w++] = p;
+        }
+        o += tot;
+    }
+}
+
+__device__ __forceinline__ bool ks_space(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }
+
+// kseq's line read: drop a trailing '\r' when the line has more than one
+// byte (kseq.h:141)
+__device__ __forceinline__ uint64_t strip_cr(const uint8_t *t, uint64_t s, uint64_t e) {
+    return (e - s > 1 && t[e - 1] == '\r') ? e - 1 : e;
+}
+
+// record r = lines 4r..4r+3 (kseq_read, kseq.h:178-218)
+__global__ void k_fq_records(const uint8_t *t, const uint64_t *nl, uint64_t nrec,
+                             fqz5_fastq_rec *recs, uint32_t *rec_size, int32_t *status) {
+    const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    const uint64_t s0 = r ? nl[4 * r - 1] + 1 : 0, e0 = nl[4 * r];
+    const uint64_t s1 = e0 + 1, e1 = nl[4 * r + 1];
+    const uint64_t s2 = e1 + 1, e2 = nl[4 * r + 2];
+    const uint64_t s3 = e2 + 1, e3 = nl[4 * r + 3];
+    int bad = 0;
+    if (e0 <= s0 || t[s0] != '@') bad = 1;            // header
+    if (e2 <= s2 || t[s2] != '+') bad = 1;            // '+' line
+    if (e1 > s1 && (t[s1] == '@' || t[s1] == '>' || t[s1] == '+')) bad = 1;
+    // name up to the first isspace(), the comment after it to the line end
+    uint64_t p = s0 + 1;
+    while (p < e0 && !ks_space(t[p])) p++;
+    fqz5_fastq_rec R;
+    R.name = s0 + 1;
+    R.name_len = uint32_t(p - (s0 + 1));
+    R.comment = p < e0 ? p + 1 : e0;
+    R.comment_len = p < e0 ? uint32_t(strip_cr(t, p + 1, e0) - (p + 1)) : 0u;
+    R.seq = s1;
+    R.seq_len = uint32_t(strip_cr(t, s1, e1) - s1);
+    R.qual = s3;
+    const uint32_t ql = uint32_t(strip_cr(t, s3, e3) - s3);
+    if (ql != R.seq_len) bad = 1;                     // kseq -2 (:213-216)
+    recs[r] = R;
+    rec_size[r] = R.name_len + 1 + 2 * R.seq_len;     // load_seqs_kseq's record_size (:472)
+    if (bad) atomicMin(status, int32_t(-1 - int32_t(r < 0x7ffffffeull ? r : 0x7ffffffeull)));
+}
+
+// per record of [a, b): name bytes (name [' ' comment] '\0') and bases
+__global__ void k_fq_counts(const fqz5_fastq_rec *recs, uint64_t a, uint64_t n, uint32_t *nb,
+                            uint32_t *sb) {
+    const uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const fqz5_fastq_rec R = recs[a + k];
+    nb[k] = R.name_len + (R.comment_len ? 1 + R.comment_len : 0) + 1;
+    sb[k] = R.seq_len;
+}
+
+// one wave per record: the names (name ' ' comment '\0'), the bases and the
+// qualities - 33 (load_seqs_kseq, fqzcomp5.c:491-565)
+__global__ void k_fq_gather(const uint8_t *t, const fqz5_fastq_rec *recs, uint64_t a, uint64_t n,
+                            const uint32_t *noff, const uint32_t *soff, uint8_t *names,
+                            uint8_t *seq, uint8_t *qual) {
+    const uint64_t k = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (k >= n) return;
+    const fqz5_fastq_rec R = recs[a + k];
+    uint8_t *o = names + noff[k];
+    for (uint32_t i = lane; i < R.name_len; i += 64) o[i] = t[R.name + i];
+    uint32_t w = R.name_len;
+    if (R.comment_len) {
+        if (lane == 0) o[w] = ' ';
+        for (uint32_t i = lane; i < R.comment_len; i += 64) o[w + 1 + i] = t[R.comment + i];
+        w += 1 + R.comment_len;
+    }
+    if (lane == 0) o[w] = 0;
+    uint8_t *so = seq + soff[k], *qo = qual + soff[k];
+    for (uint32_t i = lane; i < R.seq_len; i += 64) {
+        so[i] = t[R.seq + i];
+        qo[i] = uint8_t(t[R.qual + i] - 33);
+    }
+}
+
+// READ2 flags (fqzcomp5.c:518-527): the name (with its comment) ends in
+// "/2", or equals the previous name of the block
+__global__ void k_fq_flags(const fqz5_fastq_rec *recs, uint64_t a, uint64_t n, const uint8_t *names,
+                           const uint32_t *noff, const uint32_t *nb, uint32_t *flags) {
+    const uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint8_t *s = names + noff[k];
+    const uint32_t l = nb[k] - 1;                     // without the '\0'
+    uint32_t f = 0;
+    if (recs[a + k].name_len > 1 && l >= 2 && s[l - 1] == '2' && s[l - 2] == '/') f = 128;
+    if (k > 0 && nb[k - 1] == nb[k]) {
+        const uint8_t *q = names + noff[k - 1];
+        uint32_t i = 0;
+        while (i < l && s[i] == q[i]) i++;
+        if (i == l) f = 128;
+    }
+    flags[k] = f;
+}
+
+// output_fastq (fqzcomp5.c:3441-3480): '@' name '\n' seq '\n' '+' [name] '\n'
+// qual+33 '\n', one wave per record
+__global__ void k_fq_format(const uint8_t *names, const uint64_t *zpos, const uint8_t *seq,
+                            const uint8_t *qual, const uint64_t *soff, const uint32_t *lens,
+                            const uint64_t *ooff, uint64_t n, int plus_name, uint8_t *out) {
+    const uint64_t k = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (k >= n) return;
+    const uint64_t ns = k ? zpos[k - 1] + 1 : 0;
+    const uint32_t nl = uint32_t(zpos[k] - ns), L = lens[k];
+    uint8_t *o = out + ooff[k];
+    if (lane == 0) o[0] = '@';
+    for (uint32_t i = lane; i < nl; i += 64) o[1 + i] = names[ns + i];
+    uint64_t w = 1 + nl;
+    if (lane == 0) o[w] = '\n';
+    w++;
+    const uint8_t *sp = seq + soff[k], *qp = qual + soff[k];
+    for (uint32_t i = lane; i < L; i += 64) o[w + i] = sp[i];
+    w += L;
+    if (lane == 0) {
+        o[w] = '\n';
+        o[w + 1] = '+';
+    }
+    w += 2;
+    if (plus_name) {
+        for (uint32_t i = lane; i < nl; i += 64) o[w + i] = names[ns + i];
+        w += nl;
+    }
+    if (lane == 0) o[w] = '\n';
+    w++;
+    for (uint32_t i = lane; i < L; i += 64) o[w + i] = uint8_t(qp[i] + 33);
+    w += L;
+    if (lane == 0) o[w] = '\n';
+}
+
+dim3 grid_for(uint64_t n, uint32_t per) { return dim3(uint32_t((n + per - 1) / per ? (n + per - 1) / per : 1)); }
+
+// every `ch` position of d_text[0..len) into a device array (arena); returns it
+uint64_t *find_delims(GpuCtx &g, const uint8_t *d_text, uint64_t len, uint8_t ch, uint64_t *count) {
+    const uint64_t tiles = (len + FQ_TILE - 1) / FQ_TILE;
+    if (tiles == 0) { *count = 0; return nullptr; }
+    if (tiles >= (1ull << 31)) throw GpuError("fastq: text too large");
+    uint32_t *cnt = g.arena.alloc_n<uint32_t>(tiles + 1);
+    uint32_t *off = g.arena.alloc_n<uint32_t>(tiles + 1);
+    hipLaunchKernelGGL(k_delim_count, dim3(uint32_t(tiles)), dim3(FQ_TPB), 0, g.stream, d_text, len,
+                       ch, cnt);
+    FQZ5_HIP(hipGetLastError());
+    g.memset0(cnt + tiles, 4);
+    size_t tb = 0;
+    FQZ5_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, int(tiles + 1), g.stream));
+    void *tmp = g.arena.alloc_n<uint8_t>(tb);
+    FQZ5_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, off, int(tiles + 1), g.stream));
+    uint32_t total = 0;
+    g.download(&total, off + tiles, 1);
+    g.sync();
+    *count = total;
+    uint64_t *pos = g.arena.alloc_n<uint64_t>(size_t(total) + 1);
+    hipLaunchKernelGGL(k_delim_write, dim3(uint32_t(tiles)), dim3(FQ_TPB), 0, g.stream, d_text, len,
+                       ch, off, pos);
+    FQZ5_HIP(hipGetLastError());
+    return pos;
+}
+
+template <class T> void excl_sum(GpuCtx &g, const T *in, T *out, uint64_t n) {
+    size_t tb = 0;
+    FQZ5_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, int(n), g.stream));
+    void *tmp = g.arena.alloc_n<uint8_t>(tb ? tb : 1);
+    FQZ5_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, int(n), g.stream));
+}
+
+}  // namespace
+}  // namespace fqz5
+
+using namespace fqz5;
+
+extern "C" {
+
+int fqz5_fastq_index(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs,
+                     uint64_t max_rec, uint64_t *nrec, uint32_t *h_rec_size) {
+    GpuCtx *gp = nullptr;
+    try {
+        GpuCtx &g = gpu();
+        gp = &g;
+        *nrec = 0;
+        uint64_t nn = 0;
+        uint64_t *nl = find_delims(g, d_text, len, '\n', &nn);
+        // a last line without '\n' ends at the text end (kseq reads to EOF)
+        uint8_t last = '\n';
+        if (len) {
+            g.download(&last, d_text + len - 1, 1);
+            g.sync();
+        }
+        uint64_t *lines = nl;
+        uint64_t nlines = nn;
+        if (len && last != '\n') {
+            lines = g.arena.alloc_n<uint64_t>(size_t(nn) + 1);
+            if (nn) FQZ5_HIP(hipMemcpyAsync(lines, nl, nn * 8, hipMemcpyDeviceToDevice, g.stream));
+            const uint64_t e = len;
+            uint64_t *st = reinterpret_cast<uint64_t *>(g.staging.alloc(8));
+            *st = e;
+            FQZ5_HIP(hipMemcpyAsync(lines + nn, st, 8, hipMemcpyHostToDevice, g.stream));
+            nlines = nn + 1;
+        }
+        // trailing empty lines (kseq skips to the next header) are ignored
+        uint64_t n4 = nlines / 4;
+        if (nlines % 4) {
+            std::vector<uint64_t> tail(size_t(nlines % 4) + 1);
+            const uint64_t first = n4 * 4;
+            g.download(tail.data() + 1, lines + first, nlines - first);
+            if (first) g.download(tail.data(), lines + first - 1, 1);
+            g.sync();
+            uint64_t prev = first ? tail[0] : uint64_t(-1);
+            for (uint64_t k = 1; k <= nlines - first; k++) {
+                if (tail[k] != prev + 1) throw GpuError("fastq: not 4-line FASTQ (stray lines at the end)");
+                prev = tail[k];
+            }
+        }
+        if (n4 > max_rec) throw GpuError("fastq: more records than max_rec");
+        int32_t *st = g.arena.alloc_n<int32_t>(1);
+        const int32_t ok = 0;
+        uint32_t *rs = g.arena.alloc_n<uint32_t>(size_t(n4) + 1);
+        FQZ5_HIP(hipMemcpyAsync(st, &ok, 4, hipMemcpyHostToDevice, g.stream));
+        if (n4)
+            hipLaunchKernelGGL(k_fq_records, grid_for(n4, 256), dim3(256), 0, g.stream, d_text, lines, n4,
+                               d_recs, rs, st);
+        FQZ5_HIP(hipGetLastError());
+        int32_t status = 0;
+        g.download(&status, st, 1);
+        if (h_rec_size && n4) g.download(h_rec_size, rs, n4);
+        g.sync();
+        if (status < 0) {
+            char msg[128];
+            std::snprintf(msg, sizeof msg, "fastq: record %lld is not a 4-line FASTQ record",
+                          static_cast<long long>(-1 - int64_t(status)));
+            throw GpuError(msg);
+        }
+        *nrec = n4;
+        g.reset();
+        return 0;
+    } catch (const std::exception &e) {
+        fqz5_set_error(e.what());
+        try { if (gp) gp->reset(); } catch (...) {}
+        return -1;
+    }
+}
+
+int fqz5_fastq_blocks(const uint32_t *rec_size, uint64_t nrec, uint32_t blk_size, uint64_t *first,
+                      int max_blocks) {
+    // load_seqs_kseq (fqzcomp5.c:471-479): a record that would take a
+    // non-empty block past blk_size starts the next one
+    int nb = 0;
+    uint64_t total = 0;
+    for (uint64_t r = 0; r < nrec; r++) {
+        if (r == 0 || (total > 0 && total + rec_size[r] > blk_size)) {
+            if (nb >= max_blocks) return -1;
+            first[nb++] = r;
+            total = 0;
+        }
+        total += rec_size[r];
+    }
+    if (nb > max_blocks) return -1;
+    first[nb] = nrec;
+    return nb;
+}
+
+int fqz5_fastq_gather(const uint8_t *d_text, const fqz5_fastq_rec *d_recs, uint64_t a, uint64_t b,
+                      uint8_t *d_names, uint8_t *d_seq, uint8_t *d_qual, uint32_t *h_len,
+                      uint32_t *h_flag, uint64_t *sizes) {
+    GpuCtx *gp = nullptr;
+    try {
+        GpuCtx &g = gpu();
+        gp = &g;
+        const uint64_t n = b > a ? b - a : 0;
+        if (n >= (1ull << 31)) throw GpuError("fastq: block too large");
+        uint32_t *nb = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
+        uint32_t *sb = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
+        uint32_t *noff = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
+        uint32_t *soff = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
+        if (n) hipLaunchKernelGGL(k_fq_counts, grid_for(n, 256), dim3(256), 0, g.stream, d_recs, a, n, nb, sb);
+        g.memset0(nb + n, 4);
+        g.memset0(sb + n, 4);
+        excl_sum(g, nb, noff, n + 1);
+        excl_sum(g, sb, soff, n + 1);
+        uint32_t tot[2];
+        g.download(&tot[0], noff + n, 1);
+        g.download(&tot[1], soff + n, 1);
+        g.sync();
+        sizes[0] = tot[0];
+        sizes[1] = tot[1];
+        sizes[2] = tot[1];
+        if (d_names && d_seq && d_qual && n) {
+            hipLaunchKernelGGL(k_fq_gather, grid_for(n * 64, 256), dim3(256), 0, g.stream, d_text, d_recs,
+                               a, n, noff, soff, d_names, d_seq, d_qual);
+            FQZ5_HIP(hipGetLastError());
+            if (h_flag) {
+                uint32_t *fl = g.arena.alloc_n<uint32_t>(size_t(n));
+                hipLaunchKernelGGL(k_fq_flags, grid_for(n, 256), dim3(256), 0, g.stream, d_recs, a, n,
+                                   d_names, noff, nb, fl);
+                FQZ5_HIP(hipGetLastError());
+                g.download(h_flag, fl, n);
+            }
+            if (h_len) g.download(h_len, sb, n);
+        }
+        g.reset();
+        return 0;
+    } catch (const std::exception &e) {
+        fqz5_set_error(e.what());
+        try { if (gp) gp->reset(); } catch (...) {}
+        return -1;
+    }
+}
+
+int fqz5_fastq_format(const uint8_t *d_names, uint64_t name_len, const uint8_t *d_seq,
+                      const uint8_t *d_qual, const uint32_t *h_len, uint64_t nrec, int plus_name,
+                      uint8_t *d_out, uint64_t out_cap, uint64_t *out_len) {
+    GpuCtx *gp = nullptr;
+    try {
+        GpuCtx &g = gpu();
+        gp = &g;
+        uint64_t nz = 0;
+        uint64_t *z = find_delims(g, d_names, name_len, 0, &nz);
+        if (nz < nrec) throw GpuError("fastq_format: fewer names than records");
+        std::vector<uint64_t> hz(size_t(nrec) + 1), ooff(size_t(nrec) + 1), soff(size_t(nrec) + 1);
+        if (nrec) g.download(hz.data(), z, nrec);
+        g.sync();
+        uint64_t o = 0, s = 0, prev = uint64_t(-1);
+        for (uint64_t k = 0; k < nrec; k++) {
+            const uint64_t nl = hz[k] - (prev + 1);
+            ooff[k] = o;
+            soff[k] = s;
+            o += 1 + nl + 1 + h_len[k] + 2 + (plus_name ? nl : 0) + 1 + h_len[k] + 1;
+            s += h_len[k];
+            prev = hz[k];
+        }
+        *out_len = o;
+        if (!d_out) { g.reset(); return 0; }
+        if (o > out_cap) throw GpuError("fastq_format: output larger than out_cap");
+        const uint64_t *d_oo = g.upload(ooff.data(), nrec);
+        const uint64_t *d_so = g.upload(soff.data(), nrec);
+        const uint32_t *d_l = g.upload(h_len, nrec);
+        if (nrec)
+            hipLaunchKernelGGL(k_fq_format, grid_for(nrec * 64, 256), dim3(256), 0, g.stream, d_names, z,
+                               d_seq, d_qual, d_so, d_l, d_oo, nrec, plus_name, d_out);
+        FQZ5_HIP(hipGetLastError());
+        g.reset();
+        return 0;
+    } catch (const std::exception &e) {
+        fqz5_set_error(e.what());
+        try { if (gp) gp->reset(); } catch (...) {}
+        return -1;
+    }
+}
+
+}  // extern "C"

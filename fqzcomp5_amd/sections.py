@@ -411,24 +411,49 @@ class Run:
         if self.names:
             self.name_h, self.name_off = synth.all_names(reads)
             self.name_d = torch.from_numpy(self.name_h).to(device)
-        self.spans, self.lens, self.flags, self.fixed, self.lengths = [], [], [], [], []
+        lens, flags, nranges, sranges = [], [], [], []
         for a, b in blocks:
-            s, e = int(offs[a]), int(offs[b])
-            ln = np.ascontiguousarray(reads.lens[a:b], np.uint32)
-            fl = int(ln[0]) if len(ln) and bool(np.all(ln == ln[0])) else 0
-            k = len(self.lens)
-            self.lens.append(ln)
+            lens.append(np.ascontiguousarray(reads.lens[a:b], np.uint32))
+            sranges.append((int(offs[a]), int(offs[b])))
             if self.names:          # load_seqs_kseq derives them from the names
                 ns, ne = int(self.name_off[a]), int(self.name_off[b])
-                self.flags.append(name_flags(self.name_h[ns:ne], b - a))
+                nranges.append((ns, ne))
+                flags.append(name_flags(self.name_h[ns:ne], b - a))
             elif getattr(reads, "flags", None) is not None:
-                self.flags.append(np.ascontiguousarray(reads.flags[a:b], np.uint32))
+                flags.append(np.ascontiguousarray(reads.flags[a:b], np.uint32))
             else:
-                self.flags.append(None)
+                flags.append(None)
+        self._setup(lens, flags, nranges if self.names else None, sranges)
+
+    @classmethod
+    def from_device(cls, name_d, seq_d, qual_d, name_ranges, seq_ranges, lens, flags):
+        """A run over section inputs already in device memory (the FASTQ
+        parser's gathered blocks, fqz5file.py): per block its name and
+        sequence/quality byte ranges, record lengths and READ2 flags."""
+        run = cls.__new__(cls)
+        run.reads = None
+        run.blocks = [(0, len(ln)) for ln in lens]
+        run.names = True
+        run.name_d, run.seq_d, run.qual_d = name_d, seq_d, qual_d
+        run.name_h = run.name_off = None
+        run._setup([np.ascontiguousarray(ln, np.uint32) for ln in lens],
+                   [np.ascontiguousarray(f, np.uint32) for f in flags], name_ranges, seq_ranges)
+        return run
+
+    def _setup(self, lens, flags, name_ranges, seq_ranges):
+        """Sections (name, seq, qual per block), their encode / decode buffers."""
+        import torch
+        device = self.seq_d.device
+        self.spans, self.lens, self.flags, self.fixed, self.lengths = [], [], [], [], []
+        for k, (ln, fg, (s, e)) in enumerate(zip(lens, flags, seq_ranges)):
+            fl = int(ln[0]) if len(ln) and bool(np.all(ln == ln[0])) else 0
+            self.lens.append(ln)
+            self.flags.append(fg)
             self.fixed.append(fl)
-            if self.names:
+            if name_ranges is not None:
                 self.lengths.append(block_lengths(ln, fl if len(ln) else -1))
-                self.spans.append((SEC_NAME, int(self.name_off[a]), int(self.name_off[b]), 0, k))
+                ns, ne = name_ranges[k]
+                self.spans.append((SEC_NAME, ns, ne, 0, k))
             self.spans.append((SEC_SEQ, s, e, fl, k))
             self.spans.append((SEC_QUAL, s, e, fl, k))
         caps = []

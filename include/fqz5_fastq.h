@@ -1,0 +1,71 @@
+/*
+ * fqz5_fastq.h — FASTQ text in device memory to fqzcomp5 blocks and back
+ * (SURVEY §8 f3), on the GPU:
+ *
+ *   fqz5_fastq_index    load_seqs_kseq's record parse (fqzcomp5.c:423-623,
+ *                       kseq.h:178-218) for 4-line FASTQ: name up to the
+ *                       first isspace(), comment to the line end, one
+ *                       sequence line, '+' line, one quality line, a
+ *                       trailing '\r' dropped as kseq drops it.  Text that
+ *                       is not 4-line FASTQ fails (multi-line records,
+ *                       FASTA); it is never parsed on the host.
+ *   fqz5_fastq_blocks   the block split rule (fqzcomp5.c:471-479): a record
+ *                       that would take a non-empty block past blk_size
+ *                       (name.l + 1 + seq.l + qual.l per record) starts the
+ *                       next block.
+ *   fqz5_fastq_gather   one block's section inputs: names (name [' '
+ *                       comment] '\0'), bases, qualities - 33 (device), the
+ *                       record lengths and READ2 flags (host).
+ *   fqz5_fastq_format   output_fastq (fqzcomp5.c:3441-3480) of a decoded
+ *                       block: '@' name '\n' seq '\n' '+' [name] '\n'
+ *                       qual + 33 '\n'.
+ *
+ * Offsets are bytes into the text.  Calls return 0 (fqz5_fastq_blocks: the
+ * block count) or -1 with fqz5_last_error() set.
+ */
+#ifndef FQZ5_FASTQ_H
+#define FQZ5_FASTQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {                  /* one record of the text */
+    uint64_t name, comment, seq, qual;        /* offsets */
+    uint32_t name_len, comment_len, seq_len;  /* kseq's name.l, comment.l, seq.l */
+    uint32_t pad;
+} fqz5_fastq_rec;
+
+/* Index the records of d_text[0..len) (device) into d_recs (device, max_rec
+ * entries; len / 6 + 1 always suffice); *nrec receives their number and
+ * h_rec_size (host, max_rec entries, may be NULL) each record's
+ * load_seqs_kseq size. */
+int fqz5_fastq_index(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs,
+                     uint64_t max_rec, uint64_t *nrec, uint32_t *h_rec_size);
+
+/* Block starts (host): first[k] = the first record of block k, first[n] =
+ * nrec.  Returns n, or -1 when more than max_blocks. */
+int fqz5_fastq_blocks(const uint32_t *rec_size, uint64_t nrec, uint32_t blk_size,
+                      uint64_t *first, int max_blocks);
+
+/* Records [a, b) as one block.  sizes[3] receives the bytes of the names,
+ * bases and qualities; with d_names / d_seq / d_qual NULL only the sizes
+ * are computed.  h_len / h_flag (host, b - a entries, may be NULL): record
+ * lengths and FQZ5 READ2 flags (fqzcomp5.c:518-527). */
+int fqz5_fastq_gather(const uint8_t *d_text, const fqz5_fastq_rec *d_recs, uint64_t a,
+                      uint64_t b, uint8_t *d_names, uint8_t *d_seq, uint8_t *d_qual,
+                      uint32_t *h_len, uint32_t *h_flag, uint64_t *sizes);
+
+/* FASTQ text of a block (names '\0' after each, bases, qualities - 33 on
+ * the device; lengths on the host) into d_out (out_cap bytes); *out_len its
+ * size.  d_out NULL: the size only. */
+int fqz5_fastq_format(const uint8_t *d_names, uint64_t name_len, const uint8_t *d_seq,
+                      const uint8_t *d_qual, const uint32_t *h_len, uint64_t nrec,
+                      int plus_name, uint8_t *d_out, uint64_t out_cap, uint64_t *out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,95 @@
+"""FASTQ file -> .fqz5 file -> FASTQ on the GPU alone (fqzcomp5_amd/fqz5file.py:
+fastq.hip's record parse, block split and gather, the section coder, block
+assembly, the container): the file equals the reference CLI's single-threaded
+output byte for byte (fqzcomp5.c load_seqs_kseq / encode_block / write_index),
+and decoding either file gives the input back.  BASELINE configs[0]
+(sample.fastq at -1) is pinned by its published md5."""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from fqzcomp5_amd import fqz5file, lib, synth
+from oracle import binding
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+CLI = os.path.join(os.path.dirname(binding.REF_BIN), "fqzcomp5")
+GOLD = [os.path.join(HERE, "golden", "fastq", f) for f in
+        ("sample.fastq", "regression_srr1238539.fastq", "paired_R1_nosuffix.fastq")]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need():
+    if not lib.device_ok():
+        pytest.fail("no GPU: " + lib.last_error())
+
+
+def _ref(tmp, src, level, blk=None):
+    out = os.path.join(tmp, "ref.fqz5")
+    cmd = [CLI, f"-{level}", "-t1"] + (["-b", blk] if blk else []) + [src, out]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+    return open(out, "rb").read()
+
+
+def test_sample_fastq_config1():
+    """BASELINE configs[0]: sample.fastq at -1 is 245 bytes, md5 8b5e07bf..."""
+    z = fqz5file.compress_bytes(open(GOLD[0], "rb").read(), 1)
+    assert len(z) == 245 and hashlib.md5(z).hexdigest() == "8b5e07bf4c452ad206679f5e4bd7837a"
+    assert fqz5file.decompress_bytes(z) == open(GOLD[0], "rb").read()
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="oracle/_ref not built")
+@pytest.mark.parametrize("level", [1, 3, 5, 7, 9])
+def test_golden_files_vs_cli(tmp_path, level):
+    for src in GOLD:
+        text = open(src, "rb").read()
+        want = _ref(str(tmp_path), src, level)
+        got = fqz5file.compress_bytes(text, level)
+        assert got == want, (src, level, len(got), len(want))
+        assert fqz5file.decompress_bytes(want) == text
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="oracle/_ref not built")
+@pytest.mark.parametrize("level,kind", [(3, "illumina"), (5, "novaseq"), (7, "ont"), (9, "hifi")])
+def test_multiblock_vs_cli(tmp_path, level, kind):
+    gen = {"illumina": lambda: synth.illumina(40000, seed=31, with_names=True),
+           "novaseq": lambda: synth.novaseq(40000, seed=31, with_names=True),
+           "ont": lambda: synth.ont(300, seed=31, with_names=True),
+           "hifi": lambda: synth.hifi(150, seed=31, with_names=True)}[kind]
+    src = str(tmp_path / "in.fastq")
+    synth.write_fastq(gen(), src)
+    text = open(src, "rb").read()
+    want = _ref(str(tmp_path), src, level, "1M")
+    got = fqz5file.compress_bytes(text, level, blk_size=1_000_000)
+    assert got == want, (len(got), len(want))
+    assert fqz5file.decompress_bytes(got) == text
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="oracle/_ref not built")
+def test_crlf_and_no_final_newline(tmp_path):
+    """kseq drops a trailing '\\r' of a line longer than one byte and reads a
+    last line without '\\n' (kseq.h:141, :106)."""
+    r = synth.illumina(3000, seed=7, with_names=True)
+    text = synth.fastq_chunk(r, 0, r.num_records).tobytes()
+    crlf = text.replace(b"\n", b"\r\n")
+    for t in (crlf, text[:-1]):
+        src = str(tmp_path / "x.fastq")
+        open(src, "wb").write(t)
+        want = _ref(str(tmp_path), src, 3)
+        assert fqz5file.compress_bytes(t, 3) == want
+
+
+def test_not_4line_fastq_fails_loudly():
+    bad = b"@r1\nACGT\nACGT\n+\nIIIIIIII\n"            # a two-line sequence
+    with pytest.raises(lib.NativeError):
+        fqz5file.compress_bytes(bad, 3)
+    with pytest.raises(lib.NativeError):
+        fqz5file.compress_bytes(b">r1\nACGT\n", 3)   # FASTA
+
+
+def test_empty_input():
+    z = fqz5file.compress_bytes(b"", 3)
+    assert z[:8] == fqz5file.MAGIC and fqz5file.decompress_bytes(z) == b""

@@ -1,0 +1,6 @@
+#!/bin/bash
+set -uo pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r02n
+timeout -k 10 500 python -u tools/names_timing.py 5 4.0 > gpurun_out/r02n/t5.log 2>&1 || { tail -40 gpurun_out/r02n/t5.log; exit 1; }
+grep -E "names|encode_run|sections_try: [0-9]|rANS candidates|decode_sections|roundtrip|commit|helper" gpurun_out/r02n/t5.log | tail -30
