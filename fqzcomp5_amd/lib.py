@@ -8,7 +8,6 @@ from __future__ import annotations
 
 import ctypes as C
 import os
-import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfqz5_mi355x.so")
@@ -51,12 +50,16 @@ def load() -> C.CDLL:
     if _lib is not None:
         return _lib
     path = os.environ.get("FQZ5_LIB_VARIANT") or LIB_PATH   # tools/build_variant.sh
-    # torch bundles its own HIP runtime: when the caller uses torch, its
-    # runtime must own the device before this library's runtime starts
-    if "torch" in sys.modules:
+    # torch bundles its own HIP runtime, and the package's device buffers
+    # (sections.py, fqz5file.py) are torch tensors: its runtime must own the
+    # device before this library's runtime starts (started the other way
+    # round, torch later finds no GPU)
+    try:
         import torch
-        if torch.cuda.is_available():
-            torch.cuda.init()
+    except ImportError:
+        torch = None
+    if torch is not None and torch.cuda.is_available():
+        torch.cuda.init()
     if not os.path.exists(path):
         raise NativeError(f"{path} missing: run __graft_entry__.build()")
     lib = C.CDLL(path)
