@@ -18,9 +18,8 @@
 #include <cstring>
 #include <exception>
 #include <thread>
-#include <condition_variable>
 #include <deque>
-#include <mutex>
+#include <memory>
 #include <vector>
 
 #include "../../include/fqz5_block.h"
@@ -160,7 +159,9 @@ void encode_name_jobs(GpuCtx &g, const fqz5_section *secs, const std::vector<int
                       const std::vector<int> &meth, std::vector<NameEnc> &out) {
     out.assign(which.size(), NameEnc());
     if (which.empty()) return;
-    std::vector<std::vector<uint8_t>> host;
+    // into the pinned staging arena (kept until the context's reset): a
+    // pageable copy of a -5 run's 38 name blocks (570 MB) took ~0.5 s
+    std::vector<const uint8_t *> host;
     std::vector<int> host_of(which.size());
     std::vector<int> seen;
     for (size_t k = 0; k < which.size(); k++) {
@@ -169,14 +170,15 @@ void encode_name_jobs(GpuCtx &g, const fqz5_section *secs, const std::vector<int
         host_of[k] = int(seen.size());
         seen.push_back(which[k]);
         const fqz5_section &S = secs[which[k]];
-        host.emplace_back(S.in_size);
-        g.download(host.back().data(), S.in, S.in_size);
+        uint8_t *hb = g.staging.alloc(S.in_size + 1);
+        g.download(hb, S.in, S.in_size);
+        host.push_back(hb);
     }
     g.sync();
     std::vector<const uint8_t *> h(which.size()), d(which.size());
     std::vector<uint32_t> lens(which.size());
     for (size_t k = 0; k < which.size(); k++) {
-        h[k] = host[size_t(host_of[k])].data();
+        h[k] = host[size_t(host_of[k])];
         d[k] = secs[which[k]].in;
         lens[k] = secs[which[k]].in_size;
     }
@@ -854,41 +856,31 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         const auto t1 = std::chrono::steady_clock::now();
         // the name sections on their helper context, beside the chains: their
         // host rebuild overlaps the GPU's rANS / fqz / sequence decoding
-        // The long chains of the main batch take every CU they can (hedged
-        // copies), so the names' short GPU stages go first (~45 ms) and the
-        // chains start once they are done, while the names' host rebuild runs
-        // beside the chains.
+        // The name sections decode on their helper context beside the chains.
+        // Each hedged chain copy holds a CU (its LDS), so while the names run
+        // they count as a second hedging caller: the chains' copies take half
+        // the CUs and the names' short kernels find the rest free (their
+        // host rebuild needs no CU at all).
         std::exception_ptr nerr;
         std::thread tn;
         GpuCtx *gn = nullptr;
-        std::mutex nmu;
-        std::condition_variable ncv;
-        bool ngpu_done = nd.empty();
+        std::unique_ptr<HedgeShare> nshare;
         if (!nd.empty()) {
             gn = &gpu_aux(AUX_NAMES);
+            nshare = std::make_unique<HedgeShare>(size_t(g.cus));
             tn = std::thread([&] {
-                auto release = [&] {
-                    std::lock_guard<std::mutex> lk(nmu);
-                    ngpu_done = true;
-                    ncv.notify_all();
-                };
                 try {
                     FQZ5_HIP(hipSetDevice(gn->device));
-                    names_decode_batch(*gn, nd, release);
+                    names_decode_batch(*gn, nd);
                 } catch (...) {
                     nerr = std::current_exception();
                 }
-                release();
             });
         }
         struct Join {                                 // joined on every exit
             std::thread &t;
             ~Join() { if (t.joinable()) t.join(); }
         } join_names{tn};
-        {
-            std::unique_lock<std::mutex> lk(nmu);
-            ncv.wait(lk, [&] { return ngpu_done; });
-        }
         decompress_batch(g, reqs);
         if (trace)
             std::fprintf(stderr, "decode_sections: %zu bytes to host in %.1f ms, rANS %.1f ms\n", tot,
@@ -916,6 +908,7 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         // be the output of this call's sequence section
         if (!fqz.empty()) fqz_decode_batch(g, fqz);
         if (tn.joinable()) tn.join();
+        nshare.reset();
         if (nerr) std::rethrow_exception(nerr);
         for (size_t k = 0; k < nd.size(); k++) {
             fqz5_section_result &R = res[who_name[k]];
