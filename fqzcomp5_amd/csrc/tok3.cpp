@@ -55,85 +55,145 @@ struct Last {
 };
 
 // ---------------------------------------------------------------------------
+// The name formats search_trie special-cases (:600-644): the prefix length
+// whose trie node picks the name to compare against, and a fixed-length
+// leading token.
+int name_format(const char *data, size_t len, int *is_fixed, int *fixed_len) {
+    *fixed_len = 0;
+    *is_fixed = 0;
+    const char *d = *data == '@' ? data + 1 : data;
+    const int l = *data == '@' ? int(len) - 1 : int(len);
+    const int f = (*data == '>') ? 1 : 0;
+    auto xd = [](char c) { return c_xdigit(uint8_t(c)); };
+    if (l > 70 && d[f + 0] == 'm' && d[7] == '_' && d[f + 14] == '_' && d[f + 61] == '/')
+        return 60;                                     // PacBio
+    if (l == 17 && d[f + 5] == ':' && d[f + 11] == ':') {
+        *fixed_len = 6;                                // IonTorrent
+        *is_fixed = 1;
+        return 6;
+    }
+    if (l >= 36 && d[f + 8] == '-' && d[f + 13] == '-' && d[f + 18] == '-' && d[f + 23] == '-' &&
+        xd(d[f + 0]) && xd(d[f + 7]) && xd(d[f + 9]) && xd(d[f + 12]) && xd(d[f + 14]) &&
+        xd(d[f + 17]) && xd(d[f + 19]) && xd(d[f + 22]) && xd(d[f + 24]) && xd(d[f + 35])) {
+        *fixed_len = 36;                               // ONT uuid
+        *is_fixed = 1;
+        return 36;
+    }
+    int colons = 0;                                    // Illumina: lane:tile:x:y
+    size_t i = 0;
+    for (i = 0; i < len && data[i] > ' '; i++) {}
+    while (i > 0 && colons < 4)
+        if (data[--i] == ':') colons++;
+    if (colons == 4) {
+        *fixed_len = int(i) + 1;
+        *is_fixed = 1;
+        return int(i) + 1;
+    }
+    return INT_MAX;
+}
+
 // Trie over all names of the block (build_trie / search_trie, :477-695): a
 // node keeps the index of the last name that walked through it (24 bits, as
-// the reference's bitfield), initially the one that created it.
+// the reference's bitfield), initially the one that created it.  Fused with
+// build_trie: the reference builds the trie of every name first (a node
+// holding its first name) and then searches name by name (each visit
+// leaving the visitor's number), so at name n's visit a node holds the last
+// earlier name through it, or n itself when n is the first.  A node created
+// on first sight holds n: the same values in one pass.
+//
+// Stored as a radix trie: an edge carries a run of characters (a slice of
+// the name that made it) whose one-character nodes would all hold the same
+// name, since every visit walks a whole prefix.  A visit that ends or turns
+// off inside an edge splits it: the walked part takes the visitor, the rest
+// keeps its name.  A name thus costs a character compare per byte and a few
+// node operations instead of a node (and a sibling scan) per byte.
 struct Trie {
-    struct Node { int next = -1, sib = -1; uint8_t c = 0; uint32_t n = 0; };
+    struct Node {
+        const char *s = nullptr;                       // the edge's characters
+        uint32_t len = 0, n = 0;
+        int child = -1, sib = -1;
+        char fc = 0;                                   // s[0]
+    };
     std::vector<Node> nodes{Node()};                   // node 0: the root
 
-    // -> the name to tokenise against, or -1 (:591-695).  Fused with
-    // build_trie: the reference builds the trie of every name first (a node
-    // holding its first name) and then searches name by name (each visit
-    // leaving the visitor's number), so at name n's visit a node holds the
-    // last earlier name through it, or n itself when n is the first.  A node
-    // created here on first sight holds n: the same values in one pass.
+    // -> the name to tokenise against, or -1 (:591-695)
     int search(const char *data, size_t len, uint32_t n, int *exact, int *is_fixed,
                int *fixed_len) {
-        int from = -1, p3 = -1;
         *exact = 0;
-        *fixed_len = 0;
-        *is_fixed = 0;
-        int prefix_len;
-        const char *d = *data == '@' ? data + 1 : data;
-        const int l = *data == '@' ? int(len) - 1 : int(len);
-        const int f = (*data == '>') ? 1 : 0;
-        auto xd = [](char c) { return c_xdigit(uint8_t(c)); };
-        if (l > 70 && d[f + 0] == 'm' && d[7] == '_' && d[f + 14] == '_' && d[f + 61] == '/') {
-            prefix_len = 60;                           // PacBio
-            *is_fixed = 0;
-        } else if (l == 17 && d[f + 5] == ':' && d[f + 11] == ':') {
-            prefix_len = 6;                            // IonTorrent
-            *fixed_len = 6;
-            *is_fixed = 1;
-        } else if (l >= 36 && d[f + 8] == '-' && d[f + 13] == '-' && d[f + 18] == '-' &&
-                   d[f + 23] == '-' && xd(d[f + 0]) && xd(d[f + 7]) && xd(d[f + 9]) &&
-                   xd(d[f + 12]) && xd(d[f + 14]) && xd(d[f + 17]) && xd(d[f + 19]) &&
-                   xd(d[f + 22]) && xd(d[f + 24]) && xd(d[f + 35])) {
-            prefix_len = 36;                           // ONT uuid
-            *fixed_len = 36;
-            *is_fixed = 1;
-        } else {                                       // Illumina: lane:tile:x:y
-            int colons = 0;
-            size_t i = 0;
-            for (i = 0; i < len && data[i] > ' '; i++) {}
-            while (i > 0 && colons < 4)
-                if (data[--i] == ':') colons++;
-            if (colons == 4) {
-                *fixed_len = int(i) + 1;
-                prefix_len = int(i) + 1;
-                *is_fixed = 1;
-            } else {
-                prefix_len = INT_MAX;
-                *is_fixed = 0;
-            }
+        const int prefix_len = name_format(data, len, is_fixed, fixed_len);
+        const uint32_t nn = n & 0xffffffu;
+        // the walk reads to the first byte <= '\n'; a byte >= 0x80 ends it
+        // with -1 after the bytes before it were walked (:654-674)
+        size_t L = 0;
+        bool high = false;
+        while (L < len && uint8_t(data[L]) > '\n') {
+            if (uint8_t(data[L]) & 0x80) { high = true; break; }
+            L++;
         }
-        int from_punct = from;
+        int from = -1, from_punct = -1, p3 = -1;
+        auto visit = [&](size_t p, uint32_t val) {     // byte p's node held val
+            from = int(val);
+            const uint8_t c = uint8_t(data[p]);
+            if ((c_punct(c) || c_space(c)) && val != nn) from_punct = int(val);
+            if (int(p + 1) == prefix_len) p3 = int(val);
+        };
+        auto leaf = [&](int parent, size_t i) {       // the rest of the name, new
+            Node w;
+            w.s = data + i;
+            w.len = uint32_t(L - i);
+            w.n = nn;
+            w.fc = data[i];
+            w.sib = nodes[size_t(parent)].child;
+            nodes.push_back(w);
+            nodes[size_t(parent)].child = int(nodes.size()) - 1;
+            for (size_t p = i; p < L; p++) visit(p, nn);
+        };
         int t = 0;
-        for (size_t i = 0; i < len && uint8_t(data[i]) > '\n';) {
-            const uint8_t c0 = uint8_t(data[i++]);
-            if (c0 & 0x80) return -1;
-            const uint8_t c = c0 & 127;
-            int x = nodes[size_t(t)].next, l = -1;
-            while (x >= 0 && nodes[size_t(x)].c != c) { l = x; x = nodes[size_t(x)].sib; }
-            if (x < 0) {                               // build_trie's node, made by n
-                Node nn;
-                nn.c = c;
-                nn.n = n & 0xffffffu;
-                nodes.push_back(nn);
-                x = int(nodes.size()) - 1;
-                if (l < 0) nodes[size_t(t)].next = x;
-                else nodes[size_t(l)].sib = x;
+        size_t i = 0;
+        while (i < L) {
+            const char c = data[i];
+            int x = nodes[size_t(t)].child, l = -1;
+            while (x >= 0 && nodes[size_t(x)].fc != c) { l = x; x = nodes[size_t(x)].sib; }
+            if (x < 0) {
+                leaf(t, i);
+                break;
             }
-            t = x;
-            Node &T = nodes[size_t(t)];
-            from = int(T.n);
-            if ((c_punct(c) || c_space(c)) && T.n != (n & 0xffffffu))
-                from_punct = int(T.n);
-            if (int(i) == prefix_len) p3 = int(T.n);
-            T.n = n & 0xffffffu;
+            if (l >= 0) {                              // to the front (order is immaterial)
+                nodes[size_t(l)].sib = nodes[size_t(x)].sib;
+                nodes[size_t(x)].sib = nodes[size_t(t)].child;
+                nodes[size_t(t)].child = x;
+            }
+            const Node e = nodes[size_t(x)];
+            const size_t m = std::min<size_t>(e.len, L - i);
+            size_t k = 1;
+            while (k < m && e.s[k] == data[i + k]) k++;
+            for (size_t p = i; p < i + k; p++) visit(p, e.n);
+            if (k == e.len) {                          // the whole edge
+                nodes[size_t(x)].n = nn;
+                t = x;
+                i += k;
+                continue;
+            }
+            Node mid;                                  // split: [0, k) walked, [k, len) kept
+            mid.s = e.s;
+            mid.len = uint32_t(k);
+            mid.n = nn;
+            mid.fc = e.fc;
+            mid.child = x;
+            mid.sib = e.sib;
+            nodes[size_t(x)].s = e.s + k;
+            nodes[size_t(x)].len = e.len - uint32_t(k);
+            nodes[size_t(x)].fc = e.s[k];
+            nodes[size_t(x)].sib = -1;
+            nodes.push_back(mid);
+            const int y = int(nodes.size()) - 1;
+            nodes[size_t(t)].child = y;                // x was at the front
+            i += k;
+            if (i < L) leaf(y, i);
+            break;
         }
-        *exact = (int(n & 0xffffffu) != from) && len;
+        if (high) return -1;
+        *exact = (int(nn) != from) && len;
         return *exact ? from : (p3 != -1 ? p3 : from_punct);
     }
 };
@@ -879,6 +939,18 @@ bool tok3_dec_rebuild(Tok3Dec &D, std::vector<uint8_t> &out) {
 using namespace fqz5;
 
 extern "C" {
+
+// Host stage only (no GPU call): tokenise a copy of `blk` and return the
+// bytes of its token streams, -1 where tok3_encode_names returns NULL.  For
+// timing the tokeniser (tools/tok3_time.py).
+long long fqz5_tok3_tokenise_bytes(const char *blk, int len, int level) {
+    std::vector<char> b(blk, blk + std::max(len, 0));
+    Tok3Enc T;
+    if (!tok3_tokenise(b.data(), len, level, 0, T)) return -1;
+    long long tot = 0;
+    for (auto &d : T.desc) tot += (long long)d.size();
+    return tot;
+}
 
 uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *out_len,
                            int *last_start_p) {
