@@ -102,7 +102,9 @@ def pmc_traffic(kernel: str, tag: str = ""):
     ks = json.load(open(files[-1]))["kernels"]
     for k, v in ks.items():
         if f"::{kernel}(" in k:
-            return int(v["hbm_bytes_per_dispatch"]), os.path.relpath(files[-1], ROOT)
+            # the step's main launch of the kernel (the largest dispatch)
+            b = v.get("hbm_bytes_max_dispatch", v["hbm_bytes_per_dispatch"])
+            return int(b), os.path.relpath(files[-1], ROOT)
     return None, None
 
 
