@@ -61,8 +61,8 @@ sys.path.insert(0, ROOT)
 # queues per process those streams share queues and serialise (measured:
 # the -3 encode waited 100 ms per step behind the LZP3 helper's chain).
 # Must be set before anything initialises HIP.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 24:
-    os.environ["GPU_MAX_HW_QUEUES"] = "24"
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 32:
+    os.environ["GPU_MAX_HW_QUEUES"] = "32"
 
 FASTQ_REC = 358          # bytes of FASTQ text per synthetic 150 bp record (avg)
 BLK = 100_000_000        # -3 / -5 block size (fqzcomp5.c:4896,4904)
@@ -336,7 +336,9 @@ def dropin_item(fastq: str, level: int, threads: int, timeout: int = 600):
     fqzcomp5_gpu, the drop-in of INTEGRATION.md) on the workload's FASTQ
     file with -t<threads>: wall time of encode and decode, its .fqz5 bytes
     compared with the CLI as shipped.  Host buffers: every codec call copies
-    its block to the GPU and back (PCIe included)."""
+    its block to the GPU and back (PCIe included).  Then the library's own
+    file path (fqz5file.compress_file / decompress_file) on the same file:
+    file to file, disk cache and PCIe included."""
     import hashlib
     import tempfile
     cpu = os.path.join(ROOT, "oracle", "_ref", "fqzcomp5")
@@ -367,6 +369,24 @@ def dropin_item(fastq: str, level: int, threads: int, timeout: int = 600):
                             "roundtrip": same}
                 os.unlink(back)
             res["bytes_match"] = md5["cpu"] == md5["gpu"]
+            # this library's own file path on the same file (fqz5file:
+            # page-locked read, one copy to HBM, whole blocks, one copy back)
+            from fqzcomp5_amd import fqz5file
+            out = os.path.join(td, "native.fqz5")
+            back = os.path.join(td, "native.fastq")
+            t0 = time.perf_counter()
+            fqz5file.compress_file(fastq, out, level)
+            t1 = time.perf_counter()
+            fqz5file.decompress_file(out, back)
+            t2 = time.perf_counter()
+            with open(back, "rb") as fb, open(fastq, "rb") as fs:
+                same = fb.read() == fs.read()
+            res["gpu_file_path"] = {
+                "enc_MBps": round(nbytes / (t1 - t0) / 1e6, 2),
+                "dec_MBps": round(nbytes / (t2 - t1) / 1e6, 2),
+                "enc_s": round(t1 - t0, 3), "dec_s": round(t2 - t1, 3), "roundtrip": same,
+                "bytes_match_cli": hashlib.md5(open(out, "rb").read()).hexdigest() == md5["cpu"]}
+            os.unlink(back)
             return res
     except Exception as e:
         return {"error": str(e)[-300:]}

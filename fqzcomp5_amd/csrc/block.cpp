@@ -161,9 +161,16 @@ void encode_name_jobs(GpuCtx &g, const fqz5_section *secs, const std::vector<int
     if (which.empty()) return;
     // into the pinned staging arena (kept until the context's reset): a
     // pageable copy of a -5 run's 38 name blocks (570 MB) took ~0.5 s
+    // Each block's tokenising starts when its own download is done (an
+    // event per block), not after all of them.
     std::vector<const uint8_t *> host;
+    std::vector<hipEvent_t> evs;
     std::vector<int> host_of(which.size());
     std::vector<int> seen;
+    struct Events {
+        std::vector<hipEvent_t> &e;
+        ~Events() { for (auto x : e) (void)hipEventDestroy(x); }
+    } keep_{evs};
     for (size_t k = 0; k < which.size(); k++) {
         auto it = std::find(seen.begin(), seen.end(), which[k]);
         if (it != seen.end()) { host_of[k] = int(it - seen.begin()); continue; }
@@ -172,17 +179,23 @@ void encode_name_jobs(GpuCtx &g, const fqz5_section *secs, const std::vector<int
         const fqz5_section &S = secs[which[k]];
         uint8_t *hb = g.staging.alloc(S.in_size + 1);
         g.download(hb, S.in, S.in_size);
+        hipEvent_t e;
+        FQZ5_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        evs.push_back(e);
+        FQZ5_HIP(hipEventRecord(e, g.stream));
         host.push_back(hb);
     }
-    g.sync();
     std::vector<const uint8_t *> h(which.size()), d(which.size());
     std::vector<uint32_t> lens(which.size());
+    std::vector<hipEvent_t> ready(which.size());
     for (size_t k = 0; k < which.size(); k++) {
         h[k] = host[size_t(host_of[k])];
+        ready[k] = evs[size_t(host_of[k])];
         d[k] = secs[which[k]].in;
         lens[k] = secs[which[k]].in_size;
     }
-    names_encode_batch(g, out, h, d, lens, meth);
+    names_encode_batch(g, out, h, d, lens, meth, &ready);
+    g.sync();
 }
 
 // Trial pruning (fqz5_set_trial_prune): an fqz or sequence-model candidate
@@ -461,16 +474,58 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 std::vector<SeqEncReq> &grp = sqg[k];
                 th.push_back(on(gk, err[2 + k], [&gk, &grp] { seq_encode_prepare(gk, grp); }));
             }
-            double tc = 0;
+            // The plain O0/O1 candidates (RANS0/RANS1: the longest chains,
+            // one step per 4 input bytes) need no PACK / RLE pass: they run
+            // as a batch of their own on a helper context, so that their
+            // chains start while this thread packs and run-length codes the
+            // others' inputs (the packed chains are half as long or less).
+            std::vector<size_t> plain_at;
+            std::vector<char> is_plain(reqs.size(), 0);
+            std::vector<CompressReq> plain, rest;
+            for (size_t k = 0; k < reqs.size(); k++)
+                if ((reqs[k].order & ~1) == 0 && reqs[k].n >= (1u << 20)) plain_at.push_back(k);
+            if (plain_at.size() == reqs.size()) plain_at.clear();
+            for (size_t k : plain_at) is_plain[k] = 1;
+            if (!plain_at.empty())
+                for (size_t k = 0; k < reqs.size(); k++)
+                    (is_plain[k] ? plain : rest).push_back(std::move(reqs[k]));
+            GpuCtx &gp = gpu_aux(AUX_PLAIN);
+            gp.prof.on = g.prof.on;
+            std::exception_ptr perr;
+            std::thread tp = on(gp, perr, [&] { if (!plain.empty()) compress_batch(gp, plain); });
+            double tc = 0, tpl = 0;
             try {
-                compress_batch(g, reqs);
+                compress_batch(g, plain_at.empty() ? reqs : rest);
+                if (!plain_at.empty()) {             // back in request order
+                    size_t q = 0;
+                    for (size_t k = 0; k < reqs.size(); k++)
+                        if (!is_plain[k]) reqs[k] = std::move(rest[q++]);
+                }
                 tc = step_trace() ? now_ms() : 0;
+                tp.join();
+                tpl = step_trace() ? now_ms() : 0;
             } catch (...) {
+                if (tp.joinable()) tp.join();
                 for (auto &t : th) t.join();
                 ts.join();
                 tn.join();
                 throw;
             }
+            if (perr) {
+                for (auto &t : th) t.join();
+                ts.join();
+                tn.join();
+                std::rethrow_exception(perr);
+            }
+            for (size_t q = 0; q < plain_at.size(); q++) reqs[plain_at[q]] = std::move(plain[q]);
+            g.prof.enc_ms += gp.prof.enc_ms;
+            g.prof.enc_launches += gp.prof.enc_launches;
+            g.prof.enc_bytes += gp.prof.enc_bytes;
+            gp.prof = KernelProfile();
+            if (step_trace() && !plain_at.empty())
+                std::fprintf(stderr, "sections_try: %zu plain rANS candidates on a helper, "
+                             "done %.1f ms after the others\n", plain_at.size(), tpl - tc);
+            tc = std::max(tc, tpl);
             for (auto &t : th) t.join();
             ts.join();
             tn.join();
@@ -711,14 +766,22 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         }
         const double t1 = step_trace() ? now_ms() : 0;
         write_layouts_dev(g, ls, dsts);
+        const double t2 = step_trace() ? now_ms() : 0;
         g.reset();
+        const double t3 = step_trace() ? now_ms() : 0;
         // the fqz candidates of the try live in the aux arena: rewind it too,
         // or every step's trial buffers take fresh chunks (the r01 bench OOM)
         if (t_sess.aux) gpu_aux_reset_all();
+        // the session's host buffers (candidate tables, layouts, the name
+        // candidates' token streams: ~100 MB, mostly munmap) are freed by a
+        // detached thread, off the caller's path; nothing refers to them now
+        std::thread([old = std::make_unique<TrySession>(std::move(t_sess))]() mutable {
+            old.reset();
+        }).detach();
         t_sess = TrySession();
         if (step_trace())
-            std::fprintf(stderr, "sections_commit: late encodes %.1f ms, write + sync %.1f ms\n",
-                         t1 - t0, now_ms() - t1);
+            std::fprintf(stderr, "sections_commit: late encodes %.1f ms, write %.1f ms, sync "
+                         "%.1f ms, release %.1f ms\n", t1 - t0, t2 - t1, t3 - t2, now_ms() - t3);
         return 0;
     } catch (const std::exception &e) {
         fqz5_set_error(e.what());

@@ -25,7 +25,7 @@ namespace fqz5 {
 // (e.g. the relinked CLI) loads this library before anything touched HIP.
 __attribute__((constructor)) static void hw_queues_default() {
     const char *v = std::getenv("GPU_MAX_HW_QUEUES");
-    if (!v || std::atoi(v) < 24) setenv("GPU_MAX_HW_QUEUES", "24", 1);
+    if (!v || std::atoi(v) < 32) setenv("GPU_MAX_HW_QUEUES", "32", 1);
 }
 
 static thread_local std::string g_err;

@@ -5,12 +5,14 @@
 // stream and arena keeps concurrent calls independent.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace fqz5 {
@@ -273,6 +275,53 @@ inline std::vector<int> hedge_plan(const std::vector<uint64_t> &steps, size_t cu
     return c;
 }
 
+// XCD-grouped layout of a hedged launch: workgroup b runs on XCD b % 8
+// (observed dispatch order, MI355X_MICROARCH.md "Workgroup dispatch"), so a
+// job placed at positions of one residue has all its copies on one XCD and
+// the copies' reads of the same stream share that XCD's L2 instead of each
+// fetching it from HBM.  Jobs (longest first) go to the XCD with the fewest
+// hedged jobs, then the fewest jobs; each XCD's cus/8 slots are dealt one per
+// job, then the rest round-robin to its hedged jobs up to their copies in
+// `cp`.  Returns the job index per position, -1 for padding (empty when
+// nothing is hedged: keep the plain order).
+constexpr int XCDS = 8;
+inline std::vector<int> xcd_layout(const std::vector<int> &cp, size_t cus) {
+    std::vector<int> pos;
+    if (cp.empty() || std::all_of(cp.begin(), cp.end(), [](int c) { return c <= 1; })) return pos;
+    const size_t cap = cus / XCDS;
+    if (cp.size() > cap * XCDS) return pos;
+    std::vector<std::vector<int>> bk(XCDS);
+    std::vector<int> nh(XCDS, 0);
+    for (size_t k = 0; k < cp.size(); k++) {     // jobs arrive longest first
+        int b = 0;
+        for (int i = 1; i < XCDS; i++) {
+            const bool hk = cp[k] > 1;
+            const auto key = [&](int j) { return std::make_pair(hk ? nh[j] : 0, bk[j].size()); };
+            if (key(i) < key(b)) b = i;
+        }
+        bk[b].push_back(int(k));
+        nh[b] += cp[k] > 1;
+    }
+    size_t rows = 0;
+    std::vector<std::vector<int>> slots(XCDS);
+    for (int b = 0; b < XCDS; b++) {
+        std::vector<int> got(bk[b].size(), 1);
+        size_t spare = cap - bk[b].size();
+        for (bool more = true; more && spare;) {
+            more = false;
+            for (size_t i = 0; i < bk[b].size() && spare; i++)
+                if (got[i] < cp[bk[b][i]]) { got[i]++; spare--; more = true; }
+        }
+        for (size_t i = 0; i < bk[b].size(); i++)
+            for (int c = 0; c < got[i]; c++) slots[b].push_back(bk[b][i]);
+        rows = std::max(rows, slots[b].size());
+    }
+    pos.assign(rows * XCDS, -1);
+    for (int b = 0; b < XCDS; b++)
+        for (size_t r = 0; r < slots[b].size(); r++) pos[r * XCDS + b] = slots[b][r];
+    return pos;
+}
+
 // Hedged launches in flight in this process (decode chains, fqz range
 // chains).  Concurrent callers (the drop-in CLI's thread pool, several host
 // threads) share the spare CUs: each plans its copies for cus / active.
@@ -287,8 +336,9 @@ GpuCtx &gpu();
 // Helper contexts of the calling thread (k < AUX_CTXS), for work run by
 // helper threads concurrently with the thread's own (created on first use),
 // and a rewind of every one that exists.
-constexpr int AUX_CTXS = 10;  // 0 fqz, 1 LZP3, 2..7 sequence models, 8 stripes, 9 names
-constexpr int AUX_SEQ0 = 2, AUX_NSEQ = 6, AUX_STRIPES = 8, AUX_NAMES = 9;
+constexpr int AUX_CTXS = 11;  // 0 fqz, 1 LZP3, 2..7 sequence models, 8 stripes, 9 names,
+                              // 10 plain rANS candidates
+constexpr int AUX_SEQ0 = 2, AUX_NSEQ = 6, AUX_STRIPES = 8, AUX_NAMES = 9, AUX_PLAIN = 10;
 GpuCtx &gpu_aux(int k = 0);
 void gpu_aux_reset_all();
 

@@ -90,7 +90,14 @@ struct DecJob {
     uint32_t rows;          // table rows (1 for O0)
     uint32_t mode;          // DEC_TAB_* (dec_table_mode)
     uint32_t *done;         // hedged launch: claim word, zeroed; ~0 = a copy finished (or nullptr)
+    // O0 NX=4 with at most DEC_REG_MAX symbols covering all 2^bits slots:
+    // the symbols' start | f << 16 in slot order (the register decoder,
+    // rans_chain.hip dec4_lean_body); nreg = 0 otherwise.  nx = 0 marks a
+    // padding job of an XCD-grouped launch (exits at once).
+    uint32_t nreg;
+    uint32_t reg[8];
 };
+constexpr uint32_t DEC_REG_MAX = 8;
 
 // Decoder table placement (rans_chain.hip).  Per slot of a row of 2^bits:
 //   LDS / GLOBAL  u32 (f-1) << (bits+8) | (slot - start) << 8 | symbol

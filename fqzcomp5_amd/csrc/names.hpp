@@ -58,11 +58,14 @@ void name_add_requests(GpuCtx &g, NameEnc &E, const std::vector<LzpEncReq> &lz,
 // Stage 3, after compress_batch: E.out, E.ok.
 void name_assemble(GpuCtx &g, NameEnc &E, const std::vector<CompressReq> &reqs);
 // All stages for a set of candidates on context g (hosts stages on up to
-// 16 threads).  h_names[k] / d_names[k]: candidate k's names.
+// 16 threads).  h_names[k] / d_names[k]: candidate k's names; ready[k]
+// (optional): an event after which h_names[k] holds them (a download still
+// in flight when the batch starts).
 void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
                         const std::vector<const uint8_t *> &h_names,
                         const std::vector<const uint8_t *> &d_names,
-                        const std::vector<uint32_t> &lens, const std::vector<int> &methods);
+                        const std::vector<uint32_t> &lens, const std::vector<int> &methods,
+                        const std::vector<hipEvent_t> *ready = nullptr);
 
 struct NameDec {
     const uint8_t *comp = nullptr;   // host: the payload after [u_len][strat][c_len]

@@ -942,7 +942,16 @@ static DEV void store_slab_o0(uint16_t *ring, uint32_t s, int z, uint4 v) {
     if (w0 < O0_MIRROR) *reinterpret_cast<uint4 *>(ring + RING_WORDS + w0) = v;
 }
 
-template <bool O1>
+// Register decoder (K > 0, O0 only): the stream's K <= 8 symbols cover the
+// 2^bits slots, and per symbol i a key = start_i << 16 | (0xffff - f_i)
+// lives in a register (uniform).  With T = slot << 16 | 0xffff, the symbol
+// holding the slot is the one whose key is the largest <= T, i.e. the
+// smallest T - key_i (the keys above T wrap to >= 2^32 - 2^28), and that
+// difference is (slot - start) << 16 | f: K subtractions and a v_min3 tree,
+// no table read (~64 cycles on the chain) and no compare whose SGPR result a
+// select would wait for (~20 cycles each).  The slot is still what the group
+// keeps.
+template <bool O1, int K = 0>
 static DEV void dec4_lean_body(const DecJob &J) {
     constexpr int NX = 4;
     constexpr uint32_t G = O0_G;
@@ -987,6 +996,10 @@ static DEV void dec4_lean_body(const DecJob &J) {
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(
         (__attribute__((address_space(3))) uint16_t *)(ring)));
     uint16_t *myob = obuf + (l & 3) * G;
+    uint32_t KEY[K > 0 ? K : 1];
+#pragma unroll
+    for (int i = 0; i < (K > 0 ? K : 1); i++)
+        KEY[i] = K > 0 ? (J.reg[i] & 0xffffu) << 16 | (0xffffu - (J.reg[i] >> 16)) : 0u;
 #ifdef FQZ5_CHAIN_PROBE
     const uint64_t pr0 = __builtin_amdgcn_s_memtime(), rr0 = __builtin_amdgcn_s_memrealtime();
     uint64_t t_steps = 0, n_steps = 0;
@@ -1014,6 +1027,27 @@ static DEV void dec4_lean_body(const DecJob &J) {
                 uint32_t a[16];
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
+                    if (K > 0) {
+                        // the window read first (its address is known since
+                        // the last step), so its latency hides behind the
+                        // selection
+                        const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
+                        __builtin_amdgcn_sched_barrier(0);
+                        const uint32_t T = (x & mask) << 16 | 0xffffu;
+                        a[u] = T >> 16;
+                        const uint32_t xh = x >> bits;
+                        uint32_t d = T - KEY[0];
+#pragma unroll
+                        for (int i = 1; i < K; i++) d = min(d, T - KEY[i]);
+                        const uint32_t xd = __umul24(d & 0xffffu, xh) + (d >> 16);
+                        const bool c = xd < RANS_LOW_D;
+                        const uint64_t m = __ballot(c);
+                        const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;
+                        const uint32_t w = uint32_t(win >> r16);
+                        x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
+                        ptr = vbcnt(uint32_t(m), ptr, r16);
+                        continue;
+                    }
                     const uint32_t ea = O1 ? row + ((x & mask) << 4) : tab_lds + ((x & mask) << 4);
                     a[u] = O1 ? (ea >> 4) - idx0 : x & mask;
                     const uint32_t xh = x >> bits;          // ready before the reads return
@@ -1122,13 +1156,26 @@ static DEV void dec4_lean_body(const DecJob &J) {
 template <bool O1, int TM>
 static DEV void dec_any(const DecJob &J) {
     if (J.nx == 32) dec32_body<O1, TM>(J);
-    else if (!O1)   dec4_lean_body<false>(J);
+    else if (!O1) {
+        switch (J.nreg) {
+        case 1: dec4_lean_body<false, 1>(J); break;
+        case 2: dec4_lean_body<false, 2>(J); break;
+        case 3: dec4_lean_body<false, 3>(J); break;
+        case 4: dec4_lean_body<false, 4>(J); break;
+        case 5: dec4_lean_body<false, 5>(J); break;
+        case 6: dec4_lean_body<false, 6>(J); break;
+        case 7: dec4_lean_body<false, 7>(J); break;
+        case 8: dec4_lean_body<false, 8>(J); break;
+        default: dec4_lean_body<false>(J);
+        }
+    }
     else if (TM == DEC_TAB_LDS && dec_lean(J.rows, J.bits)) dec4_lean_body<true>(J);
     else            dec4_body<O1, TM>(J);
 }
 
 __global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
     const DecJob J = jobs[blockIdx.x];
+    if (J.nx == 0) return;                   // padding of an XCD-grouped launch
 #ifdef FQZ5_CHAIN_PROBE
     const uint64_t jt0 = __builtin_amdgcn_s_memrealtime(), jc0 = __builtin_amdgcn_s_memtime();
     struct End {

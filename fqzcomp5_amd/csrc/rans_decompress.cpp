@@ -288,6 +288,17 @@ int Decompressor::parse(const uint8_t *h, const uint8_t *d, uint32_t len, uint8_
     return id;
 }
 
+// $FQZ5_NO_REGDEC / $FQZ5_NO_XCD_GROUP: the table-in-LDS O0 decoder and the
+// plain hedge order instead (A/B measurements)
+static bool reg_decoder() {
+    static const bool on = std::getenv("FQZ5_NO_REGDEC") == nullptr;
+    return on;
+}
+static bool xcd_grouping() {
+    static const bool on = std::getenv("FQZ5_NO_XCD_GROUP") == nullptr;
+    return on;
+}
+
 void Decompressor::run_djs(const std::vector<int> &ids) {
     std::vector<uint32_t> tabs;
     std::vector<uint8_t> alphas;
@@ -364,7 +375,19 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
         const uint32_t mode = dec_table_mode(j.o1, rows, j.bits);
         djs.push_back(DecJob{j.d + j.tab_len, d_tabs + offs[k].tab,
                              j.o1 ? d_alpha + offs[k].alpha : nullptr, j.d_out, d_status + k,
-                             j.len - j.tab_len, j.n, j.nx, j.bits, rows, mode, nullptr});
+                             j.len - j.tab_len, j.n, j.nx, j.bits, rows, mode, nullptr, 0, {}});
+        if (!j.o1 && j.nx == 4 && reg_decoder()) {
+            // the register decoder: <= 8 symbols that cover every slot
+            DecJob &d = djs.back();
+            uint32_t k2 = 0, x = 0;
+            for (int s = 0; s < 256 && k2 <= DEC_REG_MAX; s++) {
+                if (!j.F[s]) continue;
+                if (k2 < DEC_REG_MAX) d.reg[k2] = x | (j.F[s] << 16);
+                k2++;
+                x += j.F[s];
+            }
+            if (k2 >= 1 && k2 <= DEC_REG_MAX && x == (1u << j.bits)) d.nreg = k2;
+        }
         bytes += double(j.n) + (j.len - j.tab_len);
         lds = std::max(lds, dec_lds_bytes(rows, j.bits, int(mode)));
     }
@@ -380,8 +403,20 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
         uint32_t *d_done = g_.arena.alloc_n<uint32_t>(nj);
         g_.memset0(d_done, nj * 4);
         for (size_t k = 0; k < nj; k++) djs[k].done = d_done + k;
-        for (size_t k = 0; k < nj; k++)
-            for (int c = 1; c < cp[k]; c++) djs.push_back(djs[k]);
+        // every copy of a stream on one XCD (xcd_layout), padding jobs nx = 0
+        const std::vector<int> pos = xcd_grouping() ? xcd_layout(cp, share.cus)
+                                                    : std::vector<int>();
+        if (!pos.empty()) {
+            std::vector<DecJob> laid(pos.size());
+            for (size_t i = 0; i < pos.size(); i++) {
+                if (pos[i] >= 0) laid[i] = djs[size_t(pos[i])];
+                else { laid[i] = djs[0]; laid[i].nx = 0; }
+            }
+            djs.swap(laid);
+        } else {
+            for (size_t k = 0; k < nj; k++)
+                for (int c = 1; c < cp[k]; c++) djs.push_back(djs[k]);
+        }
     }
     lds = g_.chain_lds(lds, djs.size());
     if (!djs.empty()) FQZ5_HIP(launch_dec(g_.upload(djs), int(djs.size()), lds, g_.stream));

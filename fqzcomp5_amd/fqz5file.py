@@ -136,37 +136,89 @@ def container(blocks: list[bytes], bases: list[int], nrec: list[int]) -> bytes:
     return b"".join(out)
 
 
-def compress_bytes(text: bytes, level: int = 3, blk_size: int | None = None,
-                   device: str = "cuda") -> bytes:
-    """fqzcomp5 -<level> (-t1 semantics) of FASTQ text, on the GPU."""
+def _pinned(n: int):
     import torch
+    return torch.empty(max(n, 1), dtype=torch.uint8, pin_memory=True)[:n]
+
+
+def _read_pinned(path: str):
+    """The file's bytes in page-locked host memory (one read, no copy)."""
+    import os
+    n = os.path.getsize(path)
+    buf = _pinned(n)
+    mv = memoryview(buf.numpy())
+    with open(path, "rb", buffering=0) as f:
+        got = 0
+        while got < n:
+            k = f.readinto(mv[got:])
+            if not k:
+                raise OSError(f"{path}: short read")
+            got += k
+    return buf
+
+
+def _encode(text_d, level: int, blk_size: int | None):
+    """FASTQ text in HBM -> (the Run holding the encoded blocks, bases, records)."""
     blk = blk_size or S.BLOCK_SIZE[level]
-    text_d = torch.from_numpy(np.frombuffer(text, np.uint8).copy()).to(device)
     run = parse_fastq(text_d, blk)
-    del text_d
     if not run.blocks:
-        return container([], [], [])
+        return None, [], []
     res, *_ = S.encode_run(run.enc_secs(), S.masks(level, full=True), S.new_state())
     if any(r.status != 0 for r in res):
         raise _lib.NativeError("section coding failed: " + _lib.last_error())
     run.assemble(res)
+    return run, [int(ln.sum()) for ln in run.lens], [len(ln) for ln in run.lens]
+
+
+def _index(offs, bases, nrec) -> bytes:
+    return INDEX_MAGIC + struct.pack("<I", len(offs)) + b"".join(
+        struct.pack("<QII", o, nb, nr) for o, nb, nr in zip(offs, bases, nrec))
+
+
+def compress_bytes(text: bytes, level: int = 3, blk_size: int | None = None,
+                   device: str = "cuda") -> bytes:
+    """fqzcomp5 -<level> (-t1 semantics) of FASTQ text, on the GPU."""
+    import torch
+    text_d = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(device) if text else \
+        torch.empty(0, dtype=torch.uint8, device=device)
+    run, bases, nrec = _encode(text_d, level, blk_size)
+    del text_d
+    if run is None:
+        return container([], [], [])
     blocks = [run.block_bytes(b) for b in range(len(run.blocks))]
-    bases = [int(ln.sum()) for ln in run.lens]
-    return container(blocks, bases, [len(ln) for ln in run.lens])
+    return container(blocks, bases, nrec)
 
 
-def compress_file(src: str, dst: str, level: int = 3, blk_size: int | None = None) -> int:
-    with open(src, "rb") as f:
-        out = compress_bytes(f.read(), level, blk_size)
+def compress_file(src: str, dst: str, level: int = 3, blk_size: int | None = None,
+                  device: str = "cuda") -> int:
+    """The file path without host copies of the data: the FASTQ read into
+    page-locked memory, one copy to HBM, the encoded blocks back in one copy
+    and written behind the header, then the index."""
+    text_d = _read_pinned(src).to(device, non_blocking=True)
+    run, bases, nrec = _encode(text_d, level, blk_size)
+    del text_d
+    if run is None:
+        out = container([], [], [])
+        with open(dst, "wb") as f:
+            f.write(out)
+        return len(out)
+    end = int(run.blk_off[-1])
+    host = _pinned(end)
+    host.copy_(run.blk_buf[:end])
+    offs = [16 + int(run.blk_off[b]) for b in range(len(run.blocks))]
+    idx = _index(offs, bases, nrec)
     with open(dst, "wb") as f:
-        f.write(out)
-    return len(out)
+        f.write(MAGIC + struct.pack("<Q", 16 + end))
+        f.write(memoryview(host.numpy()))
+        f.write(idx)
+    return 16 + end + len(idx)
 
 
-def _blocks_of(data: bytes):
+def _blocks_of(data):
     """Block byte ranges of a .fqz5 (walking block_size fields up to the
     index, fqzcomp5.c:3754-3772)."""
-    if data[:8] != MAGIC:
+    data = memoryview(data).cast("B")
+    if bytes(data[:8]) != MAGIC:
         raise ValueError("not an FQZ5 v1.1 file")
     (idx,) = struct.unpack_from("<Q", data, 8)
     end = idx if idx else len(data)
@@ -178,15 +230,14 @@ def _blocks_of(data: bytes):
     return out
 
 
-def decompress_bytes(data: bytes, plus_name: bool = False, device: str = "cuda") -> bytes:
-    """fqzcomp5 -d of a .fqz5 (its blocks parsed, CRC-checked and decoded on
-    the GPU, the FASTQ text formatted there)."""
+def _decode(data, buf, plus_name: bool, device: str):
+    """Blocks of a .fqz5 (host view `data`, device copy `buf`) -> the FASTQ
+    text of every block in one device buffer."""
     import torch
     so = _load()
     ranges = _blocks_of(data)
     if not ranges:
-        return b""
-    buf = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(device)
+        return torch.empty(0, dtype=torch.uint8, device=device)
     views, lens = [], []
     for s, e in ranges:
         v = S.BlockView()
@@ -222,22 +273,47 @@ def decompress_bytes(data: bytes, plus_name: bool = False, device: str = "cuda")
     res = S.decode(secs)
     if any(r.status != 0 for r in res):
         raise _lib.NativeError("section decoding failed: " + _lib.last_error())
-    parts = []
+    # the text of every block, one after the other in one device buffer
+    args, sizes = [], []
     for v, ln, po in zip(views, lens, places):
         size = C.c_uint64(0)
-        args = (out_d.data_ptr() + po[0], v.name_ulen, out_d.data_ptr() + po[1],
-                out_d.data_ptr() + po[2], ln.ctypes.data, len(ln), int(plus_name))
-        _check(so.fqz5_fastq_format(*args, None, 0, C.byref(size)), "fqz5_fastq_format")
-        t = torch.empty(max(int(size.value), 1), dtype=torch.uint8, device=device)
-        _check(so.fqz5_fastq_format(*args, t.data_ptr(), t.numel(), C.byref(size)),
+        a = (out_d.data_ptr() + po[0], v.name_ulen, out_d.data_ptr() + po[1],
+             out_d.data_ptr() + po[2], ln.ctypes.data, len(ln), int(plus_name))
+        _check(so.fqz5_fastq_format(*a, None, 0, C.byref(size)), "fqz5_fastq_format")
+        args.append(a)
+        sizes.append(int(size.value))
+    text = torch.empty(max(sum(sizes), 1), dtype=torch.uint8, device=device)
+    at = 0
+    for a, n in zip(args, sizes):
+        size = C.c_uint64(0)
+        _check(so.fqz5_fastq_format(*a, text.data_ptr() + at, n, C.byref(size)),
                "fqz5_fastq_format")
-        parts.append(t[:int(size.value)].cpu().numpy().tobytes())
-    return b"".join(parts)
+        at += n
+    return text[:at]
 
 
-def decompress_file(src: str, dst: str, plus_name: bool = False) -> int:
-    with open(src, "rb") as f:
-        out = decompress_bytes(f.read(), plus_name)
+def decompress_bytes(data: bytes, plus_name: bool = False, device: str = "cuda") -> bytes:
+    """fqzcomp5 -d of a .fqz5 (its blocks parsed, CRC-checked and decoded on
+    the GPU, the FASTQ text formatted there)."""
+    import torch
+    if not _blocks_of(data):
+        return b""
+    buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(device)
+    return _decode(data, buf, plus_name, device).cpu().numpy().tobytes()
+
+
+def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "cuda") -> int:
+    """The file path: the .fqz5 read into page-locked memory, one copy to
+    HBM, the FASTQ text back in one copy and written."""
+    host = _read_pinned(src)
+    hv = host.numpy()
+    if not _blocks_of(hv):
+        open(dst, "wb").close()
+        return 0
+    buf = host.to(device, non_blocking=True)
+    text = _decode(hv, buf, plus_name, device)
+    out = _pinned(int(text.numel()))
+    out.copy_(text)
     with open(dst, "wb") as f:
-        f.write(out)
-    return len(out)
+        f.write(memoryview(out.numpy()))
+    return int(text.numel())

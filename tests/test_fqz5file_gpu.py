@@ -93,3 +93,24 @@ def test_not_4line_fastq_fails_loudly():
 def test_empty_input():
     z = fqz5file.compress_bytes(b"", 3)
     assert z[:8] == fqz5file.MAGIC and fqz5file.decompress_bytes(z) == b""
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="oracle/_ref not built")
+def test_file_path_vs_cli(tmp_path):
+    """compress_file / decompress_file (page-locked reads, one copy each way)
+    write the reference CLI's file and give the input back."""
+    r = synth.illumina(40000, seed=33, with_names=True)
+    src = str(tmp_path / "in.fastq")
+    synth.write_fastq(r, src)
+    want = _ref(str(tmp_path), src, 3, "1M")
+    dst, back = str(tmp_path / "g.fqz5"), str(tmp_path / "g.fastq")
+    n = fqz5file.compress_file(src, dst, 3, blk_size=1_000_000)
+    got = open(dst, "rb").read()
+    assert n == len(got) and got == want
+    assert fqz5file.decompress_file(dst, back) == os.path.getsize(src)
+    assert open(back, "rb").read() == open(src, "rb").read()
+    empty = str(tmp_path / "e.fastq")
+    open(empty, "wb").close()
+    fqz5file.compress_file(empty, dst, 3)
+    assert open(dst, "rb").read() == fqz5file.compress_bytes(b"", 3)
+    assert fqz5file.decompress_file(dst, back) == 0 and os.path.getsize(back) == 0
