@@ -61,8 +61,9 @@ sys.path.insert(0, ROOT)
 # queues per process those streams share queues and serialise (measured:
 # the -3 encode waited 100 ms per step behind the LZP3 helper's chain).
 # Must be set before anything initialises HIP.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 32:
-    os.environ["GPU_MAX_HW_QUEUES"] = "32"
+_HWQ = int(os.environ.get("FQZ5_HW_QUEUES", "32") or 32)   # experiments: fewer queues
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < _HWQ:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_HWQ)
 
 FASTQ_REC = 358          # bytes of FASTQ text per synthetic 150 bp record (avg)
 BLK = 100_000_000        # -3 / -5 block size (fqzcomp5.c:4896,4904)

@@ -25,7 +25,9 @@ namespace fqz5 {
 // (e.g. the relinked CLI) loads this library before anything touched HIP.
 __attribute__((constructor)) static void hw_queues_default() {
     const char *v = std::getenv("GPU_MAX_HW_QUEUES");
-    if (!v || std::atoi(v) < 32) setenv("GPU_MAX_HW_QUEUES", "32", 1);
+    const char *w = std::getenv("FQZ5_HW_QUEUES");          // experiments: fewer queues
+    const int want = w ? std::atoi(w) : 32;
+    if (!v || std::atoi(v) < want) setenv("GPU_MAX_HW_QUEUES", std::to_string(want).c_str(), 1);
 }
 
 static thread_local std::string g_err;

@@ -1157,6 +1157,10 @@ template <bool O1, int TM>
 static DEV void dec_any(const DecJob &J) {
     if (J.nx == 32) dec32_body<O1, TM>(J);
     else if (!O1) {
+#ifdef FQZ5_NO_REG_VARIANTS                  // experiments: code size of the kernel
+        dec4_lean_body<false>(J);
+        return;
+#endif
         switch (J.nreg) {
         case 1: dec4_lean_body<false, 1>(J); break;
         case 2: dec4_lean_body<false, 2>(J); break;

@@ -45,6 +45,16 @@ inline bool c_space(uint8_t c) { return c == ' ' || uint8_t(c - 9) < 5; }
 inline bool c_punct(uint8_t c) { return c > 32 && c < 127 && !c_alpha(c) && !c_digit(c); }
 inline bool c_xdigit(uint8_t c) { return c_digit(c) || uint8_t((c | 32) - 'a') < 6; }
 
+// punctuation or space (the trie search's from_punct bytes), by byte
+struct PsTable {
+    uint8_t t[256];
+    PsTable() {
+        for (int c = 0; c < 256; c++) t[c] = (c_punct(uint8_t(c)) || c_space(uint8_t(c))) ? 1 : 0;
+    }
+};
+const PsTable PS_TAB;
+const uint8_t *const PS = PS_TAB.t;
+
 struct Tok { int type = 0, ival = 0, sval = 0; };    // last_context_tok
 // last_context: a name's tokens live in one arena per block (a finished
 // name's tokens never change, so a duplicate shares its original's)
@@ -115,6 +125,7 @@ struct Trie {
         char fc = 0;                                   // s[0]
     };
     std::vector<Node> nodes{Node()};                   // node 0: the root
+    std::vector<uint32_t> ps{0};                       // punct / space bytes before p
 
     // -> the name to tokenise against, or -1 (:591-695)
     int search(const char *data, size_t len, uint32_t n, int *exact, int *is_fixed,
@@ -126,16 +137,21 @@ struct Trie {
         // with -1 after the bytes before it were walked (:654-674)
         size_t L = 0;
         bool high = false;
+        if (ps.size() < len + 1) ps.resize(len + 1);
         while (L < len && uint8_t(data[L]) > '\n') {
             if (uint8_t(data[L]) & 0x80) { high = true; break; }
+            ps[L + 1] = ps[L] + PS[uint8_t(data[L])];
             L++;
         }
         int from = -1, from_punct = -1, p3 = -1;
-        auto visit = [&](size_t p, uint32_t val) {     // byte p's node held val
+        // the bytes [a, b) (b > a) walked through nodes that held val, in
+        // order: per byte p the reference sets from = val, from_punct = val
+        // if byte p is punctuation or space and val is not this name, and p3
+        // = val if p + 1 is the prefix length
+        auto run = [&](size_t a, size_t b, uint32_t val) {
             from = int(val);
-            const uint8_t c = uint8_t(data[p]);
-            if ((c_punct(c) || c_space(c)) && val != nn) from_punct = int(val);
-            if (int(p + 1) == prefix_len) p3 = int(val);
+            if (val != nn && ps[b] != ps[a]) from_punct = int(val);
+            if (int64_t(prefix_len) > int64_t(a) && int64_t(prefix_len) <= int64_t(b)) p3 = int(val);
         };
         auto leaf = [&](int parent, size_t i) {       // the rest of the name, new
             Node w;
@@ -146,7 +162,7 @@ struct Trie {
             w.sib = nodes[size_t(parent)].child;
             nodes.push_back(w);
             nodes[size_t(parent)].child = int(nodes.size()) - 1;
-            for (size_t p = i; p < L; p++) visit(p, nn);
+            if (i < L) run(i, L, nn);
         };
         int t = 0;
         size_t i = 0;
@@ -167,7 +183,7 @@ struct Trie {
             const size_t m = std::min<size_t>(e.len, L - i);
             size_t k = 1;
             while (k < m && e.s[k] == data[i + k]) k++;
-            for (size_t p = i; p < i + k; p++) visit(p, e.n);
+            run(i, i + k, e.n);
             if (k == e.len) {                          // the whole edge
                 nodes[size_t(x)].n = nn;
                 t = x;
@@ -950,6 +966,25 @@ long long fqz5_tok3_tokenise_bytes(const char *blk, int len, int level) {
     long long tot = 0;
     for (auto &d : T.desc) tot += (long long)d.size();
     return tot;
+}
+
+// Host stage only: FNV-1a of every token stream (index, size, bytes) of
+// `blk`, for CPU regression tests of the tokeniser; 0 on failure.
+unsigned long long fqz5_tok3_tokenise_digest(const char *blk, int len, int level) {
+    std::vector<char> b(blk, blk + std::max(len, 0));
+    Tok3Enc T;
+    if (!tok3_tokenise(b.data(), len, level, 0, T)) return 0;
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint8_t v) { h = (h ^ v) * 1099511628211ull; };
+    for (size_t i = 0; i < T.desc.size(); i++) {
+        const auto &d = T.desc[i];
+        if (d.empty()) continue;
+        for (int k = 0; k < 4; k++) mix(uint8_t(i >> (8 * k)));
+        for (int k = 0; k < 4; k++) mix(uint8_t(d.size() >> (8 * k)));
+        for (uint8_t v : d) mix(v);
+    }
+    mix(uint8_t(T.max_tok));
+    return h;
 }
 
 uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *out_len,

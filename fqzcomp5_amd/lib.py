@@ -15,8 +15,9 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 # helper contexts' streams need queues of their own (bench.py); effective
 # only when nothing in the process has initialised HIP yet
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 32:
-    os.environ["GPU_MAX_HW_QUEUES"] = "32"
+_HWQ = int(os.environ.get("FQZ5_HW_QUEUES", "32") or 32)   # experiments: fewer queues
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < _HWQ:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_HWQ)
 
 _libc = C.CDLL(None)
 _libc.free.argtypes = [C.c_void_p]
