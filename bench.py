@@ -87,6 +87,10 @@ def host_threads() -> int:
 
 def make_reads(gb: float, seed: int, kind: str):
     from fqzcomp5_amd import synth
+    if kind == "ont":        # configs[3]: lognormal lengths, median 10.5 kb, read-id names
+        return synth.ont(int(gb * 1e9 / 26_600), seed=seed, with_names=True)
+    if kind == "hifi":       # configs[4]: ~15 kb pairs, READ2 flags from the /2 names
+        return synth.hifi(int(gb * 1e9 / 60_100), seed=seed, with_names=True)
     n_reads = int(gb * 1e9 / FASTQ_REC)
     return (synth.novaseq if kind == "novaseq" else synth.illumina)(n_reads, seed=seed)
 
@@ -157,7 +161,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     t0 = time.time()
     seed = (1 if level <= 3 else 2) + (rank if scaling == "weak" else 0)
     reads = make_reads(gb, seed, kind)
-    blocks = synth.split_blocks(reads, BLK)
+    blocks = synth.split_blocks(reads, BLK if level in (3, 5) else S.BLOCK_SIZE[level])
     if scaling == "strong":                      # contiguous shard of one file
         nb = len(blocks)
         blocks = blocks[rank * nb // world:(rank + 1) * nb // world]
@@ -170,7 +174,10 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     avail = S.masks(level, full=True)
 
     def encode():
-        res, meth_all, sizes, tried, off = S.encode_run(enc_secs, avail, S.new_state())
+        if level >= 7:     # 500 MB / 1 GB blocks: the trial a section at a time
+            res, meth_all, sizes, tried, off = S.encode_run_bounded(enc_secs, avail, S.new_state())
+        else:
+            res, meth_all, sizes, tried, off = S.encode_run(enc_secs, avail, S.new_state())
         run.assemble(res)                          # lengths, header, CRC32
         return res, meth_all, tried, off
 
@@ -223,7 +230,12 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     ok = all(r.status == 0 for r in res) and all(r.status == 0 for r in dres)
     ok = ok and run.roundtrip_ok()
     comp_bytes = int(run.blk_off[-1])
-    quals = "8-level binned quals" if kind == "illumina" else "NovaSeq 4-level i.i.d. quals"
+    shape = {"illumina": "illumina 150 bp, Illumina names, 8-level binned quals",
+             "novaseq": "novaseq 150 bp, Illumina names, NovaSeq 4-level i.i.d. quals",
+             "ont": "ONT reads (lognormal lengths, median 10.5 kb; homopolymer-rich bases; "
+                    "AR(1) quals near Q12), read-id names",
+             "hifi": "HiFi pairs (~15 kb; 62 % Q93 quals), movie/zmw/ccs names with /1 /2"}[kind]
+    blk_mb = (BLK if level in (3, 5) else S.BLOCK_SIZE[level]) // 1_000_000
     full = set(S.preset_methods(level))
     have = set(S.level_methods(level))
     out = {
@@ -237,12 +249,12 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
         # rank 0's fastest / slowest step (spread between steps)
         "enc_ms_min_max": [round(min(enc_steps) * 1e3, 1), round(max(enc_steps) * 1e3, 1)],
         "dec_ms_min_max": [round(min(dec_steps) * 1e3, 1), round(max(dec_steps) * 1e3, 1)],
-        "data": f"synthetic (seeded {kind} 150 bp, Illumina names, {quals}); records "
+        "data": f"synthetic (seeded {shape}); records "
                 f"resident in HBM; in the timed region only the names come to the host "
                 f"(tokenising) and block headers / lengths cross PCIe",
         "config": {"workload": f"fqzcomp5 -{level} whole blocks (names, lengths, seq, qual, "
                                f"CRC) of a {gb:g} GB FASTQ "
-                               f"{'per GPU' if scaling == 'weak' else 'in total'}, 100 MB blocks",
+                               f"{'per GPU' if scaling == 'weak' else 'in total'}, {blk_mb} MB blocks",
                    "blocks_rank0": len(blocks), "level": level,
                    "fastq_bytes_rank0": fq_local,
                    "section_bytes_rank0": run.in_bytes,
@@ -415,7 +427,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--gb", type=float, default=1.0)
     ap.add_argument("--level", type=int, default=3, choices=[1, 3, 5, 7, 9])
-    ap.add_argument("--kind", default="illumina", choices=["illumina", "novaseq"])
+    ap.add_argument("--kind", default="illumina", choices=["illumina", "novaseq", "ont", "hifi"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-level5", action="store_true",

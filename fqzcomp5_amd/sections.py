@@ -324,6 +324,62 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
     return res, meth_all, g_sizes, tried, off
 
 
+def _chunks(rows, sizes, budget: int):
+    """Consecutive runs of `rows` whose `sizes` sum to at most `budget`
+    (at least one row each)."""
+    out, cur, tot = [], [], 0
+    for i in rows:
+        if cur and tot + int(sizes[i]) > budget:
+            out.append(cur)
+            cur, tot = [], 0
+        cur.append(i)
+        tot += int(sizes[i])
+    if cur:
+        out.append(cur)
+    return out
+
+
+def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState,
+                       group=None, chunk_bytes: int = 600_000_000):
+    """encode_run for the large-block presets (-7: 500 MB, -9: 1 GB blocks),
+    in bounded device memory: the same choices and bytes, at the cost of
+    coding each trial section's winner twice.
+
+    A trial section of -7/-9 tries up to 13 methods, five of them fqz (about
+    60 B of events, sort buffers and coder records per quality byte) and five
+    sequence models (about as much per base): a trial window of 500 MB blocks
+    tried at once needs more than one GPU's 288 GB.  Here the sections the
+    schedule has try methods are tried a chunk at a time (input bytes summed
+    up to `chunk_bytes`, one section at least), only their sizes kept (each
+    try rewinds the last one's buffers); the replay picks every section's
+    method from the sizes as encode_run does; then every section is coded
+    with its one method a chunk at a time (fqz5_sections_commit codes the
+    methods a session did not try, "late")."""
+    ins = np.array([s.in_size for s in secs], np.uint32)
+    ids = np.array([s.sec for s in secs], np.int32)
+    blank = np.zeros((len(secs), M_LAST), np.uint32)
+    _, _, g_ids0, off = exchange_sizes(blank, ins, ids, group)
+    sched = trial_schedule(g_ids0, avail, state)[off:off + len(secs)]
+    local = np.full((len(secs), M_LAST), np.iinfo(np.uint32).max, np.uint32)
+    so = _load()
+    prev = so.fqz5_set_trial_prune(0)         # pruning needs a whole trial window per try
+    try:
+        for ch in _chunks([i for i in range(len(secs)) if sched[i]], ins, chunk_bytes):
+            local[ch] = sections_try([secs[i] for i in ch], sched[ch])
+    finally:
+        so.fqz5_set_trial_prune(prev)
+    g_sizes, g_ins, g_ids, off = exchange_sizes(local, ins, ids, group)
+    tried = np.zeros(len(g_ids), np.uint32)
+    meth_all = trial_replay(g_ids, g_ins, g_sizes, avail, state, tried)
+    meth = meth_all[off:off + len(secs)]
+    res = []
+    for ch in _chunks(range(len(secs)), ins, chunk_bytes):
+        part = [secs[i] for i in ch]
+        sections_try(part, np.zeros(len(ch), np.uint32))    # an empty session
+        res += sections_commit(part, meth[ch])
+    return res, meth_all, g_sizes, tried, off
+
+
 def fqz_bound(n: int) -> int:
     """Room the fqz encoder needs: the coder's bound (fqz_codec.cpp) plus
     the parameter header."""

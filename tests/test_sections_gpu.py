@@ -119,3 +119,32 @@ def test_arena_constant_over_steps():
         sizes.append(lib.arena_bytes())
     assert run.roundtrip_ok()
     assert sizes[1:] == sizes[1:2] * (len(sizes) - 1), sizes
+
+
+@pytest.mark.parametrize("level,kind,nreads,blk", [(7, "ont", 500, 1_500_000),
+                                                   (9, "hifi", 600, 1_500_000)])
+def test_bounded_run_equals_run(level, kind, nreads, blk):
+    """encode_run_bounded (the trial a section at a time, then every section
+    coded with its one method, for the -7/-9 block sizes) makes the choices
+    and the bytes of encode_run; chunk_bytes small enough that every chunk
+    holds one or two sections."""
+    reads = GEN[kind](nreads, seed=13)
+    blocks = synth.split_blocks(reads, blk)
+    assert len(blocks) >= 4
+    dev = torch.device("cuda", 0)
+    run = S.Run(reads, blocks, dev, names=False)
+    av = S.masks(level, True)
+    res_a, meth_a, _, tried_a, _ = S.encode_run(run.enc_secs(), av, S.new_state())
+    got_a = [run.chosen(res_a, i) for i in range(len(res_a))]
+    run_b = S.Run(reads, blocks, dev, names=False)
+    res_b, meth_b, _, tried_b, _ = S.encode_run_bounded(run_b.enc_secs(), av, S.new_state(),
+                                                        chunk_bytes=2 * blk // 3)
+    assert all(r.status == 0 for r in res_b)
+    assert list(meth_a) == list(meth_b)
+    assert list(tried_a) == list(tried_b)
+    for i in range(len(res_b)):
+        assert run_b.chosen(res_b, i) == got_a[i], i
+    dres = S.decode(run_b.dec_secs(res_b))
+    assert all(r.status == 0 for r in dres)
+    torch.cuda.synchronize()
+    assert run_b.roundtrip_ok()
