@@ -194,7 +194,9 @@ def compress_file(src: str, dst: str, level: int = 3, blk_size: int | None = Non
     """The file path without host copies of the data: the FASTQ read into
     page-locked memory, one copy to HBM, the encoded blocks back in one copy
     and written behind the header, then the index."""
-    text_d = _read_pinned(src).to(device, non_blocking=True)
+    # a blocking copy: the library's kernels run on its own streams, which
+    # do not wait for torch's (a non-blocking copy raced the FASTQ parse)
+    text_d = _read_pinned(src).to(device)
     run, bases, nrec = _encode(text_d, level, blk_size)
     del text_d
     if run is None:
@@ -310,7 +312,7 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
     if not _blocks_of(hv):
         open(dst, "wb").close()
         return 0
-    buf = host.to(device, non_blocking=True)
+    buf = host.to(device)     # blocking: block parsing runs on the library's streams
     text = _decode(hv, buf, plus_name, device)
     out = _pinned(int(text.numel()))
     out.copy_(text)

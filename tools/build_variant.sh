@@ -8,7 +8,7 @@ name=$1; shift
 srcname=$1; shift
 here=$(cd "$(dirname "$0")" && pwd)
 src=$here/../fqzcomp5_amd/csrc
-out=$here/variants
+out=${VARIANT_DIR:-$here/variants}
 mkdir -p $out/$name
 objs=""
 for f in $src/build/*.o; do
