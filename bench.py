@@ -66,6 +66,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < _HWQ:
     os.environ["GPU_MAX_HW_QUEUES"] = str(_HWQ)
 
 FASTQ_REC = 358          # bytes of FASTQ text per synthetic 150 bp record (avg)
+GAP_S = float(os.environ.get("FQZ5_BENCH_GAP_S", "0") or 0)
 BLK = 100_000_000        # -3 / -5 block size (fqzcomp5.c:4896,4904)
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8 TB/s spec
 
@@ -200,6 +201,9 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
         a = time.perf_counter()
         res, meth_all, tried, off = encode()
         torch.cuda.synchronize()
+        if GAP_S:                    # experiments: idle GPU between the phases (untimed)
+            time.sleep(GAP_S)
+            a += GAP_S
         b = time.perf_counter()
         dres = decode(res)
         torch.cuda.synchronize()

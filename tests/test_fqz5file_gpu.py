@@ -114,3 +114,18 @@ def test_file_path_vs_cli(tmp_path):
     fqz5file.compress_file(empty, dst, 3)
     assert open(dst, "rb").read() == fqz5file.compress_bytes(b"", 3)
     assert fqz5file.decompress_file(dst, back) == 0 and os.path.getsize(back) == 0
+
+
+def test_file_path_large_roundtrip(tmp_path):
+    """The file path on a 300 MB FASTQ (3 blocks at -3): the copy to HBM must
+    be complete before the library's kernels (on its own streams) parse the
+    text or the blocks; a non-blocking copy on torch's stream raced the
+    block parse and failed the CRC check on the bench's 1 GB file."""
+    r = synth.illumina(840_000, seed=35)
+    src = str(tmp_path / "big.fastq")
+    n_in = synth.write_fastq(r, src)
+    dst, back = str(tmp_path / "big.fqz5"), str(tmp_path / "big.back")
+    fqz5file.compress_file(src, dst, 3)
+    assert fqz5file.decompress_file(dst, back) == n_in
+    with open(back, "rb") as a, open(src, "rb") as b:
+        assert a.read() == b.read()
