@@ -2,13 +2,17 @@
 // the record parse of load_seqs_kseq (fqzcomp5.c:423-623, kseq.h:178-218)
 // for 4-line FASTQ, its block split rule (fqzcomp5.c:471-477), the gather of
 // a block's name / sequence / quality sections with the records' lengths and
-// READ2 flags, and output_fastq (fqzcomp5.c:3441-3480) on decoded blocks.
+// READ2 flags, and output_fastq / output_fasta (fqzcomp5.c:3441-3480,
+// :3503-3517) on decoded blocks.
 //
 // Lines: every '\n' of the text is found by 64 KiB tiles (counts, a scan,
-// then ordered writes), so record r is lines 4r..4r+3.  Records are parsed
-// one per thread; the section bytes are gathered one wave per record at the
-// scanned offsets.  Text that is not 4-line FASTQ (multi-line sequences,
-// FASTA) is refused with an error, never parsed on the host.
+// then ordered writes), so record r is lines 4r..4r+3 (FASTQ) or 2r, 2r+1
+// (FASTA: text whose first byte is '>', one sequence line per record; the
+// block then has no quality section, fqzcomp5.c:575-578, :2258-2264).
+// Records are parsed one per thread; the section bytes are gathered one wave
+// per record at the scanned offsets.  Text that is neither 4-line FASTQ nor
+// 2-line FASTA (multi-line sequences) is refused with an error, never parsed
+// on the host.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -92,18 +96,16 @@ __device__ __forceinline__ uint64_t strip_cr(const uint8_t *t, uint64_t s, uint6
     return (e - s > 1 && t[e - 1] == '\r') ? e - 1 : e;
 }
 
-// record r = lines 4r..4r+3 (kseq_read, kseq.h:178-218)
+// record r = lines 4r..4r+3, or 2r..2r+1 for FASTA (kseq_read, kseq.h:178-218)
+template <int LPR>
 __global__ void k_fq_records(const uint8_t *t, const uint64_t *nl, uint64_t nrec,
                              fqz5_fastq_rec *recs, uint32_t *rec_size, int32_t *status) {
     const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (r >= nrec) return;
-    const uint64_t s0 = r ? nl[4 * r - 1] + 1 : 0, e0 = nl[4 * r];
-    const uint64_t s1 = e0 + 1, e1 = nl[4 * r + 1];
-    const uint64_t s2 = e1 + 1, e2 = nl[4 * r + 2];
-    const uint64_t s3 = e2 + 1, e3 = nl[4 * r + 3];
+    const uint64_t s0 = r ? nl[LPR * r - 1] + 1 : 0, e0 = nl[LPR * r];
+    const uint64_t s1 = e0 + 1, e1 = nl[LPR * r + 1];
     int bad = 0;
-    if (e0 <= s0 || t[s0] != '@') bad = 1;            // header
-    if (e2 <= s2 || t[s2] != '+') bad = 1;            // '+' line
+    if (e0 <= s0 || t[s0] != (LPR == 4 ? '@' : '>')) bad = 1;   // header
     if (e1 > s1 && (t[s1] == '@' || t[s1] == '>' || t[s1] == '+')) bad = 1;
     // name up to the first isspace(), the comment after it to the line end
     uint64_t p = s0 + 1;
@@ -115,11 +117,20 @@ __global__ void k_fq_records(const uint8_t *t, const uint64_t *nl, uint64_t nrec
     R.comment_len = p < e0 ? uint32_t(strip_cr(t, p + 1, e0) - (p + 1)) : 0u;
     R.seq = s1;
     R.seq_len = uint32_t(strip_cr(t, s1, e1) - s1);
-    R.qual = s3;
-    const uint32_t ql = uint32_t(strip_cr(t, s3, e3) - s3);
-    if (ql != R.seq_len) bad = 1;                     // kseq -2 (:213-216)
+    R.fasta = LPR == 2;
+    R.qual = 0;
+    uint32_t ql = 0;
+    if (LPR == 4) {
+        const uint64_t s2 = e1 + 1, e2 = nl[LPR * r + 2];
+        const uint64_t s3 = e2 + 1, e3 = nl[LPR * r + 3];
+        if (e2 <= s2 || t[s2] != '+') bad = 1;        // '+' line
+        R.qual = s3;
+        ql = uint32_t(strip_cr(t, s3, e3) - s3);
+        if (ql != R.seq_len) bad = 1;                 // kseq -2 (:213-216)
+    }
     recs[r] = R;
-    rec_size[r] = R.name_len + 1 + 2 * R.seq_len;     // load_seqs_kseq's record_size (:472)
+    // load_seqs_kseq's record_size name.l + 1 + seq.l + qual.l (:472)
+    rec_size[r] = R.name_len + 1 + R.seq_len + ql;
     if (bad) atomicMin(status, int32_t(-1 - int32_t(r < 0x7ffffffeull ? r : 0x7ffffffeull)));
 }
 
@@ -151,10 +162,11 @@ __global__ void k_fq_gather(const uint8_t *t, const fqz5_fastq_rec *recs, uint64
         w += 1 + R.comment_len;
     }
     if (lane == 0) o[w] = 0;
-    uint8_t *so = seq + soff[k], *qo = qual + soff[k];
-    for (uint32_t i = lane; i < R.seq_len; i += 64) {
-        so[i] = t[R.seq + i];
-        qo[i] = uint8_t(t[R.qual + i] - 33);
+    uint8_t *so = seq + soff[k];
+    for (uint32_t i = lane; i < R.seq_len; i += 64) so[i] = t[R.seq + i];
+    if (qual && !R.fasta) {
+        uint8_t *qo = qual + soff[k];
+        for (uint32_t i = lane; i < R.seq_len; i += 64) qo[i] = uint8_t(t[R.qual + i] - 33);
     }
 }
 
@@ -178,7 +190,8 @@ __global__ void k_fq_flags(const fqz5_fastq_rec *recs, uint64_t a, uint64_t n, c
 }
 
 // output_fastq (fqzcomp5.c:3441-3480): '@' name '\n' seq '\n' '+' [name] '\n'
-// qual+33 '\n', one wave per record
+// qual+33 '\n'; without qualities output_fasta (:3503-3517): '>' name '\n'
+// seq '\n'.  One wave per record.
 __global__ void k_fq_format(const uint8_t *names, const uint64_t *zpos, const uint8_t *seq,
                             const uint8_t *qual, const uint64_t *soff, const uint32_t *lens,
                             const uint64_t *ooff, uint64_t n, int plus_name, uint8_t *out) {
@@ -188,7 +201,7 @@ __global__ void k_fq_format(const uint8_t *names, const uint64_t *zpos, const ui
     const uint64_t ns = k ? zpos[k - 1] + 1 : 0;
     const uint32_t nl = uint32_t(zpos[k] - ns), L = lens[k];
     uint8_t *o = out + ooff[k];
-    if (lane == 0) o[0] = '@';
+    if (lane == 0) o[0] = qual ? '@' : '>';
     for (uint32_t i = lane; i < nl; i += 64) o[1 + i] = names[ns + i];
     uint64_t w = 1 + nl;
     if (lane == 0) o[w] = '\n';
@@ -196,6 +209,10 @@ __global__ void k_fq_format(const uint8_t *names, const uint64_t *zpos, const ui
     const uint8_t *sp = seq + soff[k], *qp = qual + soff[k];
     for (uint32_t i = lane; i < L; i += 64) o[w + i] = sp[i];
     w += L;
+    if (!qual) {
+        if (lane == 0) o[w] = '\n';
+        return;
+    }
     if (lane == 0) {
         o[w] = '\n';
         o[w + 1] = '+';
@@ -269,6 +286,13 @@ int fqz5_fastq_index(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs
             g.download(&last, d_text + len - 1, 1);
             g.sync();
         }
+        // FASTA when the text starts with '>' (a record without a quality
+        // line; the reference decides on the block's first record, :575-578)
+        uint8_t first_byte = 0;
+        if (len) g.download(&first_byte, d_text, 1);
+        g.sync();
+        const bool fasta = first_byte == '>';
+        const uint64_t lpr = fasta ? 2 : 4;
         uint64_t *lines = nl;
         uint64_t nlines = nn;
         if (len && last != '\n') {
@@ -281,16 +305,17 @@ int fqz5_fastq_index(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs
             nlines = nn + 1;
         }
         // trailing empty lines (kseq skips to the next header) are ignored
-        uint64_t n4 = nlines / 4;
-        if (nlines % 4) {
-            std::vector<uint64_t> tail(size_t(nlines % 4) + 1);
-            const uint64_t first = n4 * 4;
+        uint64_t n4 = nlines / lpr;
+        if (nlines % lpr) {
+            std::vector<uint64_t> tail(size_t(nlines % lpr) + 1);
+            const uint64_t first = n4 * lpr;
             g.download(tail.data() + 1, lines + first, nlines - first);
             if (first) g.download(tail.data(), lines + first - 1, 1);
             g.sync();
             uint64_t prev = first ? tail[0] : uint64_t(-1);
             for (uint64_t k = 1; k <= nlines - first; k++) {
-                if (tail[k] != prev + 1) throw GpuError("fastq: not 4-line FASTQ (stray lines at the end)");
+                if (tail[k] != prev + 1) throw GpuError(fasta ? "fasta: not 2-line FASTA (multi-line sequences or stray lines)"
+                                     : "fastq: not 4-line FASTQ (stray lines at the end)");
                 prev = tail[k];
             }
         }
@@ -299,9 +324,12 @@ int fqz5_fastq_index(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs
         const int32_t ok = 0;
         uint32_t *rs = g.arena.alloc_n<uint32_t>(size_t(n4) + 1);
         FQZ5_HIP(hipMemcpyAsync(st, &ok, 4, hipMemcpyHostToDevice, g.stream));
-        if (n4)
-            hipLaunchKernelGGL(k_fq_records, grid_for(n4, 256), dim3(256), 0, g.stream, d_text, lines, n4,
-                               d_recs, rs, st);
+        if (n4 && fasta)
+            hipLaunchKernelGGL(k_fq_records<2>, grid_for(n4, 256), dim3(256), 0, g.stream, d_text, lines,
+                               n4, d_recs, rs, st);
+        else if (n4)
+            hipLaunchKernelGGL(k_fq_records<4>, grid_for(n4, 256), dim3(256), 0, g.stream, d_text, lines,
+                               n4, d_recs, rs, st);
         FQZ5_HIP(hipGetLastError());
         int32_t status = 0;
         g.download(&status, st, 1);
@@ -309,13 +337,14 @@ int fqz5_fastq_index(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs
         g.sync();
         if (status < 0) {
             char msg[128];
-            std::snprintf(msg, sizeof msg, "fastq: record %lld is not a 4-line FASTQ record",
+            std::snprintf(msg, sizeof msg, fasta ? "fasta: record %lld is not a 2-line FASTA record"
+                                                 : "fastq: record %lld is not a 4-line FASTQ record",
                           static_cast<long long>(-1 - int64_t(status)));
             throw GpuError(msg);
         }
         *nrec = n4;
         g.reset();
-        return 0;
+        return fasta ? 1 : 0;
     } catch (const std::exception &e) {
         fqz5_set_error(e.what());
         try { if (gp) gp->reset(); } catch (...) {}
@@ -366,8 +395,8 @@ int fqz5_fastq_gather(const uint8_t *d_text, const fqz5_fastq_rec *d_recs, uint6
         g.sync();
         sizes[0] = tot[0];
         sizes[1] = tot[1];
-        sizes[2] = tot[1];
-        if (d_names && d_seq && d_qual && n) {
+        sizes[2] = d_qual ? tot[1] : 0;
+        if (d_names && d_seq && n) {
             hipLaunchKernelGGL(k_fq_gather, grid_for(n * 64, 256), dim3(256), 0, g.stream, d_text, d_recs,
                                a, n, noff, soff, d_names, d_seq, d_qual);
             FQZ5_HIP(hipGetLastError());
@@ -407,7 +436,8 @@ int fqz5_fastq_format(const uint8_t *d_names, uint64_t name_len, const uint8_t *
             const uint64_t nl = hz[k] - (prev + 1);
             ooff[k] = o;
             soff[k] = s;
-            o += 1 + nl + 1 + h_len[k] + 2 + (plus_name ? nl : 0) + 1 + h_len[k] + 1;
+            o += d_qual ? 1 + nl + 1 + h_len[k] + 2 + (plus_name ? nl : 0) + 1 + h_len[k] + 1
+                        : 1 + nl + 1 + h_len[k] + 1;
             s += h_len[k];
             prev = hz[k];
         }

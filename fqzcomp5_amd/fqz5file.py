@@ -15,8 +15,10 @@ offset, u32 bases, u32 records}.  Encoding follows a single-threaded (-t1)
 reference run: the codec trial runs over the blocks in file order, so the
 file equals the reference CLI's `-<level> -t1` output byte for byte.
 
-Scope: 4-line FASTQ (the parser refuses multi-line records and FASTA with an
-error; there is no host parse), files that fit in device memory.
+Scope: 4-line FASTQ and 2-line FASTA (text starting with '>': blocks without
+a quality section, decoded to output_fasta's text, fqzcomp5.c:2258-2264,
+:3503-3517); the parser refuses multi-line records with an error (there is
+no host parse); files that fit in device memory.
 """
 from __future__ import annotations
 
@@ -36,7 +38,7 @@ class FastqRec(C.Structure):
     """fqz5_fastq_rec (include/fqz5_fastq.h)"""
     _fields_ = [("name", C.c_uint64), ("comment", C.c_uint64), ("seq", C.c_uint64),
                 ("qual", C.c_uint64), ("name_len", C.c_uint32), ("comment_len", C.c_uint32),
-                ("seq_len", C.c_uint32), ("pad", C.c_uint32)]
+                ("seq_len", C.c_uint32), ("fasta", C.c_uint32)]
 
 
 _bound = False
@@ -70,18 +72,20 @@ def _check(rc, what):
 
 
 def parse_fastq(text_d, blk_size: int):
-    """FASTQ text (a device uint8 tensor) -> a sections.Run of its blocks,
-    every section input gathered in HBM."""
+    """FASTQ (or 2-line FASTA) text (a device uint8 tensor) -> a
+    sections.Run of its blocks, every section input gathered in HBM.  FASTA
+    blocks have no quality section (fqzcomp5.c:2237-2264)."""
     import torch
     so = _load()
     n = int(text_d.numel())
-    # records <= lines / 4 (+1 for a last line without '\n')
-    max_rec = (int((text_d == 10).sum().item()) + 1) // 4 + 1 if n else 1
+    # records <= lines / 4, FASTA lines / 2 (+1 for a last line without '\n')
+    lpr = 2 if n and int(text_d[0].item()) == ord(">") else 4
+    max_rec = (int((text_d == 10).sum().item()) + 1) // lpr + 1 if n else 1
     recs = torch.empty(max_rec * C.sizeof(FastqRec), dtype=torch.uint8, device=text_d.device)
     rsz = np.zeros(max_rec, np.uint32)
     nrec = C.c_uint64(0)
-    _check(so.fqz5_fastq_index(text_d.data_ptr(), n, recs.data_ptr(), max_rec, C.byref(nrec),
-                               rsz.ctypes.data), "fqz5_fastq_index")
+    fasta = _check(so.fqz5_fastq_index(text_d.data_ptr(), n, recs.data_ptr(), max_rec,
+                                       C.byref(nrec), rsz.ctypes.data), "fqz5_fastq_index") == 1
     nrec = int(nrec.value)
     max_blocks = nrec + 1
     first = np.zeros(max_blocks + 1, np.uint64)
@@ -98,7 +102,7 @@ def parse_fastq(text_d, blk_size: int):
     tot_s = sum(b for _, b in sizes)
     name_d = torch.empty(max(tot_n, 1), dtype=torch.uint8, device=text_d.device)
     seq_d = torch.empty(max(tot_s, 1), dtype=torch.uint8, device=text_d.device)
-    qual_d = torch.empty(max(tot_s, 1), dtype=torch.uint8, device=text_d.device)
+    qual_d = None if fasta else torch.empty(max(tot_s, 1), dtype=torch.uint8, device=text_d.device)
     lens, flags, nr, sr = [], [], [], []
     no = so_ = 0
     for k in range(nb):
@@ -108,7 +112,8 @@ def parse_fastq(text_d, blk_size: int):
         sz = (C.c_uint64 * 3)()
         _check(so.fqz5_fastq_gather(text_d.data_ptr(), recs.data_ptr(), a, b,
                                     name_d.data_ptr() + no, seq_d.data_ptr() + so_,
-                                    qual_d.data_ptr() + so_, ln.ctypes.data, fl.ctypes.data, sz),
+                                    None if fasta else qual_d.data_ptr() + so_, ln.ctypes.data,
+                                    fl.ctypes.data, sz),
                "fqz5_fastq_gather")
         lens.append(ln[:b - a])
         flags.append(fl[:b - a])
@@ -250,10 +255,13 @@ def _decode(data, buf, plus_name: bool, device: str):
                "fqz5_block_parse")
         if not v.crc_ok:
             raise _lib.NativeError("block CRC mismatch")
-        if v.qual_ulen == 0 and v.qual_size == 9 and v.seq_ulen:
-            raise _lib.NativeError("FASTA blocks are not supported by this build")
         views.append(v)
         lens.append(ln[:v.nrec])
+    # FASTA: a quality section of u_len 0 and c_len 0 (decode_block,
+    # fqzcomp5.c:2477-2483); the text is then output_fasta's (:3503-3517)
+    fasta = [v.qual_ulen == 0 and v.qual_size == 9 for v in views]
+    if any(fasta) and not all(fasta):
+        raise _lib.NativeError("FASTA and FASTQ blocks in one file")
     nsz = [v.name_ulen for v in views]
     ssz = [v.seq_ulen for v in views]
     out_d = torch.empty(sum(nsz) + 2 * sum(ssz) + 1, dtype=torch.uint8, device=device)
@@ -267,9 +275,10 @@ def _decode(data, buf, plus_name: bool, device: str):
                               v.name_ulen, 0, S.SEC_NAME, rl, None, len(ln), None))
         secs.append(S.Section(base + s + v.seq_off, out_d.data_ptr() + po[1], v.seq_size,
                               v.seq_ulen, 0, S.SEC_SEQ, rl, None, len(ln), None))
-        secs.append(S.Section(base + s + v.qual_off, out_d.data_ptr() + po[2], v.qual_size,
-                              v.qual_ulen, 0, S.SEC_QUAL, rl, None, len(ln),
-                              out_d.data_ptr() + po[1]))
+        if not fasta[0]:
+            secs.append(S.Section(base + s + v.qual_off, out_d.data_ptr() + po[2], v.qual_size,
+                                  v.qual_ulen, 0, S.SEC_QUAL, rl, None, len(ln),
+                                  out_d.data_ptr() + po[1]))
         places.append(po)
         o = po[2] + v.seq_ulen
     res = S.decode(secs)
@@ -280,7 +289,8 @@ def _decode(data, buf, plus_name: bool, device: str):
     for v, ln, po in zip(views, lens, places):
         size = C.c_uint64(0)
         a = (out_d.data_ptr() + po[0], v.name_ulen, out_d.data_ptr() + po[1],
-             out_d.data_ptr() + po[2], ln.ctypes.data, len(ln), int(plus_name))
+             None if fasta[0] else out_d.data_ptr() + po[2], ln.ctypes.data, len(ln),
+             int(plus_name))
         _check(so.fqz5_fastq_format(*a, None, 0, C.byref(size)), "fqz5_fastq_format")
         args.append(a)
         sizes.append(int(size.value))

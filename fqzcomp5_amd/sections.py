@@ -490,7 +490,7 @@ class Run:
         run.reads = None
         run.blocks = [(0, len(ln)) for ln in lens]
         run.names = True
-        run.name_d, run.seq_d, run.qual_d = name_d, seq_d, qual_d
+        run.name_d, run.seq_d, run.qual_d = name_d, seq_d, qual_d   # qual_d None: FASTA
         run.name_h = run.name_off = None
         run._setup([np.ascontiguousarray(ln, np.uint32) for ln in lens],
                    [np.ascontiguousarray(f, np.uint32) for f in flags], name_ranges, seq_ranges)
@@ -511,7 +511,8 @@ class Run:
                 ns, ne = name_ranges[k]
                 self.spans.append((SEC_NAME, ns, ne, 0, k))
             self.spans.append((SEC_SEQ, s, e, fl, k))
-            self.spans.append((SEC_QUAL, s, e, fl, k))
+            if self.qual_d is not None:       # FASTA blocks: no quality section
+                self.spans.append((SEC_QUAL, s, e, fl, k))
         caps = []
         for sec, s, e, fl, _ in self.spans:
             n = e - s
@@ -595,15 +596,22 @@ class Run:
         assert self.names, "blocks need the name sections"
         parts = []
         base = self.enc_buf.data_ptr()
+        per = self.secs_per_block()
         for b in range(len(self.blocks)):
-            i = 3 * b
-            (eo_n, _), (eo_s, _), (eo_q, _) = self.enc[i], self.enc[i + 1], self.enc[i + 2]
+            i = per * b
+            (eo_n, _), (eo_s, _) = self.enc[i], self.enc[i + 1]
             ln = self.lengths[b]
+            q, qs = None, 0                   # FASTA: 9 zero bytes (fqzcomp5.c:2258-2264)
+            if per == 3:
+                q, qs = base + self.enc[i + 2][0], 9 + res[i + 2].clen
             parts.append(BlockParts(len(self.lens[b]), base + eo_n, res[i].clen,
                                     C.cast(C.c_char_p(ln), C.c_void_p), len(ln),
-                                    base + eo_s, 9 + res[i + 1].clen,
-                                    base + eo_q, 9 + res[i + 2].clen))
+                                    base + eo_s, 9 + res[i + 1].clen, q, qs))
         return parts
+
+    def secs_per_block(self) -> int:
+        """Sections per block: name, seq, qual (2 for FASTA blocks)."""
+        return 3 if self.qual_d is not None else 2
 
     def assemble(self, res):
         """Write every block (fqz5_blocks_assemble) into self.blk_buf at
@@ -653,10 +661,11 @@ class Run:
             if not np.array_equal(lens, self.lens[b]):
                 raise _lib.NativeError(f"block {b}: lengths differ")
             bo = int(self.blk_off[b])
+            per = self.secs_per_block()
             for j, (off, size) in enumerate(((v.name_off, v.name_size),
                                              (v.seq_off, v.seq_size),
-                                             (v.qual_off, v.qual_size))):
-                i = 3 * b + j
+                                             (v.qual_off, v.qual_size))[:per]):
+                i = per * b + j
                 sec, s, e, fl, k = self.spans[i]
                 rl, nr = self._rec(k)
                 seq = self._seq_dec(i) if sec == SEC_QUAL else None

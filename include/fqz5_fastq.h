@@ -6,9 +6,12 @@
  *                       kseq.h:178-218) for 4-line FASTQ: name up to the
  *                       first isspace(), comment to the line end, one
  *                       sequence line, '+' line, one quality line, a
- *                       trailing '\r' dropped as kseq drops it.  Text that
- *                       is not 4-line FASTQ fails (multi-line records,
- *                       FASTA); it is never parsed on the host.
+ *                       trailing '\r' dropped as kseq drops it.  Text whose
+ *                       first byte is '>' is 2-line FASTA (header, one
+ *                       sequence line; no quality section in its blocks,
+ *                       fqzcomp5.c:575-578, :2258-2264).  Other text fails
+ *                       (multi-line sequences); it is never parsed on the
+ *                       host.
  *   fqz5_fastq_blocks   the block split rule (fqzcomp5.c:471-479): a record
  *                       that would take a non-empty block past blk_size
  *                       (name.l + 1 + seq.l + qual.l per record) starts the
@@ -18,10 +21,12 @@
  *                       record lengths and READ2 flags (host).
  *   fqz5_fastq_format   output_fastq (fqzcomp5.c:3441-3480) of a decoded
  *                       block: '@' name '\n' seq '\n' '+' [name] '\n'
- *                       qual + 33 '\n'.
+ *                       qual + 33 '\n'; without qualities output_fasta
+ *                       (:3503-3517): '>' name '\n' seq '\n'.
  *
- * Offsets are bytes into the text.  Calls return 0 (fqz5_fastq_blocks: the
- * block count) or -1 with fqz5_last_error() set.
+ * Offsets are bytes into the text.  Calls return 0 (fqz5_fastq_index: 1 for
+ * FASTA text; fqz5_fastq_blocks: the block count) or -1 with
+ * fqz5_last_error() set.
  */
 #ifndef FQZ5_FASTQ_H
 #define FQZ5_FASTQ_H
@@ -35,7 +40,7 @@ extern "C" {
 typedef struct {                  /* one record of the text */
     uint64_t name, comment, seq, qual;        /* offsets */
     uint32_t name_len, comment_len, seq_len;  /* kseq's name.l, comment.l, seq.l */
-    uint32_t pad;
+    uint32_t fasta;                           /* 1: no quality line (qual 0) */
 } fqz5_fastq_rec;
 
 /* Index the records of d_text[0..len) (device) into d_recs (device, max_rec
@@ -51,8 +56,8 @@ int fqz5_fastq_blocks(const uint32_t *rec_size, uint64_t nrec, uint32_t blk_size
                       uint64_t *first, int max_blocks);
 
 /* Records [a, b) as one block.  sizes[3] receives the bytes of the names,
- * bases and qualities; with d_names / d_seq / d_qual NULL only the sizes
- * are computed.  h_len / h_flag (host, b - a entries, may be NULL): record
+ * bases and qualities; with d_names / d_seq NULL only the sizes are
+ * computed; d_qual NULL (FASTA): no qualities (sizes[2] = 0).  h_len / h_flag (host, b - a entries, may be NULL): record
  * lengths and FQZ5 READ2 flags (fqzcomp5.c:518-527). */
 int fqz5_fastq_gather(const uint8_t *d_text, const fqz5_fastq_rec *d_recs, uint64_t a,
                       uint64_t b, uint8_t *d_names, uint8_t *d_seq, uint8_t *d_qual,
@@ -60,7 +65,7 @@ int fqz5_fastq_gather(const uint8_t *d_text, const fqz5_fastq_rec *d_recs, uint6
 
 /* FASTQ text of a block (names '\0' after each, bases, qualities - 33 on
  * the device; lengths on the host) into d_out (out_cap bytes); *out_len its
- * size.  d_out NULL: the size only. */
+ * size.  d_qual NULL: FASTA text.  d_out NULL: the size only. */
 int fqz5_fastq_format(const uint8_t *d_names, uint64_t name_len, const uint8_t *d_seq,
                       const uint8_t *d_qual, const uint32_t *h_len, uint64_t nrec,
                       int plus_name, uint8_t *d_out, uint64_t out_cap, uint64_t *out_len);

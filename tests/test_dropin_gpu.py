@@ -32,7 +32,8 @@ def _need():
 
 def _inputs(tmp):
     ins = [os.path.join(HERE, "golden", "fastq", f)
-           for f in ("regression_srr1238539.fastq", "paired_R1_nosuffix.fastq")]
+           for f in ("regression_srr1238539.fastq", "paired_R1_nosuffix.fastq",
+                     "sample.fasta")]
     syn = os.path.join(tmp, "synthetic.fastq")
     with open(syn, "wb") as f:
         f.write(synth.illumina(8000, seed=11, with_names=True).to_fastq())

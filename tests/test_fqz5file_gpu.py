@@ -86,8 +86,44 @@ def test_not_4line_fastq_fails_loudly():
     bad = b"@r1\nACGT\nACGT\n+\nIIIIIIII\n"            # a two-line sequence
     with pytest.raises(lib.NativeError):
         fqz5file.compress_bytes(bad, 3)
-    with pytest.raises(lib.NativeError):
-        fqz5file.compress_bytes(b">r1\nACGT\n", 3)   # FASTA
+    with pytest.raises(lib.NativeError):                  # multi-line FASTA
+        fqz5file.compress_bytes(b">r1\nACGT\nACGT\n>r2\nAC\n", 3)
+    with pytest.raises(lib.NativeError):                  # FASTQ record in FASTA text
+        fqz5file.compress_bytes(b">r1\nACGT\n@r2\nAC\n+\nII\n", 3)
+
+
+FASTA = [os.path.join(HERE, "golden", "fastq", f) for f in ("sample.fasta", "paired_R1.fasta")]
+
+
+def _fasta_text(r) -> bytes:
+    """2-line FASTA of synthetic reads: '>' name [' ' comment] '\n' seq '\n'."""
+    text = synth.fastq_chunk(r, 0, r.num_records).tobytes().split(b"\n")
+    out = []
+    for k in range(0, len(text) - 1, 4):
+        out += [b">" + text[k][1:], text[k + 1]]
+    return b"\n".join(out) + b"\n"
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="oracle/_ref not built")
+@pytest.mark.parametrize("level", [1, 3, 5, 7])
+def test_fasta_vs_cli(tmp_path, level):
+    """FASTA input (the reference's test.sh:359-390 group, its test_data
+    FASTA files and a synthetic multi-block file): blocks without a quality
+    section (9 zero bytes, fqzcomp5.c:2258-2264) equal the CLI's, and the
+    decode writes output_fasta's text (:3503-3517)."""
+    syn = str(tmp_path / "syn.fasta")
+    open(syn, "wb").write(_fasta_text(synth.illumina(30000, seed=41, with_names=True)))
+    for src in FASTA + [syn]:
+        text = open(src, "rb").read()
+        blk = "1M" if src == syn else None
+        want = _ref(str(tmp_path), src, level, blk)
+        got = fqz5file.compress_bytes(text, level, blk_size=1_000_000 if blk else None)
+        assert got == want, (src, level, len(got), len(want))
+        assert fqz5file.decompress_bytes(want) == text
+        back = str(tmp_path / "back.fasta")
+        subprocess.run([CLI, "-d", str(tmp_path / "ref.fqz5"), back], check=True,
+                       capture_output=True, timeout=600)
+        assert open(back, "rb").read() == text
 
 
 def test_empty_input():
