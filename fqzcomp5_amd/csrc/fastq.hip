@@ -6,13 +6,13 @@
 // :3503-3517) on decoded blocks.
 //
 // Lines: every '\n' of the text is found by 64 KiB tiles (counts, a scan,
-// then ordered writes), so record r is lines 4r..4r+3 (FASTQ) or 2r, 2r+1
-// (FASTA: text whose first byte is '>', one sequence line per record; the
-// block then has no quality section, fqzcomp5.c:575-578, :2258-2264).
-// Records are parsed one per thread; the section bytes are gathered one wave
-// per record at the scanned offsets.  Text that is neither 4-line FASTQ nor
-// 2-line FASTA (multi-line sequences) is refused with an error, never parsed
-// on the host.
+// then ordered writes), so FASTQ record r is lines 4r..4r+3.  FASTA (text
+// whose first byte is '>'): a record per header line, its sequence lines
+// joined as kseq joins them; the block then has no quality section
+// (fqzcomp5.c:575-578, :2258-2264).  Records are parsed one per thread (FASTA:
+// one wave); the section bytes are gathered one wave per record at the
+// scanned offsets.  FASTQ that is not 4-line (multi-line records) is refused
+// with an error, never parsed on the host.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -96,42 +96,108 @@ __device__ __forceinline__ uint64_t strip_cr(const uint8_t *t, uint64_t s, uint6
     return (e - s > 1 && t[e - 1] == '\r') ? e - 1 : e;
 }
 
-// record r = lines 4r..4r+3, or 2r..2r+1 for FASTA (kseq_read, kseq.h:178-218)
-template <int LPR>
-__global__ void k_fq_records(const uint8_t *t, const uint64_t *nl, uint64_t nrec,
-                             fqz5_fastq_rec *recs, uint32_t *rec_size, int32_t *status) {
-    const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (r >= nrec) return;
-    const uint64_t s0 = r ? nl[LPR * r - 1] + 1 : 0, e0 = nl[LPR * r];
-    const uint64_t s1 = e0 + 1, e1 = nl[LPR * r + 1];
-    int bad = 0;
-    if (e0 <= s0 || t[s0] != (LPR == 4 ? '@' : '>')) bad = 1;   // header
-    if (e1 > s1 && (t[s1] == '@' || t[s1] == '>' || t[s1] == '+')) bad = 1;
-    // name up to the first isspace(), the comment after it to the line end
+// the header line [s0, e0): name up to the first isspace(), the comment
+// after it to the line end (kseq.h:188-189)
+__device__ __forceinline__ void header(const uint8_t *t, uint64_t s0, uint64_t e0, fqz5_fastq_rec &R) {
     uint64_t p = s0 + 1;
     while (p < e0 && !ks_space(t[p])) p++;
-    fqz5_fastq_rec R;
     R.name = s0 + 1;
     R.name_len = uint32_t(p - (s0 + 1));
     R.comment = p < e0 ? p + 1 : e0;
     R.comment_len = p < e0 ? uint32_t(strip_cr(t, p + 1, e0) - (p + 1)) : 0u;
+}
+
+// record r = lines 4r..4r+3 (kseq_read, kseq.h:178-218)
+__global__ void k_fq_records(const uint8_t *t, const uint64_t *nl, uint64_t nrec,
+                             fqz5_fastq_rec *recs, uint32_t *rec_size, int32_t *status) {
+    const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    const uint64_t s0 = r ? nl[4 * r - 1] + 1 : 0, e0 = nl[4 * r];
+    const uint64_t s1 = e0 + 1, e1 = nl[4 * r + 1];
+    const uint64_t s2 = e1 + 1, e2 = nl[4 * r + 2];
+    const uint64_t s3 = e2 + 1, e3 = nl[4 * r + 3];
+    int bad = 0;
+    if (e0 <= s0 || t[s0] != '@') bad = 1;            // header
+    if (e2 <= s2 || t[s2] != '+') bad = 1;            // '+' line
+    if (e1 > s1 && (t[s1] == '@' || t[s1] == '>' || t[s1] == '+')) bad = 1;
+    fqz5_fastq_rec R;
+    header(t, s0, e0, R);
     R.seq = s1;
     R.seq_len = uint32_t(strip_cr(t, s1, e1) - s1);
-    R.fasta = LPR == 2;
-    R.qual = 0;
-    uint32_t ql = 0;
-    if (LPR == 4) {
-        const uint64_t s2 = e1 + 1, e2 = nl[LPR * r + 2];
-        const uint64_t s3 = e2 + 1, e3 = nl[LPR * r + 3];
-        if (e2 <= s2 || t[s2] != '+') bad = 1;        // '+' line
-        R.qual = s3;
-        ql = uint32_t(strip_cr(t, s3, e3) - s3);
-        if (ql != R.seq_len) bad = 1;                 // kseq -2 (:213-216)
-    }
+    R.qual = s3;
+    R.fasta = 0;
+    const uint32_t ql = uint32_t(strip_cr(t, s3, e3) - s3);
+    if (ql != R.seq_len) bad = 1;                     // kseq -2 (:213-216)
     recs[r] = R;
-    // load_seqs_kseq's record_size name.l + 1 + seq.l + qual.l (:472)
-    rec_size[r] = R.name_len + 1 + R.seq_len + ql;
+    rec_size[r] = R.name_len + 1 + 2 * R.seq_len;     // load_seqs_kseq's record_size (:472)
     if (bad) atomicMin(status, int32_t(-1 - int32_t(r < 0x7ffffffeull ? r : 0x7ffffffeull)));
+}
+
+// FASTA lines: a header starts with '>'; a line starting with '@' or '+'
+// would make kseq read a FASTQ record (kseq.h:194, :206) and is refused, as
+// is text whose first line is not a header
+__global__ void k_fa_lines(const uint8_t *t, const uint64_t *nl, uint64_t nlines, uint32_t *hdr,
+                           int32_t *status) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= nlines) return;
+    const uint64_t s = i ? nl[i - 1] + 1 : 0, e = nl[i];
+    const uint8_t c = e > s ? t[s] : uint8_t('\n');
+    hdr[i] = c == '>';
+    if (c == '@' || c == '+' || (i == 0 && c != '>'))
+        atomicMin(status, int32_t(-1 - int32_t(i < 0x7ffffffeull ? i : 0x7ffffffeull)));
+}
+
+__global__ void k_fa_scatter(const uint32_t *hdr, const uint32_t *pos, uint64_t nlines, uint64_t *hl) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < nlines && hdr[i]) hl[pos[i]] = i;
+}
+
+// kseq's FASTA sequence over text [sb, se) (kseq.h:194-198): every line's
+// bytes joined, empty lines skipped, a '\r' before a line end dropped unless
+// it would be the sequence's only byte (the KS_SEP_LINE strip, :141, tests
+// the whole sequence's length).  One wave: returns the byte count and, with
+// `out`, writes the bytes.
+__device__ uint32_t fa_seq(const uint8_t *t, uint64_t sb, uint64_t se, uint8_t *out) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t n = 0;
+    bool any = false;                                 // a non-'\n' byte before
+    for (uint64_t base = sb; base < se; base += 64) {
+        const uint64_t p = base + lane;
+        const uint8_t c = p < se ? t[p] : uint8_t('\n');
+        const uint64_t nonl = __builtin_amdgcn_ballot_w64(c != '\n');
+        const uint64_t below = (lane ? (~0ull >> (64 - lane)) : 0ull);
+        const bool before = any || (nonl & below) != 0;
+        bool keep = c != '\n';
+        if (c == '\r' && (p + 1 == se || t[p + 1] == '\n') && before) keep = false;
+        const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
+        if (keep && out) out[n + __builtin_popcountll(km & below)] = c;
+        n += uint32_t(__builtin_popcountll(km));
+        any = any || nonl != 0;
+    }
+    return n;
+}
+
+// one wave per FASTA record: header line hl[r], its sequence up to the next
+// header (or the text end); R.qual holds that end offset
+__global__ void k_fa_records(const uint8_t *t, uint64_t len, const uint64_t *nl, const uint64_t *hl,
+                             uint64_t nrec, fqz5_fastq_rec *recs, uint32_t *rec_size) {
+    const uint64_t r = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+    if (r >= nrec) return;
+    const uint64_t h = hl[r];
+    const uint64_t s0 = h ? nl[h - 1] + 1 : 0, e0 = nl[h];
+    const uint64_t sb = e0 + 1 < len ? e0 + 1 : len;
+    const uint64_t se = r + 1 < nrec ? nl[hl[r + 1] - 1] + 1 : len;
+    const uint32_t n = fa_seq(t, sb, se, nullptr);
+    if ((threadIdx.x & 63) == 0) {
+        fqz5_fastq_rec R;
+        header(t, s0, e0, R);
+        R.seq = sb;
+        R.qual = se;
+        R.seq_len = n;
+        R.fasta = 1;
+        recs[r] = R;
+        rec_size[r] = R.name_len + 1 + n;             // qual.l = 0 (:472)
+    }
 }
 
 // per record of [a, b): name bytes (name [' ' comment] '\0') and bases
@@ -163,10 +229,14 @@ __global__ void k_fq_gather(const uint8_t *t, const fqz5_fastq_rec *recs, uint64
     }
     if (lane == 0) o[w] = 0;
     uint8_t *so = seq + soff[k];
-    for (uint32_t i = lane; i < R.seq_len; i += 64) so[i] = t[R.seq + i];
-    if (qual && !R.fasta) {
-        uint8_t *qo = qual + soff[k];
-        for (uint32_t i = lane; i < R.seq_len; i += 64) qo[i] = uint8_t(t[R.qual + i] - 33);
+    if (R.fasta) {                                    // lines joined (fa_seq)
+        fa_seq(t, R.seq, R.qual, so);
+        return;
+    }
+    uint8_t *qo = qual + soff[k];
+    for (uint32_t i = lane; i < R.seq_len; i += 64) {
+        so[i] = t[R.seq + i];
+        qo[i] = uint8_t(t[R.qual + i] - 33);
     }
 }
 
@@ -292,7 +362,6 @@ int fqz5_fastq_index(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs
         if (len) g.download(&first_byte, d_text, 1);
         g.sync();
         const bool fasta = first_byte == '>';
-        const uint64_t lpr = fasta ? 2 : 4;
         uint64_t *lines = nl;
         uint64_t nlines = nn;
         if (len && last != '\n') {
@@ -304,32 +373,55 @@ int fqz5_fastq_index(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs
             FQZ5_HIP(hipMemcpyAsync(lines + nn, st, 8, hipMemcpyHostToDevice, g.stream));
             nlines = nn + 1;
         }
-        // trailing empty lines (kseq skips to the next header) are ignored
-        uint64_t n4 = nlines / lpr;
-        if (nlines % lpr) {
-            std::vector<uint64_t> tail(size_t(nlines % lpr) + 1);
-            const uint64_t first = n4 * lpr;
-            g.download(tail.data() + 1, lines + first, nlines - first);
-            if (first) g.download(tail.data(), lines + first - 1, 1);
-            g.sync();
-            uint64_t prev = first ? tail[0] : uint64_t(-1);
-            for (uint64_t k = 1; k <= nlines - first; k++) {
-                if (tail[k] != prev + 1) throw GpuError(fasta ? "fasta: not 2-line FASTA (multi-line sequences or stray lines)"
-                                     : "fastq: not 4-line FASTQ (stray lines at the end)");
-                prev = tail[k];
-            }
-        }
-        if (n4 > max_rec) throw GpuError("fastq: more records than max_rec");
         int32_t *st = g.arena.alloc_n<int32_t>(1);
         const int32_t ok = 0;
-        uint32_t *rs = g.arena.alloc_n<uint32_t>(size_t(n4) + 1);
         FQZ5_HIP(hipMemcpyAsync(st, &ok, 4, hipMemcpyHostToDevice, g.stream));
-        if (n4 && fasta)
-            hipLaunchKernelGGL(k_fq_records<2>, grid_for(n4, 256), dim3(256), 0, g.stream, d_text, lines,
-                               n4, d_recs, rs, st);
-        else if (n4)
-            hipLaunchKernelGGL(k_fq_records<4>, grid_for(n4, 256), dim3(256), 0, g.stream, d_text, lines,
-                               n4, d_recs, rs, st);
+        uint64_t n4 = 0;
+        uint32_t *rs = nullptr;
+        if (fasta) {
+            // records = header lines (any number of sequence lines each)
+            uint32_t *hdr = g.arena.alloc_n<uint32_t>(size_t(nlines) + 1);
+            uint32_t *pos = g.arena.alloc_n<uint32_t>(size_t(nlines) + 1);
+            if (nlines >= (1ull << 31)) throw GpuError("fasta: too many lines");
+            if (nlines)
+                hipLaunchKernelGGL(k_fa_lines, grid_for(nlines, 256), dim3(256), 0, g.stream, d_text, lines,
+                                   nlines, hdr, st);
+            g.memset0(hdr + nlines, 4);
+            excl_sum(g, hdr, pos, nlines + 1);
+            uint32_t nh = 0;
+            g.download(&nh, pos + nlines, 1);
+            g.sync();
+            n4 = nh;
+            if (n4 > max_rec) throw GpuError("fastq: more records than max_rec");
+            uint64_t *hl = g.arena.alloc_n<uint64_t>(size_t(n4) + 1);
+            rs = g.arena.alloc_n<uint32_t>(size_t(n4) + 1);
+            if (nlines)
+                hipLaunchKernelGGL(k_fa_scatter, grid_for(nlines, 256), dim3(256), 0, g.stream, hdr, pos,
+                                   nlines, hl);
+            if (n4)
+                hipLaunchKernelGGL(k_fa_records, grid_for(n4 * 64, 256), dim3(256), 0, g.stream, d_text,
+                                   len, lines, hl, n4, d_recs, rs);
+        } else {
+            // trailing empty lines (kseq skips to the next header) are ignored
+            n4 = nlines / 4;
+            if (nlines % 4) {
+                std::vector<uint64_t> tail(size_t(nlines % 4) + 1);
+                const uint64_t first = n4 * 4;
+                g.download(tail.data() + 1, lines + first, nlines - first);
+                if (first) g.download(tail.data(), lines + first - 1, 1);
+                g.sync();
+                uint64_t prev = first ? tail[0] : uint64_t(-1);
+                for (uint64_t k = 1; k <= nlines - first; k++) {
+                    if (tail[k] != prev + 1) throw GpuError("fastq: not 4-line FASTQ (stray lines at the end)");
+                    prev = tail[k];
+                }
+            }
+            if (n4 > max_rec) throw GpuError("fastq: more records than max_rec");
+            rs = g.arena.alloc_n<uint32_t>(size_t(n4) + 1);
+            if (n4)
+                hipLaunchKernelGGL(k_fq_records, grid_for(n4, 256), dim3(256), 0, g.stream, d_text, lines,
+                                   n4, d_recs, rs, st);
+        }
         FQZ5_HIP(hipGetLastError());
         int32_t status = 0;
         g.download(&status, st, 1);
@@ -337,7 +429,7 @@ int fqz5_fastq_index(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs
         g.sync();
         if (status < 0) {
             char msg[128];
-            std::snprintf(msg, sizeof msg, fasta ? "fasta: record %lld is not a 2-line FASTA record"
+            std::snprintf(msg, sizeof msg, fasta ? "fasta: line %lld starts a FASTQ record or precedes the first header"
                                                  : "fastq: record %lld is not a 4-line FASTQ record",
                           static_cast<long long>(-1 - int64_t(status)));
             throw GpuError(msg);

@@ -15,10 +15,11 @@ offset, u32 bases, u32 records}.  Encoding follows a single-threaded (-t1)
 reference run: the codec trial runs over the blocks in file order, so the
 file equals the reference CLI's `-<level> -t1` output byte for byte.
 
-Scope: 4-line FASTQ and 2-line FASTA (text starting with '>': blocks without
-a quality section, decoded to output_fasta's text, fqzcomp5.c:2258-2264,
-:3503-3517); the parser refuses multi-line records with an error (there is
-no host parse); files that fit in device memory.
+Scope: 4-line FASTQ and FASTA with any line wrapping (text starting with
+'>': blocks without a quality section, decoded to output_fasta's one-line
+text, fqzcomp5.c:2258-2264, :3503-3517); the parser refuses multi-line FASTQ
+records with an error (there is no host parse); files that fit in device
+memory.
 """
 from __future__ import annotations
 
@@ -78,8 +79,9 @@ def parse_fastq(text_d, blk_size: int):
     import torch
     so = _load()
     n = int(text_d.numel())
-    # records <= lines / 4, FASTA lines / 2 (+1 for a last line without '\n')
-    lpr = 2 if n and int(text_d[0].item()) == ord(">") else 4
+    # records <= lines / 4, FASTA records <= lines (+1 for a last line
+    # without '\n')
+    lpr = 1 if n and int(text_d[0].item()) == ord(">") else 4
     max_rec = (int((text_d == 10).sum().item()) + 1) // lpr + 1 if n else 1
     recs = torch.empty(max_rec * C.sizeof(FastqRec), dtype=torch.uint8, device=text_d.device)
     rsz = np.zeros(max_rec, np.uint32)

@@ -7,11 +7,11 @@
  *                       first isspace(), comment to the line end, one
  *                       sequence line, '+' line, one quality line, a
  *                       trailing '\r' dropped as kseq drops it.  Text whose
- *                       first byte is '>' is 2-line FASTA (header, one
- *                       sequence line; no quality section in its blocks,
+ *                       first byte is '>' is FASTA: a record per header
+ *                       line, its sequence lines joined as kseq joins them
+ *                       (kseq.h:194-198; no quality section in its blocks,
  *                       fqzcomp5.c:575-578, :2258-2264).  Other text fails
- *                       (multi-line sequences); it is never parsed on the
- *                       host.
+ *                       (multi-line FASTQ); it is never parsed on the host.
  *   fqz5_fastq_blocks   the block split rule (fqzcomp5.c:471-479): a record
  *                       that would take a non-empty block past blk_size
  *                       (name.l + 1 + seq.l + qual.l per record) starts the
@@ -40,7 +40,8 @@ extern "C" {
 typedef struct {                  /* one record of the text */
     uint64_t name, comment, seq, qual;        /* offsets */
     uint32_t name_len, comment_len, seq_len;  /* kseq's name.l, comment.l, seq.l */
-    uint32_t fasta;                           /* 1: no quality line (qual 0) */
+    uint32_t fasta;                           /* 1: FASTA, its sequence lines
+                                                 in [seq, qual) */
 } fqz5_fastq_rec;
 
 /* Index the records of d_text[0..len) (device) into d_recs (device, max_rec
