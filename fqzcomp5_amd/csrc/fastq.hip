@@ -510,9 +510,9 @@ int fqz5_fastq_gather(const uint8_t *d_text, const fqz5_fastq_rec *d_recs, uint6
     }
 }
 
-int fqz5_fastq_format(const uint8_t *d_names, uint64_t name_len, const uint8_t *d_seq,
-                      const uint8_t *d_qual, const uint32_t *h_len, uint64_t nrec, int plus_name,
-                      uint8_t *d_out, uint64_t out_cap, uint64_t *out_len) {
+static int format_impl(const uint8_t *d_names, uint64_t name_len, const uint8_t *d_seq,
+                       const uint8_t *d_qual, const uint32_t *h_len, uint64_t nrec, int plus_name,
+                       uint8_t *d_out, uint64_t out_cap, uint64_t *out_len, uint64_t *r1_len) {
     GpuCtx *gp = nullptr;
     try {
         GpuCtx &g = gpu();
@@ -533,6 +533,20 @@ int fqz5_fastq_format(const uint8_t *d_names, uint64_t name_len, const uint8_t *
             s += h_len[k];
             prev = hz[k];
         }
+        if (r1_len) {
+            // output_fastq_deinterleaved (fqzcomp5.c:3612-3676): even records
+            // to the first text, odd ones to the second, placed after it
+            uint64_t t1 = 0;
+            for (uint64_t k = 0; k < nrec; k += 2) t1 += (k + 1 < nrec ? ooff[k + 1] : o) - ooff[k];
+            uint64_t o1 = 0, o2 = t1;
+            for (uint64_t k = 0; k < nrec; k++) {
+                const uint64_t sz = (k + 1 < nrec ? ooff[k + 1] : o) - ooff[k];
+                uint64_t &w = (k & 1) ? o2 : o1;
+                ooff[k] = w;
+                w += sz;
+            }
+            *r1_len = t1;
+        }
         *out_len = o;
         if (!d_out) { g.reset(); return 0; }
         if (o > out_cap) throw GpuError("fastq_format: output larger than out_cap");
@@ -550,6 +564,22 @@ int fqz5_fastq_format(const uint8_t *d_names, uint64_t name_len, const uint8_t *
         try { if (gp) gp->reset(); } catch (...) {}
         return -1;
     }
+}
+
+int fqz5_fastq_format(const uint8_t *d_names, uint64_t name_len, const uint8_t *d_seq,
+                      const uint8_t *d_qual, const uint32_t *h_len, uint64_t nrec, int plus_name,
+                      uint8_t *d_out, uint64_t out_cap, uint64_t *out_len) {
+    return format_impl(d_names, name_len, d_seq, d_qual, h_len, nrec, plus_name, d_out, out_cap,
+                       out_len, nullptr);
+}
+
+int fqz5_fastq_format_pairs(const uint8_t *d_names, uint64_t name_len, const uint8_t *d_seq,
+                            const uint8_t *d_qual, const uint32_t *h_len, uint64_t nrec,
+                            int plus_name, uint8_t *d_out, uint64_t out_cap, uint64_t *out_len,
+                            uint64_t *r1_len) {
+    uint64_t dummy = 0;
+    return format_impl(d_names, name_len, d_seq, d_qual, h_len, nrec, plus_name, d_out, out_cap,
+                       out_len, r1_len ? r1_len : &dummy);
 }
 
 }  // extern "C"

@@ -1,13 +1,17 @@
 """FASTQ file <-> .fqz5 file on the GPU: the container
 fqzcomp5 writes, produced and read by this library alone.
 
-    compress_file(src, dst, level)   FASTQ text -> HBM -> fqz5_fastq_index /
+    compress_file(src, dst, level[, src2=])  FASTQ text -> HBM -> fqz5_fastq_index /
                                      blocks / gather (fastq.hip) -> the
                                      section coder with the level's trial
                                      (sections.encode_run) -> whole blocks
                                      (fqz5_blocks_assemble) -> file
-    decompress_file(src, dst)        file -> HBM -> fqz5_block_parse ->
+    decompress_file(src, dst[, dst2=])  file -> HBM -> fqz5_block_parse ->
                                      sections decoded -> fqz5_fastq_format
+                                     (_pairs: deinterleaved to two files)
+    compress_paired_bytes / decompress_paired_bytes: the same for R1/R2
+    pairs (encode_interleaved / decode_deinterleaved, fqzcomp5.c:3211,
+    :4049): records interleaved R1, R2, R1, ... with READ2 on the R2 ones.
 
 File layout (fqzcomp5.c:2563-2630, :2959-2969): "FQZ5\\1\\1\\0\\0", u64 index
 offset, the blocks, then "FQZ5IDX\\0", u32 nblocks and per block {u64 file
@@ -62,6 +66,9 @@ def _load():
         so.fqz5_fastq_format.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                          C.c_void_p, C.c_uint64, C.c_int, C.c_void_p,
                                          C.c_uint64, C.POINTER(C.c_uint64)]
+        so.fqz5_fastq_format_pairs.restype = C.c_int
+        so.fqz5_fastq_format_pairs.argtypes = so.fqz5_fastq_format.argtypes + [
+            C.POINTER(C.c_uint64)]
         _bound = True
     return so
 
@@ -72,27 +79,35 @@ def _check(rc, what):
     return rc
 
 
-def parse_fastq(text_d, blk_size: int):
-    """FASTQ (or 2-line FASTA) text (a device uint8 tensor) -> a
-    sections.Run of its blocks, every section input gathered in HBM.  FASTA
-    blocks have no quality section (fqzcomp5.c:2237-2264)."""
+def _index_text(text_d, at: int, n: int):
+    """fqz5_fastq_index of text_d[at:at+n]: (records as bytes on the
+    device, their load_seqs_kseq sizes, count, is FASTA)."""
     import torch
     so = _load()
-    n = int(text_d.numel())
+    part = text_d[at:at + n]
     # records <= lines / 4, FASTA records <= lines (+1 for a last line
     # without '\n')
-    lpr = 1 if n and int(text_d[0].item()) == ord(">") else 4
-    max_rec = (int((text_d == 10).sum().item()) + 1) // lpr + 1 if n else 1
+    lpr = 1 if n and int(part[0].item()) == ord(">") else 4
+    max_rec = (int((part == 10).sum().item()) + 1) // lpr + 1 if n else 1
     recs = torch.empty(max_rec * C.sizeof(FastqRec), dtype=torch.uint8, device=text_d.device)
     rsz = np.zeros(max_rec, np.uint32)
     nrec = C.c_uint64(0)
-    fasta = _check(so.fqz5_fastq_index(text_d.data_ptr(), n, recs.data_ptr(), max_rec,
+    fasta = _check(so.fqz5_fastq_index(text_d.data_ptr() + at, n, recs.data_ptr(), max_rec,
                                        C.byref(nrec), rsz.ctypes.data), "fqz5_fastq_index") == 1
     nrec = int(nrec.value)
-    max_blocks = nrec + 1
-    first = np.zeros(max_blocks + 1, np.uint64)
-    nb = _check(so.fqz5_fastq_blocks(rsz.ctypes.data, nrec, blk_size, first.ctypes.data,
-                                     max_blocks), "fqz5_fastq_blocks")
+    if at and nrec:                     # offsets into the whole text
+        v = recs[:nrec * C.sizeof(FastqRec)].view(torch.int64).view(nrec, -1)
+        v[:, :4] += at
+    return recs[:nrec * C.sizeof(FastqRec)], rsz[:nrec], nrec, fasta
+
+
+def _gather(text_d, recs, first, fasta: bool, pair_flags: bool):
+    """The blocks [first[k], first[k+1]) of the records as a sections.Run,
+    every section input gathered in HBM.  pair_flags: READ2 on the odd
+    records (load_seqs_interleaved, fqzcomp5.c:763) instead of from the names."""
+    import torch
+    so = _load()
+    nb = len(first) - 1
     sizes = []
     for k in range(nb):
         sz = (C.c_uint64 * 3)()
@@ -117,14 +132,62 @@ def parse_fastq(text_d, blk_size: int):
                                     None if fasta else qual_d.data_ptr() + so_, ln.ctypes.data,
                                     fl.ctypes.data, sz),
                "fqz5_fastq_gather")
+        if pair_flags:
+            fl[:] = 0
+            fl[1::2] = 128                  # FQZ_FREAD2
         lens.append(ln[:b - a])
         flags.append(fl[:b - a])
         nr.append((no, no + sizes[k][0]))
         sr.append((so_, so_ + sizes[k][1]))
         no += sizes[k][0]
         so_ += sizes[k][1]
-    del recs
     return S.Run.from_device(name_d, seq_d, qual_d, nr, sr, lens, flags)
+
+
+def _blocks(so, sizes: np.ndarray, blk_size: int) -> np.ndarray:
+    n = len(sizes)
+    first = np.zeros(n + 2, np.uint64)
+    sz = np.ascontiguousarray(sizes, np.uint32)
+    nb = _check(so.fqz5_fastq_blocks(sz.ctypes.data, n, blk_size, first.ctypes.data, n + 1),
+                "fqz5_fastq_blocks")
+    return first[:nb + 1]
+
+
+def parse_fastq(text_d, blk_size: int):
+    """FASTQ (or FASTA) text (a device uint8 tensor) -> a sections.Run of
+    its blocks, every section input gathered in HBM.  FASTA blocks have no
+    quality section (fqzcomp5.c:2237-2264)."""
+    so = _load()
+    recs, rsz, nrec, fasta = _index_text(text_d, 0, int(text_d.numel()))
+    run = _gather(text_d, recs, _blocks(so, rsz, blk_size), fasta, False)
+    del recs
+    return run
+
+
+def parse_paired(text_d, len1: int, blk_size: int):
+    """Two files' text in one device buffer (R1 in [0, len1), R2 after it)
+    -> the Run of their interleaved records (load_seqs_interleaved,
+    fqzcomp5.c:627-848): records R1[0], R2[0], R1[1], ...; a block ends
+    before the pair that would take it past blk_size; READ2 on R2 records.
+    R2 ending before R1 is an error; R2 records past R1's end are not read."""
+    import torch
+    so = _load()
+    r1, rs1, n1, fa1 = _index_text(text_d, 0, len1)
+    r2, rs2, n2, fa2 = _index_text(text_d, len1, int(text_d.numel()) - len1)
+    if n2 < n1:
+        raise _lib.NativeError("unpaired read detected: R2 file ended before R1")
+    if n1 and fa1 != fa2:
+        raise _lib.NativeError("paired files: one FASTA, one FASTQ")
+    w = C.sizeof(FastqRec)
+    recs = torch.stack([r1.view(n1, w), r2[:n1 * w].view(n1, w)], 1).reshape(-1) if n1 else r1
+    del r1, r2
+    pair = rs1.astype(np.uint64) + rs2[:n1].astype(np.uint64)
+    if n1 and int(pair.max()) >= 2 ** 32:
+        raise _lib.NativeError("paired record larger than 4 GB")
+    first = _blocks(so, pair.astype(np.uint32), blk_size) * 2
+    run = _gather(text_d, recs, first, fa1, True)
+    del recs
+    return run
 
 
 def container(blocks: list[bytes], bases: list[int], nrec: list[int]) -> bytes:
@@ -164,10 +227,11 @@ def _read_pinned(path: str):
     return buf
 
 
-def _encode(text_d, level: int, blk_size: int | None):
-    """FASTQ text in HBM -> (the Run holding the encoded blocks, bases, records)."""
+def _encode(text_d, level: int, blk_size: int | None, len1: int | None = None):
+    """FASTQ text in HBM -> (the Run holding the encoded blocks, bases,
+    records); with len1, the paired files R1 = text_d[:len1], R2 after it."""
     blk = blk_size or S.BLOCK_SIZE[level]
-    run = parse_fastq(text_d, blk)
+    run = parse_fastq(text_d, blk) if len1 is None else parse_paired(text_d, len1, blk)
     if not run.blocks:
         return None, [], []
     res, *_ = S.encode_run(run.enc_secs(), S.masks(level, full=True), S.new_state())
@@ -196,15 +260,43 @@ def compress_bytes(text: bytes, level: int = 3, blk_size: int | None = None,
     return container(blocks, bases, nrec)
 
 
+def compress_paired_bytes(text1: bytes, text2: bytes, level: int = 3,
+                          blk_size: int | None = None, device: str = "cuda") -> bytes:
+    """fqzcomp5 -<level> in1 in2 out (-t1 semantics): the two files'
+    records interleaved (encode_interleaved, fqzcomp5.c:3211-3440)."""
+    import torch
+    both = text1 + text2
+    text_d = torch.frombuffer(bytearray(both), dtype=torch.uint8).to(device) if both else \
+        torch.empty(0, dtype=torch.uint8, device=device)
+    run, bases, nrec = _encode(text_d, level, blk_size, len(text1))
+    del text_d
+    if run is None:
+        return container([], [], [])
+    return container([run.block_bytes(b) for b in range(len(run.blocks))], bases, nrec)
+
+
 def compress_file(src: str, dst: str, level: int = 3, blk_size: int | None = None,
-                  device: str = "cuda") -> int:
+                  device: str = "cuda", src2: str | None = None) -> int:
     """The file path without host copies of the data: the FASTQ read into
     page-locked memory, one copy to HBM, the encoded blocks back in one copy
-    and written behind the header, then the index."""
+    and written behind the header, then the index.  src2: the R2 file of a
+    pair, interleaved with src (fqzcomp5 in1 in2 out)."""
+    import torch
     # a blocking copy: the library's kernels run on its own streams, which
     # do not wait for torch's (a non-blocking copy raced the FASTQ parse)
-    text_d = _read_pinned(src).to(device)
-    run, bases, nrec = _encode(text_d, level, blk_size)
+    len1 = None
+    if src2 is None:
+        text_d = _read_pinned(src).to(device)
+    else:
+        a, b = _read_pinned(src), _read_pinned(src2)
+        len1 = a.numel()
+        text_d = torch.empty(max(a.numel() + b.numel(), 1), dtype=torch.uint8,
+                             device=device)[:a.numel() + b.numel()]
+        text_d[:len1].copy_(a)
+        text_d[len1:].copy_(b)
+        torch.cuda.synchronize(text_d.device)
+        del a, b
+    run, bases, nrec = _encode(text_d, level, blk_size, len1)
     del text_d
     if run is None:
         out = container([], [], [])
@@ -239,9 +331,11 @@ def _blocks_of(data):
     return out
 
 
-def _decode(data, buf, plus_name: bool, device: str):
+def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False):
     """Blocks of a .fqz5 (host view `data`, device copy `buf`) -> the FASTQ
-    text of every block in one device buffer."""
+    text of every block in one device buffer; pairs: (the R1 text, the R2
+    text) of output_fastq_deinterleaved (fqzcomp5.c:3612-3676), even records
+    of every block to R1 and odd ones to R2."""
     import torch
     so = _load()
     ranges = _blocks_of(data)
@@ -287,23 +381,34 @@ def _decode(data, buf, plus_name: bool, device: str):
     if any(r.status != 0 for r in res):
         raise _lib.NativeError("section decoding failed: " + _lib.last_error())
     # the text of every block, one after the other in one device buffer
-    args, sizes = [], []
+    fmt = so.fqz5_fastq_format_pairs if pairs else so.fqz5_fastq_format
+    args, sizes, r1 = [], [], []
     for v, ln, po in zip(views, lens, places):
-        size = C.c_uint64(0)
+        size, s1 = C.c_uint64(0), C.c_uint64(0)
         a = (out_d.data_ptr() + po[0], v.name_ulen, out_d.data_ptr() + po[1],
              None if fasta[0] else out_d.data_ptr() + po[2], ln.ctypes.data, len(ln),
              int(plus_name))
-        _check(so.fqz5_fastq_format(*a, None, 0, C.byref(size)), "fqz5_fastq_format")
+        _check(fmt(*a, None, 0, C.byref(size), *((C.byref(s1),) if pairs else ())),
+               "fqz5_fastq_format")
         args.append(a)
         sizes.append(int(size.value))
+        r1.append(int(s1.value))
     text = torch.empty(max(sum(sizes), 1), dtype=torch.uint8, device=device)
     at = 0
     for a, n in zip(args, sizes):
-        size = C.c_uint64(0)
-        _check(so.fqz5_fastq_format(*a, text.data_ptr() + at, n, C.byref(size)),
-               "fqz5_fastq_format")
+        size, s1 = C.c_uint64(0), C.c_uint64(0)
+        _check(fmt(*a, text.data_ptr() + at, n, C.byref(size),
+                   *((C.byref(s1),) if pairs else ())), "fqz5_fastq_format")
         at += n
-    return text[:at]
+    if not pairs:
+        return text[:at]
+    idx1, idx2, at = [], [], 0
+    for n, k in zip(sizes, r1):
+        idx1.append((at, at + k))
+        idx2.append((at + k, at + n))
+        at += n
+    cat = lambda rs: torch.cat([text[a:b] for a, b in rs]) if rs else text[:0]
+    return cat(idx1), cat(idx2)
 
 
 def decompress_bytes(data: bytes, plus_name: bool = False, device: str = "cuda") -> bytes:
@@ -316,18 +421,38 @@ def decompress_bytes(data: bytes, plus_name: bool = False, device: str = "cuda")
     return _decode(data, buf, plus_name, device).cpu().numpy().tobytes()
 
 
-def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "cuda") -> int:
+def decompress_paired_bytes(data: bytes, plus_name: bool = False,
+                            device: str = "cuda") -> tuple[bytes, bytes]:
+    """fqzcomp5 -d in out1 out2: the records deinterleaved into R1 / R2."""
+    import torch
+    if not _blocks_of(data):
+        return b"", b""
+    buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(device)
+    t1, t2 = _decode(data, buf, plus_name, device, pairs=True)
+    return t1.cpu().numpy().tobytes(), t2.cpu().numpy().tobytes()
+
+
+def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "cuda",
+                    dst2: str | None = None) -> int:
     """The file path: the .fqz5 read into page-locked memory, one copy to
-    HBM, the FASTQ text back in one copy and written."""
+    HBM, the FASTQ text back in one copy and written.  dst2: deinterleave,
+    R1 records to dst and R2 records to dst2 (fqzcomp5 -d in out1 out2)."""
     host = _read_pinned(src)
     hv = host.numpy()
     if not _blocks_of(hv):
-        open(dst, "wb").close()
+        for d in (dst, dst2):
+            if d is not None:
+                open(d, "wb").close()
         return 0
     buf = host.to(device)     # blocking: block parsing runs on the library's streams
-    text = _decode(hv, buf, plus_name, device)
-    out = _pinned(int(text.numel()))
-    out.copy_(text)
-    with open(dst, "wb") as f:
-        f.write(memoryview(out.numpy()))
-    return int(text.numel())
+    texts = _decode(hv, buf, plus_name, device, pairs=dst2 is not None)
+    if dst2 is None:
+        texts = (texts,)
+    total = 0
+    for text, d in zip(texts, (dst, dst2)):
+        out = _pinned(int(text.numel()))
+        out.copy_(text)
+        with open(d, "wb") as f:
+            f.write(memoryview(out.numpy()))
+        total += int(text.numel())
+    return total

@@ -19,7 +19,7 @@
  *   fqz5_fastq_gather   one block's section inputs: names (name [' '
  *                       comment] '\0'), bases, qualities - 33 (device), the
  *                       record lengths and READ2 flags (host).
- *   fqz5_fastq_format   output_fastq (fqzcomp5.c:3441-3480) of a decoded
+ *   fqz5_fastq_format(_pairs) output_fastq (fqzcomp5.c:3441-3480) of a decoded
  *                       block: '@' name '\n' seq '\n' '+' [name] '\n'
  *                       qual + 33 '\n'; without qualities output_fasta
  *                       (:3503-3517): '>' name '\n' seq '\n'.
@@ -70,6 +70,15 @@ int fqz5_fastq_gather(const uint8_t *d_text, const fqz5_fastq_rec *d_recs, uint6
 int fqz5_fastq_format(const uint8_t *d_names, uint64_t name_len, const uint8_t *d_seq,
                       const uint8_t *d_qual, const uint32_t *h_len, uint64_t nrec,
                       int plus_name, uint8_t *d_out, uint64_t out_cap, uint64_t *out_len);
+
+/* Paired output (fqzcomp5 -d in out1 out2: output_fastq_deinterleaved /
+ * output_fasta_deinterleaved, fqzcomp5.c:3535-3549, :3612-3676): as
+ * fqz5_fastq_format, the block's even records (R1) first and its odd
+ * records (R2) after them; *r1_len the first text's size. */
+int fqz5_fastq_format_pairs(const uint8_t *d_names, uint64_t name_len, const uint8_t *d_seq,
+                            const uint8_t *d_qual, const uint32_t *h_len, uint64_t nrec,
+                            int plus_name, uint8_t *d_out, uint64_t out_cap, uint64_t *out_len,
+                            uint64_t *r1_len);
 
 #ifdef __cplusplus
 }

@@ -205,3 +205,61 @@ def test_file_path_large_roundtrip(tmp_path):
     assert fqz5file.decompress_file(dst, back) == n_in
     with open(back, "rb") as a, open(src, "rb") as b:
         assert a.read() == b.read()
+
+
+PAIRS = [tuple(os.path.join(HERE, "golden", "fastq", f) for f in p) for p in
+         (("sample_R1.fastq", "sample_R2.fastq"),
+          ("paired_R1_nosuffix.fastq", "paired_R2_nosuffix.fastq"),
+          ("paired_R1.fasta", "paired_R2.fasta"))]
+
+
+def _ref_pair(tmp, s1, s2, level, blk=None):
+    out = os.path.join(tmp, "ref.fqz5")
+    cmd = [CLI, f"-{level}", "-t1"] + (["-b", blk] if blk else []) + [s1, s2, out]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=600)
+    o1, o2 = os.path.join(tmp, "ref_1"), os.path.join(tmp, "ref_2")
+    subprocess.run([CLI, "-d", out, o1, o2], check=True, capture_output=True, timeout=600)
+    return open(out, "rb").read(), open(o1, "rb").read(), open(o2, "rb").read()
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="oracle/_ref not built")
+@pytest.mark.parametrize("level", [1, 3, 5])
+def test_paired_vs_cli(tmp_path, level):
+    """Two files interleaved (fqzcomp5 -<level> in1 in2 out: load_seqs_interleaved,
+    fqzcomp5.c:627-848, pair-wise block split, READ2 on R2 records) equal the
+    CLI's file, and the deinterleaving decode (fqzcomp5 -d in out1 out2,
+    :3612-3676) gives the CLI's two files: the reference's paired fixtures
+    (FASTQ and FASTA), a synthetic multi-block pair, and an R2 file longer
+    than R1 (its extra records are not read)."""
+    r = synth.illumina(20000, seed=45, with_names=True)
+    text = synth.fastq_chunk(r, 0, r.num_records).tobytes().split(b"\n")
+    recs = [b"\n".join(text[k:k + 4]) + b"\n" for k in range(0, len(text) - 1, 4)]
+    s1, s2 = str(tmp_path / "syn_1.fastq"), str(tmp_path / "syn_2.fastq")
+    open(s1, "wb").write(b"".join(recs[0::2]))
+    open(s2, "wb").write(b"".join(recs[1::2]) + recs[0])
+    for a, b in PAIRS + [(s1, s2)]:
+        blk = "1M" if a == s1 else None
+        want, w1, w2 = _ref_pair(str(tmp_path), a, b, level, blk)
+        got = fqz5file.compress_paired_bytes(open(a, "rb").read(), open(b, "rb").read(), level,
+                                             blk_size=1_000_000 if blk else None)
+        assert got == want, (a, level, len(got), len(want))
+        assert fqz5file.decompress_paired_bytes(want) == (w1, w2)
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="oracle/_ref not built")
+def test_paired_file_path(tmp_path):
+    a, b = PAIRS[1]
+    want, w1, w2 = _ref_pair(str(tmp_path), a, b, 3)
+    dst = str(tmp_path / "g.fqz5")
+    fqz5file.compress_file(a, dst, 3, src2=b)
+    assert open(dst, "rb").read() == want
+    o1, o2 = str(tmp_path / "g_1"), str(tmp_path / "g_2")
+    assert fqz5file.decompress_file(dst, o1, dst2=o2) == len(w1) + len(w2)
+    assert open(o1, "rb").read() == w1 and open(o2, "rb").read() == w2
+
+
+def test_paired_r2_short_fails_loudly():
+    r1 = b"@a/1\nACGT\n+\nIIII\n@b/1\nACGT\n+\nIIII\n"
+    r2 = b"@a/2\nACGT\n+\nIIII\n"
+    with pytest.raises(lib.NativeError):
+        fqz5file.compress_paired_bytes(r1, r2, 3)
