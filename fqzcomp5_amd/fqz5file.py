@@ -212,8 +212,22 @@ def _pinned(n: int):
 
 
 def _read_pinned(path: str):
-    """The file's bytes in page-locked host memory (one read, no copy)."""
+    """The file's bytes in page-locked host memory (one read, no copy).  A
+    gzip file (the reference reads every input through zlib's gzopen,
+    fqzcomp5.c:5075-5110) is inflated on the host first: zlib's stream
+    format is serial and stays host I/O; the FASTQ text is still parsed on
+    the GPU only."""
     import os
+    with open(path, "rb") as f:
+        magic = f.read(2)
+    if magic == b"\x1f\x8b":
+        import gzip
+        with open(path, "rb") as f:
+            raw = gzip.decompress(f.read())
+        buf = _pinned(len(raw))
+        if raw:
+            buf.numpy()[:] = np.frombuffer(raw, np.uint8)
+        return buf
     n = os.path.getsize(path)
     buf = _pinned(n)
     mv = memoryview(buf.numpy())
@@ -442,7 +456,7 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
     if not _blocks_of(hv):
         for d in (dst, dst2):
             if d is not None:
-                open(d, "wb").close()
+                _write_out(d, b"")
         return 0
     buf = host.to(device)     # blocking: block parsing runs on the library's streams
     texts = _decode(hv, buf, plus_name, device, pairs=dst2 is not None)
@@ -452,7 +466,18 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
     for text, d in zip(texts, (dst, dst2)):
         out = _pinned(int(text.numel()))
         out.copy_(text)
-        with open(d, "wb") as f:
-            f.write(memoryview(out.numpy()))
+        _write_out(d, memoryview(out.numpy()))
         total += int(text.numel())
     return total
+
+
+def _write_out(path: str, data) -> None:
+    """Decoded text to `path`; gzip-compressed when the name ends in ".gz"
+    (gzopen(name, "wb"), zlib's default level, fqzcomp5.c:5113-5160)."""
+    if path.endswith(".gz"):
+        import gzip
+        with gzip.open(path, "wb", compresslevel=6) as f:
+            f.write(data)
+    else:
+        with open(path, "wb") as f:
+            f.write(data)

@@ -263,3 +263,22 @@ def test_paired_r2_short_fails_loudly():
     r2 = b"@a/2\nACGT\n+\nIIII\n"
     with pytest.raises(lib.NativeError):
         fqz5file.compress_paired_bytes(r1, r2, 3)
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="oracle/_ref not built")
+def test_gzip_io(tmp_path):
+    """gzip input is read through zlib as the reference's gzopen does, and a
+    ".gz" output name writes gzip (fqzcomp5.c:5075-5160): the .fqz5 equals the
+    CLI's from the same gzip file, the gzip output inflates to the input."""
+    import gzip
+    text = open(GOLD[2], "rb").read()
+    src = str(tmp_path / "in.fastq.gz")
+    with gzip.open(src, "wb") as f:
+        f.write(text)
+    want = _ref(str(tmp_path), src, 3)
+    dst = str(tmp_path / "g.fqz5")
+    fqz5file.compress_file(src, dst, 3)
+    assert open(dst, "rb").read() == want
+    back = str(tmp_path / "back.fastq.gz")
+    assert fqz5file.decompress_file(dst, back) == len(text)
+    assert gzip.decompress(open(back, "rb").read()) == text
