@@ -282,3 +282,21 @@ def test_gzip_io(tmp_path):
     back = str(tmp_path / "back.fastq.gz")
     assert fqz5file.decompress_file(dst, back) == len(text)
     assert gzip.decompress(open(back, "rb").read()) == text
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="oracle/_ref not built")
+def test_plus_name_vs_cli(tmp_path):
+    """fqzcomp5 -d -p: the name repeated on the '+' line (output_fastq,
+    fqzcomp5.c:3441-3500; deinterleaved :3612-3676), single and paired."""
+    a, b = PAIRS[0]
+    z1 = _ref(str(tmp_path), GOLD[1], 3)
+    out = str(tmp_path / "p.fastq")
+    subprocess.run([CLI, "-d", "-p", str(tmp_path / "ref.fqz5"), out], check=True,
+                   capture_output=True, timeout=600)
+    assert fqz5file.decompress_bytes(z1, plus_name=True) == open(out, "rb").read()
+    zp, _, _ = _ref_pair(str(tmp_path), a, b, 3)
+    o1, o2 = str(tmp_path / "p_1"), str(tmp_path / "p_2")
+    subprocess.run([CLI, "-d", "-p", str(tmp_path / "ref.fqz5"), o1, o2], check=True,
+                   capture_output=True, timeout=600)
+    assert fqz5file.decompress_paired_bytes(zp, plus_name=True) == \
+        (open(o1, "rb").read(), open(o2, "rb").read())
