@@ -93,3 +93,46 @@ def test_container_framing_vs_cli(tmp_path):
     for a, b in synth.split_blocks(r, 1_000_000):
         bases.append(int(r.lens[a:b].sum()))
     assert fqz5file.container(blocks, bases, nrec) == data
+
+
+def _pair_split_py(s1, s2, blk):
+    """load_seqs_interleaved's rule (fqzcomp5.c:703-711): a pair that would
+    take a non-empty block past blk starts the next one."""
+    out, a, tot = [], 0, 0
+    for k in range(len(s1)):
+        rs = int(s1[k]) + int(s2[k])
+        if tot > 0 and tot + rs > blk:
+            out.append((2 * a, 2 * k))
+            a, tot = k, 0
+        tot += rs
+    if len(s1):
+        out.append((2 * a, 2 * len(s1)))
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="oracle/_ref not built")
+def test_pair_split_vs_cli(tmp_path):
+    """The paired block split fqz5file.parse_paired uses (pair sizes through
+    fqz5_fastq_blocks, record indices doubled) against the restated rule and
+    against the records per block in the reference CLI's index for two files."""
+    so = fqz5file._load()
+    r = synth.illumina(12000, seed=5, with_names=True)
+    text = synth.fastq_chunk(r, 0, r.num_records).tobytes().split(b"\n")
+    recs = [b"\n".join(text[k:k + 4]) + b"\n" for k in range(0, len(text) - 1, 4)]
+    r1, r2 = recs[0::2], recs[1::2]
+    size = lambda rec: len(rec.split(b"\n")[0].split(b" ")[0]) + len(rec.split(b"\n")[1]) * 2
+    s1 = np.array([size(x) for x in r1], np.uint32)      # name.l + 1 + seq.l + qual.l
+    s2 = np.array([size(x) for x in r2], np.uint32)
+    blk = 1_000_000
+    first = fqz5file._blocks(so, (s1 + s2).astype(np.uint32), blk) * 2
+    got = [(int(first[k]), int(first[k + 1])) for k in range(len(first) - 1)]
+    assert got == _pair_split_py(s1, s2, blk) and len(got) > 1
+    a, b, out = str(tmp_path / "a.fq"), str(tmp_path / "b.fq"), str(tmp_path / "o.fqz5")
+    open(a, "wb").write(b"".join(r1))
+    open(b, "wb").write(b"".join(r2))
+    subprocess.run([CLI, "-1", "-t1", "-b", "1M", a, b, out], check=True, capture_output=True)
+    data = open(out, "rb").read()
+    (idx,) = struct.unpack_from("<Q", data, 8)
+    (n,) = struct.unpack_from("<I", data, idx + 8)
+    nrec = [struct.unpack_from("<QII", data, idx + 12 + 16 * k)[2] for k in range(n)]
+    assert nrec == [e - s for s, e in got]
