@@ -22,12 +22,18 @@ namespace fqz5 {
 // The trial's helper contexts (gpu_aux) each own streams that must run
 // beside the calling thread's; HIP's default of 4 hardware queues per
 // process makes them share queues and serialise.  Raise it when the process
-// (e.g. the relinked CLI) loads this library before anything touched HIP.
+// (e.g. the relinked CLI) loads this library before anything touched HIP:
+// FQZ5_HW_QUEUES, when set, is used as given (experiments, fewer queues
+// included); otherwise an unset GPU_MAX_HW_QUEUES or HIP's default of 4 is
+// raised to 32, and any other value the caller chose is kept.
 __attribute__((constructor)) static void hw_queues_default() {
     const char *v = std::getenv("GPU_MAX_HW_QUEUES");
-    const char *w = std::getenv("FQZ5_HW_QUEUES");          // experiments: fewer queues
-    const int want = w ? std::atoi(w) : 32;
-    if (!v || std::atoi(v) < want) setenv("GPU_MAX_HW_QUEUES", std::to_string(want).c_str(), 1);
+    const char *w = std::getenv("FQZ5_HW_QUEUES");
+    if (w) {
+        setenv("GPU_MAX_HW_QUEUES", w, 1);
+        return;
+    }
+    if (!v || !*v || std::atoi(v) == 4) setenv("GPU_MAX_HW_QUEUES", "32", 1);
 }
 
 static thread_local std::string g_err;

@@ -32,6 +32,9 @@
 #include "fqz_kernels.h"
 #include "fqz_model.hpp"
 
+// v_writelane_b32 (the LLVM intrinsic; this clang has no builtin for it)
+__device__ int amdgcn_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane");
+
 namespace fqz5 {
 namespace {
 
@@ -85,6 +88,7 @@ DEV uint32_t U(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 #define PROBE_OUT
 #endif
 DEV uint32_t RL(uint32_t v, uint32_t lane) { return __builtin_amdgcn_readlane(v, lane); }
+
 
 
 // ---------------------------------------------------------------------------
@@ -210,7 +214,7 @@ DEV PS load_ps(const FqzDevGlobal &g, uint32_t x) {
 DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     const uint32_t h = (ctx * 0x9E3779u) >> 8;                     // 24 bits
     const uint32_t set = uint32_t((uint64_t(h & 0xffffffu) * (ns8 & 0xffffffu)) >> 32);
-    return L_CACHE + __umul24(set, me);
+    return L_CACHE + (set & 0xffffu) * (me & 0xffffu);   // both < 2^16: v_mad_u32_u24
 }
 
 // ---------------------------------------------------------------------------
@@ -283,12 +287,6 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     uint32_t rlen = 0, sb0 = 0;               // record length, first staged base index
     uint32_t tpos = 0;                        // symbol index within the record
     const uint32_t dlane = L_DUMMY + 4 * l;
-    // lanes holding dwords 0 .. L+1 (write-back) and slots 0 .. L (ballot)
-    const uint32_t nd = L + 2;
-    const uint64_t wm0 = nd >= 64 ? ~0ull : ((1ull << nd) - 1);
-    const uint64_t wm1 = NE == 2 && nd > 64 ? (nd >= 128 ? ~0ull : ((1ull << (nd - 64)) - 1)) : 0ull;
-    const uint64_t lm0 = wm0 & ~1ull, lm1 = wm1;
-    const bool wr[2] = {l < nd, l + 64 < nd};
 
     auto flush = [&]() {
         for (uint32_t o = l * 4; o < fill; o += 256) {
@@ -330,18 +328,37 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         tpos++;
     };
 
-    // model registers
+    // model registers: lane dw of register r (dw = l + 64 r) holds dword dw
+    // of the cached model and the symbol byte of that slot.  Lanes past the
+    // sentinel read (and write back) the sentinel's own addresses, so every
+    // lane of the model registers is a valid slot, the tag, or a copy of the
+    // sentinel (cum = total): the decoder's ballot needs no lane mask.
     uint32_t v[NE], s[NE];
+    uint32_t voff[NE], sofs[NE];
+#pragma unroll
+    for (int r = 0; r < NE; r++) {
+        const uint32_t dw = l + 64 * r, c = dw < L + 1 ? dw : L + 1;
+        voff[r] = 4 * c;
+        sofs[r] = soff + c;
+    }
     auto rlane = [&](const uint32_t (&x)[NE], uint32_t dw) -> uint32_t {
         if (NE == 1) return RL(x[0], dw);
         const uint32_t a = RL(x[0], dw & 63u), b = RL(x[NE - 1], dw & 63u);
         return dw < 64 ? a : b;
     };
-    auto issue_model = [&]() {
+    auto issue_model_to = [&](uint32_t a, uint32_t (&mv)[NE], uint32_t (&ms)[NE]) {
 #pragma unroll
         for (int r = 0; r < NE; r++) {
-            v[r] = *reinterpret_cast<const uint32_t *>(lds + maddr + 4 * (l + 64 * r));
-            s[r] = lds[maddr + soff - 1 + l + 64 * r];
+            mv[r] = *reinterpret_cast<const uint32_t *>(lds + a + voff[r]);
+            ms[r] = lds[a + sofs[r]];
+        }
+    };
+    auto issue_model = [&]() { issue_model_to(maddr, v, s); };
+    auto write_model = [&](uint32_t a) {
+#pragma unroll
+        for (int r = 0; r < NE; r++) {
+            *reinterpret_cast<uint32_t *>(lds + a + voff[r]) = v[r];
+            lds[a + sofs[r]] = uint8_t(s[r]);
         }
     };
     // miss: write the resident model back to HBM, fetch or create ctx
@@ -363,9 +380,12 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         } else {
             for (uint32_t j = l; j <= L; j += 64) {   // slot j: freq 1 (live) or 0, cum j
                 m32[1 + j] = (j < L ? 1u : 0u) | (j << 16);
-                lds[maddr + soff + j] = uint8_t(j < L ? j : 0u);
+                lds[maddr + soff + 1 + j] = uint8_t(j < L ? j : 0u);
             }
-            if (l == 0) m32[0] = ctx;
+            if (l == 0) {
+                m32[0] = ctx;
+                lds[maddr + soff] = 0;
+            }
         }
         __builtin_amdgcn_wave_barrier();
     };
@@ -377,53 +397,50 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             miss(tag);
         }
     };
+    // halve every live slot (c_simple_model.h:106-115): prefix sums of the
+    // halved frequencies give the new cumulative counts
+    auto halve = [&]() {
+        uint32_t carry = 0;
+#pragma unroll
+        for (int r = 0; r < NE; r++) {
+            const uint32_t dw = l + 64 * r;
+            uint32_t f = dw >= 1 && dw <= L ? (v[r] & 0xffffu) : 0u;
+            f -= f >> 1;
+            uint32_t inc = f;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(inc, d, 64);
+                if (int(l) >= d) inc += o;
+            }
+            if (dw >= 1) v[r] = f | ((carry + inc - f) << 16);
+            carry += RL(inc, 63);
+        }
+    };
+    // one bubble step at lane kl >= 2 (the lanes of the registers only)
+    auto bubble = [&](uint32_t kl) {
+        const uint32_t ek = rlane(v, kl), ep = rlane(v, kl - 1);
+        const uint32_t fk = ek & 0xffffu, fp = ep & 0xffffu;
+        if (fk > fp) {
+            const uint32_t cp = ep >> 16;
+            const uint32_t sk = rlane(s, kl), sp = rlane(s, kl - 1);
+#pragma unroll
+            for (int r = 0; r < NE; r++) {
+                const uint32_t dw = l + 64 * r;
+                if (dw == kl - 1) { v[r] = fk | (cp << 16); s[r] = sk; }
+                if (dw == kl) { v[r] = fp | ((cp + fk) << 16); s[r] = sp; }
+            }
+        }
+    };
     // the list update after coding the slot in lane kl (fl_bump): +16,
-    // halve past FL_MAX, one bubble step; written back to the cache
+    // halve past FL_MAX, one bubble step (registers only)
     auto update = [&](uint32_t kl, uint32_t total) {
 #pragma unroll
         for (int r = 0; r < NE; r++) {
             const uint32_t dw = l + 64 * r;
             v[r] += dw > kl ? 0x100000u : (dw == kl ? FL_STEP : 0u);
         }
-        if (total + FL_STEP > FL_MAX) {
-            uint32_t carry = 0;
-#pragma unroll
-            for (int r = 0; r < NE; r++) {
-                const uint32_t dw = l + 64 * r;
-                uint32_t f = dw >= 1 && dw <= L ? (v[r] & 0xffffu) : 0u;
-                f -= f >> 1;
-                uint32_t inc = f;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t o = __shfl_up(inc, d, 64);
-                    if (int(l) >= d) inc += o;
-                }
-                if (dw >= 1) v[r] = f | ((carry + inc - f) << 16);
-                carry += RL(inc, 63);
-            }
-        }
-        if (kl >= 2) {
-            const uint32_t ek = rlane(v, kl), ep = rlane(v, kl - 1);
-            const uint32_t fk = ek & 0xffffu, fp = ep & 0xffffu;
-            if (fk > fp) {
-                const uint32_t cp = ep >> 16;
-                const uint32_t sk = rlane(s, kl), sp = rlane(s, kl - 1);
-#pragma unroll
-                for (int r = 0; r < NE; r++) {
-                    const uint32_t dw = l + 64 * r;
-                    if (dw == kl - 1) { v[r] = fk | (cp << 16); s[r] = sk; }
-                    if (dw == kl) { v[r] = fp | ((cp + fk) << 16); s[r] = sp; }
-                    if (dw == kl - 1 || dw == kl) lds[maddr + soff - 1 + dw] = uint8_t(s[r]);
-                }
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < NE; r++)
-            if (wr[r]) *reinterpret_cast<uint32_t *>(lds + maddr + 4 * (l + 64 * r)) = v[r];
-    };
-    auto put = [&](uint32_t sym) {
-        lds[l ? dlane : L_OBUF + fill] = uint8_t(sym);
-        fill++;
+        if (total + FL_STEP > FL_MAX) halve();
+        if (kl >= 2) bubble(kl);
     };
     // one symbol with the reference's arithmetic, any state (corrupt or
     // truncated streams, the last bytes of the input)
@@ -446,8 +463,10 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             renorm_slow(lds, in, rng, code);
             sym = rlane(s, kl);
             update(kl, total);
+            write_model(maddr);
         }
-        put(sym);
+        lds[l ? dlane : L_OBUF + fill] = uint8_t(sym);
+        fill++;
         next_uniform(sym);
     };
 
@@ -518,58 +537,72 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             if (SEQ && tpos - sb0 == SEQB) { sb0 = tpos; stage_seq(); }
             continue;
         }
-        // ---- fast loop: symbols of this record within the output page ------
+        // ---- fast run: up to 64 symbols of this record within the output
+        // page (and the staged bases); the model of the current context
+        // stays in registers while the context repeats --------------------
         uint32_t lim = left < OBUF - fill ? left : OBUF - fill;
+        if (lim > 64u) lim = 64u;
         if (SEQ && lim > SEQB - (tpos - sb0)) lim = SEQB - (tpos - sb0);
         uint32_t ulim = (in.vb - 4u) * 8u;
-        bool to_slow = false;
+        // per-step uniform context terms of the run (fqz_update_ctx uses the
+        // position and delta before this symbol's update): lane i the
+        // position term of step i, lane j the delta term of delta0 + j
+        const uint32_t delta0 = delta;
+        const uint32_t pvv = uint32_t(pt16[(P_PTAB >> 1) + (left - l < 1023u ? left - l : 1023u)]) + selterm;
+        const uint32_t dvv = pt16[(P_DTAB >> 1) + (delta + l < 255u ? delta + l : 255u)];
+        const uint32_t sqv = SEQ ? uint32_t(lds[L_SEQ + ((tpos - sb0 + l) & (SEQB - 1))]) : 0u;
+        uint32_t qs = qctx << ps.qshift;
+        const uint32_t qmask = ps.qmask, qshift = ps.qshift;
+        uint32_t vout = 0;
         uint32_t done = 0;
+        bool to_slow = false;
         PROBE_START
-        // the first step's reads: model dwords and symbols, the position
-        // and delta table entries (later steps read them at the end of the
-        // step before, or take the speculative read of slot 0's model)
-        issue_model();
-        uint32_t pv = pt16[(P_PTAB >> 1) + (left < 1023u ? left : 1023u)];
-        uint32_t dv = pt16[(P_DTAB >> 1) + (delta < 255u ? delta : 255u)];
+        load_model();
         do {
-            uint32_t sq = 0;
-            if (SEQ) sq = lds[L_SEQ + (tpos - sb0)];
-            asm volatile("" ::"v"(v[0]), "v"(s[0]), "v"(pv), "v"(dv), "v"(sq));
-            const uint32_t tag = RL(v[0], 0);
-            if (tag != ctx) {
-                miss(tag);
-                load_model();
-            }
             PROBE(0)
-            const uint32_t total = rlane(v, L + 1) >> 16;
-            const uint32_t q = quot(rng, recip(total));
+            uint32_t u = RL(pvv, done) + RL(dvv, delta - delta0);
             uint32_t seqn = 0;
-            if (SEQ) seqn = ((seq << 2) | U(sq)) & ((1u << ps.bbits) - 1u);
-            const uint32_t u = pv + dv + selterm + (seqn << ps.bloc);
-            const uint32_t qs = qctx << ps.qshift;
-            uint32_t qt[NE], an[NE], cn[NE], p[NE];
-            uint32_t cnt = 0;
+            if (SEQ) {
+                seqn = ((seq << 2) | RL(sqv, done)) & ((1u << ps.bbits) - 1u);
+                u += seqn << ps.bloc;
+            }
+            const uint32_t total = RL(v[NE - 1], 63) >> 16;
+            const uint32_t q = quot(rng, recip(total));
+            uint32_t p[NE];
+            bool gt[NE];
+            uint64_t G[NE];
 #pragma unroll
             for (int r = 0; r < NE; r++) {
-                qt[r] = QID ? s[r] : uint32_t(pt16[(P_QTAB >> 1) + s[r]]);
-                cn[r] = ((((qs + qt[r]) & ps.qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1);
-                an[r] = set_addr(cn[r], NS8, ME);
                 p[r] = (v[r] >> 16) * q;
+                gt[r] = p[r] > code;
+                G[r] = __builtin_amdgcn_ballot_w64(gt[r]);
             }
-#pragma unroll
-            for (int r = 0; r < NE; r++) {
-                const uint64_t bal = __builtin_amdgcn_ballot_w64(p[r] <= code) & (r == 0 ? lm0 : lm1);
-                cnt += __builtin_popcountll(bal);
-            }
-            const uint32_t kl = cnt;          // lane of the decoded slot (slot kl - 1)
+            // the next context of every slot of register 0 (lanes 0-63),
+            // its cache set, whether the set holds it, and the bubble test
+            const uint32_t qt = QID ? s[0] : uint32_t(pt16[(P_QTAB >> 1) + s[0]]);
+            const uint32_t qn = qs + qt;
+            const uint32_t cn = ((((qn & qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1));
+            const uint32_t an = set_addr(cn, NS8, ME);
+            const uint32_t tg = *reinterpret_cast<const uint32_t *>(lds + an);
+            const uint64_t H = __builtin_amdgcn_ballot_w64(tg == cn);
+            const uint32_t nx = an | (s[0] << 24);
+            const uint32_t qsn = qn << qshift;
+            const uint32_t fl = __builtin_amdgcn_update_dpp(0u, v[0], 0x138, 0xf, 0xf, false);   // wave_shr:1
+            const uint64_t SW = __builtin_amdgcn_ballot_w64((v[0] & 0xffffu) + FL_STEP > (fl & 0xffffu)) & ~3ull;
             PROBE(1)
-            if (kl > L) {   // t >= total or range < total: reference arithmetic
+            if (G[NE - 1] == 0) {   // t >= total: reference arithmetic
                 to_slow = true;
                 break;
             }
-            const uint32_t pk = rlane(p, kl), pk1 = rlane(p, kl + 1);
-            const uint32_t sym = rlane(s, kl);
-            const uint32_t qtk = rlane(qt, kl), cnk = rlane(cn, kl), ank = rlane(an, kl);
+            const uint32_t k1 = NE == 1 ? uint32_t(__builtin_ctzll(G[0]))
+                                        : (G[0] ? uint32_t(__builtin_ctzll(G[0])) : 64u + uint32_t(__builtin_ctzll(G[NE - 1])));
+            const uint32_t kl = k1 - 1;   // lane of the decoded slot
+            if (NE == 2 && kl >= 64) {   // slots past lane 63: reference arithmetic
+                to_slow = true;
+                break;
+            }
+            const uint32_t pk = rlane(p, kl), pk1 = rlane(p, k1);
+            const uint32_t nxk = RL(nx, kl), qsk = RL(qsn, kl);
             code -= pk;
             rng = pk1 - pk;
             const uint32_t z = uint32_t(__builtin_clz(rng)) & 24u;
@@ -578,17 +611,53 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             in.W <<= z;
             in.ub += z;
             PROBE(2)
-            update(kl, total);
+            const uint32_t ank = nxk & 0xffffffu, sym = nxk >> 24;
+            // the coded slot's update in registers (fl_bump): +16 to its
+            // frequency and to every later cum, halving past FL_MAX, one
+            // bubble step
+            auto bump = [&]() {
+#pragma unroll
+                for (int r = 0; r < NE; r++) {
+                    const uint32_t dw = l + 64 * r;
+                    v[r] += gt[r] ? 0x100000u : (dw == kl ? FL_STEP : 0u);
+                }
+                if (__builtin_expect(total + FL_STEP > FL_MAX, 0)) {
+                    halve();
+                    if (kl >= 2) bubble(kl);
+                } else if (__builtin_expect(uint32_t(SW >> kl) & 1u, 0)) {
+                    bubble(kl);
+                }
+            };
+            if (__builtin_expect(!((H >> kl) & 1u), 0)) {
+                // the next context is not cached: write back, fetch
+                bump();
+                write_model(maddr);
+                ctx = ((((qsk >> qshift) & qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1);
+                maddr = ank;
+                load_model();
+            } else if (ank != maddr) {
+                // another cached context: its read goes out first
+                uint32_t nv[NE], ns[NE];
+                issue_model_to(ank, nv, ns);
+                bump();
+                write_model(maddr);
+#pragma unroll
+                for (int r = 0; r < NE; r++) {
+                    v[r] = nv[r];
+                    s[r] = ns[r];
+                }
+                maddr = ank;
+            } else {
+                bump();   // the same context again: stays in registers
+            }
             PROBE(3)
-            put(sym);
-            qctx = qs + qtk;
+            vout = uint32_t(amdgcn_writelane(int(sym), int(done), int(vout)));
             delta += prevq != sym;
             prevq = sym;
+            qs = qsk;
             seq = seqn;
             left--;
             if (SEQ) tpos++;
-            ctx = cnk;
-            maddr = ank;
             done++;
             PROBE(4)
             if (in.ub > ulim) {
@@ -597,14 +666,17 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 ulim = (in.vb - 4u) * 8u;
             }
             if (done == lim) break;
-            // the next step's reads, in flight while the loop closes (a
-            // speculative read of slot 0's next model measured slower: the
-            // volatile loads that keep it in place are waited for at once)
-            issue_model();
-            pv = pt16[(P_PTAB >> 1) + (left < 1023u ? left : 1023u)];
-            dv = pt16[(P_DTAB >> 1) + (delta < 255u ? delta : 255u)];
             PROBE(5)
         } while (true);
+        write_model(maddr);
+        // the run's state back to the record: the context of the next
+        // symbol, its cache set, the output bytes
+        qctx = qs >> qshift;
+        if (done) {
+            ctx = RL(v[0], 0);   // the resident model is the next context's
+        }
+        if (l < done) lds[L_OBUF + fill + l] = uint8_t(vout);
+        fill += done;
         if (to_slow) slow_symbol();
         if (fill == OBUF) flush();
         if (SEQ && left && tpos - sb0 == SEQB) { sb0 = tpos; stage_seq(); }

@@ -83,9 +83,11 @@ struct FqzDecJob {
 
 // Bytes of one cached quality model for `live` symbols: the context tag,
 // live+1 entries freq | cum << 16 (the last one a sentinel with freq 0 and
-// cum = total), live+1 symbol bytes; 4-byte aligned.
+// cum = total), then a symbol byte per dword (lane) 0 .. live+1 (lane 0's
+// byte is padding, so that every lane of the decoder owns its own byte);
+// 4-byte aligned.
 constexpr uint32_t fqz_dec_model_bytes(uint32_t live) {
-    return (4u * (live + 2u) + (live + 1u) + 3u) & ~3u;
+    return (5u * (live + 2u) + 3u) & ~3u;
 }
 constexpr uint32_t FQZ_DEC_CACHE_BYTES = 163840u - 35088u - 1024u;
 constexpr uint32_t FQZ_DEC_MAX_LIVE = 126u;   // tag + entries in two lane registers

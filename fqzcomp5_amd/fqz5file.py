@@ -105,43 +105,8 @@ def _gather(text_d, recs, first, fasta: bool, pair_flags: bool):
     """The blocks [first[k], first[k+1]) of the records as a sections.Run,
     every section input gathered in HBM.  pair_flags: READ2 on the odd
     records (load_seqs_interleaved, fqzcomp5.c:763) instead of from the names."""
-    import torch
-    so = _load()
-    nb = len(first) - 1
-    sizes = []
-    for k in range(nb):
-        sz = (C.c_uint64 * 3)()
-        _check(so.fqz5_fastq_gather(text_d.data_ptr(), recs.data_ptr(), int(first[k]),
-                                    int(first[k + 1]), None, None, None, None, None, sz),
-               "fqz5_fastq_gather")
-        sizes.append((int(sz[0]), int(sz[1])))
-    tot_n = sum(a for a, _ in sizes)
-    tot_s = sum(b for _, b in sizes)
-    name_d = torch.empty(max(tot_n, 1), dtype=torch.uint8, device=text_d.device)
-    seq_d = torch.empty(max(tot_s, 1), dtype=torch.uint8, device=text_d.device)
-    qual_d = None if fasta else torch.empty(max(tot_s, 1), dtype=torch.uint8, device=text_d.device)
-    lens, flags, nr, sr = [], [], [], []
-    no = so_ = 0
-    for k in range(nb):
-        a, b = int(first[k]), int(first[k + 1])
-        ln = np.zeros(max(b - a, 1), np.uint32)
-        fl = np.zeros(max(b - a, 1), np.uint32)
-        sz = (C.c_uint64 * 3)()
-        _check(so.fqz5_fastq_gather(text_d.data_ptr(), recs.data_ptr(), a, b,
-                                    name_d.data_ptr() + no, seq_d.data_ptr() + so_,
-                                    None if fasta else qual_d.data_ptr() + so_, ln.ctypes.data,
-                                    fl.ctypes.data, sz),
-               "fqz5_fastq_gather")
-        if pair_flags:
-            fl[:] = 0
-            fl[1::2] = 128                  # FQZ_FREAD2
-        lens.append(ln[:b - a])
-        flags.append(fl[:b - a])
-        nr.append((no, no + sizes[k][0]))
-        sr.append((so_, so_ + sizes[k][1]))
-        no += sizes[k][0]
-        so_ += sizes[k][1]
-    return S.Run.from_device(name_d, seq_d, qual_d, nr, sr, lens, flags)
+    return _gather_ranges(text_d, recs, [(int(first[k]), int(first[k + 1]))
+                                         for k in range(len(first) - 1)], fasta, pair_flags)
 
 
 def _blocks(so, sizes: np.ndarray, blk_size: int) -> np.ndarray:
@@ -211,150 +176,480 @@ def _pinned(n: int):
     return torch.empty(max(n, 1), dtype=torch.uint8, pin_memory=True)[:n]
 
 
-def _read_pinned(path: str):
-    """The file's bytes in page-locked host memory (one read, no copy).  A
-    gzip file (the reference reads every input through zlib's gzopen,
-    fqzcomp5.c:5075-5110) is inflated on the host first: zlib's stream
-    format is serial and stays host I/O; the FASTQ text is still parsed on
-    the GPU only."""
-    import os
-    with open(path, "rb") as f:
-        magic = f.read(2)
-    if magic == b"\x1f\x8b":
-        import gzip
-        with open(path, "rb") as f:
-            raw = gzip.decompress(f.read())
-        buf = _pinned(len(raw))
-        if raw:
-            buf.numpy()[:] = np.frombuffer(raw, np.uint8)
-        return buf
-    n = os.path.getsize(path)
-    buf = _pinned(n)
-    mv = memoryview(buf.numpy())
-    with open(path, "rb", buffering=0) as f:
-        got = 0
-        while got < n:
-            k = f.readinto(mv[got:])
-            if not k:
-                raise OSError(f"{path}: short read")
-            got += k
-    return buf
-
-
-def _encode(text_d, level: int, blk_size: int | None, len1: int | None = None):
-    """FASTQ text in HBM -> (the Run holding the encoded blocks, bases,
-    records); with len1, the paired files R1 = text_d[:len1], R2 after it."""
-    blk = blk_size or S.BLOCK_SIZE[level]
-    run = parse_fastq(text_d, blk) if len1 is None else parse_paired(text_d, len1, blk)
-    if not run.blocks:
-        return None, [], []
-    res, *_ = S.encode_run(run.enc_secs(), S.masks(level, full=True), S.new_state())
-    if any(r.status != 0 for r in res):
-        raise _lib.NativeError("section coding failed: " + _lib.last_error())
-    run.assemble(res)
-    return run, [int(ln.sum()) for ln in run.lens], [len(ln) for ln in run.lens]
-
-
 def _index(offs, bases, nrec) -> bytes:
     return INDEX_MAGIC + struct.pack("<I", len(offs)) + b"".join(
         struct.pack("<QII", o, nb, nr) for o, nb, nr in zip(offs, bases, nrec))
 
 
-def compress_bytes(text: bytes, level: int = 3, blk_size: int | None = None,
-                   device: str = "cuda") -> bytes:
-    """fqzcomp5 -<level> (-t1 semantics) of FASTQ text, on the GPU."""
+# ---------------------------------------------------------------------------
+# streaming and multi-GPU encode
+#
+# The reference reads its input block by block (load_seqs_kseq per block,
+# fqzcomp5.c:3051, dispatched at :3077) and writes each block behind the
+# last, the index at the end (:3108-3115, write_index :2606).  Here the text
+# comes in windows of whole records (a FASTQ window ends after 4k lines, a
+# FASTA window before a header line); the last block of a window that is not
+# the end of the input may be incomplete, so it is not coded: the next window
+# starts at its first record.  The codec trial's state carries from window
+# to window, so the blocks and their methods are those of one pass over the
+# whole input.
+#
+# Over several ranks (group = a torch.distributed group, one process per
+# GPU), every rank reads and parses every window (the block split needs the
+# records in order), the window's blocks are split contiguously over the
+# ranks, each rank codes its own blocks and its share of the trial blocks'
+# work candidates (sections.encode_window), and the blocks are written with
+# positioned writes at offsets from an all-gather of the block sizes and an
+# exclusive scan; rank 0 writes the header and the index.
+# ---------------------------------------------------------------------------
+DEFAULT_WINDOW = 2_000_000_000
+
+
+class _Src:
+    """One input read sequentially (plain or gzip; a path or bytes), holding
+    the unread text from the start of the next window on."""
+
+    def __init__(self, path: str | None = None, data: bytes | None = None):
+        import gzip
+        import io
+        if data is not None:
+            self.f = io.BytesIO(data)
+        else:
+            with open(path, "rb") as f:
+                magic = f.read(2)
+            self.f = gzip.open(path, "rb") if magic == b"\x1f\x8b" else open(path, "rb")
+        self.buf = bytearray()
+        self.eof = False
+
+    def fill(self, want: int) -> None:
+        while len(self.buf) < want and not self.eof:
+            c = self.f.read(min(want - len(self.buf), 1 << 28))
+            if not c:
+                self.eof = True
+                break
+            self.buf += c
+
+    def advance(self, n: int) -> None:
+        del self.buf[:n]
+
+    def close(self) -> None:
+        self.f.close()
+
+
+class _Sink:
+    """Positioned writes into the output file (or a bytearray)."""
+
+    def __init__(self, path: str | None, create: bool):
+        import os
+        self.path, self.mem, self.fd = path, None, None
+        if path is None:
+            self.mem = bytearray()
+        else:
+            flags = os.O_WRONLY | (os.O_CREAT | os.O_TRUNC if create else 0)
+            self.fd = os.open(path, flags, 0o644)
+
+    def write_at(self, off: int, data) -> None:
+        import os
+        mv = memoryview(data).cast("B")
+        if self.mem is not None:
+            if len(self.mem) < off + len(mv):
+                self.mem.extend(b"\0" * (off + len(mv) - len(self.mem)))
+            self.mem[off:off + len(mv)] = mv
+            return
+        while len(mv):
+            k = os.pwrite(self.fd, mv, off)
+            mv, off = mv[k:], off + k
+
+    def close(self) -> None:
+        import os
+        if self.fd is not None:
+            os.close(self.fd)
+            self.fd = None
+
+
+def _allgather_obj(x, group):
+    import torch.distributed as dist
+    ws, _ = S._world(group)
+    if ws == 1:
+        return [x]
+    out = [None] * ws
+    dist.all_gather_object(out, x, group=group)
+    return out
+
+
+def _barrier(group):
+    import torch.distributed as dist
+    if S._world(group)[0] > 1:
+        dist.barrier(group=group)
+
+
+def _complete_records(text_d, n: int, eof: bool) -> tuple[list[int], bool]:
+    """Record ends of text_d[:n] (exclusive offsets, increasing) that are
+    known to be complete, and whether the text is FASTA.  FASTQ: after every
+    4th line; FASTA: before every header line after the first; at the end of
+    the input, the end of the text closes the last record."""
     import torch
-    text_d = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(device) if text else \
-        torch.empty(0, dtype=torch.uint8, device=device)
-    run, bases, nrec = _encode(text_d, level, blk_size)
-    del text_d
-    if run is None:
-        return container([], [], [])
-    blocks = [run.block_bytes(b) for b in range(len(run.blocks))]
-    return container(blocks, bases, nrec)
+    if n == 0:
+        return [], False
+    t = text_d[:n]
+    fasta = int(t[0].item()) == ord(">")
+    if fasta:
+        starts = ((t[1:] == ord(">")) & (t[:-1] == 10)).nonzero().flatten() + 1
+        ends = starts.cpu().tolist()
+    else:
+        nl = (t == 10).nonzero().flatten()
+        ends = (nl[3::4] + 1).cpu().tolist()
+    if eof and (not ends or ends[-1] != n):
+        ends.append(n)
+    del torch
+    return ends, fasta
+
+
+def _rec_start(recs, r: int) -> int:
+    """Text offset of record r's header line (its name field less one)."""
+    import torch
+    w = C.sizeof(FastqRec)
+    return int(recs[r * w:r * w + 8].view(torch.int64).item()) - 1
+
+
+class _Window:
+    """One window of the input, parsed: record table, block starts (records),
+    the blocks to code now, and the text to consume after them."""
+    pass
+
+
+def _next_window(srcs: list, blk: int, wbytes: int, device: str):
+    """Parse the next window of whole records from the source(s); returns a
+    _Window or None at the end of the input.  Grows the window until it holds
+    one complete block (or the rest of the input)."""
+    import torch
+    so = _load()
+    paired = len(srcs) == 2
+    want = wbytes
+    while True:
+        for s in srcs:
+            s.fill(want)
+        devs, ends = [], []
+        for s in srcs:
+            if s.buf:
+                cpu = torch.frombuffer(s.buf, dtype=torch.uint8)
+                d = cpu.to(device)            # blocking (pageable): done before the parse
+                del cpu
+            else:
+                d = torch.empty(0, dtype=torch.uint8, device=device)
+            devs.append(d)
+            ends.append(_complete_records(d, int(d.numel()), s.eof)[0])
+        k = min(len(e) for e in ends) if paired else len(ends[0])
+        r1_done = srcs[0].eof and k == len(ends[0])      # all of R1 in the window
+        if paired and not r1_done and srcs[1].eof and k == len(ends[1]):
+            raise _lib.NativeError("unpaired read detected: R2 file ended before R1")
+        if k == 0:
+            if r1_done:
+                return None
+            want *= 2
+            continue
+        cut = [e[k - 1] for e in ends]
+        if paired:
+            text_d = torch.cat([devs[0][:cut[0]], devs[1][:cut[1]]])
+            len1 = cut[0]
+        else:
+            text_d, len1 = devs[0][:cut[0]], None
+        del devs
+        if len1 is None:
+            recs, rsz, nrec, fasta = _index_text(text_d, 0, int(text_d.numel()))
+            first = _blocks(so, rsz, blk)
+        else:
+            r1, rs1, n1, fa1 = _index_text(text_d, 0, len1)
+            r2, rs2, n2, fa2 = _index_text(text_d, len1, int(text_d.numel()) - len1)
+            if n2 < n1:
+                raise _lib.NativeError("unpaired read detected: R2 file ended before R1")
+            if n1 and fa1 != fa2:
+                raise _lib.NativeError("paired files: one FASTA, one FASTQ")
+            w = C.sizeof(FastqRec)
+            recs = torch.stack([r1.view(n1, w), r2[:n1 * w].view(n1, w)], 1).reshape(-1) \
+                if n1 else r1
+            del r1, r2
+            pair = rs1.astype(np.uint64) + rs2[:n1].astype(np.uint64)
+            if n1 and int(pair.max()) >= 2 ** 32:
+                raise _lib.NativeError("paired record larger than 4 GB")
+            first = _blocks(so, pair.astype(np.uint32), blk) * 2
+            fasta = fa1
+        nb = len(first) - 1
+        keep = nb if r1_done else nb - 1
+        if keep <= 0:
+            want *= 2
+            continue
+        W = _Window()
+        W.text_d, W.recs, W.first, W.fasta, W.pairs = text_d, recs, first[:keep + 1], fasta, paired
+        if keep < nb:                          # the next window starts at block `keep`
+            r = int(first[keep])
+            W.consume = [_rec_start(recs, r)] + \
+                ([_rec_start(recs, r + 1) - len1] if paired else [])
+        else:
+            W.consume = [len(srcs[0].buf)] + ([len(srcs[1].buf)] if paired else [])
+        return W
+
+
+def _encode_stream(srcs: list, sink: _Sink, level: int, blk_size: int | None, device: str,
+                   group=None, window_bytes: int | None = None) -> int:
+    """The sources' FASTQ -> .fqz5 written through `sink` (see above);
+    returns the file size."""
+    import torch
+    so = _load()
+    ws, rk = S._world(group)
+    blk = blk_size or S.BLOCK_SIZE[level]
+    # a window holds several blocks per rank, so that every GPU has blocks
+    # whose serial chains run side by side
+    wbytes = window_bytes or max(DEFAULT_WINDOW, 2 * ws * blk + blk)
+    av = S.masks(level, full=True)
+    state = S.new_state()
+    pos = 16                                  # file offset of the next block
+    index = []
+    while True:
+        W = _next_window(srcs, blk, wbytes, device)
+        if W is None:
+            break
+        nb = len(W.first) - 1
+        # per block: its records, section input sizes (fqz5_fastq_gather's
+        # sizing pass), the sections in encode_block order
+        per = 2 if W.fasta else 3
+        ids, ins, bases, nrec = [], [], [], []
+        for b in range(nb):
+            a, e = int(W.first[b]), int(W.first[b + 1])
+            sz = (C.c_uint64 * 3)()
+            _check(so.fqz5_fastq_gather(W.text_d.data_ptr(), W.recs.data_ptr(), a, e, None,
+                                        None, None, None, None, sz), "fqz5_fastq_gather")
+            ids += [S.SEC_NAME, S.SEC_SEQ] + ([] if W.fasta else [S.SEC_QUAL])
+            ins += [int(sz[0]), int(sz[1])] + ([] if W.fasta else [int(sz[1])])
+            bases.append(int(sz[1]))
+            nrec.append(e - a)
+        ids = np.array(ids, np.int32)
+        ins = np.array(ins, np.uint32)
+        blk_owner = (np.arange(nb) * ws) // nb
+        owner = np.repeat(blk_owner, per)
+        sched = S.trial_schedule(ids, av, state)
+        need = sorted({b for b in range(nb) if blk_owner[b] == rk or sched[per * b:per * b + per].any()})
+        # the needed blocks' section inputs, gathered in HBM
+        run = _gather_ranges(W.text_d, W.recs, [(int(W.first[b]), int(W.first[b + 1]))
+                                                for b in need], W.fasta, W.pairs)
+        secs = [None] * (nb * per)
+        local = run.enc_secs()
+        for j, b in enumerate(need):
+            for q in range(per):
+                secs[per * b + q] = local[per * j + q]
+        res, meth, _ = S.encode_window(secs, ids, ins, owner, av, state, group,
+                                       bounded=level >= 7)
+        mine = [j for j, b in enumerate(need) if blk_owner[b] == rk]
+        full_res = [None] * (len(need) * per)
+        for j, b in enumerate(need):
+            for q in range(per):
+                full_res[per * j + q] = res[per * b + q]
+        for j in mine:
+            for q in range(per):
+                r = full_res[per * j + q]
+                if r is None or r.status != 0:
+                    raise _lib.NativeError("section coding failed: " + _lib.last_error())
+        sizes = []
+        if mine:
+            run.assemble(full_res, mine)
+            sizes = [int(run.blk_off[i + 1] - run.blk_off[i]) for i in range(len(mine))]
+        all_sizes = _allgather_obj(sizes, group)
+        # blocks in file order: rank-contiguous, so rank-major order
+        flat = [z for zs in all_sizes for z in zs]
+        assert len(flat) == nb
+        starts = np.concatenate([[0], np.cumsum(flat)]).astype(np.int64) + pos
+        if mine:
+            end = int(run.blk_off[len(mine)])
+            host = _pinned(end)
+            host.copy_(run.blk_buf[:end])
+            b0 = need[mine[0]]
+            sink.write_at(int(starts[b0]), host.numpy())
+            del host
+        for b in range(nb):
+            index.append((int(starts[b]), bases[b], nrec[b]))
+        pos = int(starts[-1])
+        for s, c in zip(srcs, W.consume):
+            s.advance(c)
+        del run, W
+    if rk == 0:
+        if index:
+            idx = _index([o for o, _, _ in index], [b for _, b, _ in index],
+                         [n for _, _, n in index])
+            sink.write_at(pos, idx)
+        else:
+            idx = b""
+        sink.write_at(0, MAGIC + struct.pack("<Q", pos))
+        total = pos + len(idx)
+    else:
+        total = 0
+    return int(_allgather_obj(total, group)[0])
+
+
+def _gather_ranges(text_d, recs, ranges, fasta: bool, pair_flags: bool):
+    """Blocks given as record ranges [a, b) (not necessarily adjacent) as a
+    sections.Run, every section input gathered in HBM."""
+    import torch
+    so = _load()
+    sizes = []
+    for a, b in ranges:
+        sz = (C.c_uint64 * 3)()
+        _check(so.fqz5_fastq_gather(text_d.data_ptr(), recs.data_ptr(), a, b, None, None, None,
+                                    None, None, sz), "fqz5_fastq_gather")
+        sizes.append((int(sz[0]), int(sz[1])))
+    tot_n = sum(a for a, _ in sizes)
+    tot_s = sum(b for _, b in sizes)
+    name_d = torch.empty(max(tot_n, 1), dtype=torch.uint8, device=text_d.device)
+    seq_d = torch.empty(max(tot_s, 1), dtype=torch.uint8, device=text_d.device)
+    qual_d = None if fasta else torch.empty(max(tot_s, 1), dtype=torch.uint8, device=text_d.device)
+    lens, flags, nr, sr = [], [], [], []
+    no = so_ = 0
+    for (a, b), (zn, zs) in zip(ranges, sizes):
+        ln = np.zeros(max(b - a, 1), np.uint32)
+        fl = np.zeros(max(b - a, 1), np.uint32)
+        sz = (C.c_uint64 * 3)()
+        _check(so.fqz5_fastq_gather(text_d.data_ptr(), recs.data_ptr(), a, b,
+                                    name_d.data_ptr() + no, seq_d.data_ptr() + so_,
+                                    None if fasta else qual_d.data_ptr() + so_, ln.ctypes.data,
+                                    fl.ctypes.data, sz),
+               "fqz5_fastq_gather")
+        if pair_flags:
+            fl[:] = 0
+            fl[1::2] = 128                  # FQZ_FREAD2 (a range starts at an R1 record)
+        lens.append(ln[:b - a])
+        flags.append(fl[:b - a])
+        nr.append((no, no + zn))
+        sr.append((so_, so_ + zs))
+        no += zn
+        so_ += zs
+    return S.Run.from_device(name_d, seq_d, qual_d, nr, sr, lens, flags)
+
+
+def compress_bytes(text: bytes, level: int = 3, blk_size: int | None = None,
+                   device: str = "cuda", window_bytes: int | None = None) -> bytes:
+    """fqzcomp5 -<level> (-t1 semantics) of FASTQ text, on the GPU."""
+    sink = _Sink(None, True)
+    _encode_stream([_Src(data=text)], sink, level, blk_size, device, None, window_bytes)
+    return bytes(sink.mem)
 
 
 def compress_paired_bytes(text1: bytes, text2: bytes, level: int = 3,
-                          blk_size: int | None = None, device: str = "cuda") -> bytes:
+                          blk_size: int | None = None, device: str = "cuda",
+                          window_bytes: int | None = None) -> bytes:
     """fqzcomp5 -<level> in1 in2 out (-t1 semantics): the two files'
     records interleaved (encode_interleaved, fqzcomp5.c:3211-3440)."""
-    import torch
-    both = text1 + text2
-    text_d = torch.frombuffer(bytearray(both), dtype=torch.uint8).to(device) if both else \
-        torch.empty(0, dtype=torch.uint8, device=device)
-    run, bases, nrec = _encode(text_d, level, blk_size, len(text1))
-    del text_d
-    if run is None:
-        return container([], [], [])
-    return container([run.block_bytes(b) for b in range(len(run.blocks))], bases, nrec)
+    sink = _Sink(None, True)
+    _encode_stream([_Src(data=text1), _Src(data=text2)], sink, level, blk_size, device, None,
+                   window_bytes)
+    return bytes(sink.mem)
 
 
 def compress_file(src: str, dst: str, level: int = 3, blk_size: int | None = None,
-                  device: str = "cuda", src2: str | None = None) -> int:
-    """The file path without host copies of the data: the FASTQ read into
-    page-locked memory, one copy to HBM, the encoded blocks back in one copy
-    and written behind the header, then the index.  src2: the R2 file of a
-    pair, interleaved with src (fqzcomp5 in1 in2 out)."""
-    import torch
-    # a blocking copy: the library's kernels run on its own streams, which
-    # do not wait for torch's (a non-blocking copy raced the FASTQ parse)
-    len1 = None
-    if src2 is None:
-        text_d = _read_pinned(src).to(device)
-    else:
-        a, b = _read_pinned(src), _read_pinned(src2)
-        len1 = a.numel()
-        text_d = torch.empty(max(a.numel() + b.numel(), 1), dtype=torch.uint8,
-                             device=device)[:a.numel() + b.numel()]
-        text_d[:len1].copy_(a)
-        text_d[len1:].copy_(b)
-        torch.cuda.synchronize(text_d.device)
-        del a, b
-    run, bases, nrec = _encode(text_d, level, blk_size, len1)
-    del text_d
-    if run is None:
-        out = container([], [], [])
-        with open(dst, "wb") as f:
-            f.write(out)
-        return len(out)
-    end = int(run.blk_off[-1])
-    host = _pinned(end)
-    host.copy_(run.blk_buf[:end])
-    offs = [16 + int(run.blk_off[b]) for b in range(len(run.blocks))]
-    idx = _index(offs, bases, nrec)
-    with open(dst, "wb") as f:
-        f.write(MAGIC + struct.pack("<Q", 16 + end))
-        f.write(memoryview(host.numpy()))
-        f.write(idx)
-    return 16 + end + len(idx)
+                  device: str = "cuda", src2: str | None = None, group=None,
+                  window_bytes: int | None = None) -> int:
+    """fqzcomp5 -<level> src [src2] dst on the GPU(s): the input streamed in
+    windows of whole records, each window's complete blocks coded and written
+    behind the last (see above); src2: the R2 file of a pair, interleaved
+    with src (fqzcomp5 in1 in2 out).  group: a torch.distributed group, one
+    process per GPU, every rank calling with the same arguments; the file
+    equals the single-process one byte for byte.  Returns the file size."""
+    ws, rk = S._world(group)
+    if rk == 0:
+        _Sink(dst, True).close()              # create / truncate before anyone writes
+    _barrier(group)
+    sink = _Sink(dst, False)
+    srcs = [_Src(src)] + ([_Src(src2)] if src2 else [])
+    try:
+        return _encode_stream(srcs, sink, level, blk_size, device, group, window_bytes)
+    finally:
+        sink.close()
+        for s in srcs:
+            s.close()
+        _barrier(group)
 
 
 def _blocks_of(data):
     """Block byte ranges of a .fqz5 (walking block_size fields up to the
-    index, fqzcomp5.c:3754-3772)."""
+    index, fqzcomp5.c:3754-3772); a block that runs past the data or the
+    index is an error (the reference's read fails there)."""
     data = memoryview(data).cast("B")
-    if bytes(data[:8]) != MAGIC:
+    if len(data) < 16 or bytes(data[:8]) != MAGIC:
         raise ValueError("not an FQZ5 v1.1 file")
     (idx,) = struct.unpack_from("<Q", data, 8)
+    if idx > len(data) or (idx and idx < 16):
+        raise ValueError("truncated .fqz5: index offset past the end of the file")
     end = idx if idx else len(data)
     p, out = 16, []
     while p < end:
+        if p + 4 > end:
+            raise ValueError("truncated .fqz5: a block header runs past the end")
         (bsz,) = struct.unpack_from("<I", data, p)
+        if p + 4 + bsz > end or bsz < 8:
+            raise ValueError("truncated .fqz5: a block runs past the end of the file")
         out.append((p, p + 4 + bsz))
         p += 4 + bsz
     return out
 
 
-def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False):
-    """Blocks of a .fqz5 (host view `data`, device copy `buf`) -> the FASTQ
-    text of every block in one device buffer; pairs: (the R1 text, the R2
-    text) of output_fastq_deinterleaved (fqzcomp5.c:3612-3676), even records
-    of every block to R1 and odd ones to R2."""
+def block_fields(data, s: int, e: int) -> dict:
+    """The header fields of the block data[s:e] read on the host, as
+    decode_block reads them (fqzcomp5.c:2290-2420): record count, the name,
+    sequence and quality sections' sizes, the lengths section.  Raises
+    ValueError when a field points past the block or the sizes disagree
+    (the decoders write u_len bytes into outputs sized by these fields)."""
+    d = memoryview(data).cast("B")
+
+    def get(fmt, at):
+        z = struct.calcsize(fmt)
+        if at + z > e:
+            raise ValueError("corrupt block: header runs past the block")
+        return struct.unpack_from(fmt, d, at), at + z
+
+    (bsz, nrec, _crc), p = get("<III", s)
+    if s + 4 + bsz != e:
+        raise ValueError("corrupt block: block size field")
+    (nu, _st, nc), p = get("<IBI", p)
+    p += nc
+    (nb,), p = get("<B", p)
+    if nb:
+        p += nb
+    else:
+        (lz,), p = get("<I", p)
+        p += lz
+    (_s1, su, sc), p = get("<BII", p)
+    p += sc
+    (_s2, qu, qc), p = get("<BII", p)
+    p += qc
+    if p > e:
+        raise ValueError("corrupt block: a section runs past the block")
+    fasta = qu == 0 and qc == 0
+    if not fasta and qu != su:
+        raise ValueError("corrupt block: quality and sequence sizes differ")
+    return dict(nrec=nrec, name_ulen=nu, seq_ulen=su, qual_ulen=qu, fasta=fasta)
+
+
+def check_blocks(data, ranges=None) -> list[dict]:
+    """block_fields of every block (host only)."""
+    if ranges is None:
+        ranges = _blocks_of(data)
+    return [block_fields(data, s, e) for s, e in ranges]
+
+
+def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges=None):
+    """Blocks of a .fqz5 (host view `data`, device copy `buf`; `ranges` the
+    block byte ranges within them, all blocks of the file by default) ->
+    the FASTQ text of every block in one device buffer; pairs: (the R1
+    text, the R2 text) of output_fastq_deinterleaved (fqzcomp5.c:3612-3676),
+    even records of every block to R1 and odd ones to R2."""
     import torch
     so = _load()
-    ranges = _blocks_of(data)
+    if ranges is None:
+        ranges = _blocks_of(data)
     if not ranges:
         return torch.empty(0, dtype=torch.uint8, device=device)
+    try:
+        check_blocks(data, ranges)
+    except ValueError as err:
+        raise _lib.NativeError(str(err)) from None
     views, lens = [], []
     for s, e in ranges:
         v = S.BlockView()
@@ -365,8 +660,14 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False):
                "fqz5_block_parse")
         if not v.crc_ok:
             raise _lib.NativeError("block CRC mismatch")
+        ln = ln[:v.nrec]
+        # the decoders write u_len bytes into outputs sized by the block's
+        # own fields: refuse fields that disagree (decode_block allocates
+        # from them, fqzcomp5.c:2433-2519)
+        if int(ln.astype(np.uint64).sum()) != v.seq_ulen:
+            raise _lib.NativeError("corrupt block: record lengths do not sum to the bases")
         views.append(v)
-        lens.append(ln[:v.nrec])
+        lens.append(ln)
     # FASTA: a quality section of u_len 0 and c_len 0 (decode_block,
     # fqzcomp5.c:2477-2483); the text is then output_fasta's (:3503-3517)
     fasta = [v.qual_ulen == 0 and v.qual_size == 9 for v in views]
@@ -446,29 +747,125 @@ def decompress_paired_bytes(data: bytes, plus_name: bool = False,
     return t1.cpu().numpy().tobytes(), t2.cpu().numpy().tobytes()
 
 
+def _file_blocks(f, size: int):
+    """Block byte ranges of a .fqz5 file: from the index when the header
+    names one (write_index, fqzcomp5.c:2606), else by walking the block
+    size fields; checked against the file size."""
+    f.seek(0)
+    head = f.read(16)
+    if len(head) < 16 or head[:8] != MAGIC:
+        raise ValueError("not an FQZ5 v1.1 file")
+    (idx,) = struct.unpack_from("<Q", head, 8)
+    if idx > size or (idx and idx < 16):
+        raise ValueError("truncated .fqz5: index offset past the end of the file")
+    end = idx if idx else size
+    out, p = [], 16
+    while p < end:
+        f.seek(p)
+        h = f.read(4)
+        if len(h) < 4:
+            raise ValueError("truncated .fqz5: a block header runs past the end")
+        (bsz,) = struct.unpack("<I", h)
+        if p + 4 + bsz > end or bsz < 8:
+            raise ValueError("truncated .fqz5: a block runs past the end of the file")
+        out.append((p, p + 4 + bsz))
+        p += 4 + bsz
+    return out
+
+
 def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "cuda",
-                    dst2: str | None = None) -> int:
-    """The file path: the .fqz5 read into page-locked memory, one copy to
-    HBM, the FASTQ text back in one copy and written.  dst2: deinterleave,
-    R1 records to dst and R2 records to dst2 (fqzcomp5 -d in out1 out2)."""
-    host = _read_pinned(src)
-    hv = host.numpy()
-    if not _blocks_of(hv):
-        for d in (dst, dst2):
-            if d is not None:
-                _write_out(d, b"")
-        return 0
-    buf = host.to(device)     # blocking: block parsing runs on the library's streams
-    texts = _decode(hv, buf, plus_name, device, pairs=dst2 is not None)
-    if dst2 is None:
-        texts = (texts,)
-    total = 0
-    for text, d in zip(texts, (dst, dst2)):
-        out = _pinned(int(text.numel()))
-        out.copy_(text)
-        _write_out(d, memoryview(out.numpy()))
-        total += int(text.numel())
-    return total
+                    dst2: str | None = None, group=None, window_bytes: int | None = None) -> int:
+    """fqzcomp5 -d src dst [dst2] on the GPU(s): blocks read and decoded in
+    windows of at most `window_bytes` of compressed data (the reference
+    decodes block by block, fqzcomp5.c:3754-3800), the text written behind
+    the last.  dst2: deinterleave, R1 records to dst and R2 records to dst2
+    (fqzcomp5 -d in out1 out2).  group: one process per GPU, the blocks split
+    contiguously over the ranks, each rank's text written at its offset from
+    an all-gather of the text sizes.  Returns the text bytes written."""
+    import os
+    ws, rk = S._world(group)
+    outs = [dst] + ([dst2] if dst2 is not None else [])
+    if ws > 1 and any(d.endswith(".gz") for d in outs):
+        raise ValueError("gzip output needs a single process")
+    size = os.path.getsize(src)
+    with open(src, "rb") as f:
+        ranges = _file_blocks(f, size)
+        nb = len(ranges)
+        mine = [b for b in range(nb) if (b * ws) // max(nb, 1) == rk] if nb else []
+        wb = window_bytes or DEFAULT_WINDOW
+        groups, cur, tot = [], [], 0
+        for b in mine:
+            z = ranges[b][1] - ranges[b][0]
+            if cur and tot + z > wb:
+                groups.append(cur)
+                cur, tot = [], 0
+            cur.append(b)
+            tot += z
+        if cur:
+            groups.append(cur)
+        single = ws == 1
+        gz = [d.endswith(".gz") for d in outs]
+        streams = []
+        if single:
+            import gzip
+            streams = [gzip.GzipFile(filename="", mode="wb", compresslevel=6, mtime=0,
+                                     fileobj=open(d, "wb")) if z else open(d, "wb")
+                       for d, z in zip(outs, gz)]
+        held = [[] for _ in outs]              # multi-rank: this rank's text, in order
+        written = [0 for _ in outs]
+        try:
+            for gb in groups:
+                a, e = ranges[gb[0]][0], ranges[gb[-1]][1]
+                host = _pinned(e - a)
+                f.seek(a)
+                mv = memoryview(host.numpy())
+                got = 0
+                while got < e - a:
+                    k = f.readinto(mv[got:])
+                    if not k:
+                        raise OSError(f"{src}: short read")
+                    got += k
+                hv = host.numpy()
+                buf = host.to(device)      # blocking: block parsing runs on the library's streams
+                texts = _decode(hv, buf, plus_name, device, pairs=dst2 is not None,
+                                ranges=[(ranges[b][0] - a, ranges[b][1] - a) for b in gb])
+                if dst2 is None:
+                    texts = (texts,)
+                for j, t in enumerate(texts):
+                    out = _pinned(int(t.numel()))
+                    out.copy_(t)
+                    if single:
+                        streams[j].write(memoryview(out.numpy()))
+                    else:
+                        held[j].append(out)
+                    written[j] += int(t.numel())
+                del buf, host, texts
+        finally:
+            for st in streams:
+                if isinstance(st, __import__("gzip").GzipFile):
+                    st.close()
+                    st.fileobj.close()
+                else:
+                    st.close()
+    if single:
+        return sum(written)
+    # several ranks: text offsets from the ranks' sizes, positioned writes
+    all_w = _allgather_obj(written, group)
+    for j, d in enumerate(outs):
+        if rk == 0:
+            _Sink(d, True).close()
+    _barrier(group)
+    for j, d in enumerate(outs):
+        off = sum(w[j] for w in all_w[:rk])
+        sink = _Sink(d, False)
+        try:
+            for out in held[j]:
+                sink.write_at(off, out.numpy())
+                off += int(out.numel())
+        finally:
+            sink.close()
+    _barrier(group)
+    return sum(sum(w) for w in all_w)
 
 
 def _write_out(path: str, data) -> None:
@@ -476,7 +873,9 @@ def _write_out(path: str, data) -> None:
     (gzopen(name, "wb"), zlib's default level, fqzcomp5.c:5113-5160)."""
     if path.endswith(".gz"):
         import gzip
-        with gzip.open(path, "wb", compresslevel=6) as f:
+        # no file name and mtime 0 in the header, as zlib's gzopen writes it
+        with open(path, "wb") as raw, gzip.GzipFile(filename="", mode="wb", compresslevel=6,
+                                                    mtime=0, fileobj=raw) as f:
             f.write(data)
     else:
         with open(path, "wb") as f:

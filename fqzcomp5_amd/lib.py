@@ -15,9 +15,12 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 # helper contexts' streams need queues of their own (bench.py); effective
 # only when nothing in the process has initialised HIP yet
-_HWQ = int(os.environ.get("FQZ5_HW_QUEUES", "32") or 32)   # experiments: fewer queues
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < _HWQ:
-    os.environ["GPU_MAX_HW_QUEUES"] = str(_HWQ)
+# (the rule of capi.cpp's hw_queues_default: FQZ5_HW_QUEUES as given, else
+# an unset value or HIP's default of 4 raised to 32, any other value kept)
+if os.environ.get("FQZ5_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["FQZ5_HW_QUEUES"]
+elif os.environ.get("GPU_MAX_HW_QUEUES", "") in ("", "4"):
+    os.environ["GPU_MAX_HW_QUEUES"] = "32"
 
 _libc = C.CDLL(None)
 _libc.free.argtypes = [C.c_void_p]

@@ -380,6 +380,131 @@ def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState
     return res, meth_all, g_sizes, tried, off
 
 
+def _world(group):
+    import torch.distributed as dist
+    if group is None or not dist.is_available() or not dist.is_initialized():
+        return 1, 0
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def allreduce_min(a: np.ndarray, group) -> np.ndarray:
+    """Element-wise minimum over the ranks of `group` (int64 on the wire)."""
+    import torch
+    import torch.distributed as dist
+    if _world(group)[0] == 1:
+        return a
+    dev = torch.device("cuda", torch.cuda.current_device()) \
+        if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.from_numpy(np.ascontiguousarray(a, np.int64)).to(dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return t.cpu().numpy().astype(a.dtype)
+
+
+def work_share(methods: list[int], world: int, rank: int) -> int:
+    """The work-candidate methods (fqz, sequence models, LZP3) this rank
+    tries for the trial sections: method j of the sorted list goes to rank
+    j mod world, so one rank holds a method for the whole trial window (the
+    exact pruning needs that) and the ranks split the windows' chains."""
+    m = 0
+    for j, meth in enumerate(sorted(methods)):
+        if j % world == rank:
+            m |= 1 << meth
+    return m
+
+
+def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
+                  state: TrialState, group=None, bounded: bool = False,
+                  chunk_bytes: int = 600_000_000, prune: bool = True):
+    """Code the sections of consecutive blocks (file order) over the ranks of
+    `group`; every rank passes the same section ids / input sizes / owners,
+    its Section for every section it holds the data of (None elsewhere) and
+    the same state.  owner[i] is the rank that commits
+    section i; the trial sections (the schedule's trial and re-trial blocks)
+    are tried on every rank that holds them, each rank trying its share of
+    the work candidates (work_share) plus every rANS / name candidate, so
+    that the serial fqz and sequence-model chains of a trial window run on
+    as many GPUs as there are methods, not all on the first block's owner.
+    One collective, an element-wise minimum of the candidate sizes (a size
+    is the same wherever it is computed; untried candidates are UINT32_MAX),
+    then every rank replays the trial (fqz5_trial_replay, file order) and
+    commits its own sections.
+
+    bounded: the -7/-9 path of encode_run_bounded (tries chunked by
+    chunk_bytes, no pruning, every section coded again at commit).
+    Returns (results: SectionResult per section or None when not owned,
+    methods of every section, sizes)."""
+    ws, rk = _world(group)
+    n = len(secs)
+    ids = np.asarray(ids, np.int32)
+    ins = np.asarray(ins, np.uint32)
+    owner = np.asarray(owner, np.int64)
+    av = np.asarray(avail, np.uint32)
+    sched = trial_schedule(ids, av, state)
+    SPEC = RANS_MASK | NAME_MASK
+    work = sorted({m for i in range(n) for m in range(M_LAST) if (int(sched[i]) >> m) & 1
+                   and (1 << m) & WORK_MASK})
+    share = work_share(work, ws, rk)
+    masks = np.zeros(n, np.uint32)
+    for i in range(n):
+        mine = owner[i] == rk
+        if bounded:
+            # the scheduled sections only (their rANS on the owner), the
+            # rest coded once at commit
+            if sched[i]:
+                masks[i] = (int(sched[i]) & ~WORK_MASK & (SPEC if mine else 0)) | \
+                    (int(sched[i]) & share)
+        else:
+            if mine:
+                masks[i] = int(av[ids[i]]) & SPEC
+            if sched[i] and (int(sched[i]) & share):
+                # the exact pruning of this rank's methods needs the earlier
+                # methods' sizes of the whole trial window here
+                masks[i] |= (int(sched[i]) & SPEC) | (int(sched[i]) & share)
+    rows = [i for i in range(n) if masks[i] or owner[i] == rk]
+    for i in rows:
+        if secs[i] is None:
+            raise ValueError(f"section {i}: rank {rk} needs its data")
+    local = np.full((n, M_LAST), np.iinfo(np.uint32).max, np.uint32)
+    so = _load()
+    if bounded:
+        prev = so.fqz5_set_trial_prune(0)
+        try:
+            tried_rows = [i for i in rows if masks[i]]
+            for ch in _chunks(tried_rows, ins, chunk_bytes):
+                local[ch] = sections_try([secs[i] for i in ch], masks[ch])
+        finally:
+            so.fqz5_set_trial_prune(prev)
+    else:
+        # pruning of a family: its trial window whole in this call
+        for fam in (FQZ_MASK, SEQ_MASK):
+            frows = np.nonzero(sched & fam)[0]
+            if len(frows):
+                prune = prune and len(frows) == TRIAL_WINDOW
+        prev = so.fqz5_set_trial_prune(1 if prune else 0)
+        try:
+            if rows:
+                local[rows] = sections_try([secs[i] for i in rows], masks[rows])
+        finally:
+            so.fqz5_set_trial_prune(prev)
+    sizes = allreduce_min(local, group)
+    tried = np.zeros(n, np.uint32)
+    meth = trial_replay(ids, ins, sizes, av, state, tried)
+    res: list = [None] * n
+    mine = [i for i in rows if owner[i] == rk]
+    if bounded:
+        for ch in _chunks(mine, ins, chunk_bytes):
+            part = [secs[i] for i in ch]
+            sections_try(part, np.zeros(len(ch), np.uint32))    # an empty session
+            for i, r in zip(ch, sections_commit(part, meth[ch])):
+                res[i] = r
+    elif rows:
+        m = np.where(owner[rows] == rk, meth[rows], 0).astype(np.int32)
+        for i, r in zip(rows, sections_commit([secs[i] for i in rows], m)):
+            if owner[i] == rk:
+                res[i] = r
+    return res, meth, sizes
+
+
 def fqz_bound(n: int) -> int:
     """Room the fqz encoder needs: the coder's bound (fqz_codec.cpp) plus
     the parameter header."""
@@ -523,8 +648,7 @@ class Run:
                                     (0, 1, 64, 65, 128, 129, 192, 193, (fl << 8) + 9)),
                                 fqz_bound(n)))
         self.enc_buf = torch.empty(sum(caps), dtype=torch.uint8, device=device)
-        self.dec_buf = torch.empty(sum(e - s for _, s, e, _, _ in self.spans),
-                                   dtype=torch.uint8, device=device)
+        self._dec_buf = None          # decode outputs, allocated on first use
         self.enc, self.dec = [], []
         eo = do = 0
         for (sec, s, e, fl, k), cap in zip(self.spans, caps):
@@ -535,6 +659,14 @@ class Run:
         self.in_bytes = sum(e - s for _, s, e, _, _ in self.spans)
         self.blk_buf = None
         self.blk_off = None
+
+    @property
+    def dec_buf(self):
+        import torch
+        if self._dec_buf is None:
+            self._dec_buf = torch.empty(max(sum(e - s for _, s, e, _, _ in self.spans), 1),
+                                        dtype=torch.uint8, device=self.seq_d.device)
+        return self._dec_buf
 
     def _src(self, sec):
         return {SEC_NAME: self.name_d, SEC_SEQ: self.seq_d, SEC_QUAL: self.qual_d}[sec]
@@ -592,12 +724,12 @@ class Run:
         return ok
 
     # ---- whole blocks (encode_block / decode_block) -----------------------
-    def _parts(self, res) -> list[BlockParts]:
+    def _parts(self, res, which=None) -> list[BlockParts]:
         assert self.names, "blocks need the name sections"
         parts = []
         base = self.enc_buf.data_ptr()
         per = self.secs_per_block()
-        for b in range(len(self.blocks)):
+        for b in (range(len(self.blocks)) if which is None else which):
             i = per * b
             (eo_n, _), (eo_s, _) = self.enc[i], self.enc[i + 1]
             ln = self.lengths[b]
@@ -613,12 +745,13 @@ class Run:
         """Sections per block: name, seq, qual (2 for FASTA blocks)."""
         return 3 if self.qual_d is not None else 2
 
-    def assemble(self, res):
-        """Write every block (fqz5_blocks_assemble) into self.blk_buf at
-        self.blk_off; returns the block sizes."""
+    def assemble(self, res, which=None):
+        """Write every block (or the blocks `which`, in that order) with
+        fqz5_blocks_assemble into self.blk_buf at self.blk_off; returns the
+        block sizes."""
         import torch
         so = _load_blk()
-        parts = self._parts(res)
+        parts = self._parts(res, which)
         sizes = [int(so.fqz5_block_size(C.byref(p))) for p in parts]
         off = np.zeros(len(parts) + 1, np.uint64)
         np.cumsum(sizes, out=off[1:])

@@ -1,0 +1,137 @@
+"""The streaming and multi-GPU file path on the GPU (fqzcomp5_amd/fqz5file.py;
+VERDICT r02 items 4 and 5).
+
+* windows: the input read in windows of whole records, the last block of a
+  window carried into the next, the trial state carried across windows —
+  the file equals the reference CLI's (-t1) byte for byte at -3/-5/-7 and
+  for paired input, and decodes back in windows;
+* ranks: two processes (gloo, both on this GPU) write the same file as one
+  process, each coding its contiguous share of the blocks and its share of
+  the trial's work candidates, and decode it back together;
+* the -7 preset: a 1.1 GB ONT file in the preset's 500 MB blocks equals the
+  reference CLI's -7 -t1 output (md5 recorded by tests/golden/make_golden_l7.py).
+"""
+import hashlib
+import json
+import os
+import socket
+import subprocess
+
+import pytest
+import torch.multiprocessing as mp
+
+from fqzcomp5_amd import fqz5file, synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "oracle", "_ref", "fqzcomp5")
+pytestmark = pytest.mark.gpu
+
+
+def _cli(args, cwd=None):
+    subprocess.run([CLI] + args, check=True, capture_output=True, cwd=cwd)
+
+
+def _illumina(path, n=60000, seed=21):
+    synth.write_fastq(synth.illumina(n, seed=seed, with_names=True), path)
+
+
+@pytest.mark.parametrize("level", [3, 5, 7])
+def test_windows_equal_cli(tmp_path, level):
+    src = str(tmp_path / "in.fastq")
+    _illumina(src)
+    want, got, back = (str(tmp_path / x) for x in ("w.fqz5", "g.fqz5", "b.fastq"))
+    _cli([f"-{level}", "-t1", "-b", "1M", src, want])
+    # ~3 blocks per window: every window carries its last block over
+    n = fqz5file.compress_file(src, got, level, blk_size=1_000_000, window_bytes=3_500_000)
+    assert n == os.path.getsize(want)
+    assert open(got, "rb").read() == open(want, "rb").read()
+    assert fqz5file.decompress_file(got, back, window_bytes=1_500_000) == os.path.getsize(src)
+    assert open(back, "rb").read() == open(src, "rb").read()
+
+
+def test_windows_paired_equal_cli(tmp_path):
+    r1, r2 = str(tmp_path / "r1.fastq"), str(tmp_path / "r2.fastq")
+    a = synth.illumina(20000, seed=5, with_names=True)
+    b = synth.illumina(20000, seed=6, with_names=True)
+    synth.write_fastq(a, r1)
+    synth.write_fastq(b, r2)
+    want, got = str(tmp_path / "w.fqz5"), str(tmp_path / "g.fqz5")
+    _cli(["-3", "-t1", "-b", "1M", r1, r2, want])
+    fqz5file.compress_file(r1, got, 3, blk_size=1_000_000, src2=r2, window_bytes=2_000_000)
+    assert open(got, "rb").read() == open(want, "rb").read()
+    o1, o2 = str(tmp_path / "o1.fastq"), str(tmp_path / "o2.fastq")
+    fqz5file.decompress_file(got, o1, dst2=o2, window_bytes=1_000_000)
+    assert open(o1, "rb").read() == open(r1, "rb").read()
+    assert open(o2, "rb").read() == open(r2, "rb").read()
+
+
+def _rank(rank, world, port, args, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.init()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        src, dst, back, level = args
+        n = fqz5file.compress_file(src, dst, level, blk_size=1_000_000, group=dist.group.WORLD,
+                                   window_bytes=6_000_000)
+        m = fqz5file.decompress_file(dst, back, group=dist.group.WORLD, window_bytes=1_000_000)
+        q.put((rank, n, m, None))
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        q.put((rank, 0, 0, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("level", [5, 7])
+def test_two_ranks_equal_one_process(tmp_path, level):
+    src = str(tmp_path / "in.fastq")
+    _illumina(src, n=50000, seed=31)
+    one, two, back = (str(tmp_path / x) for x in ("one.fqz5", "two.fqz5", "back.fastq"))
+    fqz5file.compress_file(src, one, level, blk_size=1_000_000)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank, args=(r, 2, port, (src, two, back, level), q))
+          for r in range(2)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(2)]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(e is None for *_, e in out), out
+    assert all(p.exitcode == 0 for p in ps)
+    assert open(two, "rb").read() == open(one, "rb").read()
+    assert open(back, "rb").read() == open(src, "rb").read()
+
+
+def _md5(path):
+    h = hashlib.md5()
+    with open(path, "rb") as f:
+        for c in iter(lambda: f.read(1 << 24), b""):
+            h.update(c)
+    return h.hexdigest()
+
+
+def test_l7_preset_blocks_equal_cli(tmp_path):
+    """configs[3]'s shape at the preset block size (500 MB, fqzcomp5.c:4918):
+    3 blocks of a 1.1 GB ONT file through the file path, equal to the
+    reference's -7 -t1 output (its md5, recorded here by make_golden_l7.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_golden_l7 as G
+    rec = json.load(open(os.path.join(ROOT, "tests", "golden", "l7_ont.json")))
+    src = str(tmp_path / "ont.fastq")
+    assert G.make_input(src) == rec["in_bytes"]
+    dst, back = str(tmp_path / "ont.fqz5"), str(tmp_path / "back.fastq")
+    assert fqz5file.compress_file(src, dst, 7) == rec["out_bytes"]
+    assert _md5(dst) == rec["out_md5"]
+    os.unlink(src)
+    fqz5file.decompress_file(dst, back)
+    assert _md5(back) == rec["in_md5"]

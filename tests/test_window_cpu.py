@@ -1,0 +1,220 @@
+"""Host logic of the streaming / multi-GPU file path (fqzcomp5_amd/fqz5file.py,
+sections.encode_window), on the CPU.
+
+* encode_window over two gloo ranks, with the GPU calls (sections_try /
+  sections_commit) replaced by a deterministic fake codec: the methods
+  chosen equal a single process's, every rank commits only its own sections,
+  the trial sections' work candidates (fqz, sequence models, LZP3) are split
+  over the ranks by method and each is tried exactly once, and the collective
+  is the only exchange (fqzcomp5.c:1899-1958 trial, :3108-3115 offsets).
+* the window cut rule (_complete_records) on FASTQ and FASTA text.
+* the .fqz5 reader's checks: truncated files and blocks whose sizes disagree
+  are refused on the host, before any device work.
+"""
+import os
+import socket
+import struct
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from fqzcomp5_amd import fqz5file
+from fqzcomp5_amd import sections as S
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "oracle", "_ref", "fqzcomp5")
+
+
+def _layout(nblocks: int, level: int):
+    ids, ins = [], []
+    rng = np.random.default_rng(7)
+    for _ in range(nblocks):
+        for sec in (S.SEC_NAME, S.SEC_SEQ, S.SEC_QUAL):
+            ids.append(sec)
+            ins.append(int(rng.integers(50_000, 100_000)))
+    return np.array(ids, np.int32), np.array(ins, np.uint32)
+
+
+def _fake_size(i: int, m: int, n: int) -> int:
+    """A deterministic candidate size: any method may win anywhere."""
+    h = (i * 2654435761 + m * 40503 + 17) & 0xFFFFFFFF
+    return n // 4 + h % (n // 3)
+
+
+class _Fake:
+    """Stands in for the GPU calls: records what was tried / committed."""
+
+    def __init__(self):
+        self.tried, self.committed, self.sess = [], [], None
+
+    def sections_try(self, secs, masks):
+        out = np.full((len(secs), S.M_LAST), 0xFFFFFFFF, np.uint32)
+        for k, (s, m) in enumerate(zip(secs, masks)):
+            for b in range(S.M_LAST):
+                if (int(m) >> b) & 1:
+                    out[k, b] = _fake_size(s.nrec, b, s.in_size)
+                    self.tried.append((s.nrec, b))
+        self.sess = [s.nrec for s in secs]
+        return out
+
+    def sections_commit(self, secs, meth):
+        assert [s.nrec for s in secs] == self.sess, "commit without its try"
+        res = []
+        for s, m in zip(secs, meth):
+            r = S.SectionResult()
+            r.method, r.status = int(m), 0 if m > 0 else -1
+            if m > 0:
+                self.committed.append((s.nrec, int(m)))
+            res.append(r)
+        self.sess = None
+        return res
+
+
+def _run(world: int, rank: int, nblocks: int, level: int, bounded: bool):
+    ids, ins = _layout(nblocks, level)
+    n = len(ids)
+    secs = []
+    for i in range(n):   # Section.nrec carries the section index for the fake
+        secs.append(S.Section(None, None, int(ins[i]), 0, 0, int(ids[i]), None, None, i, None))
+    owner = np.repeat((np.arange(nblocks) * world) // nblocks, 3)
+    fake = _Fake()
+    S.sections_try, S.sections_commit = fake.sections_try, fake.sections_commit
+    st = S.new_state()
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        group = dist.group.WORLD
+    res, meth, sizes = S.encode_window(secs, ids, ins, owner, S.masks(level, full=True), st,
+                                       group, bounded=bounded)
+    return dict(meth=meth.tolist(), tried=fake.tried, committed=fake.committed,
+                owned=[i for i in range(n) if res[i] is not None])
+
+
+def _worker(rank, world, port, q, args):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _run(world, rank, *args)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("level,nblocks,bounded", [(5, 6, False), (7, 5, True), (9, 4, True)])
+def test_encode_window_two_ranks(level, nblocks, bounded):
+    single = _run(1, 0, nblocks, level, bounded)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, (nblocks, level, bounded)))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, out = q.get(timeout=120)
+        got[r] = out
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # the same choices as one process
+    assert got[0]["meth"] == got[1]["meth"] == single["meth"]
+    # every section committed once, by its owner, with its method
+    owner = (np.arange(nblocks) * world) // nblocks
+    for r in range(world):
+        assert all(owner[i // 3] == r for i in got[r]["owned"])
+        assert all(owner[i // 3] == r for i, _ in got[r]["committed"])
+    assert sorted(got[0]["committed"] + got[1]["committed"]) == sorted(single["committed"])
+    # the trial's work candidates: split over the ranks, each tried once
+    work = lambda t: sorted((i, m) for i, m in t if (1 << m) & S.WORK_MASK)
+    w0, w1, ws = work(got[0]["tried"]), work(got[1]["tried"]), work(single["tried"])
+    assert w0 and w1, "both ranks run work candidates"
+    assert not set(w0) & set(w1)
+    assert sorted(w0 + w1) == ws
+    # and all of block 0's (the first trial block) are not on one rank
+    assert {m for i, m in w0 if i < 3} and {m for i, m in w1 if i < 3}
+
+
+def test_work_share_partitions_methods():
+    ms = [S.FQZ0, S.FQZ1, S.FQZ2, S.FQZ3, S.FQZ4, S.SEQ10, S.LZP3]
+    for world in (1, 2, 3, 8):
+        shares = [S.work_share(ms, world, r) for r in range(world)]
+        assert sum(bin(x).count("1") for x in shares) == len(ms)
+        acc = 0
+        for x in shares:
+            assert not acc & x
+            acc |= x
+        assert acc == sum(1 << m for m in ms)
+
+
+def test_window_cut_rules():
+    fq = b"@a\nAC\n+\nII\n@b\nGT\n+\nII\n@c\nA"
+    t = torch.frombuffer(bytearray(fq), dtype=torch.uint8)
+    ends, fa = fqz5file._complete_records(t, len(fq), False)
+    assert not fa and ends == [11, 22]
+    ends, _ = fqz5file._complete_records(t, len(fq), True)
+    assert ends == [11, 22, len(fq)]
+    fa_txt = b">x\nACGT\nAC\n>y 1\nGG\n\n>z\nT"
+    t = torch.frombuffer(bytearray(fa_txt), dtype=torch.uint8)
+    ends, fa = fqz5file._complete_records(t, len(fa_txt), False)
+    assert fa and ends == [fa_txt.index(b">y"), fa_txt.index(b">z")]
+    ends, _ = fqz5file._complete_records(t, len(fa_txt), True)
+    assert ends[-1] == len(fa_txt)
+
+
+@pytest.fixture(scope="module")
+def cli_file(tmp_path_factory):
+    if not os.path.exists(CLI):
+        pytest.skip("reference CLI not built")
+    from fqzcomp5_amd import synth
+    d = tmp_path_factory.mktemp("blk")
+    src, out = str(d / "in.fastq"), str(d / "o.fqz5")
+    synth.write_fastq(synth.illumina(8000, seed=4, with_names=True), src)
+    subprocess.run([CLI, "-3", "-t1", "-b", "500k", src, out], check=True, capture_output=True)
+    return open(out, "rb").read()
+
+
+def test_truncated_file_refused(cli_file):
+    data = cli_file
+    ranges = fqz5file._blocks_of(data)
+    assert len(ranges) > 1 and [f["seq_ulen"] == f["qual_ulen"] for f in
+                                fqz5file.check_blocks(data)] == [True] * len(ranges)
+    idx = struct.unpack_from("<Q", data, 8)[0]
+    with pytest.raises(ValueError):      # the index offset past the end
+        fqz5file._blocks_of(data[:idx - 1])
+    cut = bytearray(data[:ranges[1][0] + 100])
+    cut[8:16] = struct.pack("<Q", 0)     # no index: the block walk runs off the end
+    with pytest.raises(ValueError):
+        fqz5file._blocks_of(bytes(cut))
+
+
+def test_mismatched_sizes_refused(cli_file):
+    data = bytearray(cli_file)
+    s, e = fqz5file._blocks_of(data)[0]
+    f = fqz5file.block_fields(data, s, e)
+    # walk to the quality section header and grow its u_len by one, then
+    # fix the CRC so that only the size check can catch it
+    p = s + 12
+    nu, _, nc = struct.unpack_from("<IBI", data, p)
+    p += 9 + nc
+    nb = data[p]
+    p += 1 + (nb if nb else 4 + struct.unpack_from("<I", data, p + 1)[0])
+    _, su, sc = struct.unpack_from("<BII", data, p)
+    p += 9 + sc
+    st, qu, qc = struct.unpack_from("<BII", data, p)
+    assert qu == su == f["seq_ulen"]
+    struct.pack_into("<BII", data, p, st, qu + 1, qc)
+    struct.pack_into("<I", data, s + 8, zlib.crc32(bytes(data[s + 12:e])))
+    with pytest.raises(ValueError, match="quality and sequence"):
+        fqz5file.check_blocks(bytes(data))

@@ -1,0 +1,87 @@
+/* fqz_stats.c — decoder design statistics (tool, not product): runs the
+ * oracle's fqz decoder (oracle/fqz_oracle.c) over a stream and counts, per
+ * quality symbol, the decoded slot, one-step bubble swaps, halvings, repeats
+ * of the previous context, and the misses of direct-mapped caches of a few
+ * sizes.  Build: gcc -O2 -I oracle tools/fqz_stats.c oracle/rans_oracle.c -lm -o /tmp/fqz_stats
+ * (see tools/fqz_stats.py for the driver).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include "cm_common.h"
+
+static struct {
+    void *base;
+    size_t stride;
+    unsigned long long n, ksum, kge[8], swaps, halves, same, uniq;
+    int prev;
+    unsigned char seen[65536];
+    int tags[8][65536];
+} S;
+static const unsigned NSETS[8] = {256, 512, 760, 1024, 2048, 2456, 3548, 65536};
+static unsigned long long MISS[8];
+
+static unsigned fl_decode_stats(flist *m, rcoder *c, int cap) {
+    if (cap != 96 || !S.base) return fl_decode(m, c, cap);
+    const int ctx = (int)(((char *)m - (char *)S.base) / (long)S.stride);
+    const uint32_t tot0 = m->total;
+    uint32_t t = 0;
+    {
+        rcoder cc = *c;
+        t = rc_target(&cc, m->total);
+    }
+    int k = 1;
+    uint32_t acc = 0;
+    while ((acc += m->fr[k]) <= t && k < 258) k++;
+    S.n++;
+    S.ksum += (unsigned long long)k;
+    for (int b = 0; b < 8; b++) S.kge[b] += k > (1 << b);
+    const uint16_t before = m->fr[k];
+    (void)before;
+    unsigned s = fl_decode(m, c, cap);
+    if (tot0 + FL_STEP > FL_CAP_MAX) S.halves++;
+    if (m->sy[k] != s) S.swaps++;
+    S.same += ctx == S.prev;
+    S.prev = ctx;
+    if (!S.seen[ctx]) { S.seen[ctx] = 1; S.uniq++; }
+    const uint32_t h = (((uint32_t)ctx * 0x9E3779u) >> 8) & 0xffffffu;   /* the decoder's set_addr */
+    for (int i = 0; i < 8; i++) {
+        const unsigned set = NSETS[i] == 65536 ? (unsigned)ctx : (unsigned)(((uint64_t)h * NSETS[i]) >> 24);
+        if (S.tags[i][set] != ctx + 1) { MISS[i]++; S.tags[i][set] = ctx + 1; }
+    }
+    return s;
+}
+static void *cap_malloc(size_t n) {
+    void *p = malloc(n);
+    if (n == sizeof(flist) * 65536) {   /* the quality models (models_new) */
+        S.base = p;
+        S.stride = sizeof(flist);
+    }
+    return p;
+}
+#define fl_decode fl_decode_stats
+#define malloc cap_malloc
+#include "fqz_oracle.c"
+#undef malloc
+
+int main(int argc, char **argv) {
+    if (argc < 2) return 2;
+    FILE *f = fopen(argv[1], "rb");
+    if (!f) return 2;
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    uint8_t *in = malloc((size_t)n);
+    if (fread(in, 1, (size_t)n, f) != (size_t)n) return 2;
+    fclose(f);
+    S.prev = -1;
+    size_t out = 0;
+    uint8_t *o = ora_fqz_decompress(in, (size_t)n, &out, NULL, 0, NULL);
+    if (!o) { fprintf(stderr, "decode failed\n"); return 1; }
+    printf("{\"n\": %llu, \"k_mean\": %.3f, \"k_gt\": [", S.n, (double)S.ksum / (double)S.n);
+    for (int b = 0; b < 8; b++) printf("%s%.4f", b ? ", " : "", (double)S.kge[b] / (double)S.n);
+    printf("], \"swap\": %.4f, \"halve\": %.5f, \"same_ctx\": %.4f, \"contexts\": %llu, \"miss\": {",
+           (double)S.swaps / (double)S.n, (double)S.halves / (double)S.n, (double)S.same / (double)S.n, S.uniq);
+    for (int i = 0; i < 8; i++) printf("%s\"%u\": %.4f", i ? ", " : "", NSETS[i], (double)MISS[i] / (double)S.n);
+    printf("}}\n");
+    return 0;
+}
