@@ -217,6 +217,192 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     return L_CACHE + (set & 0xffffu) * (me & 0xffffu);   // both < 2^16: v_mad_u32_u24
 }
 
+
+// ---------------------------------------------------------------------------
+// The fast run of k_fqz_dec<NE = 1> as one hand-scheduled loop (a symbol per
+// iteration).  The model of the current context is in v (lane j: dword j of
+// the cached model: tag, freq | cum << 16 per slot, sentinel copies) and s
+// (lane j: the symbol of slot j).  Per symbol:
+//   u       the context terms of this position and delta (pvv / dvv lanes)
+//   total   the sentinel's cum; q = floor(range / total) from RN(1/total);
+//           a total that the +16 would take past FL_MAX leaves (flags 2)
+//   p_j     cum_j * q;  G = lanes with p_j > code;  kl = first of G - 1
+//   every lane j: the context its symbol would lead to (fqz_update_ctx), its
+//           cache set and whether that set holds it (the tag), qctx << qshift,
+//           and whether the bump would bubble slot j over slot j-1
+//   bump    +16 to lane kl's frequency and every later cum; one bubble step
+//           by DPP lane shifts when it swaps
+//   the model is written back, the next context's read issued (a context
+//   not in the cache leaves, flags 1, after the symbol), and the range coder
+//   (c_range_coder.h RC_Decode: code -= cum q, range = freq q, renormalise)
+//   and the context state run while the read is in flight.
+// It leaves after `lim` symbols or when the input window needs a refill.
+// gfx950 wait states: an SGPR written by a VALU compare and read as a VALU
+// mask gets two, DPP reads of a VGPR written by the VALU two, M0 before the
+// writelane one.
+// ---------------------------------------------------------------------------
+#define FQZ_QT_QID                                                          \
+    "v_add_u32 %[t0], %[qs], %[s]\n"
+#define FQZ_QT_TAB                                                          \
+    "v_lshl_add_u32 %[t0], %[s], 1, %[qtab]\n"                              \
+    "ds_read_u16 %[t0], %[t0]\n"                                            \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "v_add_u32 %[t0], %[qs], %[t0]\n"
+#define FQZ_SEQ_NONE ""
+#define FQZ_SEQ_CTX                                                         \
+    "v_readlane_b32 %[x], %[sqv], %[done]\n"                                \
+    "s_lshl_b32 %[sn], %[seq], 2\n"                                         \
+    "s_or_b32 %[sn], %[sn], %[x]\n"                                         \
+    "s_and_b32 %[sn], %[sn], %[bmask]\n"                                    \
+    "s_lshl_b32 %[x], %[sn], %[bloc]\n"                                     \
+    "s_add_u32 %[u], %[u], %[x]\n"
+#define FQZ_SEQ_COMMIT "s_mov_b32 %[seq], %[sn]\n"
+// the coded slot's update (fl_bump): +16 to lane kl's frequency (E) and to
+// every later cum (G); one bubble step (SW & E) by DPP lane shifts
+#define FQZ_BUMP_SWAP                                                       \
+    "v_cndmask_b32 %[t4], 0, 16, %[E]\n"                                    \
+    "v_cndmask_b32 %[t4], %[t4], %[cbig], %[G]\n"                           \
+    "s_and_b64 %[SW], %[SW], %[E]\n"                                        \
+    "v_add_u32 %[v], %[v], %[t4]\n"                                         \
+    "s_cbranch_scc0 3f\n"                                                   \
+    "s_nop 1\n"                                                             \
+    "v_mov_b32_dpp %[t4], %[v] wave_shr:1 row_mask:0xf bank_mask:0xf\n"     \
+    "v_mov_b32_dpp %[t5], %[v] wave_shl:1 row_mask:0xf bank_mask:0xf\n"     \
+    "v_mov_b32_dpp %[t6], %[s] wave_shr:1 row_mask:0xf bank_mask:0xf\n"     \
+    "v_mov_b32_dpp %[t7], %[s] wave_shl:1 row_mask:0xf bank_mask:0xf\n"     \
+    "v_and_b32 %[t3], 0xffff, %[v]\n"                                       \
+    "v_lshrrev_b32 %[t2], 16, %[t4]\n"                                      \
+    "v_add_u32 %[t3], %[t3], %[t2]\n"                                       \
+    "v_and_b32 %[t2], 0xffff, %[t4]\n"                                      \
+    "v_lshl_or_b32 %[t3], %[t3], 16, %[t2]\n"                               \
+    "v_and_b32 %[t2], 0xffff0000, %[v]\n"                                   \
+    "v_and_b32 %[t5], 0xffff, %[t5]\n"                                      \
+    "v_or_b32 %[t5], %[t5], %[t2]\n"                                        \
+    "s_lshr_b64 %[SW], %[E], 1\n"                                           \
+    "v_cndmask_b32 %[v], %[v], %[t3], %[E]\n"                               \
+    "v_cndmask_b32 %[s], %[s], %[t6], %[E]\n"                               \
+    "s_nop 1\n"                                                             \
+    "v_cndmask_b32 %[v], %[v], %[t5], %[SW]\n"                              \
+    "v_cndmask_b32 %[s], %[s], %[t7], %[SW]\n"                              \
+    "3:\n"
+// the range coder (c_range_coder.h RC_Decode) and the context state
+#define FQZ_CODER_STATE(SEQCOMMIT)                                          \
+    "s_sub_u32 %[code], %[code], %[pk]\n"                                   \
+    "s_sub_u32 %[rng], %[pk1], %[pk]\n"                                     \
+    "s_flbit_i32_b32 %[z], %[rng]\n"                                        \
+    "s_lshr_b32 %[nxk], %[nxk], 24\n"                                       \
+    "s_mov_b32 m0, %[done]\n"                                               \
+    "s_and_b32 %[z], %[z], 24\n"                                            \
+    "s_cmp_lg_u32 %[prevq], %[nxk]\n"                                       \
+    "s_addc_u32 %[delta], %[delta], 0\n"                                    \
+    "v_writelane_b32 %[vout], %[nxk], m0\n"                                 \
+    "s_mov_b32 %[prevq], %[nxk]\n"                                          \
+    "s_mov_b32 %[qs], %[qsk]\n"                                             \
+    SEQCOMMIT                                                               \
+    "s_cmp_eq_u32 %[z], 0\n"                                                \
+    "s_cbranch_scc1 5f\n"                                                   \
+    "s_lshl_b32 %[rng], %[rng], %[z]\n"                                     \
+    "s_sub_u32 %[x], 32, %[z]\n"                                            \
+    "s_lshr_b32 %[tot], %[whi], %[x]\n"                                     \
+    "s_lshl_b32 %[code], %[code], %[z]\n"                                   \
+    "s_or_b32 %[code], %[code], %[tot]\n"                                   \
+    "s_lshr_b32 %[tot], %[wlo], %[x]\n"                                     \
+    "s_lshl_b32 %[whi], %[whi], %[z]\n"                                     \
+    "s_or_b32 %[whi], %[whi], %[tot]\n"                                     \
+    "s_lshl_b32 %[wlo], %[wlo], %[z]\n"                                     \
+    "s_add_u32 %[ub], %[ub], %[z]\n"                                        \
+    "5:\n"                                                                  \
+    "s_add_u32 %[done], %[done], 1\n"
+#define FQZ_RUN_ASM(QT, SEQCTX, SEQCOMMIT)                                  \
+    "s_mov_b32 %[m0s], m0\n"                                                \
+    "1:\n"                                                                  \
+    "v_readlane_b32 %[u], %[pvv], %[done]\n"                                \
+    "s_sub_u32 %[x], %[delta], %[delta0]\n"                                 \
+    "v_readlane_b32 %[tot], %[v], 63\n"                                     \
+    "v_cvt_f64_u32 %[d0], %[rng]\n"                                         \
+    "v_readlane_b32 %[x], %[dvv], %[x]\n"                                   \
+    "s_lshr_b32 %[tot], %[tot], 16\n"                                       \
+    "s_add_u32 %[u], %[u], %[x]\n"                                          \
+    SEQCTX                                                                  \
+    "s_cmpk_gt_u32 %[tot], 65503\n"                                         \
+    "s_cbranch_scc1 2f\n"                                                   \
+    "v_cvt_f64_u32 %[d1], %[tot]\n"                                         \
+    QT                                                                      \
+    "v_rcp_f64 %[d2], %[d1]\n"                                              \
+    "v_and_b32 %[t1], %[qmask], %[t0]\n"                                    \
+    "v_lshlrev_b32 %[t1], %[qloc], %[t1]\n"                                 \
+    "v_add_u32 %[t1], %[u], %[t1]\n"                                        \
+    "v_and_b32 %[t1], 0xffff, %[t1]\n"                                      \
+    "v_fma_f64 %[d1], -%[d1], %[d2], 1.0\n"                                 \
+    "v_mul_u32_u24 %[t2], 0x9e3779, %[t1]\n"                                \
+    "v_fma_f64 %[d2], %[d2], %[d1], %[d2]\n"                                \
+    "v_lshrrev_b32 %[t2], 8, %[t2]\n"                                       \
+    "v_fma_f64 %[d0], %[d0], %[d2], %[c19]\n"                               \
+    "v_mul_hi_u32_u24 %[t2], %[ns8], %[t2]\n"                               \
+    "v_cvt_u32_f64 %[t3], %[d0]\n"                                          \
+    "v_mad_u32_u24 %[t2], %[t2], %[vme], %[base]\n"                         \
+    "v_lshrrev_b32 %[t4], 16, %[v]\n"                                       \
+    "ds_read_b32 %[t5], %[t2]\n"                                            \
+    "v_mul_lo_u32 %[t3], %[t4], %[t3]\n"                                    \
+    "v_lshl_or_b32 %[t7], %[s], 24, %[t2]\n"                                \
+    "v_lshlrev_b32 %[t0], %[qshift], %[t0]\n"                               \
+    "v_and_b32 %[t4], 0xffff, %[v]\n"                                       \
+    "v_mov_b32_dpp %[t6], %[v] wave_shr:1 row_mask:0xf bank_mask:0xf\n"     \
+    "v_cmp_gt_u32 %[G], %[t3], %[code]\n"                                   \
+    "v_add_u32 %[t4], 16, %[t4]\n"                                          \
+    "v_and_b32 %[t6], 0xffff, %[t6]\n"                                      \
+    "v_cmp_gt_u32 %[SW], %[t4], %[t6]\n"                                    \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "v_cmp_eq_u32 %[H], %[t5], %[t1]\n"                                     \
+    "s_cmp_eq_u64 %[G], 0\n"                                                \
+    "s_cbranch_scc1 2f\n"                                                   \
+    "s_ff1_i32_b64 %[k1], %[G]\n"                                           \
+    "s_lshr_b64 %[E], %[G], 1\n"                                            \
+    "s_sub_u32 %[kl], %[k1], 1\n"                                           \
+    "s_andn2_b64 %[E], %[E], %[G]\n"                                        \
+    "v_readlane_b32 %[nxk], %[t7], %[kl]\n"                                 \
+    "v_readlane_b32 %[pk], %[t3], %[kl]\n"                                  \
+    "v_readlane_b32 %[pk1], %[t3], %[k1]\n"                                 \
+    "v_readlane_b32 %[qsk], %[t0], %[kl]\n"                                 \
+    "s_andn2_b64 %[SW], %[SW], 3\n"                                         \
+    "s_and_b32 %[an], %[nxk], 0xffffff\n"                                   \
+    "s_and_b64 %[H], %[H], %[E]\n"                                          \
+    "s_cselect_b32 %[flags], 0, 1\n"                                        \
+    "s_cbranch_scc0 7f\n"                                                   \
+    "s_cmp_eq_u32 %[an], %[maddr]\n"                                        \
+    "s_cbranch_scc1 8f\n"                                                   \
+    "v_add_u32 %[t4], %[an], %[voff]\n"                                     \
+    "v_add_u32 %[t5], %[an], %[soff]\n"                                     \
+    "ds_read_b32 %[nv], %[t4]\n"                                            \
+    "ds_read_u8 %[ns], %[t5]\n"                                             \
+    "7:\n"                                                                  \
+    FQZ_BUMP_SWAP                                                           \
+    "v_add_u32 %[t2], %[maddr], %[voff]\n"                                  \
+    "v_add_u32 %[t3], %[maddr], %[soff]\n"                                  \
+    "ds_write_b32 %[t2], %[v]\n"                                            \
+    "ds_write_b8 %[t3], %[s]\n"                                             \
+    "s_mov_b32 %[maddr], %[an]\n"                                           \
+    FQZ_CODER_STATE(SEQCOMMIT)                                              \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "s_cmp_lg_u32 %[flags], 0\n"                                            \
+    "s_cbranch_scc1 6f\n"                                                   \
+    "v_mov_b32 %[v], %[nv]\n"                                               \
+    "v_mov_b32 %[s], %[ns]\n"                                               \
+    "s_branch 9f\n"                                                         \
+    "8:\n"                                                                  \
+    FQZ_BUMP_SWAP                                                           \
+    FQZ_CODER_STATE(SEQCOMMIT)                                              \
+    "9:\n"                                                                  \
+    "s_cmp_gt_u32 %[ub], %[ulim]\n"                                         \
+    "s_cbranch_scc1 6f\n"                                                   \
+    "s_cmp_lt_u32 %[done], %[lim]\n"                                        \
+    "s_cbranch_scc1 1b\n"                                                   \
+    "s_branch 6f\n"                                                         \
+    "2:\n"                                                                  \
+    "s_mov_b32 %[flags], 2\n"                                               \
+    "6:\n"                                                                  \
+    "s_mov_b32 m0, %[m0s]\n"
+
 // ---------------------------------------------------------------------------
 // the decoder.  Model in lanes: lane j holds dword j of the cached model,
 // [tag | entry of slot 0 .. entry of slot L], entries freq | cum << 16, the
@@ -232,6 +418,9 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     const uint32_t gfl = U(g.gflags), nparam = U(g.nparam);
     const uint32_t L = U(g.max_sym) + 1;              // live symbols per quality model
     const uint32_t ME = J.ment, NS = J.nsets, NS8 = NS << 8;
+    // the hand-scheduled run addresses LDS by these offsets: the dynamic
+    // block must start at LDS address 0 (no static __shared__ here)
+    if (uint32_t(size_t((__attribute__((address_space(3))) uint8_t *)lds)) != 0) __builtin_trap();
     const uint32_t soff = 4u * (L + 2u);              // symbol bytes within a model
     const uint32_t n = uint32_t(J.n);
 
@@ -523,7 +712,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 sbase = nullptr;
                 if (J.seq && rec - 1 < J.nseq && J.seq_off[rec - 1] != ~0ull) {
                     sbase = J.seq + J.seq_off[rec - 1];
-                    for (uint32_t b = 0; b < ps.boff; b++) seq = (seq << 2) | base2(sbase[b]);
+                    for (uint32_t b = 0; b < ps.boff; b++) seq = (seq << 2) | base2(uint8_t(U(sbase[b])));
                 }
                 sb0 = 0;
                 stage_seq();
@@ -547,17 +736,100 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         // per-step uniform context terms of the run (fqz_update_ctx uses the
         // position and delta before this symbol's update): lane i the
         // position term of step i, lane j the delta term of delta0 + j
-        const uint32_t delta0 = delta;
+        const uint32_t delta0 = U(delta);
         const uint32_t pvv = uint32_t(pt16[(P_PTAB >> 1) + (left - l < 1023u ? left - l : 1023u)]) + selterm;
         const uint32_t dvv = pt16[(P_DTAB >> 1) + (delta + l < 255u ? delta + l : 255u)];
         const uint32_t sqv = SEQ ? uint32_t(lds[L_SEQ + ((tpos - sb0 + l) & (SEQB - 1))]) : 0u;
         uint32_t qs = qctx << ps.qshift;
-        const uint32_t qmask = ps.qmask, qshift = ps.qshift;
+        const uint32_t qmask = U(ps.qmask), qshift = U(ps.qshift);
         uint32_t vout = 0;
         uint32_t done = 0;
-        bool to_slow = false;
+        bool to_slow = false, fetch = false;
         PROBE_START
         load_model();
+        if constexpr (NE == 1) {
+            // the run's scalar state, as uniform values (the asm keeps it in SGPRs)
+            uint32_t wlo = U(uint32_t(in.W)), whi = U(uint32_t(in.W >> 32));
+            rng = U(rng);
+            code = U(code);
+            in.ub = U(in.ub);
+            qs = U(qs);
+            maddr = U(maddr);
+            delta = U(delta);
+            prevq = U(prevq);
+            seq = U(seq);
+            lim = U(lim);
+            ulim = U(ulim);
+            uint32_t flags = 0, u = 0, qsk = 0;
+            const uint32_t lane = l, base = L_CACHE, vme = ME, cbig = 0x100000u;
+            const uint32_t ns8 = U(NS8), qloc = U(ps.qloc), bmask = U((1u << ps.bbits) - 1u), bloc = U(ps.bloc);
+            const uint32_t qtab = U(L_PAR + ps.x * PBYTES + P_QTAB);   // LDS address (the dynamic base is 0)
+            const uint32_t voff0 = voff[0], sofs0 = sofs[0];
+            const double c19 = 0x1p-19;
+            uint32_t &v0 = v[0], &s0 = s[0];
+            uint32_t tot, x, k1, kl, pk, pk1, nxk, z, m0s, sn, an, nv, ns;
+            uint64_t G, H, SW, E;
+            uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
+            double d0, d1, d2;
+            for (;;) {
+#define FQZ_RUN_OPERANDS                                                                      \
+                : [v] "+v"(v0), [s] "+v"(s0), [vout] "+v"(vout), [rng] "+s"(rng),             \
+                  [code] "+s"(code), [wlo] "+s"(wlo), [whi] "+s"(whi), [ub] "+s"(in.ub),     \
+                  [qs] "+s"(qs), [maddr] "+s"(maddr), [delta] "+s"(delta),                   \
+                  [prevq] "+s"(prevq), [done] "+s"(done), [seq] "+s"(seq),                    \
+                  [flags] "=&s"(flags), [u] "=&s"(u), [qsk] "=&s"(qsk), [tot] "=&s"(tot),     \
+                  [x] "=&s"(x), [k1] "=&s"(k1), [kl] "=&s"(kl), [pk] "=&s"(pk),               \
+                  [pk1] "=&s"(pk1), [nxk] "=&s"(nxk), [z] "=&s"(z), [m0s] "=&s"(m0s), [sn] "=&s"(sn), [an] "=&s"(an), \
+                  [G] "=&s"(G), [H] "=&s"(H), [SW] "=&s"(SW), [E] "=&s"(E),                   \
+                  [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),             \
+                  [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7),             \
+                  [d0] "=&v"(d0), [d1] "=&v"(d1), [d2] "=&v"(d2), [nv] "=&v"(nv), [ns] "=&v"(ns) \
+                : [lim] "s"(lim), [ulim] "s"(ulim), [delta0] "s"(delta0),                     \
+                  [qmask] "s"(qmask), [qshift] "s"(qshift), [qloc] "s"(qloc),                 \
+                  [ns8] "s"(ns8), [base] "s"(base), [qtab] "s"(qtab), [bmask] "s"(bmask),     \
+                  [bloc] "s"(bloc), [voff] "v"(voff0), [soff] "v"(sofs0), [lane] "v"(lane),   \
+                  [cbig] "v"(cbig), [c19] "v"(c19), [vme] "v"(vme), [pvv] "v"(pvv),          \
+                  [dvv] "v"(dvv), [sqv] "v"(sqv)                                              \
+                : "memory", "scc"
+                if constexpr (QID && SEQ) asm volatile(FQZ_RUN_ASM(FQZ_QT_QID, FQZ_SEQ_CTX, FQZ_SEQ_COMMIT) FQZ_RUN_OPERANDS);
+                else if constexpr (QID) asm volatile(FQZ_RUN_ASM(FQZ_QT_QID, FQZ_SEQ_NONE, FQZ_SEQ_NONE) FQZ_RUN_OPERANDS);
+                else if constexpr (SEQ) asm volatile(FQZ_RUN_ASM(FQZ_QT_TAB, FQZ_SEQ_CTX, FQZ_SEQ_COMMIT) FQZ_RUN_OPERANDS);
+                else asm volatile(FQZ_RUN_ASM(FQZ_QT_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE) FQZ_RUN_OPERANDS);
+#undef FQZ_RUN_OPERANDS
+                // (the compiler takes every output of an asm with VGPR outputs
+                // for divergent: the scalar ones are re-read as uniform)
+                rng = U(rng);
+                code = U(code);
+                wlo = U(wlo);
+                whi = U(whi);
+                in.ub = U(in.ub);
+                qs = U(qs);
+                maddr = U(maddr);
+                delta = U(delta);
+                prevq = U(prevq);
+                done = U(done);
+                seq = U(seq);
+                flags = U(flags);
+                u = U(u);
+                qsk = U(qsk);
+                if (flags == 2) { to_slow = true; break; }
+                if (flags == 1) {   // the next context is not cached: the next run fetches it
+                    ctx = ((((qsk >> qshift) & qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1);
+                    fetch = true;
+                    break;
+                }
+                if (done == lim) break;
+                in.W = (uint64_t(whi) << 32) | wlo;   // the input window needs a refill
+                refill(lds, in);
+                wlo = uint32_t(in.W);
+                whi = uint32_t(in.W >> 32);
+                if (in.vb < 4u) break;
+                ulim = (in.vb - 4u) * 8u;
+            }
+            in.W = (uint64_t(whi) << 32) | wlo;
+            left -= done;
+            if (SEQ) tpos += done;
+        } else
         do {
             PROBE(0)
             uint32_t u = RL(pvv, done) + RL(dvv, delta - delta0);
@@ -603,6 +875,29 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             }
             const uint32_t pk = rlane(p, kl), pk1 = rlane(p, k1);
             const uint32_t nxk = RL(nx, kl), qsk = RL(qsn, kl);
+            const uint32_t ank = nxk & 0xffffffu, sym = nxk >> 24;
+            const bool hit = (H >> kl) & 1u;
+            // the coded slot's update in registers (fl_bump): +16 to its
+            // frequency and to every later cum, halving past FL_MAX, one
+            // bubble step; then written back
+#pragma unroll
+            for (int r = 0; r < NE; r++) {
+                const uint32_t dw = l + 64 * r;
+                v[r] += gt[r] ? 0x100000u : (dw == kl ? FL_STEP : 0u);
+            }
+            if (__builtin_expect(total + FL_STEP > FL_MAX, 0)) {
+                halve();
+                if (kl >= 2) bubble(kl);
+            } else if (__builtin_expect(uint32_t(SW >> kl) & 1u, 0)) {
+                bubble(kl);
+            }
+            write_model(maddr);
+            maddr = ank;
+            // the next context's model (the same cache set again when the
+            // context repeats: the write above lands first); a context not
+            // in the cache ends the run, the next one fetches it
+            if (hit) issue_model();
+            // the coder (c_range_coder.h RC_Decode), beside the read
             code -= pk;
             rng = pk1 - pk;
             const uint32_t z = uint32_t(__builtin_clz(rng)) & 24u;
@@ -610,47 +905,6 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             code = uint32_t(((uint64_t(code) << 32) | uint32_t(in.W >> 32)) >> (32u - z));
             in.W <<= z;
             in.ub += z;
-            PROBE(2)
-            const uint32_t ank = nxk & 0xffffffu, sym = nxk >> 24;
-            // the coded slot's update in registers (fl_bump): +16 to its
-            // frequency and to every later cum, halving past FL_MAX, one
-            // bubble step
-            auto bump = [&]() {
-#pragma unroll
-                for (int r = 0; r < NE; r++) {
-                    const uint32_t dw = l + 64 * r;
-                    v[r] += gt[r] ? 0x100000u : (dw == kl ? FL_STEP : 0u);
-                }
-                if (__builtin_expect(total + FL_STEP > FL_MAX, 0)) {
-                    halve();
-                    if (kl >= 2) bubble(kl);
-                } else if (__builtin_expect(uint32_t(SW >> kl) & 1u, 0)) {
-                    bubble(kl);
-                }
-            };
-            if (__builtin_expect(!((H >> kl) & 1u), 0)) {
-                // the next context is not cached: write back, fetch
-                bump();
-                write_model(maddr);
-                ctx = ((((qsk >> qshift) & qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1);
-                maddr = ank;
-                load_model();
-            } else if (ank != maddr) {
-                // another cached context: its read goes out first
-                uint32_t nv[NE], ns[NE];
-                issue_model_to(ank, nv, ns);
-                bump();
-                write_model(maddr);
-#pragma unroll
-                for (int r = 0; r < NE; r++) {
-                    v[r] = nv[r];
-                    s[r] = ns[r];
-                }
-                maddr = ank;
-            } else {
-                bump();   // the same context again: stays in registers
-            }
-            PROBE(3)
             vout = uint32_t(amdgcn_writelane(int(sym), int(done), int(vout)));
             delta += prevq != sym;
             prevq = sym;
@@ -659,22 +913,28 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             left--;
             if (SEQ) tpos++;
             done++;
-            PROBE(4)
+            PROBE(2)
+            if (__builtin_expect(!hit, 0)) {
+                ctx = ((((qsk >> qshift) & qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1);
+                fetch = true;
+                break;
+            }
             if (in.ub > ulim) {
                 refill(lds, in);
                 if (in.vb < 4u) break;
                 ulim = (in.vb - 4u) * 8u;
             }
             if (done == lim) break;
-            PROBE(5)
+            PROBE(3)
         } while (true);
-        write_model(maddr);
         // the run's state back to the record: the context of the next
-        // symbol, its cache set, the output bytes
-        qctx = qs >> qshift;
-        if (done) {
-            ctx = RL(v[0], 0);   // the resident model is the next context's
+        // symbol, its cache set (written back unless the run ended on a
+        // context outside the cache), the output bytes
+        if (!fetch) {
+            write_model(maddr);
+            if (done) ctx = RL(v[0], 0);   // the resident model is the next context's
         }
+        qctx = qs >> qshift;
         if (l < done) lds[L_OBUF + fill + l] = uint8_t(vout);
         fill += done;
         if (to_slow) slow_symbol();

@@ -76,6 +76,26 @@ def test_fqz_random_vs_oracle():
         assert back == q, it
 
 
+@pytest.mark.parametrize("kind,strat", [("novaseq", 3), ("novaseq", 4), ("ont", 0), ("ont", 3),
+                                        ("hifi", 0), ("illumina", 1)])
+def test_fqz_decoder_paths_roundtrip(kind, strat):
+    """Blocks long enough that hot models halve many times (FL_MAX) and the
+    decoder's fast run leaves for the reference arithmetic, the cache
+    misses and the input refills mid-run; with sequence context (strats 3
+    and 4) the run's context state must survive every such exit."""
+    from fqzcomp5_amd import synth
+    r = {"novaseq": lambda: synth.novaseq(12000, seed=9),
+         "illumina": lambda: synth.illumina(12000, seed=9),
+         "ont": lambda: synth.ont(160, seed=9),
+         "hifi": lambda: synth.hifi(40, seed=9)}[kind]()
+    q, lens, seq = r.qual.tobytes(), r.lens.astype(np.uint32), r.seq.tobytes()
+    flags = np.asarray(r.flags if getattr(r, "flags", None) is not None
+                       else np.zeros(len(lens)), np.uint32)
+    got = lib.fqz_compress(q, lens.copy(), flags.copy(), strat, seq)
+    back, _ = lib.fqz_decompress(got, lens.copy(), flags.copy(), seq)
+    assert back == q
+
+
 def test_fqz_large_roundtrip(golden):
     cs, vec, _ = golden
     name, q, lens, flags, seq = cs["bin8_big"]
