@@ -72,6 +72,8 @@ FASTQ_REC = 358          # bytes of FASTQ text per synthetic 150 bp record (avg)
 GAP_S = float(os.environ.get("FQZ5_BENCH_GAP_S", "0") or 0)
 BLK = 100_000_000        # -3 / -5 block size (fqzcomp5.c:4896,4904)
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8 TB/s spec
+# fqz5_profile_read_all's kernels (include/fqz5_mi355x.h)
+PROF_KERNELS = ["k_enc_chain", "k_rans_dec", "k_fqz_dec", "k_fqz_rc", "k_seq_dec"]
 
 
 def log(*a):
@@ -155,15 +157,50 @@ def cpu_baseline(fastq: str, level: int, threads: int, gpu_blocks, exe_name="fqz
             "fqz5_bytes": fsize, "blocks_match_gpu": bool(same), "roundtrip": bool(rt)}
 
 
+def t1_check(reads, blocks, level, gpu_blocks, nblk: int, timeout: int = 900):
+    """The reference CLI with one thread (-t1: its trial runs in file order,
+    fqzcomp5.c:1911-1913) on the workload's first `nblk` blocks, their bytes
+    compared with the GPU's first blocks.  The multi-threaded reference run
+    of cpu_baseline decides its trial by timing, so its blocks can differ
+    from -t1 ones; this is the deterministic comparison."""
+    import tempfile
+    from fqzcomp5_amd import synth
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import fqz5_container as F
+    exe = os.path.join(ROOT, "oracle", "_ref", "fqzcomp5")
+    if not os.path.exists(exe):
+        return {"error": "oracle/_ref/fqzcomp5 not built"}
+    from fqzcomp5_amd import sections as S
+    nblk = min(nblk, len(blocks))
+    try:
+        with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+            src, out = os.path.join(td, "t1.fastq"), os.path.join(td, "t1.fqz5")
+            with open(src, "wb") as f:
+                f.write(synth.fastq_chunk(reads, blocks[0][0], blocks[nblk - 1][1]).tobytes())
+            bs = BLK if level in (3, 5) else S.BLOCK_SIZE[level]
+            t0 = time.perf_counter()
+            subprocess.run([exe, f"-{level}", "-t1", "-b", str(bs), src, out], check=True,
+                           capture_output=True, timeout=timeout)
+            t1 = time.perf_counter()
+            raw = F.raw_blocks(out)
+        same = [bool(a == b) for a, b in zip(raw, gpu_blocks[:nblk])]
+        return {"blocks": nblk, "blocks_match_gpu": same, "all_match": all(same) and len(raw) == nblk,
+                "ref_enc_s": round(t1 - t0, 2),
+                "cmd": f"oracle/_ref/fqzcomp5 -{level} -t1 -b {bs} (first {nblk} blocks)"}
+    except Exception as e:       # never lose the line for the check
+        return {"error": str(e)[-300:]}
+
+
 def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local, dist,
-            scaling="weak", pmc_tag="", dropin=False):
+            scaling="weak", pmc_tag="", dropin=False, t1_blocks=0):
     """One workload: warmup + `steps` timed steps (barrier + synchronize on
     both sides, max over ranks) and the result fields of its JSON line."""
     import torch
     from fqzcomp5_amd import lib, sections as S, synth
 
     t0 = time.time()
-    seed = (1 if level <= 3 else 2) + (rank if scaling == "weak" else 0)
+    # configs[1]'s seed for its Illumina data at any level, configs[2]'s otherwise
+    seed = (1 if level <= 3 or kind == "illumina" else 2) + (rank if scaling == "weak" else 0)
     reads = make_reads(gb, seed, kind)
     blocks = synth.split_blocks(reads, BLK if level in (3, 5) else S.BLOCK_SIZE[level])
     if scaling == "strong":                      # contiguous shard of one file
@@ -222,6 +259,8 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     dt = time.perf_counter() - t0
     prof = (C.c_double * 6)()
     so.fqz5_profile_read(prof)
+    kprof = (C.c_double * (3 * len(PROF_KERNELS)))()
+    so.fqz5_profile_read_all(kprof, len(PROF_KERNELS))
     so.fqz5_profile(0)
     fq1 = S.trial_counts()
     arena1 = lib.arena_bytes()
@@ -277,11 +316,16 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                    "fqz_trial": {"tried": fq1[0] - fq0[0], "pruned": fq1[1] - fq0[1]}},
     }
     # ---- roofline of the dominant kernel ---------------------------------
+    # every chain kernel's launch time from HIP events on the stream it runs
+    # on (fqz5_profile_read_all: rANS encode / decode, fqz decode, the fqz
+    # and sequence-model range chain, sequence-model decode); the dominant
+    # one is the kernel with the most time in the timed steps
     enc_ms, enc_n, enc_b, dec_ms, dec_n, dec_b = list(prof)
-    if enc_ms >= dec_ms:
-        name, ms, n, b = "k_enc_chain", enc_ms, enc_n, enc_b
-    else:
-        name, ms, n, b = "k_rans_dec", dec_ms, dec_n, dec_b
+    kp = list(kprof)
+    per_kernel = {k: {"ms": round(kp[3 * i], 3), "launches": int(kp[3 * i + 1]),
+                      "bytes": int(kp[3 * i + 2])} for i, k in enumerate(PROF_KERNELS)}
+    name = max(PROF_KERNELS, key=lambda k: per_kernel[k]["ms"])
+    ms, n, b = per_kernel[name]["ms"], per_kernel[name]["launches"], per_kernel[name]["bytes"]
     avg_ms = ms / max(n, 1)
     ach = (b / max(n, 1)) / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
     traffic, tsrc = pmc_traffic(name, pmc_tag)
@@ -295,6 +339,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                        "bytes_per_launch": int(b / max(n, 1)),
                        "enc_avg_ms": round(enc_ms / max(enc_n, 1), 3),
                        "dec_avg_ms": round(dec_ms / max(dec_n, 1), 3),
+                       "kernels": per_kernel,
                        "chains": {"streams_per_launch": len(run.spans),
                                   "longest_stream_steps": longest // 4,
                                   "dec_ns_per_step_longest": round(
@@ -318,6 +363,8 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                 out["cpu_baseline"] = {"error": str(e)[-300:]}
             if dropin:
                 out["dropin_cli"] = dropin_item(fastq, level, cpu_threads)
+        if t1_blocks:
+            out["cpu_baseline"]["t1_blocks"] = t1_check(reads, blocks, level, gpu_blocks, t1_blocks)
     del run, reads
     torch.cuda.empty_cache()
     return out
@@ -469,7 +516,7 @@ def main():
 
     m = measure(args.level, args.kind, args.gb, args.steps, args.warmup, not args.no_cpu,
                 threads, world, rank, local, dist, scaling=args.scaling,
-                pmc_tag="_l5" if args.level == 5 else "",
+                pmc_tag="" if args.level == 3 else f"_l{args.level}",
                 dropin=not args.no_dropin and args.level == 3)
     out = {"metric": "input MB/s encode+decode, 100MB blocks, -3 and -5; bit-exact vs CPU",
            "value": m["value"], "unit": "MB/s", "n_gpus": world, "steps": args.steps,
@@ -489,7 +536,18 @@ def main():
     if not args.no_level5 and args.level == 3:
         out["level5"] = measure(5, "novaseq", 4.0 if args.scaling == "weak" else 4.0 * world,
                                 args.steps, args.warmup, not args.no_cpu, threads, world,
-                                rank, local, dist, scaling=args.scaling, pmc_tag="_l5")
+                                rank, local, dist, scaling=args.scaling, pmc_tag="_l5",
+                                t1_blocks=4)
+        # -5 on configs[1]'s data: the random-walk binned Illumina qualities,
+        # where the trial picks fqz (FQZ1/FQZ3, fqzcomp5.c:4906-4907), so the
+        # fqz range coder and decoder are in the timed region; each block's
+        # quality section is one fqz chain, so a step lasts about one block's
+        # decode: fewer steps
+        out["level5_illumina"] = measure(5, "illumina", args.gb if args.scaling == "weak"
+                                         else args.gb * world, min(args.steps, 2),
+                                         min(args.warmup, 1), not args.no_cpu, threads, world,
+                                         rank, local, dist, scaling=args.scaling,
+                                         pmc_tag="_l5i", t1_blocks=4)
     if rank == 0 and world == 1 and not args.no_crc:
         out["crc32"] = crc_item(lib, torch)
     if rank == 0:

@@ -37,6 +37,18 @@ __attribute__((constructor)) static void hw_queues_default() {
 }
 
 static thread_local std::string g_err;
+
+// the process-wide kernel profile (gpu_ctx.hpp: ProfKernel)
+static std::mutex g_prof_mu;
+static double g_prof[PK_N][3];
+static std::atomic<bool> g_prof_on{false};
+void prof_add(int kernel, double ms, double bytes) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof[kernel][0] += ms;
+    g_prof[kernel][1] += 1;
+    g_prof[kernel][2] += bytes;
+}
+bool prof_on() { return g_prof_on.load(); }
 static thread_local std::unique_ptr<GpuCtx> g_ctx;
 
 GpuCtx &gpu() {
@@ -352,9 +364,22 @@ void fqz5_profile(int on) {
         GpuCtx &g = gpu();
         g.prof = KernelProfile();
         g.prof.on = on != 0;
+        {
+            std::lock_guard<std::mutex> lk(g_prof_mu);
+            for (int k = 0; k < PK_N; k++) g_prof[k][0] = g_prof[k][1] = g_prof[k][2] = 0;
+        }
+        g_prof_on.store(on != 0);
     } catch (const std::exception &e) {
         g_err = e.what();
     }
+}
+
+int fqz5_profile_read_all(double *out, int nk) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    const int n = nk < int(PK_N) ? nk : int(PK_N);
+    for (int k = 0; k < n; k++)
+        for (int j = 0; j < 3; j++) out[3 * k + j] = g_prof[k][j];
+    return int(PK_N);
 }
 
 void fqz5_profile_read(double *out6) {

@@ -635,7 +635,9 @@ void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
         for (size_t k = 0; k < rj.size(); k++) rj[k].done = d_done + k;
         for (size_t c = 1; c < copies; c++) rj.insert(rj.end(), rj.begin(), rj.begin() + long(np));
     }
+    EventPair ev(prof_on(), g.stream);
     FQZ5_HIP(launch_fqz_rc(g.upload(rj), int(rj.size()), g.stream));
+    ev.stop(g.stream);
     std::vector<uint32_t> P(size_t(np), 0);
     for (int k = 0; k < np; k++) {
         FqzEvJob &J = *js[size_t(k)];
@@ -650,6 +652,11 @@ void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
         g.download(&P[size_t(k)], pos + J.nev, 1);
     }
     g.sync();
+    if (ev.on) {   // 16 B of event record in, q and the byte-shift count out per event
+        double ev_n = 0;
+        for (FqzEvJob *J : js) ev_n += J->nev;
+        prof_add(PK_FQZ_RC, ev.ms(), ev_n * 21.0);
+    }
     std::vector<FqzEvJob> cj;
     for (int k = 0; k < np; k++) {
         FqzEvJob &J = *js[size_t(k)];
@@ -834,9 +841,18 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
                     for (FqzDecReq *R : rs)
                         if (R->w->ne == ne && int(R->w->seq_ctx) == sq && int(R->w->qid) == qi)
                             js.push_back(R->w->D);
-                    if (!js.empty())
+                    if (!js.empty()) {
+                        EventPair ev(prof_on(), g.stream);
                         FQZ5_HIP(launch_fqz_dec(g.upload(js), int(js.size()), ne, sq != 0,
                                                 qi != 0, g.stream));
+                        ev.stop(g.stream);
+                        if (ev.on) {   // compressed bytes in, quality bytes out
+                            g.sync();
+                            double b = 0;
+                            for (const FqzDecJob &J : js) b += double(J.in_len) + double(J.n);
+                            prof_add(PK_FQZ_DEC, ev.ms(), b);
+                        }
+                    }
                 }
         for (FqzDecReq *R : rs) {
             FqzDecReq::Work &W = *R->w;
@@ -865,9 +881,11 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
             std::fprintf(stderr, "[fqz dec] n=%u ment=%u sets=%u recs=%u dups=%u revs=%u misses=%u slow=%u\n",
                          W.total, W.D.ment, W.D.nsets, c[0], c[1], c[2], c[3], c[4]);
             if (pr[0] | pr[1])
-                std::fprintf(stderr, "[fqz dec] cycles/symbol: wait %.1f chain %.1f coder %.1f update %.1f tail %.1f loop %.1f\n",
-                             double(pr[0]) / W.total, double(pr[1]) / W.total, double(pr[2]) / W.total,
-                             double(pr[3]) / W.total, double(pr[4]) / W.total, double(pr[5]) / W.total);
+                std::fprintf(stderr, "[fqz dec] probe: %.1f cycles/symbol inside the run asm over %llu symbols "
+                             "(%.1f%% of %u), %llu asm calls; raw %llu %llu %llu\n",
+                             double(pr[0]) / double(pr[1] ? pr[1] : 1), (unsigned long long)pr[1],
+                             100.0 * double(pr[1]) / W.total, W.total, (unsigned long long)pr[2],
+                             (unsigned long long)pr[3], (unsigned long long)pr[4], (unsigned long long)pr[5]);
         }
     std::vector<std::vector<uint32_t>> lens(live.size());
     for (size_t i = 0; i < live.size(); i++) {

@@ -791,11 +791,20 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                   [cbig] "v"(cbig), [c19] "v"(c19), [vme] "v"(vme), [pvv] "v"(pvv),          \
                   [dvv] "v"(dvv), [sqv] "v"(sqv)                                              \
                 : "memory", "scc"
+#ifdef FQZ5_DEC_PROBE
+                const uint32_t done_in = done;
+                const uint64_t ta = __builtin_amdgcn_s_memtime();
+#endif
                 if constexpr (QID && SEQ) asm volatile(FQZ_RUN_ASM(FQZ_QT_QID, FQZ_SEQ_CTX, FQZ_SEQ_COMMIT) FQZ_RUN_OPERANDS);
                 else if constexpr (QID) asm volatile(FQZ_RUN_ASM(FQZ_QT_QID, FQZ_SEQ_NONE, FQZ_SEQ_NONE) FQZ_RUN_OPERANDS);
                 else if constexpr (SEQ) asm volatile(FQZ_RUN_ASM(FQZ_QT_TAB, FQZ_SEQ_CTX, FQZ_SEQ_COMMIT) FQZ_RUN_OPERANDS);
                 else asm volatile(FQZ_RUN_ASM(FQZ_QT_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE) FQZ_RUN_OPERANDS);
 #undef FQZ_RUN_OPERANDS
+#ifdef FQZ5_DEC_PROBE
+                pr[0] += __builtin_amdgcn_s_memtime() - ta;   // cycles inside the run asm
+                pr[1] += U(done) - done_in;                   // symbols it decoded
+                pr[2] += 1;                                   // calls
+#endif
                 // (the compiler takes every output of an asm with VGPR outputs
                 // for divergent: the scalar ones are re-read as uniform)
                 rng = U(rng);

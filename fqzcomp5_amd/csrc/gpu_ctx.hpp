@@ -108,8 +108,16 @@ class PinnedArena {
     size_t cur_ = 0;
 };
 
-// Live per-kernel timing (HIP events on the context stream), read by the
-// benchmark for the roofline of the rANS chain kernels.
+// Live per-kernel timing (HIP events on the launching context's stream),
+// read by the benchmark to find the dominant kernel of a step and its
+// roofline.  One process-wide table of the chain kernels of every codec
+// family, filled from every context (helper contexts included) while
+// fqz5_profile(1) is on: launch time, launches, algorithmic bytes (the
+// kernel's input plus output of its jobs).
+enum ProfKernel { PK_ENC_CHAIN, PK_RANS_DEC, PK_FQZ_DEC, PK_FQZ_RC, PK_SEQ_DEC, PK_N };
+void prof_add(int kernel, double ms, double bytes);
+bool prof_on();
+
 struct KernelProfile {
     bool on = false;
     double enc_ms = 0, dec_ms = 0;

@@ -619,7 +619,7 @@ void Compressor::stage_encode() {
         eall.push_back(e);
         lds_r = std::max(lds_r, enc_replay_lds_bytes(j.o1, uint32_t(j.A)));
     }
-    EventPair ev(g_.prof.on && !order.empty(), g_.stream);
+    EventPair ev((g_.prof.on || prof_on()) && !order.empty(), g_.stream);
     lds_s = g_.chain_lds(lds_s, ejs.size() + ejb.size());
     lds_b = g_.chain_lds(lds_b, ejs.size() + ejb.size());
     if (!ejs.empty()) {
@@ -647,9 +647,13 @@ void Compressor::stage_encode() {
     g_.sync();
     const double td = trace ? now() : 0;
     if (ev.on) {
-        g_.prof.enc_ms += ev.ms();
+        const double ms = ev.ms();
+        double bytes = 0;
+        for (int i : order) bytes += double(jobs_[i].n) + lens[i];
+        g_.prof.enc_ms += ms;
         g_.prof.enc_launches += 1;
-        for (int i : order) g_.prof.enc_bytes += double(jobs_[i].n) + lens[i];
+        g_.prof.enc_bytes += bytes;
+        if (prof_on()) prof_add(PK_ENC_CHAIN, ms, bytes);
     }
     for (size_t i = 0; i < jobs_.size(); i++) jobs_[i].payload = jobs_[i].n ? lens[i] : 0;
     for (size_t i = nmain; i < jobs_.size(); i++) finish_job(jobs_[i]);

@@ -391,7 +391,7 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
         bytes += double(j.n) + (j.len - j.tab_len);
         lds = std::max(lds, dec_lds_bytes(rows, j.bits, int(mode)));
     }
-    EventPair ev(g_.prof.on && !ord.empty(), g_.stream);
+    EventPair ev((g_.prof.on || prof_on()) && !ord.empty(), g_.stream);
     // hedge: the long streams several times on different CUs, while the
     // copies fit one per CU (hedge_plan)
     std::vector<uint64_t> steps;
@@ -425,9 +425,11 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
     g_.download(st.data(), d_status, st.size());
     g_.sync();
     if (ev.on) {
-        g_.prof.dec_ms += ev.ms();
+        const double ms = ev.ms();
+        g_.prof.dec_ms += ms;
         g_.prof.dec_launches += 1;
         g_.prof.dec_bytes += bytes;
+        if (prof_on()) prof_add(PK_RANS_DEC, ms, bytes);
     }
     for (size_t k = 0; k < used.size(); k++)
         if (st[k]) djs_[used[k]].ok = false;

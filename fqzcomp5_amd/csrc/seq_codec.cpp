@@ -219,10 +219,17 @@ void seq_decode_batch(GpuCtx &g, std::vector<SeqDecReq> &reqs) {
         who.push_back(i);
     }
     if (js.empty()) return;
+    EventPair ev(prof_on(), g.stream);
     FQZ5_HIP(launch_seq_dec(g.upload(js), int(js.size()), g.stream));
+    ev.stop(g.stream);
     std::vector<int32_t> st(js.size(), -1);
     for (size_t k = 0; k < js.size(); k++) g.download(&st[k], js[k].status, 1);
     g.sync();
+    if (ev.on) {   // compressed bytes in, bases out
+        double b = 0;
+        for (const SeqDecJob &J : js) b += double(J.in_len) + double(J.n);
+        prof_add(PK_SEQ_DEC, ev.ms(), b);
+    }
     for (size_t k = 0; k < js.size(); k++) reqs[who[k]].ok = st[k] == 0;
 }
 

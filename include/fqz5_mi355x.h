@@ -247,6 +247,13 @@ uint64_t fqz5_arena_bytes(void);
 void fqz5_profile(int on);
 void fqz5_profile_read(double *out6);
 
+/* The chain kernels of every codec family, from every context of the
+ * process (helper contexts included) since fqz5_profile(1): per kernel
+ * {launch ms, launches, algorithmic bytes} in the order k_enc_chain (rANS
+ * encode), k_rans_dec, k_fqz_dec, k_fqz_rc (fqz and sequence-model range
+ * chains), k_seq_dec.  Fills min(nk, count) kernels; returns the count. */
+int fqz5_profile_read_all(double *out, int nk);
+
 /* fqz encoder: quality models with at least `min_events` events in a block
  * are run one wavefront per model (the list in lanes); smaller ones one
  * lane per model.  0 disables the per-model wavefronts; the default is
