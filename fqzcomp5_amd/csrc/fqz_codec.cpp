@@ -819,7 +819,7 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
             W.seq_ctx = W.seq_ctx || pm.bbits > 0;
             W.dedup = W.dedup || pm.dedup;
             for (int i = 0; i < 256; i++) {
-                W.qid = W.qid && (pm.qtab[i] & 0xffffu) == unsigned(i);
+                W.qid = W.qid && (pm.qtab[i] & 0xffffu) == (G.p[0].qtab[i] & 0xffffu);   // one shared qtab
                 W.map_mode = W.map_mode || pm.qmap[i] != unsigned(i);
             }
         }

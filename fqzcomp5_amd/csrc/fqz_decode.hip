@@ -41,7 +41,6 @@ namespace {
 constexpr uint32_t RING = 4096, HALF = 2048;   // staged input bytes
 constexpr uint32_t OBUF = 4096;                // output page
 constexpr uint32_t SEQB = 2048;                // staged sequence bases
-constexpr uint32_t TAG_EMPTY = 0xffffffffu;
 constexpr uint32_t PBYTES = 3072;              // qtab u16[256], ptab u16[1024], dtab u16[256]
 constexpr uint32_t P_QTAB = 0, P_PTAB = 512, P_DTAB = 2560;
 
@@ -219,196 +218,240 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 
 
 // ---------------------------------------------------------------------------
-// The fast run of k_fqz_dec<NE = 1> as one hand-scheduled loop (a symbol per
-// iteration).  The model of the current context is in v (lane j: dword j of
-// the cached model: tag, freq | cum << 16 per slot, sentinel copies) and s
-// (lane j: the symbol of slot j).  Per symbol:
+// The fast run of k_fqz_dec<NE = 1> as one hand-scheduled loop, a symbol per
+// iteration.  The model of the current context sits in a VGPR pair, lane j
+// holding slot j (e = freq | cum << 16 in the low register, w = qtab value |
+// symbol << 24 in the high one), with the sentinel (e = context | total <<
+// 16) broadcast to every lane in tv.  Per symbol:
 //   u       the context terms of this position and delta (pvv / dvv lanes)
-//   total   the sentinel's cum; q = floor(range / total) from RN(1/total);
-//           a total that the +16 would take past FL_MAX leaves (flags 2)
+//   q       floor(range / total) from RN(1/total) (rcp + one Newton step)
 //   p_j     cum_j * q;  G = lanes with p_j > code;  kl = first of G - 1
-//   every lane j: the context its symbol would lead to (fqz_update_ctx), its
-//           cache set and whether that set holds it (the tag), qctx << qshift,
-//           and whether the bump would bubble slot j over slot j-1
+//   every lane j: the context its symbol leads to (fqz_update_ctx), that
+//           context's cache set, qctx << qshift, whether it is this context
+//           again (SM), and whether the bump would bubble slot j over j-1
+//   the next model's read is issued from lane kl's set as soon as kl is
+//   known, into the other register pair; the checks (a total that the +16
+//   would take past FL_MAX, the sentinel's context not the current one,
+//   t >= total) leave with flags 2 before any state changes
 //   bump    +16 to lane kl's frequency and every later cum; one bubble step
-//           by DPP lane shifts when it swaps
-//   the model is written back, the next context's read issued (a context
-//   not in the cache leaves, flags 1, after the symbol), and the range coder
-//   (c_range_coder.h RC_Decode: code -= cum q, range = freq q, renormalise)
-//   and the context state run while the read is in flight.
-// It leaves after `lim` symbols or when the input window needs a refill.
-// gfx950 wait states: an SGPR written by a VALU compare and read as a VALU
-// mask gets two, DPP reads of a VGPR written by the VALU two, M0 before the
-// writelane one.
+//           by DPP lane shifts when it swaps; the model is written back
+//   coder   c_range_coder.h RC_Decode: code -= cum q, range = freq q,
+//           renormalise by whole bytes from the 64-bit window
+// Two register pairs (A: v[2:3], B: v[4:5]) and two copies of the scalar
+// state that a context change replaces (context, qctx << qshift, previous
+// symbol, model address, sequence context): iteration X moves into Y when
+// the context changes and loops on itself when it repeats.  code is s41 with
+// s40 its scratch ({s40, s41} << z brings the window's top bits in), the
+// window is s[42:43].  m0 counts the run's symbols (lane selects).
+// It leaves after `lim` symbols or when the input window needs a refill,
+// writing the current model back (unless its sentinel names another
+// context: the read of a context that shares the set).
+// gfx950 wait states: DPP reads of a VGPR written by the VALU get two, an
+// SGPR written by the SALU and read as a VALU mask two (s_nop 1).
 // ---------------------------------------------------------------------------
-#define FQZ_QT_QID                                                          \
-    "v_add_u32 %[t0], %[qs], %[s]\n"
-#define FQZ_QT_TAB                                                          \
-    "v_lshl_add_u32 %[t0], %[s], 1, %[qtab]\n"                              \
-    "ds_read_u16 %[t0], %[t0]\n"                                            \
+#define FQZ_QT1_W(WX) ""
+#define FQZ_QT2_W(X, WX) "v_add_u32 %[t0], %[qs" X "], " WX "\n"
+#define FQZ_QT1_TAB(WX)                                                     \
+    "v_lshrrev_b32 %[t0], 24, " WX "\n"                                     \
+    "v_lshl_add_u32 %[t0], %[t0], 1, %[qtab]\n"                             \
+    "ds_read_u16 %[t0], %[t0]\n"
+#define FQZ_QT2_TAB(X, WX)                                                  \
     "s_waitcnt lgkmcnt(0)\n"                                                \
-    "v_add_u32 %[t0], %[qs], %[t0]\n"
-#define FQZ_SEQ_NONE ""
-#define FQZ_SEQ_CTX                                                         \
-    "v_readlane_b32 %[x], %[sqv], %[done]\n"                                \
-    "s_lshl_b32 %[sn], %[seq], 2\n"                                         \
-    "s_or_b32 %[sn], %[sn], %[x]\n"                                         \
-    "s_and_b32 %[sn], %[sn], %[bmask]\n"                                    \
-    "s_lshl_b32 %[x], %[sn], %[bloc]\n"                                     \
+    "v_add_u32 %[t0], %[qs" X "], %[t0]\n"
+#define FQZ_SEQ_NONE(X, Y) ""
+#define FQZ_SEQ_CTX(X, Y)                                                   \
+    "v_readlane_b32 %[x], %[sqv], m0\n"                                     \
+    "s_lshl_b32 %[sq" Y "], %[sq" X "], 2\n"                                \
+    "s_or_b32 %[sq" Y "], %[sq" Y "], %[x]\n"                               \
+    "s_and_b32 %[sq" Y "], %[sq" Y "], %[bmask]\n"                          \
+    "s_lshl_b32 %[x], %[sq" Y "], %[bloc]\n"                                \
     "s_add_u32 %[u], %[u], %[x]\n"
-#define FQZ_SEQ_COMMIT "s_mov_b32 %[seq], %[sn]\n"
-// the coded slot's update (fl_bump): +16 to lane kl's frequency (E) and to
-// every later cum (G); one bubble step (SW & E) by DPP lane shifts
-#define FQZ_BUMP_SWAP                                                       \
-    "v_cndmask_b32 %[t4], 0, 16, %[E]\n"                                    \
-    "v_cndmask_b32 %[t4], %[t4], %[cbig], %[G]\n"                           \
-    "s_and_b64 %[SW], %[SW], %[E]\n"                                        \
-    "v_add_u32 %[v], %[v], %[t4]\n"                                         \
-    "s_cbranch_scc0 3f\n"                                                   \
-    "s_nop 1\n"                                                             \
-    "v_mov_b32_dpp %[t4], %[v] wave_shr:1 row_mask:0xf bank_mask:0xf\n"     \
-    "v_mov_b32_dpp %[t5], %[v] wave_shl:1 row_mask:0xf bank_mask:0xf\n"     \
-    "v_mov_b32_dpp %[t6], %[s] wave_shr:1 row_mask:0xf bank_mask:0xf\n"     \
-    "v_mov_b32_dpp %[t7], %[s] wave_shl:1 row_mask:0xf bank_mask:0xf\n"     \
-    "v_and_b32 %[t3], 0xffff, %[v]\n"                                       \
-    "v_lshrrev_b32 %[t2], 16, %[t4]\n"                                      \
-    "v_add_u32 %[t3], %[t3], %[t2]\n"                                       \
-    "v_and_b32 %[t2], 0xffff, %[t4]\n"                                      \
-    "v_lshl_or_b32 %[t3], %[t3], 16, %[t2]\n"                               \
-    "v_and_b32 %[t2], 0xffff0000, %[v]\n"                                   \
-    "v_and_b32 %[t5], 0xffff, %[t5]\n"                                      \
-    "v_or_b32 %[t5], %[t5], %[t2]\n"                                        \
-    "s_lshr_b64 %[SW], %[E], 1\n"                                           \
-    "v_cndmask_b32 %[v], %[v], %[t3], %[E]\n"                               \
-    "v_cndmask_b32 %[s], %[s], %[t6], %[E]\n"                               \
-    "s_nop 1\n"                                                             \
-    "v_cndmask_b32 %[v], %[v], %[t5], %[SW]\n"                              \
-    "v_cndmask_b32 %[s], %[s], %[t7], %[SW]\n"                              \
-    "3:\n"
-// the range coder (c_range_coder.h RC_Decode) and the context state
-#define FQZ_CODER_STATE(SEQCOMMIT)                                          \
-    "s_sub_u32 %[code], %[code], %[pk]\n"                                   \
-    "s_sub_u32 %[rng], %[pk1], %[pk]\n"                                     \
-    "s_flbit_i32_b32 %[z], %[rng]\n"                                        \
-    "s_lshr_b32 %[nxk], %[nxk], 24\n"                                       \
-    "s_mov_b32 m0, %[done]\n"                                               \
-    "s_and_b32 %[z], %[z], 24\n"                                            \
-    "s_cmp_lg_u32 %[prevq], %[nxk]\n"                                       \
-    "s_addc_u32 %[delta], %[delta], 0\n"                                    \
-    "v_writelane_b32 %[vout], %[nxk], m0\n"                                 \
-    "s_mov_b32 %[prevq], %[nxk]\n"                                          \
-    "s_mov_b32 %[qs], %[qsk]\n"                                             \
-    SEQCOMMIT                                                               \
-    "s_cmp_eq_u32 %[z], 0\n"                                                \
-    "s_cbranch_scc1 5f\n"                                                   \
-    "s_lshl_b32 %[rng], %[rng], %[z]\n"                                     \
-    "s_sub_u32 %[x], 32, %[z]\n"                                            \
-    "s_lshr_b32 %[tot], %[whi], %[x]\n"                                     \
-    "s_lshl_b32 %[code], %[code], %[z]\n"                                   \
-    "s_or_b32 %[code], %[code], %[tot]\n"                                   \
-    "s_lshr_b32 %[tot], %[wlo], %[x]\n"                                     \
-    "s_lshl_b32 %[whi], %[whi], %[z]\n"                                     \
-    "s_or_b32 %[whi], %[whi], %[tot]\n"                                     \
-    "s_lshl_b32 %[wlo], %[wlo], %[z]\n"                                     \
-    "s_add_u32 %[ub], %[ub], %[z]\n"                                        \
-    "5:\n"                                                                  \
-    "s_add_u32 %[done], %[done], 1\n"
-#define FQZ_RUN_ASM(QT, SEQCTX, SEQCOMMIT)                                  \
-    "s_mov_b32 %[m0s], m0\n"                                                \
-    "1:\n"                                                                  \
-    "v_readlane_b32 %[u], %[pvv], %[done]\n"                                \
-    "s_sub_u32 %[x], %[delta], %[delta0]\n"                                 \
-    "v_readlane_b32 %[tot], %[v], 63\n"                                     \
+#define FQZ_SEQ_SAME(X, Y) "s_mov_b32 %[sq" X "], %[sq" Y "]\n"
+// the symbol's decode and the next context's hypotheses; leaves for SAMEL
+// when the context repeats
+#define FQZ_TOP(X, Y, EX, WX, QT1, QT2, SEQCTX, SAMEL)                      \
+    "v_readlane_b32 %[u], %[pvv], m0\n"                                     \
+    "v_readlane_b32 %[x], %[dvv], %[dd]\n"                                  \
     "v_cvt_f64_u32 %[d0], %[rng]\n"                                         \
-    "v_readlane_b32 %[x], %[dvv], %[x]\n"                                   \
-    "s_lshr_b32 %[tot], %[tot], 16\n"                                       \
-    "s_add_u32 %[u], %[u], %[x]\n"                                          \
-    SEQCTX                                                                  \
-    "s_cmpk_gt_u32 %[tot], 65503\n"                                         \
-    "s_cbranch_scc1 2f\n"                                                   \
-    "v_cvt_f64_u32 %[d1], %[tot]\n"                                         \
-    QT                                                                      \
-    "v_rcp_f64 %[d2], %[d1]\n"                                              \
-    "v_and_b32 %[t1], %[qmask], %[t0]\n"                                    \
-    "v_lshlrev_b32 %[t1], %[qloc], %[t1]\n"                                 \
-    "v_add_u32 %[t1], %[u], %[t1]\n"                                        \
-    "v_and_b32 %[t1], 0xffff, %[t1]\n"                                      \
-    "v_fma_f64 %[d1], -%[d1], %[d2], 1.0\n"                                 \
-    "v_mul_u32_u24 %[t2], 0x9e3779, %[t1]\n"                                \
-    "v_fma_f64 %[d2], %[d2], %[d1], %[d2]\n"                                \
-    "v_lshrrev_b32 %[t2], 8, %[t2]\n"                                       \
-    "v_fma_f64 %[d0], %[d0], %[d2], %[c19]\n"                               \
-    "v_mul_hi_u32_u24 %[t2], %[ns8], %[t2]\n"                               \
-    "v_cvt_u32_f64 %[t3], %[d0]\n"                                          \
-    "v_mad_u32_u24 %[t2], %[t2], %[vme], %[base]\n"                         \
-    "v_lshrrev_b32 %[t4], 16, %[v]\n"                                       \
-    "ds_read_b32 %[t5], %[t2]\n"                                            \
-    "v_mul_lo_u32 %[t3], %[t4], %[t3]\n"                                    \
-    "v_lshl_or_b32 %[t7], %[s], 24, %[t2]\n"                                \
-    "v_lshlrev_b32 %[t0], %[qshift], %[t0]\n"                               \
-    "v_and_b32 %[t4], 0xffff, %[v]\n"                                       \
-    "v_mov_b32_dpp %[t6], %[v] wave_shr:1 row_mask:0xf bank_mask:0xf\n"     \
-    "v_cmp_gt_u32 %[G], %[t3], %[code]\n"                                   \
-    "v_add_u32 %[t4], 16, %[t4]\n"                                          \
-    "v_and_b32 %[t6], 0xffff, %[t6]\n"                                      \
-    "v_cmp_gt_u32 %[SW], %[t4], %[t6]\n"                                    \
     "s_waitcnt lgkmcnt(0)\n"                                                \
-    "v_cmp_eq_u32 %[H], %[t5], %[t1]\n"                                     \
-    "s_cmp_eq_u64 %[G], 0\n"                                                \
-    "s_cbranch_scc1 2f\n"                                                   \
+    "v_lshrrev_b32 %[t6], 16, %[tv" X "]\n"                                 \
+    QT1(WX)                                                                 \
+    "s_add_u32 %[u], %[u], %[x]\n"                                          \
+    "v_cvt_f64_u32 %[d1], %[t6]\n"                                          \
+    SEQCTX(X, Y)                                                            \
+    "v_cmp_ne_u16_e64 %[TG], %[c" X "], %[tv" X "]\n"                       \
+    "v_rcp_f64 %[d2], %[d1]\n"                                              \
+    "v_cmp_lt_u32_e64 %[HV], %[c65503], %[t6]\n"                            \
+    "v_lshrrev_b32 %[t4], 16, " EX "\n"                                     \
+    "v_fma_f64 %[d1], -%[d1], %[d2], 1.0\n"                                 \
+    QT2(X, WX)                                                              \
+    "v_add_u16 %[t5], 16, " EX "\n"                                         \
+    "v_fma_f64 %[d2], %[d2], %[d1], %[d2]\n"                                \
+    "v_and_b32 %[t1], %[qmask], %[t0]\n"                                    \
+    "v_mov_b32_dpp %[t6], " EX " wave_shr:1 row_mask:0xf bank_mask:0xf\n"   \
+    "v_fma_f64 %[d0], %[d0], %[d2], %[c19]\n"                               \
+    "v_lshl_add_u32 %[t1], %[t1], %[qlocv], %[u]\n"                         \
+    "v_and_b32 %[t1], 0xffff, %[t1]\n"                                      \
+    "v_cvt_u32_f64 %[t3], %[d0]\n"                                          \
+    "v_mul_u32_u24 %[t2], 0x9e3779, %[t1]\n"                                \
+    "v_mul_lo_u32 %[t3], %[t4], %[t3]\n"                                    \
+    "v_lshrrev_b32 %[t2], 8, %[t2]\n"                                       \
+    "v_cmp_eq_u32_e64 %[SM], %[c" X "], %[t1]\n"                            \
+    "v_mul_hi_u32_u24 %[t2], %[ns8], %[t2]\n"                               \
+    "v_cmp_gt_u32_e64 %[G], %[t3], s41\n"                                   \
+    "v_mad_u32_u24 %[t2], %[t2], %[vme], %[base]\n"                         \
+    "v_cmp_lt_u16_e64 %[SW], %[t6], %[t5]\n"                                \
     "s_ff1_i32_b64 %[k1], %[G]\n"                                           \
     "s_lshr_b64 %[E], %[G], 1\n"                                            \
     "s_sub_u32 %[kl], %[k1], 1\n"                                           \
     "s_andn2_b64 %[E], %[E], %[G]\n"                                        \
-    "v_readlane_b32 %[nxk], %[t7], %[kl]\n"                                 \
+    "v_readlane_b32 %[ma" Y "], %[t2], %[kl]\n"                             \
+    "s_and_b64 %[SM], %[SM], %[E]\n"                                        \
+    "s_cbranch_scc1 " SAMEL "\n"
+// the checks; SLOWL leaves with the state unchanged
+#define FQZ_CHECK(SLOWL)                                                    \
+    "s_or_b64 %[TG], %[TG], %[HV]\n"                                        \
+    "s_andn2_b64 %[E], %[E], %[TG]\n"                                       \
+    "s_cbranch_scc0 " SLOWL "\n"
+// the coded slot's update (fl_bump): +16 to lane kl's frequency (E) and to
+// every later cum (G); one bubble step (SW & E) by DPP lane shifts
+#define FQZ_BUMP(EX, WX)                                                    \
+    "v_cndmask_b32 %[t4], 0, 16, %[E]\n"                                    \
+    "v_cndmask_b32 %[t4], %[t4], %[cbig], %[G]\n"                           \
+    "s_and_b64 %[SW], %[SW], %[E]\n"                                        \
+    "v_add_u32 " EX ", " EX ", %[t4]\n"                                     \
+    "s_cbranch_scc0 3f\n"                                                   \
+    "s_nop 1\n"                                                             \
+    "v_mov_b32_dpp %[t4], " EX " wave_shr:1 row_mask:0xf bank_mask:0xf\n"   \
+    "v_mov_b32_dpp %[t5], " EX " wave_shl:1 row_mask:0xf bank_mask:0xf\n"   \
+    "v_mov_b32_dpp %[t6], " WX " wave_shr:1 row_mask:0xf bank_mask:0xf\n"   \
+    "v_mov_b32_dpp %[t1], " WX " wave_shl:1 row_mask:0xf bank_mask:0xf\n"   \
+    "v_and_b32 %[t3], 0xffff, " EX "\n"                                     \
+    "v_lshrrev_b32 %[t2], 16, %[t4]\n"                                      \
+    "v_add_u32 %[t3], %[t3], %[t2]\n"                                       \
+    "v_and_b32 %[t2], 0xffff, %[t4]\n"                                      \
+    "v_lshl_or_b32 %[t3], %[t3], 16, %[t2]\n"                               \
+    "v_and_b32 %[t2], 0xffff0000, " EX "\n"                                 \
+    "v_and_b32 %[t5], 0xffff, %[t5]\n"                                      \
+    "v_or_b32 %[t5], %[t5], %[t2]\n"                                        \
+    "s_lshr_b64 %[SW], %[E], 1\n"                                           \
+    "v_cndmask_b32 " EX ", " EX ", %[t3], %[E]\n"                           \
+    "v_cndmask_b32 " WX ", " WX ", %[t6], %[E]\n"                           \
+    "s_nop 1\n"                                                             \
+    "v_cndmask_b32 " EX ", " EX ", %[t5], %[SW]\n"                          \
+    "v_cndmask_b32 " WX ", " WX ", %[t1], %[SW]\n"                          \
+    "3:\n"
+// the slot's values: range coder terms, qctx, symbol (into pv Y)
+#define FQZ_TAKE(Y, WX)                                                     \
     "v_readlane_b32 %[pk], %[t3], %[kl]\n"                                  \
     "v_readlane_b32 %[pk1], %[t3], %[k1]\n"                                 \
     "v_readlane_b32 %[qsk], %[t0], %[kl]\n"                                 \
-    "s_andn2_b64 %[SW], %[SW], 3\n"                                         \
-    "s_and_b32 %[an], %[nxk], 0xffffff\n"                                   \
-    "s_and_b64 %[H], %[H], %[E]\n"                                          \
-    "s_cselect_b32 %[flags], 0, 1\n"                                        \
-    "s_cbranch_scc0 7f\n"                                                   \
-    "s_cmp_eq_u32 %[an], %[maddr]\n"                                        \
-    "s_cbranch_scc1 8f\n"                                                   \
-    "v_add_u32 %[t4], %[an], %[voff]\n"                                     \
-    "v_add_u32 %[t5], %[an], %[soff]\n"                                     \
-    "ds_read_b32 %[nv], %[t4]\n"                                            \
-    "ds_read_u8 %[ns], %[t5]\n"                                             \
-    "7:\n"                                                                  \
-    FQZ_BUMP_SWAP                                                           \
-    "v_add_u32 %[t2], %[maddr], %[voff]\n"                                  \
-    "v_add_u32 %[t3], %[maddr], %[soff]\n"                                  \
-    "ds_write_b32 %[t2], %[v]\n"                                            \
-    "ds_write_b8 %[t3], %[s]\n"                                             \
-    "s_mov_b32 %[maddr], %[an]\n"                                           \
-    FQZ_CODER_STATE(SEQCOMMIT)                                              \
-    "s_waitcnt lgkmcnt(0)\n"                                                \
-    "s_cmp_lg_u32 %[flags], 0\n"                                            \
-    "s_cbranch_scc1 6f\n"                                                   \
-    "v_mov_b32 %[v], %[nv]\n"                                               \
-    "v_mov_b32 %[s], %[ns]\n"                                               \
-    "s_branch 9f\n"                                                         \
-    "8:\n"                                                                  \
-    FQZ_BUMP_SWAP                                                           \
-    FQZ_CODER_STATE(SEQCOMMIT)                                              \
-    "9:\n"                                                                  \
+    "v_readlane_b32 %[pv" Y "], " WX ", %[kl]\n"
+// renormalise by whole bytes (z = 0, 8, 16 or 24 bits); EXITL when the
+// window needs a refill
+#define FQZ_RENORM(EXITL)                                                   \
+    "s_and_b32 %[z], %[z], 24\n"                                            \
+    "s_cbranch_scc0 4f\n"                                                   \
+    "s_mov_b32 s40, s43\n"                                                  \
+    "s_lshl_b64 s[40:41], s[40:41], %[z]\n"                                 \
+    "s_lshl_b64 s[42:43], s[42:43], %[z]\n"                                 \
+    "s_lshl_b32 %[rng], %[rng], %[z]\n"                                     \
+    "s_add_u32 %[ub], %[ub], %[z]\n"                                        \
     "s_cmp_gt_u32 %[ub], %[ulim]\n"                                         \
-    "s_cbranch_scc1 6f\n"                                                   \
-    "s_cmp_lt_u32 %[done], %[lim]\n"                                        \
-    "s_cbranch_scc1 1b\n"                                                   \
-    "s_branch 6f\n"                                                         \
-    "2:\n"                                                                  \
+    "s_cbranch_scc1 " EXITL "\n"                                            \
+    "4:\n"                                                                  \
+    "s_cmp_lt_u32 m0, %[lim]\n"
+// the coder and the context state; the symbol to output lane m0
+#define FQZ_CODER(X, Y, QSD)                                                \
+    "s_sub_u32 s41, s41, %[pk]\n"                                           \
+    "s_sub_u32 %[rng], %[pk1], %[pk]\n"                                     \
+    "s_lshr_b32 %[pv" Y "], %[pv" Y "], 24\n"                               \
+    "s_flbit_i32_b32 %[z], %[rng]\n"                                        \
+    "s_lshl_b32 %[qs" QSD "], %[qsk], %[qshift]\n"                          \
+    "v_writelane_b32 %[vout], %[pv" Y "], m0\n"                             \
+    "s_cmp_lg_u32 %[pv" X "], %[pv" Y "]\n"                                 \
+    "s_addc_u32 %[dd], %[dd], 0\n"                                          \
+    "s_add_u32 m0, m0, 1\n"
+// context change: the next model into (MY, tv Y), this one written back
+#define FQZ_SWITCH(X, Y, MX, EX, WX, MY, SLOWL, EXITL)                      \
+    "v_add_u32 %[t4], %[ma" Y "], %[voff]\n"                                \
+    "v_add_u32 %[t5], %[ma" Y "], %[vsent]\n"                               \
+    "ds_read_b64 " MY ", %[t4]\n"                                           \
+    "ds_read_b32 %[tv" Y "], %[t5]\n"                                       \
+    FQZ_CHECK(SLOWL)                                                        \
+    "v_readlane_b32 %[c" Y "], %[t1], %[kl]\n"                              \
+    FQZ_TAKE(Y, WX)                                                         \
+    FQZ_BUMP(EX, WX)                                                        \
+    "v_add_u32 %[t2], %[ma" X "], %[voff]\n"                                \
+    "ds_write_b64 %[t2], " MX "\n"                                          \
+    FQZ_CODER(X, Y, Y)                                                      \
+    FQZ_RENORM(EXITL)
+// the same context again: the model stays in (MX, tv X)
+#define FQZ_SAME(X, Y, EX, WX, SEQSAME, SLOWL, EXITL)                       \
+    FQZ_CHECK(SLOWL)                                                        \
+    FQZ_TAKE(Y, WX)                                                         \
+    FQZ_BUMP(EX, WX)                                                        \
+    "v_add_u32 %[tv" X "], %[cbig], %[tv" X "]\n"                           \
+    FQZ_CODER(X, Y, X)                                                      \
+    "s_mov_b32 %[pv" X "], %[pv" Y "]\n"                                    \
+    SEQSAME(X, Y)                                                           \
+    FQZ_RENORM(EXITL)
+#define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME)                              \
+    "s_mov_b32 %[m0s], m0\n"                                                \
+    "s_mov_b32 m0, %[done]\n"                                               \
+    "s_mov_b32 %[flags], 0\n"                                               \
+    "10:\n"                                                                 \
+    FQZ_TOP("A", "B", "v2", "v3", QT1, QT2, SEQCTX, "11f")                  \
+    FQZ_SWITCH("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", "12f", "31f")      \
+    "s_cbranch_scc0 31f\n"                                                  \
+    "20:\n"                                                                 \
+    FQZ_TOP("B", "A", "v4", "v5", QT1, QT2, SEQCTX, "21f")                  \
+    FQZ_SWITCH("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", "22f", "30f")      \
+    "s_cbranch_scc1 10b\n"                                                  \
+    "s_branch 30f\n"                                                        \
+    "11:\n"                                                                 \
+    FQZ_SAME("A", "B", "v2", "v3", SEQSAME, "12f", "30f")                   \
+    "s_cbranch_scc1 10b\n"                                                  \
+    "s_branch 30f\n"                                                        \
+    "21:\n"                                                                 \
+    FQZ_SAME("B", "A", "v4", "v5", SEQSAME, "22f", "31f")                   \
+    "s_cbranch_scc1 20b\n"                                                  \
+    "s_branch 31f\n"                                                        \
+    "12:\n"                                                                 \
     "s_mov_b32 %[flags], 2\n"                                               \
-    "6:\n"                                                                  \
+    "s_branch 30f\n"                                                        \
+    "22:\n"                                                                 \
+    "s_mov_b32 %[flags], 2\n"                                               \
+    "31:\n"                                                                 \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "v_mov_b32 v2, v4\n"                                                    \
+    "v_mov_b32 v3, v5\n"                                                    \
+    "v_mov_b32 %[tvA], %[tvB]\n"                                            \
+    "s_mov_b32 %[cA], %[cB]\n"                                              \
+    "s_mov_b32 %[qsA], %[qsB]\n"                                            \
+    "s_mov_b32 %[pvA], %[pvB]\n"                                            \
+    "s_mov_b32 %[maA], %[maB]\n"                                            \
+    "s_mov_b32 %[sqA], %[sqB]\n"                                            \
+    "30:\n"                                                                 \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "v_cmp_ne_u16_e64 %[TG], %[cA], %[tvA]\n"                               \
+    "s_cmp_lg_u64 %[TG], 0\n"                                               \
+    "s_cbranch_scc1 5f\n"                                                   \
+    "v_add_u32 %[t2], %[maA], %[voff]\n"                                    \
+    "ds_write_b64 %[t2], v[2:3]\n"                                          \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "5:\n"                                                                  \
+    "s_mov_b32 %[done], m0\n"                                               \
     "s_mov_b32 m0, %[m0s]\n"
 
 // ---------------------------------------------------------------------------
-// the decoder.  Model in lanes: lane j holds dword j of the cached model,
-// [tag | entry of slot 0 .. entry of slot L], entries freq | cum << 16, the
-// sentinel slot L with freq 0 and cum = total; symbol bytes follow.
+// the decoder.  Model in lanes: lane j holds slot j of the cached model
+// (fqz_dec_model_bytes): a guard slot, the L list slots, the sentinel whose
+// cum is the total and whose low half names the context the model belongs
+// to.  QW: every parameter set shares one qtab, whose value for the slot's
+// symbol sits in w (else the run reads the record's table).
 // ---------------------------------------------------------------------------
-template <int NE, bool SEQ, bool QID>
+template <int NE, bool SEQ, bool QW>
 __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const FqzDecJob J = load_job(Js + blockIdx.x);   // one block of a batch per workgroup
@@ -421,7 +464,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     // the hand-scheduled run addresses LDS by these offsets: the dynamic
     // block must start at LDS address 0 (no static __shared__ here)
     if (uint32_t(size_t((__attribute__((address_space(3))) uint8_t *)lds)) != 0) __builtin_trap();
-    const uint32_t soff = 4u * (L + 2u);              // symbol bytes within a model
+    const uint32_t sent = 8u * (L + 1u);              // the sentinel slot within a model
     const uint32_t n = uint32_t(J.n);
 
     // ---- set-up: small models, parameter tables, cache tags, bitmap ------
@@ -436,7 +479,24 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         for (uint32_t i = l; i < 256; i += 64) pt[(P_DTAB >> 1) + i] = uint16_t(g.p[x].dtab[i]);
     }
     for (uint32_t i = l; i < FQZ_CTX / 32; i += 64) reinterpret_cast<uint32_t *>(lds + L_BITS)[i] = 0;
-    for (uint32_t s = l; s < NS; s += 64) *reinterpret_cast<uint32_t *>(lds + L_CACHE + s * ME) = TAG_EMPTY;
+    const uint16_t *qt0 = reinterpret_cast<const uint16_t *>(lds + L_PAR + P_QTAB);
+    __builtin_amdgcn_wave_barrier();
+    // a fresh model (every live symbol frequency 1) in slots 0 .. L; the
+    // sentinel is written apart
+    auto fresh_slots = [&](uint32_t a) {
+        for (uint32_t j = l; j <= L; j += 64) {
+            const uint32_t e = j ? 1u | ((j - 1u) << 16) : 0xffffu;
+            const uint32_t w = j ? uint32_t(qt0[j - 1u]) | ((j - 1u) << 24) : 0u;
+            *reinterpret_cast<uint2 *>(lds + a + 8u * j) = make_uint2(e, w);
+        }
+    };
+    // every cache set starts as the fresh model of a context that maps to
+    // it, so that a set always holds some context's true state (sets no
+    // context maps to are never read)
+    for (uint32_t c = l; c < FQZ_CTX; c += 64)
+        *reinterpret_cast<uint2 *>(lds + set_addr(c, NS8, ME) + sent) = make_uint2(c | (L << 16), 0u);
+    for (uint32_t s = 0; s < NS; s++) fresh_slots(L_CACHE + s * ME);
+    __builtin_amdgcn_wave_barrier();
 
     In in;
     in.r = rsrc(J.in, uint32_t(J.in_len));
@@ -517,18 +577,17 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         tpos++;
     };
 
-    // model registers: lane dw of register r (dw = l + 64 r) holds dword dw
-    // of the cached model and the symbol byte of that slot.  Lanes past the
-    // sentinel read (and write back) the sentinel's own addresses, so every
-    // lane of the model registers is a valid slot, the tag, or a copy of the
-    // sentinel (cum = total): the decoder's ballot needs no lane mask.
+    // model registers: lane dw of register r (dw = l + 64 r) holds slot dw
+    // of the cached model, e in v and w in s.  Lanes past the sentinel read
+    // (and write back) the sentinel's own slot, so every lane of the model
+    // registers is the guard, a list slot or a copy of the sentinel (cum =
+    // total): the decoder's ballot needs no lane mask.
     uint32_t v[NE], s[NE];
-    uint32_t voff[NE], sofs[NE];
+    uint32_t voff[NE];
 #pragma unroll
     for (int r = 0; r < NE; r++) {
-        const uint32_t dw = l + 64 * r, c = dw < L + 1 ? dw : L + 1;
-        voff[r] = 4 * c;
-        sofs[r] = soff + c;
+        const uint32_t dw = l + 64 * r;
+        voff[r] = 8u * (dw < L + 1 ? dw : L + 1);
     }
     auto rlane = [&](const uint32_t (&x)[NE], uint32_t dw) -> uint32_t {
         if (NE == 1) return RL(x[0], dw);
@@ -538,50 +597,43 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     auto issue_model_to = [&](uint32_t a, uint32_t (&mv)[NE], uint32_t (&ms)[NE]) {
 #pragma unroll
         for (int r = 0; r < NE; r++) {
-            mv[r] = *reinterpret_cast<const uint32_t *>(lds + a + voff[r]);
-            ms[r] = lds[a + sofs[r]];
+            const uint2 ew = *reinterpret_cast<const uint2 *>(lds + a + voff[r]);
+            mv[r] = ew.x;
+            ms[r] = ew.y;
         }
     };
     auto issue_model = [&]() { issue_model_to(maddr, v, s); };
     auto write_model = [&](uint32_t a) {
 #pragma unroll
-        for (int r = 0; r < NE; r++) {
-            *reinterpret_cast<uint32_t *>(lds + a + voff[r]) = v[r];
-            lds[a + sofs[r]] = uint8_t(s[r]);
-        }
+        for (int r = 0; r < NE; r++) *reinterpret_cast<uint2 *>(lds + a + voff[r]) = make_uint2(v[r], s[r]);
     };
-    // miss: write the resident model back to HBM, fetch or create ctx
+    auto model_sentinel = [&]() { return rlane(v, L + 1); };         // context | total << 16
+    auto model_ctx = [&]() { return model_sentinel() & 0xffffu; };   // the context it belongs to
+    // miss: write the resident model (context `tag`) back to HBM, fetch or
+    // create ctx's
     auto miss = [&](uint32_t tag) {
         nmiss++;
         uint32_t *m32 = reinterpret_cast<uint32_t *>(lds + maddr);
         uint32_t *bits = reinterpret_cast<uint32_t *>(lds + L_BITS);
-        if (tag != TAG_EMPTY) {
-            uint32_t *dst = reinterpret_cast<uint32_t *>(J.back + size_t(tag) * ME);
-            for (uint32_t o = l; o < ME / 4; o += 64)
-                __hip_atomic_store(dst + o, m32[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (l == 0) bits[tag >> 5] |= 1u << (tag & 31);
-            __builtin_amdgcn_wave_barrier();
-        }
+        uint32_t *dst = reinterpret_cast<uint32_t *>(J.back + size_t(tag) * ME);
+        for (uint32_t o = l; o < ME / 4; o += 64)
+            __hip_atomic_store(dst + o, m32[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (l == 0) bits[tag >> 5] |= 1u << (tag & 31);
+        __builtin_amdgcn_wave_barrier();
         if ((U(bits[ctx >> 5]) >> (ctx & 31)) & 1u) {
             const uint32_t *src = reinterpret_cast<const uint32_t *>(J.back + size_t(ctx) * ME);
             for (uint32_t o = l; o < ME / 4; o += 64)
                 m32[o] = __hip_atomic_load(src + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            for (uint32_t j = l; j <= L; j += 64) {   // slot j: freq 1 (live) or 0, cum j
-                m32[1 + j] = (j < L ? 1u : 0u) | (j << 16);
-                lds[maddr + soff + 1 + j] = uint8_t(j < L ? j : 0u);
-            }
-            if (l == 0) {
-                m32[0] = ctx;
-                lds[maddr + soff] = 0;
-            }
+            fresh_slots(maddr);
+            if (l == 0) *reinterpret_cast<uint2 *>(lds + maddr + sent) = make_uint2(ctx | (L << 16), 0u);
         }
         __builtin_amdgcn_wave_barrier();
     };
     auto load_model = [&]() {
         for (;;) {
             issue_model();
-            const uint32_t tag = RL(v[0], 0);
+            const uint32_t tag = model_ctx();
             if (tag == ctx) return;
             miss(tag);
         }
@@ -601,7 +653,8 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 const uint32_t o = __shfl_up(inc, d, 64);
                 if (int(l) >= d) inc += o;
             }
-            if (dw >= 1) v[r] = f | ((carry + inc - f) << 16);
+            // (the sentinel and its copies keep their context in the low half)
+            if (dw >= 1) v[r] = (dw <= L ? f : (v[r] & 0xffffu)) | ((carry + inc - f) << 16);
             carry += RL(inc, 63);
         }
     };
@@ -650,7 +703,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             code -= (ek >> 16) * rng;
             rng *= ek & 0xffffu;
             renorm_slow(lds, in, rng, code);
-            sym = rlane(s, kl);
+            sym = rlane(s, kl) >> 24;
             update(kl, total);
             write_model(maddr);
         }
@@ -748,46 +801,47 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         PROBE_START
         load_model();
         if constexpr (NE == 1) {
-            // the run's scalar state, as uniform values (the asm keeps it in SGPRs)
-            uint32_t wlo = U(uint32_t(in.W)), whi = U(uint32_t(in.W >> 32));
+            // the run's scalar state, as uniform values (the asm keeps it in
+            // SGPRs: A the current copy, B the other)
+            uint64_t cw = uint64_t(U(code)) << 32;   // {scratch, code}
+            uint64_t win = (uint64_t(U(uint32_t(in.W >> 32))) << 32) | U(uint32_t(in.W));
+            uint64_t mA = (uint64_t(s[0]) << 32) | v[0], mB = 0;
+            uint32_t tvA = model_sentinel(), tvB = 0;
+            uint32_t cA = U(ctx), qsA = U(qs), pvA = U(prevq), maA = U(maddr), sqA = U(seq);
+            uint32_t cB, qsB, pvB, maB, sqB;
+            uint32_t dd = 0;
             rng = U(rng);
-            code = U(code);
             in.ub = U(in.ub);
-            qs = U(qs);
-            maddr = U(maddr);
-            delta = U(delta);
-            prevq = U(prevq);
-            seq = U(seq);
             lim = U(lim);
             ulim = U(ulim);
-            uint32_t flags = 0, u = 0, qsk = 0;
-            const uint32_t lane = l, base = L_CACHE, vme = ME, cbig = 0x100000u;
-            const uint32_t ns8 = U(NS8), qloc = U(ps.qloc), bmask = U((1u << ps.bbits) - 1u), bloc = U(ps.bloc);
+            uint32_t flags = 0;
+            const uint32_t base = L_CACHE, vme = ME, cbig = 0x100000u, c65503 = 65503u;
+            const uint32_t ns8 = U(NS8), qlocv = ps.qloc, bmask = U((1u << ps.bbits) - 1u), bloc = U(ps.bloc);
             const uint32_t qtab = U(L_PAR + ps.x * PBYTES + P_QTAB);   // LDS address (the dynamic base is 0)
-            const uint32_t voff0 = voff[0], sofs0 = sofs[0];
+            const uint32_t voff0 = voff[0], vsent = sent;
             const double c19 = 0x1p-19;
-            uint32_t &v0 = v[0], &s0 = s[0];
-            uint32_t tot, x, k1, kl, pk, pk1, nxk, z, m0s, sn, an, nv, ns;
-            uint64_t G, H, SW, E;
-            uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
+            uint32_t u, x, k1, kl, pk, pk1, qsk, z, m0s;
+            uint64_t G, E, SW, SM, TG, HV;
+            uint32_t t0, t1, t2, t3, t4, t5, t6;
             double d0, d1, d2;
             for (;;) {
 #define FQZ_RUN_OPERANDS                                                                      \
-                : [v] "+v"(v0), [s] "+v"(s0), [vout] "+v"(vout), [rng] "+s"(rng),             \
-                  [code] "+s"(code), [wlo] "+s"(wlo), [whi] "+s"(whi), [ub] "+s"(in.ub),     \
-                  [qs] "+s"(qs), [maddr] "+s"(maddr), [delta] "+s"(delta),                   \
-                  [prevq] "+s"(prevq), [done] "+s"(done), [seq] "+s"(seq),                    \
-                  [flags] "=&s"(flags), [u] "=&s"(u), [qsk] "=&s"(qsk), [tot] "=&s"(tot),     \
-                  [x] "=&s"(x), [k1] "=&s"(k1), [kl] "=&s"(kl), [pk] "=&s"(pk),               \
-                  [pk1] "=&s"(pk1), [nxk] "=&s"(nxk), [z] "=&s"(z), [m0s] "=&s"(m0s), [sn] "=&s"(sn), [an] "=&s"(an), \
-                  [G] "=&s"(G), [H] "=&s"(H), [SW] "=&s"(SW), [E] "=&s"(E),                   \
+                : [mA] "+{v[2:3]}"(mA), [mB] "+{v[4:5]}"(mB), [cw] "+{s[40:41]}"(cw),          \
+                  [win] "+{s[42:43]}"(win), [vout] "+v"(vout), [tvA] "+v"(tvA), [tvB] "=&v"(tvB), \
+                  [rng] "+s"(rng), [ub] "+s"(in.ub), [dd] "+s"(dd), [done] "+s"(done),        \
+                  [cA] "+s"(cA), [qsA] "+s"(qsA), [pvA] "+s"(pvA), [maA] "+s"(maA), [sqA] "+s"(sqA), \
+                  [cB] "=&s"(cB), [qsB] "=&s"(qsB), [pvB] "=&s"(pvB), [maB] "=&s"(maB), [sqB] "=&s"(sqB), \
+                  [flags] "=&s"(flags), [u] "=&s"(u), [x] "=&s"(x), [k1] "=&s"(k1), [kl] "=&s"(kl), \
+                  [pk] "=&s"(pk), [pk1] "=&s"(pk1), [qsk] "=&s"(qsk), [z] "=&s"(z), [m0s] "=&s"(m0s), \
+                  [G] "=&s"(G), [E] "=&s"(E), [SW] "=&s"(SW), [SM] "=&s"(SM), [TG] "=&s"(TG),  \
+                  [HV] "=&s"(HV),                                                              \
                   [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),             \
-                  [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7),             \
-                  [d0] "=&v"(d0), [d1] "=&v"(d1), [d2] "=&v"(d2), [nv] "=&v"(nv), [ns] "=&v"(ns) \
-                : [lim] "s"(lim), [ulim] "s"(ulim), [delta0] "s"(delta0),                     \
-                  [qmask] "s"(qmask), [qshift] "s"(qshift), [qloc] "s"(qloc),                 \
+                  [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6),                              \
+                  [d0] "=&v"(d0), [d1] "=&v"(d1), [d2] "=&v"(d2)                               \
+                : [lim] "s"(lim), [ulim] "s"(ulim), [qmask] "s"(qmask), [qshift] "s"(qshift), \
                   [ns8] "s"(ns8), [base] "s"(base), [qtab] "s"(qtab), [bmask] "s"(bmask),     \
-                  [bloc] "s"(bloc), [voff] "v"(voff0), [soff] "v"(sofs0), [lane] "v"(lane),   \
+                  [bloc] "s"(bloc), [c65503] "s"(c65503),                                       \
+                  [voff] "v"(voff0), [vsent] "v"(vsent), [qlocv] "v"(qlocv),                   \
                   [cbig] "v"(cbig), [c19] "v"(c19), [vme] "v"(vme), [pvv] "v"(pvv),          \
                   [dvv] "v"(dvv), [sqv] "v"(sqv)                                              \
                 : "memory", "scc"
@@ -795,10 +849,10 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 const uint32_t done_in = done;
                 const uint64_t ta = __builtin_amdgcn_s_memtime();
 #endif
-                if constexpr (QID && SEQ) asm volatile(FQZ_RUN_ASM(FQZ_QT_QID, FQZ_SEQ_CTX, FQZ_SEQ_COMMIT) FQZ_RUN_OPERANDS);
-                else if constexpr (QID) asm volatile(FQZ_RUN_ASM(FQZ_QT_QID, FQZ_SEQ_NONE, FQZ_SEQ_NONE) FQZ_RUN_OPERANDS);
-                else if constexpr (SEQ) asm volatile(FQZ_RUN_ASM(FQZ_QT_TAB, FQZ_SEQ_CTX, FQZ_SEQ_COMMIT) FQZ_RUN_OPERANDS);
-                else asm volatile(FQZ_RUN_ASM(FQZ_QT_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE) FQZ_RUN_OPERANDS);
+                if constexpr (QW && SEQ) asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_CTX, FQZ_SEQ_SAME) FQZ_RUN_OPERANDS);
+                else if constexpr (QW) asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_NONE, FQZ_SEQ_NONE) FQZ_RUN_OPERANDS);
+                else if constexpr (SEQ) asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME) FQZ_RUN_OPERANDS);
+                else asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE) FQZ_RUN_OPERANDS);
 #undef FQZ_RUN_OPERANDS
 #ifdef FQZ5_DEC_PROBE
                 pr[0] += __builtin_amdgcn_s_memtime() - ta;   // cycles inside the run asm
@@ -808,36 +862,39 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 // (the compiler takes every output of an asm with VGPR outputs
                 // for divergent: the scalar ones are re-read as uniform)
                 rng = U(rng);
-                code = U(code);
-                wlo = U(wlo);
-                whi = U(whi);
                 in.ub = U(in.ub);
-                qs = U(qs);
-                maddr = U(maddr);
-                delta = U(delta);
-                prevq = U(prevq);
+                dd = U(dd);
                 done = U(done);
-                seq = U(seq);
+                cA = U(cA);
+                qsA = U(qsA);
+                pvA = U(pvA);
+                maA = U(maA);
+                sqA = U(sqA);
                 flags = U(flags);
-                u = U(u);
-                qsk = U(qsk);
-                if (flags == 2) { to_slow = true; break; }
-                if (flags == 1) {   // the next context is not cached: the next run fetches it
-                    ctx = ((((qsk >> qshift) & qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1);
-                    fetch = true;
+                cw = (uint64_t(U(uint32_t(cw >> 32))) << 32);
+                win = (uint64_t(U(uint32_t(win >> 32))) << 32) | U(uint32_t(win));
+                if (flags == 2) {   // a context not in its set (the next run fetches it) or the slow path
+                    to_slow = (U(*reinterpret_cast<const uint32_t *>(lds + maA + sent)) & 0xffffu) == cA;
                     break;
                 }
                 if (done == lim) break;
-                in.W = (uint64_t(whi) << 32) | wlo;   // the input window needs a refill
+                in.W = win;   // the input window needs a refill
                 refill(lds, in);
-                wlo = uint32_t(in.W);
-                whi = uint32_t(in.W >> 32);
+                win = in.W;
                 if (in.vb < 4u) break;
                 ulim = (in.vb - 4u) * 8u;
             }
-            in.W = (uint64_t(whi) << 32) | wlo;
+            in.W = win;
+            code = uint32_t(cw >> 32);
+            ctx = cA;
+            qs = qsA;
+            prevq = pvA;
+            maddr = maA;
+            seq = sqA;
+            delta = delta0 + dd;
             left -= done;
             if (SEQ) tpos += done;
+            fetch = true;   // the run wrote its model back
         } else
         do {
             PROBE(0)
@@ -860,13 +917,13 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             }
             // the next context of every slot of register 0 (lanes 0-63),
             // its cache set, whether the set holds it, and the bubble test
-            const uint32_t qt = QID ? s[0] : uint32_t(pt16[(P_QTAB >> 1) + s[0]]);
+            const uint32_t qt = QW ? s[0] : uint32_t(pt16[(P_QTAB >> 1) + (s[0] >> 24)]);
             const uint32_t qn = qs + qt;
             const uint32_t cn = ((((qn & qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1));
             const uint32_t an = set_addr(cn, NS8, ME);
-            const uint32_t tg = *reinterpret_cast<const uint32_t *>(lds + an);
+            const uint32_t tg = *reinterpret_cast<const uint16_t *>(lds + an + sent);
             const uint64_t H = __builtin_amdgcn_ballot_w64(tg == cn);
-            const uint32_t nx = an | (s[0] << 24);
+            const uint32_t nx = an | (s[0] & 0xff000000u);
             const uint32_t qsn = qn << qshift;
             const uint32_t fl = __builtin_amdgcn_update_dpp(0u, v[0], 0x138, 0xf, 0xf, false);   // wave_shr:1
             const uint64_t SW = __builtin_amdgcn_ballot_w64((v[0] & 0xffffu) + FL_STEP > (fl & 0xffffu)) & ~3ull;
@@ -941,7 +998,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         // context outside the cache), the output bytes
         if (!fetch) {
             write_model(maddr);
-            if (done) ctx = RL(v[0], 0);   // the resident model is the next context's
+            if (done) ctx = model_ctx();   // the resident model is the next context's
         }
         qctx = qs >> qshift;
         if (l < done) lds[L_OBUF + fill + l] = uint8_t(vout);
@@ -1030,9 +1087,9 @@ __global__ void k_fqz_div_selftest(uint32_t *bad) {
 
 }  // namespace
 
-template <int NE, bool SEQ, bool QID>
+template <int NE, bool SEQ, bool QW>
 static hipError_t launch_dec(const FqzDecJob *j, int n, hipStream_t s) {
-    auto *f = k_fqz_dec<NE, SEQ, QID>;
+    auto *f = k_fqz_dec<NE, SEQ, QW>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(f),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return e;

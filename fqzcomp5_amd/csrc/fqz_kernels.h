@@ -81,13 +81,13 @@ struct FqzDecJob {
     uint32_t *counts;           // out: [nrecs, ndups, nrevs, misses, slow symbols]
 };
 
-// Bytes of one cached quality model for `live` symbols: the context tag,
-// live+1 entries freq | cum << 16 (the last one a sentinel with freq 0 and
-// cum = total), then a symbol byte per dword (lane) 0 .. live+1 (lane 0's
-// byte is padding, so that every lane of the decoder owns its own byte);
-// 4-byte aligned.
+// Bytes of one cached quality model for `live` symbols: live + 2 slots of
+// 8 bytes {e, w}, read by the decoder's lane j as one 64-bit word: slot 0 a
+// guard (e = 0xffff), slots 1..live the sorted list (e = freq | cum << 16,
+// w = qtab value | symbol << 24), slot live+1 the sentinel (e = context |
+// total << 16).
 constexpr uint32_t fqz_dec_model_bytes(uint32_t live) {
-    return (5u * (live + 2u) + 3u) & ~3u;
+    return 8u * (live + 2u);
 }
 constexpr uint32_t FQZ_DEC_CACHE_BYTES = 163840u - 35088u - 1024u;
 constexpr uint32_t FQZ_DEC_MAX_LIVE = 126u;   // tag + entries in two lane registers
@@ -159,8 +159,8 @@ hipError_t launch_fqz_hist(const FqzStatJob &j, int nchunks, int mode, hipStream
 hipError_t launch_fqz_model_init(uint8_t *models, int live, hipStream_t s);
 hipError_t launch_fqz_encode(const FqzEncJob &j, hipStream_t s);
 // fqz_decode.hip: ne = lane registers per model (live + 2 <= 64 ? 1 : 2),
-// seq = sequence bases in the context, qid = identity qtab in every
-// parameter block; map_mode 0 none / 1 one qmap / 2 per record
+// seq = sequence bases in the context, qid = one qtab shared by every
+// parameter block (its values ride in the cached models); map_mode 0 none / 1 one qmap / 2 per record
 hipError_t launch_fqz_dec(const FqzDecJob *d_jobs, int njobs, int ne, bool seq, bool qid,
                           hipStream_t s);
 hipError_t launch_fqz_dec_fix(const FqzDecJob &j, int map_mode, bool dups, bool revs, hipStream_t s);
