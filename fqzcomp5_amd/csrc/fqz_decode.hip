@@ -211,7 +211,7 @@ DEV PS load_ps(const FqzDevGlobal &g, uint32_t x) {
 // cache set of a context: multiplicative hash with 24-bit multiplies
 // (full rate), then a 24-bit fraction scaled to the set count
 DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
-    const uint32_t h = (ctx * 0x9E3779u) >> 8;                     // 24 bits
+    const uint32_t h = ctx * 0x9E3779u;                             // low 24 bits used
     const uint32_t set = uint32_t((uint64_t(h & 0xffffffu) * (ns8 & 0xffffffu)) >> 32);
     return L_CACHE + (set & 0xffffu) * (me & 0xffffu);   // both < 2^16: v_mad_u32_u24
 }
@@ -268,34 +268,36 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_add_u32 %[u], %[u], %[x]\n"
 #define FQZ_SEQ_SAME(X, Y) "s_mov_b32 %[sq" X "], %[sq" Y "]\n"
 // the symbol's decode and the next context's hypotheses; leaves for SAMEL
-// when the context repeats
-#define FQZ_TOP(X, Y, EX, WX, QT1, QT2, SEQCTX, SAMEL)                      \
+// when the context repeats.  The wait is for the model read (the write-back
+// issued after it may still be in flight); an iteration of the same context
+// enters at SKIPL, past it.
+#define FQZ_TOP(X, Y, EX, WX, QT1, QT2, SEQCTX, SKIPL, SAMEL)               \
+    "s_waitcnt lgkmcnt(1)\n"                                                \
+    SKIPL ":\n"                                                             \
     "v_readlane_b32 %[u], %[pvv], m0\n"                                     \
-    "v_readlane_b32 %[x], %[dvv], %[dd]\n"                                  \
-    "v_cvt_f64_u32 %[d0], %[rng]\n"                                         \
-    "s_waitcnt lgkmcnt(0)\n"                                                \
     "v_lshrrev_b32 %[t6], 16, %[tv" X "]\n"                                 \
-    QT1(WX)                                                                 \
-    "s_add_u32 %[u], %[u], %[x]\n"                                          \
+    "v_readlane_b32 %[x], %[dvv], %[dd]\n"                                  \
     "v_cvt_f64_u32 %[d1], %[t6]\n"                                          \
+    QT1(WX)                                                                 \
+    "v_cvt_f64_u32 %[d0], %[rng]\n"                                         \
+    "v_rcp_f64 %[d2], %[d1]\n"                                              \
+    "s_add_u32 %[u], %[u], %[x]\n"                                          \
     SEQCTX(X, Y)                                                            \
     "v_cmp_ne_u16_e64 %[TG], %[c" X "], %[tv" X "]\n"                       \
-    "v_rcp_f64 %[d2], %[d1]\n"                                              \
-    "v_cmp_lt_u32_e64 %[HV], %[c65503], %[t6]\n"                            \
     "v_lshrrev_b32 %[t4], 16, " EX "\n"                                     \
     "v_fma_f64 %[d1], -%[d1], %[d2], 1.0\n"                                 \
     QT2(X, WX)                                                              \
-    "v_add_u16 %[t5], 16, " EX "\n"                                         \
+    "v_cmp_lt_u32_e64 %[HV], %[c65503], %[t6]\n"                            \
     "v_fma_f64 %[d2], %[d2], %[d1], %[d2]\n"                                \
     "v_and_b32 %[t1], %[qmask], %[t0]\n"                                    \
-    "v_mov_b32_dpp %[t6], " EX " wave_shr:1 row_mask:0xf bank_mask:0xf\n"   \
+    "v_add_u16 %[t5], 16, " EX "\n"                                         \
     "v_fma_f64 %[d0], %[d0], %[d2], %[c19]\n"                               \
     "v_lshl_add_u32 %[t1], %[t1], %[qlocv], %[u]\n"                         \
-    "v_and_b32 %[t1], 0xffff, %[t1]\n"                                      \
+    "v_mov_b32_dpp %[t6], " EX " wave_shr:1 row_mask:0xf bank_mask:0xf\n"   \
     "v_cvt_u32_f64 %[t3], %[d0]\n"                                          \
-    "v_mul_u32_u24 %[t2], 0x9e3779, %[t1]\n"                                \
+    "v_and_b32 %[t1], 0xffff, %[t1]\n"                                      \
     "v_mul_lo_u32 %[t3], %[t4], %[t3]\n"                                    \
-    "v_lshrrev_b32 %[t2], 8, %[t2]\n"                                       \
+    "v_mul_u32_u24 %[t2], 0x9e3779, %[t1]\n"                                \
     "v_cmp_eq_u32_e64 %[SM], %[c" X "], %[t1]\n"                            \
     "v_mul_hi_u32_u24 %[t2], %[ns8], %[t2]\n"                               \
     "v_cmp_gt_u32_e64 %[G], %[t3], s41\n"                                   \
@@ -314,13 +316,18 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_andn2_b64 %[E], %[E], %[TG]\n"                                       \
     "s_cbranch_scc0 " SLOWL "\n"
 // the coded slot's update (fl_bump): +16 to lane kl's frequency (E) and to
-// every later cum (G); one bubble step (SW & E) by DPP lane shifts
-#define FQZ_BUMP(EX, WX)                                                    \
+// every later cum (G); a bubble step (SW & E) goes out of line to SWL and
+// comes back to RETL
+#define FQZ_BUMP(EX, SWL, RETL)                                             \
     "v_cndmask_b32 %[t4], 0, 16, %[E]\n"                                    \
     "v_cndmask_b32 %[t4], %[t4], %[cbig], %[G]\n"                           \
     "s_and_b64 %[SW], %[SW], %[E]\n"                                        \
     "v_add_u32 " EX ", " EX ", %[t4]\n"                                     \
-    "s_cbranch_scc0 3f\n"                                                   \
+    "s_cbranch_scc1 " SWL "f\n"                                             \
+    RETL ":\n"
+// one bubble step by DPP lane shifts: slot kl over slot kl-1
+#define FQZ_SWAP(EX, WX, SWL, RETL)                                         \
+    SWL ":\n"                                                               \
     "s_nop 1\n"                                                             \
     "v_mov_b32_dpp %[t4], " EX " wave_shr:1 row_mask:0xf bank_mask:0xf\n"   \
     "v_mov_b32_dpp %[t5], " EX " wave_shl:1 row_mask:0xf bank_mask:0xf\n"   \
@@ -340,18 +347,23 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_nop 1\n"                                                             \
     "v_cndmask_b32 " EX ", " EX ", %[t5], %[SW]\n"                          \
     "v_cndmask_b32 " WX ", " WX ", %[t1], %[SW]\n"                          \
-    "3:\n"
+    "s_branch " RETL "b\n"
 // the slot's values: range coder terms, qctx, symbol (into pv Y)
 #define FQZ_TAKE(Y, WX)                                                     \
     "v_readlane_b32 %[pk], %[t3], %[kl]\n"                                  \
     "v_readlane_b32 %[pk1], %[t3], %[k1]\n"                                 \
     "v_readlane_b32 %[qsk], %[t0], %[kl]\n"                                 \
     "v_readlane_b32 %[pv" Y "], " WX ", %[kl]\n"
-// renormalise by whole bytes (z = 0, 8, 16 or 24 bits); EXITL when the
-// window needs a refill
-#define FQZ_RENORM(EXITL)                                                   \
+// renormalise by whole bytes (z = 0, 8, 16 or 24 bits) out of line at RNL,
+// back at RETL; then the run's symbol limit
+#define FQZ_RENORM(RNL, RETL)                                               \
     "s_and_b32 %[z], %[z], 24\n"                                            \
-    "s_cbranch_scc0 4f\n"                                                   \
+    "s_cbranch_scc1 " RNL "f\n"                                             \
+    RETL ":\n"                                                              \
+    "s_cmp_lt_u32 m0, %[lim]\n"
+// EXITL when the window needs a refill
+#define FQZ_RENORM_OUT(RNL, RETL, EXITL)                                    \
+    RNL ":\n"                                                               \
     "s_mov_b32 s40, s43\n"                                                  \
     "s_lshl_b64 s[40:41], s[40:41], %[z]\n"                                 \
     "s_lshl_b64 s[42:43], s[42:43], %[z]\n"                                 \
@@ -359,8 +371,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_add_u32 %[ub], %[ub], %[z]\n"                                        \
     "s_cmp_gt_u32 %[ub], %[ulim]\n"                                         \
     "s_cbranch_scc1 " EXITL "\n"                                            \
-    "4:\n"                                                                  \
-    "s_cmp_lt_u32 m0, %[lim]\n"
+    "s_branch " RETL "b\n"
 // the coder and the context state; the symbol to output lane m0
 #define FQZ_CODER(X, Y, QSD)                                                \
     "s_sub_u32 s41, s41, %[pk]\n"                                           \
@@ -373,7 +384,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_addc_u32 %[dd], %[dd], 0\n"                                          \
     "s_add_u32 m0, m0, 1\n"
 // context change: the next model into (MY, tv Y), this one written back
-#define FQZ_SWITCH(X, Y, MX, EX, WX, MY, SLOWL, EXITL)                      \
+#define FQZ_SWITCH(X, Y, MX, EX, WX, MY, SLOWL, SWL, RNL, R1, R2)           \
     "v_add_u32 %[t4], %[ma" Y "], %[voff]\n"                                \
     "v_add_u32 %[t5], %[ma" Y "], %[vsent]\n"                               \
     "ds_read_b64 " MY ", %[t4]\n"                                           \
@@ -381,42 +392,54 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     FQZ_CHECK(SLOWL)                                                        \
     "v_readlane_b32 %[c" Y "], %[t1], %[kl]\n"                              \
     FQZ_TAKE(Y, WX)                                                         \
-    FQZ_BUMP(EX, WX)                                                        \
+    FQZ_BUMP(EX, SWL, R1)                                                   \
     "v_add_u32 %[t2], %[ma" X "], %[voff]\n"                                \
     "ds_write_b64 %[t2], " MX "\n"                                          \
     FQZ_CODER(X, Y, Y)                                                      \
-    FQZ_RENORM(EXITL)
+    FQZ_RENORM(RNL, R2)
 // the same context again: the model stays in (MX, tv X)
-#define FQZ_SAME(X, Y, EX, WX, SEQSAME, SLOWL, EXITL)                       \
+#define FQZ_SAME(X, Y, EX, WX, SEQSAME, SLOWL, SWL, RNL, R1, R2)            \
     FQZ_CHECK(SLOWL)                                                        \
     FQZ_TAKE(Y, WX)                                                         \
-    FQZ_BUMP(EX, WX)                                                        \
+    FQZ_BUMP(EX, SWL, R1)                                                   \
     "v_add_u32 %[tv" X "], %[cbig], %[tv" X "]\n"                           \
     FQZ_CODER(X, Y, X)                                                      \
     "s_mov_b32 %[pv" X "], %[pv" Y "]\n"                                    \
     SEQSAME(X, Y)                                                           \
-    FQZ_RENORM(EXITL)
+    FQZ_RENORM(RNL, R2)
+// labels: 10/20 the A/B iteration (13/23 past its wait), 11/21 their
+// same-context paths, 12/22 the slow exits; 30 exits in the A state, 31 in
+// the B state; 41-48 out-of-line bubble steps and renormalisations, 51-58
+// their way back
 #define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME)                              \
     "s_mov_b32 %[m0s], m0\n"                                                \
     "s_mov_b32 m0, %[done]\n"                                               \
     "s_mov_b32 %[flags], 0\n"                                               \
     "10:\n"                                                                 \
-    FQZ_TOP("A", "B", "v2", "v3", QT1, QT2, SEQCTX, "11f")                  \
-    FQZ_SWITCH("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", "12f", "31f")      \
+    FQZ_TOP("A", "B", "v2", "v3", QT1, QT2, SEQCTX, "13", "11f")            \
+    FQZ_SWITCH("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", "12f", "41", "42", "51", "52") \
     "s_cbranch_scc0 31f\n"                                                  \
     "20:\n"                                                                 \
-    FQZ_TOP("B", "A", "v4", "v5", QT1, QT2, SEQCTX, "21f")                  \
-    FQZ_SWITCH("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", "22f", "30f")      \
+    FQZ_TOP("B", "A", "v4", "v5", QT1, QT2, SEQCTX, "23", "21f")            \
+    FQZ_SWITCH("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", "22f", "43", "44", "53", "54") \
     "s_cbranch_scc1 10b\n"                                                  \
     "s_branch 30f\n"                                                        \
     "11:\n"                                                                 \
-    FQZ_SAME("A", "B", "v2", "v3", SEQSAME, "12f", "30f")                   \
-    "s_cbranch_scc1 10b\n"                                                  \
+    FQZ_SAME("A", "B", "v2", "v3", SEQSAME, "12f", "45", "46", "55", "56")  \
+    "s_cbranch_scc1 13b\n"                                                  \
     "s_branch 30f\n"                                                        \
     "21:\n"                                                                 \
-    FQZ_SAME("B", "A", "v4", "v5", SEQSAME, "22f", "31f")                   \
-    "s_cbranch_scc1 20b\n"                                                  \
+    FQZ_SAME("B", "A", "v4", "v5", SEQSAME, "22f", "47", "48", "57", "58")  \
+    "s_cbranch_scc1 23b\n"                                                  \
     "s_branch 31f\n"                                                        \
+    FQZ_SWAP("v2", "v3", "41", "51")                                        \
+    FQZ_RENORM_OUT("42", "52", "31f")                                       \
+    FQZ_SWAP("v4", "v5", "43", "53")                                        \
+    FQZ_RENORM_OUT("44", "54", "30f")                                       \
+    FQZ_SWAP("v2", "v3", "45", "55")                                        \
+    FQZ_RENORM_OUT("46", "56", "30f")                                       \
+    FQZ_SWAP("v4", "v5", "47", "57")                                        \
+    FQZ_RENORM_OUT("48", "58", "31f")                                       \
     "12:\n"                                                                 \
     "s_mov_b32 %[flags], 2\n"                                               \
     "s_branch 30f\n"                                                        \

@@ -16,9 +16,16 @@ static struct {
     int prev;
     unsigned char seen[65536];
     int tags[8][65536];
+    int wtags[6][65536];              /* set-associative: ways consecutive, MRU first */
+    unsigned char evicted[6][65536];
 } S;
 static const unsigned NSETS[8] = {256, 512, 760, 1024, 2048, 2456, 3548, 65536};
 static unsigned long long MISS[8];
+/* models in the cache x ways (LRU within a set): the 8-byte-slot decoder's
+ * capacity for 42 live symbols (362 models) and a 5-byte layout's (580) */
+static const unsigned WMODELS[6] = {362, 362, 362, 580, 580, 580};
+static const unsigned WWAYS[6] = {1, 2, 4, 1, 2, 4};
+static unsigned long long WMISS[6], WREFETCH[6];
 
 static unsigned fl_decode_stats(flist *m, rcoder *c, int cap) {
     if (cap != 96 || !S.base) return fl_decode(m, c, cap);
@@ -43,7 +50,22 @@ static unsigned fl_decode_stats(flist *m, rcoder *c, int cap) {
     S.same += ctx == S.prev;
     S.prev = ctx;
     if (!S.seen[ctx]) { S.seen[ctx] = 1; S.uniq++; }
-    const uint32_t h = (((uint32_t)ctx * 0x9E3779u) >> 8) & 0xffffffu;   /* the decoder's set_addr */
+    const uint32_t h = ((uint32_t)ctx * 0x9E3779u) & 0xffffffu;   /* the decoder's set_addr */
+    for (int i = 0; i < 6; i++) {
+        const unsigned ways = WWAYS[i], nset = WMODELS[i] / ways;
+        const unsigned set = (unsigned)(((uint64_t)h * nset) >> 24);
+        int *t = &S.wtags[i][set * ways];
+        unsigned w = 0;
+        while (w < ways && t[w] != ctx + 1) w++;
+        if (w == ways) {   /* miss: evict the LRU way */
+            WMISS[i]++;
+            if (S.evicted[i][ctx]) WREFETCH[i]++;
+            w = ways - 1;
+            if (t[w]) S.evicted[i][t[w] - 1] = 1;
+        }
+        for (; w > 0; w--) t[w] = t[w - 1];
+        t[0] = ctx + 1;
+    }
     for (int i = 0; i < 8; i++) {
         const unsigned set = NSETS[i] == 65536 ? (unsigned)ctx : (unsigned)(((uint64_t)h * NSETS[i]) >> 24);
         if (S.tags[i][set] != ctx + 1) { MISS[i]++; S.tags[i][set] = ctx + 1; }
@@ -82,6 +104,10 @@ int main(int argc, char **argv) {
     printf("], \"swap\": %.4f, \"halve\": %.5f, \"same_ctx\": %.4f, \"contexts\": %llu, \"miss\": {",
            (double)S.swaps / (double)S.n, (double)S.halves / (double)S.n, (double)S.same / (double)S.n, S.uniq);
     for (int i = 0; i < 8; i++) printf("%s\"%u\": %.4f", i ? ", " : "", NSETS[i], (double)MISS[i] / (double)S.n);
+    printf("}, \"assoc\": {");
+    for (int i = 0; i < 6; i++)
+        printf("%s\"%ux%u\": [%.4f, %.4f]", i ? ", " : "", WMODELS[i], WWAYS[i], (double)WMISS[i] / (double)S.n,
+               (double)WREFETCH[i] / (double)S.n);
     printf("}}\n");
     return 0;
 }

@@ -26,3 +26,4 @@ for kind in ("novaseq", "illumina8", "ont", "hifi"):
         print(f"{kind:9s} {st}: k {r['k_mean']:.2f} k>1 {r['k_gt'][0]:.2f} k>2 {r['k_gt'][1]:.2f} "
               f"k>4 {r['k_gt'][2]:.2f} swap {r['swap']:.3f} halve {r['halve']:.4f} same {r['same_ctx']:.3f} "
               f"ctx {r['contexts']} miss " + " ".join(f"{k}:{v:.3f}" for k, v in r['miss'].items()), flush=True)
+        print("          assoc (miss, refetch): " + " ".join(f"{k}:{v[0]:.3f}/{v[1]:.3f}" for k, v in r['assoc'].items()), flush=True)
