@@ -815,6 +815,11 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
         D.ment = fqz_dec_model_bytes(nlive);
         D.nsets = FQZ_DEC_CACHE_BYTES / D.ment;
         D.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * D.ment);
+        if (nlive > 62) {
+            D.back_hi = g.arena.alloc_n<uint32_t>(size_t(FQZ_CTX) * 64);
+            D.hi_bits = g.arena.alloc_n<uint32_t>(FQZ_CTX / 32);
+            g.memset0(D.hi_bits, FQZ_CTX / 8);
+        }
         for (const Param &pm : G.p) {
             W.seq_ctx = W.seq_ctx || pm.bbits > 0;
             W.dedup = W.dedup || pm.dedup;

@@ -270,9 +270,9 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 // the symbol's decode and the next context's hypotheses; leaves for SAMEL
 // when the context repeats.  The wait is for the model read (the write-back
 // issued after it may still be in flight); an iteration of the same context
-// enters at SKIPL, past it.
-#define FQZ_TOP(X, Y, EX, WX, QT1, QT2, SEQCTX, SKIPL, SAMEL)               \
-    "s_waitcnt lgkmcnt(1)\n"                                                \
+// enters at SKIPL, past it.  WCNT: the writes issued after the read.
+#define FQZ_TOP(X, Y, EX, WX, QT1, QT2, SEQCTX, WCNT, SKIPL, SAMEL)         \
+    "s_waitcnt lgkmcnt(" WCNT ")\n"                                         \
     SKIPL ":\n"                                                             \
     "v_readlane_b32 %[u], %[pvv], m0\n"                                     \
     "v_lshrrev_b32 %[t6], 16, %[tv" X "]\n"                                 \
@@ -383,8 +383,17 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_cmp_lg_u32 %[pv" X "], %[pv" Y "]\n"                                 \
     "s_addc_u32 %[dd], %[dd], 0\n"                                          \
     "s_add_u32 m0, m0, 1\n"
+// the sentinel (total + 16), when no lane carries it (NE = 2)
+#define FQZ_SENT_NONE(X) ""
+#define FQZ_SENT_WB(X)                                                      \
+    "v_add_u32 %[tv" X "], %[cbig], %[tv" X "]\n"                           \
+    "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
+    "ds_write_b32 %[t5], %[tv" X "]\n"
+#define FQZ_SENT_EXIT(X)                                                    \
+    "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
+    "ds_write_b32 %[t5], %[tv" X "]\n"
 // context change: the next model into (MY, tv Y), this one written back
-#define FQZ_SWITCH(X, Y, MX, EX, WX, MY, SLOWL, SWL, RNL, R1, R2)           \
+#define FQZ_SWITCH(X, Y, MX, EX, WX, MY, SENTWB, SLOWL, SWL, RNL, R1, R2)   \
     "v_add_u32 %[t4], %[ma" Y "], %[voff]\n"                                \
     "v_add_u32 %[t5], %[ma" Y "], %[vsent]\n"                               \
     "ds_read_b64 " MY ", %[t4]\n"                                           \
@@ -395,6 +404,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     FQZ_BUMP(EX, SWL, R1)                                                   \
     "v_add_u32 %[t2], %[ma" X "], %[voff]\n"                                \
     "ds_write_b64 %[t2], " MX "\n"                                          \
+    SENTWB(X)                                                               \
     FQZ_CODER(X, Y, Y)                                                      \
     FQZ_RENORM(RNL, R2)
 // the same context again: the model stays in (MX, tv X)
@@ -411,17 +421,17 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 // same-context paths, 12/22 the slow exits; 30 exits in the A state, 31 in
 // the B state; 41-48 out-of-line bubble steps and renormalisations, 51-58
 // their way back
-#define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME)                              \
+#define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME, SENTWB, SENTEX, WCNT)        \
     "s_mov_b32 %[m0s], m0\n"                                                \
     "s_mov_b32 m0, %[done]\n"                                               \
     "s_mov_b32 %[flags], 0\n"                                               \
     "10:\n"                                                                 \
-    FQZ_TOP("A", "B", "v2", "v3", QT1, QT2, SEQCTX, "13", "11f")            \
-    FQZ_SWITCH("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", "12f", "41", "42", "51", "52") \
+    FQZ_TOP("A", "B", "v2", "v3", QT1, QT2, SEQCTX, WCNT, "13", "11f")      \
+    FQZ_SWITCH("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", SENTWB, "12f", "41", "42", "51", "52") \
     "s_cbranch_scc0 31f\n"                                                  \
     "20:\n"                                                                 \
-    FQZ_TOP("B", "A", "v4", "v5", QT1, QT2, SEQCTX, "23", "21f")            \
-    FQZ_SWITCH("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", "22f", "43", "44", "53", "54") \
+    FQZ_TOP("B", "A", "v4", "v5", QT1, QT2, SEQCTX, WCNT, "23", "21f")      \
+    FQZ_SWITCH("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", SENTWB, "22f", "43", "44", "53", "54") \
     "s_cbranch_scc1 10b\n"                                                  \
     "s_branch 30f\n"                                                        \
     "11:\n"                                                                 \
@@ -462,6 +472,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_cbranch_scc1 5f\n"                                                   \
     "v_add_u32 %[t2], %[maA], %[voff]\n"                                    \
     "ds_write_b64 %[t2], v[2:3]\n"                                          \
+    SENTEX("A")                                                             \
     "s_waitcnt lgkmcnt(0)\n"                                                \
     "5:\n"                                                                  \
     "s_mov_b32 %[done], m0\n"                                               \
@@ -487,7 +498,10 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     // the hand-scheduled run addresses LDS by these offsets: the dynamic
     // block must start at LDS address 0 (no static __shared__ here)
     if (uint32_t(size_t((__attribute__((address_space(3))) uint8_t *)lds)) != 0) __builtin_trap();
-    const uint32_t sent = 8u * (L + 1u);              // the sentinel slot within a model
+    // the cached model: slots 0 .. LL and the sentinel S (NE = 2: the list
+    // slots past lane 63 stay in HBM, J.back_hi)
+    const uint32_t LL = L < 63u ? L : 63u, S = LL + 1u;
+    const uint32_t sent = 8u * S;                     // the sentinel slot within a model
     const uint32_t n = uint32_t(J.n);
 
     // ---- set-up: small models, parameter tables, cache tags, bitmap ------
@@ -504,10 +518,10 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     for (uint32_t i = l; i < FQZ_CTX / 32; i += 64) reinterpret_cast<uint32_t *>(lds + L_BITS)[i] = 0;
     const uint16_t *qt0 = reinterpret_cast<const uint16_t *>(lds + L_PAR + P_QTAB);
     __builtin_amdgcn_wave_barrier();
-    // a fresh model (every live symbol frequency 1) in slots 0 .. L; the
+    // a fresh model (every live symbol frequency 1) in slots 0 .. LL; the
     // sentinel is written apart
     auto fresh_slots = [&](uint32_t a) {
-        for (uint32_t j = l; j <= L; j += 64) {
+        for (uint32_t j = l; j <= LL; j += 64) {
             const uint32_t e = j ? 1u | ((j - 1u) << 16) : 0xffffu;
             const uint32_t w = j ? uint32_t(qt0[j - 1u]) | ((j - 1u) << 24) : 0u;
             *reinterpret_cast<uint2 *>(lds + a + 8u * j) = make_uint2(e, w);
@@ -600,38 +614,23 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         tpos++;
     };
 
-    // model registers: lane dw of register r (dw = l + 64 r) holds slot dw
-    // of the cached model, e in v and w in s.  Lanes past the sentinel read
-    // (and write back) the sentinel's own slot, so every lane of the model
-    // registers is the guard, a list slot or a copy of the sentinel (cum =
-    // total): the decoder's ballot needs no lane mask.
-    uint32_t v[NE], s[NE];
-    uint32_t voff[NE];
-#pragma unroll
-    for (int r = 0; r < NE; r++) {
-        const uint32_t dw = l + 64 * r;
-        voff[r] = 8u * (dw < L + 1 ? dw : L + 1);
-    }
-    auto rlane = [&](const uint32_t (&x)[NE], uint32_t dw) -> uint32_t {
-        if (NE == 1) return RL(x[0], dw);
-        const uint32_t a = RL(x[0], dw & 63u), b = RL(x[NE - 1], dw & 63u);
-        return dw < 64 ? a : b;
+    // the fast path's model registers: lane j holds slot j of the cached
+    // model, e in v0 and w in s0.  NE = 1: lanes past the sentinel read (and
+    // write back) the sentinel's own slot, so every lane is the guard, a list
+    // slot or a copy of the sentinel (cum = total) and the decoder's ballot
+    // needs no lane mask.  NE = 2: the 64 lanes are the guard and slots
+    // 0 .. 62; the sentinel is read apart (a code past slot 62's range takes
+    // the slow path).
+    uint32_t v0 = 0, s0 = 0;
+    const uint32_t voff0 = 8u * (l < S ? l : S);
+    auto issue_model = [&]() {
+        const uint2 ew = *reinterpret_cast<const uint2 *>(lds + maddr + voff0);
+        v0 = ew.x;
+        s0 = ew.y;
     };
-    auto issue_model_to = [&](uint32_t a, uint32_t (&mv)[NE], uint32_t (&ms)[NE]) {
-#pragma unroll
-        for (int r = 0; r < NE; r++) {
-            const uint2 ew = *reinterpret_cast<const uint2 *>(lds + a + voff[r]);
-            mv[r] = ew.x;
-            ms[r] = ew.y;
-        }
-    };
-    auto issue_model = [&]() { issue_model_to(maddr, v, s); };
-    auto write_model = [&](uint32_t a) {
-#pragma unroll
-        for (int r = 0; r < NE; r++) *reinterpret_cast<uint2 *>(lds + a + voff[r]) = make_uint2(v[r], s[r]);
-    };
-    auto model_sentinel = [&]() { return rlane(v, L + 1); };         // context | total << 16
-    auto model_ctx = [&]() { return model_sentinel() & 0xffffu; };   // the context it belongs to
+    auto write_model = [&](uint32_t a) { *reinterpret_cast<uint2 *>(lds + a + voff0) = make_uint2(v0, s0); };
+    // the sentinel: context | total << 16
+    auto model_sentinel = [&]() { return U(*reinterpret_cast<const uint32_t *>(lds + maddr + sent)); };
     // miss: write the resident model (context `tag`) back to HBM, fetch or
     // create ctx's
     auto miss = [&](uint32_t tag) {
@@ -655,11 +654,71 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     };
     auto load_model = [&]() {
         for (;;) {
-            issue_model();
-            const uint32_t tag = model_ctx();
-            if (tag == ctx) return;
+            const uint32_t tag = model_sentinel() & 0xffffu;
+            if (tag == ctx) break;
             miss(tag);
         }
+        issue_model();
+    };
+
+    // ---- the slow path: the whole model in registers, lane dw of register
+    // r (dw = l + 64 r) holding slot dw, the sentinel and its copies past L.
+    // NE = 2: the slots past lane 63 as freq | sym << 16 per context in
+    // J.back_hi (fresh until J.hi_bits marks them written).
+    uint32_t fv[NE], fs[NE];
+    auto rlane = [&](const uint32_t (&x)[NE], uint32_t dw) -> uint32_t {
+        if (NE == 1) return RL(x[0], dw);
+        const uint32_t a = RL(x[0], dw & 63u), b = RL(x[NE - 1], dw & 63u);
+        return dw < 64 ? a : b;
+    };
+    auto full_model = [&]() {
+        load_model();
+        fv[0] = v0;
+        fs[0] = s0;
+        if constexpr (NE == 2) {
+            const uint32_t sv = model_sentinel(), dw = 64u + l;
+            const bool hi = (__hip_atomic_load(J.hi_bits + (ctx >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >>
+                             (ctx & 31)) & 1u;
+            uint32_t f = 0, sy = 0;
+            if (dw <= L) {
+                if (hi) {
+                    const uint32_t x = __hip_atomic_load(J.back_hi + size_t(ctx) * 64u + l, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    f = x & 0xffffu;
+                    sy = x >> 16;
+                } else {
+                    f = 1;
+                    sy = dw - 1u;
+                }
+            }
+            uint32_t inc = f;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(inc, d, 64);
+                if (int(l) >= d) inc += o;
+            }
+            const uint32_t e63 = RL(v0, 63), cb = (e63 >> 16) + (e63 & 0xffffu);
+            fv[1] = dw <= L ? f | ((cb + inc - f) << 16) : sv;
+            fs[1] = dw <= L ? uint32_t(qt0[sy]) | (sy << 24) : 0u;
+        }
+    };
+    auto write_full = [&]() {
+        v0 = fv[0];
+        s0 = fs[0];
+        write_model(maddr);
+        if constexpr (NE == 2) {
+            const uint32_t sv = rlane(fv, L + 1), dw = 64u + l;
+            if (l == 0) *reinterpret_cast<uint2 *>(lds + maddr + sent) = make_uint2(sv, 0u);
+            if (dw <= L)
+                __hip_atomic_store(J.back_hi + size_t(ctx) * 64u + l, (fv[1] & 0xffffu) | ((fs[1] >> 24) << 16),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (l == 0) {
+                uint32_t *hb = J.hi_bits + (ctx >> 5);
+                __hip_atomic_store(hb, __hip_atomic_load(hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                                       (1u << (ctx & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     };
     // halve every live slot (c_simple_model.h:106-115): prefix sums of the
     // halved frequencies give the new cumulative counts
@@ -668,7 +727,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
 #pragma unroll
         for (int r = 0; r < NE; r++) {
             const uint32_t dw = l + 64 * r;
-            uint32_t f = dw >= 1 && dw <= L ? (v[r] & 0xffffu) : 0u;
+            uint32_t f = dw >= 1 && dw <= L ? (fv[r] & 0xffffu) : 0u;
             f -= f >> 1;
             uint32_t inc = f;
 #pragma unroll
@@ -677,42 +736,42 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 if (int(l) >= d) inc += o;
             }
             // (the sentinel and its copies keep their context in the low half)
-            if (dw >= 1) v[r] = (dw <= L ? f : (v[r] & 0xffffu)) | ((carry + inc - f) << 16);
+            if (dw >= 1) fv[r] = (dw <= L ? f : (fv[r] & 0xffffu)) | ((carry + inc - f) << 16);
             carry += RL(inc, 63);
         }
     };
-    // one bubble step at lane kl >= 2 (the lanes of the registers only)
+    // one bubble step at lane kl >= 2
     auto bubble = [&](uint32_t kl) {
-        const uint32_t ek = rlane(v, kl), ep = rlane(v, kl - 1);
+        const uint32_t ek = rlane(fv, kl), ep = rlane(fv, kl - 1);
         const uint32_t fk = ek & 0xffffu, fp = ep & 0xffffu;
         if (fk > fp) {
             const uint32_t cp = ep >> 16;
-            const uint32_t sk = rlane(s, kl), sp = rlane(s, kl - 1);
+            const uint32_t sk = rlane(fs, kl), sp = rlane(fs, kl - 1);
 #pragma unroll
             for (int r = 0; r < NE; r++) {
                 const uint32_t dw = l + 64 * r;
-                if (dw == kl - 1) { v[r] = fk | (cp << 16); s[r] = sk; }
-                if (dw == kl) { v[r] = fp | ((cp + fk) << 16); s[r] = sp; }
+                if (dw == kl - 1) { fv[r] = fk | (cp << 16); fs[r] = sk; }
+                if (dw == kl) { fv[r] = fp | ((cp + fk) << 16); fs[r] = sp; }
             }
         }
     };
     // the list update after coding the slot in lane kl (fl_bump): +16,
-    // halve past FL_MAX, one bubble step (registers only)
+    // halve past FL_MAX, one bubble step
     auto update = [&](uint32_t kl, uint32_t total) {
 #pragma unroll
         for (int r = 0; r < NE; r++) {
             const uint32_t dw = l + 64 * r;
-            v[r] += dw > kl ? 0x100000u : (dw == kl ? FL_STEP : 0u);
+            fv[r] += dw > kl ? 0x100000u : (dw == kl ? FL_STEP : 0u);
         }
         if (total + FL_STEP > FL_MAX) halve();
         if (kl >= 2) bubble(kl);
     };
     // one symbol with the reference's arithmetic, any state (corrupt or
-    // truncated streams, the last bytes of the input)
+    // truncated streams, the last bytes of the input, NE = 2 slots past 62)
     auto slow_symbol = [&]() {
         nslow++;
-        load_model();
-        const uint32_t total = rlane(v, L + 1) >> 16;
+        full_model();
+        const uint32_t total = rlane(fv, L + 1) >> 16;
         uint32_t t = 0;
         if (total && rng >= total) {   // the division stays even when no symbol follows
             rng /= total;
@@ -721,14 +780,14 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         uint32_t sym = 0;
         if (t < total) {   // (t > FL_MAX implies t >= total)
             uint32_t kl = 1;
-            while (kl < L && (rlane(v, kl + 1) >> 16) <= t) kl++;
-            const uint32_t ek = rlane(v, kl);
+            while (kl < L && (rlane(fv, kl + 1) >> 16) <= t) kl++;
+            const uint32_t ek = rlane(fv, kl);
             code -= (ek >> 16) * rng;
             rng *= ek & 0xffffu;
             renorm_slow(lds, in, rng, code);
-            sym = rlane(s, kl) >> 24;
+            sym = rlane(fs, kl) >> 24;
             update(kl, total);
-            write_model(maddr);
+            write_full();
         }
         lds[l ? dlane : L_OBUF + fill] = uint8_t(sym);
         fill++;
@@ -820,15 +879,15 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         const uint32_t qmask = U(ps.qmask), qshift = U(ps.qshift);
         uint32_t vout = 0;
         uint32_t done = 0;
-        bool to_slow = false, fetch = false;
+        bool to_slow = false;
         PROBE_START
         load_model();
-        if constexpr (NE == 1) {
+        {
             // the run's scalar state, as uniform values (the asm keeps it in
             // SGPRs: A the current copy, B the other)
             uint64_t cw = uint64_t(U(code)) << 32;   // {scratch, code}
             uint64_t win = (uint64_t(U(uint32_t(in.W >> 32))) << 32) | U(uint32_t(in.W));
-            uint64_t mA = (uint64_t(s[0]) << 32) | v[0], mB = 0;
+            uint64_t mA = (uint64_t(s0) << 32) | v0, mB = 0;
             uint32_t tvA = model_sentinel(), tvB = 0;
             uint32_t cA = U(ctx), qsA = U(qs), pvA = U(prevq), maA = U(maddr), sqA = U(seq);
             uint32_t cB, qsB, pvB, maB, sqB;
@@ -841,7 +900,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             const uint32_t base = L_CACHE, vme = ME, cbig = 0x100000u, c65503 = 65503u;
             const uint32_t ns8 = U(NS8), qlocv = ps.qloc, bmask = U((1u << ps.bbits) - 1u), bloc = U(ps.bloc);
             const uint32_t qtab = U(L_PAR + ps.x * PBYTES + P_QTAB);   // LDS address (the dynamic base is 0)
-            const uint32_t voff0 = voff[0], vsent = sent;
+            const uint32_t vsent = sent;
             const double c19 = 0x1p-19;
             uint32_t u, x, k1, kl, pk, pk1, qsk, z, m0s;
             uint64_t G, E, SW, SM, TG, HV;
@@ -872,10 +931,18 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 const uint32_t done_in = done;
                 const uint64_t ta = __builtin_amdgcn_s_memtime();
 #endif
-                if constexpr (QW && SEQ) asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_CTX, FQZ_SEQ_SAME) FQZ_RUN_OPERANDS);
-                else if constexpr (QW) asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_NONE, FQZ_SEQ_NONE) FQZ_RUN_OPERANDS);
-                else if constexpr (SEQ) asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME) FQZ_RUN_OPERANDS);
-                else asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE) FQZ_RUN_OPERANDS);
+#define FQZ_RUN_NE(SENTWB, SENTEX, WCNT)                                                                           \
+                if constexpr (QW && SEQ)                                                                     \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT) FQZ_RUN_OPERANDS); \
+                else if constexpr (QW)                                                                       \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT) FQZ_RUN_OPERANDS); \
+                else if constexpr (SEQ)                                                                      \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT) FQZ_RUN_OPERANDS); \
+                else                                                                                         \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT) FQZ_RUN_OPERANDS);
+                if constexpr (NE == 1) { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1") }
+                else { FQZ_RUN_NE(FQZ_SENT_WB, FQZ_SENT_EXIT, "2") }
+#undef FQZ_RUN_NE
 #undef FQZ_RUN_OPERANDS
 #ifdef FQZ5_DEC_PROBE
                 pr[0] += __builtin_amdgcn_s_memtime() - ta;   // cycles inside the run asm
@@ -917,111 +984,6 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             delta = delta0 + dd;
             left -= done;
             if (SEQ) tpos += done;
-            fetch = true;   // the run wrote its model back
-        } else
-        do {
-            PROBE(0)
-            uint32_t u = RL(pvv, done) + RL(dvv, delta - delta0);
-            uint32_t seqn = 0;
-            if (SEQ) {
-                seqn = ((seq << 2) | RL(sqv, done)) & ((1u << ps.bbits) - 1u);
-                u += seqn << ps.bloc;
-            }
-            const uint32_t total = RL(v[NE - 1], 63) >> 16;
-            const uint32_t q = quot(rng, recip(total));
-            uint32_t p[NE];
-            bool gt[NE];
-            uint64_t G[NE];
-#pragma unroll
-            for (int r = 0; r < NE; r++) {
-                p[r] = (v[r] >> 16) * q;
-                gt[r] = p[r] > code;
-                G[r] = __builtin_amdgcn_ballot_w64(gt[r]);
-            }
-            // the next context of every slot of register 0 (lanes 0-63),
-            // its cache set, whether the set holds it, and the bubble test
-            const uint32_t qt = QW ? s[0] : uint32_t(pt16[(P_QTAB >> 1) + (s[0] >> 24)]);
-            const uint32_t qn = qs + qt;
-            const uint32_t cn = ((((qn & qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1));
-            const uint32_t an = set_addr(cn, NS8, ME);
-            const uint32_t tg = *reinterpret_cast<const uint16_t *>(lds + an + sent);
-            const uint64_t H = __builtin_amdgcn_ballot_w64(tg == cn);
-            const uint32_t nx = an | (s[0] & 0xff000000u);
-            const uint32_t qsn = qn << qshift;
-            const uint32_t fl = __builtin_amdgcn_update_dpp(0u, v[0], 0x138, 0xf, 0xf, false);   // wave_shr:1
-            const uint64_t SW = __builtin_amdgcn_ballot_w64((v[0] & 0xffffu) + FL_STEP > (fl & 0xffffu)) & ~3ull;
-            PROBE(1)
-            if (G[NE - 1] == 0) {   // t >= total: reference arithmetic
-                to_slow = true;
-                break;
-            }
-            const uint32_t k1 = NE == 1 ? uint32_t(__builtin_ctzll(G[0]))
-                                        : (G[0] ? uint32_t(__builtin_ctzll(G[0])) : 64u + uint32_t(__builtin_ctzll(G[NE - 1])));
-            const uint32_t kl = k1 - 1;   // lane of the decoded slot
-            if (NE == 2 && kl >= 64) {   // slots past lane 63: reference arithmetic
-                to_slow = true;
-                break;
-            }
-            const uint32_t pk = rlane(p, kl), pk1 = rlane(p, k1);
-            const uint32_t nxk = RL(nx, kl), qsk = RL(qsn, kl);
-            const uint32_t ank = nxk & 0xffffffu, sym = nxk >> 24;
-            const bool hit = (H >> kl) & 1u;
-            // the coded slot's update in registers (fl_bump): +16 to its
-            // frequency and to every later cum, halving past FL_MAX, one
-            // bubble step; then written back
-#pragma unroll
-            for (int r = 0; r < NE; r++) {
-                const uint32_t dw = l + 64 * r;
-                v[r] += gt[r] ? 0x100000u : (dw == kl ? FL_STEP : 0u);
-            }
-            if (__builtin_expect(total + FL_STEP > FL_MAX, 0)) {
-                halve();
-                if (kl >= 2) bubble(kl);
-            } else if (__builtin_expect(uint32_t(SW >> kl) & 1u, 0)) {
-                bubble(kl);
-            }
-            write_model(maddr);
-            maddr = ank;
-            // the next context's model (the same cache set again when the
-            // context repeats: the write above lands first); a context not
-            // in the cache ends the run, the next one fetches it
-            if (hit) issue_model();
-            // the coder (c_range_coder.h RC_Decode), beside the read
-            code -= pk;
-            rng = pk1 - pk;
-            const uint32_t z = uint32_t(__builtin_clz(rng)) & 24u;
-            rng <<= z;
-            code = uint32_t(((uint64_t(code) << 32) | uint32_t(in.W >> 32)) >> (32u - z));
-            in.W <<= z;
-            in.ub += z;
-            vout = uint32_t(amdgcn_writelane(int(sym), int(done), int(vout)));
-            delta += prevq != sym;
-            prevq = sym;
-            qs = qsk;
-            seq = seqn;
-            left--;
-            if (SEQ) tpos++;
-            done++;
-            PROBE(2)
-            if (__builtin_expect(!hit, 0)) {
-                ctx = ((((qsk >> qshift) & qmask) << ps.qloc) + u) & uint32_t(FQZ_CTX - 1);
-                fetch = true;
-                break;
-            }
-            if (in.ub > ulim) {
-                refill(lds, in);
-                if (in.vb < 4u) break;
-                ulim = (in.vb - 4u) * 8u;
-            }
-            if (done == lim) break;
-            PROBE(3)
-        } while (true);
-        // the run's state back to the record: the context of the next
-        // symbol, its cache set (written back unless the run ended on a
-        // context outside the cache), the output bytes
-        if (!fetch) {
-            write_model(maddr);
-            if (done) ctx = model_ctx();   // the resident model is the next context's
         }
         qctx = qs >> qshift;
         if (l < done) lds[L_OBUF + fill + l] = uint8_t(vout);

@@ -73,6 +73,8 @@ struct FqzDecJob {
     // backed by FQZ_CTX x ment bytes in HBM; qmap / duplicate / reversal
     // fix-ups are applied afterwards from the record lists it writes.
     uint8_t *back;
+    uint32_t *back_hi;          // live > 62: list slots past lane 63, FQZ_CTX x 64 words
+    uint32_t *hi_bits;          //   and which contexts' are written (FQZ_CTX bits, zeroed)
     uint32_t ment, nsets;       // cached model bytes, direct-mapped sets
     uint32_t cap_list, pad2;    // capacity of each record list
     uint4 *recs;                // nparam > 1: non-duplicate records {start, len, param, 0}
@@ -81,16 +83,16 @@ struct FqzDecJob {
     uint32_t *counts;           // out: [nrecs, ndups, nrevs, misses, slow symbols]
 };
 
-// Bytes of one cached quality model for `live` symbols: live + 2 slots of
-// 8 bytes {e, w}, read by the decoder's lane j as one 64-bit word: slot 0 a
-// guard (e = 0xffff), slots 1..live the sorted list (e = freq | cum << 16,
-// w = qtab value | symbol << 24), slot live+1 the sentinel (e = context |
-// total << 16).
+// Bytes of one cached quality model for `live` symbols: slots of 8 bytes
+// {e, w}, read by the decoder's lane j as one 64-bit word: slot 0 a guard
+// (e = 0xffff), then the sorted list (e = freq | cum << 16, w = qtab value |
+// symbol << 24) up to lane 63, then the sentinel (e = context | total << 16).
+// With more than 62 live symbols the list slots past lane 63 stay in HBM.
 constexpr uint32_t fqz_dec_model_bytes(uint32_t live) {
-    return 8u * (live + 2u);
+    return 8u * ((live < 63u ? live : 63u) + 2u);
 }
 constexpr uint32_t FQZ_DEC_CACHE_BYTES = 163840u - 35088u - 1024u;
-constexpr uint32_t FQZ_DEC_MAX_LIVE = 126u;   // tag + entries in two lane registers
+constexpr uint32_t FQZ_DEC_MAX_LIVE = 126u;   // guard + slots + sentinel in two lane registers (slow path)
 
 // Parallel encoder (fqz_kernels.hip): the block becomes a list of coding
 // events (record headers and quality symbols) in stream order; events are

@@ -399,7 +399,7 @@ template <int CAP> DEV void model_run(FList<CAP> *m, const FqzEvJob &J, uint32_t
 // [256 (b % nblk), +256) of block b / nblk
 // Hot quality models (at least hot_min events, at most FQZ_HOT_LIVE live
 // symbols) go to k_fqz_model_hot instead; hot_min = 0 disables that path.
-constexpr uint32_t FQZ_HOT_LIVE = 62;            // slots 0..live+1 in 64 lanes
+constexpr uint32_t FQZ_HOT_LIVE = 126;           // slots 0..live+1 in two lane registers
 DEV bool fqz_is_hot(uint32_t m, uint32_t cnt, uint32_t live, uint32_t hot_min) {
     return hot_min && m < FQZ_M_SEL && live <= FQZ_HOT_LIVE && cnt >= hot_min;
 }
@@ -443,32 +443,46 @@ __global__ void k_fqz_hot_list(const FqzEvJob *Js, uint32_t *hot, uint32_t strid
     if (k + 1 < stride) list[1 + k] = m;
 }
 
-// Phase 3, hot models: one wave per model with the list in lanes (lane k =
-// slot k: fr, cum = the sum of fr over slots 1..k-1, sy) and the model's
-// events in chunks of 64, one per lane.  Runs of events that hit the head
-// symbol are coded in parallel in closed form (event n of a run: cum 0,
-// freq f1 + 16n, total tot + 16n, while no halving is due), every other
-// event takes the list update (fl_bump: +16, halve past FL_MAX, one bubble
-// step) with ballots and readlanes.  Codes are identical to
+// Phase 3, hot models: one wave per model with the list in lanes (lane dw =
+// l + 64 r of register r = slot dw: fr, cum = the sum of fr over slots
+// 1..dw-1, sy; NE = 2 for alphabets past 62 symbols, as HiFi's Q0-Q93) and
+// the model's events in chunks of 64, one per lane.  Runs of events that hit
+// the head symbol are coded in parallel in closed form (event n of a run:
+// cum 0, freq f1 + 16n, total tot + 16n, while no halving is due), every
+// other event takes the list update (fl_bump: +16, halve past FL_MAX, one
+// bubble step) with ballots and readlanes.  Codes are identical to
 // model_run's.
-__global__ __launch_bounds__(64) void k_fqz_model_hot(const FqzEvJob *Js, const uint32_t *hot,
-                                                      uint32_t stride) {
-    const FqzEvJob J = load_job(Js + blockIdx.y);
-    const uint32_t *list = hot + size_t(blockIdx.y) * stride;
-    const uint32_t nh = min(__builtin_amdgcn_readfirstlane(list[0]), stride - 1);
-    const uint32_t L = __builtin_amdgcn_readfirstlane(J.g->max_sym) + 1;   // live symbols
+template <int NE>
+DEV void hot_models(const FqzEvJob &J, const uint32_t *list, uint32_t nh, uint32_t L) {
     const uint32_t l = threadIdx.x;
     const auto rsv = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(J.sval), 0,
                                                        J.nev * 8u, 0x00020000);
-    const uint64_t slots = ((L >= 63 ? ~0ull : (2ull << L) - 1)) & ~1ull;   // lanes 1..L
+    auto rlane = [&](const uint32_t (&x)[NE], uint32_t dw) -> uint32_t {
+        if (NE == 1) return __builtin_amdgcn_readlane(x[0], dw);
+        const uint32_t a = __builtin_amdgcn_readlane(x[0], dw & 63u);
+        const uint32_t b = __builtin_amdgcn_readlane(x[NE - 1], dw & 63u);
+        return dw < 64 ? a : b;
+    };
+    uint64_t slots[NE];   // lanes of slots 1..L
+#pragma unroll
+    for (int r = 0; r < NE; r++) {
+        const uint32_t b0 = 64u * r;
+        const uint32_t lo = b0 < 1u ? 1u : b0, hi = L + 1u < b0 + 64u ? L + 1u : b0 + 64u;   // [lo, hi)
+        slots[r] = hi > lo ? (((hi - lo) == 64 ? ~0ull : ((1ull << (hi - lo)) - 1)) << (lo - b0)) : 0ull;
+    }
     for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
         const uint32_t m = __builtin_amdgcn_readfirstlane(list[1 + h]);
         const uint32_t lo = __builtin_amdgcn_readfirstlane(J.seg_lo[m]);
         const uint32_t hi = __builtin_amdgcn_readfirstlane(J.seg_hi[m]);
         // fl_init(live = L)
-        uint32_t fr = l == 0 ? FL_MAX : (l <= L ? 1u : 0u);
-        uint32_t cum = l == 0 ? 0u : (l <= L + 1 ? l - 1 : L);
-        uint32_t sy = l ? l - 1 : 0u;
+        uint32_t fr[NE], cum[NE], sy[NE];
+#pragma unroll
+        for (int r = 0; r < NE; r++) {
+            const uint32_t dw = l + 64u * r;
+            fr[r] = dw == 0 ? FL_MAX : (dw <= L ? 1u : 0u);
+            cum[r] = dw == 0 ? 0u : (dw <= L + 1 ? dw - 1 : L);
+            sy[r] = dw ? dw - 1 : 0u;
+        }
         uint32_t tot = L;
         uint32_t sn = __builtin_amdgcn_raw_buffer_load_b32(rsv, (lo + l) * 8u, 0, 0);
         for (uint32_t k0 = lo; k0 < hi; k0 += 64) {
@@ -476,7 +490,7 @@ __global__ __launch_bounds__(64) void k_fqz_model_hot(const FqzEvJob *Js, const 
             if (k0 + 64 < hi) sn = __builtin_amdgcn_raw_buffer_load_b32(rsv, (k0 + 64 + l) * 8u, 0, 0);
             const uint32_t nv = min(64u, hi - k0);
             uint64_t P = nv == 64 ? ~0ull : ((1ull << nv) - 1);
-            uint32_t s1 = __builtin_amdgcn_readlane(sy, 1), f1 = __builtin_amdgcn_readlane(fr, 1);
+            uint32_t s1 = __builtin_amdgcn_readlane(sy[0], 1), f1 = __builtin_amdgcn_readlane(fr[0], 1);
             uint64_t *code = J.code + k0;
             while (P) {
                 // ---- a run of head hits, coded in parallel ----------------
@@ -491,8 +505,9 @@ __global__ __launch_bounds__(64) void k_fqz_model_hot(const FqzEvJob *Js, const 
                         code[l] = (uint64_t(f1 + FL_STEP * n) << 16) |
                                   (uint64_t(tot + FL_STEP * n) << 32);
                     }
-                    fr += l == 1 ? FL_STEP * run : 0u;
-                    cum += l >= 2 ? FL_STEP * run : 0u;
+                    fr[0] += l == 1 ? FL_STEP * run : 0u;
+#pragma unroll
+                    for (int r = 0; r < NE; r++) cum[r] += l + 64u * r >= 2 ? FL_STEP * run : 0u;
                     f1 += FL_STEP * run;
                     tot += FL_STEP * run;
                     P &= ~(((run == 64) ? ~0ull : ((1ull << run) - 1)) << start);
@@ -501,44 +516,72 @@ __global__ __launch_bounds__(64) void k_fqz_model_hot(const FqzEvJob *Js, const 
                 // ---- one event through fl_bump ----------------------------
                 const uint32_t j0 = uint32_t(__builtin_ctzll(P));
                 const uint32_t sj = __builtin_amdgcn_readlane(sym, j0);
-                const uint64_t sm = uint64_t(__ballot(sy == sj)) & slots;
-                const uint32_t sl = sm ? uint32_t(__builtin_ctzll(sm)) : L + 1;   // always found
-                const uint32_t fs = __builtin_amdgcn_readlane(fr, sl);
-                const uint32_t cs = __builtin_amdgcn_readlane(cum, sl);
+                uint32_t sl = L + 1;   // always found
+#pragma unroll
+                for (int r = NE - 1; r >= 0; r--) {
+                    const uint64_t sm = uint64_t(__ballot(sy[r] == sj)) & slots[r];
+                    if (sm) sl = 64u * r + uint32_t(__builtin_ctzll(sm));
+                }
+                const uint32_t fs = rlane(fr, sl);
+                const uint32_t cs = rlane(cum, sl);
                 if (l == j0) code[l] = uint64_t(cs) | (uint64_t(fs) << 16) | (uint64_t(tot) << 32);
-                fr += l == sl ? FL_STEP : 0u;
-                cum += l > sl ? FL_STEP : 0u;
+#pragma unroll
+                for (int r = 0; r < NE; r++) {
+                    const uint32_t dw = l + 64u * r;
+                    fr[r] += dw == sl ? FL_STEP : 0u;
+                    cum[r] += dw > sl ? FL_STEP : 0u;
+                }
                 tot += FL_STEP;
                 if (tot > FL_MAX) {                 // halve slots 1..L, rebuild cum
-                    const bool live = l >= 1 && l <= L;
-                    if (live) fr -= fr >> 1;
-                    const uint32_t x = live ? fr : 0u;
-                    uint32_t inc = x;
+                    uint32_t carry = 0;
 #pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const uint32_t o = __shfl_up(inc, d, 64);
-                        if (int(l) >= d) inc += o;
+                    for (int r = 0; r < NE; r++) {
+                        const uint32_t dw = l + 64u * r;
+                        const bool live = dw >= 1 && dw <= L;
+                        if (live) fr[r] -= fr[r] >> 1;
+                        const uint32_t x = live ? fr[r] : 0u;
+                        uint32_t inc = x;
+#pragma unroll
+                        for (int d = 1; d < 64; d <<= 1) {
+                            const uint32_t o = __shfl_up(inc, d, 64);
+                            if (int(l) >= d) inc += o;
+                        }
+                        if (dw >= 1) cum[r] = carry + inc - x;
+                        carry += __builtin_amdgcn_readlane(inc, 63);
                     }
-                    if (l >= 1) cum = inc - x;
-                    tot = __builtin_amdgcn_readlane(inc, 63);
+                    tot = carry;
                 }
                 if (sl >= 2) {                      // one bubble step
-                    const uint32_t fa = __builtin_amdgcn_readlane(fr, sl - 1);
-                    const uint32_t fb = __builtin_amdgcn_readlane(fr, sl);
+                    const uint32_t fa = rlane(fr, sl - 1);
+                    const uint32_t fb = rlane(fr, sl);
                     if (fb > fa) {
-                        const uint32_t sa = __builtin_amdgcn_readlane(sy, sl - 1);
-                        const uint32_t sb = __builtin_amdgcn_readlane(sy, sl);
-                        const uint32_t ca = __builtin_amdgcn_readlane(cum, sl - 1);
-                        if (l == sl - 1) { fr = fb; sy = sb; }
-                        if (l == sl) { fr = fa; sy = sa; cum = ca + fb; }
+                        const uint32_t sa = rlane(sy, sl - 1);
+                        const uint32_t sb = rlane(sy, sl);
+                        const uint32_t ca = rlane(cum, sl - 1);
+#pragma unroll
+                        for (int r = 0; r < NE; r++) {
+                            const uint32_t dw = l + 64u * r;
+                            if (dw == sl - 1) { fr[r] = fb; sy[r] = sb; }
+                            if (dw == sl) { fr[r] = fa; sy[r] = sa; cum[r] = ca + fb; }
+                        }
                     }
                 }
-                s1 = __builtin_amdgcn_readlane(sy, 1);
-                f1 = __builtin_amdgcn_readlane(fr, 1);
+                s1 = __builtin_amdgcn_readlane(sy[0], 1);
+                f1 = __builtin_amdgcn_readlane(fr[0], 1);
                 P &= ~(1ull << j0);
             }
         }
     }
+}
+
+__global__ __launch_bounds__(64) void k_fqz_model_hot(const FqzEvJob *Js, const uint32_t *hot,
+                                                      uint32_t stride) {
+    const FqzEvJob J = load_job(Js + blockIdx.y);
+    const uint32_t *list = hot + size_t(blockIdx.y) * stride;
+    const uint32_t nh = min(__builtin_amdgcn_readfirstlane(list[0]), stride - 1);
+    const uint32_t L = __builtin_amdgcn_readfirstlane(J.g->max_sym) + 1;   // live symbols
+    if (L + 2 <= 64) hot_models<1>(J, list, nh, L);
+    else hot_models<2>(J, list, nh, L);
 }
 
 // Entropy of a block's events under the adaptive models: sum of
