@@ -887,10 +887,12 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
                          W.total, W.D.ment, W.D.nsets, c[0], c[1], c[2], c[3], c[4]);
             if (pr[0] | pr[1])
                 std::fprintf(stderr, "[fqz dec] probe: %.1f cycles/symbol inside the run asm over %llu symbols "
-                             "(%.1f%% of %u), %llu asm calls; raw %llu %llu %llu\n",
+                             "(%.1f%% of %u), %llu asm calls; %.0f cycles per miss() call, %.0f cycles "
+                             "between runs (%llu)\n",
                              double(pr[0]) / double(pr[1] ? pr[1] : 1), (unsigned long long)pr[1],
                              100.0 * double(pr[1]) / W.total, W.total, (unsigned long long)pr[2],
-                             (unsigned long long)pr[3], (unsigned long long)pr[4], (unsigned long long)pr[5]);
+                             double(pr[3]) / double(c[3] ? c[3] : 1), double(pr[4]) / double(pr[5] ? pr[5] : 1),
+                             (unsigned long long)pr[5]);
         }
     std::vector<std::vector<uint32_t>> lens(live.size());
     for (size_t i = 0; i < live.size(); i++) {

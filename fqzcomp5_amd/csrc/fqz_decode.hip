@@ -69,7 +69,7 @@ DEV void st8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
 DEV uint32_t U(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 #ifdef FQZ5_DEC_PROBE   // cycle stamps per stage of the fast loop (tools/)
-#define PROBE_DECL uint64_t pr_t = 0, pr[6] = {0, 0, 0, 0, 0, 0};
+#define PROBE_DECL uint64_t pr_t = 0, pr_x = 0, pr[6] = {0, 0, 0, 0, 0, 0};
 #define PROBE_START pr_t = __builtin_amdgcn_s_memtime();
 #define PROBE(i)                                        \
     {                                                   \
@@ -310,10 +310,10 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "v_readlane_b32 %[ma" Y "], %[t2], %[kl]\n"                             \
     "s_and_b64 %[SM], %[SM], %[E]\n"                                        \
     "s_cbranch_scc1 " SAMEL "\n"
-// the checks; SLOWL leaves with the state unchanged
+// the checks; SLOWL leaves with the state unchanged (TG kept: a miss)
 #define FQZ_CHECK(SLOWL)                                                    \
-    "s_or_b64 %[TG], %[TG], %[HV]\n"                                        \
-    "s_andn2_b64 %[E], %[E], %[TG]\n"                                       \
+    "s_or_b64 %[HV], %[HV], %[TG]\n"                                        \
+    "s_andn2_b64 %[E], %[E], %[HV]\n"                                       \
     "s_cbranch_scc0 " SLOWL "\n"
 // the coded slot's update (fl_bump): +16 to lane kl's frequency (E) and to
 // every later cum (G); a bubble step (SW & E) goes out of line to SWL and
@@ -361,7 +361,10 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_cbranch_scc1 " RNL "f\n"                                             \
     RETL ":\n"                                                              \
     "s_cmp_lt_u32 m0, %[lim]\n"
-// EXITL when the window needs a refill
+// When the window runs low (ub > ulim) its next 4 bytes come from the LDS
+// input ring (stream bytes rb + 8 .. rb + 11, big-endian into the window
+// below its valid bits); EXITL when the ring does not hold them yet (the
+// run's caller stages the next half) or the input ends.
 #define FQZ_RENORM_OUT(RNL, RETL, EXITL)                                    \
     RNL ":\n"                                                               \
     "s_mov_b32 s40, s43\n"                                                  \
@@ -370,8 +373,95 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_lshl_b32 %[rng], %[rng], %[z]\n"                                     \
     "s_add_u32 %[ub], %[ub], %[z]\n"                                        \
     "s_cmp_gt_u32 %[ub], %[ulim]\n"                                         \
+    "s_cbranch_scc0 " RETL "b\n"                                            \
+    "s_cmp_ge_u32 %[rb], %[rbend]\n"                                        \
     "s_cbranch_scc1 " EXITL "\n"                                            \
+    "s_add_u32 %[x], %[rb], 8\n"                                            \
+    "s_and_b32 %[k1], %[x], 0xffc\n"                                        \
+    "s_and_b32 %[kl], %[x], 3\n"                                            \
+    "s_add_u32 %[k1], %[k1], %[lring]\n"                                    \
+    "v_mov_b32 %[t4], %[k1]\n"                                              \
+    "ds_read_b32 %[t5], %[t4]\n"                                            \
+    "ds_read_b32 %[t6], %[t4] offset:4\n"                                   \
+    "s_lshl_b32 %[kl], %[kl], 3\n"                                          \
+    "s_sub_u32 %[ub], %[ub], 32\n"                                          \
+    "s_add_u32 %[rb], %[rb], 4\n"                                           \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "v_alignbit_b32 %[t5], %[t6], %[t5], %[kl]\n"                           \
+    "v_perm_b32 %[t5], %[t5], %[t5], %[bswp]\n"                             \
+    "s_mov_b32 s45, 0\n"                                                    \
+    "v_readfirstlane_b32 s44, %[t5]\n"                                      \
+    "s_lshl_b64 s[44:45], s[44:45], %[ub]\n"                                \
+    "s_or_b64 s[42:43], s[42:43], s[44:45]\n"                               \
     "s_branch " RETL "b\n"
+// A miss (the set holds another context, ev): ev's model, read again from
+// the set (the read that found it may predate the last write-back of the
+// same set), goes back to HBM
+// (J.back, agent-coherent stores) and into the LDS bitmap of evicted
+// contexts; the current context's comes from HBM when the bitmap has it,
+// else fresh (fe / fw; the sentinel lanes get context | L << 16); then the
+// set is rewritten and the symbol starts over at SKIPL.
+#define FQZ_MSENT_NONE(X) ""
+#define FQZ_MSENT_ST(X)                                                     \
+    "v_mad_u32_u24 %[t5], %[x], %[vme], %[vsent]\n"                         \
+    "global_store_dword %[t5], %[tv" X "], %[back] sc1\n"
+#define FQZ_MSENT_LD(X)                                                     \
+    "v_mad_u32_u24 %[t5], %[c" X "], %[vme], %[vsent]\n"                    \
+    "global_load_dword %[tv" X "], %[t5], %[back] sc1\n"
+#define FQZ_MSENT_RD(X)                                                     \
+    "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
+    "ds_read_b32 %[tv" X "], %[t5]\n"
+#define FQZ_MSENT_WR(X)                                                     \
+    "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
+    "ds_write_b32 %[t5], %[tv" X "]\n"
+#define FQZ_MISS(X, MX, EX, WX, MISSL, SKIPL, MST, MLD, MWB)                \
+    MISSL ":\n"                                                             \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "v_add_u32 %[t4], %[ma" X "], %[voff]\n"                                \
+    "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
+    "ds_read_b64 " MX ", %[t4]\n"                                           \
+    "ds_read_b32 %[tv" X "], %[t5]\n"                                       \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "v_readfirstlane_b32 %[x], %[tv" X "]\n"                                \
+    "s_and_b32 %[x], %[x], 0xffff\n"                                        \
+    "v_mad_u32_u24 %[t4], %[x], %[vme], %[voff]\n"                          \
+    "global_store_dwordx2 %[t4], " MX ", %[back] sc1\n"                     \
+    MST(X)                                                                  \
+    "s_lshr_b32 %[k1], %[x], 3\n"                                           \
+    "s_and_b32 %[k1], %[k1], 0x1ffc\n"                                      \
+    "s_add_u32 %[k1], %[k1], %[lbits]\n"                                    \
+    "s_lshl_b32 %[kl], 1, %[x]\n"                                           \
+    "v_mov_b32 %[t5], %[k1]\n"                                              \
+    "v_mov_b32 %[t6], %[kl]\n"                                              \
+    "ds_or_b32 %[t5], %[t6]\n"                                              \
+    "s_lshr_b32 %[k1], %[c" X "], 3\n"                                      \
+    "s_and_b32 %[k1], %[k1], 0x1ffc\n"                                      \
+    "s_add_u32 %[k1], %[k1], %[lbits]\n"                                    \
+    "v_mov_b32 %[t5], %[k1]\n"                                              \
+    "ds_read_b32 %[t6], %[t5]\n"                                            \
+    "s_add_u32 %[nm], %[nm], 1\n"                                           \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "v_readfirstlane_b32 %[kl], %[t6]\n"                                    \
+    "s_bitcmp1_b32 %[kl], %[c" X "]\n"                                      \
+    "s_cbranch_scc0 6f\n"                                                   \
+    "v_mad_u32_u24 %[t4], %[c" X "], %[vme], %[voff]\n"                     \
+    "global_load_dwordx2 " MX ", %[t4], %[back] sc1\n"                      \
+    MLD(X)                                                                  \
+    "s_waitcnt vmcnt(0)\n"                                                  \
+    "s_branch 7f\n"                                                         \
+    "6:\n"                                                                  \
+    "s_or_b32 %[k1], %[c" X "], %[lsh]\n"                                   \
+    "v_mov_b32 %[tv" X "], %[k1]\n"                                         \
+    "v_cmp_eq_u32_e64 %[G], %[voff], %[vsent]\n"                            \
+    "v_mov_b32 " WX ", %[fw]\n"                                             \
+    "s_nop 1\n"                                                             \
+    "v_cndmask_b32 " EX ", %[fe], %[tv" X "], %[G]\n"                       \
+    "7:\n"                                                                  \
+    "v_add_u32 %[t4], %[ma" X "], %[voff]\n"                                \
+    "ds_write_b64 %[t4], " MX "\n"                                          \
+    MWB(X)                                                                  \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "s_branch " SKIPL "b\n"
 // the coder and the context state; the symbol to output lane m0
 #define FQZ_CODER(X, Y, QSD)                                                \
     "s_sub_u32 s41, s41, %[pk]\n"                                           \
@@ -421,7 +511,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 // same-context paths, 12/22 the slow exits; 30 exits in the A state, 31 in
 // the B state; 41-48 out-of-line bubble steps and renormalisations, 51-58
 // their way back
-#define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME, SENTWB, SENTEX, WCNT)        \
+#define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME, SENTWB, SENTEX, WCNT, MST, MLD, MWB) \
     "s_mov_b32 %[m0s], m0\n"                                                \
     "s_mov_b32 m0, %[done]\n"                                               \
     "s_mov_b32 %[flags], 0\n"                                               \
@@ -450,10 +540,16 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     FQZ_RENORM_OUT("46", "56", "30f")                                       \
     FQZ_SWAP("v4", "v5", "47", "57")                                        \
     FQZ_RENORM_OUT("48", "58", "31f")                                       \
+    FQZ_MISS("A", "v[2:3]", "v2", "v3", "60", "13", MST, MLD, MWB)          \
+    FQZ_MISS("B", "v[4:5]", "v4", "v5", "61", "23", MST, MLD, MWB)          \
     "12:\n"                                                                 \
+    "s_cmp_lg_u64 %[TG], 0\n"                                               \
+    "s_cbranch_scc1 60b\n"                                                  \
     "s_mov_b32 %[flags], 2\n"                                               \
     "s_branch 30f\n"                                                        \
     "22:\n"                                                                 \
+    "s_cmp_lg_u64 %[TG], 0\n"                                               \
+    "s_cbranch_scc1 61b\n"                                                  \
     "s_mov_b32 %[flags], 2\n"                                               \
     "31:\n"                                                                 \
     "s_waitcnt lgkmcnt(0)\n"                                                \
@@ -635,6 +731,9 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     // create ctx's
     auto miss = [&](uint32_t tag) {
         nmiss++;
+#ifdef FQZ5_DEC_PROBE
+        const uint64_t tm = __builtin_amdgcn_s_memtime();
+#endif
         uint32_t *m32 = reinterpret_cast<uint32_t *>(lds + maddr);
         uint32_t *bits = reinterpret_cast<uint32_t *>(lds + L_BITS);
         uint32_t *dst = reinterpret_cast<uint32_t *>(J.back + size_t(tag) * ME);
@@ -651,6 +750,10 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             if (l == 0) *reinterpret_cast<uint2 *>(lds + maddr + sent) = make_uint2(ctx | (L << 16), 0u);
         }
         __builtin_amdgcn_wave_barrier();
+#ifdef FQZ5_DEC_PROBE
+        (void)U(m32[0]);
+        pr[3] += __builtin_amdgcn_s_memtime() - tm;   // cycles in miss()
+#endif
     };
     auto load_model = [&]() {
         for (;;) {
@@ -891,8 +994,23 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             uint32_t tvA = model_sentinel(), tvB = 0;
             uint32_t cA = U(ctx), qsA = U(qs), pvA = U(prevq), maA = U(maddr), sqA = U(seq);
             uint32_t cB, qsB, pvB, maB, sqB;
-            uint32_t dd = 0;
+            uint32_t dd = 0, nm = 0;
+            uint64_t scr;
+            // the miss path: the backing store, fresh slots (guard, list; the
+            // sentinel lanes are set from the context)
+            const uint64_t back = reinterpret_cast<uint64_t>(J.back);
+            const uint32_t lsh = U(L << 16);
+            const uint32_t fe = l == 0 ? 0xffffu : (l <= LL ? 1u | ((l - 1u) << 16) : 0u);
+            const uint32_t fw = l == 0 || l > LL ? 0u : uint32_t(qt0[l - 1u]) | ((l - 1u) << 24);
             rng = U(rng);
+            in.rb = U(in.rb);
+            const uint32_t bswp = 0x00010203u;   // v_perm byte reversal
+            // the window refills in the run while the ring holds rb + 8 .. rb + 11
+            auto rb_end = [&]() {
+                const uint32_t e = in.len < in.lp ? in.len : in.lp;
+                return U(e >= 12u ? e - 11u : 0u);
+            };
+            uint32_t rbend = rb_end();
             in.ub = U(in.ub);
             lim = U(lim);
             ulim = U(ulim);
@@ -909,7 +1027,9 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             for (;;) {
 #define FQZ_RUN_OPERANDS                                                                      \
                 : [mA] "+{v[2:3]}"(mA), [mB] "+{v[4:5]}"(mB), [cw] "+{s[40:41]}"(cw),          \
-                  [win] "+{s[42:43]}"(win), [vout] "+v"(vout), [tvA] "+v"(tvA), [tvB] "=&v"(tvB), \
+                  [win] "+{s[42:43]}"(win), [scr] "=&{s[44:45]}"(scr), [rb] "+s"(in.rb),        \
+                  [nm] "+s"(nm),                                                               \
+                  [vout] "+v"(vout), [tvA] "+v"(tvA), [tvB] "=&v"(tvB),                           \
                   [rng] "+s"(rng), [ub] "+s"(in.ub), [dd] "+s"(dd), [done] "+s"(done),        \
                   [cA] "+s"(cA), [qsA] "+s"(qsA), [pvA] "+s"(pvA), [maA] "+s"(maA), [sqA] "+s"(sqA), \
                   [cB] "=&s"(cB), [qsB] "=&s"(qsB), [pvB] "=&s"(pvB), [maB] "=&s"(maB), [sqB] "=&s"(sqB), \
@@ -922,7 +1042,9 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                   [d0] "=&v"(d0), [d1] "=&v"(d1), [d2] "=&v"(d2)                               \
                 : [lim] "s"(lim), [ulim] "s"(ulim), [qmask] "s"(qmask), [qshift] "s"(qshift), \
                   [ns8] "s"(ns8), [base] "s"(base), [qtab] "s"(qtab), [bmask] "s"(bmask),     \
-                  [bloc] "s"(bloc), [c65503] "s"(c65503),                                       \
+                  [bloc] "s"(bloc), [c65503] "s"(c65503), [rbend] "s"(rbend), [bswp] "s"(bswp), \
+                  [lring] "i"(L_RING), [lbits] "i"(L_BITS), [back] "s"(back), [lsh] "s"(lsh),   \
+                  [fe] "v"(fe), [fw] "v"(fw),                                                  \
                   [voff] "v"(voff0), [vsent] "v"(vsent), [qlocv] "v"(qlocv),                   \
                   [cbig] "v"(cbig), [c19] "v"(c19), [vme] "v"(vme), [pvv] "v"(pvv),          \
                   [dvv] "v"(dvv), [sqv] "v"(sqv)                                              \
@@ -930,22 +1052,27 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
 #ifdef FQZ5_DEC_PROBE
                 const uint32_t done_in = done;
                 const uint64_t ta = __builtin_amdgcn_s_memtime();
+                if (pr_x) {
+                    pr[4] += ta - pr_x;   // cycles between runs
+                    pr[5] += 1;
+                }
 #endif
-#define FQZ_RUN_NE(SENTWB, SENTEX, WCNT)                                                                           \
+#define FQZ_RUN_NE(SENTWB, SENTEX, WCNT, MST, MLD, MWB)                                                                           \
                 if constexpr (QW && SEQ)                                                                     \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MWB) FQZ_RUN_OPERANDS); \
                 else if constexpr (QW)                                                                       \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MWB) FQZ_RUN_OPERANDS); \
                 else if constexpr (SEQ)                                                                      \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MWB) FQZ_RUN_OPERANDS); \
                 else                                                                                         \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT) FQZ_RUN_OPERANDS);
-                if constexpr (NE == 1) { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1") }
-                else { FQZ_RUN_NE(FQZ_SENT_WB, FQZ_SENT_EXIT, "2") }
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MWB) FQZ_RUN_OPERANDS);
+                if constexpr (NE == 1) { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1", FQZ_MSENT_NONE, FQZ_MSENT_NONE, FQZ_MSENT_RD) }
+                else { FQZ_RUN_NE(FQZ_SENT_WB, FQZ_SENT_EXIT, "2", FQZ_MSENT_ST, FQZ_MSENT_LD, FQZ_MSENT_WR) }
 #undef FQZ_RUN_NE
 #undef FQZ_RUN_OPERANDS
 #ifdef FQZ5_DEC_PROBE
-                pr[0] += __builtin_amdgcn_s_memtime() - ta;   // cycles inside the run asm
+                pr_x = __builtin_amdgcn_s_memtime();
+                pr[0] += pr_x - ta;                           // cycles inside the run asm
                 pr[1] += U(done) - done_in;                   // symbols it decoded
                 pr[2] += 1;                                   // calls
 #endif
@@ -953,8 +1080,10 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 // for divergent: the scalar ones are re-read as uniform)
                 rng = U(rng);
                 in.ub = U(in.ub);
+                in.rb = U(in.rb);
                 dd = U(dd);
                 done = U(done);
+                nm = U(nm);
                 cA = U(cA);
                 qsA = U(qsA);
                 pvA = U(pvA);
@@ -973,6 +1102,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 win = in.W;
                 if (in.vb < 4u) break;
                 ulim = (in.vb - 4u) * 8u;
+                rbend = rb_end();
             }
             in.W = win;
             code = uint32_t(cw >> 32);
@@ -982,6 +1112,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             maddr = maA;
             seq = sqA;
             delta = delta0 + dd;
+            nmiss += nm;
             left -= done;
             if (SEQ) tpos += done;
         }
