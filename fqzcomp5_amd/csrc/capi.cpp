@@ -328,6 +328,22 @@ int fqz5_rans_uncompress_batch(fqz5_rans_job *jobs, int n) {
     GUARD_END(-1)
 }
 
+int fqz5_stream_wait(void *stream) {
+    try {
+        GpuCtx &g = gpu();
+        // one event per thread, re-recorded: the library stream waits for
+        // the work enqueued on `stream` so far (device-side, no host sync)
+        static thread_local hipEvent_t ev = nullptr;
+        if (!ev) FQZ5_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        FQZ5_HIP(hipEventRecord(ev, static_cast<hipStream_t>(stream)));
+        FQZ5_HIP(hipStreamWaitEvent(g.stream, ev, 0));
+        return 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
 void *fqz5_stream(void) {
     try {
         return gpu().stream;

@@ -401,22 +401,28 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 // contexts; the current context's comes from HBM when the bitmap has it,
 // else fresh (fe / fw; the sentinel lanes get context | L << 16); then the
 // set is rewritten and the symbol starts over at SKIPL.
-#define FQZ_MSENT_NONE(X) ""
-#define FQZ_MSENT_ST(X)                                                     \
+#define FQZ_MSENT_NONE(X, Y) ""
+#define FQZ_MSENT_ST(X, Y)                                                  \
     "v_mad_u32_u24 %[t5], %[x], %[vme], %[vsent]\n"                         \
     "global_store_dword %[t5], %[tv" X "], %[back] sc1\n"
-#define FQZ_MSENT_LD(X)                                                     \
+#define FQZ_MSENT_LD(X, Y)                                                  \
     "v_mad_u32_u24 %[t5], %[c" X "], %[vme], %[vsent]\n"                    \
-    "global_load_dword %[tv" X "], %[t5], %[back] sc1\n"
+    "global_load_dword %[tv" Y "], %[t5], %[back] sc1\n"
+#define FQZ_MSENT_MOV(X, Y) "v_mov_b32 %[tv" X "], %[tv" Y "]\n"
 #define FQZ_MSENT_RD(X)                                                     \
     "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
     "ds_read_b32 %[tv" X "], %[t5]\n"
 #define FQZ_MSENT_WR(X)                                                     \
     "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
     "ds_write_b32 %[t5], %[tv" X "]\n"
-#define FQZ_MISS(X, MX, EX, WX, MISSL, SKIPL, MST, MLD, MWB)                \
+// the fetch of the current context's model from HBM is issued first (into
+// the other register pair, free during a miss) and overlaps the rest
+#define FQZ_MISS(X, Y, MX, EX, WX, MY, EY, WY, MISSL, SKIPL, MST, MLD, MMOV, MWB) \
     MISSL ":\n"                                                             \
     "s_waitcnt lgkmcnt(0)\n"                                                \
+    "v_mad_u32_u24 %[t4], %[c" X "], %[vme], %[voff]\n"                     \
+    "global_load_dwordx2 " MY ", %[t4], %[back] sc1\n"                      \
+    MLD(X, Y)                                                               \
     "v_add_u32 %[t4], %[ma" X "], %[voff]\n"                                \
     "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
     "ds_read_b64 " MX ", %[t4]\n"                                           \
@@ -426,7 +432,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_and_b32 %[x], %[x], 0xffff\n"                                        \
     "v_mad_u32_u24 %[t4], %[x], %[vme], %[voff]\n"                          \
     "global_store_dwordx2 %[t4], " MX ", %[back] sc1\n"                     \
-    MST(X)                                                                  \
+    MST(X, Y)                                                               \
     "s_lshr_b32 %[k1], %[x], 3\n"                                           \
     "s_and_b32 %[k1], %[k1], 0x1ffc\n"                                      \
     "s_add_u32 %[k1], %[k1], %[lbits]\n"                                    \
@@ -443,11 +449,11 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_waitcnt lgkmcnt(0)\n"                                                \
     "v_readfirstlane_b32 %[kl], %[t6]\n"                                    \
     "s_bitcmp1_b32 %[kl], %[c" X "]\n"                                      \
-    "s_cbranch_scc0 6f\n"                                                   \
-    "v_mad_u32_u24 %[t4], %[c" X "], %[vme], %[voff]\n"                     \
-    "global_load_dwordx2 " MX ", %[t4], %[back] sc1\n"                      \
-    MLD(X)                                                                  \
     "s_waitcnt vmcnt(0)\n"                                                  \
+    "s_cbranch_scc0 6f\n"                                                   \
+    "v_mov_b32 " EX ", " EY "\n"                                            \
+    "v_mov_b32 " WX ", " WY "\n"                                            \
+    MMOV(X, Y)                                                              \
     "s_branch 7f\n"                                                         \
     "6:\n"                                                                  \
     "s_or_b32 %[k1], %[c" X "], %[lsh]\n"                                   \
@@ -511,7 +517,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 // same-context paths, 12/22 the slow exits; 30 exits in the A state, 31 in
 // the B state; 41-48 out-of-line bubble steps and renormalisations, 51-58
 // their way back
-#define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME, SENTWB, SENTEX, WCNT, MST, MLD, MWB) \
+#define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) \
     "s_mov_b32 %[m0s], m0\n"                                                \
     "s_mov_b32 m0, %[done]\n"                                               \
     "s_mov_b32 %[flags], 0\n"                                               \
@@ -540,8 +546,8 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     FQZ_RENORM_OUT("46", "56", "30f")                                       \
     FQZ_SWAP("v4", "v5", "47", "57")                                        \
     FQZ_RENORM_OUT("48", "58", "31f")                                       \
-    FQZ_MISS("A", "v[2:3]", "v2", "v3", "60", "13", MST, MLD, MWB)          \
-    FQZ_MISS("B", "v[4:5]", "v4", "v5", "61", "23", MST, MLD, MWB)          \
+    FQZ_MISS("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", "v4", "v5", "60", "13", MST, MLD, MMOV, MWB) \
+    FQZ_MISS("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", "v2", "v3", "61", "23", MST, MLD, MMOV, MWB) \
     "12:\n"                                                                 \
     "s_cmp_lg_u64 %[TG], 0\n"                                               \
     "s_cbranch_scc1 60b\n"                                                  \
@@ -1057,17 +1063,17 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                     pr[5] += 1;
                 }
 #endif
-#define FQZ_RUN_NE(SENTWB, SENTEX, WCNT, MST, MLD, MWB)                                                                           \
+#define FQZ_RUN_NE(SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB)                                                                           \
                 if constexpr (QW && SEQ)                                                                     \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MWB) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) FQZ_RUN_OPERANDS); \
                 else if constexpr (QW)                                                                       \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MWB) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) FQZ_RUN_OPERANDS); \
                 else if constexpr (SEQ)                                                                      \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MWB) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) FQZ_RUN_OPERANDS); \
                 else                                                                                         \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MWB) FQZ_RUN_OPERANDS);
-                if constexpr (NE == 1) { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1", FQZ_MSENT_NONE, FQZ_MSENT_NONE, FQZ_MSENT_RD) }
-                else { FQZ_RUN_NE(FQZ_SENT_WB, FQZ_SENT_EXIT, "2", FQZ_MSENT_ST, FQZ_MSENT_LD, FQZ_MSENT_WR) }
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) FQZ_RUN_OPERANDS);
+                if constexpr (NE == 1) { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1", FQZ_MSENT_NONE, FQZ_MSENT_NONE, FQZ_MSENT_NONE, FQZ_MSENT_RD) }
+                else { FQZ_RUN_NE(FQZ_SENT_WB, FQZ_SENT_EXIT, "2", FQZ_MSENT_ST, FQZ_MSENT_LD, FQZ_MSENT_MOV, FQZ_MSENT_WR) }
 #undef FQZ_RUN_NE
 #undef FQZ_RUN_OPERANDS
 #ifdef FQZ5_DEC_PROBE

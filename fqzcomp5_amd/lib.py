@@ -90,6 +90,8 @@ def load() -> C.CDLL:
     lib.fqz5_rans_uncompress_batch.restype = C.c_int
     lib.fqz5_rans_uncompress_batch.argtypes = [C.POINTER(RansJob), C.c_int]
     lib.fqz5_stream.restype = C.c_void_p
+    lib.fqz5_stream_wait.restype = C.c_int
+    lib.fqz5_stream_wait.argtypes = [C.c_void_p]
     lib.fqz5_device_ok.restype = C.c_int
     lib.fqz5_last_error.restype = C.c_char_p
     lib.fqz_compress.restype = C.c_void_p
@@ -362,6 +364,14 @@ def unlzp(data: bytes, out_cap: int) -> bytes | None:
 def crc32(data: bytes, crc: int = 0) -> int:
     """zlib.crc32 computed on the GPU (fqz5_crc32, host buffer)."""
     return int(load().fqz5_crc32(crc, bytes(data), len(data)))
+
+
+def stream_wait(stream: int) -> None:
+    """Order the library's stream after the work enqueued so far on
+    `stream` (a hipStream_t as int, e.g. torch's Stream.cuda_stream):
+    fqz5_stream_wait, the ordering contract of the device-pointer calls."""
+    if load().fqz5_stream_wait(C.c_void_p(stream)):
+        raise NativeError("fqz5_stream_wait failed: " + last_error())
 
 
 def crc32_dev(ptr: int, n: int, crc: int = 0) -> int:

@@ -214,6 +214,22 @@ int fqz5_rans_uncompress_batch(fqz5_rans_job *jobs, int n);
 /* HIP stream (hipStream_t) that the calling thread's batches run on. */
 void *fqz5_stream(void);
 
+/* Ordering contract of the device-pointer entry points (fqz5_crc32_dev,
+ * fqz5_rans_*_batch, fqz5_sections_*, fqz5_encode_sections,
+ * fqz5_decode_sections, fqz5_blocks_assemble, fqz5_block_parse,
+ * fqz5_block_lengths, fqz5_fastq_*):
+ *  - inputs: they read device buffers on fqz5_stream().  A buffer written on
+ *    another stream must be complete first: synchronise that stream, or call
+ *    fqz5_stream_wait(producer) before the entry point (device-side wait,
+ *    the host does not block);
+ *  - outputs: every device output is written when the call returns (the
+ *    calls synchronise fqz5_stream() before returning), so any stream may
+ *    read it afterwards.
+ * fqz5_stream_wait: the calling thread's fqz5_stream() waits for all work
+ * enqueued on `stream` (a hipStream_t; NULL = the null stream) so far.
+ * Returns 0 or -1. */
+int fqz5_stream_wait(void *stream);
+
 /* 1 if a HIP device is usable, else 0 (and fqz5_last_error() is set). */
 int fqz5_device_ok(void);
 
