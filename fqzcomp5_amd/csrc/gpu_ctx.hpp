@@ -164,9 +164,16 @@ struct GpuCtx {
     // there are no more chains than CUs, ask for more than half a CU's LDS
     // so that no two chains share a CU (measured: 20 chains of one launch
     // ran ~15 % slower per step than one alone when allowed to pack).
+    // LDS of a launch of one-wave chain workgroups, padded so that no two
+    // chains share a SIMD: one workgroup per CU while they fit, else at most
+    // four per CU (the dispatcher gives them four different SIMDs).  Two
+    // chains on one SIMD share its issue slots and each runs at half speed
+    // (measured: 46 such pairs in a 393-workgroup -5 decode launch).
     uint32_t chain_lds(uint32_t lds, size_t jobs) const {
-        constexpr uint32_t HALF_CU = 80 * 1024 + 16;
-        return jobs <= size_t(cus) && lds < HALF_CU ? HALF_CU : lds;
+        constexpr uint32_t HALF_CU = 80 * 1024 + 16, FIFTH_CU = 32 * 1024 + 16;
+        if (jobs <= size_t(cus)) return lds < HALF_CU ? HALF_CU : lds;
+        if (jobs <= 4 * size_t(cus)) return lds < FIFTH_CU ? FIFTH_CU : lds;
+        return lds;
     }
 
     // high_prio: the streams of a helper context (gpu_aux) get the device's

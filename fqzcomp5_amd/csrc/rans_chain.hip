@@ -1192,7 +1192,7 @@ __global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
                 g_jobt[blockIdx.x][0] = t0;
                 g_jobt[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
                 g_jobt[blockIdx.x][2] = __builtin_amdgcn_s_memtime() - c0;
-                g_jobt[blockIdx.x][3] = uint64_t(J.n) << 32 | (xcc & 0xf) << 24 | ((hw >> 8) & 0xf) << 16 | ((hw >> 13) & 0x7) << 8 | ((hw >> 4) & 3);
+                g_jobt[blockIdx.x][3] = uint64_t(J.n) << 32 | (xcc & 0xf) << 24 | ((hw >> 8) & 0x1f) << 16 | ((hw >> 13) & 0x7) << 8 | ((hw >> 4) & 3);
                 g_jobt[blockIdx.x][6] = uint64_t(J.alpha ? J.rows : 0u) | uint64_t(J.nx) << 16 | uint64_t(J.mode) << 24;
                 g_jobt[blockIdx.x][7] = J.in_len;
             }
