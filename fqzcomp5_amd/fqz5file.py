@@ -22,8 +22,8 @@ file equals the reference CLI's `-<level> -t1` output byte for byte.
 Scope: 4-line FASTQ and FASTA with any line wrapping (text starting with
 '>': blocks without a quality section, decoded to output_fasta's one-line
 text, fqzcomp5.c:2258-2264, :3503-3517); the parser refuses multi-line FASTQ
-records with an error (there is no host parse); files that fit in device
-memory.
+records with an error (there is no host parse).  Files of any size stream
+through in windows of whole records (see below), on one or several ranks.
 """
 from __future__ import annotations
 
