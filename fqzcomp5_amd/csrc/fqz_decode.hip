@@ -396,18 +396,19 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_branch " RETL "b\n"
 // A miss (the set holds another context, ev): ev's model, read again from
 // the set (the read that found it may predate the last write-back of the
-// same set), goes back to HBM
-// (J.back, agent-coherent stores) and into the LDS bitmap of evicted
+// same set), goes back to HBM (J.back, work-group scope: sc0; the store is
+// private to this wave, so its lines stay in the XCD's L2, where device
+// scope, sc1, would send every fetch past it) and into the LDS bitmap of evicted
 // contexts; the current context's comes from HBM when the bitmap has it,
 // else fresh (fe / fw; the sentinel lanes get context | L << 16); then the
 // set is rewritten and the symbol starts over at SKIPL.
 #define FQZ_MSENT_NONE(X, Y) ""
 #define FQZ_MSENT_ST(X, Y)                                                  \
     "v_mad_u32_u24 %[t5], %[x], %[vme], %[vsent]\n"                         \
-    "global_store_dword %[t5], %[tv" X "], %[back] sc1\n"
+    "global_store_dword %[t5], %[tv" X "], %[back] sc0\n"
 #define FQZ_MSENT_LD(X, Y)                                                  \
     "v_mad_u32_u24 %[t5], %[c" X "], %[vme], %[vsent]\n"                    \
-    "global_load_dword %[tv" Y "], %[t5], %[back] sc1\n"
+    "global_load_dword %[tv" Y "], %[t5], %[back] sc0\n"
 #define FQZ_MSENT_MOV(X, Y) "v_mov_b32 %[tv" X "], %[tv" Y "]\n"
 #define FQZ_MSENT_RD(X)                                                     \
     "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
@@ -421,7 +422,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     MISSL ":\n"                                                             \
     "s_waitcnt lgkmcnt(0)\n"                                                \
     "v_mad_u32_u24 %[t4], %[c" X "], %[vme], %[voff]\n"                     \
-    "global_load_dwordx2 " MY ", %[t4], %[back] sc1\n"                      \
+    "global_load_dwordx2 " MY ", %[t4], %[back] sc0\n"                      \
     MLD(X, Y)                                                               \
     "v_add_u32 %[t4], %[ma" X "], %[voff]\n"                                \
     "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
@@ -431,7 +432,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "v_readfirstlane_b32 %[x], %[tv" X "]\n"                                \
     "s_and_b32 %[x], %[x], 0xffff\n"                                        \
     "v_mad_u32_u24 %[t4], %[x], %[vme], %[voff]\n"                          \
-    "global_store_dwordx2 %[t4], " MX ", %[back] sc1\n"                     \
+    "global_store_dwordx2 %[t4], " MX ", %[back] sc0\n"                     \
     MST(X, Y)                                                               \
     "s_lshr_b32 %[k1], %[x], 3\n"                                           \
     "s_and_b32 %[k1], %[k1], 0x1ffc\n"                                      \
@@ -744,13 +745,13 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         uint32_t *bits = reinterpret_cast<uint32_t *>(lds + L_BITS);
         uint32_t *dst = reinterpret_cast<uint32_t *>(J.back + size_t(tag) * ME);
         for (uint32_t o = l; o < ME / 4; o += 64)
-            __hip_atomic_store(dst + o, m32[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(dst + o, m32[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (l == 0) bits[tag >> 5] |= 1u << (tag & 31);
         __builtin_amdgcn_wave_barrier();
         if ((U(bits[ctx >> 5]) >> (ctx & 31)) & 1u) {
             const uint32_t *src = reinterpret_cast<const uint32_t *>(J.back + size_t(ctx) * ME);
             for (uint32_t o = l; o < ME / 4; o += 64)
-                m32[o] = __hip_atomic_load(src + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                m32[o] = __hip_atomic_load(src + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else {
             fresh_slots(maddr);
             if (l == 0) *reinterpret_cast<uint2 *>(lds + maddr + sent) = make_uint2(ctx | (L << 16), 0u);
@@ -786,13 +787,13 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         fs[0] = s0;
         if constexpr (NE == 2) {
             const uint32_t sv = model_sentinel(), dw = 64u + l;
-            const bool hi = (__hip_atomic_load(J.hi_bits + (ctx >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >>
+            const bool hi = (__hip_atomic_load(J.hi_bits + (ctx >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
                              (ctx & 31)) & 1u;
             uint32_t f = 0, sy = 0;
             if (dw <= L) {
                 if (hi) {
                     const uint32_t x = __hip_atomic_load(J.back_hi + size_t(ctx) * 64u + l, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
                     f = x & 0xffffu;
                     sy = x >> 16;
                 } else {
@@ -820,11 +821,11 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             if (l == 0) *reinterpret_cast<uint2 *>(lds + maddr + sent) = make_uint2(sv, 0u);
             if (dw <= L)
                 __hip_atomic_store(J.back_hi + size_t(ctx) * 64u + l, (fv[1] & 0xffffu) | ((fs[1] >> 24) << 16),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (l == 0) {
                 uint32_t *hb = J.hi_bits + (ctx >> 5);
-                __hip_atomic_store(hb, __hip_atomic_load(hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
-                                       (1u << (ctx & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(hb, __hip_atomic_load(hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) |
+                                       (1u << (ctx & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
         __builtin_amdgcn_wave_barrier();
