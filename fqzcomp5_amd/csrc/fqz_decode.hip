@@ -403,33 +403,42 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 // else fresh (fe / fw; the sentinel lanes get context | L << 16); then the
 // set is rewritten and the symbol starts over at SKIPL.
 #define FQZ_MSENT_NONE(X, Y) ""
+#define FQZ_MSENT_NONE1(X) ""
 #define FQZ_MSENT_ST(X, Y)                                                  \
     "v_mad_u32_u24 %[t5], %[x], %[vme], %[vsent]\n"                         \
     "global_store_dword %[t5], %[tv" X "], %[back] sc0\n"
 #define FQZ_MSENT_LD(X, Y)                                                  \
     "v_mad_u32_u24 %[t5], %[c" X "], %[vme], %[vsent]\n"                    \
     "global_load_dword %[tv" Y "], %[t5], %[back] sc0\n"
-#define FQZ_MSENT_MOV(X, Y) "v_mov_b32 %[tv" X "], %[tv" Y "]\n"
-#define FQZ_MSENT_RD(X)                                                     \
-    "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
-    "ds_read_b32 %[tv" X "], %[t5]\n"
+#define FQZ_MSENT_MOV(X, Y, EX) "v_mov_b32 %[tv" X "], %[tv" Y "]\n"
+#define FQZ_MSENT_LANE(X, Y, EX)                                            \
+    "v_readlane_b32 %[x], " EX ", %[sidx]\n"                                \
+    "v_mov_b32 %[tv" X "], %[x]\n"
 #define FQZ_MSENT_WR(X)                                                     \
     "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
     "ds_write_b32 %[t5], %[tv" X "]\n"
 // the fetch of the current context's model from HBM is issued first (into
-// the other register pair, free during a miss) and overlaps the rest
+// the other register pair, free during a miss), then the set and the
+// bitmap word are read together; the rest overlaps the fetch
 #define FQZ_MISS(X, Y, MX, EX, WX, MY, EY, WY, MISSL, SKIPL, MST, MLD, MMOV, MWB) \
     MISSL ":\n"                                                             \
     "s_waitcnt lgkmcnt(0)\n"                                                \
     "v_mad_u32_u24 %[t4], %[c" X "], %[vme], %[voff]\n"                     \
     "global_load_dwordx2 " MY ", %[t4], %[back] sc0\n"                      \
     MLD(X, Y)                                                               \
+    "s_lshr_b32 %[k1], %[c" X "], 3\n"                                      \
+    "s_and_b32 %[k1], %[k1], 0x1ffc\n"                                      \
+    "s_add_u32 %[k1], %[k1], %[lbits]\n"                                    \
     "v_add_u32 %[t4], %[ma" X "], %[voff]\n"                                \
     "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
+    "v_mov_b32 %[t6], %[k1]\n"                                              \
     "ds_read_b64 " MX ", %[t4]\n"                                           \
     "ds_read_b32 %[tv" X "], %[t5]\n"                                       \
+    "ds_read_b32 %[t6], %[t6]\n"                                            \
+    "s_add_u32 %[nm], %[nm], 1\n"                                           \
     "s_waitcnt lgkmcnt(0)\n"                                                \
     "v_readfirstlane_b32 %[x], %[tv" X "]\n"                                \
+    "v_readfirstlane_b32 %[kl], %[t6]\n"                                    \
     "s_and_b32 %[x], %[x], 0xffff\n"                                        \
     "v_mad_u32_u24 %[t4], %[x], %[vme], %[voff]\n"                          \
     "global_store_dwordx2 %[t4], " MX ", %[back] sc0\n"                     \
@@ -437,24 +446,16 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_lshr_b32 %[k1], %[x], 3\n"                                           \
     "s_and_b32 %[k1], %[k1], 0x1ffc\n"                                      \
     "s_add_u32 %[k1], %[k1], %[lbits]\n"                                    \
-    "s_lshl_b32 %[kl], 1, %[x]\n"                                           \
+    "s_lshl_b32 %[z], 1, %[x]\n"                                            \
     "v_mov_b32 %[t5], %[k1]\n"                                              \
-    "v_mov_b32 %[t6], %[kl]\n"                                              \
+    "v_mov_b32 %[t6], %[z]\n"                                               \
     "ds_or_b32 %[t5], %[t6]\n"                                              \
-    "s_lshr_b32 %[k1], %[c" X "], 3\n"                                      \
-    "s_and_b32 %[k1], %[k1], 0x1ffc\n"                                      \
-    "s_add_u32 %[k1], %[k1], %[lbits]\n"                                    \
-    "v_mov_b32 %[t5], %[k1]\n"                                              \
-    "ds_read_b32 %[t6], %[t5]\n"                                            \
-    "s_add_u32 %[nm], %[nm], 1\n"                                           \
-    "s_waitcnt lgkmcnt(0)\n"                                                \
-    "v_readfirstlane_b32 %[kl], %[t6]\n"                                    \
     "s_bitcmp1_b32 %[kl], %[c" X "]\n"                                      \
     "s_waitcnt vmcnt(0)\n"                                                  \
     "s_cbranch_scc0 6f\n"                                                   \
     "v_mov_b32 " EX ", " EY "\n"                                            \
     "v_mov_b32 " WX ", " WY "\n"                                            \
-    MMOV(X, Y)                                                              \
+    MMOV(X, Y, EX)                                                          \
     "s_branch 7f\n"                                                         \
     "6:\n"                                                                  \
     "s_or_b32 %[k1], %[c" X "], %[lsh]\n"                                   \
@@ -467,7 +468,6 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "v_add_u32 %[t4], %[ma" X "], %[voff]\n"                                \
     "ds_write_b64 %[t4], " MX "\n"                                          \
     MWB(X)                                                                  \
-    "s_waitcnt lgkmcnt(0)\n"                                                \
     "s_branch " SKIPL "b\n"
 // the coder and the context state; the symbol to output lane m0
 #define FQZ_CODER(X, Y, QSD)                                                \
@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             // the miss path: the backing store, fresh slots (guard, list; the
             // sentinel lanes are set from the context)
             const uint64_t back = reinterpret_cast<uint64_t>(J.back);
-            const uint32_t lsh = U(L << 16);
+            const uint32_t lsh = U(L << 16), sidx = U(S);
             const uint32_t fe = l == 0 ? 0xffffu : (l <= LL ? 1u | ((l - 1u) << 16) : 0u);
             const uint32_t fw = l == 0 || l > LL ? 0u : uint32_t(qt0[l - 1u]) | ((l - 1u) << 24);
             rng = U(rng);
@@ -1051,7 +1051,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                   [ns8] "s"(ns8), [base] "s"(base), [qtab] "s"(qtab), [bmask] "s"(bmask),     \
                   [bloc] "s"(bloc), [c65503] "s"(c65503), [rbend] "s"(rbend), [bswp] "s"(bswp), \
                   [lring] "i"(L_RING), [lbits] "i"(L_BITS), [back] "s"(back), [lsh] "s"(lsh),   \
-                  [fe] "v"(fe), [fw] "v"(fw),                                                  \
+                  [fe] "v"(fe), [fw] "v"(fw), [sidx] "s"(sidx),                                 \
                   [voff] "v"(voff0), [vsent] "v"(vsent), [qlocv] "v"(qlocv),                   \
                   [cbig] "v"(cbig), [c19] "v"(c19), [vme] "v"(vme), [pvv] "v"(pvv),          \
                   [dvv] "v"(dvv), [sqv] "v"(sqv)                                              \
@@ -1073,7 +1073,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                     asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) FQZ_RUN_OPERANDS); \
                 else                                                                                         \
                     asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) FQZ_RUN_OPERANDS);
-                if constexpr (NE == 1) { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1", FQZ_MSENT_NONE, FQZ_MSENT_NONE, FQZ_MSENT_NONE, FQZ_MSENT_RD) }
+                if constexpr (NE == 1) { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1", FQZ_MSENT_NONE, FQZ_MSENT_NONE, FQZ_MSENT_LANE, FQZ_MSENT_NONE1) }
                 else { FQZ_RUN_NE(FQZ_SENT_WB, FQZ_SENT_EXIT, "2", FQZ_MSENT_ST, FQZ_MSENT_LD, FQZ_MSENT_MOV, FQZ_MSENT_WR) }
 #undef FQZ_RUN_NE
 #undef FQZ_RUN_OPERANDS
