@@ -54,6 +54,8 @@ struct SeqDecJob {
 };
 hipError_t launch_seq_models_init(uint32_t *models, size_t nctx, hipStream_t s);
 // one workgroup per job (device array)
-hipError_t launch_seq_dec(const SeqDecJob *d_jobs, int njobs, hipStream_t s);
+// lookahead: k >= 3, the decoder that loads each base's counts three
+// bases ahead (k_seq_dec_la); else the one-step decoder
+hipError_t launch_seq_dec(const SeqDecJob *d_jobs, int njobs, hipStream_t s, bool lookahead);
 
 }  // namespace fqz5

@@ -450,6 +450,275 @@ __global__ __launch_bounds__(64) void k_seq_dec(const SeqDecJob *Js) {
 }
 
 // ---------------------------------------------------------------------------
+// The decoder with a lookahead of SD bases (k >= SD).  The counts a base
+// reads are loaded SD steps before it by the whole wave:
+//  - forward: the contexts SD bases after fw are the 4^SD consecutive models
+//    ((fw << 2 SD) & mask) + x, one dword per lane (SD = 3: 64 lanes);
+//  - reverse (both strands): after SD bases rv becomes (rv >> 2 SD) +
+//    (J << (2k - 2 SD)), J < 4^SD: a gather, one model per lane.
+// A window is issued at the end of the step 1 + SD before the one it serves
+// (after that step's stores), so the last SD steps' stores are not in it:
+// those (context, counts) pairs are kept and applied in time order over the
+// value read from the window.  At a record or run start the SD windows are
+// primed from the first context (window d: 4^d live lanes).  The scalar
+// state (coder, contexts, run models) is uniform; every lane runs it.
+// ---------------------------------------------------------------------------
+constexpr int SD = 3;
+__global__ __launch_bounds__(64) void k_seq_dec_la(const SeqDecJob *Js) {
+    __shared__ FList<256> run[3], lit;
+    const uint32_t l = threadIdx.x;
+    const SeqDecJob J = Js[blockIdx.x];   // one block per workgroup
+    for (int c = 0; c < 3; c++) fl_init(&run[c], 256);
+    fl_init(&lit, 256);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t st[3] = {0x0101u, 0x0101u, 0x0101u};
+    const uint8_t *in = J.in;
+    const uint32_t len = J.in_len, n = J.n, mask = J.mask, top = 2u * J.k - 2u;
+    const uint32_t ia = uint32_t(reinterpret_cast<uintptr_t>(in) & 15u);
+    const auto rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(in - ia), 0,
+                                                       int(len + ia), 0x00020000);
+    const uint32_t iend = len + ia;
+    // whole 16-byte chunks through the scalar cache (s_load: lgkmcnt, so the
+    // model windows' vmcnt waits do not see them); the chunk with the end in
+    // it by bounded byte loads
+    const __attribute__((address_space(4))) uint32_t *cin =
+        (const __attribute__((address_space(4))) uint32_t *)(uintptr_t(in - ia));
+    auto ld16 = [&](uint32_t off) {
+        if (off + 16u <= iend) {
+            const uint32_t w = off >> 2;
+            return make_uint4(cin[w], cin[w + 1], cin[w + 2], cin[w + 3]);
+        }
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint32_t i = 0; i < 16u; i++)
+            w[i >> 2] |= uint32_t(__builtin_amdgcn_raw_buffer_load_b8(rin, off + i, 0, 0)) << (8u * (i & 3u));
+        return make_uint4(__builtin_amdgcn_readfirstlane(w[0]), __builtin_amdgcn_readfirstlane(w[1]),
+                          __builtin_amdgcn_readfirstlane(w[2]), __builtin_amdgcn_readfirstlane(w[3]));
+    };
+    uint32_t cb = 0;
+    uint4 cur = ld16(0), nxt = ld16(16);
+    uint32_t ip = 0;
+    auto next_byte = [&]() -> uint32_t {
+        const uint32_t o = ip++ + ia;
+        if (o - cb >= 16u) {
+            cb += 16u;
+            cur = nxt;
+            nxt = ld16(cb + 16u);
+        }
+        const uint32_t r = o - cb;
+        const uint32_t w = r < 8u ? (r < 4u ? cur.x : cur.y) : (r < 12u ? cur.z : cur.w);
+        return (w >> (8u * (r & 3u))) & 255u;
+    };
+    uint32_t code = 0, rng = 0xFFFFFFFFu;
+    bool bad = false;
+    if (len >= 5) {
+        for (int i = 0; i < 5; i++) code = (code << 8) | next_byte();
+    } else {
+        bad = n > 0;
+    }
+    auto target = [&](uint32_t tot) -> uint32_t {
+        if (!tot || rng < tot) return 0u;
+        rng /= tot;
+        return code / rng;
+    };
+    uint64_t bb = 0;
+    uint32_t bn = 0;
+    auto fill = [&]() {
+        while (bn <= 56u) {
+            bb |= uint64_t(next_byte()) << (56u - bn);
+            bn += 8u;
+        }
+    };
+    auto used = [&]() { return ip - (bn >> 3); };
+    auto take = [&](uint32_t cum, uint32_t f) {
+        code -= cum * rng;
+        rng *= f;
+        while (rng < (1u << 24)) {
+            if (used() >= len) {
+                bad = true;
+                return;
+            }
+            if (!bn) fill();
+            code = (code << 8) | uint32_t(bb >> 56);
+            bb <<= 8;
+            bn -= 8u;
+            rng <<= 8;
+        }
+    };
+    auto get_fl = [&](FList<256> *m) -> uint32_t {
+        const uint32_t t = target(m->total);
+        if (t > FL_MAX) {
+            bad = true;
+            return 0u;
+        }
+        uint32_t acc = 0;
+        int k = 1;
+        while (acc + m->fr[k] <= t) acc += m->fr[k++];
+        if (k > 256) {
+            bad = true;
+            return 0u;
+        }
+        take(acc, m->fr[k]);
+        const uint32_t s = m->sy[k];
+        __builtin_amdgcn_wave_barrier();
+        fl_bump(m, k);
+        __builtin_amdgcn_wave_barrier();
+        return s;
+    };
+    auto get_st = [&](uint32_t c) -> uint32_t {
+        const uint32_t F = st[c], f0 = F & 255u, tot = f0 + (F >> 8);
+        const uint32_t bit = target(tot) >= f0;
+        take(bit ? f0 : 0u, bit ? F >> 8 : f0);
+        st[c] = sm4_bump(F, bit, tot);
+        return bit;
+    };
+
+    uint32_t *M = J.models;
+    // models and output through buffer ops (vmcnt only, no flat counters)
+    const auto rM = __builtin_amdgcn_make_buffer_rsrc(M, 0, int((mask + 1u) * 4u), 0x00020000);
+    const auto rO = __builtin_amdgcn_make_buffer_rsrc(J.out, 0, int(n), 0x00020000);
+    auto ldM = [&](uint32_t ctx) { return __builtin_amdgcn_raw_buffer_load_b32(rM, ctx * 4u, 0, 0); };
+    auto stM = [&](uint32_t ctx, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, rM, ctx * 4u, 0, 0); };
+    const bool both = J.both != 0;
+    const uint32_t rsh = 2u * J.k - 2u * SD;   // the reverse window's lane shift, steady state
+    // the window ring (lane values) and, per slot, its base context and the
+    // reverse window's base and shift
+    uint32_t W[SD], R[SD], wb[SD], rb[SD], rs[SD];
+    // the stores the windows may miss: per step slot, forward and reverse
+    uint32_t hf[SD], hfv[SD], hr[SD], hrv[SD];
+    uint32_t fw = seed_fw(mask), rv = seed_rv(J.k, mask);
+    uint32_t si = 0, state = 0, p = 0, idle = 0;
+    uint32_t F = 0;
+    uint32_t next_seg = J.nseg > 1 ? J.seg[1] : 0xFFFFFFFFu;
+    // prime the windows from fw / rv for the next SD steps; F = counts of fw
+    auto prime = [&]() {
+        F = __builtin_amdgcn_readfirstlane(ldM(fw));
+#pragma unroll
+        for (int d = 1; d <= SD; d++) {
+            const int slot = d % SD;
+            const uint32_t b0 = (fw << (2 * d)) & mask;
+            W[slot] = ldM((b0 + l) & mask);
+            wb[slot] = b0;
+            if (both) {
+                const uint32_t r0 = rv >> (2 * d), sh = 2u * J.k - 2u * uint32_t(d);
+                R[slot] = ldM((r0 + (l << sh)) & mask);
+                rb[slot] = r0;
+                rs[slot] = sh;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < SD; i++) hf[i] = hr[i] = 0xFFFFFFFFu;
+    };
+    // one base of a record's run, ring position U (= step % SD)
+#define SEQ_LA_STEP(U)                                                                          \
+    {                                                                                           \
+        constexpr int u = (U), n1 = ((U) + 1) % SD;                                             \
+        if (bn < 8u) fill();                                                                    \
+        const uint32_t tot = sm4_total(F);                                                      \
+        const uint32_t q = quot(rng, recip(tot));                                               \
+        const uint32_t c0 = F & 255u, c1 = c0 + ((F >> 8) & 255u), c2 = c1 + ((F >> 16) & 255u); \
+        const uint32_t b = uint32_t(c0 * q <= code) + uint32_t(c1 * q <= code) +                \
+                           uint32_t(c2 * q <= code);                                            \
+        code -= sm4_cum(F, b) * q;                                                              \
+        rng = q * ((F >> (8u * b)) & 255u);                                                     \
+        const bool sh = rng < (1u << 24);                                                       \
+        code = sh ? (code << 8) | uint32_t(bb >> 56) : code;                                    \
+        rng = sh ? rng << 8 : rng;                                                              \
+        bb = sh ? bb << 8 : bb;                                                                 \
+        bn -= sh ? 8u : 0u;                                                                     \
+        const uint32_t Fu = sm4_bump(F, b, tot);                                                \
+        stM(fw, Fu);                                                                            \
+        __builtin_amdgcn_raw_buffer_store_b8(uint8_t(((0x54474341u >> (8u * b)) & 255u) | (state << 5)), rO, p, 0, 0); \
+        hf[u] = fw;                                                                             \
+        hfv[u] = Fu;                                                                            \
+        const uint32_t fn = ((fw << 2) + b) & mask;                                             \
+        uint32_t Fn = __builtin_amdgcn_readlane(W[n1], (fn - wb[n1]) & 63u);                    \
+        uint32_t G = 0, rn = 0;                                                                 \
+        if (both) {                                                                             \
+            const uint32_t b2 = rv & 3u;                                                        \
+            rn = (rv >> 2) + ((3u - b) << top);                                                 \
+            G = __builtin_amdgcn_readlane(R[n1], ((rn - rb[n1]) >> rs[n1]) & 63u);              \
+            /* the stores since the window, oldest first */                                    \
+            _Pragma("unroll") for (int i = 1; i <= SD; i++) {                                   \
+                const int h = (u + i) % SD;                                                     \
+                if (rn == hf[h]) G = hfv[h];                                                    \
+                if (i < SD && rn == hr[h]) G = hrv[h];                                          \
+            }                                                                                   \
+            const uint32_t Gu = sm4_bump(G, b2, sm4_total(G));                                  \
+            stM(rn, Gu);                                                                        \
+            hr[u] = rn;                                                                         \
+            hrv[u] = Gu;                                                                        \
+        }                                                                                       \
+        _Pragma("unroll") for (int i = 1; i <= SD; i++) {                                       \
+            const int h = (u + i) % SD;                                                         \
+            if (fn == hf[h]) Fn = hfv[h];                                                       \
+            if (both && fn == hr[h]) Fn = hrv[h];                                               \
+        }                                                                                       \
+        /* the window SD steps after the next base */                                          \
+        const uint32_t nb0 = (fn << (2 * SD)) & mask;                                           \
+        W[n1] = ldM((nb0 + l) & mask);                                                          \
+        wb[n1] = nb0;                                                                           \
+        if (both) {                                                                             \
+            const uint32_t r0 = rn >> (2 * SD);                                                 \
+            R[n1] = ldM((r0 + (l << rsh)) & mask);                                              \
+            rb[n1] = r0;                                                                        \
+            rs[n1] = rsh;                                                                       \
+            rv = rn;                                                                            \
+        }                                                                                       \
+        fw = fn;                                                                                \
+        F = Fn;                                                                                 \
+        p++;                                                                                    \
+    }
+    while (p < n && !bad) {
+        uint32_t runlen = 0, d;
+        do {
+            d = get_fl(&run[state]);
+            runlen += d;
+        } while (d == 255u && !bad && runlen <= n);
+        if (bad) break;
+        if (runlen > n - p) runlen = n - p;
+        if (runlen == 0 && ++idle > 2) {
+            bad = true;
+            break;
+        }
+        const uint32_t end = p + runlen;
+        bool primed = false;
+        while (p < end && !bad) {
+            if (p == next_seg) {                           // a record starts
+                si++;
+                next_seg = si + 1 < J.nseg ? J.seg[si + 1] : 0xFFFFFFFFu;
+                fw = seed_fw(mask);
+                rv = seed_rv(J.k, mask);
+                primed = false;
+            }
+            const uint32_t stop = end < next_seg ? end : next_seg;
+            if (state == 2u) {
+                for (; p < stop && !bad; p++) __builtin_amdgcn_raw_buffer_store_b8(uint8_t(get_fl(&lit)), rO, p, 0, 0);
+                continue;
+            }
+            if (!primed) {
+                prime();
+                primed = true;
+            }
+            // the ring position of p: steps since the priming, mod SD
+            while (p + SD <= stop) {
+                SEQ_LA_STEP(0)
+                SEQ_LA_STEP(1)
+                SEQ_LA_STEP(2)
+            }
+            if (p < stop) SEQ_LA_STEP(0)
+            if (p < stop) SEQ_LA_STEP(1)
+            // a segment end inside the ring: the next piece starts primed anew
+            primed = false;
+        }
+        if (p >= n || bad) break;
+        state = switch_to(state, get_st(state));
+    }
+#undef SEQ_LA_STEP
+    if (used() > len) bad = true;
+    if (l == 0) *J.status = bad ? -1 : 0;
+}
+
+// ---------------------------------------------------------------------------
 static dim3 grid_of(uint64_t n) { return dim3(unsigned((n + 255) / 256)); }
 
 hipError_t launch_seq_heads(const SeqJob &j, hipStream_t s) {
@@ -484,8 +753,11 @@ hipError_t launch_seq_models_init(uint32_t *models, size_t nctx, hipStream_t s) 
     return hipGetLastError();
 }
 
-hipError_t launch_seq_dec(const SeqDecJob *d_jobs, int njobs, hipStream_t s) {
-    if (njobs) hipLaunchKernelGGL(k_seq_dec, dim3(njobs), dim3(64), 0, s, d_jobs);
+hipError_t launch_seq_dec(const SeqDecJob *d_jobs, int njobs, hipStream_t s, bool lookahead) {
+    if (njobs) {
+        if (lookahead) hipLaunchKernelGGL(k_seq_dec_la, dim3(njobs), dim3(64), 0, s, d_jobs);
+        else hipLaunchKernelGGL(k_seq_dec, dim3(njobs), dim3(64), 0, s, d_jobs);
+    }
     return hipGetLastError();
 }
 

@@ -220,7 +220,11 @@ void seq_decode_batch(GpuCtx &g, std::vector<SeqDecReq> &reqs) {
     }
     if (js.empty()) return;
     EventPair ev(prof_on(), g.stream);
-    FQZ5_HIP(launch_seq_dec(g.upload(js), int(js.size()), g.stream));
+    // k >= 3: the lookahead decoder; the rest (k = 1, 2) the one-step one
+    std::vector<SeqDecJob> la, one;
+    for (const SeqDecJob &J : js) (J.k >= 3 ? la : one).push_back(J);
+    if (!la.empty()) FQZ5_HIP(launch_seq_dec(g.upload(la), int(la.size()), g.stream, true));
+    if (!one.empty()) FQZ5_HIP(launch_seq_dec(g.upload(one), int(one.size()), g.stream, false));
     ev.stop(g.stream);
     std::vector<int32_t> st(js.size(), -1);
     for (size_t k = 0; k < js.size(); k++) g.download(&st[k], js[k].status, 1);
