@@ -843,8 +843,9 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
         finally:
             for st in streams:
                 if isinstance(st, __import__("gzip").GzipFile):
+                    raw = st.fileobj          # (close() drops the reference)
                     st.close()
-                    st.fileobj.close()
+                    raw.close()
                 else:
                     st.close()
     if single:
