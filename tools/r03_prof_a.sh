@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round profile on the GPU box: the driver's bench command, the rocprofv3
+# kernel-trace summaries of the same workloads (configs[1] -3 and configs[2]
+# -5), and the HBM traffic PMC passes of both workloads (FETCH_SIZE and
+# WRITE_SIZE each in a pass of its own; MI355X_MICROARCH.md HBM section).
+# Usage: tools/profile.sh <tag>   (outputs under gpurun_out/prof_<tag>)
+set -euo pipefail
+TAG=${1:-r03}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+B3="--no-cpu --no-level5 --no-crc --no-dropin"
+B5="--no-cpu --no-crc --no-dropin --level 5 --kind novaseq --gb 4"
+B5I="--no-cpu --no-crc --no-dropin --no-level5 --level 5 --kind illumina --gb 1"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt3 -o kt -- \
+    python3 bench.py $B3 --steps 5 --warmup 1 > $OUT/kt3.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt5 -o kt -- \
+    python3 bench.py $B5 --steps 5 --warmup 1 > $OUT/kt5.log 2>&1
+timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- \
+    python3 bench.py $B3 --steps 1 --warmup 0 > $OUT/fetch.log 2>&1
+timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- \
+    python3 bench.py $B3 --steps 1 --warmup 0 > $OUT/write.log 2>&1
+python3 tools/pmc_summary.py $OUT $OUT/pmc.json > /dev/null
+timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/l5/fetch -o fetch -- \
+    python3 bench.py $B5 --steps 1 --warmup 0 > $OUT/fetch5.log 2>&1
+timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/l5/write -o write -- \
+    python3 bench.py $B5 --steps 1 --warmup 0 > $OUT/write5.log 2>&1
+python3 tools/pmc_summary.py $OUT/l5 $OUT/pmc_l5.json > /dev/null
+echo done
