@@ -112,7 +112,7 @@ def pmc_traffic(kernel: str, tag: str = ""):
         return None, None
     ks = json.load(open(files[-1]))["kernels"]
     for k, v in ks.items():
-        if f"::{kernel}(" in k:
+        if f"::{kernel}(" in k or f"::{kernel}<" in k:
             # the step's main launch of the kernel (the largest dispatch)
             b = v.get("hbm_bytes_max_dispatch", v["hbm_bytes_per_dispatch"])
             return int(b), os.path.relpath(files[-1], ROOT)
