@@ -396,9 +396,9 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_branch " RETL "b\n"
 // A miss (the set holds another context, ev): ev's model, read again from
 // the set (the read that found it may predate the last write-back of the
-// same set), goes back to HBM (J.back, work-group scope: sc0; the store is
-// private to this wave, so its lines stay in the XCD's L2, where device
-// scope, sc1, would send every fetch past it) and into the LDS bitmap of evicted
+// same set), goes back to HBM (J.back, plain stores and loads: the store is
+// private to this wave, so its lines may stay in the caches; device scope,
+// sc1, sent every fetch past the XCD's L2) and into the LDS bitmap of evicted
 // contexts; the current context's comes from HBM when the bitmap has it,
 // else fresh (fe / fw; the sentinel lanes get context | L << 16); then the
 // set is rewritten and the symbol starts over at SKIPL.
@@ -406,10 +406,10 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 #define FQZ_MSENT_NONE1(X) ""
 #define FQZ_MSENT_ST(X, Y)                                                  \
     "v_mad_u32_u24 %[t5], %[x], %[vme], %[vsent]\n"                         \
-    "global_store_dword %[t5], %[tv" X "], %[back] sc0\n"
+    "global_store_dword %[t5], %[tv" X "], %[back]\n"
 #define FQZ_MSENT_LD(X, Y)                                                  \
     "v_mad_u32_u24 %[t5], %[c" X "], %[vme], %[vsent]\n"                    \
-    "global_load_dword %[tv" Y "], %[t5], %[back] sc0\n"
+    "global_load_dword %[tv" Y "], %[t5], %[back]\n"
 #define FQZ_MSENT_MOV(X, Y, EX) "v_mov_b32 %[tv" X "], %[tv" Y "]\n"
 #define FQZ_MSENT_LANE(X, Y, EX)                                            \
     "v_readlane_b32 %[x], " EX ", %[sidx]\n"                                \
@@ -419,12 +419,13 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "ds_write_b32 %[t5], %[tv" X "]\n"
 // the fetch of the current context's model from HBM is issued first (into
 // the other register pair, free during a miss), then the set and the
-// bitmap word are read together; the rest overlaps the fetch
-#define FQZ_MISS(X, Y, MX, EX, WX, MY, EY, WY, MISSL, SKIPL, MST, MLD, MMOV, MWB) \
+// bitmap word are read together; the rest overlaps the fetch.  The wait is
+// for the fetch only (MVW: the write-back stores issued after it)
+#define FQZ_MISS(X, Y, MX, EX, WX, MY, EY, WY, MISSL, SKIPL, MST, MLD, MMOV, MWB, MVW) \
     MISSL ":\n"                                                             \
     "s_waitcnt lgkmcnt(0)\n"                                                \
     "v_mad_u32_u24 %[t4], %[c" X "], %[vme], %[voff]\n"                     \
-    "global_load_dwordx2 " MY ", %[t4], %[back] sc0\n"                      \
+    "global_load_dwordx2 " MY ", %[t4], %[back]\n"                      \
     MLD(X, Y)                                                               \
     "s_lshr_b32 %[k1], %[c" X "], 3\n"                                      \
     "s_and_b32 %[k1], %[k1], 0x1ffc\n"                                      \
@@ -441,7 +442,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "v_readfirstlane_b32 %[kl], %[t6]\n"                                    \
     "s_and_b32 %[x], %[x], 0xffff\n"                                        \
     "v_mad_u32_u24 %[t4], %[x], %[vme], %[voff]\n"                          \
-    "global_store_dwordx2 %[t4], " MX ", %[back] sc0\n"                     \
+    "global_store_dwordx2 %[t4], " MX ", %[back]\n"                     \
     MST(X, Y)                                                               \
     "s_lshr_b32 %[k1], %[x], 3\n"                                           \
     "s_and_b32 %[k1], %[k1], 0x1ffc\n"                                      \
@@ -451,7 +452,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "v_mov_b32 %[t6], %[z]\n"                                               \
     "ds_or_b32 %[t5], %[t6]\n"                                              \
     "s_bitcmp1_b32 %[kl], %[c" X "]\n"                                      \
-    "s_waitcnt vmcnt(0)\n"                                                  \
+    "s_waitcnt vmcnt(" MVW ")\n"                                            \
     "s_cbranch_scc0 6f\n"                                                   \
     "v_mov_b32 " EX ", " EY "\n"                                            \
     "v_mov_b32 " WX ", " WY "\n"                                            \
@@ -518,7 +519,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 // same-context paths, 12/22 the slow exits; 30 exits in the A state, 31 in
 // the B state; 41-48 out-of-line bubble steps and renormalisations, 51-58
 // their way back
-#define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) \
+#define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW) \
     "s_mov_b32 %[m0s], m0\n"                                                \
     "s_mov_b32 m0, %[done]\n"                                               \
     "s_mov_b32 %[flags], 0\n"                                               \
@@ -547,8 +548,8 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     FQZ_RENORM_OUT("46", "56", "30f")                                       \
     FQZ_SWAP("v4", "v5", "47", "57")                                        \
     FQZ_RENORM_OUT("48", "58", "31f")                                       \
-    FQZ_MISS("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", "v4", "v5", "60", "13", MST, MLD, MMOV, MWB) \
-    FQZ_MISS("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", "v2", "v3", "61", "23", MST, MLD, MMOV, MWB) \
+    FQZ_MISS("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", "v4", "v5", "60", "13", MST, MLD, MMOV, MWB, MVW) \
+    FQZ_MISS("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", "v2", "v3", "61", "23", MST, MLD, MMOV, MWB, MVW) \
     "12:\n"                                                                 \
     "s_cmp_lg_u64 %[TG], 0\n"                                               \
     "s_cbranch_scc1 60b\n"                                                  \
@@ -745,13 +746,13 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         uint32_t *bits = reinterpret_cast<uint32_t *>(lds + L_BITS);
         uint32_t *dst = reinterpret_cast<uint32_t *>(J.back + size_t(tag) * ME);
         for (uint32_t o = l; o < ME / 4; o += 64)
-            __hip_atomic_store(dst + o, m32[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(dst + o, m32[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         if (l == 0) bits[tag >> 5] |= 1u << (tag & 31);
         __builtin_amdgcn_wave_barrier();
         if ((U(bits[ctx >> 5]) >> (ctx & 31)) & 1u) {
             const uint32_t *src = reinterpret_cast<const uint32_t *>(J.back + size_t(ctx) * ME);
             for (uint32_t o = l; o < ME / 4; o += 64)
-                m32[o] = __hip_atomic_load(src + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                m32[o] = __hip_atomic_load(src + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         } else {
             fresh_slots(maddr);
             if (l == 0) *reinterpret_cast<uint2 *>(lds + maddr + sent) = make_uint2(ctx | (L << 16), 0u);
@@ -787,13 +788,13 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         fs[0] = s0;
         if constexpr (NE == 2) {
             const uint32_t sv = model_sentinel(), dw = 64u + l;
-            const bool hi = (__hip_atomic_load(J.hi_bits + (ctx >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
+            const bool hi = (__hip_atomic_load(J.hi_bits + (ctx >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >>
                              (ctx & 31)) & 1u;
             uint32_t f = 0, sy = 0;
             if (dw <= L) {
                 if (hi) {
                     const uint32_t x = __hip_atomic_load(J.back_hi + size_t(ctx) * 64u + l, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                                                         __HIP_MEMORY_SCOPE_WAVEFRONT);
                     f = x & 0xffffu;
                     sy = x >> 16;
                 } else {
@@ -821,11 +822,11 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             if (l == 0) *reinterpret_cast<uint2 *>(lds + maddr + sent) = make_uint2(sv, 0u);
             if (dw <= L)
                 __hip_atomic_store(J.back_hi + size_t(ctx) * 64u + l, (fv[1] & 0xffffu) | ((fs[1] >> 24) << 16),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             if (l == 0) {
                 uint32_t *hb = J.hi_bits + (ctx >> 5);
-                __hip_atomic_store(hb, __hip_atomic_load(hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) |
-                                       (1u << (ctx & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(hb, __hip_atomic_load(hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) |
+                                       (1u << (ctx & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1064,17 +1065,17 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                     pr[5] += 1;
                 }
 #endif
-#define FQZ_RUN_NE(SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB)                                                                           \
+#define FQZ_RUN_NE(SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW)                                                                           \
                 if constexpr (QW && SEQ)                                                                     \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW) FQZ_RUN_OPERANDS); \
                 else if constexpr (QW)                                                                       \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW) FQZ_RUN_OPERANDS); \
                 else if constexpr (SEQ)                                                                      \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW) FQZ_RUN_OPERANDS); \
                 else                                                                                         \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB) FQZ_RUN_OPERANDS);
-                if constexpr (NE == 1) { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1", FQZ_MSENT_NONE, FQZ_MSENT_NONE, FQZ_MSENT_LANE, FQZ_MSENT_NONE1) }
-                else { FQZ_RUN_NE(FQZ_SENT_WB, FQZ_SENT_EXIT, "2", FQZ_MSENT_ST, FQZ_MSENT_LD, FQZ_MSENT_MOV, FQZ_MSENT_WR) }
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW) FQZ_RUN_OPERANDS);
+                if constexpr (NE == 1) { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1", FQZ_MSENT_NONE, FQZ_MSENT_NONE, FQZ_MSENT_LANE, FQZ_MSENT_NONE1, "1") }
+                else { FQZ_RUN_NE(FQZ_SENT_WB, FQZ_SENT_EXIT, "2", FQZ_MSENT_ST, FQZ_MSENT_LD, FQZ_MSENT_MOV, FQZ_MSENT_WR, "2") }
 #undef FQZ_RUN_NE
 #undef FQZ_RUN_OPERANDS
 #ifdef FQZ5_DEC_PROBE
