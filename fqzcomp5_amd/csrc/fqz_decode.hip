@@ -223,6 +223,9 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 // holding slot j (e = freq | cum << 16 in the low register, w = qtab value |
 // symbol << 24 in the high one), with the sentinel (e = context | total <<
 // 16) broadcast to every lane in tv.  Per symbol:
+//   miss    the sentinel names another context (the set holds another
+//           context's model): the miss path (below) brings this one in and
+//           the symbol starts over, before any work that needs the model
 //   u       the context terms of this position and delta (pvv / dvv lanes)
 //   q       floor(range / total) from RN(1/total) (rcp + one Newton step)
 //   p_j     cum_j * q;  G = lanes with p_j > code;  kl = first of G - 1
@@ -231,8 +234,8 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 //           again (SM), and whether the bump would bubble slot j over j-1
 //   the next model's read is issued from lane kl's set as soon as kl is
 //   known, into the other register pair; the checks (a total that the +16
-//   would take past FL_MAX, the sentinel's context not the current one,
-//   t >= total) leave with flags 2 before any state changes
+//   would take past FL_MAX, t >= total) leave with flags 2 before any
+//   state changes
 //   bump    +16 to lane kl's frequency and every later cum; one bubble step
 //           by DPP lane shifts when it swaps; the model is written back
 //   coder   c_range_coder.h RC_Decode: code -= cum q, range = freq q,
@@ -271,19 +274,20 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 // when the context repeats.  The wait is for the model read (the write-back
 // issued after it may still be in flight); an iteration of the same context
 // enters at SKIPL, past it.  WCNT: the writes issued after the read.
-#define FQZ_TOP(X, Y, EX, WX, QT1, QT2, SEQCTX, WCNT, SKIPL, SAMEL)         \
+#define FQZ_TOP(X, Y, EX, WX, QT1, QT2, SEQCTX, WCNT, SKIPL, SAMEL, MISSL)  \
     "s_waitcnt lgkmcnt(" WCNT ")\n"                                         \
     SKIPL ":\n"                                                             \
+    "v_cmp_ne_u16_e32 vcc, %[c" X "], %[tv" X "]\n"                         \
     "v_readlane_b32 %[u], %[pvv], m0\n"                                     \
     "v_lshrrev_b32 %[t6], 16, %[tv" X "]\n"                                 \
     "v_readlane_b32 %[x], %[dvv], %[dd]\n"                                  \
     "v_cvt_f64_u32 %[d1], %[t6]\n"                                          \
     QT1(WX)                                                                 \
     "v_cvt_f64_u32 %[d0], %[rng]\n"                                         \
+    "s_cbranch_vccnz " MISSL "\n"                                           \
     "v_rcp_f64 %[d2], %[d1]\n"                                              \
     "s_add_u32 %[u], %[u], %[x]\n"                                          \
     SEQCTX(X, Y)                                                            \
-    "v_cmp_ne_u16_e64 %[TG], %[c" X "], %[tv" X "]\n"                       \
     "v_lshrrev_b32 %[t4], 16, " EX "\n"                                     \
     "v_fma_f64 %[d1], -%[d1], %[d2], 1.0\n"                                 \
     QT2(X, WX)                                                              \
@@ -310,9 +314,8 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "v_readlane_b32 %[ma" Y "], %[t2], %[kl]\n"                             \
     "s_and_b64 %[SM], %[SM], %[E]\n"                                        \
     "s_cbranch_scc1 " SAMEL "\n"
-// the checks; SLOWL leaves with the state unchanged (TG kept: a miss)
+// the checks; SLOWL leaves with the state unchanged
 #define FQZ_CHECK(SLOWL)                                                    \
-    "s_or_b64 %[HV], %[HV], %[TG]\n"                                        \
     "s_andn2_b64 %[E], %[E], %[HV]\n"                                       \
     "s_cbranch_scc0 " SLOWL "\n"
 // the coded slot's update (fl_bump): +16 to lane kl's frequency (E) and to
@@ -407,26 +410,36 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 #define FQZ_MSENT_ST(X, Y)                                                  \
     "v_mad_u32_u24 %[t5], %[x], %[vme], %[vsent]\n"                         \
     "global_store_dword %[t5], %[tv" X "], %[back]\n"
-#define FQZ_MSENT_LD(X, Y)                                                  \
-    "v_mad_u32_u24 %[t5], %[c" X "], %[vme], %[vsent]\n"                    \
-    "global_load_dword %[tv" Y "], %[t5], %[back]\n"
-#define FQZ_MSENT_MOV(X, Y, EX) "v_mov_b32 %[tv" X "], %[tv" Y "]\n"
+// a context's model from HBM into v[6:7] (and tvp: PFT)
+#define FQZ_FETCH(C, PFT)                                                   \
+    "v_mad_u32_u24 %[t4], %[c" C "], %[vme], %[voff]\n"                     \
+    "global_load_dwordx2 v[6:7], %[t4], %[back]\n"                          \
+    PFT(C)
+#define FQZ_IF_0(a, b) b
+#define FQZ_IF_1(a, b) a
+#define FQZ_IF(P, a, b) FQZ_IF_##P(a, b)
+#define FQZ_PF_NONE(Y) ""
+#define FQZ_PF_SENT(Y)                                                      \
+    "v_mad_u32_u24 %[t5], %[c" Y "], %[vme], %[vsent]\n"                    \
+    "global_load_dword %[tvp], %[t5], %[back]\n"
+#define FQZ_MSENT_MOV(X, Y, EX) "v_mov_b32 %[tv" X "], %[tvp]\n"
 #define FQZ_MSENT_LANE(X, Y, EX)                                            \
     "v_readlane_b32 %[x], " EX ", %[sidx]\n"                                \
     "v_mov_b32 %[tv" X "], %[x]\n"
 #define FQZ_MSENT_WR(X)                                                     \
     "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
     "ds_write_b32 %[t5], %[tv" X "]\n"
-// the fetch of the current context's model from HBM is issued first (into
-// the other register pair, free during a miss), then the set and the
-// bitmap word are read together; the rest overlaps the fetch.  The wait is
-// for the fetch only (MVW: the write-back stores issued after it)
-#define FQZ_MISS(X, Y, MX, EX, WX, MY, EY, WY, MISSL, SKIPL, MST, MLD, MMOV, MWB, MVW) \
+// With PF = 1 (a run that misses often) the model of every context the run
+// switches to (and of the one it starts in, which the caller may not have
+// brought in) is fetched from HBM at the switch, speculatively, so that a
+// miss finds it on its way; with PF = 0 the miss fetches it first thing.
+// The miss reads the set and the bitmap word together and writes the
+// resident model back; the wait is for the fetch only (MVW: the write-back
+// stores issued after it).
+#define FQZ_MISS(X, Y, MX, EX, WX, MY, EY, WY, MISSL, SKIPL, MST, PF, PFT, MMOV, MWB, MVW) \
     MISSL ":\n"                                                             \
     "s_waitcnt lgkmcnt(0)\n"                                                \
-    "v_mad_u32_u24 %[t4], %[c" X "], %[vme], %[voff]\n"                     \
-    "global_load_dwordx2 " MY ", %[t4], %[back]\n"                      \
-    MLD(X, Y)                                                               \
+    FQZ_IF(PF, "", FQZ_FETCH(X, PFT))                                       \
     "s_lshr_b32 %[k1], %[c" X "], 3\n"                                      \
     "s_and_b32 %[k1], %[k1], 0x1ffc\n"                                      \
     "s_add_u32 %[k1], %[k1], %[lbits]\n"                                    \
@@ -454,8 +467,8 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "s_bitcmp1_b32 %[kl], %[c" X "]\n"                                      \
     "s_waitcnt vmcnt(" MVW ")\n"                                            \
     "s_cbranch_scc0 6f\n"                                                   \
-    "v_mov_b32 " EX ", " EY "\n"                                            \
-    "v_mov_b32 " WX ", " WY "\n"                                            \
+    "v_mov_b32 " EX ", v6\n"                                                \
+    "v_mov_b32 " WX ", v7\n"                                                \
     MMOV(X, Y, EX)                                                          \
     "s_branch 7f\n"                                                         \
     "6:\n"                                                                  \
@@ -491,7 +504,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "v_add_u32 %[t5], %[ma" X "], %[vsent]\n"                               \
     "ds_write_b32 %[t5], %[tv" X "]\n"
 // context change: the next model into (MY, tv Y), this one written back
-#define FQZ_SWITCH(X, Y, MX, EX, WX, MY, SENTWB, SLOWL, SWL, RNL, R1, R2)   \
+#define FQZ_SWITCH(X, Y, MX, EX, WX, MY, SENTWB, PF, PFT, SLOWL, SWL, RNL, R1, R2) \
     "v_add_u32 %[t4], %[ma" Y "], %[voff]\n"                                \
     "v_add_u32 %[t5], %[ma" Y "], %[vsent]\n"                               \
     "ds_read_b64 " MY ", %[t4]\n"                                           \
@@ -499,6 +512,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     FQZ_CHECK(SLOWL)                                                        \
     "v_readlane_b32 %[c" Y "], %[t1], %[kl]\n"                              \
     FQZ_TAKE(Y, WX)                                                         \
+    FQZ_IF(PF, FQZ_FETCH(Y, PFT), "")                                       \
     FQZ_BUMP(EX, SWL, R1)                                                   \
     "v_add_u32 %[t2], %[ma" X "], %[voff]\n"                                \
     "ds_write_b64 %[t2], " MX "\n"                                          \
@@ -519,17 +533,18 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
 // same-context paths, 12/22 the slow exits; 30 exits in the A state, 31 in
 // the B state; 41-48 out-of-line bubble steps and renormalisations, 51-58
 // their way back
-#define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW) \
+#define FQZ_RUN_ASM(QT1, QT2, SEQCTX, SEQSAME, SENTWB, SENTEX, WCNT, MST, PF, PFT, MMOV, MWB, MVW) \
     "s_mov_b32 %[m0s], m0\n"                                                \
     "s_mov_b32 m0, %[done]\n"                                               \
     "s_mov_b32 %[flags], 0\n"                                               \
+    FQZ_IF(PF, FQZ_FETCH("A", PFT), "")                                     \
     "10:\n"                                                                 \
-    FQZ_TOP("A", "B", "v2", "v3", QT1, QT2, SEQCTX, WCNT, "13", "11f")      \
-    FQZ_SWITCH("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", SENTWB, "12f", "41", "42", "51", "52") \
+    FQZ_TOP("A", "B", "v2", "v3", QT1, QT2, SEQCTX, WCNT, "13", "11f", "60f") \
+    FQZ_SWITCH("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", SENTWB, PF, PFT, "12f", "41", "42", "51", "52") \
     "s_cbranch_scc0 31f\n"                                                  \
     "20:\n"                                                                 \
-    FQZ_TOP("B", "A", "v4", "v5", QT1, QT2, SEQCTX, WCNT, "23", "21f")      \
-    FQZ_SWITCH("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", SENTWB, "22f", "43", "44", "53", "54") \
+    FQZ_TOP("B", "A", "v4", "v5", QT1, QT2, SEQCTX, WCNT, "23", "21f", "61f") \
+    FQZ_SWITCH("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", SENTWB, PF, PFT, "22f", "43", "44", "53", "54") \
     "s_cbranch_scc1 10b\n"                                                  \
     "s_branch 30f\n"                                                        \
     "11:\n"                                                                 \
@@ -548,16 +563,12 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     FQZ_RENORM_OUT("46", "56", "30f")                                       \
     FQZ_SWAP("v4", "v5", "47", "57")                                        \
     FQZ_RENORM_OUT("48", "58", "31f")                                       \
-    FQZ_MISS("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", "v4", "v5", "60", "13", MST, MLD, MMOV, MWB, MVW) \
-    FQZ_MISS("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", "v2", "v3", "61", "23", MST, MLD, MMOV, MWB, MVW) \
+    FQZ_MISS("A", "B", "v[2:3]", "v2", "v3", "v[4:5]", "v4", "v5", "60", "13", MST, PF, PFT, MMOV, MWB, MVW) \
+    FQZ_MISS("B", "A", "v[4:5]", "v4", "v5", "v[2:3]", "v2", "v3", "61", "23", MST, PF, PFT, MMOV, MWB, MVW) \
     "12:\n"                                                                 \
-    "s_cmp_lg_u64 %[TG], 0\n"                                               \
-    "s_cbranch_scc1 60b\n"                                                  \
     "s_mov_b32 %[flags], 2\n"                                               \
     "s_branch 30f\n"                                                        \
     "22:\n"                                                                 \
-    "s_cmp_lg_u64 %[TG], 0\n"                                               \
-    "s_cbranch_scc1 61b\n"                                                  \
     "s_mov_b32 %[flags], 2\n"                                               \
     "31:\n"                                                                 \
     "s_waitcnt lgkmcnt(0)\n"                                                \
@@ -579,6 +590,7 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     SENTEX("A")                                                             \
     "s_waitcnt lgkmcnt(0)\n"                                                \
     "5:\n"                                                                  \
+    "s_waitcnt vmcnt(0)\n"                                                  \
     "s_mov_b32 %[done], m0\n"                                               \
     "s_mov_b32 m0, %[m0s]\n"
 
@@ -667,6 +679,8 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
     uint32_t obase = 0, fill = 0;             // output page covers [obase, obase + fill)
     uint32_t rec = 0, prev_len = 0, left = 0;
     uint32_t nrecs = 0, ndups = 0, nrevs = 0, nmiss = 0, nslow = 0;
+    // the run's prefetch mode, from the miss rate of the last >= 256 symbols
+    uint32_t pf_syms = 0, pf_miss = 0, pfon = 0;
     PROBE_DECL
     bool first_len = true;
     int status = 0;
@@ -1002,8 +1016,8 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
             uint32_t tvA = model_sentinel(), tvB = 0;
             uint32_t cA = U(ctx), qsA = U(qs), pvA = U(prevq), maA = U(maddr), sqA = U(seq);
             uint32_t cB, qsB, pvB, maB, sqB;
-            uint32_t dd = 0, nm = 0;
-            uint64_t scr;
+            uint32_t dd = 0, nm = 0, tvp;
+            uint64_t scr, pf;
             // the miss path: the backing store, fresh slots (guard, list; the
             // sentinel lanes are set from the context)
             const uint64_t back = reinterpret_cast<uint64_t>(J.back);
@@ -1036,7 +1050,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
 #define FQZ_RUN_OPERANDS                                                                      \
                 : [mA] "+{v[2:3]}"(mA), [mB] "+{v[4:5]}"(mB), [cw] "+{s[40:41]}"(cw),          \
                   [win] "+{s[42:43]}"(win), [scr] "=&{s[44:45]}"(scr), [rb] "+s"(in.rb),        \
-                  [nm] "+s"(nm),                                                               \
+                  [nm] "+s"(nm), [pf] "=&{v[6:7]}"(pf), [tvp] "=&v"(tvp),                       \
                   [vout] "+v"(vout), [tvA] "+v"(tvA), [tvB] "=&v"(tvB),                           \
                   [rng] "+s"(rng), [ub] "+s"(in.ub), [dd] "+s"(dd), [done] "+s"(done),        \
                   [cA] "+s"(cA), [qsA] "+s"(qsA), [pvA] "+s"(pvA), [maA] "+s"(maA), [sqA] "+s"(sqA), \
@@ -1056,7 +1070,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                   [voff] "v"(voff0), [vsent] "v"(vsent), [qlocv] "v"(qlocv),                   \
                   [cbig] "v"(cbig), [c19] "v"(c19), [vme] "v"(vme), [pvv] "v"(pvv),          \
                   [dvv] "v"(dvv), [sqv] "v"(sqv)                                              \
-                : "memory", "scc"
+                : "memory", "scc", "vcc"
 #ifdef FQZ5_DEC_PROBE
                 const uint32_t done_in = done;
                 const uint64_t ta = __builtin_amdgcn_s_memtime();
@@ -1065,17 +1079,23 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                     pr[5] += 1;
                 }
 #endif
-#define FQZ_RUN_NE(SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW)                                                                           \
+#define FQZ_RUN_NE(SENTWB, SENTEX, WCNT, MST, PF, PFT, MMOV, MWB, MVW)                                                                           \
                 if constexpr (QW && SEQ)                                                                     \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, PF, PFT, MMOV, MWB, MVW) FQZ_RUN_OPERANDS); \
                 else if constexpr (QW)                                                                       \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_W, FQZ_QT2_W, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, PF, PFT, MMOV, MWB, MVW) FQZ_RUN_OPERANDS); \
                 else if constexpr (SEQ)                                                                      \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW) FQZ_RUN_OPERANDS); \
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_CTX, FQZ_SEQ_SAME, SENTWB, SENTEX, WCNT, MST, PF, PFT, MMOV, MWB, MVW) FQZ_RUN_OPERANDS); \
                 else                                                                                         \
-                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, MLD, MMOV, MWB, MVW) FQZ_RUN_OPERANDS);
-                if constexpr (NE == 1) { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1", FQZ_MSENT_NONE, FQZ_MSENT_NONE, FQZ_MSENT_LANE, FQZ_MSENT_NONE1, "1") }
-                else { FQZ_RUN_NE(FQZ_SENT_WB, FQZ_SENT_EXIT, "2", FQZ_MSENT_ST, FQZ_MSENT_LD, FQZ_MSENT_MOV, FQZ_MSENT_WR, "2") }
+                    asm volatile(FQZ_RUN_ASM(FQZ_QT1_TAB, FQZ_QT2_TAB, FQZ_SEQ_NONE, FQZ_SEQ_NONE, SENTWB, SENTEX, WCNT, MST, PF, PFT, MMOV, MWB, MVW) FQZ_RUN_OPERANDS);
+                const uint32_t nm_in = nm, done_at = done;
+                if constexpr (NE == 1) {
+                    if (pfon) { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1", FQZ_MSENT_NONE, 1, FQZ_PF_NONE, FQZ_MSENT_LANE, FQZ_MSENT_NONE1, "1") }
+                    else { FQZ_RUN_NE(FQZ_SENT_NONE, FQZ_SENT_NONE, "1", FQZ_MSENT_NONE, 0, FQZ_PF_NONE, FQZ_MSENT_LANE, FQZ_MSENT_NONE1, "1") }
+                } else {
+                    if (pfon) { FQZ_RUN_NE(FQZ_SENT_WB, FQZ_SENT_EXIT, "2", FQZ_MSENT_ST, 1, FQZ_PF_SENT, FQZ_MSENT_MOV, FQZ_MSENT_WR, "2") }
+                    else { FQZ_RUN_NE(FQZ_SENT_WB, FQZ_SENT_EXIT, "2", FQZ_MSENT_ST, 0, FQZ_PF_SENT, FQZ_MSENT_MOV, FQZ_MSENT_WR, "2") }
+                }
 #undef FQZ_RUN_NE
 #undef FQZ_RUN_OPERANDS
 #ifdef FQZ5_DEC_PROBE
@@ -1092,6 +1112,13 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
                 dd = U(dd);
                 done = U(done);
                 nm = U(nm);
+                pf_syms += done - done_at;
+                pf_miss += nm - nm_in;
+                if (pf_syms >= 256u) {   // prefetch when more than one symbol in 8 misses
+                    pfon = U(pf_miss * 8u > pf_syms ? 1u : 0u);
+                    pf_syms = 0;
+                    pf_miss = 0;
+                }
                 cA = U(cA);
                 qsA = U(qsA);
                 pvA = U(pvA);
