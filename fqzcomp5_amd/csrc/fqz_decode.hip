@@ -284,10 +284,10 @@ DEV uint32_t set_addr(uint32_t ctx, uint32_t ns8, uint32_t me) {
     "v_cvt_f64_u32 %[d1], %[t6]\n"                                          \
     QT1(WX)                                                                 \
     "v_cvt_f64_u32 %[d0], %[rng]\n"                                         \
-    "s_cbranch_vccnz " MISSL "\n"                                           \
     "v_rcp_f64 %[d2], %[d1]\n"                                              \
     "s_add_u32 %[u], %[u], %[x]\n"                                          \
     SEQCTX(X, Y)                                                            \
+    "s_cbranch_vccnz " MISSL "\n"                                           \
     "v_lshrrev_b32 %[t4], 16, " EX "\n"                                     \
     "v_fma_f64 %[d1], -%[d1], %[d2], 1.0\n"                                 \
     QT2(X, WX)                                                              \
