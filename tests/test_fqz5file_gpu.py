@@ -92,6 +92,19 @@ def test_not_4line_fastq_fails_loudly():
         fqz5file.compress_bytes(b">r1\nACGT\n+\nIIII\n", 3)
 
 
+def test_empty_first_sequence_block_keeps_qualities():
+    """Known divergence (file path): the reference takes a block
+    for FASTA when its first record has no quality (load_seqs_kseq,
+    fqzcomp5.c:574-578), so a FASTQ block that starts with an empty-sequence
+    record gets a 9-zero quality section and decodes as FASTA text.  This
+    path decides FASTA once, for the text, from its first byte: such a block
+    keeps a quality section and the file round-trips to the same FASTQ."""
+    text = b"@r1\n\n+\n\n@r2\nACGT\n+\nIIII\n@r3\nGG\n+\n#I\n"
+    for level in (1, 3, 5):
+        z = fqz5file.compress_bytes(text, level)
+        assert fqz5file.decompress_bytes(z) == text
+
+
 FASTA = [os.path.join(HERE, "golden", "fastq", f) for f in ("sample.fasta", "paired_R1.fasta")]
 
 
