@@ -217,6 +217,9 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
     std::exception_ptr err0;
     std::thread gpu_early([&] {
         try {
+            // a new thread starts on device 0: g's arena may grow (hipMalloc
+            // on the current device) and must land on g's device
+            FQZ5_HIP(hipSetDevice(g.device));
             for (size_t k : early) {
                 name_prepare(h_names[k], lens[k], 0, name_level(methods[k]), jobs[k]);
                 name_add_lzp(g, jobs[k], d_names[k], lz0);

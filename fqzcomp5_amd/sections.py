@@ -340,7 +340,8 @@ def _chunks(rows, sizes, budget: int):
 
 
 def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState,
-                       group=None, chunk_bytes: int = 600_000_000):
+                       group=None, chunk_bytes: int = 600_000_000,
+                       commit_bytes: int = 2_400_000_000):
     """encode_run for the large-block presets (-7: 500 MB, -9: 1 GB blocks),
     in bounded device memory: the same choices and bytes, at the cost of
     coding each trial section's winner twice.
@@ -354,7 +355,12 @@ def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState
     try rewinds the last one's buffers); the replay picks every section's
     method from the sizes as encode_run does; then every section is coded
     with its one method a chunk at a time (fqz5_sections_commit codes the
-    methods a session did not try, "late")."""
+    methods a session did not try, "late").  A commit codes one candidate
+    per section (at most ~64 B of device memory per input byte, an fqz
+    section's), so its chunks are `commit_bytes` of input: the range chains
+    of several blocks' fqz / sequence-model sections then run side by side
+    instead of one chunk after another (-7: the four 250 MB quality
+    sections' FQZ0 chains in one launch)."""
     ins = np.array([s.in_size for s in secs], np.uint32)
     ids = np.array([s.sec for s in secs], np.int32)
     blank = np.zeros((len(secs), M_LAST), np.uint32)
@@ -373,7 +379,7 @@ def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState
     meth_all = trial_replay(g_ids, g_ins, g_sizes, avail, state, tried)
     meth = meth_all[off:off + len(secs)]
     res = []
-    for ch in _chunks(range(len(secs)), ins, chunk_bytes):
+    for ch in _chunks(range(len(secs)), ins, max(commit_bytes, chunk_bytes)):
         part = [secs[i] for i in ch]
         sections_try(part, np.zeros(len(ch), np.uint32))    # an empty session
         res += sections_commit(part, meth[ch])
@@ -414,7 +420,8 @@ def work_share(methods: list[int], world: int, rank: int) -> int:
 
 def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
                   state: TrialState, group=None, bounded: bool = False,
-                  chunk_bytes: int = 600_000_000, prune: bool = True):
+                  chunk_bytes: int = 600_000_000, prune: bool = True,
+                  commit_bytes: int = 2_400_000_000):
     """Code the sections of consecutive blocks (file order) over the ranks of
     `group`; every rank passes the same section ids / input sizes / owners,
     its Section for every section it holds the data of (None elsewhere) and
@@ -430,7 +437,8 @@ def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
     commits its own sections.
 
     bounded: the -7/-9 path of encode_run_bounded (tries chunked by
-    chunk_bytes, no pruning, every section coded again at commit).
+    chunk_bytes, no pruning, every section coded again at commit, in chunks
+    of commit_bytes).
     Returns (results: SectionResult per section or None when not owned,
     methods of every section, sizes)."""
     ws, rk = _world(group)
@@ -492,7 +500,7 @@ def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
     res: list = [None] * n
     mine = [i for i in rows if owner[i] == rk]
     if bounded:
-        for ch in _chunks(mine, ins, chunk_bytes):
+        for ch in _chunks(mine, ins, max(commit_bytes, chunk_bytes)):
             part = [secs[i] for i in ch]
             sections_try(part, np.zeros(len(ch), np.uint32))    # an empty session
             for i, r in zip(ch, sections_commit(part, meth[ch])):

@@ -127,7 +127,8 @@ def test_bounded_run_equals_run(level, kind, nreads, blk):
     """encode_run_bounded (the trial a section at a time, then every section
     coded with its one method, for the -7/-9 block sizes) makes the choices
     and the bytes of encode_run; chunk_bytes small enough that every chunk
-    holds one or two sections."""
+    holds one or two sections; the commit in one chunk (-7) or in chunks
+    as small as the tries' (-9)."""
     reads = GEN[kind](nreads, seed=13)
     blocks = synth.split_blocks(reads, blk)
     assert len(blocks) >= 4
@@ -138,7 +139,9 @@ def test_bounded_run_equals_run(level, kind, nreads, blk):
     got_a = [run.chosen(res_a, i) for i in range(len(res_a))]
     run_b = S.Run(reads, blocks, dev, names=False)
     res_b, meth_b, _, tried_b, _ = S.encode_run_bounded(run_b.enc_secs(), av, S.new_state(),
-                                                        chunk_bytes=2 * blk // 3)
+                                                        chunk_bytes=2 * blk // 3,
+                                                        commit_bytes=(2 * blk // 3 if level == 9
+                                                                      else 2_400_000_000))
     assert all(r.status == 0 for r in res_b)
     assert list(meth_a) == list(meth_b)
     assert list(tried_a) == list(tried_b)
