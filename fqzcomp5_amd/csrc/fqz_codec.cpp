@@ -657,17 +657,24 @@ void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
         for (FqzEvJob *J : js) ev_n += J->nev;
         prof_add(PK_FQZ_RC, ev.ms(), ev_n * 21.0);
     }
-    std::vector<FqzEvJob> cj;
     for (int k = 0; k < np; k++) {
         FqzEvJob &J = *js[size_t(k)];
         J.nwords = (P[size_t(k)] + 5 + 3) / 4 + 2;
         J.acc = reinterpret_cast<unsigned long long *>(g.arena.alloc_n<uint64_t>(J.nwords));
         g.memset0(J.acc, size_t(J.nwords) * 8);
         FQZ5_HIP(launch_fqz_bytes(J, 0, g.stream));
-        cj.push_back(J);
+        // carries through the columns: codes, their scan, digits
+        uint32_t *sw = g.arena.alloc_n<uint32_t>(J.nwords);
+        uint8_t *code = g.arena.alloc_n<uint8_t>(J.nwords);
+        uint8_t *pref = g.arena.alloc_n<uint8_t>(J.nwords);
+        FQZ5_HIP(launch_fqz_norm(J, 1, sw, code, g.stream));
+        size_t tb = 0;
+        FQZ5_HIP(fqz_carry_scan(code, pref, int(J.nwords), nullptr, tb, g.stream));
+        void *tmp = g.arena.alloc_n<uint8_t>(tb);
+        FQZ5_HIP(fqz_carry_scan(code, pref, int(J.nwords), tmp, tb, g.stream));
+        FQZ5_HIP(launch_fqz_norm(J, 2, sw, pref, g.stream));
+        FQZ5_HIP(launch_fqz_bytes(J, 2, g.stream));
     }
-    FQZ5_HIP(launch_fqz_carry(g.upload(cj), np, g.stream));
-    for (int k = 0; k < np; k++) FQZ5_HIP(launch_fqz_bytes(*js[size_t(k)], 2, g.stream));
 }
 
 // The range chain and the output bytes of every parallel request not in

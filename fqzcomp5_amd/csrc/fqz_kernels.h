@@ -138,6 +138,7 @@ hipError_t launch_fqz_events(const FqzEvJob &j, int phase, hipStream_t s);
 // hot: per job a list of stride words (zeroed); models with at least hot_min
 // events go to the one-wave-per-model kernel (hot_min = 0: none do)
 constexpr uint32_t FQZ_HOT_GRID = 64;            // waves per job for hot models
+constexpr uint32_t FQZ_HOT_GRID_MAX = 2048;     // at most, one per hot model
 constexpr uint32_t FQZ_HOT_MIN = 16384;
 hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t *hot,
                                  uint32_t stride, uint32_t hot_min, hipStream_t s);
@@ -146,12 +147,20 @@ hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
 hipError_t launch_fqz_entropy(const FqzEvJob &j, double *partial, uint32_t nblk, hipStream_t s);
 hipError_t launch_rec_entropy(const uint4 *rec, uint32_t nev, double *partial, uint32_t nblk,
                               hipStream_t s);
-hipError_t launch_fqz_carry(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
+// carry normalisation of the output columns: phase 1 writes s_w and the
+// carry code per word, phase 2 (code = the scanned prefix codes) the digits
+constexpr uint8_t FQZ_CARRY_KILL = 0, FQZ_CARRY_PROP = 1, FQZ_CARRY_GEN = 2;
+hipError_t launch_fqz_norm(const FqzEvJob &j, int phase, uint32_t *sw, uint8_t *code,
+                           hipStream_t s);
 hipError_t launch_fqz_expand(const FqzEvJob &j, hipStream_t s);
 hipError_t launch_fqz_bytes(const FqzEvJob &j, int phase, hipStream_t s);
 // fqz_sort.hip
 hipError_t fqz_exclusive_scan(const uint32_t *in, uint32_t *out, int n, void *tmp, size_t &bytes,
                               hipStream_t s);
+// inclusive scan of the carry codes (the composition of kill / propagate /
+// generate maps of a carry bit)
+hipError_t fqz_carry_scan(const uint8_t *in, uint8_t *out, int n, void *tmp, size_t &bytes,
+                          hipStream_t s);
 hipError_t fqz_sort_by_model(const uint32_t *k_in, uint32_t *k_out, const uint64_t *v_in,
                              uint64_t *v_out, int n, int key_bits, void *tmp, size_t &bytes,
                              hipStream_t s);

@@ -12,6 +12,7 @@
 // the serial literal encoder for multi-parameter blocks.  The decoder
 // (a18) is fqz_decode.hip.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 
 #include "fqz_kernels.h"
@@ -803,25 +804,30 @@ __global__ void k_fqz_accum(FqzEvJob J) {
     if (v >> 32) atomicAdd(&J.acc[(e >> 2) + 1], (unsigned long long)(v >> 32));
 }
 
-// Phase B: carry propagation through the columns.  The wave loads 64
-// columns at a time; the carry walks them in lane order on scalar registers.
-__global__ __launch_bounds__(64) void k_fqz_carry(const FqzEvJob *Js) {
-    const FqzEvJob J = load_job(Js + blockIdx.x);   // one wave per block of a batch
-    const int l = int(threadIdx.x);
-    unsigned long long carry = 0;
-    for (uint32_t w0 = 0; w0 < J.nwords; w0 += 64) {
-        const uint32_t w = w0 + uint32_t(l);
-        const unsigned long long v = w < J.nwords ? J.acc[w] : 0ull;
-        uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32), res = 0;
-        for (int k = 0; k < 64; k++) {
-            const uint32_t h = uint32_t(__builtin_amdgcn_readlane(int(hi), k));
-            const uint32_t w32 = uint32_t(__builtin_amdgcn_readlane(int(lo), k));
-            const unsigned long long t = ((unsigned long long)h << 32 | w32) + carry;
-            if (l == k) res = uint32_t(t);
-            carry = t >> 32;
-        }
-        if (w < J.nwords) J.acc[w] = res;
-    }
+// Phase B: carry propagation through the columns, in parallel.  The
+// serial form is t = acc[w] + carry; digit_w = t mod 2^32; carry = t >> 32.
+// hi(acc[w]) < 2^31 (a column takes one low part per event and nev < 2^31),
+// so the carry out of word w is hi(acc[w]) + b_{w+1} with a bit
+//   b_{w+1} = [s_w + b_w >= 2^32],   s_w = lo(acc[w]) + hi(acc[w-1]),
+// and digit_w = (s_w + b_w) mod 2^32.  Word w thus kills (s_w < 2^32 - 1),
+// propagates (s_w = 2^32 - 1) or generates (s_w >= 2^32) the bit: B1 writes
+// s_w mod 2^32 and that code, an inclusive scan composes the codes
+// (fqz_carry_scan: the later one wins unless it propagates), and B2 adds
+// b_w = [prefix w-1 generates] to every digit.
+__global__ void k_fqz_norm1(FqzEvJob J, uint32_t *sw, uint8_t *code) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= J.nwords) return;
+    const unsigned long long a0 = J.acc[w], a1 = w ? J.acc[w - 1] : 0ull;
+    const unsigned long long sv = (a0 & 0xffffffffull) + (a1 >> 32);
+    sw[w] = uint32_t(sv);
+    code[w] = sv >> 32 ? FQZ_CARRY_GEN : (uint32_t(sv) == 0xffffffffu ? FQZ_CARRY_PROP : FQZ_CARRY_KILL);
+}
+
+__global__ void k_fqz_norm2(FqzEvJob J, const uint32_t *sw, const uint8_t *pref) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= J.nwords) return;
+    const uint32_t b = (w && pref[w - 1] == FQZ_CARRY_GEN) ? 1u : 0u;
+    J.acc[w] = uint32_t(sw[w] + b);
 }
 
 // Phase C: bytes, most significant first.
@@ -863,7 +869,12 @@ hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t *ho
     if (hot_min) {
         hipLaunchKernelGGL(k_fqz_hot_list, dim3((FQZ_M_SEL + 255) / 256, njobs), dim3(256), 0, s,
                            d_jobs, hot, stride, hot_min);
-        hipLaunchKernelGGL(k_fqz_model_hot, dim3(FQZ_HOT_GRID, njobs), dim3(64), 0, s, d_jobs,
+        // a wave per hot model (up to stride - 1 of them per block), at
+        // least FQZ_HOT_GRID: the launch then lasts as long as the longest
+        // model's chain, not a wave's share of a thousand models (-7 ONT:
+        // ~1 000 hot models per FQZ0 candidate)
+        const uint32_t grid = std::min(std::max(stride - 1, FQZ_HOT_GRID), FQZ_HOT_GRID_MAX);
+        hipLaunchKernelGGL(k_fqz_model_hot, dim3(grid, njobs), dim3(64), 0, s, d_jobs,
                            hot, stride);
     }
     hipLaunchKernelGGL(k_fqz_model_pass, dim3(nblk * uint32_t(njobs)), dim3(256), lds, s,
@@ -876,8 +887,12 @@ hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_fqz_carry(const FqzEvJob *d_jobs, int njobs, hipStream_t s) {
-    if (njobs) hipLaunchKernelGGL(k_fqz_carry, dim3(njobs), dim3(64), 0, s, d_jobs);
+hipError_t launch_fqz_norm(const FqzEvJob &j, int phase, uint32_t *sw, uint8_t *code,
+                           hipStream_t s) {
+    if (!j.nwords) return hipSuccess;
+    const dim3 grid((j.nwords + 255) / 256);
+    if (phase == 1) hipLaunchKernelGGL(k_fqz_norm1, grid, dim3(256), 0, s, j, sw, code);
+    else hipLaunchKernelGGL(k_fqz_norm2, grid, dim3(256), 0, s, j, sw, code);
     return hipGetLastError();
 }
 
