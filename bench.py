@@ -315,7 +315,11 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                    "arena_bytes": [int(arena0), int(arena1)],
                    # candidates in the timed steps, and how many were provably
                    # losing and skipped their range chain (output unchanged)
-                   "fqz_trial": {"tried": fq1[0] - fq0[0], "pruned": fq1[1] - fq0[1]}},
+                   "fqz_trial": {"tried": fq1[0] - fq0[0], "pruned": fq1[1] - fq0[1],
+                                 # -7/-9: whether the candidates' size intervals
+                                 # decided the trial (else tried again exactly)
+                                 "intervals_decided": S.last_bounds_decided if level >= 7
+                                 else None}},
     }
     # ---- roofline of the dominant kernel ---------------------------------
     # every chain kernel's launch time from HIP events on the stream it runs

@@ -122,7 +122,9 @@ struct TrySession {
     std::vector<std::vector<int>> fqz_of;
     std::vector<SeqEncReq> seq;                   // sequence CM candidates
     std::vector<uint64_t> seq_lb;                 // pruned candidates: size lower bound (else 0)
+    std::vector<uint64_t> fqz_ub, seq_ub;         // pruned candidates: size upper bound
     std::vector<std::vector<int>> seq_of;
+    std::vector<uint32_t> upper;                  // the sizes matrix with upper bounds
     std::deque<std::vector<uint32_t>> recs;       // their (rewritable) lengths / flags
     std::vector<NameEnc> names;                   // name-section candidates (host bytes)
     std::vector<std::vector<int>> name_of;
@@ -206,6 +208,12 @@ void encode_name_jobs(GpuCtx &g, const fqz5_section *secs, const std::vector<int
 // the sections of this call that try such methods form one whole trial
 // window per section kind.
 std::atomic<int> g_prune{0};
+// Bounds-only tries (fqz5_set_trial_bounds): every fqz and sequence-model
+// candidate skips its range chain and reports its size as the interval
+// [lower, upper] (entropy, entropy plus the coder's slack): the caller
+// decides the trial from the intervals when they separate the candidates,
+// and codes the winners at commit (encode_run_bounded).
+std::atomic<int> g_bounds{0};
 std::atomic<uint64_t> g_fqz_tried{0}, g_fqz_pruned{0};
 
 // Which requests of one family of work candidates (fqz methods FQZ0..FQZ4 on
@@ -296,6 +304,17 @@ extern "C" {
 void fqz5_trial_init(fqz5_trial_state *st) { std::memset(st, 0, sizeof *st); }
 
 int fqz5_set_trial_prune(int on) { return g_prune.exchange(on ? 1 : 0); }
+
+int fqz5_set_trial_bounds(int on) { return g_bounds.exchange(on ? 1 : 0); }
+
+int fqz5_sections_try_upper(uint32_t *upper, int nsec) {
+    if (nsec < 0 || size_t(nsec) * FQZ5_M_LAST != t_sess.upper.size()) {
+        fqz5_set_error("fqz5_sections_try_upper: no try of that many sections on this thread");
+        return -1;
+    }
+    std::memcpy(upper, t_sess.upper.data(), t_sess.upper.size() * sizeof(uint32_t));
+    return 0;
+}
 
 void fqz5_trial_counts(uint64_t *out2) {
     out2[0] = g_fqz_tried.load();
@@ -544,7 +563,10 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 reqs.push_back(std::move(lzr[size_t(lzr_of[size_t(i)][LZP3])]));
             }
             std::vector<char> skip_f(fq.size(), 0), skip_s(sq.size(), 0);
-            if (g_prune.load()) {
+            if (g_bounds.load()) {
+                for (size_t k = 0; k < fq.size(); k++) skip_f[k] = fqz_size_lower_bound(fq[k]) > 0;
+                for (size_t k = 0; k < sq.size(); k++) skip_s[k] = seq_size_upper_bound(sq[k]) > 0;
+            } else if (g_prune.load()) {
                 skip_f = prune_plan(reqs, t_sess.fqz_of, FQZ0, FQZ4, fq.size(),
                                     [&](size_t k) { return fqz_size_lower_bound(fq[k]); });
                 skip_s = prune_plan(reqs, t_sess.seq_of, SEQ10, SEQ14B, sq.size(),
@@ -561,10 +583,14 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             }
             tf.join();
             if (ferr) std::rethrow_exception(ferr);
-            for (size_t k = 0; k < fq.size(); k++)
+            for (size_t k = 0; k < fq.size(); k++) {
                 t_sess.fqz_lb.push_back(skip_f[k] ? fqz_size_lower_bound(fq[k]) : 0);
-            for (size_t k = 0; k < sq.size(); k++)
+                t_sess.fqz_ub.push_back(skip_f[k] ? fqz_size_upper_bound(fq[k]) : 0);
+            }
+            for (size_t k = 0; k < sq.size(); k++) {
                 t_sess.seq_lb.push_back(skip_s[k] ? seq_size_lower_bound(sq[k]) : 0);
+                t_sess.seq_ub.push_back(skip_s[k] ? seq_size_upper_bound(sq[k]) : 0);
+            }
             g_fqz_tried += fq.size() + sq.size();
             for (char c : skip_f) g_fqz_pruned += c ? 1 : 0;
             for (char c : skip_s) g_fqz_pruned += c ? 1 : 0;
@@ -577,12 +603,16 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             if (!sq.empty()) seq_encode_batch(g, sq);
             t_sess.fqz_lb.assign(fq.size(), 0);
             t_sess.seq_lb.assign(sq.size(), 0);
+            t_sess.fqz_ub.assign(fq.size(), 0);
+            t_sess.seq_ub.assign(sq.size(), 0);
             g_fqz_tried += fq.size() + sq.size();
         }
         t_sess.open = true;
         if (step_trace()) std::fprintf(stderr, "sections_try: %.1f ms\n", now_ms() - t0);
         // sizes as compress_with_methods sees them: UINT_MAX when not run,
-        // 0 when the codec returned NULL (out_len = *out_size = 0)
+        // 0 when the codec returned NULL (out_len = *out_size = 0); a
+        // skipped candidate's lower bound here, its upper bound in `upper`
+        t_sess.upper.assign(size_t(nsec) * FQZ5_M_LAST, 0);
         for (int i = 0; i < nsec; i++)
             for (int m = 0; m < FQZ5_M_LAST; m++) {
                 const int ri = t_sess.req_of[i][m], fi = t_sess.fqz_of[i][m];
@@ -603,7 +633,13 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                     sz = t_sess.fqz[size_t(fi)].ok ? layout_size(t_sess.fqz[size_t(fi)].out)
                          : lb ? uint32_t(std::min<uint64_t>(lb, UINT32_MAX - 1)) : 0;
                 }
+                uint32_t up = sz;
+                if (si >= 0 && !t_sess.seq[size_t(si)].ok && t_sess.seq_ub[size_t(si)])
+                    up = uint32_t(std::min<uint64_t>(t_sess.seq_ub[size_t(si)], UINT32_MAX - 1));
+                if (fi >= 0 && !t_sess.fqz[size_t(fi)].ok && t_sess.fqz_ub[size_t(fi)])
+                    up = uint32_t(std::min<uint64_t>(t_sess.fqz_ub[size_t(fi)], UINT32_MAX - 1));
                 sizes[size_t(i) * FQZ5_M_LAST + m] = sz;
+                t_sess.upper[size_t(i) * FQZ5_M_LAST + m] = up;
             }
         return 0;
     } catch (const std::exception &e) {

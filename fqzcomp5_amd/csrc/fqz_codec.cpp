@@ -400,6 +400,19 @@ void copy_gparams(Global &G, const fqz_gparams *gp) {
 
 }  // namespace
 
+// Coder output bytes P (before the 5 flush bytes) from the events' entropy
+// sum H = sum log2(total / freq) and slack S = sum -log2(1 - total 2^-24):
+// 8 P >= H - 8 (the final range over the initial one is at least 2^-8) and
+// 8 P <= H + S (the final range is at most the initial 2^32 - 1); margins
+// cover the rounding of the double sums.
+uint64_t rc_bytes_lower(double bits) {
+    bits = bits * (1.0 - 1e-9) - 8.0 - 64.0;
+    return bits > 0 ? uint64_t(bits / 8.0) : 0;
+}
+uint64_t rc_bytes_upper(double bits, double slack) {
+    return uint64_t(((bits + slack) * (1.0 + 1e-9) + 64.0) / 8.0);
+}
+
 struct FqzEncReq::Work {
     Global G;
     std::vector<uint8_t> hdr;
@@ -410,6 +423,7 @@ struct FqzEncReq::Work {
     uint32_t last[2] = {0, 0};          // last record's event offset and count
     uint32_t P = 0, clen = 0;
     uint64_t lb = 0;                    // lower bound of the output size (0: unknown)
+    uint64_t ub = 0;                    // upper bound (valid when lb is)
 };
 
 // Every block of the batch goes through each stage before the next one:
@@ -593,22 +607,24 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         uint32_t *hot = g.arena.alloc_n<uint32_t>(size_t(stride) * size_t(np));
         g.memset0(hot, size_t(stride) * size_t(np) * 4);
         FQZ5_HIP(launch_fqz_model_pass(g.upload(jobs), np, hot, stride, hot_min, g.stream));
-        // the entropy of each block's events: a lower bound of its size
+        // the entropy of each block's events and the coder's slack: lower
+        // and upper bounds of its size
         constexpr uint32_t EB = 1024;
-        double *part = g.arena.alloc_n<double>(size_t(EB) * size_t(np));
-        for (int k = 0; k < np; k++) FQZ5_HIP(launch_fqz_entropy(jobs[size_t(k)], part + size_t(k) * EB, EB, g.stream));
-        std::vector<double> hp(size_t(EB) * size_t(np));
+        double *part = g.arena.alloc_n<double>(2 * size_t(EB) * size_t(np));
+        for (int k = 0; k < np; k++)
+            FQZ5_HIP(launch_fqz_entropy(jobs[size_t(k)], part + 2 * size_t(k) * EB, EB, g.stream));
+        std::vector<double> hp(2 * size_t(EB) * size_t(np));
         g.download(hp.data(), part, hp.size());
         g.sync();
         for (int k = 0; k < np; k++) {
-            double bits = 0;
-            for (uint32_t b = 0; b < EB; b++) bits += hp[size_t(k) * EB + b];
-            // 8 P >= bits - 8 (log2 of the final over the initial range);
-            // a margin covers the rounding of the double sums
-            bits = bits * (1.0 - 1e-9) - 8.0 - 64.0;
-            const uint64_t P = bits > 0 ? uint64_t(bits / 8.0) : 0;
+            double bits = 0, slack = 0;
+            for (uint32_t b = 0; b < EB; b++) {
+                bits += hp[2 * size_t(k) * EB + b];
+                slack += hp[(2 * size_t(k) + 1) * EB + b];
+            }
             FqzEncReq::Work &W = *par[size_t(k)]->w;
-            W.lb = uint64_t(W.hdr.size()) + P + 5;
+            W.lb = uint64_t(W.hdr.size()) + rc_bytes_lower(bits) + 5;
+            W.ub = uint64_t(W.hdr.size()) + rc_bytes_upper(bits, slack) + 5;
         }
     }
 }
@@ -707,6 +723,8 @@ void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vecto
         if (W.clen > W.room) continue;   // (cannot happen: the bound covers the coder)
         if (W.lb > uint64_t(W.hdr.size()) + W.clen)   // the entropy bound is a theorem
             throw std::runtime_error("fqz: size below its entropy bound");
+        if (W.ub < uint64_t(W.hdr.size()) + W.clen)   // and so is the slack bound
+            throw std::runtime_error("fqz: size above its upper bound");
         Piece h;
         h.host = W.hdr;
         Piece d;
@@ -719,6 +737,7 @@ void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vecto
 }
 
 uint64_t fqz_size_lower_bound(const FqzEncReq &r) { return r.w ? r.w->lb : 0; }
+uint64_t fqz_size_upper_bound(const FqzEncReq &r) { return r.w && r.w->lb ? r.w->ub : 0; }
 
 void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
     fqz_encode_prepare(g, reqs);
@@ -850,9 +869,37 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
             for (int sq = 0; sq < 2; sq++)
                 for (int qi = 0; qi < 2; qi++) {
                     std::vector<FqzDecJob> js;
+                    std::vector<uint64_t> steps;
                     for (FqzDecReq *R : rs)
-                        if (R->w->ne == ne && int(R->w->seq_ctx) == sq && int(R->w->qid) == qi)
+                        if (R->w->ne == ne && int(R->w->seq_ctx) == sq && int(R->w->qid) == qi) {
                             js.push_back(R->w->D);
+                            steps.push_back(R->w->D.n);
+                        }
+                    // hedge: copies of the long blocks on spare CUs (one
+                    // workgroup per CU: its LDS), as the rANS decode chains
+                    // (DESIGN.md section 4); a copy needs its own backing store
+                    HedgeShare share(size_t(g.cus));
+                    const bool long_block =
+                        !steps.empty() && *std::max_element(steps.begin(), steps.end()) >= (1u << 20);
+                    const std::vector<int> cp = long_block ? hedge_plan(steps, share.cus)
+                                                           : std::vector<int>(js.size(), 1);
+                    const size_t nj = js.size();
+                    for (size_t k = 0; k < nj; k++) {
+                        if (cp[k] <= 1) continue;
+                        uint32_t *done = g.arena.alloc_n<uint32_t>(1);
+                        g.memset0(done, 4);
+                        js[k].done = done;
+                        for (int c = 1; c < cp[k]; c++) {
+                            FqzDecJob J = js[k];
+                            J.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * J.ment);
+                            if (ne == 2) {
+                                J.back_hi = g.arena.alloc_n<uint32_t>(size_t(FQZ_CTX) * 64);
+                                J.hi_bits = g.arena.alloc_n<uint32_t>(FQZ_CTX / 32);
+                                g.memset0(J.hi_bits, FQZ_CTX / 8);
+                            }
+                            js.push_back(J);
+                        }
+                    }
                     if (!js.empty()) {
                         EventPair ev(prof_on(), g.stream);
                         FQZ5_HIP(launch_fqz_dec(g.upload(js), int(js.size()), ne, sq != 0,
@@ -861,7 +908,7 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
                         if (ev.on) {   // compressed bytes in, quality bytes out
                             g.sync();
                             double b = 0;
-                            for (const FqzDecJob &J : js) b += double(J.in_len) + double(J.n);
+                            for (size_t k = 0; k < nj; k++) b += double(js[k].in_len) + double(js[k].n);
                             prof_add(PK_FQZ_DEC, ev.ms(), b);
                         }
                     }

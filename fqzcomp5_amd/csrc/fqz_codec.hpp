@@ -40,6 +40,11 @@ void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs);
 void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs);
 void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vector<char> *skip);
 uint64_t fqz_size_lower_bound(const FqzEncReq &r);
+// ... and its upper bound (the coder's slack over the entropy), 0 if unknown
+uint64_t fqz_size_upper_bound(const FqzEncReq &r);
+// coder bytes from the entropy sum (and slack sum) of a range-coded event list
+uint64_t rc_bytes_lower(double bits);
+uint64_t rc_bytes_upper(double bits, double slack);
 struct FqzEvJob;
 // The range coder back end shared by fqz and the sequence model: for jobs
 // whose rec[] (stream order), nev, out and out_len are set, the range

@@ -919,7 +919,17 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         next_uniform(sym);
     };
 
+    // hedged copies: every 64 loop turns (~4 K symbols) lane 0 reads *done
+    // by an atomic (at L2, coherent), and the copy leaves once another has
+    // finished the block
+    uint32_t turns = 0;
+    bool lost = false;
     for (;;) {
+        if (J.done && (++turns & 63u) == 0u) {
+            uint32_t d = 0;
+            if (l == 0) d = __hip_atomic_fetch_add(J.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (RL(d, 0)) { lost = true; break; }
+        }
         if (left == 0) {
             // ---- record header (fqzcomp_qual.c:1484-1540) --------------------
             if (obase + fill >= n) break;
@@ -1158,7 +1168,9 @@ __global__ __launch_bounds__(64) void k_fqz_dec(const FqzDecJob *Js) {
         if (fill == OBUF) flush();
         if (SEQ && left && tpos - sb0 == SEQB) { sb0 = tpos; stage_seq(); }
     }
+    if (lost) return;   // another copy decodes (decoded) this block
     if (status == 0) flush();
+    if (J.done && l == 0) __hip_atomic_store(J.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (l == 0) {
         *J.status = status;
         *J.nrec_out = rec;

@@ -81,6 +81,10 @@ struct FqzDecJob {
     uint2 *dups;                // duplicate records {start, len}
     uint2 *revs;                // reversed records {start, len}
     uint32_t *counts;           // out: [nrecs, ndups, nrevs, misses, slow symbols]
+    // hedged (not null): copies of the block decode on other CUs with their
+    // own backing store, everything else shared (identical writes); the
+    // first copy to finish sets *done and the others leave
+    uint32_t *done;
 };
 
 // Bytes of one cached quality model for `live` symbols: slots of 8 bytes
@@ -143,7 +147,8 @@ constexpr uint32_t FQZ_HOT_MIN = 16384;
 hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t *hot,
                                  uint32_t stride, uint32_t hot_min, hipStream_t s);
 hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
-// per workgroup: sum over its events of log2(total / freq) (after the model pass)
+// per workgroup b: sum over its events of log2(total / freq) (after the model
+// pass) in partial[b], of -log2(1 - total 2^-24) in partial[nblk + b]
 hipError_t launch_fqz_entropy(const FqzEvJob &j, double *partial, uint32_t nblk, hipStream_t s);
 hipError_t launch_rec_entropy(const uint4 *rec, uint32_t nev, double *partial, uint32_t nblk,
                               hipStream_t s);

@@ -590,41 +590,53 @@ __global__ __launch_bounds__(64) void k_fqz_model_hot(const FqzEvJob *Js, const 
 // per workgroup (the host adds them).  The coder's byte count P satisfies
 // 8 P >= this - 8, so it bounds the output size from
 // below before the range chain runs.
+// The upper bound: floor(range / total) >= range/total
+// - 1 and range >= 2^24 before every event, so an event narrows the range by
+// at most (total / freq) / (1 - total / 2^24): 8 P <= sum log2(total / freq)
+// + sum -log2(1 - total 2^-24).  partial[gridDim.x + b] gets the second sum.
+DEV double rc_slack(double t) { return -log1p(-t * 0x1p-24) * 1.4426950408889634; }
+
+DEV void entropy_reduce(double acc, double slack, double *partial) {
+    __shared__ double red[256], rs[256];
+    red[threadIdx.x] = acc;
+    rs[threadIdx.x] = slack;
+    __syncthreads();
+    for (uint32_t o = 128; o; o >>= 1) {
+        if (threadIdx.x < o) {
+            red[threadIdx.x] += red[threadIdx.x + o];
+            rs[threadIdx.x] += rs[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        partial[blockIdx.x] = red[0];
+        partial[gridDim.x + blockIdx.x] = rs[0];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_fqz_entropy(FqzEvJob J, double *partial) {
-    __shared__ double red[256];
-    double acc = 0.0;
+    double acc = 0.0, slack = 0.0;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < J.nev; k += gridDim.x * blockDim.x) {
         const uint64_t c = J.code[k];
         const uint32_t f = uint32_t(c >> 16) & 0xffffu, t = uint32_t(c >> 32);
         acc += log2(double(t)) - log2(double(f));
+        slack += rc_slack(double(t));
     }
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (uint32_t o = 128; o; o >>= 1) {
-        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    entropy_reduce(acc, slack, partial);
 }
 
 // The same bound from coder records {RN(1/total) (2 words), freq, cum} in
 // stream order (the sequence model's events): log2(total) = -log2(RN(1/total))
 // to within 2^-52 relative, far inside the host's margin.
 __global__ __launch_bounds__(256) void k_rec_entropy(const uint4 *rec, uint32_t nev, double *partial) {
-    __shared__ double red[256];
-    double acc = 0.0;
+    double acc = 0.0, slack = 0.0;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nev; k += gridDim.x * blockDim.x) {
         const uint4 r = rec[k];
         const double rn = __longlong_as_double((long long)((uint64_t(r.y) << 32) | r.x));
         acc += -log2(rn) - log2(double(r.z));
+        slack += rc_slack(rint(1.0 / rn));
     }
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (uint32_t o = 128; o; o >>= 1) {
-        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    entropy_reduce(acc, slack, partial);
 }
 
 hipError_t launch_rec_entropy(const uint4 *rec, uint32_t nev, double *partial, uint32_t nblk,

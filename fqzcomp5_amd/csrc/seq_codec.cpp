@@ -53,6 +53,7 @@ struct SeqWork {
     FqzEvJob E{};
     uint32_t nev = 0;
     uint64_t lb = 0;                    // output bytes >= lb
+    uint64_t ub = 0;                    // output bytes <= ub
     uint32_t clen = 0;
     bool ready = false;                 // events built (records did not run out)
 };
@@ -126,9 +127,9 @@ static void seq_prepare_dev(GpuCtx &g, SeqWork &W, const uint8_t *d_in, uint32_t
 }
 
 void seq_encode_prepare(GpuCtx &g, std::vector<SeqEncReq> &reqs) {
-    constexpr uint32_t EB = 256;
-    double *part = g.arena.alloc_n<double>(size_t(EB) * std::max<size_t>(reqs.size(), 1));
-    g.memset0(part, size_t(EB) * std::max<size_t>(reqs.size(), 1) * sizeof(double));
+    constexpr uint32_t EB = 256;   // per request: EB entropy partials, then EB slack partials
+    double *part = g.arena.alloc_n<double>(2 * size_t(EB) * std::max<size_t>(reqs.size(), 1));
+    g.memset0(part, 2 * size_t(EB) * std::max<size_t>(reqs.size(), 1) * sizeof(double));
     for (size_t i = 0; i < reqs.size(); i++) {
         SeqEncReq &R = reqs[i];
         R.ok = false;
@@ -137,20 +138,23 @@ void seq_encode_prepare(GpuCtx &g, std::vector<SeqEncReq> &reqs) {
         if (R.k < 1 || R.k > int(SEQ_K_MAX)) throw GpuError("seq: context size out of range (1..14)");
         std::vector<uint32_t> seg;
         if (!R.lens || !seq_segments(R.lens, R.nrec, R.n, seg)) continue;
-        seq_prepare_dev(g, *R.w, R.d_in, R.n, seg, R.both, R.k, part + i * EB, EB);
+        seq_prepare_dev(g, *R.w, R.d_in, R.n, seg, R.both, R.k, part + 2 * i * EB, EB);
         R.w->ready = true;
     }
-    std::vector<double> hp(size_t(EB) * reqs.size());
+    std::vector<double> hp(2 * size_t(EB) * reqs.size());
     g.download(hp.data(), part, hp.size());
     g.sync();
     for (size_t i = 0; i < reqs.size(); i++) {
         SeqWork &W = *reqs[i].w;
         if (!W.ready) continue;
-        double bits = 0;
-        for (uint32_t b = 0; b < EB; b++) bits += hp[i * EB + b];
-        // 8 P >= bits - 8, with a margin for the sums
-        bits = bits * (1.0 - 1e-9) - 8.0 - 64.0;
-        W.lb = bits > 0 ? uint64_t(bits / 8.0) : 0;
+        double bits = 0, slack = 0;
+        for (uint32_t b = 0; b < EB; b++) {
+            bits += hp[2 * i * EB + b];
+            slack += hp[(2 * i + 1) * EB + b];
+        }
+        // the coder's P bytes and its 5 flush bytes
+        W.lb = rc_bytes_lower(bits);
+        W.ub = rc_bytes_upper(bits, slack) + 5;
     }
 }
 
@@ -177,6 +181,8 @@ void seq_encode_finish(GpuCtx &g, std::vector<SeqEncReq> &reqs, const std::vecto
         SeqWork &W = *R->w;
         if (W.lb > W.clen)   // the entropy bound is a theorem
             throw GpuError("seq: size below its entropy bound");
+        if (W.ub < W.clen)   // and so is the slack bound
+            throw GpuError("seq: size above its upper bound");
         Piece p;
         p.dev = W.E.out;
         p.len = W.clen;
@@ -186,6 +192,7 @@ void seq_encode_finish(GpuCtx &g, std::vector<SeqEncReq> &reqs, const std::vecto
 }
 
 uint64_t seq_size_lower_bound(const SeqEncReq &r) { return r.w && r.w->ready ? r.w->lb : 0; }
+uint64_t seq_size_upper_bound(const SeqEncReq &r) { return r.w && r.w->ready ? r.w->ub : 0; }
 
 void seq_encode_batch(GpuCtx &g, std::vector<SeqEncReq> &reqs) {
     seq_encode_prepare(g, reqs);

@@ -28,6 +28,8 @@ void seq_encode_prepare(GpuCtx &g, std::vector<SeqEncReq> &reqs);
 void seq_encode_finish(GpuCtx &g, std::vector<SeqEncReq> &reqs, const std::vector<char> *skip);
 // Output size lower bound after prepare (entropy of the events), 0 if none.
 uint64_t seq_size_lower_bound(const SeqEncReq &r);
+// ... and the upper bound (entropy plus the coder's slack), 0 if none.
+uint64_t seq_size_upper_bound(const SeqEncReq &r);
 void seq_encode_batch(GpuCtx &g, std::vector<SeqEncReq> &reqs);
 
 struct SeqDecReq {

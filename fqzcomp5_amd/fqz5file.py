@@ -381,6 +381,7 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
             continue
         W = _Window()
         W.text_d, W.recs, W.first, W.fasta, W.pairs = text_d, recs, first[:keep + 1], fasta, paired
+        W.final = bool(r1_done and keep == nb)   # the input ends with this window
         if keep < nb:                          # the next window starts at block `keep`
             r = int(first[keep])
             W.consume = [_rec_start(recs, r)] + \
@@ -438,7 +439,7 @@ def _encode_stream(srcs: list, sink: _Sink, level: int, blk_size: int | None, de
             for q in range(per):
                 secs[per * b + q] = local[per * j + q]
         res, meth, _ = S.encode_window(secs, ids, ins, owner, av, state, group,
-                                       bounded=level >= 7)
+                                       bounded=level >= 7, final=W.final)
         mine = [j for j, b in enumerate(need) if blk_owner[b] == rk]
         full_res = [None] * (len(need) * per)
         for j, b in enumerate(need):

@@ -111,6 +111,7 @@ _bound = False
 
 
 TRIAL_WINDOW = 3      # FQZ5_METRICS_TRIAL (fqzcomp5.c:152)
+last_bounds_decided = None   # whether the last bounded run's intervals decided its trial
 
 
 def trial_counts() -> tuple[int, int]:
@@ -127,6 +128,10 @@ def _load():
         so.fqz5_trial_init.argtypes = [C.POINTER(TrialState)]
         so.fqz5_set_trial_prune.restype = C.c_int
         so.fqz5_set_trial_prune.argtypes = [C.c_int]
+        so.fqz5_set_trial_bounds.restype = C.c_int
+        so.fqz5_set_trial_bounds.argtypes = [C.c_int]
+        so.fqz5_sections_try_upper.restype = C.c_int
+        so.fqz5_sections_try_upper.argtypes = [C.POINTER(C.c_uint32), C.c_int]
         so.fqz5_trial_counts.argtypes = [C.POINTER(C.c_uint64)]
         so.fqz5_trial_schedule.argtypes = [C.POINTER(C.c_int32), C.c_int,
                                            C.POINTER(C.c_uint32), C.POINTER(TrialState),
@@ -218,6 +223,160 @@ def trial_replay(sec_ids, in_sizes, sizes: np.ndarray, avail: np.ndarray,
                          C.byref(state), out.ctypes.data_as(C.POINTER(C.c_int32)),
                          None if tried is None else
                          tried.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return out
+
+
+def sections_try_bounds(secs: list[Section], masks: np.ndarray):
+    """sections_try with every fqz / sequence-model candidate's range chain
+    skipped (fqz5_set_trial_bounds): (lower, upper) size matrices, equal
+    wherever the size is exact."""
+    so = _load()
+    prev = so.fqz5_set_trial_bounds(1)
+    try:
+        lo = sections_try(secs, masks)
+    finally:
+        so.fqz5_set_trial_bounds(prev)
+    hi = np.zeros(len(secs) * M_LAST, np.uint32)
+    if so.fqz5_sections_try_upper(hi.ctypes.data_as(C.POINTER(C.c_uint32)), len(secs)):
+        raise _lib.NativeError("fqz5_sections_try_upper: " + _lib.last_error())
+    return lo, hi.reshape(len(secs), M_LAST)
+
+
+def _first_min_open(lo, hi, ratios: bool = False) -> list:
+    """Which candidates keep the first smallest of values known only within
+    [lo[j], hi[j]] open (compress_with_methods keeps the first smallest size,
+    fqzcomp5.c:2111-2119; metrics_method the first smallest ratio,
+    :1913-1920): empty when the winner is the same for every choice of
+    values, else the winner and every candidate whose interval lets it tie or
+    win.  Pairs of exact values are always decided.  Values are Fractions or
+    ints."""
+    w = min(range(len(lo)), key=lambda j: (lo[j], j))
+    out = []
+    for j in range(len(lo)):
+        if j == w or (lo[j] == hi[j] and lo[w] == hi[w]):
+            continue
+        # ratios: a margin for the reference's double arithmetic
+        gap = hi[w] * (1 + 1e-9) if ratios else hi[w]
+        if (j < w and not gap < lo[j]) or (j > w and not gap <= lo[j]):
+            out.append(j)
+    return out + [w] if out else []
+
+
+def _first_min_fixed(lo, hi, ratios: bool = False) -> bool:
+    return not _first_min_open(lo, hi, ratios)
+
+
+def trial_decided(lo: np.ndarray, hi: np.ndarray, ids, ins, tried, sched, state_in: TrialState,
+                  final: bool, why: list | None = None, open_pairs: set | None = None) -> bool:
+    """Whether the trial replay (metrics_method / compress_with_methods,
+    fqzcomp5.c:1899-2127) picks the same methods for every size matrix
+    between lo and hi (per section and method).  The decisions that read
+    sizes: each tried section keeps its first smallest candidate, and each
+    completed trial window (TRIAL_WINDOW tried sections of a kind) picks the
+    first smallest (csize + 1) / usize summed over it, at the next section of
+    its kind (sched: the trial schedule, nonzero on trial and re-trial
+    sections; tried: the methods each section tried).  Interval sizes stand
+    in for exact ones only when every such decision falls inside this call
+    (or the input ends with it: `final`), so the state carried out holds no
+    interval-derived sums a later call could read; and not when the call
+    starts inside a trial window.  open_pairs (if given) receives the
+    (section, method) pairs of interval sizes that leave a decision open:
+    exact sizes for them decide it."""
+    from fractions import Fraction
+    ids = [int(x) for x in ids]
+    n = len(ids)
+    for k in range(4):
+        if 0 < state_in.sec[k].trial < TRIAL_WINDOW:
+            return False
+    ok = True
+
+    def no(msg, pairs):
+        if why is not None:
+            why.append(msg)
+        if open_pairs is not None:
+            open_pairs.update((i, m) for i, m in pairs if lo[i, m] != hi[i, m])
+        return False
+
+    for i in range(n):
+        ms = [m for m in range(M_LAST) if (int(tried[i]) >> m) & 1]
+        op = _first_min_open([int(lo[i, m]) for m in ms], [int(hi[i, m]) for m in ms]) \
+            if len(ms) > 1 else []
+        if op:
+            ok = no(f"section {i} (kind {ids[i]}): " + ", ".join(
+                f"m{m} [{int(lo[i, m])}, {int(hi[i, m])}]" for m in ms),
+                [(i, ms[j]) for j in op])
+    for k in sorted(set(ids)):
+        rows = [i for i in range(n) if ids[i] == k and sched[i]]
+        for g0 in range(0, len(rows), TRIAL_WINDOW):
+            grp = rows[g0:g0 + TRIAL_WINDOW]
+            later = any(ids[j] == k for j in range(grp[-1] + 1, n))
+            if not later:
+                if final:
+                    continue          # no decision follows within the input
+                return False
+            if len(grp) < TRIAL_WINDOW:
+                return False          # (cannot happen: a window completes first)
+            us, cl, ch = {}, {}, {}
+            for i in grp:
+                for m in range(M_LAST):
+                    if (int(tried[i]) >> m) & 1:
+                        us[m] = us.get(m, 0) + int(ins[i])
+                        cl[m] = cl.get(m, 0) + int(lo[i, m])
+                        ch[m] = ch.get(m, 0) + int(hi[i, m])
+            ms = sorted(m for m in us if us[m])
+            op = _first_min_open([Fraction(cl[m] + 1, us[m]) for m in ms],
+                                 [Fraction(ch[m] + 1, us[m]) for m in ms], ratios=True) \
+                if len(ms) > 1 else []
+            if op:
+                ok = no(f"window of kind {k} at sections {grp}: " + ", ".join(
+                    f"m{m} [{cl[m]}, {ch[m]}]" for m in ms),
+                    [(i, ms[j]) for j in op for i in grp if (int(tried[i]) >> ms[j]) & 1])
+    return ok
+
+
+def refine_exact(secs: list, lo: np.ndarray, hi: np.ndarray, pairs, ins, chunk_bytes: int):
+    """Exact sizes for the (section, method) pairs whose intervals left a
+    trial decision open: those sections try just those methods with their
+    range chains (sections_try, no pruning), lo = hi = the size."""
+    so = _load()
+    want = {}
+    for i, m in pairs:
+        want[i] = want.get(i, 0) | (1 << m)
+    rows = sorted(want)
+    prev = so.fqz5_set_trial_prune(0)
+    try:
+        for ch in _chunks(rows, ins, chunk_bytes):
+            got = sections_try([secs[i] for i in ch], np.array([want[i] for i in ch], np.uint32))
+            for r, i in enumerate(ch):
+                for m in range(M_LAST):
+                    if (want[i] >> m) & 1:
+                        lo[i, m] = hi[i, m] = got[r, m]
+    finally:
+        so.fqz5_set_trial_prune(prev)
+
+
+def bounds_usable(ids, sched, state_in: TrialState, final: bool) -> bool:
+    """The structural half of trial_decided, known before any try: the call
+    does not start inside a trial window, and every window's decision falls
+    inside the call (or the input ends with it)."""
+    ids = [int(x) for x in ids]
+    for k in range(4):
+        if 0 < state_in.sec[k].trial < TRIAL_WINDOW:
+            return False
+    if final:
+        return True
+    for k in sorted(set(ids)):
+        rows = [i for i in range(len(ids)) if ids[i] == k and sched[i]]
+        for g0 in range(0, len(rows), TRIAL_WINDOW):
+            grp = rows[g0:g0 + TRIAL_WINDOW]
+            if not any(ids[j] == k for j in range(grp[-1] + 1, len(ids))):
+                return False
+    return True
+
+
+def _copy_state(st: TrialState) -> TrialState:
+    out = TrialState()
+    C.memmove(C.byref(out), C.byref(st), C.sizeof(TrialState))
     return out
 
 
@@ -341,7 +500,7 @@ def _chunks(rows, sizes, budget: int):
 
 def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState,
                        group=None, chunk_bytes: int = 600_000_000,
-                       commit_bytes: int = 2_400_000_000):
+                       commit_bytes: int = 2_400_000_000, bounds: bool = True):
     """encode_run for the large-block presets (-7: 500 MB, -9: 1 GB blocks),
     in bounded device memory: the same choices and bytes, at the cost of
     coding each trial section's winner twice.
@@ -360,23 +519,80 @@ def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState
     section's), so its chunks are `commit_bytes` of input: the range chains
     of several blocks' fqz / sequence-model sections then run side by side
     instead of one chunk after another (-7: the four 250 MB quality
-    sections' FQZ0 chains in one launch)."""
+    sections' FQZ0 chains in one launch).
+
+    bounds: the tries skip every fqz / sequence-model range chain and give
+    size intervals (fqz5_set_trial_bounds); trial_decided checks that the
+    intervals fix every choice the trial makes (else the tries run again with
+    exact sizes), so the choices are those of exact sizes.  The returned
+    sizes then hold the intervals' lower ends for those candidates.  The
+    call is taken to hold the whole input (a decision left for a later call
+    would read interval sums from the state)."""
     ins = np.array([s.in_size for s in secs], np.uint32)
     ids = np.array([s.sec for s in secs], np.int32)
     blank = np.zeros((len(secs), M_LAST), np.uint32)
     _, _, g_ids0, off = exchange_sizes(blank, ins, ids, group)
-    sched = trial_schedule(g_ids0, avail, state)[off:off + len(secs)]
-    local = np.full((len(secs), M_LAST), np.iinfo(np.uint32).max, np.uint32)
+    sched_all = trial_schedule(g_ids0, avail, state)
+    sched = sched_all[off:off + len(secs)]
     so = _load()
-    prev = so.fqz5_set_trial_prune(0)         # pruning needs a whole trial window per try
-    try:
-        for ch in _chunks([i for i in range(len(secs)) if sched[i]], ins, chunk_bytes):
-            local[ch] = sections_try([secs[i] for i in ch], sched[ch])
-    finally:
-        so.fqz5_set_trial_prune(prev)
-    g_sizes, g_ins, g_ids, off = exchange_sizes(local, ins, ids, group)
+    state0 = _copy_state(state)
+    tries = [i for i in range(len(secs)) if sched[i]]
+
+    def try_all(use_bounds: bool):
+        lo = np.full((len(secs), M_LAST), np.iinfo(np.uint32).max, np.uint32)
+        hi = lo.copy()
+        prev = so.fqz5_set_trial_prune(0)     # pruning needs a whole trial window per try
+        try:
+            for ch in _chunks(tries, ins, chunk_bytes):
+                part = [secs[i] for i in ch]
+                if use_bounds:
+                    lo[ch], hi[ch] = sections_try_bounds(part, sched[ch])
+                else:
+                    lo[ch] = hi[ch] = sections_try(part, sched[ch])
+        finally:
+            so.fqz5_set_trial_prune(prev)
+        return lo, hi
+
+    # First the fqz / sequence-model candidates' size intervals only (no
+    # range chains): when they separate the candidates of every decision
+    # the trial makes, the winners are coded once at commit; else the tries
+    # run again with exact sizes.
+    bounds = bounds and bounds_usable(g_ids0, sched_all, state, final=True)
+    lo, hi = try_all(bounds)
+    g_sizes, g_ins, g_ids, off = exchange_sizes(lo, ins, ids, group)
     tried = np.zeros(len(g_ids), np.uint32)
     meth_all = trial_replay(g_ids, g_ins, g_sizes, avail, state, tried)
+    if bounds:
+        g_hi = exchange_sizes(hi, ins, ids, group)[0]
+        # every rank sees the same rows, so every rank decides the same
+        import sys
+        single = group is None or _world(group)[0] == 1
+        ok = False
+        for _ in range(M_LAST):
+            why, pairs = [], set()
+            ok = trial_decided(g_sizes, g_hi, g_ids, g_ins, tried, sched_all, state0,
+                               final=True, why=why, open_pairs=pairs)
+            if ok or not pairs or not single:
+                break
+            # exact sizes for the candidates that leave a decision open,
+            # then the replay again from the entry state
+            print(f"[sections] size intervals leave a trial decision open ({why[0]}): "
+                  f"{len(pairs)} candidates coded exactly", file=sys.stderr, flush=True)
+            refine_exact(secs, lo, hi, sorted(pairs), ins, chunk_bytes)
+            g_sizes, g_hi = lo, hi
+            C.memmove(C.byref(state), C.byref(state0), C.sizeof(TrialState))
+            tried = np.zeros(len(g_ids), np.uint32)
+            meth_all = trial_replay(g_ids, g_ins, g_sizes, avail, state, tried)
+        global last_bounds_decided
+        last_bounds_decided = ok
+        if not ok:
+            print(f"[sections] size intervals do not decide the trial ({why[0] if why else ''}): "
+                  "trying again with exact sizes", file=sys.stderr, flush=True)
+            C.memmove(C.byref(state), C.byref(state0), C.sizeof(TrialState))
+            lo, _ = try_all(False)
+            g_sizes, g_ins, g_ids, off = exchange_sizes(lo, ins, ids, group)
+            tried = np.zeros(len(g_ids), np.uint32)
+            meth_all = trial_replay(g_ids, g_ins, g_sizes, avail, state, tried)
     meth = meth_all[off:off + len(secs)]
     res = []
     for ch in _chunks(range(len(secs)), ins, max(commit_bytes, chunk_bytes)):
@@ -421,7 +637,8 @@ def work_share(methods: list[int], world: int, rank: int) -> int:
 def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
                   state: TrialState, group=None, bounded: bool = False,
                   chunk_bytes: int = 600_000_000, prune: bool = True,
-                  commit_bytes: int = 2_400_000_000):
+                  commit_bytes: int = 2_400_000_000, bounds: bool = True,
+                  final: bool = False):
     """Code the sections of consecutive blocks (file order) over the ranks of
     `group`; every rank passes the same section ids / input sizes / owners,
     its Section for every section it holds the data of (None elsewhere) and
@@ -438,7 +655,8 @@ def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
 
     bounded: the -7/-9 path of encode_run_bounded (tries chunked by
     chunk_bytes, no pruning, every section coded again at commit, in chunks
-    of commit_bytes).
+    of commit_bytes; with `bounds`, the work candidates' size intervals
+    first, as in encode_run_bounded; final: the input ends with this call).
     Returns (results: SectionResult per section or None when not owned,
     methods of every section, sizes)."""
     ws, rk = _world(group)
@@ -473,15 +691,29 @@ def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
         if secs[i] is None:
             raise ValueError(f"section {i}: rank {rk} needs its data")
     local = np.full((n, M_LAST), np.iinfo(np.uint32).max, np.uint32)
+    hi_local = None
     so = _load()
-    if bounded:
+    state0 = _copy_state(state)
+    use_bounds = bounded and bounds and bounds_usable(ids, sched, state, final)
+
+    def bounded_tries(with_bounds: bool):
+        lo = np.full((n, M_LAST), np.iinfo(np.uint32).max, np.uint32)
+        hi = lo.copy()
         prev = so.fqz5_set_trial_prune(0)
         try:
             tried_rows = [i for i in rows if masks[i]]
             for ch in _chunks(tried_rows, ins, chunk_bytes):
-                local[ch] = sections_try([secs[i] for i in ch], masks[ch])
+                part = [secs[i] for i in ch]
+                if with_bounds:
+                    lo[ch], hi[ch] = sections_try_bounds(part, masks[ch])
+                else:
+                    lo[ch] = hi[ch] = sections_try(part, masks[ch])
         finally:
             so.fqz5_set_trial_prune(prev)
+        return lo, hi
+
+    if bounded:
+        local, hi_local = bounded_tries(use_bounds)
     else:
         # pruning of a family: its trial window whole in this call
         for fam in (FQZ_MASK, SEQ_MASK):
@@ -497,6 +729,26 @@ def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
     sizes = allreduce_min(local, group)
     tried = np.zeros(n, np.uint32)
     meth = trial_replay(ids, ins, sizes, av, state, tried)
+    if use_bounds:
+        global last_bounds_decided
+        hi_all = allreduce_min(hi_local, group)
+        for _ in range(M_LAST):
+            pairs = set()
+            last_bounds_decided = trial_decided(sizes, hi_all, ids, ins, tried, sched, state0,
+                                                final, open_pairs=pairs)
+            if last_bounds_decided or not pairs or ws > 1:
+                break
+            # one rank: exact sizes for the candidates left open, replay again
+            refine_exact(secs, sizes, hi_all, sorted(pairs), ins, chunk_bytes)
+            C.memmove(C.byref(state), C.byref(state0), C.sizeof(TrialState))
+            tried = np.zeros(n, np.uint32)
+            meth = trial_replay(ids, ins, sizes, av, state, tried)
+        if not last_bounds_decided:        # the intervals overlap: exact sizes
+            C.memmove(C.byref(state), C.byref(state0), C.sizeof(TrialState))
+            local, _ = bounded_tries(False)
+            sizes = allreduce_min(local, group)
+            tried = np.zeros(n, np.uint32)
+            meth = trial_replay(ids, ins, sizes, av, state, tried)
     res: list = [None] * n
     mine = [i for i in rows if owner[i] == rk]
     if bounded:

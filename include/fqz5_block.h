@@ -116,6 +116,20 @@ int fqz5_sections_commit(const fqz5_section *secs, int n, const int32_t *methods
  * section kind); otherwise the call does not prune.  Returns the previous
  * setting. */
 int fqz5_set_trial_prune(int on);
+/* Bounds-only tries for the large-block presets (encode_run_bounded): with
+ * on = 1 every fqz and sequence-model candidate of a fqz5_sections_try skips
+ * its range chain; `sizes` then holds its size lower bound (entropy of its
+ * events) and fqz5_sections_try_upper its upper bound (entropy plus the
+ * coder's slack, -log2(1 - total / 2^24) per event), every other entry
+ * equal in both.  The caller decides the trial when the intervals separate
+ * the candidates (fqzcomp5.c:1972-2127: per section the first smallest
+ * size; the trial window's smallest (csize + 1) / usize, :1913-1924) and
+ * commits the winners; otherwise it tries again with on = 0.  Returns the
+ * previous setting. */
+int fqz5_set_trial_bounds(int on);
+/* The upper-bound sizes matrix (nsec * FQZ5_M_LAST) of this thread's last
+ * fqz5_sections_try, which had `nsec` sections; -1 if there was none. */
+int fqz5_sections_try_upper(uint32_t *upper, int nsec);
 /* {fqz candidates tried, of which pruned} since the library was loaded. */
 void fqz5_trial_counts(uint64_t *out2);
 

@@ -121,14 +121,17 @@ def test_arena_constant_over_steps():
     assert sizes[1:] == sizes[1:2] * (len(sizes) - 1), sizes
 
 
+@pytest.mark.parametrize("bounds", [True, False])
 @pytest.mark.parametrize("level,kind,nreads,blk", [(7, "ont", 500, 1_500_000),
                                                    (9, "hifi", 600, 1_500_000)])
-def test_bounded_run_equals_run(level, kind, nreads, blk):
+def test_bounded_run_equals_run(level, kind, nreads, blk, bounds):
     """encode_run_bounded (the trial a section at a time, then every section
     coded with its one method, for the -7/-9 block sizes) makes the choices
     and the bytes of encode_run; chunk_bytes small enough that every chunk
     holds one or two sections; the commit in one chunk (-7) or in chunks
-    as small as the tries' (-9)."""
+    as small as the tries' (-9).  bounds: the tries give the fqz / sequence
+    model candidates' size intervals only, decided by trial_decided (or
+    tried again exactly)."""
     reads = GEN[kind](nreads, seed=13)
     blocks = synth.split_blocks(reads, blk)
     assert len(blocks) >= 4
@@ -141,7 +144,9 @@ def test_bounded_run_equals_run(level, kind, nreads, blk):
     res_b, meth_b, _, tried_b, _ = S.encode_run_bounded(run_b.enc_secs(), av, S.new_state(),
                                                         chunk_bytes=2 * blk // 3,
                                                         commit_bytes=(2 * blk // 3 if level == 9
-                                                                      else 2_400_000_000))
+                                                                      else 2_400_000_000),
+                                                        bounds=bounds)
+    print(f"-{level} {kind}: intervals decided the trial: {S.last_bounds_decided}")
     assert all(r.status == 0 for r in res_b)
     assert list(meth_a) == list(meth_b)
     assert list(tried_a) == list(tried_b)

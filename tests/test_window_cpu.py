@@ -48,8 +48,19 @@ def _fake_size(i: int, m: int, n: int) -> int:
 class _Fake:
     """Stands in for the GPU calls: records what was tried / committed."""
 
-    def __init__(self):
+    def __init__(self, width: int = 0):
         self.tried, self.committed, self.sess = [], [], None
+        self.width = width      # bounds tries: fqz / sequence-model interval width
+
+    def sections_try_bounds(self, secs, masks):
+        lo = self.sections_try(secs, masks)
+        hi = lo.copy()
+        iv = [m for m in range(S.M_LAST) if (1 << m) & (S.FQZ_MASK | S.SEQ_MASK)]
+        sel = lo[:, iv] != 0xFFFFFFFF
+        v = lo[:, iv].astype(np.int64)
+        lo[:, iv] = np.where(sel, np.maximum(v - self.width, 1), v).astype(np.uint32)
+        hi[:, iv] = np.where(sel, v + self.width, v).astype(np.uint32)
+        return lo, hi
 
     def sections_try(self, secs, masks):
         out = np.full((len(secs), S.M_LAST), 0xFFFFFFFF, np.uint32)
@@ -74,24 +85,27 @@ class _Fake:
         return res
 
 
-def _run(world: int, rank: int, nblocks: int, level: int, bounded: bool):
+def _run(world: int, rank: int, nblocks: int, level: int, bounded: bool, width: int = 0,
+         bounds: bool = True):
     ids, ins = _layout(nblocks, level)
     n = len(ids)
     secs = []
     for i in range(n):   # Section.nrec carries the section index for the fake
         secs.append(S.Section(None, None, int(ins[i]), 0, 0, int(ids[i]), None, None, i, None))
     owner = np.repeat((np.arange(nblocks) * world) // nblocks, 3)
-    fake = _Fake()
+    fake = _Fake(width)
     S.sections_try, S.sections_commit = fake.sections_try, fake.sections_commit
+    S.sections_try_bounds = fake.sections_try_bounds
     st = S.new_state()
     group = None
     if world > 1:
         import torch.distributed as dist
         group = dist.group.WORLD
     res, meth, sizes = S.encode_window(secs, ids, ins, owner, S.masks(level, full=True), st,
-                                       group, bounded=bounded)
+                                       group, bounded=bounded, bounds=bounds)
     return dict(meth=meth.tolist(), tried=fake.tried, committed=fake.committed,
-                owned=[i for i in range(n) if res[i] is not None])
+                owned=[i for i in range(n) if res[i] is not None],
+                decided=S.last_bounds_decided)
 
 
 def _worker(rank, world, port, q, args):
@@ -218,3 +232,45 @@ def test_mismatched_sizes_refused(cli_file):
     struct.pack_into("<I", data, s + 8, zlib.crc32(bytes(data[s + 12:e])))
     with pytest.raises(ValueError, match="quality and sequence"):
         fqz5file.check_blocks(bytes(data))
+
+
+@pytest.mark.parametrize("width", [0, 5, 20000])
+def test_bounded_intervals_choose_as_exact_sizes(width):
+    """The -7 bounded window with interval tries (every fqz / sequence-model
+    size known to +-width only) picks the methods of exact sizes: decided
+    from the intervals when they separate the candidates, else the open
+    candidates are coded exactly and the trial replayed (width 20000: the
+    intervals overlap)."""
+    exact = _run(1, 0, 5, 7, True, bounds=False)
+    got = _run(1, 0, 5, 7, True, width=width)
+    assert got["meth"] == exact["meth"]
+    assert sorted(got["committed"]) == sorted(exact["committed"])
+    assert got["decided"]
+    work = lambda t: [x for x in t if (1 << x[1]) & S.WORK_MASK]
+    if width == 0:       # every work candidate tried once
+        assert sorted(work(got["tried"])) == sorted(set(work(got["tried"])))
+    if width == 20000:   # some again, exactly
+        assert len(work(got["tried"])) > len(set(work(got["tried"])))
+
+
+def test_bounded_intervals_two_ranks_fall_back():
+    """Over two ranks overlapping intervals send every rank back to exact
+    tries; the choices still equal one process's exact ones."""
+    exact = _run(1, 0, 5, 7, True, bounds=False)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, (5, 7, True, 20000)))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, out = q.get(timeout=120)
+        got[r] = out
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0]["meth"] == got[1]["meth"] == exact["meth"]
+    assert not got[0]["decided"] and not got[1]["decided"]
