@@ -307,6 +307,17 @@ int fqz5_set_trial_prune(int on) { return g_prune.exchange(on ? 1 : 0); }
 
 int fqz5_set_trial_bounds(int on) { return g_bounds.exchange(on ? 1 : 0); }
 
+int fqz5_arenas_release(void) {
+    try {
+        t_sess = TrySession();
+        gpu_release_all();
+        return 0;
+    } catch (const std::exception &e) {
+        fqz5_set_error(e.what());
+        return -1;
+    }
+}
+
 int fqz5_sections_try_upper(uint32_t *upper, int nsec) {
     if (nsec < 0 || size_t(nsec) * FQZ5_M_LAST != t_sess.upper.size()) {
         fqz5_set_error("fqz5_sections_try_upper: no try of that many sections on this thread");

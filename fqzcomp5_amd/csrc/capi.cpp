@@ -102,6 +102,20 @@ void gpu_aux_reset_all() {
     for (auto &a : g_aux)
         if (a) a->reset();
 }
+void gpu_release_all() {
+    if (g_ctx) {
+        g_ctx->sync();
+        g_ctx->arena.release();
+        g_ctx->staging.reset();
+    }
+    for (auto &a : g_aux)
+        if (a) {
+            a->sync();
+            FQZ5_HIP(hipStreamSynchronize(a->stream2));
+            a->arena.release();
+            a->staging.reset();
+        }
+}
 static uint64_t arena_bytes() {
     uint64_t t = g_ctx ? g_ctx->arena.bytes() : 0;
     for (auto &a : g_aux) t += a ? a->arena.bytes() : 0;

@@ -60,6 +60,12 @@ class DevArena {
         for (auto &c : chunks_) c.used = 0;
         cur_ = 0;
     }
+    // give every chunk back to the device (nothing may still use them)
+    void release() {
+        for (auto &c : chunks_) (void)hipFree(c.base);
+        chunks_.clear();
+        cur_ = 0;
+    }
     // device bytes held (all chunks, used or not)
     size_t bytes() const {
         size_t t = 0;
@@ -356,5 +362,9 @@ constexpr int AUX_CTXS = 11;  // 0 fqz, 1 LZP3, 2..7 sequence models, 8 stripes,
 constexpr int AUX_SEQ0 = 2, AUX_NSEQ = 6, AUX_STRIPES = 8, AUX_NAMES = 9, AUX_PLAIN = 10;
 GpuCtx &gpu_aux(int k = 0);
 void gpu_aux_reset_all();
+// After synchronising them, free the device arenas of the calling thread's
+// context and of its helper contexts (their high-water marks otherwise stay
+// held: -7 tries and commits on different contexts would add them up).
+void gpu_release_all();
 
 }  // namespace fqz5

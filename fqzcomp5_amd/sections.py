@@ -130,6 +130,8 @@ def _load():
         so.fqz5_set_trial_prune.argtypes = [C.c_int]
         so.fqz5_set_trial_bounds.restype = C.c_int
         so.fqz5_set_trial_bounds.argtypes = [C.c_int]
+        so.fqz5_arenas_release.restype = C.c_int
+        so.fqz5_arenas_release.argtypes = []
         so.fqz5_sections_try_upper.restype = C.c_int
         so.fqz5_sections_try_upper.argtypes = [C.POINTER(C.c_uint32), C.c_int]
         so.fqz5_trial_counts.argtypes = [C.POINTER(C.c_uint64)]
@@ -343,9 +345,12 @@ def refine_exact(secs: list, lo: np.ndarray, hi: np.ndarray, pairs, ins, chunk_b
     for i, m in pairs:
         want[i] = want.get(i, 0) | (1 << m)
     rows = sorted(want)
+    # a chunk's device memory goes with its work candidates (~60 B per input
+    # byte each); a full try chunk holds ~5 of them per chunk_bytes
+    cost = {i: int(ins[i]) * max(1, bin(want[i] & WORK_MASK).count("1")) for i in rows}
     prev = so.fqz5_set_trial_prune(0)
     try:
-        for ch in _chunks(rows, ins, chunk_bytes):
+        for ch in _chunks(rows, cost, 5 * chunk_bytes):
             got = sections_try([secs[i] for i in ch], np.array([want[i] for i in ch], np.uint32))
             for r, i in enumerate(ch):
                 for m in range(M_LAST):
@@ -594,6 +599,10 @@ def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState
             tried = np.zeros(len(g_ids), np.uint32)
             meth_all = trial_replay(g_ids, g_ins, g_sizes, avail, state, tried)
     meth = meth_all[off:off + len(secs)]
+    # the tries' arenas (helper contexts) back to the device before the
+    # commit's candidates take theirs
+    if so.fqz5_arenas_release():
+        raise _lib.NativeError("fqz5_arenas_release: " + _lib.last_error())
     res = []
     for ch in _chunks(range(len(secs)), ins, max(commit_bytes, chunk_bytes)):
         part = [secs[i] for i in ch]
@@ -752,6 +761,8 @@ def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
     res: list = [None] * n
     mine = [i for i in rows if owner[i] == rk]
     if bounded:
+        if so.fqz5_arenas_release():
+            raise _lib.NativeError("fqz5_arenas_release: " + _lib.last_error())
         for ch in _chunks(mine, ins, max(commit_bytes, chunk_bytes)):
             part = [secs[i] for i in ch]
             sections_try(part, np.zeros(len(ch), np.uint32))    # an empty session

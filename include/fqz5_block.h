@@ -130,6 +130,11 @@ int fqz5_set_trial_bounds(int on);
 /* The upper-bound sizes matrix (nsec * FQZ5_M_LAST) of this thread's last
  * fqz5_sections_try, which had `nsec` sections; -1 if there was none. */
 int fqz5_sections_try_upper(uint32_t *upper, int nsec);
+/* End this thread's try session (its candidates are dropped) and free the
+ * device arenas of the thread's GPU context and helper contexts, after
+ * synchronising them.  The large-block path calls it between its tries and
+ * its commit, whose candidates run on other contexts. */
+int fqz5_arenas_release(void);
 /* {fqz candidates tried, of which pruned} since the library was loaded. */
 void fqz5_trial_counts(uint64_t *out2);
 
