@@ -723,7 +723,7 @@ void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vecto
         if (W.clen > W.room) continue;   // (cannot happen: the bound covers the coder)
         if (W.lb > uint64_t(W.hdr.size()) + W.clen)   // the entropy bound is a theorem
             throw std::runtime_error("fqz: size below its entropy bound");
-        if (W.ub < uint64_t(W.hdr.size()) + W.clen)   // and so is the slack bound
+        if (W.ub && W.ub < uint64_t(W.hdr.size()) + W.clen)   // and so is the slack bound (0: none, serial path)
             throw std::runtime_error("fqz: size above its upper bound");
         Piece h;
         h.host = W.hdr;
