@@ -112,6 +112,7 @@ _bound = False
 
 TRIAL_WINDOW = 3      # FQZ5_METRICS_TRIAL (fqzcomp5.c:152)
 last_bounds_decided = None   # whether the last bounded run's intervals decided its trial
+bounds_widen = 0             # tests: bytes added to every interval's upper end
 
 
 def trial_counts() -> tuple[int, int]:
@@ -336,6 +337,38 @@ def trial_decided(lo: np.ndarray, hi: np.ndarray, ids, ins, tried, sched, state_
     return ok
 
 
+def refine_session(secs: list, ids, sched, lo: np.ndarray, hi: np.ndarray, pairs, ins,
+                   chunk_bytes: int) -> bool:
+    """refine_exact as one try session over every section, which the commit
+    can then use: the open pairs exactly, and each section outside the trial
+    of a kind with open candidates tries those candidates too (its method is
+    the window's pick, one of them when it is open), so a decided trial
+    commits with the winners already coded.  Returns False, trying nothing,
+    when the session would not fit the device memory budget (~60 B per input
+    byte and work candidate, 5 x chunk_bytes of such bytes)."""
+    want, kinds = {}, {}
+    for i, m in pairs:
+        want[i] = want.get(i, 0) | (1 << m)
+        kinds[int(ids[i])] = kinds.get(int(ids[i]), 0) | (1 << m)
+    for j in range(len(secs)):
+        if not sched[j] and int(ids[j]) in kinds:
+            want[j] = want.get(j, 0) | kinds[int(ids[j])]
+    cost = sum(int(ins[i]) * max(1, bin(want[i] & WORK_MASK).count("1")) for i in want)
+    if cost > 5 * chunk_bytes:
+        return False
+    so = _load()
+    if so.fqz5_arenas_release():
+        raise _lib.NativeError("fqz5_arenas_release: " + _lib.last_error())
+    prev = so.fqz5_set_trial_prune(0)
+    try:
+        got = sections_try(secs, np.array([want.get(i, 0) for i in range(len(secs))], np.uint32))
+    finally:
+        so.fqz5_set_trial_prune(prev)
+    for i, m in pairs:
+        lo[i, m] = hi[i, m] = got[i, m]
+    return True
+
+
 def refine_exact(secs: list, lo: np.ndarray, hi: np.ndarray, pairs, ins, chunk_bytes: int):
     """Exact sizes for the (section, method) pairs whose intervals left a
     trial decision open: those sections try just those methods with their
@@ -505,7 +538,8 @@ def _chunks(rows, sizes, budget: int):
 
 def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState,
                        group=None, chunk_bytes: int = 600_000_000,
-                       commit_bytes: int = 2_400_000_000, bounds: bool = True):
+                       commit_bytes: int = 2_400_000_000, bounds: bool = True,
+                       merge_commit: bool = True):
     """encode_run for the large-block presets (-7: 500 MB, -9: 1 GB blocks),
     in bounded device memory: the same choices and bytes, at the cost of
     coding each trial section's winner twice.
@@ -532,12 +566,15 @@ def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState
     exact sizes), so the choices are those of exact sizes.  The returned
     sizes then hold the intervals' lower ends for those candidates.  The
     call is taken to hold the whole input (a decision left for a later call
-    would read interval sums from the state)."""
+    would read interval sums from the state).  merge_commit: on one rank, the
+    refinement of open decisions is one session over every section
+    (refine_session) that the commit then reuses."""
     ins = np.array([s.in_size for s in secs], np.uint32)
     ids = np.array([s.sec for s in secs], np.int32)
     blank = np.zeros((len(secs), M_LAST), np.uint32)
     _, _, g_ids0, off = exchange_sizes(blank, ins, ids, group)
     sched_all = trial_schedule(g_ids0, avail, state)
+    session = False
     sched = sched_all[off:off + len(secs)]
     so = _load()
     state0 = _copy_state(state)
@@ -556,6 +593,9 @@ def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState
                     lo[ch] = hi[ch] = sections_try(part, sched[ch])
         finally:
             so.fqz5_set_trial_prune(prev)
+        if use_bounds and bounds_widen:        # tests: leave decisions open
+            iv = lo != hi
+            hi[iv] = np.minimum(hi[iv].astype(np.int64) + bounds_widen, 2**32 - 2).astype(np.uint32)
         return lo, hi
 
     # First the fqz / sequence-model candidates' size intervals only (no
@@ -573,6 +613,7 @@ def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState
         import sys
         single = group is None or _world(group)[0] == 1
         ok = False
+        session = False      # the last try session covers every section
         for _ in range(M_LAST):
             why, pairs = [], set()
             ok = trial_decided(g_sizes, g_hi, g_ids, g_ins, tried, sched_all, state0,
@@ -583,7 +624,10 @@ def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState
             # then the replay again from the entry state
             print(f"[sections] size intervals leave a trial decision open ({why[0]}): "
                   f"{len(pairs)} candidates coded exactly", file=sys.stderr, flush=True)
-            refine_exact(secs, lo, hi, sorted(pairs), ins, chunk_bytes)
+            session = merge_commit and not session and refine_session(
+                secs, ids, sched, lo, hi, sorted(pairs), ins, chunk_bytes)
+            if not session:
+                refine_exact(secs, lo, hi, sorted(pairs), ins, chunk_bytes)
             g_sizes, g_hi = lo, hi
             C.memmove(C.byref(state), C.byref(state0), C.sizeof(TrialState))
             tried = np.zeros(len(g_ids), np.uint32)
@@ -599,6 +643,10 @@ def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState
             tried = np.zeros(len(g_ids), np.uint32)
             meth_all = trial_replay(g_ids, g_ins, g_sizes, avail, state, tried)
     meth = meth_all[off:off + len(secs)]
+    if bounds and last_bounds_decided and session:
+        # the refinement's session tried every section's possible winners:
+        # the commit codes the rest (late) and reuses those
+        return sections_commit(secs, meth), meth_all, g_sizes, tried, off
     # the tries' arenas (helper contexts) back to the device before the
     # commit's candidates take theirs
     if so.fqz5_arenas_release():

@@ -121,7 +121,7 @@ def test_arena_constant_over_steps():
     assert sizes[1:] == sizes[1:2] * (len(sizes) - 1), sizes
 
 
-@pytest.mark.parametrize("bounds", [True, False])
+@pytest.mark.parametrize("bounds", [True, False, "widen"])
 @pytest.mark.parametrize("level,kind,nreads,blk", [(7, "ont", 500, 1_500_000),
                                                    (9, "hifi", 600, 1_500_000)])
 def test_bounded_run_equals_run(level, kind, nreads, blk, bounds):
@@ -131,7 +131,9 @@ def test_bounded_run_equals_run(level, kind, nreads, blk, bounds):
     holds one or two sections; the commit in one chunk (-7) or in chunks
     as small as the tries' (-9).  bounds: the tries give the fqz / sequence
     model candidates' size intervals only, decided by trial_decided (or
-    tried again exactly)."""
+    tried again exactly).  "widen": every interval widened by 10 MB, so every
+    decision is left open and refined by one session over all sections that
+    the commit reuses (refine_session)."""
     reads = GEN[kind](nreads, seed=13)
     blocks = synth.split_blocks(reads, blk)
     assert len(blocks) >= 4
@@ -141,11 +143,16 @@ def test_bounded_run_equals_run(level, kind, nreads, blk, bounds):
     res_a, meth_a, _, tried_a, _ = S.encode_run(run.enc_secs(), av, S.new_state())
     got_a = [run.chosen(res_a, i) for i in range(len(res_a))]
     run_b = S.Run(reads, blocks, dev, names=False)
-    res_b, meth_b, _, tried_b, _ = S.encode_run_bounded(run_b.enc_secs(), av, S.new_state(),
-                                                        chunk_bytes=2 * blk // 3,
+    S.bounds_widen = 10_000_000 if bounds == "widen" else 0
+    try:
+        res_b, meth_b, _, tried_b, _ = S.encode_run_bounded(run_b.enc_secs(), av, S.new_state(),
+                                                        chunk_bytes=(50_000_000 if bounds == "widen"
+                                                                     else 2 * blk // 3),
                                                         commit_bytes=(2 * blk // 3 if level == 9
                                                                       else 2_400_000_000),
-                                                        bounds=bounds)
+                                                        bounds=bool(bounds))
+    finally:
+        S.bounds_widen = 0
     print(f"-{level} {kind}: intervals decided the trial: {S.last_bounds_decided}")
     assert all(r.status == 0 for r in res_b)
     assert list(meth_a) == list(meth_b)
