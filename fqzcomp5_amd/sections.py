@@ -793,10 +793,22 @@ def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
             pairs = set()
             last_bounds_decided = trial_decided(sizes, hi_all, ids, ins, tried, sched, state0,
                                                 final, open_pairs=pairs)
-            if last_bounds_decided or not pairs or ws > 1:
+            if last_bounds_decided or not pairs:
                 break
-            # one rank: exact sizes for the candidates left open, replay again
-            refine_exact(secs, sizes, hi_all, sorted(pairs), ins, chunk_bytes)
+            # exact sizes for the candidates left open (every rank holds the
+            # trial sections; the pairs are dealt out over the ranks and the
+            # sizes combined by the same element-wise minimum), replay again
+            held = [pr for pr in sorted(pairs) if secs[pr[0]] is not None]
+            if ws > 1 and len(held) != len(pairs):
+                break
+            mine_p = held[rk::ws]
+            ex = np.full((n, M_LAST), np.iinfo(np.uint32).max, np.uint32)
+            ex_hi = ex.copy()
+            if mine_p:
+                refine_exact(secs, ex, ex_hi, mine_p, ins, chunk_bytes)
+            ex = allreduce_min(ex, group)
+            for i, m in pairs:
+                sizes[i, m] = hi_all[i, m] = ex[i, m]
             C.memmove(C.byref(state), C.byref(state0), C.sizeof(TrialState))
             tried = np.zeros(n, np.uint32)
             meth = trial_replay(ids, ins, sizes, av, state, tried)

@@ -253,9 +253,10 @@ def test_bounded_intervals_choose_as_exact_sizes(width):
         assert len(work(got["tried"])) > len(set(work(got["tried"])))
 
 
-def test_bounded_intervals_two_ranks_fall_back():
-    """Over two ranks overlapping intervals send every rank back to exact
-    tries; the choices still equal one process's exact ones."""
+def test_bounded_intervals_two_ranks_refine():
+    """Over two ranks the candidates that overlapping intervals leave open
+    are coded exactly, split over the ranks; the choices equal one process's
+    exact ones."""
     exact = _run(1, 0, 5, 7, True, bounds=False)
     world = 2
     ctx = mp.get_context("spawn")
@@ -273,4 +274,9 @@ def test_bounded_intervals_two_ranks_fall_back():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got[0]["meth"] == got[1]["meth"] == exact["meth"]
-    assert not got[0]["decided"] and not got[1]["decided"]
+    assert got[0]["decided"] and got[1]["decided"]
+    # some work candidates were coded twice over the ranks (interval, then
+    # exact), each exact one on one rank only
+    work = lambda t: [x for x in t if (1 << x[1]) & S.WORK_MASK]
+    w0, w1 = work(got[0]["tried"]), work(got[1]["tried"])
+    assert len(w0) + len(w1) > len(set(w0) | set(w1))
