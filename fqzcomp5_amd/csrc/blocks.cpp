@@ -150,6 +150,7 @@ int fqz5_block_parse(const uint8_t *d_block, uint64_t avail, fqz5_block_view *v,
         v->name_size = 9 + c_len;
         uint64_t o = 12ull + 9 + c_len;
         uint8_t lh[6];
+        uint64_t lens_sum = 0;
         get(o, 1, lh);
         if (lh[0] > 0) {                               // fixed length (:2385-2395)
             const uint64_t k = std::min<uint64_t>(5, end - std::min(end, o + 1));
@@ -160,6 +161,7 @@ int fqz5_block_parse(const uint8_t *d_block, uint64_t avail, fqz5_block_view *v,
             v->fixed_len = int32_t(fl);
             if (lens)
                 for (uint32_t i = 0; i < std::min(v->nrec, lens_cap); i++) lens[i] = fl;
+            lens_sum = uint64_t(fl) * v->nrec;
             o += 1 + uint64_t(vl);
         } else {                                       // [0][u32 blen][varints] (:2396-2408)
             uint8_t b4[4];
@@ -174,6 +176,7 @@ int fqz5_block_parse(const uint8_t *d_block, uint64_t avail, fqz5_block_view *v,
                 const int vl = varint_get(p, pe, &x);
                 if (!vl) throw GpuError("fqz5_block_parse: bad length varint");
                 if (lens && i < lens_cap) lens[i] = x;
+                lens_sum += x;
                 p += vl;
             }
             o += uint64_t(p - vb.data());
@@ -192,6 +195,14 @@ int fqz5_block_parse(const uint8_t *d_block, uint64_t avail, fqz5_block_view *v,
         v->qual_size = 9 + c_len;
         o += 9ull + c_len;
         if (o > end) throw GpuError("fqz5_block_parse: sections past the block end");
+        // the decoders write u_len bytes into outputs sized from these
+        // fields: a quality section (not FASTA's 9 zero bytes) decodes to one
+        // byte per base, and the record lengths cover the bases exactly
+        const bool fasta = v->qual_ulen == 0 && v->qual_size == 9;
+        if (!fasta && v->qual_ulen != v->seq_ulen)
+            throw GpuError("fqz5_block_parse: quality and sequence sizes differ");
+        if (lens_sum != v->seq_ulen)
+            throw GpuError("fqz5_block_parse: record lengths do not sum to the bases");
         g.reset();
         return 0;
     } catch (const std::exception &e) {

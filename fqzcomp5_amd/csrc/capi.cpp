@@ -89,6 +89,17 @@ bool hedge_chains() {
     return v != 0;
 }
 
+static std::atomic<int> g_dec_small{-1};
+bool small_decoder_on() {
+    int v = g_dec_small.load();
+    if (v < 0) {
+        const char *e = std::getenv("FQZ5_DEC_SMALL");
+        v = e && e[0] == '1' ? 1 : 0;
+        g_dec_small.store(v);
+    }
+    return v != 0;
+}
+
 // The calling thread's helper contexts: their own streams and arenas, for
 // work the thread hands to helper threads to run beside its own
 // (fqz5_sections_try: LZP3, fqz and sequence-model candidates beside the
@@ -382,6 +393,17 @@ const char *fqz5_last_error(void) { return g_err.c_str(); }
 uint64_t fqz5_arena_bytes(void) { return arena_bytes(); }
 
 unsigned fqz5_set_hot_min(unsigned min_events) { return fqz_set_hot_min(min_events); }
+
+void fqz5_fqz_dec_counts(uint64_t *out2) {
+    out2[0] = fqz_dec_blocks(false);
+    out2[1] = fqz_dec_blocks(true);
+}
+
+int fqz5_set_dec_small(int on) {
+    const int prev = small_decoder_on() ? 1 : 0;
+    g_dec_small.store(on ? 1 : 0);
+    return prev;
+}
 
 int fqz5_set_hedge(int on) {
     const int prev = hedge_chains() ? 1 : 0;

@@ -1,4 +1,3 @@
-#include <atomic>
 // fqz_codec.cpp — fqz_compress / fqz_decompress on the GPU
 // (htscodecs fqzcomp_qual.c:1008-1646, fork ABI).
 //
@@ -9,6 +8,7 @@
 // serial model + range-coder kernel writes the stream.  Decode parses the
 // parameters on the host and runs the serial decode kernel.
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -769,11 +769,15 @@ uint8_t *fqz_encode_gpu(int vers, fqz_slice *s, const uint8_t *in, size_t n, siz
     return out;
 }
 
+static std::atomic<uint64_t> g_dec_blocks[2];
+uint64_t fqz_dec_blocks(bool small) { return g_dec_blocks[small ? 1 : 0].load(); }
+
 struct FqzDecReq::Work {
     Global G;
     FqzDecJob D{};
     int ne = 1, map_mode = 0;
     bool seq_ctx = false, qid = true, dedup = false, rev = false;
+    bool small = false, dt = false;   // the small-alphabet decoder; delta terms
     uint32_t total = 0, cap = 0;
     int32_t st = 0;
 };
@@ -840,7 +844,7 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
         g.memset0(D.counts, 32 * sizeof(uint32_t));
         D.ment = fqz_dec_model_bytes(nlive);
         D.nsets = FQZ_DEC_CACHE_BYTES / D.ment;
-        D.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * D.ment);
+        D.back = nullptr;
         if (nlive > 62) {
             D.back_hi = g.arena.alloc_n<uint32_t>(size_t(FQZ_CTX) * 64);
             D.hi_bits = g.arena.alloc_n<uint32_t>(FQZ_CTX / 32);
@@ -858,6 +862,26 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
         W.rev = (G.gflags & GF_REV) != 0;
         if (W.map_mode) W.map_mode = G.nparam > 1 ? 2 : 1;
         W.ne = nlive + 2 <= 64 ? 1 : 2;
+        // the small-alphabet decoder: <= 9 live symbols, qtab the identity on
+        // them, no sequence bases in the context (fqz_decode_small.hip)
+        bool ident = true;
+        for (const Param &pm : G.p) {
+            for (uint32_t i = 0; i < nlive; i++) ident = ident && (pm.qtab[i] & 0xffffu) == i;
+            for (int i = 0; i < 256; i++) W.dt = W.dt || pm.dtab[i] != 0;
+        }
+        W.small = small_decoder_on() && nlive <= FQZ_SMALL_MAX_LIVE && nlive >= 2 && ident && !W.seq_ctx;
+        if (W.small) {
+            D.ment = FQZ_SMALL_MODEL_BYTES;
+            D.nsets = fqz_small_sets(uint32_t(G.nparam));
+            if (const char *e = std::getenv("FQZ5_DEC_SETS"))   // tests: force misses
+                D.nsets = std::max<uint32_t>(1, std::min<uint32_t>(D.nsets, uint32_t(std::atoi(e))));
+            D.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * D.ment);
+            D.back_hi = nullptr;
+            D.hi_bits = nullptr;
+            if (const char *e = std::getenv("FQZ5_DEC_SMALL_DBG")) D.pad2 = uint32_t(std::strtoul(e, nullptr, 0));
+        } else {
+            D.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * D.ment);
+        }
         // record lists: sized for the records the caller announced, grown to
         // the byte count (every record holds at least one byte) on overflow
         W.cap = std::max<uint32_t>({D.nlengths, D.nseq, 1u}) + 1024;
@@ -865,54 +889,72 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
         live.push_back(&R);
     }
     auto launch_group = [&](const std::vector<FqzDecReq *> &rs) {
-        for (int ne = 1; ne <= 2; ne++)
-            for (int sq = 0; sq < 2; sq++)
-                for (int qi = 0; qi < 2; qi++) {
-                    std::vector<FqzDecJob> js;
-                    std::vector<uint64_t> steps;
-                    for (FqzDecReq *R : rs)
-                        if (R->w->ne == ne && int(R->w->seq_ctx) == sq && int(R->w->qid) == qi) {
-                            js.push_back(R->w->D);
-                            steps.push_back(R->w->D.n);
-                        }
-                    // hedge: copies of the long blocks on spare CUs (one
-                    // workgroup per CU: its LDS), as the rANS decode chains
-                    // (DESIGN.md section 4); a copy needs its own backing store
-                    HedgeShare share(size_t(g.cus));
-                    const bool long_block =
-                        !steps.empty() && *std::max_element(steps.begin(), steps.end()) >= (1u << 20);
-                    const std::vector<int> cp = long_block ? hedge_plan(steps, share.cus)
-                                                           : std::vector<int>(js.size(), 1);
-                    const size_t nj = js.size();
-                    for (size_t k = 0; k < nj; k++) {
-                        if (cp[k] <= 1) continue;
-                        uint32_t *done = g.arena.alloc_n<uint32_t>(1);
-                        g.memset0(done, 4);
-                        js[k].done = done;
-                        for (int c = 1; c < cp[k]; c++) {
-                            FqzDecJob J = js[k];
-                            J.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * J.ment);
-                            if (ne == 2) {
-                                J.back_hi = g.arena.alloc_n<uint32_t>(size_t(FQZ_CTX) * 64);
-                                J.hi_bits = g.arena.alloc_n<uint32_t>(FQZ_CTX / 32);
-                                g.memset0(J.hi_bits, FQZ_CTX / 8);
-                            }
-                            js.push_back(J);
-                        }
-                    }
-                    if (!js.empty()) {
-                        EventPair ev(prof_on(), g.stream);
-                        FQZ5_HIP(launch_fqz_dec(g.upload(js), int(js.size()), ne, sq != 0,
-                                                qi != 0, g.stream));
-                        ev.stop(g.stream);
-                        if (ev.on) {   // compressed bytes in, quality bytes out
-                            g.sync();
-                            double b = 0;
-                            for (size_t k = 0; k < nj; k++) b += double(js[k].in_len) + double(js[k].n);
-                            prof_add(PK_FQZ_DEC, ev.ms(), b);
-                        }
-                    }
+        // variants: the general decoder by (ne, seq, qid), then the small one
+        // by dt (variant 8 + dt)
+        for (int var = 0; var < 10; var++) {
+            const bool smallv = var >= 8;
+            const int ne = 1 + (var >> 2), sq = (var >> 1) & 1, qi = var & 1, dtv = var & 1;
+            std::vector<FqzDecJob> js;
+            std::vector<uint64_t> steps;
+            std::vector<uint32_t> live_syms;
+            for (FqzDecReq *R : rs) {
+                const FqzDecReq::Work &W = *R->w;
+                const bool mine = smallv ? (W.small && int(W.dt) == dtv)
+                                         : (!W.small && W.ne == ne && int(W.seq_ctx) == sq && int(W.qid) == qi);
+                if (mine) {
+                    js.push_back(W.D);
+                    steps.push_back(W.D.n);
+                    live_syms.push_back(uint32_t(W.G.max_sym) + 1);
                 }
+            }
+            // hedge: copies of the long blocks on spare CUs (one
+            // workgroup per CU: its LDS), as the rANS decode chains
+            // (DESIGN.md section 4); a copy needs its own backing store
+            HedgeShare share(size_t(g.cus));
+            const bool long_block =
+                !steps.empty() && *std::max_element(steps.begin(), steps.end()) >= (1u << 20);
+            const std::vector<int> cp = long_block ? hedge_plan(steps, share.cus)
+                                                   : std::vector<int>(js.size(), 1);
+            const size_t nj = js.size();
+            for (size_t k = 0; k < nj; k++) {
+                if (cp[k] <= 1) continue;
+                uint32_t *done = g.arena.alloc_n<uint32_t>(1);
+                g.memset0(done, 4);
+                js[k].done = done;
+                for (int c = 1; c < cp[k]; c++) {
+                    FqzDecJob J = js[k];
+                    J.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * J.ment);
+                    if (!smallv && ne == 2) {
+                        J.back_hi = g.arena.alloc_n<uint32_t>(size_t(FQZ_CTX) * 64);
+                        J.hi_bits = g.arena.alloc_n<uint32_t>(FQZ_CTX / 32);
+                        g.memset0(J.hi_bits, FQZ_CTX / 8);
+                    }
+                    js.push_back(J);
+                    live_syms.push_back(live_syms[k]);
+                }
+            }
+            // the small decoder's backing stores start as every context's
+            // fresh model (again on a second launch of the same block)
+            if (smallv)
+                for (size_t k = 0; k < js.size(); k++)
+                    FQZ5_HIP(launch_fqz_small_back(js[k].back, live_syms[k], g.stream));
+            if (!js.empty()) {
+                g_dec_blocks[smallv ? 1 : 0] += nj;
+                EventPair ev(prof_on(), g.stream);
+                if (smallv)
+                    FQZ5_HIP(launch_fqz_dec_small(g.upload(js), int(js.size()), dtv != 0, g.stream));
+                else
+                    FQZ5_HIP(launch_fqz_dec(g.upload(js), int(js.size()), ne, sq != 0,
+                                            qi != 0, g.stream));
+                ev.stop(g.stream);
+                if (ev.on) {   // compressed bytes in, quality bytes out
+                    g.sync();
+                    double b = 0;
+                    for (size_t k = 0; k < nj; k++) b += double(js[k].in_len) + double(js[k].n);
+                    prof_add(PK_FQZ_DEC, ev.ms(), b);
+                }
+            }
+        }
         for (FqzDecReq *R : rs) {
             FqzDecReq::Work &W = *R->w;
             FQZ5_HIP(launch_fqz_dec_fix(W.D, W.map_mode, W.dedup, W.rev, g.stream));

@@ -98,6 +98,19 @@ constexpr uint32_t fqz_dec_model_bytes(uint32_t live) {
 constexpr uint32_t FQZ_DEC_CACHE_BYTES = 163840u - 35088u - 1024u;
 constexpr uint32_t FQZ_DEC_MAX_LIVE = 126u;   // guard + slots + sentinel in two lane registers (slow path)
 
+// The small-alphabet decoder (fqz_decode_small.hip): models of at most 9
+// live symbols as 24 bytes (u16 cumulative counts of slots 1..8, the tag,
+// the total, the slots' symbols as nibbles) in a direct-mapped LDS cache
+// after FQZ_SMALL_LDS_FIXED bytes and FQZ_SMALL_PARAM_BYTES per parameter
+// block; the backing store is FQZ_CTX models of 24 bytes.
+constexpr uint32_t FQZ_SMALL_MAX_LIVE = 9u;
+constexpr uint32_t FQZ_SMALL_MODEL_BYTES = 24u;
+constexpr uint32_t FQZ_SMALL_LDS_FIXED = 10512u;
+constexpr uint32_t FQZ_SMALL_PARAM_BYTES = 2560u;
+constexpr uint32_t fqz_small_sets(uint32_t nparam) {
+    return (163840u - FQZ_SMALL_LDS_FIXED - nparam * FQZ_SMALL_PARAM_BYTES) / FQZ_SMALL_MODEL_BYTES;
+}
+
 // Parallel encoder (fqz_kernels.hip): the block becomes a list of coding
 // events (record headers and quality symbols) in stream order; events are
 // stably sorted by the model they use, every model runs over its own
@@ -180,6 +193,11 @@ hipError_t launch_fqz_encode(const FqzEncJob &j, hipStream_t s);
 hipError_t launch_fqz_dec(const FqzDecJob *d_jobs, int njobs, int ne, bool seq, bool qid,
                           hipStream_t s);
 hipError_t launch_fqz_dec_fix(const FqzDecJob &j, int map_mode, bool dups, bool revs, hipStream_t s);
+// fqz_decode_small.hip: jobs with ment = FQZ_SMALL_MODEL_BYTES, nsets <=
+// fqz_small_sets(nparam) and a backing store filled by launch_fqz_small_back;
+// dt = some parameter block has delta terms
+hipError_t launch_fqz_dec_small(const FqzDecJob *d_jobs, int njobs, bool dt, hipStream_t s);
+hipError_t launch_fqz_small_back(uint8_t *back, uint32_t live, hipStream_t s);
 hipError_t fqz_div_selftest(uint32_t *d_bad, hipStream_t s);
 
 }  // namespace fqz5

@@ -260,6 +260,10 @@ struct GpuCtx {
 // Hedged chain launches (rANS decode, fqz range chain): on unless
 // $FQZ5_NO_HEDGE is set or fqz5_set_hedge(0).
 bool hedge_chains();
+// the small-alphabet fqz decoder (fqz5_set_dec_small, $FQZ5_DEC_SMALL)
+bool small_decoder_on();
+// quality blocks decoded by the general (false) / small (true) fqz decoder
+uint64_t fqz_dec_blocks(bool small);
 // Copies of each of `jobs` chains: up to 4 while they fit one per CU.
 inline size_t hedge_copies(size_t jobs, size_t cus) {
     if (!hedge_chains() || !jobs) return 1;

@@ -610,12 +610,33 @@ def block_fields(data, s: int, e: int) -> dict:
         raise ValueError("corrupt block: block size field")
     (nu, _st, nc), p = get("<IBI", p)
     p += nc
+
+    def varint(at, end):
+        # var_get_u32 as the reference's lengths walk reads it
+        # (fqzcomp5.c:2384-2404; csrc/rans_format.hpp varint_get): the bytes
+        # it reads, not the header's own count, set the offsets
+        if at >= end:
+            raise ValueError("corrupt block: bad length varint")
+        v = n = 0
+        while True:
+            c = d[at + n]
+            n += 1
+            v = ((v << 7) | (c & 0x7f)) & 0xffffffff
+            if not (c & 0x80 and n < 6 and at + n < end):
+                return v, at + n
+
     (nb,), p = get("<B", p)
+    lens_sum = None
     if nb:
-        p += nb
+        fixed, p = varint(p, min(e, p + 5))
+        lens_sum = fixed * nrec
     else:
-        (lz,), p = get("<I", p)
-        p += lz
+        (_lz,), p = get("<I", p)
+        lens_sum = 0
+        end = min(e, p + 5 * nrec)
+        for _ in range(nrec):
+            x, p = varint(p, end)
+            lens_sum += x
     (_s1, su, sc), p = get("<BII", p)
     p += sc
     (_s2, qu, qc), p = get("<BII", p)
@@ -625,6 +646,8 @@ def block_fields(data, s: int, e: int) -> dict:
     fasta = qu == 0 and qc == 0
     if not fasta and qu != su:
         raise ValueError("corrupt block: quality and sequence sizes differ")
+    if lens_sum != su:
+        raise ValueError("corrupt block: record lengths do not sum to the bases")
     return dict(nrec=nrec, name_ulen=nu, seq_ulen=su, qual_ulen=qu, fasta=fasta)
 
 
@@ -667,6 +690,8 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges
         # from them, fqzcomp5.c:2433-2519)
         if int(ln.astype(np.uint64).sum()) != v.seq_ulen:
             raise _lib.NativeError("corrupt block: record lengths do not sum to the bases")
+        if not (v.qual_ulen == 0 and v.qual_size == 9) and v.qual_ulen != v.seq_ulen:
+            raise _lib.NativeError("corrupt block: quality and sequence sizes differ")
         views.append(v)
         lens.append(ln)
     # FASTA: a quality section of u_len 0 and c_len 0 (decode_block,

@@ -69,6 +69,8 @@ def load() -> C.CDLL:
     lib = C.CDLL(path)
     lib.fqz5_set_hedge.restype = C.c_int
     lib.fqz5_set_hedge.argtypes = [C.c_int]
+    lib.fqz5_set_dec_small.restype = C.c_int
+    lib.fqz5_set_dec_small.argtypes = [C.c_int]
     lib.fqz5_set_hot_min.restype = C.c_uint
     lib.fqz5_set_hot_min.argtypes = [C.c_uint]
     lib.rans_compress_bound_4x16.restype = C.c_uint

@@ -191,7 +191,10 @@ typedef struct {                  /* one block read back (decode_block) */
 
 /* Parse the block at d_block (device, `avail` bytes readable): the layout,
  * the CRC check and, when lens != NULL (nrec entries), the record lengths.
- * Returns 0, or -1 on a malformed block. */
+ * Returns 0, or -1 on a malformed block: a field past the block, a quality
+ * section whose u_len is not the sequence u_len (FASTA's 9 zero bytes
+ * aside), or record lengths that do not sum to the sequence u_len (the
+ * section outputs are sized from these fields). */
 int fqz5_block_parse(const uint8_t *d_block, uint64_t avail, fqz5_block_view *v,
                      uint32_t *lens, uint32_t lens_cap);
 

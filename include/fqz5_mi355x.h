@@ -284,6 +284,17 @@ unsigned fqz5_set_hot_min(unsigned min_events);
  * $FQZ5_NO_HEDGE is set), 0 = off; returns the previous setting. */
 int fqz5_set_hedge(int on);
 
+/* The fqz decoder for small alphabets (at most 9 live symbols, qtab the
+ * identity on them, no sequence context: Illumina 8-level and NovaSeq
+ * data): 24-byte models in an LDS cache of ~6 280 sets instead of the
+ * general decoder's 8 bytes per list slot.  Output bytes do not depend on
+ * it.  1 = on (default unless $FQZ5_DEC_SMALL is "0"), 0 = off; returns
+ * the previous setting. */
+int fqz5_set_dec_small(int on);
+/* Quality blocks decoded since the library was loaded: out2[0] by the
+ * general fqz decoder, out2[1] by the small-alphabet one. */
+void fqz5_fqz_dec_counts(uint64_t *out2);
+
 /* Device check of the fqz decoder's division: floor(n / t) computed as
  * (u32)fma(n, recip(t), 2^-19) for every t < 2^16 and ~2000 n each.
  * Returns the number of mismatches (0), or -1 on a device error. */

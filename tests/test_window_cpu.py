@@ -234,6 +234,52 @@ def test_mismatched_sizes_refused(cli_file):
         fqz5file.check_blocks(bytes(data))
 
 
+def test_lengths_header_count_not_trusted(cli_file):
+    """The fixed-length header [nb][varint] is walked by the varint's own
+    bytes, as decode_block reads it (fqzcomp5.c:2384-2395), not by nb: a
+    CRC-valid block whose nb lies parses to the same sections, and a quality
+    u_len past the bases behind that lie is refused (the decoders size their
+    outputs from these fields)."""
+    data = bytearray(cli_file)
+    s, e = fqz5file._blocks_of(data)[0]
+    f0 = fqz5file.block_fields(data, s, e)
+    p = s + 12
+    nu, _, nc = struct.unpack_from("<IBI", data, p)
+    p += 9 + nc
+    assert data[p] > 0                      # fixed-length block
+    vl = 1
+    while data[p + vl] & 0x80:
+        vl += 1
+    data[p] = 5                             # claims 5 bytes, the varint is vl
+    crc = lambda: struct.pack_into("<I", data, s + 8, zlib.crc32(bytes(data[s + 12:e])))
+    crc()
+    f = fqz5file.block_fields(bytes(data), s, e)
+    assert (f["seq_ulen"], f["qual_ulen"], f["nrec"]) == (f0["seq_ulen"], f0["qual_ulen"], f0["nrec"])
+    q = p + 1 + vl
+    _, su, sc = struct.unpack_from("<BII", data, q)
+    q += 9 + sc
+    st, qu, qc = struct.unpack_from("<BII", data, q)
+    struct.pack_into("<BII", data, q, st, qu + 4096, qc)
+    crc()
+    with pytest.raises(ValueError, match="quality and sequence"):
+        fqz5file.block_fields(bytes(data), s, e)
+
+
+def test_lengths_sum_checked(cli_file):
+    """Record lengths that do not cover the bases are refused (a CRC-valid
+    block with the fixed length one larger)."""
+    data = bytearray(cli_file)
+    s, e = fqz5file._blocks_of(data)[0]
+    p = s + 12
+    nu, _, nc = struct.unpack_from("<IBI", data, p)
+    p += 9 + nc
+    assert data[p] > 0
+    data[p + data[p]] += 1                  # the last varint byte: length + 1
+    struct.pack_into("<I", data, s + 8, zlib.crc32(bytes(data[s + 12:e])))
+    with pytest.raises(ValueError, match="lengths do not sum"):
+        fqz5file.block_fields(bytes(data), s, e)
+
+
 @pytest.mark.parametrize("width", [0, 5, 20000])
 def test_bounded_intervals_choose_as_exact_sizes(width):
     """The -7 bounded window with interval tries (every fqz / sequence-model

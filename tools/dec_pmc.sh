@@ -4,7 +4,7 @@
 # waitcnt (MI355X_MICROARCH.md, SQ block), one rocprofv3 pass per group.
 set -u
 export TMPDIR=/tmp
-out=gpurun_out/r03/pmc_dec
+out=gpurun_out/pmc_dec
 mkdir -p $out
 kind=${1:-novaseq}; strat=${2:-0}
 timeout -k 10 120 python -u tools/fqz_dec_once.py $kind $strat 27000 > $out/once.log 2>&1 || exit 1

@@ -3,7 +3,7 @@
 python tools/pmc_db.py <kernel substring> <nsym> <db> [<db> ...]
 Sums each counter over the dispatches of the kernel whose name contains
 the substring and prints it, with per-symbol values when nsym > 0 (the
-decoder PMC runs, tools/r03_dec_pmc.sh).  SQ_WAVE_CYCLES and the SQ wait /
+decoder PMC runs, tools/dec_pmc.sh).  SQ_WAVE_CYCLES and the SQ wait /
 active counters count in units of 4 cycles per wave on gfx950 (the SQ
 samples every fourth clock), so cycle counters are also shown x4.
 """
