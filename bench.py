@@ -192,9 +192,11 @@ def t1_check(reads, blocks, level, gpu_blocks, nblk: int, timeout: int = 900):
 
 
 def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local, dist,
-            scaling="weak", pmc_tag="", dropin=False, t1_blocks=0):
+            scaling="weak", pmc_tag="", dropin=False, t1_blocks=0, hybrid=False):
     """One workload: warmup + `steps` timed steps (barrier + synchronize on
-    both sides, max over ranks) and the result fields of its JSON line."""
+    both sides, max over ranks) and the result fields of its JSON line.
+    hybrid: then time the decode again with the adaptive-model chains on host
+    cores beside the GPU (fqz5_set_host_decode(1)), reported apart."""
     import torch
     from fqzcomp5_amd import lib, sections as S, synth
 
@@ -277,6 +279,38 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     # ---- correctness: every decoded section equals its input -------------
     ok = all(r.status == 0 for r in res) and all(r.status == 0 for r in dres)
     ok = ok and run.roundtrip_ok()
+    # ---- the same decode with the fqz / sequence-model chains on host
+    # cores (the library's own C++ decoders, host_dec.cpp) beside the GPU's
+    # rANS and names; the GPU-only figures above stay the item's numbers ----
+    hyb = None
+    if hybrid:
+        prev = so.fqz5_set_host_decode(1)
+        try:
+            decode(res)                            # warm: the host model buffers
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            hs = []
+            for _ in range(steps):
+                b = time.perf_counter()
+                hres = decode(res)
+                torch.cuda.synchronize()
+                hs.append(time.perf_counter() - b)
+        finally:
+            so.fqz5_set_host_decode(prev)
+        h_ok = all(r.status == 0 for r in hres) and run.roundtrip_ok()
+        th = torch.tensor([sum(hs)], dtype=torch.float64,
+                          device=dev if world == 1 or dist.get_backend() == "nccl" else torch.device("cpu"))
+        if world > 1:
+            dist.all_reduce(th, op=dist.ReduceOp.MAX)
+        t_hdec = float(th.item())
+        hyb = {"dec_ms_per_step": round(t_hdec / steps * 1e3, 2),
+               "dec_MBps": round(fq_all * steps / t_hdec / 1e6, 2),
+               "value": round(fq_all * steps / (t_enc + t_hdec) / 1e6, 2),
+               "host_threads": int(so.fqz5_host_threads()),
+               "roundtrip_ok": bool(h_ok),
+               "note": "decode with fqz quality and sequence-model sections on host cores "
+                       "(fqz5_set_host_decode(1)); encode as above; same bytes"}
     comp_bytes = int(run.blk_off[-1])
     shape = {"illumina": "illumina 150 bp, Illumina names, 8-level binned quals",
              "novaseq": "novaseq 150 bp, Illumina names, NovaSeq 4-level i.i.d. quals",
@@ -312,6 +346,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                    "methods_chosen": sorted({int(m) for m in meth_all}),
                    "roundtrip_ok": bool(ok),
                    "parallelism": f"blocks sharded over {world} GPU(s) ({scaling})",
+                   "fqz_decoders": dict(zip(("general", "small"), _fqz_dec_counts(so))),
                    "arena_bytes": [int(arena0), int(arena1)],
                    # candidates in the timed steps, and how many were provably
                    # losing and skipped their range chain (output unchanged)
@@ -321,6 +356,8 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                                  "intervals_decided": S.last_bounds_decided if level >= 7
                                  else None}},
     }
+    if hyb is not None:
+        out["hybrid"] = hyb
     # ---- roofline of the dominant kernel ---------------------------------
     # every chain kernel's launch time from HIP events on the stream it runs
     # on (fqz5_profile_read_all: rANS encode / decode, fqz decode, the fqz
@@ -378,6 +415,12 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     del run, reads
     torch.cuda.empty_cache()
     return out
+
+
+def _fqz_dec_counts(so):
+    out = (C.c_uint64 * 2)()
+    so.fqz5_fqz_dec_counts(out)
+    return [int(out[0]), int(out[1])]
 
 
 def crc_item(lib, torch, gib: int = 4, reps: int = 5):
@@ -567,7 +610,7 @@ def main():
                                          else args.gb * world, min(args.steps, 2),
                                          min(args.warmup, 1), not args.no_cpu, threads, world,
                                          rank, local, dist, scaling=args.scaling,
-                                         pmc_tag="_l5i", t1_blocks=4)
+                                         pmc_tag="_l5i", t1_blocks=4, hybrid=True)
     if rank == 0 and world == 1 and not args.no_crc:
         out["crc32"] = crc_item(lib, torch)
     if rank == 0:

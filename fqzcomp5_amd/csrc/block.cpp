@@ -28,6 +28,7 @@
 #include "seq_codec.hpp"
 #include "lzp_codec.hpp"
 #include "names.hpp"
+#include "host_dec.hpp"
 #include "rans_format.hpp"
 
 namespace fqz5 {
@@ -878,6 +879,7 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         std::vector<size_t> lzp_rans;                 // its rANS stage in reqs
         std::vector<NameDec> nd;                      // name sections (decode_names)
         std::vector<int> who_name;
+        std::vector<const uint8_t *> seq_h;           // host stream of each seqd entry
         off = 0;
         for (int i = 0; i < nsec; i++) {
             const uint8_t *h = host + off;
@@ -919,6 +921,7 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
                 continue;
             }
             if ((h[0] & 7) == 1 && secs[i].sec == FQZ5_SEC_SEQ) {   // decode_seq (:2421-2430)
+                seq_h.push_back(h + 9);
                 SeqDecReq q;
                 q.d_in = secs[i].in + 9;
                 q.in_size = clen;
@@ -964,6 +967,51 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             who.push_back(i);
         }
         const auto t1 = std::chrono::steady_clock::now();
+        // ---- the adaptive-model chains on host cores (fqz5_set_host_decode):
+        // sequence-model sections and quality sections without a sequence
+        // context start now, beside the GPU's rANS and names; quality
+        // sections with one wait for their block's bases ---------------------
+        struct HostChain { uint8_t *buf = nullptr; size_t cap = 0, n = 0; int sec = -1; bool ok = false; };
+        std::vector<HostChain> hc;
+        std::vector<size_t> hc_fqz;                   // fqz index of each host fqz chain
+        std::vector<int> hc_kind;                     // 0 seq, 1 fqz (no sequence), 2 fqz (sequence)
+        host::Jobs hjobs;
+        const int hmode = host_decode_mode();
+        if (hmode) {
+            for (size_t k = 0; k < seqd.size(); k++) {
+                HostChain c;
+                c.cap = c.n = seqd[k].n;
+                c.buf = g.staging.alloc(c.cap + 1);
+                c.sec = who_seq[k];
+                hc.push_back(c);
+                hc_fqz.push_back(k);
+                hc_kind.push_back(0);
+            }
+            for (size_t k = 0; k < fqz.size(); k++) {
+                const FqzDecReq &f = fqz[k];
+                uint32_t tl = 0;
+                const int vk = varint_get(f.h_in, f.h_in + f.in_size, &tl);
+                const bool seqctx = vk > 0 && size_t(vk) + 1 < f.in_size && (f.h_in[vk + 1] & 8u) && f.d_seq;
+                HostChain c;
+                c.cap = f.out_cap;
+                c.buf = g.staging.alloc(c.cap + 1);
+                c.sec = who_fqz[k];
+                hc.push_back(c);
+                hc_fqz.push_back(k);
+                hc_kind.push_back(seqctx ? 2 : 1);
+            }
+            hjobs.start(hc.size(), [&](size_t j) {
+                HostChain &c = hc[j];
+                if (hc_kind[j] == 0) {
+                    const SeqDecReq &q = seqd[hc_fqz[j]];
+                    c.ok = host::seq_decode(seq_h[hc_fqz[j]], q.in_size, q.lens, q.nrec, q.both, q.k, c.buf,
+                                            q.n) == 0;
+                } else if (hc_kind[j] == 1) {
+                    const FqzDecReq &f = fqz[hc_fqz[j]];
+                    c.ok = host::fqz_decode(f.h_in, f.in_size, c.buf, c.cap, &c.n, nullptr, 0, nullptr, 0) == 0;
+                }
+            });
+        }
         // the name sections on their helper context, beside the chains: their
         // host rebuild overlaps the GPU's rANS / fqz / sequence decoding
         // The name sections decode on their helper context beside the chains.
@@ -1013,10 +1061,56 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
                 R.usize = run[k].out_len;
             }
         }
-        if (!seqd.empty()) seq_decode_batch(g, seqd);
+        if (!hmode && !seqd.empty()) seq_decode_batch(g, seqd);
         // after the rANS and sequence sections: a quality section's sequence context may
         // be the output of this call's sequence section
-        if (!fqz.empty()) fqz_decode_batch(g, fqz);
+        if (!hmode && !fqz.empty()) fqz_decode_batch(g, fqz);
+        if (hmode) {
+            hjobs.join();
+            // the quality chains with a sequence context: their block's bases
+            // on the host (a host-decoded sequence section's buffer, or a copy
+            // of the GPU's output), per record pointers as the reference's s->seq
+            std::vector<std::vector<const uint8_t *>> recp(hc.size());
+            for (size_t j = 0; j < hc.size(); j++) {
+                if (hc_kind[j] != 2) continue;
+                const FqzDecReq &f = fqz[hc_fqz[j]];
+                const uint8_t *bases = nullptr;
+                for (size_t m = 0; m < hc.size(); m++)
+                    if (hc_kind[m] == 0 && secs[hc[m].sec].out == f.d_seq) bases = hc[m].ok ? hc[m].buf : nullptr;
+                uint64_t nb = 0;
+                for (int r = 0; r < f.nrec; r++) nb += f.lens[r];
+                if (!bases) {
+                    uint8_t *b = g.staging.alloc(nb + 1);
+                    g.download(b, f.d_seq, nb);
+                    bases = b;
+                }
+                recp[j].resize(size_t(std::max(f.nrec, 1)));
+                uint64_t o = 0;
+                for (int r = 0; r < f.nrec; r++) {
+                    recp[j][size_t(r)] = bases + o;
+                    o += f.lens[r];
+                }
+            }
+            g.sync();
+            host::Jobs hb;
+            std::vector<size_t> late;
+            for (size_t j = 0; j < hc.size(); j++)
+                if (hc_kind[j] == 2) late.push_back(j);
+            hb.start(late.size(), [&](size_t t) {
+                HostChain &c = hc[late[t]];
+                const FqzDecReq &f = fqz[hc_fqz[late[t]]];
+                c.ok = host::fqz_decode(f.h_in, f.in_size, c.buf, c.cap, &c.n, nullptr, 0,
+                                        recp[late[t]].data(), f.nrec) == 0;
+            });
+            hb.join();
+            for (HostChain &c : hc) {
+                fqz5_section_result &R = res[c.sec];
+                R.status = c.ok ? 0 : -1;
+                R.usize = uint32_t(c.n);
+                if (c.ok && c.n)
+                    FQZ5_HIP(hipMemcpyAsync(secs[c.sec].out, c.buf, c.n, hipMemcpyHostToDevice, g.stream));
+            }
+        }
         if (tn.joinable()) tn.join();
         nshare.reset();
         if (nerr) std::rethrow_exception(nerr);
@@ -1035,12 +1129,12 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             R.status = reqs[k].ok ? 0 : -1;
             R.usize = reqs[k].out_size;
         }
-        for (size_t k = 0; k < seqd.size(); k++) {
+        for (size_t k = 0; k < seqd.size() && !hmode; k++) {
             fqz5_section_result &R = res[who_seq[k]];
             R.status = seqd[k].ok ? 0 : -1;
             R.usize = seqd[k].n;
         }
-        for (size_t k = 0; k < fqz.size(); k++) {
+        for (size_t k = 0; k < fqz.size() && !hmode; k++) {
             fqz5_section_result &R = res[who_fqz[k]];
             R.status = fqz[k].ok ? 0 : -1;
             R.usize = uint32_t(fqz[k].out_size);

@@ -16,6 +16,7 @@
 #include "fqz_kernels.h"
 #include "arith_kernels.h"
 #include "fqz_codec.hpp"
+#include "host_dec.hpp"
 
 namespace fqz5 {
 
@@ -98,6 +99,17 @@ bool small_decoder_on() {
         g_dec_small.store(v);
     }
     return v != 0;
+}
+
+static std::atomic<int> g_host_dec{-1};
+int host_decode_mode() {
+    int v = g_host_dec.load();
+    if (v < 0) {
+        const char *e = std::getenv("FQZ5_HOST_DECODE");
+        v = e ? std::atoi(e) : 0;
+        g_host_dec.store(v);
+    }
+    return v;
 }
 
 // The calling thread's helper contexts: their own streams and arenas, for
@@ -393,6 +405,14 @@ const char *fqz5_last_error(void) { return g_err.c_str(); }
 uint64_t fqz5_arena_bytes(void) { return arena_bytes(); }
 
 unsigned fqz5_set_hot_min(unsigned min_events) { return fqz_set_hot_min(min_events); }
+
+int fqz5_host_threads(void) { return host::threads(); }
+
+int fqz5_set_host_decode(int mode) {
+    const int prev = host_decode_mode();
+    g_host_dec.store(mode ? 1 : 0);
+    return prev;
+}
 
 void fqz5_fqz_dec_counts(uint64_t *out2) {
     out2[0] = fqz_dec_blocks(false);

@@ -407,6 +407,26 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
         next_uniform(sym);
     };
 
+    // debug (FQZ5_DEC_SMALL_DBG 0x1000, one symbol per run): the reference's
+    // decision for the next symbol, to compare with the run's
+    uint32_t dbg_seen = 0;
+    auto predict = [&](uint32_t &kout, uint32_t &bub, uint32_t &tot) {
+        ensure();
+        const uint32_t uw = *reinterpret_cast<const uint16_t *>(lds + maddr + voff);
+        tot = U(*reinterpret_cast<const uint16_t *>(lds + maddr + 18));
+        uint32_t r2 = rng, t = 0;
+        if (tot && r2 >= tot) { r2 /= tot; t = code / r2; }
+        const bool live = l < L;
+        const uint32_t up = live ? uw : 0u;
+        const uint32_t lo_l = __shfl_up(up, 1, 64);
+        const uint32_t lo = l ? lo_l : 0u;
+        const uint32_t f = live ? up - lo : 0u;
+        const uint64_t gt = __ballot(live && up > t);
+        kout = gt ? uint32_t(__builtin_ctzll(gt)) : 99u;
+        bub = 0;
+        if (kout >= 1 && kout < 99) bub = RL(f, kout) + 16 > RL(f, kout - 1) ? 1u : 0u;
+        return uw;
+    };
     uint32_t turns = 0;
     bool lost = false;
     for (;;) {
@@ -472,6 +492,8 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
         uint32_t lim = left < SOBUF - fill ? left : SOBUF - fill;
         if (lim > 64u) lim = 64u;
         if (J.pad2 & 0x800) lim = 1;
+        uint32_t pk_c = 0, pb_c = 0, pt_c = 0, pu_c = 0;
+        if (J.pad2 & 0x1000) pu_c = predict(pk_c, pb_c, pt_c);
         uint32_t ulim = (in.vb - 4u) * 8u;
         // per-step context terms of the run (fqz_update_ctx uses the position
         // and delta before this symbol's update): lane i the position term of
@@ -570,6 +592,19 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
             delta = delta0 + dd;
             nmiss += nm;
             left -= done;
+        }
+        if ((J.pad2 & 0x1000) && !dbg_seen && flags != 2 && done == 1 &&
+            (pb_c || pk_c >= (L < 8u ? L : 8u) || pt_c > 65503u)) {
+            dbg_seen = 1;
+            const uint32_t uv = RL(pu_c, l < 9 ? l : 8);
+            if (l == 0) {
+                J.counts[20] = 1;
+                J.counts[21] = obase + fill;
+                J.counts[22] = pk_c;
+                J.counts[23] = pb_c;
+                J.counts[24] = pt_c;
+            }
+            if (l < 7) J.counts[25 + l] = uv;
         }
         qctx = qs >> qshift;
         if (l < done) lds[S_OBUF + fill + l] = uint8_t(vout);

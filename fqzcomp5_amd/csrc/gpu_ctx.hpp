@@ -262,6 +262,8 @@ struct GpuCtx {
 bool hedge_chains();
 // the small-alphabet fqz decoder (fqz5_set_dec_small, $FQZ5_DEC_SMALL)
 bool small_decoder_on();
+// the block decoder's adaptive-model chains on host cores (fqz5_set_host_decode)
+int host_decode_mode();
 // quality blocks decoded by the general (false) / small (true) fqz decoder
 uint64_t fqz_dec_blocks(bool small);
 // Copies of each of `jobs` chains: up to 4 while they fit one per CU.

@@ -1,0 +1,59 @@
+// host_dec.hpp — the adaptive-model decode chains on host cores (host_dec.cpp)
+#pragma once
+#include <atomic>
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <thread>
+#include <algorithm>
+#include <vector>
+
+namespace fqz5 {
+namespace host {
+
+// uncompress_block_fqz2f (fqzcomp_qual.c:1410-1634) of `in` into out (at
+// most out_cap bytes; *out_size the decoded size).  lengths: the first
+// nlengths record lengths out.  seq: per record its bases (the reference's
+// s->seq[rec], nrec of them; nullptr: none).  Returns 0 or -1.
+int fqz_decode(const uint8_t *in, size_t in_size, uint8_t *out, size_t out_cap, size_t *out_size,
+               int *lengths, int nlengths, const uint8_t *const *seq, int nrec);
+
+// decode_seq (fqzcomp5.c:1272-1406): n bases of records lens[nrec] with a
+// k-mer context model (both: both strands update).  Returns 0 or -1.
+int seq_decode(const uint8_t *in, uint32_t in_size, const uint32_t *lens, int nrec, int both, int k,
+               uint8_t *out, uint32_t n);
+
+// Host threads for the chains: $FQZ5_HOST_THREADS, else the cores this
+// process may use (at most 16, the CPU share of one GPU on the MI355X boxes).
+int threads();
+
+// fn(i) for i in [0, n) on up to threads() host threads, started by start()
+// and waited for by join() (or the destructor); the work list is shared, so
+// long and short jobs balance.
+class Jobs {
+  public:
+    void start(size_t n, std::function<void(size_t)> fn) {
+        fn_ = std::move(fn);
+        n_ = n;
+        next_ = 0;
+        const size_t t = std::min<size_t>(n, size_t(threads()));
+        for (size_t k = 0; k < t; k++)
+            th_.emplace_back([this] {
+                for (size_t i; (i = next_.fetch_add(1)) < n_;) fn_(i);
+            });
+    }
+    void join() {
+        for (auto &t : th_) t.join();
+        th_.clear();
+    }
+    ~Jobs() { join(); }
+
+  private:
+    std::function<void(size_t)> fn_;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    std::vector<std::thread> th_;
+};
+
+}  // namespace host
+}  // namespace fqz5

@@ -71,6 +71,10 @@ def load() -> C.CDLL:
     lib.fqz5_set_hedge.argtypes = [C.c_int]
     lib.fqz5_set_dec_small.restype = C.c_int
     lib.fqz5_set_dec_small.argtypes = [C.c_int]
+    lib.fqz5_set_host_decode.restype = C.c_int
+    lib.fqz5_set_host_decode.argtypes = [C.c_int]
+    lib.fqz5_host_threads.restype = C.c_int
+    lib.fqz5_host_threads.argtypes = []
     lib.fqz5_set_hot_min.restype = C.c_uint
     lib.fqz5_set_hot_min.argtypes = [C.c_uint]
     lib.rans_compress_bound_4x16.restype = C.c_uint
@@ -124,6 +128,12 @@ def load() -> C.CDLL:
     lib.fqz5_seq_decode.restype = C.c_void_p
     lib.fqz5_seq_decode.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint32), C.c_int,
                                     C.c_int, C.c_int, C.c_uint]
+    lib.fqz5_seq_decode_host.restype = C.c_void_p
+    lib.fqz5_seq_decode_host.argtypes = [C.c_char_p, C.c_uint, C.POINTER(C.c_uint32), C.c_int,
+                                    C.c_int, C.c_int, C.c_uint]
+    lib.fqz5_fqz_decompress_host.restype = C.c_void_p
+    lib.fqz5_fqz_decompress_host.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t),
+                                   C.POINTER(C.c_int), C.c_int, C.POINTER(FqzSlice)]
     _lib = lib
     return lib
 
@@ -295,8 +305,10 @@ def fqz_compress(qual: bytes, lens, flags, strat: int, seq: bytes | None = None,
     return out
 
 
-def fqz_decompress(comp: bytes, lens=None, flags=None, seq: bytes | None = None):
-    """fqz_decompress on the GPU; returns (bytes, record lengths)."""
+def fqz_decompress(comp: bytes, lens=None, flags=None, seq: bytes | None = None,
+                   host: bool = False):
+    """fqz_decompress on the GPU (host=True: fqz5_fqz_decompress_host, the
+    same decoder on a host core); returns (bytes, record lengths)."""
     import numpy as np
     lens = np.zeros(0, np.uint32) if lens is None else lens
     flags = np.zeros(len(lens), np.uint32) if flags is None else flags
@@ -304,7 +316,9 @@ def fqz_decompress(comp: bytes, lens=None, flags=None, seq: bytes | None = None)
     n = C.c_size_t(0)
     nl = len(lens_a)
     L = (C.c_int * max(nl, 1))()
-    p = load().fqz_decompress(bytes(comp), len(comp), C.byref(n), L, nl, C.byref(s))
+    so = load()
+    fn = so.fqz5_fqz_decompress_host if host else so.fqz_decompress
+    p = fn(bytes(comp), len(comp), C.byref(n), L, nl, C.byref(s))
     if not p:
         raise NativeError("fqz_decompress failed: " + last_error())
     out = C.string_at(p, n.value)
@@ -329,10 +343,13 @@ def seq_encode(seq: bytes, lens, both: int, k: int) -> bytes:
     return out
 
 
-def seq_decode(comp: bytes, lens, both: int, k: int, out_size: int) -> bytes:
-    """fqz5_seq_decode (decode_seq, fqzcomp5.c:1272) on the GPU."""
+def seq_decode(comp: bytes, lens, both: int, k: int, out_size: int, host: bool = False) -> bytes:
+    """fqz5_seq_decode (decode_seq, fqzcomp5.c:1272) on the GPU (host=True:
+    fqz5_seq_decode_host on a host core)."""
     la, nr = _seq_lens(lens)
-    p = load().fqz5_seq_decode(bytes(comp), len(comp), la, nr, both, k, out_size)
+    so = load()
+    fn = so.fqz5_seq_decode_host if host else so.fqz5_seq_decode
+    p = fn(bytes(comp), len(comp), la, nr, both, k, out_size)
     if not p:
         raise NativeError("fqz5_seq_decode failed: " + last_error())
     out = C.string_at(p, out_size)

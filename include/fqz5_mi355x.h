@@ -139,6 +139,28 @@ char *fqz5_seq_decode(unsigned char *in, unsigned int in_size, unsigned int *len
                       int nrecords, int both_strands, int ctx_size,
                       unsigned int out_size);
 
+/* ---- the same decoders on a host core (host_dec.cpp) ------------------- */
+
+/* fqz_decompress and fqz5_seq_decode on the calling thread's host core:
+ * same arguments, same bytes, same NULL cases.  One block is one dependent
+ * chain, which one host core runs 5-15x faster than one GPU wave; the block
+ * decoder uses them for its adaptive-model sections when
+ * fqz5_set_host_decode asks for it. */
+char *fqz5_fqz_decompress_host(char *in, size_t in_size, size_t *out_size,
+                               int *lengths, int nlengths, fqz_slice *s);
+char *fqz5_seq_decode_host(unsigned char *in, unsigned int in_size, unsigned int *len,
+                           int nrecords, int both_strands, int ctx_size,
+                           unsigned int out_size);
+
+/* Where fqz5_decode_sections (fqz5_block.h) runs the adaptive-model chains
+ * (fqz quality sections, SEQ10..SEQ14B sequence sections): 0 = on the GPU
+ * (default unless $FQZ5_HOST_DECODE is set), 1 = on host cores (up to
+ * $FQZ5_HOST_THREADS threads) beside the GPU's rANS, LZP and name work.
+ * Output bytes do not depend on it.  Returns the previous setting. */
+int fqz5_set_host_decode(int mode);
+/* The host threads that leg uses. */
+int fqz5_host_threads(void);
+
 /* ---- CRC32 (zlib crc32, fqzcomp5.c:2268-2269, :2310-2311, :4443, :4670) --- */
 
 /* zlib's crc32(crc, buf, len) computed on the GPU (same value; buf == NULL
