@@ -799,6 +799,56 @@ def _file_blocks(f, size: int):
     return out
 
 
+def _block_text_size(f, s: int, e: int, plus_name: bool) -> int:
+    """The FASTQ (or FASTA) text size of block [s, e) of an open .fqz5, from
+    its headers alone (a few small reads): output_fastq writes '@' name '\n'
+    seq '\n' '+' [name] '\n' qual '\n' per record (fqzcomp5.c:3441-3480),
+    output_fasta '>' name '\n' seq '\n' (:3503-3517); the name section
+    decodes to each name and a '\0'."""
+    f.seek(s)
+    h = f.read(21)
+    if len(h) < 21:
+        raise ValueError("truncated .fqz5: a block header runs past the end")
+    nrec, = struct.unpack_from("<I", h, 4)
+    name_ulen, = struct.unpack_from("<I", h, 12)
+    c_len, = struct.unpack_from("<I", h, 17)
+    p = s + 21 + c_len
+    f.seek(p)
+    nb = f.read(1)
+    if not nb:
+        raise ValueError("truncated .fqz5: lengths past the block")
+    if nb[0]:
+        vl = f.read(5)
+        n = 1
+        while n < len(vl) and vl[n - 1] & 0x80:
+            n += 1
+        p += 1 + n
+    else:
+        # [0][u32][a varint per record]: walk them (read in one go)
+        f.seek(p + 5)
+        v = f.read(min(5 * nrec, max(e - p - 5, 0)))
+        k = 0
+        for _ in range(nrec):
+            while k < len(v) and v[k] & 0x80:
+                k += 1
+            k += 1
+        p += 5 + k
+    f.seek(p)
+    sh = f.read(9)
+    if len(sh) < 9:
+        raise ValueError("truncated .fqz5: sequence header past the block")
+    seq_ulen, seq_clen = struct.unpack_from("<II", sh, 1)
+    f.seek(p + 9 + seq_clen)
+    qh = f.read(9)
+    if len(qh) < 9:
+        raise ValueError("truncated .fqz5: quality header past the block")
+    qual_ulen, qual_clen = struct.unpack_from("<II", qh, 1)
+    names = name_ulen - nrec
+    if qual_ulen == 0 and qual_clen == 0:                    # FASTA
+        return names + seq_ulen + 2 * nrec
+    return names * (2 if plus_name else 1) + 2 * seq_ulen + 6 * nrec
+
+
 def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "cuda",
                     dst2: str | None = None, group=None, window_bytes: int | None = None) -> int:
     """fqzcomp5 -d src dst [dst2] on the GPU(s): blocks read and decoded in
@@ -806,14 +856,19 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
     decodes block by block, fqzcomp5.c:3754-3800), the text written behind
     the last.  dst2: deinterleave, R1 records to dst and R2 records to dst2
     (fqzcomp5 -d in out1 out2).  group: one process per GPU, the blocks split
-    contiguously over the ranks, each rank's text written at its offset from
-    an all-gather of the text sizes.  Returns the text bytes written."""
+    contiguously over the ranks; every window's text goes out as soon as it
+    is decoded (host memory stays one window): at its offset from the block
+    headers' text sizes (one output), or into a per-rank spill file copied
+    into place at the end (R1/R2: the split of a block's text between the two
+    files needs its decoded names).  Returns the text bytes written."""
     import os
     ws, rk = S._world(group)
     outs = [dst] + ([dst2] if dst2 is not None else [])
     if ws > 1 and any(d.endswith(".gz") for d in outs):
         raise ValueError("gzip output needs a single process")
     size = os.path.getsize(src)
+    single = ws == 1
+    spill = not single and dst2 is not None
     with open(src, "rb") as f:
         ranges = _file_blocks(f, size)
         nb = len(ranges)
@@ -829,15 +884,24 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
             tot += z
         if cur:
             groups.append(cur)
-        single = ws == 1
         gz = [d.endswith(".gz") for d in outs]
-        streams = []
+        streams, sinks, at = [], [], 0
         if single:
             import gzip
             streams = [gzip.GzipFile(filename="", mode="wb", compresslevel=6, mtime=0,
                                      fileobj=open(d, "wb")) if z else open(d, "wb")
                        for d, z in zip(outs, gz)]
-        held = [[] for _ in outs]              # multi-rank: this rank's text, in order
+        elif spill:
+            streams = [open(f"{d}.part{rk}", "wb") for d in outs]
+        else:
+            # one output: every block's text size from its headers, so this
+            # rank's text starts at the sum over the blocks before its first
+            sizes = [_block_text_size(f, s, e, plus_name) for s, e in ranges]
+            at = sum(sizes[:mine[0]]) if mine else 0
+            if rk == 0:
+                _Sink(dst, True).close()
+            _barrier(group)
+            sinks = [_Sink(dst, False)]
         written = [0 for _ in outs]
         try:
             for gb in groups:
@@ -860,11 +924,15 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
                 for j, t in enumerate(texts):
                     out = _pinned(int(t.numel()))
                     out.copy_(t)
-                    if single:
-                        streams[j].write(memoryview(out.numpy()))
+                    if sinks:
+                        want = sum(sizes[b] for b in gb)
+                        if int(t.numel()) != want:
+                            raise _lib.NativeError("decoded text size differs from the block headers'")
+                        sinks[j].write_at(at + written[j], out.numpy())
                     else:
-                        held[j].append(out)
+                        streams[j].write(memoryview(out.numpy()))
                     written[j] += int(t.numel())
+                    del out
                 del buf, host, texts
         finally:
             for st in streams:
@@ -874,23 +942,29 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
                     raw.close()
                 else:
                     st.close()
+            for sk in sinks:
+                sk.close()
     if single:
         return sum(written)
-    # several ranks: text offsets from the ranks' sizes, positioned writes
     all_w = _allgather_obj(written, group)
-    for j, d in enumerate(outs):
-        if rk == 0:
-            _Sink(d, True).close()
-    _barrier(group)
-    for j, d in enumerate(outs):
-        off = sum(w[j] for w in all_w[:rk])
-        sink = _Sink(d, False)
-        try:
-            for out in held[j]:
-                sink.write_at(off, out.numpy())
-                off += int(out.numel())
-        finally:
-            sink.close()
+    if spill:
+        # the spill files into place at their offsets from the ranks' sizes
+        for j, d in enumerate(outs):
+            if rk == 0:
+                _Sink(d, True).close()
+        _barrier(group)
+        for j, d in enumerate(outs):
+            off = sum(w[j] for w in all_w[:rk])
+            sink = _Sink(d, False)
+            part = f"{d}.part{rk}"
+            try:
+                with open(part, "rb") as pf:
+                    for c in iter(lambda: pf.read(1 << 26), b""):
+                        sink.write_at(off, c)
+                        off += len(c)
+            finally:
+                sink.close()
+                os.unlink(part)
     _barrier(group)
     return sum(sum(w) for w in all_w)
 

@@ -199,6 +199,29 @@ def cli_file(tmp_path_factory):
     return open(out, "rb").read()
 
 
+def test_block_text_sizes_from_headers(tmp_path):
+    """decompress_file's multi-rank offsets: each block's FASTQ text size from
+    its headers alone equals the text the block came from (and with the
+    name repeated on the '+' line, that plus the names)."""
+    if not os.path.exists(CLI):
+        pytest.skip("reference CLI not built")
+    from fqzcomp5_amd import synth
+    r = synth.illumina(9000, seed=12, with_names=True)
+    src, out = str(tmp_path / "in.fastq"), str(tmp_path / "o.fqz5")
+    synth.write_fastq(r, src)
+    subprocess.run([CLI, "-5", "-t1", "-b", "400k", src, out], check=True, capture_output=True)
+    text = open(src, "rb").read()
+    with open(out, "rb") as f:
+        ranges = fqz5file._file_blocks(f, os.path.getsize(out))
+        assert len(ranges) > 2
+        sizes = [fqz5file._block_text_size(f, s, e, False) for s, e in ranges]
+        plus = [fqz5file._block_text_size(f, s, e, True) for s, e in ranges]
+    assert sum(sizes) == len(text)
+    names = sum(len(r.name(i).split(b" ")[0]) + (len(r.name(i)) - len(r.name(i).split(b" ")[0]))
+                for i in range(r.num_records))
+    assert sum(plus) == len(text) + names
+
+
 def test_truncated_file_refused(cli_file):
     data = cli_file
     ranges = fqz5file._blocks_of(data)
