@@ -338,14 +338,17 @@ def trial_decided(lo: np.ndarray, hi: np.ndarray, ids, ins, tried, sched, state_
 
 
 def refine_session(secs: list, ids, sched, lo: np.ndarray, hi: np.ndarray, pairs, ins,
-                   chunk_bytes: int) -> bool:
+                   chunk_bytes: int, commit_bytes: int | None = None) -> bool:
     """refine_exact as one try session over every section, which the commit
     can then use: the open pairs exactly, and each section outside the trial
     of a kind with open candidates tries those candidates too (its method is
     the window's pick, one of them when it is open), so a decided trial
     commits with the winners already coded.  Returns False, trying nothing,
     when the session would not fit the device memory budget (~60 B per input
-    byte and work candidate, 5 x chunk_bytes of such bytes)."""
+    byte and work candidate, 5 x chunk_bytes of such bytes), counting the
+    sections the commit then codes late in the same session (one candidate
+    each), and when all sections' inputs exceed the commit's chunk
+    (commit_bytes): the commit of a reused session is not chunked."""
     want, kinds = {}, {}
     for i, m in pairs:
         want[i] = want.get(i, 0) | (1 << m)
@@ -354,7 +357,10 @@ def refine_session(secs: list, ids, sched, lo: np.ndarray, hi: np.ndarray, pairs
         if not sched[j] and int(ids[j]) in kinds:
             want[j] = want.get(j, 0) | kinds[int(ids[j])]
     cost = sum(int(ins[i]) * max(1, bin(want[i] & WORK_MASK).count("1")) for i in want)
+    cost += sum(int(ins[j]) for j in range(len(secs)) if j not in want)   # coded late
     if cost > 5 * chunk_bytes:
+        return False
+    if commit_bytes is not None and sum(int(x) for x in ins[:len(secs)]) > commit_bytes:
         return False
     so = _load()
     if so.fqz5_arenas_release():
@@ -625,7 +631,7 @@ def encode_run_bounded(secs: list[Section], avail: np.ndarray, state: TrialState
             print(f"[sections] size intervals leave a trial decision open ({why[0]}): "
                   f"{len(pairs)} candidates coded exactly", file=sys.stderr, flush=True)
             session = merge_commit and not session and refine_session(
-                secs, ids, sched, lo, hi, sorted(pairs), ins, chunk_bytes)
+                secs, ids, sched, lo, hi, sorted(pairs), ins, chunk_bytes, commit_bytes)
             if not session:
                 refine_exact(secs, lo, hi, sorted(pairs), ins, chunk_bytes)
             g_sizes, g_hi = lo, hi
@@ -799,7 +805,9 @@ def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
             # trial sections; the pairs are dealt out over the ranks and the
             # sizes combined by the same element-wise minimum), replay again
             held = [pr for pr in sorted(pairs) if secs[pr[0]] is not None]
-            if ws > 1 and len(held) != len(pairs):
+            # stop refining on every rank together when any rank lacks a
+            # section's data (the collectives below must pair up)
+            if ws > 1 and int(allreduce_min(np.array([int(len(held) == len(pairs))]), group)[0]) == 0:
                 break
             mine_p = held[rk::ws]
             ex = np.full((n, M_LAST), np.iinfo(np.uint32).max, np.uint32)

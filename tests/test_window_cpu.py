@@ -349,3 +349,23 @@ def test_bounded_intervals_two_ranks_refine():
     work = lambda t: [x for x in t if (1 << x[1]) & S.WORK_MASK]
     w0, w1 = work(got[0]["tried"]), work(got[1]["tried"])
     assert len(w0) + len(w1) > len(set(w0) | set(w1))
+
+
+def test_refine_session_counts_late_sections():
+    """a reused refinement session commits every section at once
+    (no chunks), so refine_session refuses when the sections the commit codes
+    late would take the session past its budget, or the inputs past one
+    commit chunk; it returns False before any device work."""
+    nsec = 12
+    ids = np.array([S.SEC_NAME, S.SEC_SEQ, S.SEC_QUAL] * (nsec // 3), np.int32)
+    ins = np.full(nsec, 1_000_000, np.uint32)
+    sched = np.zeros(nsec, np.uint32)
+    secs = [None] * nsec
+    lo = np.zeros((nsec, S.M_LAST), np.uint32)
+    hi = lo.copy()
+    pairs = [(2, S.FQZ1)]
+    # the open pair and its kind's sections alone fit, the late ones do not
+    assert not S.refine_session(secs, ids, sched, lo, hi, pairs, ins, chunk_bytes=1_500_000)
+    # inputs past one commit chunk
+    assert not S.refine_session(secs, ids, sched, lo, hi, pairs, ins, chunk_bytes=10 ** 9,
+                                commit_bytes=nsec * 1_000_000 - 1)
