@@ -101,6 +101,26 @@ def _index_text(text_d, at: int, n: int):
     return recs[:nrec * C.sizeof(FastqRec)], rsz[:nrec], nrec, fasta
 
 
+def _seq_lens_of(recs, rids) -> np.ndarray:
+    """Sequence lengths of the records `rids` (the device record table)."""
+    import torch
+    if not len(rids):
+        return np.zeros(0, np.uint32)
+    w = C.sizeof(FastqRec)
+    tab = recs.view(-1, w)
+    idx = torch.as_tensor(np.asarray(rids, np.int64), device=recs.device)
+    return tab[idx, 40:44].contiguous().view(torch.int32).flatten().cpu().numpy().astype(np.uint32)
+
+
+def _fasta_blocks(recs, starts, fasta: bool) -> list[bool]:
+    """load_seqs_kseq's per-block rule (fqzcomp5.c:574-578, :805-809): a
+    block is FASTA (no quality section) when its first record has no
+    quality, i.e. in FASTQ text when that record's sequence is empty."""
+    if fasta:
+        return [True] * len(starts)
+    return [bool(x == 0) for x in _seq_lens_of(recs, starts)]
+
+
 def _gather(text_d, recs, first, fasta: bool, pair_flags: bool):
     """The blocks [first[k], first[k+1]) of the records as a sections.Run,
     every section input gathered in HBM.  pair_flags: READ2 on the odd
@@ -412,16 +432,19 @@ def _encode_stream(srcs: list, sink: _Sink, level: int, blk_size: int | None, de
             break
         nb = len(W.first) - 1
         # per block: its records, section input sizes (fqz5_fastq_gather's
-        # sizing pass), the sections in encode_block order
-        per = 2 if W.fasta else 3
+        # sizing pass), the sections in encode_block order (no quality
+        # section in a FASTA block)
+        bfa = _fasta_blocks(W.recs, [int(W.first[b]) for b in range(nb)], W.fasta)
+        per = [2 if f else 3 for f in bfa]
+        sec0 = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
         ids, ins, bases, nrec = [], [], [], []
         for b in range(nb):
             a, e = int(W.first[b]), int(W.first[b + 1])
             sz = (C.c_uint64 * 3)()
             _check(so.fqz5_fastq_gather(W.text_d.data_ptr(), W.recs.data_ptr(), a, e, None,
                                         None, None, None, None, sz), "fqz5_fastq_gather")
-            ids += [S.SEC_NAME, S.SEC_SEQ] + ([] if W.fasta else [S.SEC_QUAL])
-            ins += [int(sz[0]), int(sz[1])] + ([] if W.fasta else [int(sz[1])])
+            ids += [S.SEC_NAME, S.SEC_SEQ] + ([] if bfa[b] else [S.SEC_QUAL])
+            ins += [int(sz[0]), int(sz[1])] + ([] if bfa[b] else [int(sz[1])])
             bases.append(int(sz[1]))
             nrec.append(e - a)
         ids = np.array(ids, np.int32)
@@ -429,25 +452,26 @@ def _encode_stream(srcs: list, sink: _Sink, level: int, blk_size: int | None, de
         blk_owner = (np.arange(nb) * ws) // nb
         owner = np.repeat(blk_owner, per)
         sched = S.trial_schedule(ids, av, state)
-        need = sorted({b for b in range(nb) if blk_owner[b] == rk or sched[per * b:per * b + per].any()})
+        need = sorted({b for b in range(nb)
+                       if blk_owner[b] == rk or sched[sec0[b]:sec0[b + 1]].any()})
         # the needed blocks' section inputs, gathered in HBM
         run = _gather_ranges(W.text_d, W.recs, [(int(W.first[b]), int(W.first[b + 1]))
                                                 for b in need], W.fasta, W.pairs)
-        secs = [None] * (nb * per)
+        secs = [None] * int(sec0[-1])
         local = run.enc_secs()
         for j, b in enumerate(need):
-            for q in range(per):
-                secs[per * b + q] = local[per * j + q]
+            for q in range(per[b]):
+                secs[sec0[b] + q] = local[run.blk_sec0[j] + q]
         res, meth, _ = S.encode_window(secs, ids, ins, owner, av, state, group,
                                        bounded=level >= 7, final=W.final)
         mine = [j for j, b in enumerate(need) if blk_owner[b] == rk]
-        full_res = [None] * (len(need) * per)
+        full_res = [None] * len(local)
         for j, b in enumerate(need):
-            for q in range(per):
-                full_res[per * j + q] = res[per * b + q]
+            for q in range(per[b]):
+                full_res[run.blk_sec0[j] + q] = res[sec0[b] + q]
         for j in mine:
-            for q in range(per):
-                r = full_res[per * j + q]
+            for q in range(per[need[j]]):
+                r = full_res[run.blk_sec0[j] + q]
                 if r is None or r.status != 0:
                     raise _lib.NativeError("section coding failed: " + _lib.last_error())
         sizes = []
@@ -502,6 +526,7 @@ def _gather_ranges(text_d, recs, ranges, fasta: bool, pair_flags: bool):
     name_d = torch.empty(max(tot_n, 1), dtype=torch.uint8, device=text_d.device)
     seq_d = torch.empty(max(tot_s, 1), dtype=torch.uint8, device=text_d.device)
     qual_d = None if fasta else torch.empty(max(tot_s, 1), dtype=torch.uint8, device=text_d.device)
+    bfa = _fasta_blocks(recs, [a for a, _ in ranges], fasta)
     lens, flags, nr, sr = [], [], [], []
     no = so_ = 0
     for (a, b), (zn, zs) in zip(ranges, sizes):
@@ -522,7 +547,7 @@ def _gather_ranges(text_d, recs, ranges, fasta: bool, pair_flags: bool):
         sr.append((so_, so_ + zs))
         no += zn
         so_ += zs
-    return S.Run.from_device(name_d, seq_d, qual_d, nr, sr, lens, flags)
+    return S.Run.from_device(name_d, seq_d, qual_d, nr, sr, lens, flags, bfa)
 
 
 def compress_bytes(text: bytes, level: int = 3, blk_size: int | None = None,
@@ -697,22 +722,20 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges
     # FASTA: a quality section of u_len 0 and c_len 0 (decode_block,
     # fqzcomp5.c:2477-2483); the text is then output_fasta's (:3503-3517)
     fasta = [v.qual_ulen == 0 and v.qual_size == 9 for v in views]
-    if any(fasta) and not all(fasta):
-        raise _lib.NativeError("FASTA and FASTQ blocks in one file")
     nsz = [v.name_ulen for v in views]
     ssz = [v.seq_ulen for v in views]
     out_d = torch.empty(sum(nsz) + 2 * sum(ssz) + 1, dtype=torch.uint8, device=device)
     secs, places = [], []
     o = 0
     base = buf.data_ptr()
-    for (s, e), v, ln in zip(ranges, views, lens):
+    for (s, e), v, ln, fa in zip(ranges, views, lens, fasta):
         rl = ln.ctypes.data_as(C.POINTER(C.c_uint32))
         po = (o, o + v.name_ulen, o + v.name_ulen + v.seq_ulen)
         secs.append(S.Section(base + s + v.name_off, out_d.data_ptr() + po[0], v.name_size,
                               v.name_ulen, 0, S.SEC_NAME, rl, None, len(ln), None))
         secs.append(S.Section(base + s + v.seq_off, out_d.data_ptr() + po[1], v.seq_size,
                               v.seq_ulen, 0, S.SEC_SEQ, rl, None, len(ln), None))
-        if not fasta[0]:
+        if not fa:
             secs.append(S.Section(base + s + v.qual_off, out_d.data_ptr() + po[2], v.qual_size,
                                   v.qual_ulen, 0, S.SEC_QUAL, rl, None, len(ln),
                                   out_d.data_ptr() + po[1]))
@@ -724,10 +747,10 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges
     # the text of every block, one after the other in one device buffer
     fmt = so.fqz5_fastq_format_pairs if pairs else so.fqz5_fastq_format
     args, sizes, r1 = [], [], []
-    for v, ln, po in zip(views, lens, places):
+    for v, ln, po, fa in zip(views, lens, places, fasta):
         size, s1 = C.c_uint64(0), C.c_uint64(0)
         a = (out_d.data_ptr() + po[0], v.name_ulen, out_d.data_ptr() + po[1],
-             None if fasta[0] else out_d.data_ptr() + po[2], ln.ctypes.data, len(ln),
+             None if fa else out_d.data_ptr() + po[2], ln.ctypes.data, len(ln),
              int(plus_name))
         _check(fmt(*a, None, 0, C.byref(size), *((C.byref(s1),) if pairs else ())),
                "fqz5_fastq_format")

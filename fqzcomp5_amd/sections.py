@@ -946,16 +946,20 @@ class Run:
         self._setup(lens, flags, nranges if self.names else None, sranges)
 
     @classmethod
-    def from_device(cls, name_d, seq_d, qual_d, name_ranges, seq_ranges, lens, flags):
+    def from_device(cls, name_d, seq_d, qual_d, name_ranges, seq_ranges, lens, flags,
+                    fasta=None):
         """A run over section inputs already in device memory (the FASTQ
         parser's gathered blocks, fqz5file.py): per block its name and
-        sequence/quality byte ranges, record lengths and READ2 flags."""
+        sequence/quality byte ranges, record lengths and READ2 flags.
+        fasta: per block, no quality section (load_seqs_kseq's per-block
+        rule, fqzcomp5.c:574-578); every block when qual_d is None."""
         run = cls.__new__(cls)
         run.reads = None
         run.blocks = [(0, len(ln)) for ln in lens]
         run.names = True
         run.name_d, run.seq_d, run.qual_d = name_d, seq_d, qual_d   # qual_d None: FASTA
         run.name_h = run.name_off = None
+        run.blk_fasta = list(fasta) if fasta is not None else None
         run._setup([np.ascontiguousarray(ln, np.uint32) for ln in lens],
                    [np.ascontiguousarray(f, np.uint32) for f in flags], name_ranges, seq_ranges)
         return run
@@ -964,9 +968,15 @@ class Run:
         """Sections (name, seq, qual per block), their encode / decode buffers."""
         import torch
         device = self.seq_d.device
+        nblk = len(lens)
+        bf = getattr(self, "blk_fasta", None)
+        self.blk_fasta = [self.qual_d is None or bool(bf is not None and bf[k])
+                          for k in range(nblk)]
+        self.blk_sec0 = []            # per block: its first section's index
         self.spans, self.lens, self.flags, self.fixed, self.lengths = [], [], [], [], []
         for k, (ln, fg, (s, e)) in enumerate(zip(lens, flags, seq_ranges)):
             fl = int(ln[0]) if len(ln) and bool(np.all(ln == ln[0])) else 0
+            self.blk_sec0.append(len(self.spans))
             self.lens.append(ln)
             self.flags.append(fg)
             self.fixed.append(fl)
@@ -975,7 +985,7 @@ class Run:
                 ns, ne = name_ranges[k]
                 self.spans.append((SEC_NAME, ns, ne, 0, k))
             self.spans.append((SEC_SEQ, s, e, fl, k))
-            if self.qual_d is not None:       # FASTA blocks: no quality section
+            if not self.blk_fasta[k]:         # FASTA blocks: no quality section
                 self.spans.append((SEC_QUAL, s, e, fl, k))
         caps = []
         for sec, s, e, fl, _ in self.spans:
@@ -1067,22 +1077,21 @@ class Run:
         assert self.names, "blocks need the name sections"
         parts = []
         base = self.enc_buf.data_ptr()
-        per = self.secs_per_block()
         for b in (range(len(self.blocks)) if which is None else which):
-            i = per * b
+            i = self.blk_sec0[b]
             (eo_n, _), (eo_s, _) = self.enc[i], self.enc[i + 1]
             ln = self.lengths[b]
             q, qs = None, 0                   # FASTA: 9 zero bytes (fqzcomp5.c:2258-2264)
-            if per == 3:
+            if not self.blk_fasta[b]:
                 q, qs = base + self.enc[i + 2][0], 9 + res[i + 2].clen
             parts.append(BlockParts(len(self.lens[b]), base + eo_n, res[i].clen,
                                     C.cast(C.c_char_p(ln), C.c_void_p), len(ln),
                                     base + eo_s, 9 + res[i + 1].clen, q, qs))
         return parts
 
-    def secs_per_block(self) -> int:
-        """Sections per block: name, seq, qual (2 for FASTA blocks)."""
-        return 3 if self.qual_d is not None else 2
+    def secs_per_block(self, b: int = 0) -> int:
+        """Sections of block b: name, seq, qual (2 for a FASTA block)."""
+        return 2 if self.blk_fasta[b] else 3
 
     def assemble(self, res, which=None):
         """Write every block (or the blocks `which`, in that order) with
@@ -1133,11 +1142,11 @@ class Run:
             if not np.array_equal(lens, self.lens[b]):
                 raise _lib.NativeError(f"block {b}: lengths differ")
             bo = int(self.blk_off[b])
-            per = self.secs_per_block()
+            per = self.secs_per_block(b)
             for j, (off, size) in enumerate(((v.name_off, v.name_size),
                                              (v.seq_off, v.seq_size),
                                              (v.qual_off, v.qual_size))[:per]):
-                i = per * b + j
+                i = self.blk_sec0[b] + j
                 sec, s, e, fl, k = self.spans[i]
                 rl, nr = self._rec(k)
                 seq = self._seq_dec(i) if sec == SEC_QUAL else None

@@ -92,17 +92,30 @@ def test_not_4line_fastq_fails_loudly():
         fqz5file.compress_bytes(b">r1\nACGT\n+\nIIII\n", 3)
 
 
-def test_empty_first_sequence_block_keeps_qualities():
-    """Known divergence (file path): the reference takes a block
-    for FASTA when its first record has no quality (load_seqs_kseq,
-    fqzcomp5.c:574-578), so a FASTQ block that starts with an empty-sequence
-    record gets a 9-zero quality section and decodes as FASTA text.  This
-    path decides FASTA once, for the text, from its first byte: such a block
-    keeps a quality section and the file round-trips to the same FASTQ."""
-    text = b"@r1\n\n+\n\n@r2\nACGT\n+\nIIII\n@r3\nGG\n+\n#I\n"
-    for level in (1, 3, 5):
-        z = fqz5file.compress_bytes(text, level)
-        assert fqz5file.decompress_bytes(z) == text
+def test_fasta_rule_per_block_vs_reference():
+    """load_seqs_kseq's per-block FASTA rule (fqzcomp5.c:574-578, :805-809):
+    a block whose first record has an empty sequence is coded without a
+    quality section and decodes to FASTA text (:2477-2483, :3833).  The
+    .fqz5 and decoded md5s are the CLI's (tests/golden/fasta_rule.json,
+    make_golden_fasta_rule.py): a tiny file, a 1M-block file whose second and
+    third blocks start with an empty record, and a pair of files."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    import make_golden_fasta_rule as fr
+    ins = fr.make_inputs()
+    md5 = lambda b: hashlib.md5(b).hexdigest()
+    for g in json.load(open(os.path.join(HERE, "golden", "fasta_rule.json"))):
+        t = ins[g["case"]]
+        assert [md5(x) for x in t] == g["in_md5"]
+        if len(t) == 1:
+            z = fqz5file.compress_bytes(t[0], g["level"], blk_size=fr.BLK)
+            dec = [fqz5file.decompress_bytes(z)]
+        else:
+            z = fqz5file.compress_paired_bytes(t[0], t[1], g["level"], blk_size=fr.BLK)
+            dec = list(fqz5file.decompress_paired_bytes(z))
+        assert (len(z), md5(z)) == (g["fqz5_bytes"], g["fqz5_md5"]), (g["case"], g["level"])
+        assert [md5(d) for d in dec] == g["dec_md5"], (g["case"], g["level"])
 
 
 FASTA = [os.path.join(HERE, "golden", "fastq", f) for f in ("sample.fasta", "paired_R1.fasta")]
