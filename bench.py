@@ -230,6 +230,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     for _ in range(warmup):
         decode(encode()[0])
     arena0 = lib.arena_bytes()
+    lib.arena_peak(reset=True)
     so = lib.load()
     fq0 = S.trial_counts()
     so.fqz5_profile(1)
@@ -266,6 +267,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     so.fqz5_profile(0)
     fq1 = S.trial_counts()
     arena1 = lib.arena_bytes()
+    arena_pk = lib.arena_peak()
     # the exchange's tensors live where the process group's backend wants them
     xdev = dev if world == 1 or dist.get_backend() == "nccl" else torch.device("cpu")
     tm = torch.tensor([dt, t_enc, t_dec], dtype=torch.float64, device=xdev)
@@ -347,7 +349,11 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                    "roundtrip_ok": bool(ok),
                    "parallelism": f"blocks sharded over {world} GPU(s) ({scaling})",
                    "fqz_decoders": dict(zip(("general", "small"), _fqz_dec_counts(so))),
-                   "arena_bytes": [int(arena0), int(arena1)],
+                   # device bytes of the arenas' shared chunk pool (idle
+                   # chunks included): held before / after the timed steps
+                   # and the peak during them
+                   "arena_bytes": {"held_start": int(arena0), "held_end": int(arena1),
+                                   "peak": int(arena_pk)},
                    # candidates in the timed steps, and how many were provably
                    # losing and skipped their range chain (output unchanged)
                    "fqz_trial": {"tried": fq1[0] - fq0[0], "pruned": fq1[1] - fq0[1],

@@ -9,6 +9,9 @@
 #include <mutex>
 #include <cstdio>
 #include <string>
+#include <csignal>
+#include <execinfo.h>
+#include <unistd.h>
 
 #include "../../include/fqz5_mi355x.h"
 #include "rans_codec.hpp"
@@ -17,6 +20,24 @@
 #include "arith_kernels.h"
 #include "fqz_codec.hpp"
 #include "host_dec.hpp"
+
+// $FQZ5_SEGV_TRACE: on SIGSEGV print the native call stack (library offsets,
+// for llvm-symbolizer) before the default action (a diagnostic for faults in
+// host code, which the Python fault handler shows only as its own frames)
+namespace {
+void segv_trace(int sig) {
+    void *bt[64];
+    const int n = backtrace(bt, 64);
+    const char msg[] = "[fqz5] native stack at the fault:\n";
+    (void)!write(2, msg, sizeof msg - 1);
+    backtrace_symbols_fd(bt, n, 2);
+    std::signal(sig, SIG_DFL);
+    std::raise(sig);
+}
+__attribute__((constructor)) void segv_trace_install() {
+    if (std::getenv("FQZ5_SEGV_TRACE")) std::signal(SIGSEGV, segv_trace);
+}
+}  // namespace
 
 namespace fqz5 {
 
@@ -139,11 +160,7 @@ void gpu_release_all() {
             a->staging.reset();
         }
 }
-static uint64_t arena_bytes() {
-    uint64_t t = g_ctx ? g_ctx->arena.bytes() : 0;
-    for (auto &a : g_aux) t += a ? a->arena.bytes() : 0;
-    return t;
-}
+static uint64_t arena_bytes() { return ChunkPool::get().held(); }
 
 // Size a stream decodes to, from its header (needed when the caller did
 // not give an output buffer).  0 with ok=false if it cannot be known.
@@ -403,6 +420,7 @@ int fqz5_device_ok(void) {
 const char *fqz5_last_error(void) { return g_err.c_str(); }
 
 uint64_t fqz5_arena_bytes(void) { return arena_bytes(); }
+uint64_t fqz5_arena_peak(int reset) { return ChunkPool::get().peak(reset != 0); }
 
 unsigned fqz5_set_hot_min(unsigned min_events) { return fqz_set_hot_min(min_events); }
 

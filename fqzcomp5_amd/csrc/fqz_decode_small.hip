@@ -85,6 +85,12 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
 // set address in every lane.  Labels: 10/11 the top (11 past the wait),
 // 12 the slow exit, 20 the same-context tail, 40/41 renormalisation out of
 // line (back at 30/31), 60 a miss, 90 the exit.
+// The bubble test (tools/probe/dpp_probe.hip measured it on gfx950): with
+// row_shr:1, v_sub_u32_dpp d, x, x gives x[i-1] - x[i]; bound_ctrl:0 reads
+// 0 for lane 0 of a row, without it lane 0 keeps d.  So t4 = U_i - U_{i+1}
+// = -f(i) (f(i) the frequency of lane i's slot) and vsw = f(i) - f(i-1); a
+// decode in lane k >= 1 bubbles when f(k) + 16 > f(k-1), i.e. vsw > -16;
+// vsw's lane 0 stays INT_MIN (never).
 // gfx950 wait states kept by the order: a DPP read of a VGPR two VALU
 // instructions after its write; an SGPR written by the SALU and read as a
 // VALU mask two instructions later; a VGPR written by the VALU and read by
@@ -141,7 +147,7 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "s_waitcnt lgkmcnt(0)\n"                                                \
     "11:\n"                                                                 \
     "v_cmp_ne_u16_e32 vcc, %[c], v2\n"                                      \
-    "v_subrev_u32_dpp %[t4], %[vU], %[vU] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n" \
+    "v_sub_u32_dpp %[t4], %[vU], %[vU] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n" \
     "v_readlane_b32 %[u], %[pvv], m0\n"                                     \
     "v_lshrrev_b32 %[t6], 16, v2\n"                                         \
     DTU                                                                     \
@@ -153,7 +159,7 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "s_cbranch_vccnz 60f\n"                                                 \
     "v_bfe_u32 %[t0], v3, %[vsh4], 4\n"                                     \
     "v_fma_f64 %[d1], -%[d1], %[d2], 1.0\n"                                 \
-    "v_cmp_gt_i32_e64 %[SW], 16, %[vsw]\n"                                  \
+    "v_cmp_lt_i32_e64 %[SW], -16, %[vsw]\n"                                 \
     "v_cmp_lt_u32_e64 %[HV], %[c65503], %[t6]\n"                            \
     "v_fma_f64 %[d2], %[d2], %[d1], %[d2]\n"                                \
     "v_add_u32 %[t0], %[qs], %[t0]\n"                                       \
@@ -510,7 +516,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
             uint64_t mAS = 0;
             uint32_t cc = U(ctx), pv = U(prevq), ma = U(maddr);
             uint32_t dd = 0, nm = 0;
-            uint32_t vU = 0, vaddr = 0, vsw = l == 0 ? 0x7fffffffu : 0u;
+            uint32_t vU = 0, vaddr = 0, vsw = l == 0 ? 0x80000000u : 0u;
             uint64_t scr;
             const uint64_t back = reinterpret_cast<uint64_t>(J.back);
             rng = U(rng);

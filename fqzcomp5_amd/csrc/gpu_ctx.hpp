@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -29,14 +31,102 @@ struct GpuError : std::runtime_error {
                                    hipGetErrorString(e_));                    \
     } while (0)
 
-// Device memory arena.  Chunks are kept across batches; reset() rewinds.
+// Device memory: one process-wide pool of chunks shared by every context's
+// arena.  An arena takes chunks from the pool as it grows and gives them all
+// back at reset() (after its stream has drained), so the device footprint
+// is the peak of what the contexts use at the same time, not the sum of each
+// context's own peak.  Idle chunks beyond
+// $FQZ5_ARENA_IDLE_GB (default 16) go back to the device.
+class ChunkPool {
+  public:
+    static ChunkPool &get() {
+        static ChunkPool *p = new ChunkPool();   // never destroyed (thread exits use it)
+        return *p;
+    }
+    // a chunk of at least `need` bytes (its size in *got)
+    void *take(size_t need, size_t *got) {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            auto it = idle_.lower_bound(need);
+            if (it != idle_.end()) {
+                void *b = it->second;
+                *got = it->first;
+                idle_bytes_ -= it->first;
+                idle_.erase(it);
+                return b;
+            }
+        }
+        void *b = nullptr;
+        hipError_t e = hipMalloc(&b, need);
+        if (e != hipSuccess) {              // the idle chunks back to the device, once more
+            trim(0);
+            FQZ5_HIP(hipMalloc(&b, need));
+        }
+        std::lock_guard<std::mutex> lk(m_);
+        held_ += need;
+        peak_ = std::max(peak_, held_);
+        *got = need;
+        return b;
+    }
+    void give(void *b, size_t sz) {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            idle_.emplace(sz, b);
+            idle_bytes_ += sz;
+        }
+        if (idle_bytes_ > idle_cap()) trim(idle_cap());
+    }
+    void drop(void *b, size_t sz) {
+        (void)hipFree(b);
+        std::lock_guard<std::mutex> lk(m_);
+        held_ -= sz;
+    }
+    // idle chunks back to the device until at most `keep` bytes stay idle
+    void trim(size_t keep) {
+        std::vector<std::pair<size_t, void *>> out;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            while (idle_bytes_ > keep && !idle_.empty()) {
+                auto it = std::prev(idle_.end());        // the largest first
+                out.emplace_back(it->first, it->second);
+                idle_bytes_ -= it->first;
+                held_ -= it->first;
+                idle_.erase(it);
+            }
+        }
+        for (auto &c : out) (void)hipFree(c.second);
+    }
+    size_t held() { std::lock_guard<std::mutex> lk(m_); return held_; }
+    size_t peak(bool reset) {
+        std::lock_guard<std::mutex> lk(m_);
+        const size_t p = peak_;
+        if (reset) peak_ = held_;
+        return p;
+    }
+
+  private:
+    static size_t idle_cap() {
+        static const size_t c = [] {
+            const char *e = std::getenv("FQZ5_ARENA_IDLE_GB");
+            return size_t((e ? std::atof(e) : 16.0) * 1e9);
+        }();
+        return c;
+    }
+    std::mutex m_;
+    std::multimap<size_t, void *> idle_;
+    size_t idle_bytes_ = 0, held_ = 0, peak_ = 0;
+};
+
+// A bump arena over pool chunks; reset() rewinds and returns the chunks.
 class DevArena {
   public:
     ~DevArena() {
-        for (auto &c : chunks_) (void)hipFree(c.base);
+        for (auto &c : chunks_) ChunkPool::get().drop(c.base, c.size);
     }
-    void *alloc(size_t n, size_t align = 256) {
+    void *alloc(size_t n, size_t align = 256, const char *file = __builtin_FILE(),
+                int line = __builtin_LINE()) {
         if (n == 0) n = 1;
+        if (trace_on()) trace(n, file, line);
         for (; cur_ < chunks_.size(); cur_++) {
             Chunk &c = chunks_[cur_];
             size_t off = (c.used + align - 1) & ~(align - 1);
@@ -45,26 +135,33 @@ class DevArena {
                 return static_cast<uint8_t *>(c.base) + off;
             }
         }
-        size_t sz = n + align > (size_t(256) << 20) ? n + align : (size_t(256) << 20);
-        Chunk c{nullptr, sz, 0};
-        FQZ5_HIP(hipMalloc(&c.base, sz));
+        const size_t need = n + align > (size_t(256) << 20) ? n + align : (size_t(256) << 20);
+        Chunk c{nullptr, 0, 0};
+        c.base = ChunkPool::get().take(need, &c.size);
         chunks_.push_back(c);
         cur_ = chunks_.size() - 1;
         chunks_[cur_].used = n;
         return c.base;
     }
-    template <class T> T *alloc_n(size_t n) {
-        return static_cast<T *>(alloc(n * sizeof(T), alignof(T) > 256 ? alignof(T) : 256));
+    template <class T> T *alloc_n(size_t n, const char *file = __builtin_FILE(),
+                                  int line = __builtin_LINE()) {
+        return static_cast<T *>(alloc(n * sizeof(T), alignof(T) > 256 ? alignof(T) : 256, file,
+                                      line));
     }
+    // (only once nothing queued uses the arena any more)
     void reset() {
-        for (auto &c : chunks_) c.used = 0;
-        cur_ = 0;
-    }
-    // give every chunk back to the device (nothing may still use them)
-    void release() {
-        for (auto &c : chunks_) (void)hipFree(c.base);
+        if (trace_on()) trace_dump();
+        for (auto &c : chunks_) ChunkPool::get().give(c.base, c.size);
         chunks_.clear();
         cur_ = 0;
+    }
+    // every chunk and the pool's idle ones back to the device
+    void release() {
+        if (trace_on()) trace_dump();
+        for (auto &c : chunks_) ChunkPool::get().drop(c.base, c.size);
+        chunks_.clear();
+        cur_ = 0;
+        ChunkPool::get().trim(0);
     }
     // device bytes held (all chunks, used or not)
     size_t bytes() const {
@@ -77,6 +174,38 @@ class DevArena {
     struct Chunk { void *base; size_t size, used; };
     std::vector<Chunk> chunks_;
     size_t cur_ = 0;
+    // FQZ5_ARENA_TRACE=<MB>: per call site, the bytes taken between two
+    // resets, printed at the reset when their sum is at least <MB> (a
+    // diagnostic for the footprint per input byte)
+    std::vector<std::pair<std::string, size_t>> sites_;
+    static size_t trace_on() {
+        static const size_t mb = [] {
+            const char *e = std::getenv("FQZ5_ARENA_TRACE");
+            return e ? size_t(std::strtoull(e, nullptr, 10)) : size_t(0);
+        }();
+        return mb;
+    }
+    void trace(size_t n, const char *file, int line) {
+        const char *b = std::strrchr(file, '/');
+        std::string k = std::string(b ? b + 1 : file) + ":" + std::to_string(line);
+        for (auto &s : sites_)
+            if (s.first == k) { s.second += n; return; }
+        sites_.emplace_back(k, n);
+    }
+    void trace_dump() {
+        size_t tot = 0;
+        for (auto &s : sites_) tot += s.second;
+        if (tot >= (trace_on() << 20)) {
+            std::sort(sites_.begin(), sites_.end(),
+                      [](const auto &a, const auto &b) { return a.second > b.second; });
+            std::fprintf(stderr, "[arena] %.3f GB (pool %.3f GB, peak %.3f GB):", tot / 1e9,
+                         ChunkPool::get().held() / 1e9, ChunkPool::get().peak(false) / 1e9);
+            for (size_t i = 0; i < sites_.size() && i < 14; i++)
+                std::fprintf(stderr, " %s=%.3f", sites_[i].first.c_str(), sites_[i].second / 1e9);
+            std::fprintf(stderr, "\n");
+        }
+        sites_.clear();
+    }
 };
 
 // Pinned host staging: every host->device upload is first copied here so
@@ -238,6 +367,7 @@ struct GpuCtx {
     // Rewind both arenas; only after everything queued has completed.
     void reset() {
         sync();
+        if (stream2) FQZ5_HIP(hipStreamSynchronize(stream2));   // (its chunks go to the pool)
         arena.reset();
         staging.reset();
     }

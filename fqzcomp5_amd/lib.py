@@ -154,10 +154,19 @@ def device_ok() -> bool:
 
 
 def arena_bytes() -> int:
-    """Device bytes held by this thread's GPU arenas (fqz5_arena_bytes)."""
+    """Device bytes the arenas hold, process-wide (fqz5_arena_bytes)."""
     so = load()
     so.fqz5_arena_bytes.restype = C.c_uint64
     return int(so.fqz5_arena_bytes())
+
+
+def arena_peak(reset: bool = False) -> int:
+    """The most device bytes the arenas held since the last reset
+    (fqz5_arena_peak)."""
+    so = load()
+    so.fqz5_arena_peak.restype = C.c_uint64
+    so.fqz5_arena_peak.argtypes = [C.c_int]
+    return int(so.fqz5_arena_peak(1 if reset else 0))
 
 
 def header_symbols() -> list[str]:

@@ -273,10 +273,12 @@ int fqz5_unlzp(unsigned char *in, int in_len, unsigned char *out, int out_cap);
 /* Last error message of the calling thread ("" if none). */
 const char *fqz5_last_error(void);
 
-/* Device bytes held by the calling thread's arenas (its GPU context and
- * the helper context of fqz5_sections_try).  Constant from step to step of
- * a repeated workload once the first step has sized them. */
+/* Device bytes the arenas hold, process-wide: the chunks of every
+ * thread's contexts, in use or idle in the shared pool (at most
+ * $FQZ5_ARENA_IDLE_GB idle).  fqz5_arena_peak: the most held since the last
+ * fqz5_arena_peak(1) (reset: 1 starts a new peak from the current holding). */
 uint64_t fqz5_arena_bytes(void);
+uint64_t fqz5_arena_peak(int reset);
 
 /* Kernel timing with HIP events on fqz5_stream() (benchmark roofline).
  * fqz5_profile(1) resets and enables; fqz5_profile_read fills

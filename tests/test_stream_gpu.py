@@ -135,3 +135,25 @@ def test_l7_preset_blocks_equal_cli(tmp_path):
     os.unlink(src)
     fqz5file.decompress_file(dst, back)
     assert _md5(back) == rec["in_md5"]
+
+
+def test_l9_paired_preset_blocks_equal_cli(tmp_path):
+    """configs[4] at reduced size: two-file paired HiFi
+    (load_seqs_interleaved, fqzcomp5.c:627-865) at -9 with the preset's 1 GB
+    blocks (:4931), 2.28 GB in 3 blocks, through compress_file(src2=...):
+    equal to the reference's -9 -t1 r1 r2 output (its md5, recorded by
+    tests/golden/make_golden_l9_pairs.py), and decoded back to both files."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_golden_l9_pairs as G
+    rec = json.load(open(os.path.join(ROOT, "tests", "golden", "l9_pairs.json")))
+    r1, r2 = str(tmp_path / "r1.fastq"), str(tmp_path / "r2.fastq")
+    assert G.make_inputs(r1, r2) == (rec["r1_bytes"], rec["r2_bytes"])
+    dst = str(tmp_path / "pairs.fqz5")
+    assert fqz5file.compress_file(r1, dst, 9, src2=r2) == rec["out_bytes"]
+    assert _md5(dst) == rec["out_md5"]
+    os.unlink(r1)
+    os.unlink(r2)
+    b1, b2 = str(tmp_path / "b1.fastq"), str(tmp_path / "b2.fastq")
+    fqz5file.decompress_file(dst, b1, dst2=b2)
+    assert (_md5(b1), _md5(b2)) == (rec["r1_md5"], rec["r2_md5"])

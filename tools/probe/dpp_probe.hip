@@ -1,6 +1,6 @@
 // dpp_probe.hip — what the small fqz decoder's DPP sequence computes on the
-// hardware (tool, not product): f_i = U_i - U_{i-1} (row_shr:1, bound_ctrl),
-// d_i = f_{i-1} - f_i (row_shr:1, no bound_ctrl), SW = 16 > d (signed).
+// hardware (tool, not product): v_sub_u32_dpp row_shr:1 of U (bound_ctrl),
+// then of that (no bound_ctrl), SW = 16 > d (signed); measured: x[i-1] - x[i].
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -10,7 +10,7 @@ __global__ void k(const uint32_t *U, uint32_t *out) {
     uint32_t vU = U[l], t4 = 0, vsw = l == 0 ? 0x7fffffffu : 0u, t5 = 0;
     uint64_t SW;
     asm volatile(
-        "v_subrev_u32_dpp %[t4], %[vU], %[vU] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n"
+        "v_sub_u32_dpp %[t4], %[vU], %[vU] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n"
         "s_nop 4\n"
         "v_sub_u32_dpp %[vsw], %[t4], %[t4] row_shr:1 row_mask:0xf bank_mask:0xf\n"
         "s_nop 4\n"
