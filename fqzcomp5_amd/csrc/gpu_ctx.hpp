@@ -151,6 +151,11 @@ class DevArena {
     // (only once nothing queued uses the arena any more)
     void reset() {
         if (trace_on()) trace_dump();
+        if (!shared()) {                 // $FQZ5_ARENA_POOL=0: keep them (rewind only)
+            for (auto &c : chunks_) c.used = 0;
+            cur_ = 0;
+            return;
+        }
         for (auto &c : chunks_) ChunkPool::get().give(c.base, c.size);
         chunks_.clear();
         cur_ = 0;
@@ -174,6 +179,13 @@ class DevArena {
     struct Chunk { void *base; size_t size, used; };
     std::vector<Chunk> chunks_;
     size_t cur_ = 0;
+    static bool shared() {
+        static const bool on = [] {
+            const char *e = std::getenv("FQZ5_ARENA_POOL");
+            return !(e && e[0] == '0');
+        }();
+        return on;
+    }
     // FQZ5_ARENA_TRACE=<MB>: per call site, the bytes taken between two
     // resets, printed at the reset when their sum is at least <MB> (a
     // diagnostic for the footprint per input byte)

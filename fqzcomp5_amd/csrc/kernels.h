@@ -96,8 +96,18 @@ struct DecJob {
     // padding job of an XCD-grouped launch (exits at once).
     uint32_t nreg;
     uint32_t reg[8];
+    // O1 NX=4 with at most DEC_O1KEY_MAX (context, symbol) pairs, rows <= 8
+    // (bits 12) or 16 (bits <= 10): the replicated-state register decoder
+    // (rans_chain.hip dec4_o1reg_body).  okeys: 16 * (pairs / 16 rounded up)
+    // keys ctx << rowsh | start << 16 | (0xffff - ((f-1) << 4 | sym)), the
+    // last group padded with key 0; 0: not this decoder.
+    uint32_t okeys;
+    uint32_t rowsh;
+    uint32_t okey[64];
 };
 constexpr uint32_t DEC_REG_MAX = 8;
+constexpr uint32_t DEC_O1KEY_MAX = 64;
+constexpr uint32_t DEC_O1REG_LDS_BYTES = 16384;
 
 // Decoder table placement (rans_chain.hip).  Per slot of a row of 2^bits:
 //   LDS / GLOBAL  u32 (f-1) << (bits+8) | (slot - start) << 8 | symbol

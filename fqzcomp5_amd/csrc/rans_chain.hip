@@ -1153,6 +1153,166 @@ static DEV void dec4_lean_body(const DecJob &J) {
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// NX = 4, O1 with few (context, symbol) pairs: the replicated-state register
+// decoder.  State z lives in all 16 lanes of row z (lanes 16z..16z+15), each
+// lane holding up to 4 of the stream's keys
+//   K = ctx << rowsh | start << 16 | (0xffff - ((f-1) << 4 | sym))
+// (rowsh 29 for 12-bit slots and <= 8 contexts, 28 for <= 10 bits and <= 16).
+// With T = ctx << rowsh | slot << 16 | 0xffff, T - K is
+//   (slot - start) << 16 | (f-1) << 4 | sym   for the key of this context
+//                                              whose start is the largest <= slot,
+// below 2^(rowsh-1), and at least that for every other key (other contexts
+// differ in the top bits, a guard bit apart; larger starts wrap).  So one
+// subtraction per key held and a 16-lane minimum (4 DPP row rotations, every
+// lane of the row ending with it) give f, slot - start and the symbol, which
+// is the next context: no table read on the chain (the LDS table of the
+// general O1 path, ~220 cycles a step at -5, dec4_body).  rANS_static4x16pr.c
+// :525-821 (O1 decode), rANS_static16_int.h:468 (decode_freq1).
+// ---------------------------------------------------------------------------
+static DEV uint32_t row_min16(uint32_t d) {
+    // (DPP reads a VGPR two wait states after its VALU write)
+    asm volatile(
+        "s_nop 1\n"
+        "v_min_u32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_min_u32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_min_u32_dpp %0, %0, %0 row_ror:2 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_min_u32_dpp %0, %0, %0 row_ror:1 row_mask:0xf bank_mask:0xf\n"
+        : "+v"(d));
+    return d;
+}
+
+template <int NK>
+static DEV void dec4_o1reg_body(const DecJob &J) {
+    constexpr int NX = 4;
+    constexpr uint32_t G = O0_G;
+    static_assert(O0_RING_BYTES + 4 * G + 256 <= DEC_O1REG_LDS_BYTES, "o1reg LDS");
+    uint8_t *lds = reinterpret_cast<uint8_t *>(chain_lds);
+    uint16_t *ring = reinterpret_cast<uint16_t *>(lds);
+    uint8_t *obuf = lds + O0_RING_BYTES;                 // symbols, lane-major z*G + tt
+    uint8_t *a2b = obuf + 4 * G;                         // symbol index -> byte
+    const int l = int(threadIdx.x);
+    const uint32_t z = uint32_t(l) >> 4, jl = uint32_t(l) & 15u;
+    const uint32_t n = J.n;
+    const int bits = J.bits;
+    const uint32_t mask = (1u << bits) - 1;
+    const uint32_t rowsh = J.rowsh;
+    for (uint32_t i = l; i < J.rows; i += 64) a2b[i] = J.alpha[i];
+    uint32_t KEY[NK];
+#pragma unroll
+    for (int k = 0; k < NK; k++) KEY[k] = J.okey[16 * k + jl];
+    uint32_t x;
+    {
+        const uint8_t *p = J.in + 4 * z;
+        x = p[0] | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+    }
+    const uint32_t nwords = (J.in_len - 4 * uint32_t(NX)) / 2;
+    const auto wsrc = buf(J.in + 4 * NX, nwords * 2);
+    uint32_t slabs = 0;
+    uint4 pf = load_slab(wsrc, 0, l);
+    // lane z owns the bytes [z*isz, z*isz + lenz), the last the tail
+    // (rANS_static4x16pr.c:464-481)
+    const uint32_t isz = n / NX;
+    const uint32_t lenz = z == NX - 1 ? n - uint32_t(NX - 1) * isz : isz;
+    const uint32_t T = n - uint32_t(NX - 1) * isz;
+    const uint32_t Tfull = isz;
+    uint32_t ptr = 0;                                  // words consumed (same in every lane)
+    uint32_t rowb = 0xffffu;                           // context 0 at a segment start
+    const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(
+        (__attribute__((address_space(3))) uint16_t *)(ring)));
+    uint8_t *myob = obuf + z * G;
+    constexpr uint64_t LAST = 0x8000800080008000ull;   // lane 16z+15 of every row
+
+    for (uint32_t t0 = 0; t0 < T; t0 += G) {
+        while (slabs * SLAB_WORDS < ptr + 2560 && slabs * SLAB_WORDS < nwords + SLAB_WORDS) {
+            store_slab_o0(ring, slabs, l, pf);
+            slabs++;
+            pf = load_slab(wsrc, slabs, l);
+        }
+        __syncthreads();
+        const uint32_t hedge = hedge_claim(J, t0 / G);
+        const uint32_t gp = ptr;
+        const uint32_t wbase = ring_lds + 2 * ((gp & (RING_WORDS - 1)) - gp);
+        const uint32_t t1 = (T - t0 < G) ? T : t0 + G;
+        const uint32_t tf = t1 < Tfull ? t1 : (t0 > Tfull ? t0 : Tfull);
+        uint32_t t = t0;
+        for (; t + 16 <= tf; t += 16) {               // every state active
+            uint32_t a[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) {
+                const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
+                __builtin_amdgcn_sched_barrier(0);
+                const uint32_t Tk = ((x & mask) << 16) | rowb;
+                uint32_t d = Tk - KEY[0];
+#pragma unroll
+                for (int k = 1; k < NK; k++) d = min(d, Tk - KEY[k]);
+                const uint32_t xh = x >> bits;
+                d = row_min16(d);
+                const uint32_t xd = __umul24((d >> 4) & 0xfffu, xh) + (xh + (d >> 16));
+                rowb = (d << rowsh) | 0xffffu;
+                a[u] = d;
+                const bool c = xd < RANS_LOW_D;
+                const uint64_t m = __ballot(c) & LAST;
+                const uint32_t r16 = __builtin_amdgcn_mbcnt_hi(
+                    uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)) << 4;
+                const uint32_t w = uint32_t(win >> r16);
+                x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
+                ptr += uint32_t(__popcll(m));
+            }
+            if (jl == 0) {
+                uint32_t v[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    v[q] = (a[4 * q] & 15u) | (a[4 * q + 1] & 15u) << 8 |
+                           (a[4 * q + 2] & 15u) << 16 | (a[4 * q + 3] & 15u) << 24;
+                *reinterpret_cast<uint4 *>(myob + (t - t0)) = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+        }
+        // the rest of the group one step at a time; states past their bytes
+        // (all but the last one's tail) stand still
+        for (; t < t1; t++) {
+            const bool act = t < lenz;
+            const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
+            const uint32_t Tk = ((x & mask) << 16) | rowb;
+            uint32_t d = Tk - KEY[0];
+#pragma unroll
+            for (int k = 1; k < NK; k++) d = min(d, Tk - KEY[k]);
+            const uint32_t xh = x >> bits;
+            d = row_min16(d);
+            const uint32_t xd = __umul24((d >> 4) & 0xfffu, xh) + (xh + (d >> 16));
+            const bool c = act && xd < RANS_LOW_D;
+            const uint64_t m = __ballot(c) & LAST;
+            const uint32_t r16 = __builtin_amdgcn_mbcnt_hi(
+                uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)) << 4;
+            const uint32_t w = uint32_t(win >> r16);
+            if (act) {
+                x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
+                rowb = (d << rowsh) | 0xffffu;
+                if (jl == 0) myob[t - t0] = uint8_t(d & 15u);
+            }
+            ptr += uint32_t(__popcll(m));
+        }
+        ptr = __builtin_amdgcn_readfirstlane(ptr);
+        __syncthreads();
+        if (hedge_first(hedge, t0 / G)) {
+            const auto out = buf(J.out, n);
+            const uint32_t steps = t1 - t0, cnt = steps * NX;
+            for (uint32_t i = l; i < cnt; i += 64) {
+                const uint32_t zc = i / steps, tt = i % steps;
+                const uint32_t lz = (zc == NX - 1) ? n - uint32_t(NX - 1) * isz : isz;
+                if (t0 + tt < lz) st8(out, zc * isz + t0 + tt, a2b[obuf[zc * G + tt]]);
+            }
+        }
+        __syncthreads();
+        if (hedge_lost(hedge)) return;
+    }
+    if (l == 0) *J.status = (ptr <= nwords) ? 0 : -1;
+    hedge_won(J);
+}
+
 template <bool O1, int TM>
 static DEV void dec_any(const DecJob &J) {
     if (J.nx == 32) dec32_body<O1, TM>(J);
@@ -1200,7 +1360,14 @@ __global__ __launch_bounds__(64) void k_rans_dec(const DecJob *jobs) {
     } end_{jt0, jc0, J};
 #endif
     const int tm = int(J.mode);
-    if (J.alpha != nullptr) {
+    if (J.alpha != nullptr && J.okeys) {
+        switch (J.okeys >> 4) {
+        case 1: dec4_o1reg_body<1>(J); break;
+        case 2: dec4_o1reg_body<2>(J); break;
+        case 3: dec4_o1reg_body<3>(J); break;
+        default: dec4_o1reg_body<4>(J);
+        }
+    } else if (J.alpha != nullptr) {
         if (tm == DEC_TAB_LDS) dec_any<true, DEC_TAB_LDS>(J);
         else if (tm == DEC_TAB_SPLIT) dec_any<true, DEC_TAB_SPLIT>(J);
         else dec_any<true, DEC_TAB_GLOBAL>(J);

@@ -299,6 +299,40 @@ static bool xcd_grouping() {
     return on;
 }
 
+// The O1 register decoder's keys (rans_chain.hip dec4_o1reg_body): every
+// context row complete (its frequencies cover the 2^bits slots), at most 8
+// contexts with 12-bit slots or 16 with <= 10, at most DEC_O1KEY_MAX (context,
+// symbol) pairs.  $FQZ5_NO_O1REG: the table decoders instead.
+static bool o1reg_decoder() {
+    static const bool on = std::getenv("FQZ5_NO_O1REG") == nullptr;
+    return on;
+}
+static bool o1_keys(const DJ &j, DecJob &d) {
+    const uint32_t rows = uint32_t(j.alpha.size()), M = 1u << j.bits;
+    if (j.bits > 12 || rows > (j.bits == 12 ? 8u : 16u)) return false;
+    const uint32_t rowsh = j.bits == 12 ? 29u : 28u;
+    uint32_t nk = 0;
+    for (uint32_t r = 0; r < rows; r++) {
+        const uint32_t *F = &j.F[size_t(r) * 256];
+        uint32_t x = 0;
+        for (uint32_t s = 0; s < 256; s++) {
+            if (!F[s]) continue;
+            const auto it = std::lower_bound(j.alpha.begin(), j.alpha.end(), uint8_t(s));
+            if (it == j.alpha.end() || *it != s || nk >= DEC_O1KEY_MAX || F[s] > M) return false;
+            const uint32_t sym = uint32_t(it - j.alpha.begin());
+            d.okey[nk++] = r << rowsh | x << 16 | (0xffffu - ((F[s] - 1) << 4 | sym));
+            x += F[s];
+        }
+        if (x != M) return false;
+    }
+    if (!nk) return false;
+    const uint32_t nk16 = (nk + 15) & ~15u;
+    for (uint32_t k = nk; k < nk16; k++) d.okey[k] = d.okey[0];
+    d.okeys = nk16;
+    d.rowsh = rowsh;
+    return true;
+}
+
 void Decompressor::run_djs(const std::vector<int> &ids) {
     std::vector<uint32_t> tabs;
     std::vector<uint8_t> alphas;
@@ -388,6 +422,8 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
             }
             if (k2 >= 1 && k2 <= DEC_REG_MAX && x == (1u << j.bits)) d.nreg = k2;
         }
+        if (j.o1 && j.nx == 4 && o1reg_decoder() && o1_keys(j, djs.back()))
+            lds = std::max(lds, DEC_O1REG_LDS_BYTES);
         bytes += double(j.n) + (j.len - j.tab_len);
         lds = std::max(lds, dec_lds_bytes(rows, j.bits, int(mode)));
     }

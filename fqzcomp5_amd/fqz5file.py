@@ -223,6 +223,25 @@ def _index(offs, bases, nrec) -> bytes:
 # exclusive scan; rank 0 writes the header and the index.
 # ---------------------------------------------------------------------------
 DEFAULT_WINDOW = 2_000_000_000
+# Device bytes the encode of a window takes per input byte, by level (the
+# arenas' pool peak over the input size, bench.py's arena_bytes.peak): the
+# candidates' outputs and the fqz / sequence-model event tables of the trial
+# blocks dominate.
+FOOTPRINT = {1: 24, 2: 24, 3: 40, 4: 40, 5: 64, 6: 64, 7: 64, 8: 64, 9: 64}
+
+
+def window_bytes_for(level: int, blk: int, ws: int = 1, hbm: int | None = None) -> int:
+    """The encode window: as much input as fits 0.8 x HBM at the level's
+    footprint on every rank (each codes about window / ws of it), at least
+    two blocks per rank and one over (the last block of a window waits for
+    the next), at most 8 GB per rank."""
+    if hbm is None:
+        import torch
+        hbm = torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory \
+            if torch.cuda.is_available() else 64 << 30
+    per_rank = int(0.8 * hbm) // FOOTPRINT.get(level, 64)
+    per_rank = min(per_rank, 8_000_000_000)
+    return max(ws * per_rank, 2 * ws * blk + blk)
 
 
 class _Src:
@@ -232,12 +251,14 @@ class _Src:
     def __init__(self, path: str | None = None, data: bytes | None = None):
         import gzip
         import io
+        self.path, self.gz = path, False
         if data is not None:
             self.f = io.BytesIO(data)
         else:
             with open(path, "rb") as f:
                 magic = f.read(2)
-            self.f = gzip.open(path, "rb") if magic == b"\x1f\x8b" else open(path, "rb")
+            self.gz = magic == b"\x1f\x8b"
+            self.f = gzip.open(path, "rb") if self.gz else open(path, "rb")
         self.buf = bytearray()
         self.eof = False
 
@@ -354,6 +375,7 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
             if s.buf:
                 cpu = torch.frombuffer(s.buf, dtype=torch.uint8)
                 d = cpu.to(device)            # blocking (pageable): done before the parse
+                H2D[0] += int(cpu.numel())
                 del cpu
             else:
                 d = torch.empty(0, dtype=torch.uint8, device=device)
@@ -411,91 +433,425 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
         return W
 
 
-def _encode_stream(srcs: list, sink: _Sink, level: int, blk_size: int | None, device: str,
-                   group=None, window_bytes: int | None = None) -> int:
-    """The sources' FASTQ -> .fqz5 written through `sink` (see above);
-    returns the file size."""
+# ---------------------------------------------------------------------------
+# Windows read once over the ranks (plain files, several ranks).  The window
+# [P, P + Wn) of each input is cut into one byte range per rank; each rank
+# reads and uploads only its range (and the byte before it), counts its
+# newlines on the GPU, and after one exchange of the counts knows which of
+# its line starts are record starts (FASTQ: every 4th line from the window
+# start; FASTA: a '>' line).  It parses the records that start in its range
+# (fqz5_fastq_index), and a second exchange gives every rank every record's
+# start, load_seqs_kseq size, name-section and sequence bytes: the block
+# split (fqz5_fastq_blocks) is then computed alike on every rank.  A block
+# belongs to the rank holding its first record; a rank then gathers its own
+# blocks (and the trial blocks whose work candidates it shares) from the text
+# it already holds, reading from the file only the bytes it lacks (the end of
+# its last block, other ranks' trial blocks).  Reference: load_seqs_kseq's
+# split, fqzcomp5.c:423-623; dispatch :3051-3120.
+# ---------------------------------------------------------------------------
+H2D = [0]          # input text bytes this process uploaded (tests, bench)
+
+
+def _upload(buf, device: str):
     import torch
-    so = _load()
+    a = np.frombuffer(buf, np.uint8) if not isinstance(buf, np.ndarray) else buf
+    H2D[0] += int(a.size)
+    if not a.size:
+        return torch.empty(0, dtype=torch.uint8, device=device)
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+class _PosFile:
+    """A plain input file read at positions."""
+
+    def __init__(self, path: str):
+        import os
+        self.fd = os.open(path, os.O_RDONLY)
+        self.size = os.fstat(self.fd).st_size
+
+    def read(self, a: int, b: int) -> np.ndarray:
+        import os
+        out = np.empty(max(b - a, 0), np.uint8)
+        got = 0
+        while got < out.size:
+            c = os.pread(self.fd, out.size - got, a + got)
+            if not c:
+                raise _lib.NativeError("input file shrank while being read")
+            out[got:got + len(c)] = np.frombuffer(c, np.uint8)
+            got += len(c)
+        return out
+
+    def close(self) -> None:
+        import os
+        os.close(self.fd)
+
+
+def _allgather_np(x, group):
+    return _allgather_obj(x, group)
+
+
+def _record_end(f: _PosFile, s: int, fasta: bool) -> int:
+    """End (exclusive) of the record starting at file offset s: FASTQ after
+    its 4th line, FASTA before the next '>' line; the end of the file closes
+    the last record."""
+    need, at, piece = 4, s, 1 << 16
+    while at < f.size:
+        b = f.read(at, min(f.size, at + piece))
+        if fasta:
+            hit = np.flatnonzero((b[:-1] == 10) & (b[1:] == ord(">")))
+            if hit.size:
+                return at + int(hit[0]) + 1
+            at += max(b.size - 1, 1)
+        else:
+            nl = np.flatnonzero(b == 10)
+            if nl.size >= need:
+                return at + int(nl[need - 1]) + 1
+            need -= nl.size
+            at += b.size
+        piece *= 2
+    return f.size
+
+
+class _Scan:
+    """One input's window scanned over the ranks (see above)."""
+    pass
+
+
+def _scan(f: _PosFile, P: int, Wn: int, device: str, group, fasta=None) -> _Scan:
+    import torch
     ws, rk = S._world(group)
-    blk = blk_size or S.BLOCK_SIZE[level]
-    # a window holds several blocks per rank, so that every GPU has blocks
-    # whose serial chains run side by side
-    wbytes = window_bytes or max(DEFAULT_WINDOW, 2 * ws * blk + blk)
-    av = S.masks(level, full=True)
-    state = S.new_state()
-    pos = 16                                  # file offset of the next block
-    index = []
+    lo, hi = P + rk * Wn // ws, P + (rk + 1) * Wn // ws
+    # bytes [lo - 1, hi): the byte before the range decides whether lo
+    # starts a line (a newline stands in before the window start)
+    h = f.read(max(lo - 1, P), hi)
+    if lo == P:
+        h = np.concatenate([np.array([10], np.uint8), h])
+    t = _upload(h, device)
+    n = hi - lo
+    nl = (t[:n] == 10) if n else torch.zeros(0, dtype=torch.bool, device=device)
+    head = int(t[1].item()) if rk == 0 and t.numel() > 1 else -1
+    cnt = int(nl.sum().item()) if n else 0
+    got = _allgather_np((cnt, head), group)
+    if fasta is None:
+        fasta = got[0][1] == ord(">")
+    base = sum(c for c, _ in got[:rk])
+    if n:
+        if fasta:
+            st = nl & (t[1:n + 1] == ord(">"))
+        else:
+            # (an '@' line: blank lines after the last record start none)
+            line = torch.cumsum(nl.to(torch.int64), 0) + (base - 1)
+            st = nl & (line % 4 == 0) & (t[1:n + 1] == ord("@"))
+        starts = (st.nonzero().flatten() + lo).cpu().numpy().astype(np.int64)
+    else:
+        starts = np.zeros(0, np.int64)
+    firsts = _allgather_np(int(starts[0]) if starts.size else -1, group)
+    # the end of this rank's last record: the next rank's first start, or
+    # (the window's last record) found by reading on
+    nxt = [x for x in firsts[rk + 1:] if x >= 0]
+    sc = _Scan()
+    sc.fasta = fasta
+    sc.lo = int(starts[0]) if starts.size else hi
+    if starts.size:
+        end = nxt[0] if nxt else _record_end(f, int(starts[-1]), fasta)
+        text = t[int(starts[0]) - (lo - 1):]
+        if end > hi:
+            text = torch.cat([text, _upload(f.read(hi, end), device)])
+        else:
+            text = text[:end - int(starts[0])]
+        sc.hi = end
+        recs, rsz, nrec, fa = _index_text(text, 0, int(text.numel()))
+        if nrec != starts.size:
+            raise _lib.NativeError("window scan: the record parse disagrees with the line count")
+        w = C.sizeof(FastqRec)
+        u = recs.view(nrec, w)[:, 32:44].contiguous().view(torch.int32).view(nrec, 3).cpu().numpy()
+        nsz = (u[:, 0] + np.where(u[:, 1] > 0, u[:, 1] + 1, 0) + 1).astype(np.uint64)
+        slen = u[:, 2].astype(np.uint64)
+    else:
+        text, sc.hi = t[:0], hi
+        rsz = np.zeros(0, np.uint32)
+        nsz = slen = np.zeros(0, np.uint64)
+    del t, nl
+    sc.text = text                       # this rank's records' text, [lo, hi) of the file
+    parts = _allgather_np((starts, rsz.astype(np.uint32), nsz, slen, sc.hi), group)
+    sc.start = np.concatenate([p[0] for p in parts]).astype(np.int64)
+    sc.rsz = np.concatenate([p[1] for p in parts]).astype(np.uint32)
+    sc.nsz = np.concatenate([p[2] for p in parts]).astype(np.uint64)
+    sc.slen = np.concatenate([p[3] for p in parts]).astype(np.uint64)
+    counts = [len(p[0]) for p in parts]
+    sc.rank_of = np.repeat(np.arange(ws), counts)
+    ends = [p[4] for p in parts if len(p[0])]
+    sc.end = np.append(sc.start[1:], ends[-1] if ends else P).astype(np.int64)   # per record
+    sc.n = int(sc.start.size)
+    return sc
+
+
+def _need_text(f: _PosFile, sc: _Scan, ranges, device: str):
+    """The text of the byte ranges (file order, disjoint) as one device
+    buffer: the parts this rank holds from its scan sliced, the rest read."""
+    import torch
+    pieces = []
+    for a, e in ranges:
+        x0, x1 = max(a, sc.lo), min(e, sc.hi)
+        if x0 < x1:
+            if a < x0:
+                pieces.append(_upload(f.read(a, x0), device))
+            pieces.append(sc.text[x0 - sc.lo:x1 - sc.lo])
+            if x1 < e:
+                pieces.append(_upload(f.read(x1, e), device))
+        else:
+            pieces.append(_upload(f.read(a, e), device))
+    if not pieces:
+        return torch.empty(0, dtype=torch.uint8, device=device)
+    return torch.cat(pieces) if len(pieces) > 1 else pieces[0]
+
+
+def _merge(ranges):
+    out = []
+    for a, e in ranges:
+        if out and out[-1][1] == a:
+            out[-1] = (out[-1][0], e)
+        else:
+            out.append((a, e))
+    return out
+
+
+class _RankWindow:
+    """A window read once over the ranks: the per-block fields every rank
+    knows, and gather() for the blocks this rank codes or tries."""
+
+    def __init__(self, files, pos, scans, k, first, keep, final, group, device):
+        ws, rk = S._world(group)
+        self.files, self.pos, self.scans, self.device = files, pos, scans, device
+        self.paired = len(files) == 2
+        self.first, self.nb, self.final = first, keep, final
+        mul = 2 if self.paired else 1
+        fa = scans[0].fasta
+        self.text_fasta = fa
+        self.fasta, self.name_bytes, self.seq_bytes, self.nrec, self.owner = [], [], [], [], []
+        for b in range(keep):
+            a, e = int(first[b]) // mul, int(first[b + 1]) // mul
+            self.fasta.append(fa or int(scans[0].slen[a]) == 0)
+            self.name_bytes.append(int(sum(int(s.nsz[a:e].sum()) for s in scans)))
+            self.seq_bytes.append(int(sum(int(s.slen[a:e].sum()) for s in scans)))
+            self.nrec.append((e - a) * mul)
+            self.owner.append(int(scans[0].rank_of[a]))
+        self.owner = np.array(self.owner, np.int64)
+        # the next window starts at block `keep` (R1 and R2 at the same pair)
+        if keep < len(first) - 1:
+            r = int(first[keep]) // mul
+            self.next_pos = [int(s.start[r]) for s in scans]
+        else:
+            self.next_pos = [int(s.end[k - 1]) if k else p for s, p in zip(scans, pos)]
+
+    def gather(self, need):
+        """A sections.Run of the blocks `need` (in that order)."""
+        import torch
+        mul = 2 if self.paired else 1
+        texts, lens = [], []
+        for f, sc in zip(self.files, self.scans):
+            rng = []
+            for b in need:
+                a, e = int(self.first[b]) // mul, int(self.first[b + 1]) // mul
+                rng.append((int(sc.start[a]), int(sc.end[e - 1])))
+            t = _need_text(f, sc, _merge(rng), self.device)
+            texts.append(t)
+            lens.append(int(t.numel()))
+        nrecs = [self.nrec[b] for b in need]
+        loc = np.concatenate([[0], np.cumsum(nrecs)]).astype(np.int64)
+        if not self.paired:
+            text_d = texts[0]
+            recs, _, nrec, _ = _index_text(text_d, 0, lens[0])
+        else:
+            text_d = torch.cat(texts) if lens[1] else texts[0]
+            r1, _, n1, _ = _index_text(text_d, 0, lens[0])
+            r2, _, n2, _ = _index_text(text_d, lens[0], lens[1])
+            if n1 != n2:
+                raise _lib.NativeError("window gather: R1 and R2 record counts differ")
+            w = C.sizeof(FastqRec)
+            recs = torch.stack([r1.view(n1, w), r2.view(n2, w)], 1).reshape(-1) if n1 else r1
+            nrec = 2 * n1
+        if nrec != int(loc[-1]):
+            raise _lib.NativeError("window gather: record count differs from the scan")
+        run = _gather_ranges(text_d, recs, [(int(loc[j]), int(loc[j + 1]))
+                                            for j in range(len(need))],
+                             self.text_fasta, self.paired)
+        for j, b in enumerate(need):          # the scan's sizes are the ones coded
+            i = run.blk_sec0[j]
+            if (run.spans[i][2] - run.spans[i][1], run.spans[i + 1][2] - run.spans[i + 1][1]) != \
+                    (self.name_bytes[b], self.seq_bytes[b]):
+                raise _lib.NativeError("window gather: section sizes differ from the scan")
+        return run
+
+    def advance(self):
+        self.pos[:] = self.next_pos
+
+
+def _next_window_ranks(files, pos, blk: int, wbytes: int, device: str, group):
+    """The next window of the inputs at file offsets `pos`, read once over
+    the ranks; None at the end of the input."""
+    so = _load()
+    paired = len(files) == 2
+    want = wbytes
+    if pos[0] >= files[0].size:
+        return None
     while True:
-        W = _next_window(srcs, blk, wbytes, device)
-        if W is None:
-            break
+        wn = [min(want, f.size - p) for f, p in zip(files, pos)]
+        eof = [p + w >= f.size for f, p, w in zip(files, pos, wn)]
+        scans = [_scan(files[0], pos[0], wn[0], device, group)]
+        if paired:
+            scans.append(_scan(files[1], pos[1], wn[1], device, group))
+            if scans[0].n and scans[1].n and scans[0].fasta != scans[1].fasta:
+                raise _lib.NativeError("paired files: one FASTA, one FASTQ")
+        k = min(s.n for s in scans)
+        r1_done = eof[0] and k == scans[0].n
+        if paired and not r1_done and eof[1] and k == scans[1].n:
+            raise _lib.NativeError("unpaired read detected: R2 file ended before R1")
+        if k == 0:
+            if r1_done:
+                return None
+            want *= 2
+            continue
+        if paired:
+            pair = scans[0].rsz[:k].astype(np.uint64) + scans[1].rsz[:k].astype(np.uint64)
+            if int(pair.max()) >= 2 ** 32:
+                raise _lib.NativeError("paired record larger than 4 GB")
+            first = _blocks(so, pair.astype(np.uint32), blk) * 2
+        else:
+            first = _blocks(so, scans[0].rsz[:k], blk)
+        nb = len(first) - 1
+        keep = nb if r1_done else nb - 1
+        if keep <= 0:
+            want *= 2
+            continue
+        return _RankWindow(files, pos, scans, k, first, keep, bool(r1_done and keep == nb),
+                           group, device)
+
+
+class _LocalWindow:
+    """A window every rank reads whole (one rank, or gzip / in-memory
+    input): the same per-block fields as _RankWindow."""
+
+    def __init__(self, W, srcs, ws):
+        so = _load()
+        self.W, self.srcs = W, srcs
         nb = len(W.first) - 1
-        # per block: its records, section input sizes (fqz5_fastq_gather's
-        # sizing pass), the sections in encode_block order (no quality
-        # section in a FASTA block)
-        bfa = _fasta_blocks(W.recs, [int(W.first[b]) for b in range(nb)], W.fasta)
-        per = [2 if f else 3 for f in bfa]
-        sec0 = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
-        ids, ins, bases, nrec = [], [], [], []
+        self.nb, self.final = nb, W.final
+        self.fasta = _fasta_blocks(W.recs, [int(W.first[b]) for b in range(nb)], W.fasta)
+        self.name_bytes, self.seq_bytes, self.nrec = [], [], []
         for b in range(nb):
             a, e = int(W.first[b]), int(W.first[b + 1])
             sz = (C.c_uint64 * 3)()
             _check(so.fqz5_fastq_gather(W.text_d.data_ptr(), W.recs.data_ptr(), a, e, None,
                                         None, None, None, None, sz), "fqz5_fastq_gather")
-            ids += [S.SEC_NAME, S.SEC_SEQ] + ([] if bfa[b] else [S.SEC_QUAL])
-            ins += [int(sz[0]), int(sz[1])] + ([] if bfa[b] else [int(sz[1])])
-            bases.append(int(sz[1]))
-            nrec.append(e - a)
-        ids = np.array(ids, np.int32)
-        ins = np.array(ins, np.uint32)
-        blk_owner = (np.arange(nb) * ws) // nb
-        owner = np.repeat(blk_owner, per)
-        sched = S.trial_schedule(ids, av, state)
-        need = sorted({b for b in range(nb)
-                       if blk_owner[b] == rk or sched[sec0[b]:sec0[b + 1]].any()})
-        # the needed blocks' section inputs, gathered in HBM
-        run = _gather_ranges(W.text_d, W.recs, [(int(W.first[b]), int(W.first[b + 1]))
-                                                for b in need], W.fasta, W.pairs)
-        secs = [None] * int(sec0[-1])
-        local = run.enc_secs()
-        for j, b in enumerate(need):
-            for q in range(per[b]):
-                secs[sec0[b] + q] = local[run.blk_sec0[j] + q]
-        res, meth, _ = S.encode_window(secs, ids, ins, owner, av, state, group,
-                                       bounded=level >= 7, final=W.final)
-        mine = [j for j, b in enumerate(need) if blk_owner[b] == rk]
-        full_res = [None] * len(local)
-        for j, b in enumerate(need):
-            for q in range(per[b]):
-                full_res[run.blk_sec0[j] + q] = res[sec0[b] + q]
-        for j in mine:
-            for q in range(per[need[j]]):
-                r = full_res[run.blk_sec0[j] + q]
-                if r is None or r.status != 0:
-                    raise _lib.NativeError("section coding failed: " + _lib.last_error())
-        sizes = []
-        if mine:
-            run.assemble(full_res, mine)
-            sizes = [int(run.blk_off[i + 1] - run.blk_off[i]) for i in range(len(mine))]
-        all_sizes = _allgather_obj(sizes, group)
-        # blocks in file order: rank-contiguous, so rank-major order
-        flat = [z for zs in all_sizes for z in zs]
-        assert len(flat) == nb
-        starts = np.concatenate([[0], np.cumsum(flat)]).astype(np.int64) + pos
-        if mine:
-            end = int(run.blk_off[len(mine)])
-            host = _pinned(end)
-            host.copy_(run.blk_buf[:end])
-            b0 = need[mine[0]]
-            sink.write_at(int(starts[b0]), host.numpy())
-            del host
-        for b in range(nb):
-            index.append((int(starts[b]), bases[b], nrec[b]))
-        pos = int(starts[-1])
-        for s, c in zip(srcs, W.consume):
+            self.name_bytes.append(int(sz[0]))
+            self.seq_bytes.append(int(sz[1]))
+            self.nrec.append(e - a)
+        self.owner = (np.arange(nb) * ws) // nb
+
+    def gather(self, need):
+        W = self.W
+        return _gather_ranges(W.text_d, W.recs, [(int(W.first[b]), int(W.first[b + 1]))
+                                                 for b in need], W.fasta, W.pairs)
+
+    def advance(self):
+        for s, c in zip(self.srcs, self.W.consume):
             s.advance(c)
-        del run, W
+
+
+def _code_window(W, sink: _Sink, level: int, pos: int, index: list, av, state, group) -> int:
+    """Code the window's blocks over the ranks and write them at file
+    offset `pos` on (see above); appends their index entries and returns
+    the offset after them."""
+    ws, rk = S._world(group)
+    nb = W.nb
+    # per block the sections in encode_block order (no quality section in a
+    # FASTA block)
+    per = [2 if f else 3 for f in W.fasta]
+    sec0 = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
+    ids, ins = [], []
+    for b in range(nb):
+        ids += [S.SEC_NAME, S.SEC_SEQ] + ([] if W.fasta[b] else [S.SEC_QUAL])
+        ins += [W.name_bytes[b], W.seq_bytes[b]] + ([] if W.fasta[b] else [W.seq_bytes[b]])
+    ids = np.array(ids, np.int32)
+    ins = np.array(ins, np.uint32)
+    blk_owner = np.asarray(W.owner, np.int64)
+    owner = np.repeat(blk_owner, per)
+    sched = S.trial_schedule(ids, av, state)
+    need = sorted({b for b in range(nb)
+                   if blk_owner[b] == rk or sched[sec0[b]:sec0[b + 1]].any()})
+    # the needed blocks' section inputs, gathered in HBM
+    run = W.gather(need)
+    secs = [None] * int(sec0[-1])
+    local = run.enc_secs()
+    for j, b in enumerate(need):
+        for q in range(per[b]):
+            secs[sec0[b] + q] = local[run.blk_sec0[j] + q]
+    res, meth, _ = S.encode_window(secs, ids, ins, owner, av, state, group,
+                                   bounded=level >= 7, final=W.final)
+    mine = [j for j, b in enumerate(need) if blk_owner[b] == rk]
+    full_res = [None] * len(local)
+    for j, b in enumerate(need):
+        for q in range(per[b]):
+            full_res[run.blk_sec0[j] + q] = res[sec0[b] + q]
+    for j in mine:
+        for q in range(per[need[j]]):
+            r = full_res[run.blk_sec0[j] + q]
+            if r is None or r.status != 0:
+                raise _lib.NativeError("section coding failed: " + _lib.last_error())
+    sizes = []
+    if mine:
+        run.assemble(full_res, mine)
+        sizes = [int(run.blk_off[i + 1] - run.blk_off[i]) for i in range(len(mine))]
+    all_sizes = _allgather_obj(sizes, group)
+    # blocks in file order: rank-contiguous, so rank-major order
+    flat = [z for zs in all_sizes for z in zs]
+    assert len(flat) == nb
+    starts = np.concatenate([[0], np.cumsum(flat)]).astype(np.int64) + pos
+    if mine:
+        end = int(run.blk_off[len(mine)])
+        host = _pinned(end)
+        host.copy_(run.blk_buf[:end])
+        b0 = need[mine[0]]
+        sink.write_at(int(starts[b0]), host.numpy())
+        del host
+    for b in range(nb):
+        index.append((int(starts[b]), W.seq_bytes[b], W.nrec[b]))
+    return int(starts[-1])
+
+
+def _encode_stream(srcs: list, sink: _Sink, level: int, blk_size: int | None, device: str,
+                   group=None, window_bytes: int | None = None) -> int:
+    """The sources' FASTQ -> .fqz5 written through `sink` (see above);
+    returns the file size."""
+    ws, rk = S._world(group)
+    blk = blk_size or S.BLOCK_SIZE[level]
+    # a window holds several blocks per rank, so that every GPU has blocks
+    # whose serial chains run side by side
+    wbytes = window_bytes or window_bytes_for(level, blk, ws)
+    av = S.masks(level, full=True)
+    state = S.new_state()
+    pos = 16                                  # file offset of the next block
+    index = []
+    # several ranks on plain files: each reads its share of every window once
+    files = [_PosFile(s.path) for s in srcs] \
+        if ws > 1 and all(s.path and not s.gz for s in srcs) else None
+    at = [0] * len(srcs)
+    try:
+        while True:
+            if files:
+                W = _next_window_ranks(files, at, blk, wbytes, device, group)
+            else:
+                w0 = _next_window(srcs, blk, wbytes, device)
+                W = _LocalWindow(w0, srcs, ws) if w0 is not None else None
+            if W is None:
+                break
+            pos = _code_window(W, sink, level, pos, index, av, state, group)
+            W.advance()
+            del W
+    finally:
+        for f in files or []:
+            f.close()
     if rk == 0:
         if index:
             idx = _index([o for o, _, _ in index], [b for _, b, _ in index],

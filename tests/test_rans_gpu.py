@@ -162,3 +162,29 @@ def test_hedged_launches_same_bytes():
         assert fq[0] == fq[1]
     finally:
         so.fqz5_set_hedge(prev)
+
+
+def test_o1_register_decoder_alphabets():
+    """The O1 register decoder (rans_chain.hip dec4_o1reg_body: <= 8
+    contexts at 12-bit slots, <= 16 at 10, <= 64 (context, symbol) pairs)
+    against the oracle's streams: alphabets of 1-16 symbols, skewed and
+    flat, lengths with every tail n % 4 and inputs short enough for 10-bit
+    slots, with RLE / PACK in front."""
+    from fqzcomp5_amd import synth
+    ora = binding.oracle()
+    rng = np.random.default_rng(77)
+    q = synth.novaseq(30000, seed=4).qual
+    cases = [q.tobytes(), q[:100003].tobytes(), q[:4097].tobytes()]
+    for nsym in (1, 2, 3, 4, 5, 7, 8, 11, 16):
+        alpha = rng.choice(np.arange(1, 90), nsym, replace=False)
+        p = rng.dirichlet(np.full(nsym, 0.4))
+        for n in (5, 63, 1001, 65538, 400001):
+            cases.append(rng.choice(alpha, n, p=p).astype(np.uint8).tobytes())
+    bad = []
+    for d in cases:
+        for o in (1, 65, 129, 193):
+            c = ora.rans_compress(d, o)
+            got = _or_none(lib.rans_uncompress, c)
+            if got != d:
+                bad.append((len(d), hex(o), len(set(d))))
+    assert not bad, bad[:20]

@@ -72,13 +72,15 @@ def _rank(rank, world, port, args, q):
     torch.cuda.init()
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        src, dst, back, level = args
+        src, dst, back, level, wb = args
+        fqz5file.H2D[0] = 0
         n = fqz5file.compress_file(src, dst, level, blk_size=1_000_000, group=dist.group.WORLD,
-                                   window_bytes=6_000_000)
+                                   window_bytes=wb)
+        h2d = fqz5file.H2D[0]
         m = fqz5file.decompress_file(dst, back, group=dist.group.WORLD, window_bytes=1_000_000)
-        q.put((rank, n, m, None))
+        q.put((rank, n, m, h2d, None))
     except Exception as e:  # noqa: BLE001 - reported to the parent
-        q.put((rank, 0, 0, repr(e)))
+        q.put((rank, 0, 0, 0, repr(e)))
     finally:
         dist.destroy_process_group()
 
@@ -91,24 +93,70 @@ def _free_port():
 
 @pytest.mark.parametrize("level", [5, 7])
 def test_two_ranks_equal_one_process(tmp_path, level):
+    """Two ranks write the one-process file byte for byte, each reading its
+    share of every window once: a rank's host-to-device
+    text is at most 0.6 x the file (its half, the trial blocks it shares,
+    the ends of its last blocks), and the file decodes back on two ranks."""
     src = str(tmp_path / "in.fastq")
-    _illumina(src, n=50000, seed=31)
+    _illumina(src, n=300000, seed=31)
+    size = os.path.getsize(src)
     one, two, back = (str(tmp_path / x) for x in ("one.fqz5", "two.fqz5", "back.fastq"))
     fqz5file.compress_file(src, one, level, blk_size=1_000_000)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_rank, args=(r, 2, port, (src, two, back, level), q))
+    ps = [ctx.Process(target=_rank, args=(r, 2, port, (src, two, back, level, 40_000_000), q))
           for r in range(2)]
     for p in ps:
         p.start()
-    out = [q.get(timeout=300) for _ in range(2)]
+    out = [q.get(timeout=400) for _ in range(2)]
     for p in ps:
         p.join(timeout=60)
     assert all(e is None for *_, e in out), out
     assert all(p.exitcode == 0 for p in ps)
     assert open(two, "rb").read() == open(one, "rb").read()
     assert open(back, "rb").read() == open(src, "rb").read()
+    for rank, _, _, h2d, _ in out:
+        assert h2d <= 0.6 * size, (rank, h2d, size)
+
+
+def test_two_ranks_paired_small_windows(tmp_path):
+    """Paired files on two ranks with windows of a few blocks (every window
+    carries a block over, R1 and R2 cut at different bytes): the file equals
+    the one-process file."""
+    r1, r2 = str(tmp_path / "r1.fastq"), str(tmp_path / "r2.fastq")
+    synth.write_fastq(synth.illumina(20000, seed=5, with_names=True), r1)
+    synth.write_fastq(synth.novaseq(20000, seed=6, with_names=True), r2)
+    one, two = str(tmp_path / "one.fqz5"), str(tmp_path / "two.fqz5")
+    fqz5file.compress_file(r1, one, 3, blk_size=1_000_000, src2=r2)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_pairs, args=(r, 2, port, (r1, r2, two), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(2)]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(e is None for *_, e in out), out
+    assert open(two, "rb").read() == open(one, "rb").read()
+
+
+def _rank_pairs(rank, world, port, args, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.init()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        r1, r2, dst = args
+        fqz5file.compress_file(r1, dst, 3, blk_size=1_000_000, src2=r2, group=dist.group.WORLD,
+                               window_bytes=3_000_000)
+        q.put((rank, None))
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
 
 
 def _md5(path):

@@ -369,3 +369,36 @@ def test_refine_session_counts_late_sections():
     # inputs past one commit chunk
     assert not S.refine_session(secs, ids, sched, lo, hi, pairs, ins, chunk_bytes=10 ** 9,
                                 commit_bytes=nsec * 1_000_000 - 1)
+
+
+def test_rank_window_record_ends(tmp_path):
+    """The multi-rank window's host helpers: the end of a record read on from
+    its start (FASTQ: 4 lines, FASTA: up to the next '>' line, the file end
+    closing the last one) and the merge of adjacent byte ranges."""
+    t = b"@r1 c\nACGT\n+\nIIII\n@r2\nAC\n+\n@I\n@r3\nG\n+\nI"
+    p = tmp_path / "a.fq"
+    p.write_bytes(t)
+    f = fqz5file._PosFile(str(p))
+    assert [fqz5file._record_end(f, t.index(x), False) for x in (b"@r1", b"@r2", b"@r3")] == \
+        [t.index(b"@r2"), t.index(b"@r3"), len(t)]
+    f.close()
+    u = b">a\nACG\nTT\n>b\nGG\n>c\nA\n" + b"C" * 200000 + b"\n>d\nA\n"
+    q = tmp_path / "a.fa"
+    q.write_bytes(u)
+    g = fqz5file._PosFile(str(q))
+    assert [fqz5file._record_end(g, u.index(x), True) for x in (b">a", b">b", b">c", b">d")] == \
+        [u.index(b">b"), u.index(b">c"), u.index(b">d"), len(u)]
+    g.close()
+    assert fqz5file._merge([(0, 5), (5, 9), (12, 14), (14, 20)]) == [(0, 9), (12, 20)]
+
+
+def test_window_sized_from_footprint():
+    """The encode window from the level's device footprint: 0.8 x HBM per
+    rank at FOOTPRINT bytes per input byte, at most 8 GB per rank, and never
+    fewer than two blocks per rank and one over."""
+    hbm = 288 << 30
+    w5 = fqz5file.window_bytes_for(5, 100_000_000, 1, hbm)
+    assert w5 * fqz5file.FOOTPRINT[5] <= 0.8 * hbm and w5 >= 3_000_000_000
+    assert fqz5file.window_bytes_for(5, 100_000_000, 4, hbm) == 4 * w5
+    assert fqz5file.window_bytes_for(1, 1_000_000, 1, hbm) == 8_000_000_000
+    assert fqz5file.window_bytes_for(9, 1_000_000_000, 8, 8 << 30) == 17_000_000_000
