@@ -205,3 +205,27 @@ def test_l9_paired_preset_blocks_equal_cli(tmp_path):
     b1, b2 = str(tmp_path / "b1.fastq"), str(tmp_path / "b2.fastq")
     fqz5file.decompress_file(dst, b1, dst2=b2)
     assert (_md5(b1), _md5(b2)) == (rec["r1_md5"], rec["r2_md5"])
+
+
+def test_l5_illumina_file_equals_cli(tmp_path):
+    """-5 on 1.54 GB of random-walk Illumina (15 preset
+    blocks) through compress_file, the window sized from the level's
+    footprint: equal to the reference's -5 -t1 output (md5 recorded by
+    tests/golden/make_golden_l5.py), the arenas' device peak under 64 GB,
+    and decoded back."""
+    import sys
+    from fqzcomp5_amd import lib
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_golden_l5 as G
+    rec = json.load(open(os.path.join(ROOT, "tests", "golden", "l5_illumina.json")))
+    src = str(tmp_path / "illumina.fastq")
+    assert G.make_input(src) == rec["in_bytes"]
+    dst, back = str(tmp_path / "illumina.fqz5"), str(tmp_path / "back.fastq")
+    lib.arena_peak(reset=True)
+    assert fqz5file.compress_file(src, dst, 5) == rec["out_bytes"]
+    peak = lib.arena_peak()
+    assert _md5(dst) == rec["out_md5"]
+    assert peak <= 64e9, peak
+    os.unlink(src)
+    fqz5file.decompress_file(dst, back)
+    assert _md5(back) == rec["in_md5"]
