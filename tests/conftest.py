@@ -6,6 +6,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# a fault in the library's host code prints its native call stack
+# (capi.cpp's env-gated SIGSEGV handler, read when the library loads)
+os.environ.setdefault("FQZ5_SEGV_TRACE", "1")
 
 
 def pytest_configure(config):
