@@ -878,7 +878,6 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
             D.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * D.ment);
             D.back_hi = nullptr;
             D.hi_bits = nullptr;
-            if (const char *e = std::getenv("FQZ5_DEC_SMALL_DBG")) D.pad2 = uint32_t(std::strtoul(e, nullptr, 0));
         } else {
             D.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * D.ment);
         }
@@ -981,13 +980,6 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
             g.sync();
             std::fprintf(stderr, "[fqz dec] n=%u ment=%u sets=%u recs=%u dups=%u revs=%u misses=%u slow=%u\n",
                          W.total, W.D.ment, W.D.nsets, c[0], c[1], c[2], c[3], c[4]);
-            uint32_t dbg[12];
-            g.download(dbg, W.D.counts + 20, 12);
-            g.sync();
-            if (dbg[0])
-                std::fprintf(stderr, "[fqz dec] small-decoder check: symbol %u went fast, reference slot %u "
-                             "bubble %u total %u U %u %u %u %u %u %u %u\n", dbg[1], dbg[2], dbg[3], dbg[4],
-                             dbg[5], dbg[6], dbg[7], dbg[8], dbg[9], dbg[10], dbg[11]);
             if (pr[0] | pr[1])
                 std::fprintf(stderr, "[fqz dec] probe: %.1f cycles/symbol inside the run asm over %llu symbols "
                              "(%.1f%% of %u), %llu asm calls; %.0f cycles per miss() call, %.0f cycles "

@@ -198,8 +198,7 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "s_lshl_b32 %[qs], %[qsk], %[qshift]\n"                                 \
     "s_add_u32 m0, m0, 1\n"                                                 \
     "ds_write_b16 %[vaddr], %[vU]\n"                                        \
-    "s_or_b32 %[x], %[c], %[nsb]\n"                                         \
-    "s_cmp_eq_u32 %[cn], %[x]\n"                                            \
+    "s_cmp_eq_u32 %[cn], %[c]\n"                                            \
     "s_cbranch_scc1 20f\n"                                                  \
     "s_mov_b32 %[c], %[cn]\n"                                               \
     "s_mov_b32 %[ma], %[man]\n"                                             \
@@ -413,26 +412,6 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
         next_uniform(sym);
     };
 
-    // debug (FQZ5_DEC_SMALL_DBG 0x1000, one symbol per run): the reference's
-    // decision for the next symbol, to compare with the run's
-    uint32_t dbg_seen = 0;
-    auto predict = [&](uint32_t &kout, uint32_t &bub, uint32_t &tot) {
-        ensure();
-        const uint32_t uw = *reinterpret_cast<const uint16_t *>(lds + maddr + voff);
-        tot = U(*reinterpret_cast<const uint16_t *>(lds + maddr + 18));
-        uint32_t r2 = rng, t = 0;
-        if (tot && r2 >= tot) { r2 /= tot; t = code / r2; }
-        const bool live = l < L;
-        const uint32_t up = live ? uw : 0u;
-        const uint32_t lo_l = __shfl_up(up, 1, 64);
-        const uint32_t lo = l ? lo_l : 0u;
-        const uint32_t f = live ? up - lo : 0u;
-        const uint64_t gt = __ballot(live && up > t);
-        kout = gt ? uint32_t(__builtin_ctzll(gt)) : 99u;
-        bub = 0;
-        if (kout >= 1 && kout < 99) bub = RL(f, kout) + 16 > RL(f, kout - 1) ? 1u : 0u;
-        return uw;
-    };
     uint32_t turns = 0;
     bool lost = false;
     for (;;) {
@@ -497,9 +476,6 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
         // page ----------------------------------------------------------------
         uint32_t lim = left < SOBUF - fill ? left : SOBUF - fill;
         if (lim > 64u) lim = 64u;
-        if (J.pad2 & 0x800) lim = 1;
-        uint32_t pk_c = 0, pb_c = 0, pt_c = 0, pu_c = 0;
-        if (J.pad2 & 0x1000) pu_c = predict(pk_c, pb_c, pt_c);
         uint32_t ulim = (in.vb - 4u) * 8u;
         // per-step context terms of the run (fqz_update_ctx uses the position
         // and delta before this symbol's update): lane i the position term of
@@ -526,15 +502,13 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
                 const uint32_t e = in.len < in.lp ? in.len : in.lp;
                 return U(e >= 12u ? e - 11u : 0u);
             };
-            uint32_t rbend = (J.pad2 & 0x100) ? 0u : rb_end();
+            uint32_t rbend = rb_end();
             in.ub = U(in.ub);
             lim = U(lim);
             ulim = U(ulim);
             const uint32_t base = U(CB), cbig = 0x100000u, c65503 = 65503u;
             const uint32_t ns8 = U(NS8), qlocv = ps.qloc, qmask = U(ps.qmask);
-            const uint32_t dbg = U(J.pad2);
-            const uint32_t lfast = U(dbg == 0x51 ? 0u : (dbg & 0x200) ? 1u : (L < 8u ? L : 8u)), vsh4 = 4u * (l & 7u);
-            const uint32_t nsb = (dbg & 0x400) ? 0x10000u : 0u;
+            const uint32_t lfast = U(L < 8u ? L : 8u), vsh4 = 4u * (l & 7u);
             const uint32_t vm63 = l == 63 ? 0u : ~0u;   // p_{k-1} of slot 1 read from lane 63: 0
             const double c19 = 0x1p-19;
             uint32_t u, x, k1, pk, pk1, cn, man, qsk, sym, z, m0s;
@@ -559,7 +533,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
                   [ns8] "s"(ns8), [base] "s"(base), [lfast] "s"(lfast), [c65503] "s"(c65503), \
                   [rbend] "s"(rbend), [bswp] "s"(bswp), [lring] "i"(S_RING), [back] "s"(back),  \
                   [voff] "v"(voff), [vsh4] "v"(vsh4), [qlocv] "v"(qlocv), [cbig] "v"(cbig),   \
-                  [c19] "v"(c19), [pvv] "v"(pvv), [dvv] "v"(dvv), [nsb] "s"(nsb),              \
+                  [c19] "v"(c19), [pvv] "v"(pvv), [dvv] "v"(dvv),                              \
                   [vm63] "v"(vm63)                                                             \
                 : "memory", "scc", "vcc"
                 if constexpr (DT)
@@ -588,7 +562,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
                 win = in.W;
                 if (in.vb < 4u) break;
                 ulim = (in.vb - 4u) * 8u;
-                rbend = (J.pad2 & 0x100) ? 0u : rb_end();
+                rbend = rb_end();
             }
             in.W = win;
             code = uint32_t(cw >> 32);
@@ -598,19 +572,6 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
             delta = delta0 + dd;
             nmiss += nm;
             left -= done;
-        }
-        if ((J.pad2 & 0x1000) && !dbg_seen && flags != 2 && done == 1 &&
-            (pb_c || pk_c >= (L < 8u ? L : 8u) || pt_c > 65503u)) {
-            dbg_seen = 1;
-            const uint32_t uv = RL(pu_c, l < 9 ? l : 8);
-            if (l == 0) {
-                J.counts[20] = 1;
-                J.counts[21] = obase + fill;
-                J.counts[22] = pk_c;
-                J.counts[23] = pb_c;
-                J.counts[24] = pt_c;
-            }
-            if (l < 7) J.counts[25 + l] = uv;
         }
         qctx = qs >> qshift;
         if (l < done) lds[S_OBUF + fill + l] = uint8_t(vout);
