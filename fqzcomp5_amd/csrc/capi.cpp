@@ -115,8 +115,8 @@ static std::atomic<int> g_dec_small{-1};
 bool small_decoder_on() {
     int v = g_dec_small.load();
     if (v < 0) {
-        const char *e = std::getenv("FQZ5_DEC_SMALL");
-        v = e && e[0] == '1' ? 1 : 0;
+        const char *e = std::getenv("FQZ5_DEC_SMALL");   // on unless "0"
+        v = e && e[0] == '0' ? 0 : 1;
         g_dec_small.store(v);
     }
     return v != 0;

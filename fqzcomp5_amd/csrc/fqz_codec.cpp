@@ -522,7 +522,7 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         W.parallel = G.nparam == 1 && !(G.gflags & GF_MULTI) && nrec > 0;
         for (int r = 0; W.parallel && r < nrec; r++) W.parallel = R.lens[r] > 0;
         if (!W.parallel) {
-            E.models = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * FQZ_QMODEL_BYTES);
+            E.models = g.fqz_tmp.alloc_n<uint8_t>(size_t(FQZ_CTX) * FQZ_QMODEL_BYTES);
             FQZ5_HIP(launch_fqz_model_init(E.models, G.max_sym + 1, g.stream));
             FQZ5_HIP(launch_fqz_encode(E, g.stream));
             continue;
@@ -541,14 +541,14 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         uint64_t o = 0;
         for (int r = 0; r < nrec; r++) off[size_t(r)] = o, o += R.lens[r];
         J.off = g.upload(off);
-        J.nev_rec = g.arena.alloc_n<uint32_t>(size_t(nrec));
-        uint32_t *ev_off = g.arena.alloc_n<uint32_t>(size_t(nrec));
+        J.nev_rec = g.fqz_tmp.alloc_n<uint32_t>(size_t(nrec));
+        uint32_t *ev_off = g.fqz_tmp.alloc_n<uint32_t>(size_t(nrec));
         J.ev_off = ev_off;
-        J.dup = g.arena.alloc_n<uint8_t>(size_t(nrec));
+        J.dup = g.fqz_tmp.alloc_n<uint8_t>(size_t(nrec));
         FQZ5_HIP(launch_fqz_events(J, 0, g.stream));
         size_t tb = 0;
         FQZ5_HIP(fqz_exclusive_scan(J.nev_rec, ev_off, nrec, nullptr, tb, g.stream));
-        void *tmp = g.arena.alloc_n<uint8_t>(tb);
+        void *tmp = g.fqz_tmp.alloc_n<uint8_t>(tb);
         FQZ5_HIP(fqz_exclusive_scan(J.nev_rec, ev_off, nrec, tmp, tb, g.stream));
         g.download(&W.last[0], ev_off + nrec - 1, 1);
         g.download(&W.last[1], J.nev_rec + nrec - 1, 1);
@@ -562,26 +562,26 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         const uint64_t nev = uint64_t(R->w->last[0]) + R->w->last[1];
         if (nev >= (1ull << 31)) throw std::runtime_error("fqz: block too large");
         J.nev = uint32_t(nev);
-        J.key = g.arena.alloc_n<uint32_t>(nev);
-        J.val = g.arena.alloc_n<uint64_t>(nev);
-        uint32_t *skey = g.arena.alloc_n<uint32_t>(nev);
-        uint64_t *sval = g.arena.alloc_n<uint64_t>(nev);
+        J.key = g.fqz_tmp.alloc_n<uint32_t>(nev);
+        J.val = g.fqz_tmp.alloc_n<uint64_t>(nev);
+        uint32_t *skey = g.fqz_tmp.alloc_n<uint32_t>(nev);
+        uint64_t *sval = g.fqz_tmp.alloc_n<uint64_t>(nev);
         J.skey = skey;
         J.sval = sval;
-        J.code = g.arena.alloc_n<uint64_t>(nev);
+        J.code = g.fqz_tmp.alloc_n<uint64_t>(nev);
         FQZ5_HIP(launch_fqz_events(J, 1, g.stream));
         size_t tb = 0;
         FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(nev), int(FQZ_MODEL_BITS),
                                    nullptr, tb, g.stream));
-        void *tmp = g.arena.alloc_n<uint8_t>(tb);
+        void *tmp = g.fqz_tmp.alloc_n<uint8_t>(tb);
         FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(nev), int(FQZ_MODEL_BITS), tmp,
                                    tb, g.stream));
-        J.seg_lo = g.arena.alloc_n<uint32_t>(FQZ_NMODELS);
-        J.seg_hi = g.arena.alloc_n<uint32_t>(FQZ_NMODELS);
+        J.seg_lo = g.fqz_tmp.alloc_n<uint32_t>(FQZ_NMODELS);
+        J.seg_hi = g.fqz_tmp.alloc_n<uint32_t>(FQZ_NMODELS);
         g.memset0(J.seg_lo, FQZ_NMODELS * 4);
         g.memset0(J.seg_hi, FQZ_NMODELS * 4);
         FQZ5_HIP(launch_fqz_events(J, 2, g.stream));
-        J.scratch = g.arena.alloc_n<uint8_t>(8192);
+        J.scratch = g.fqz_tmp.alloc_n<uint8_t>(8192);
         jobs.push_back(J);
     }
     const int np = int(par.size());
@@ -604,13 +604,13 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         uint32_t stride = 1;
         for (const FqzEvJob &J : jobs)
             stride = std::max(stride, 1u + std::min(FQZ_M_SEL, J.nev / std::max(hot_min, 1u) + 1));
-        uint32_t *hot = g.arena.alloc_n<uint32_t>(size_t(stride) * size_t(np));
+        uint32_t *hot = g.fqz_tmp.alloc_n<uint32_t>(size_t(stride) * size_t(np));
         g.memset0(hot, size_t(stride) * size_t(np) * 4);
         FQZ5_HIP(launch_fqz_model_pass(g.upload(jobs), np, hot, stride, hot_min, g.stream));
         // the entropy of each block's events and the coder's slack: lower
         // and upper bounds of its size
         constexpr uint32_t EB = 1024;
-        double *part = g.arena.alloc_n<double>(2 * size_t(EB) * size_t(np));
+        double *part = g.fqz_tmp.alloc_n<double>(2 * size_t(EB) * size_t(np));
         for (int k = 0; k < np; k++)
             FQZ5_HIP(launch_fqz_entropy(jobs[size_t(k)], part + 2 * size_t(k) * EB, EB, g.stream));
         std::vector<double> hp(2 * size_t(EB) * size_t(np));
@@ -637,8 +637,8 @@ void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
     if (!np) return;
     std::vector<FqzEvJob> rj;
     for (FqzEvJob *J : js) {
-        J->addend = g.arena.alloc_n<uint32_t>(J->nev);
-        J->shifts = g.arena.alloc_n<uint32_t>(J->nev + 1);
+        J->addend = g.fqz_tmp.alloc_n<uint32_t>(J->nev);
+        J->shifts = g.fqz_tmp.alloc_n<uint32_t>(J->nev + 1);
         J->done = nullptr;
         rj.push_back(*J);
     }
@@ -646,7 +646,7 @@ void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
     HedgeShare share(size_t(g.cus));
     const size_t copies = hedge_copies(rj.size(), share.cus);
     if (copies > 1) {
-        uint32_t *d_done = g.arena.alloc_n<uint32_t>(rj.size());
+        uint32_t *d_done = g.fqz_tmp.alloc_n<uint32_t>(rj.size());
         g.memset0(d_done, rj.size() * 4);
         for (size_t k = 0; k < rj.size(); k++) rj[k].done = d_done + k;
         for (size_t c = 1; c < copies; c++) rj.insert(rj.end(), rj.begin(), rj.begin() + long(np));
@@ -657,11 +657,11 @@ void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
     std::vector<uint32_t> P(size_t(np), 0);
     for (int k = 0; k < np; k++) {
         FqzEvJob &J = *js[size_t(k)];
-        uint32_t *pos = g.arena.alloc_n<uint32_t>(J.nev + 1);
+        uint32_t *pos = g.fqz_tmp.alloc_n<uint32_t>(J.nev + 1);
         g.memset0(J.shifts + J.nev, 4);
         size_t tb = 0;
         FQZ5_HIP(fqz_exclusive_scan(J.shifts, pos, int(J.nev + 1), nullptr, tb, g.stream));
-        void *tmp = g.arena.alloc_n<uint8_t>(tb);
+        void *tmp = g.fqz_tmp.alloc_n<uint8_t>(tb);
         FQZ5_HIP(fqz_exclusive_scan(J.shifts, pos, int(J.nev + 1), tmp, tb, g.stream));
         J.pos = pos;
         J.nshift = pos + J.nev;
@@ -676,17 +676,17 @@ void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
     for (int k = 0; k < np; k++) {
         FqzEvJob &J = *js[size_t(k)];
         J.nwords = (P[size_t(k)] + 5 + 3) / 4 + 2;
-        J.acc = reinterpret_cast<unsigned long long *>(g.arena.alloc_n<uint64_t>(J.nwords));
+        J.acc = reinterpret_cast<unsigned long long *>(g.fqz_tmp.alloc_n<uint64_t>(J.nwords));
         g.memset0(J.acc, size_t(J.nwords) * 8);
         FQZ5_HIP(launch_fqz_bytes(J, 0, g.stream));
         // carries through the columns: codes, their scan, digits
-        uint32_t *sw = g.arena.alloc_n<uint32_t>(J.nwords);
-        uint8_t *code = g.arena.alloc_n<uint8_t>(J.nwords);
-        uint8_t *pref = g.arena.alloc_n<uint8_t>(J.nwords);
+        uint32_t *sw = g.fqz_tmp.alloc_n<uint32_t>(J.nwords);
+        uint8_t *code = g.fqz_tmp.alloc_n<uint8_t>(J.nwords);
+        uint8_t *pref = g.fqz_tmp.alloc_n<uint8_t>(J.nwords);
         FQZ5_HIP(launch_fqz_norm(J, 1, sw, code, g.stream));
         size_t tb = 0;
         FQZ5_HIP(fqz_carry_scan(code, pref, int(J.nwords), nullptr, tb, g.stream));
-        void *tmp = g.arena.alloc_n<uint8_t>(tb);
+        void *tmp = g.fqz_tmp.alloc_n<uint8_t>(tb);
         FQZ5_HIP(fqz_carry_scan(code, pref, int(J.nwords), tmp, tb, g.stream));
         FQZ5_HIP(launch_fqz_norm(J, 2, sw, pref, g.stream));
         FQZ5_HIP(launch_fqz_bytes(J, 2, g.stream));
@@ -704,7 +704,7 @@ void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vecto
     for (int k = 0; k < np; k++) {
         FqzEncReq::Work &W = *par[size_t(k)]->w;
         FqzEvJob &J = W.J;
-        J.rec = g.arena.alloc_n<uint4>(J.nev);
+        J.rec = g.fqz_tmp.alloc_n<uint4>(J.nev);
         FQZ5_HIP(launch_fqz_expand(J, g.stream));
         J.out = W.E.out;
         J.out_len = W.E.out_len;
@@ -714,7 +714,9 @@ void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vecto
 
     for (size_t i = 0; i < reqs.size(); i++)
         if (!(skip && (*skip)[i])) g.download(&reqs[i].w->clen, reqs[i].w->E.out_len, 1);
-    g.sync();
+    // the outputs and sizes are all that is left to need: the event tables
+    // and the coder's buffers go back to the pool
+    g.tmp_done(g.fqz_tmp);
     for (size_t i = 0; i < reqs.size(); i++) {
         FqzEncReq &R = reqs[i];
         FqzEncReq::Work &W = *R.w;
@@ -771,6 +773,13 @@ uint8_t *fqz_encode_gpu(int vers, fqz_slice *s, const uint8_t *in, size_t n, siz
 
 static std::atomic<uint64_t> g_dec_blocks[2];
 uint64_t fqz_dec_blocks(bool small) { return g_dec_blocks[small ? 1 : 0].load(); }
+int small_copies() {
+    static const int n = [] {
+        const char *e = std::getenv("FQZ5_SMALL_COPIES");
+        return e ? std::max(1, std::atoi(e)) : 2;
+    }();
+    return n;
+}
 
 struct FqzDecReq::Work {
     Global G;
@@ -912,8 +921,12 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
             HedgeShare share(size_t(g.cus));
             const bool long_block =
                 !steps.empty() && *std::max_element(steps.begin(), steps.end()) >= (1u << 20);
-            const std::vector<int> cp = long_block ? hedge_plan(steps, share.cus)
-                                                   : std::vector<int>(js.size(), 1);
+            std::vector<int> cp = long_block ? hedge_plan(steps, share.cus)
+                                             : std::vector<int>(js.size(), 1);
+            // the small decoder's copies each keep a 1.5 MB backing store
+            // that should stay in its XCD's L2 ($FQZ5_SMALL_COPIES, default 2)
+            if (smallv)
+                for (int &c : cp) c = std::min(c, small_copies());
             const size_t nj = js.size();
             for (size_t k = 0; k < nj; k++) {
                 if (cp[k] <= 1) continue;

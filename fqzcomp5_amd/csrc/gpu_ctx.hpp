@@ -303,6 +303,10 @@ struct GpuCtx {
     hipStream_t stream2 = nullptr;   // second queue for concurrent launches
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     DevArena arena;
+    // scratch of one codec's batch (its event tables, sort and scan
+    // buffers), returned to the pool as soon as the batch's outputs exist
+    // (tmp_done), so a try session holds its candidates' outputs only
+    DevArena fqz_tmp, lzp_tmp;
     PinnedArena staging;
     int device = 0;
     int cus = 256;                   // compute units (MI355X: 256)
@@ -381,7 +385,15 @@ struct GpuCtx {
         sync();
         if (stream2) FQZ5_HIP(hipStreamSynchronize(stream2));   // (its chunks go to the pool)
         arena.reset();
+        fqz_tmp.reset();
+        lzp_tmp.reset();
         staging.reset();
+    }
+    // a scratch arena back to the pool once the streams have drained
+    void tmp_done(DevArena &a) {
+        sync();
+        if (stream2) FQZ5_HIP(hipStreamSynchronize(stream2));
+        a.reset();
     }
     template <class T> T *upload(const std::vector<T> &v FQZ5_CS_ARGS) {
 #ifdef FQZ5_COPY_STATS
@@ -408,6 +420,7 @@ bool small_decoder_on();
 int host_decode_mode();
 // quality blocks decoded by the general (false) / small (true) fqz decoder
 uint64_t fqz_dec_blocks(bool small);
+int small_copies();   // hedged copies of a small-decoder block
 // Copies of each of `jobs` chains: up to 4 while they fit one per CU.
 inline size_t hedge_copies(size_t jobs, size_t cus) {
     if (!hedge_chains() || !jobs) return 1;

@@ -34,21 +34,21 @@ void lzp_encode_batch(GpuCtx &g, std::vector<LzpEncReq> &reqs) {
             g.memset0(J.out_len, 4);
             continue;
         }
-        J.key = g.arena.alloc_n<uint32_t>(n);
-        J.skey = g.arena.alloc_n<uint32_t>(n);
-        J.val = g.arena.alloc_n<uint32_t>(n);
-        J.sval = g.arena.alloc_n<uint32_t>(n);
-        J.pred = g.arena.alloc_n<uint32_t>(n);
-        J.rev = g.arena.alloc_n<uint32_t>(n);
-        J.nxt = g.arena.alloc_n<uint32_t>(n);
-        J.base = g.arena.alloc_n<uint32_t>(n);
-        J.ml = g.arena.alloc_n<uint16_t>(n);
-        J.spec = g.arena.alloc_n<uint8_t>(n);
-        J.walk = g.arena.alloc_n<uint8_t>(n);
-        J.exitp = g.arena.alloc_n<uint32_t>(J.nchunk);
-        J.conv = g.arena.alloc_n<uint32_t>(J.nchunk);
-        J.size = g.arena.alloc_n<uint32_t>(n);
-        J.off = g.arena.alloc_n<uint32_t>(n);
+        J.key = g.lzp_tmp.alloc_n<uint32_t>(n);
+        J.skey = g.lzp_tmp.alloc_n<uint32_t>(n);
+        J.val = g.lzp_tmp.alloc_n<uint32_t>(n);
+        J.sval = g.lzp_tmp.alloc_n<uint32_t>(n);
+        J.pred = g.lzp_tmp.alloc_n<uint32_t>(n);
+        J.rev = g.lzp_tmp.alloc_n<uint32_t>(n);
+        J.nxt = g.lzp_tmp.alloc_n<uint32_t>(n);
+        J.base = g.lzp_tmp.alloc_n<uint32_t>(n);
+        J.ml = g.lzp_tmp.alloc_n<uint16_t>(n);
+        J.spec = g.lzp_tmp.alloc_n<uint8_t>(n);
+        J.walk = g.lzp_tmp.alloc_n<uint8_t>(n);
+        J.exitp = g.lzp_tmp.alloc_n<uint32_t>(J.nchunk);
+        J.conv = g.lzp_tmp.alloc_n<uint32_t>(J.nchunk);
+        J.size = g.lzp_tmp.alloc_n<uint32_t>(n);
+        J.off = g.lzp_tmp.alloc_n<uint32_t>(n);
         g.memset0(J.spec, n);
         g.memset0(J.walk, n);
         FQZ5_HIP(hipMemsetAsync(J.conv, 0xff, size_t(J.nchunk) * 4, g.stream));
@@ -60,7 +60,7 @@ void lzp_encode_batch(GpuCtx &g, std::vector<LzpEncReq> &reqs) {
         FQZ5_HIP(lzp_sort_ends(J, nullptr, t4, g.stream));
         FQZ5_HIP(lzp_end_scan(J, nullptr, t5, g.stream));
         const size_t tmax = std::max({tb, t2, t3, t4, t5});
-        void *tmp = g.arena.alloc_n<uint8_t>(tmax);
+        void *tmp = g.lzp_tmp.alloc_n<uint8_t>(tmax);
         tb = t2 = t3 = t4 = t5 = tmax;
         FQZ5_HIP(lzp_sort(J, tmp, tb, g.stream));
         FQZ5_HIP(launch_lzp_pred(J, g.stream));
@@ -80,7 +80,7 @@ void lzp_encode_batch(GpuCtx &g, std::vector<LzpEncReq> &reqs) {
     }
     std::vector<uint32_t> L(reqs.size(), 0);
     for (size_t r = 0; r < reqs.size(); r++) g.download(&L[r], lens[r], 1);
-    g.sync();
+    g.tmp_done(g.lzp_tmp);                 // (syncs) the parse buffers back to the pool
     for (size_t r = 0; r < reqs.size(); r++) reqs[r].out_len = L[r];
 }
 
