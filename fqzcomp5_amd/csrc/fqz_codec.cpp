@@ -562,20 +562,23 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         const uint64_t nev = uint64_t(R->w->last[0]) + R->w->last[1];
         if (nev >= (1ull << 31)) throw std::runtime_error("fqz: block too large");
         J.nev = uint32_t(nev);
-        J.key = g.fqz_tmp.alloc_n<uint32_t>(nev);
-        J.val = g.fqz_tmp.alloc_n<uint64_t>(nev);
-        uint32_t *skey = g.fqz_tmp.alloc_n<uint32_t>(nev);
-        uint64_t *sval = g.fqz_tmp.alloc_n<uint64_t>(nev);
+        J.key = g.sort_tmp.alloc_n<uint32_t>(nev);
+        J.val = g.sort_tmp.alloc_n<uint64_t>(nev);
+        uint32_t *skey = g.ev_tmp.alloc_n<uint32_t>(nev);
+        uint64_t *sval = g.ev_tmp.alloc_n<uint64_t>(nev);
         J.skey = skey;
         J.sval = sval;
-        J.code = g.fqz_tmp.alloc_n<uint64_t>(nev);
+        J.code = g.ev_tmp.alloc_n<uint64_t>(nev);
         FQZ5_HIP(launch_fqz_events(J, 1, g.stream));
         size_t tb = 0;
         FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(nev), int(FQZ_MODEL_BITS),
                                    nullptr, tb, g.stream));
-        void *tmp = g.fqz_tmp.alloc_n<uint8_t>(tb);
+        void *tmp = g.sort_tmp.alloc_n<uint8_t>(tb);
         FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(nev), int(FQZ_MODEL_BITS), tmp,
                                    tb, g.stream));
+        // the unsorted events and the sort's buffers back to the pool, so
+        // the next block's reuse them (the peak holds one block's, not all)
+        g.tmp_done(g.sort_tmp);
         J.seg_lo = g.fqz_tmp.alloc_n<uint32_t>(FQZ_NMODELS);
         J.seg_hi = g.fqz_tmp.alloc_n<uint32_t>(FQZ_NMODELS);
         g.memset0(J.seg_lo, FQZ_NMODELS * 4);
@@ -627,6 +630,7 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
             W.ub = uint64_t(W.hdr.size()) + rc_bytes_upper(bits, slack) + 5;
         }
     }
+    g.tmp_done(g.sort_tmp);                // the unsorted events back to the pool
 }
 
 // The range coder back end for event jobs whose rec[] holds every event in
@@ -710,6 +714,7 @@ void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vecto
         J.out_len = W.E.out_len;
         js.push_back(&J);
     }
+    g.tmp_done(g.ev_tmp);                  // the sorted events, now records, back to the pool
     rc_backend(g, js);
 
     for (size_t i = 0; i < reqs.size(); i++)

@@ -306,7 +306,9 @@ struct GpuCtx {
     // scratch of one codec's batch (its event tables, sort and scan
     // buffers), returned to the pool as soon as the batch's outputs exist
     // (tmp_done), so a try session holds its candidates' outputs only
-    DevArena fqz_tmp, lzp_tmp;
+    // (fqz: the unsorted events and the sort's buffers die with the sort,
+    // the sorted events and their codes with the expansion into records)
+    DevArena fqz_tmp, lzp_tmp, sort_tmp, ev_tmp;
     PinnedArena staging;
     int device = 0;
     int cus = 256;                   // compute units (MI355X: 256)
@@ -387,6 +389,8 @@ struct GpuCtx {
         arena.reset();
         fqz_tmp.reset();
         lzp_tmp.reset();
+        sort_tmp.reset();
+        ev_tmp.reset();
         staging.reset();
     }
     // a scratch arena back to the pool once the streams have drained
