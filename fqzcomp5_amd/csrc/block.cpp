@@ -625,16 +625,26 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
         // 0 when the codec returned NULL (out_len = *out_size = 0); a
         // skipped candidate's lower bound here, its upper bound in `upper`
         t_sess.upper.assign(size_t(nsec) * FQZ5_M_LAST, 0);
-        for (int i = 0; i < nsec; i++)
+        for (int i = 0; i < nsec; i++) {
+            // encode_names returns NULL without writing *out_size, so a
+            // failing name candidate is seen with the size the previous name
+            // candidate of this section wrote (fqzcomp5.c:2036-2044, :1433-
+            // 1440); never strictly the best, but it enters the trial's
+            // totals (metrics_update) and can win the later blocks
+            uint32_t stale = UINT32_MAX;
             for (int m = 0; m < FQZ5_M_LAST; m++) {
                 const int ri = t_sess.req_of[i][m], fi = t_sess.fqz_of[i][m];
                 const int si = t_sess.seq_of[i][m], ni = t_sess.name_of[i][m];
                 uint32_t sz = UINT32_MAX;
                 if (ri >= 0) sz = reqs[ri].ok ? layout_size(reqs[ri].out) : 0;
                 // a name candidate's size is its whole section (encode_names'
-                // *out_size); one that fails (encode_names NULL) is never chosen
-                if (ni >= 0 && t_sess.names[size_t(ni)].ok)
-                    sz = uint32_t(t_sess.names[size_t(ni)].out.size());
+                // *out_size)
+                if (ni >= 0) {
+                    if (t_sess.names[size_t(ni)].ok)
+                        stale = sz = uint32_t(t_sess.names[size_t(ni)].out.size());
+                    else
+                        sz = stale;
+                }
                 if (si >= 0) {
                     const uint64_t lb = t_sess.seq_lb[size_t(si)];   // pruned: its lower bound
                     sz = t_sess.seq[size_t(si)].ok ? layout_size(t_sess.seq[size_t(si)].out)
@@ -653,6 +663,7 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
                 sizes[size_t(i) * FQZ5_M_LAST + m] = sz;
                 t_sess.upper[size_t(i) * FQZ5_M_LAST + m] = up;
             }
+        }
         return 0;
     } catch (const std::exception &e) {
         fqz5_set_error(e.what());
