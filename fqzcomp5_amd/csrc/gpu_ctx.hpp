@@ -35,8 +35,8 @@ struct GpuError : std::runtime_error {
 // arena.  An arena takes chunks from the pool as it grows and gives them all
 // back at reset() (after its stream has drained), so the device footprint
 // is the peak of what the contexts use at the same time, not the sum of each
-// context's own peak.  Idle chunks beyond
-// $FQZ5_ARENA_IDLE_GB (default 16) go back to the device.
+// context's own peak.  Idle chunks beyond a quarter
+// of the device's memory ($FQZ5_ARENA_IDLE_GB) go back to the device.
 class ChunkPool {
   public:
     static ChunkPool &get() {
@@ -105,10 +105,17 @@ class ChunkPool {
     }
 
   private:
+    // Idle chunks kept for reuse: a quarter of the device's memory (or
+    // $FQZ5_ARENA_IDLE_GB).  Trimming calls hipFree, which waits for every
+    // kernel on the device to finish: a trim in the middle of a step stalls
+    // the calling thread behind the longest chain (measured: the names
+    // helper of a -3 step blocked ~150 ms), so steady state must not trim.
     static size_t idle_cap() {
         static const size_t c = [] {
-            const char *e = std::getenv("FQZ5_ARENA_IDLE_GB");
-            return size_t((e ? std::atof(e) : 16.0) * 1e9);
+            if (const char *e = std::getenv("FQZ5_ARENA_IDLE_GB")) return size_t(std::atof(e) * 1e9);
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) != hipSuccess || !tot) tot = size_t(64) << 30;
+            return tot / 4;
         }();
         return c;
     }
