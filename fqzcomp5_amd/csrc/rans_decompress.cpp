@@ -302,9 +302,14 @@ static bool xcd_grouping() {
 // The O1 register decoder's keys (rans_chain.hip dec4_o1reg_body): every
 // context row complete (its frequencies cover the 2^bits slots), at most 8
 // contexts with 12-bit slots or 16 with <= 10, at most DEC_O1KEY_MAX (context,
-// symbol) pairs.  $FQZ5_NO_O1REG: the table decoders instead.
+// symbol) pairs.  Off unless $FQZ5_O1REG=1: measured slower than the LDS
+// table step (NovaSeq qualities, one stream: 101.7 against 65.8 ns per
+// step; the -5 launch 146 against 94), DESIGN.md section 4.
 static bool o1reg_decoder() {
-    static const bool on = std::getenv("FQZ5_NO_O1REG") == nullptr;
+    static const bool on = [] {
+        const char *e = std::getenv("FQZ5_O1REG");
+        return e && e[0] == '1';
+    }();
     return on;
 }
 static bool o1_keys(const DJ &j, DecJob &d) {

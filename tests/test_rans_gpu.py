@@ -165,11 +165,13 @@ def test_hedged_launches_same_bytes():
 
 
 def test_o1_register_decoder_alphabets():
-    """The O1 register decoder (rans_chain.hip dec4_o1reg_body: <= 8
-    contexts at 12-bit slots, <= 16 at 10, <= 64 (context, symbol) pairs)
-    against the oracle's streams: alphabets of 1-16 symbols, skewed and
-    flat, lengths with every tail n % 4 and inputs short enough for 10-bit
-    slots, with RLE / PACK in front."""
+    """Small O1 alphabets (the O1 register decoder's domain, rans_chain.hip
+    dec4_o1reg_body: <= 8 contexts at 12-bit slots, <= 16 at 10, <= 64
+    (context, symbol) pairs; it runs when $FQZ5_O1REG=1 was set when the
+    library loaded, else the table decoders do) against the oracle's
+    streams: alphabets of 1-16 symbols, skewed and flat, lengths with every
+    tail n % 4 and inputs short enough for 10-bit slots, with RLE / PACK in
+    front."""
     from fqzcomp5_amd import synth
     ora = binding.oracle()
     rng = np.random.default_rng(77)
