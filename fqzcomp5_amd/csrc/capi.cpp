@@ -146,19 +146,20 @@ void gpu_aux_reset_all() {
     for (auto &a : g_aux)
         if (a) a->reset();
 }
+static void release_ctx(GpuCtx &c) {
+    c.sync();
+    FQZ5_HIP(hipStreamSynchronize(c.stream2));
+    c.arena.release();
+    c.fqz_tmp.release();
+    c.lzp_tmp.release();
+    c.sort_tmp.release();
+    c.ev_tmp.release();
+    c.staging.reset();
+}
 void gpu_release_all() {
-    if (g_ctx) {
-        g_ctx->sync();
-        g_ctx->arena.release();
-        g_ctx->staging.reset();
-    }
+    if (g_ctx) release_ctx(*g_ctx);
     for (auto &a : g_aux)
-        if (a) {
-            a->sync();
-            FQZ5_HIP(hipStreamSynchronize(a->stream2));
-            a->arena.release();
-            a->staging.reset();
-        }
+        if (a) release_ctx(*a);
 }
 static uint64_t arena_bytes() { return ChunkPool::get().held(); }
 

@@ -211,8 +211,9 @@ def test_l5_illumina_file_equals_cli(tmp_path):
     """-5 on 1.54 GB of random-walk Illumina (15 preset
     blocks) through compress_file, the window sized from the level's
     footprint: equal to the reference's -5 -t1 output (md5 recorded by
-    tests/golden/make_golden_l5.py), the arenas' device peak under 64 GB,
-    and decoded back."""
+    tests/golden/make_golden_l5.py), the arenas' device peak within the
+    footprint the window is sized by (fqz5file.FOOTPRINT), and decoded
+    back."""
     import sys
     from fqzcomp5_amd import lib
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
@@ -225,7 +226,7 @@ def test_l5_illumina_file_equals_cli(tmp_path):
     assert fqz5file.compress_file(src, dst, 5) == rec["out_bytes"]
     peak = lib.arena_peak()
     assert _md5(dst) == rec["out_md5"]
-    assert peak <= 64e9, peak
+    assert peak <= fqz5file.FOOTPRINT[5] * rec["in_bytes"], peak
     os.unlink(src)
     fqz5file.decompress_file(dst, back)
     assert _md5(back) == rec["in_md5"]
