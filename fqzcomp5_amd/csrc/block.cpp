@@ -458,7 +458,18 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             GpuCtx &ga = gpu_aux(0), &gb = gpu_aux(2), &gc = gpu_aux(1);
             // sequence-model candidates: one helper context each (their
             // passes are latency-bound and overlap well), up to AUX_NSEQ
-            const size_t nsq = std::min<size_t>(sq.size(), size_t(AUX_NSEQ));
+            // (each runs one block at a time with ~120 B of device memory per
+            // base while it prepares: as many side by side as fit a quarter of
+            // HBM; -9's 1 GB blocks take them one after another)
+            size_t nsq = std::min<size_t>(sq.size(), size_t(AUX_NSEQ));
+            {
+                uint64_t mx = 1;
+                for (const SeqEncReq &q : sq) mx = std::max<uint64_t>(mx, q.n);
+                size_t fr = 0, tot = 0;
+                if (hipMemGetInfo(&fr, &tot) != hipSuccess || !tot) tot = size_t(64) << 30;
+                const uint64_t fit = (uint64_t(tot) / 4) / (120 * mx);
+                nsq = std::max<size_t>(1, std::min<size_t>(nsq, size_t(fit)));
+            }
             std::vector<std::vector<SeqEncReq>> sqg(nsq);
             for (size_t k = 0; k < sq.size(); k++) sqg[k % std::max<size_t>(nsq, 1)].push_back(sq[k]);
             std::vector<CompressReq> lzr;

@@ -73,12 +73,12 @@ static void seq_prepare_dev(GpuCtx &g, SeqWork &W, const uint8_t *d_in, uint32_t
     J.seg = g.upload(seg);
     uint32_t nev = 0;
     if (n) {
-        J.flag = g.fqz_tmp.alloc_n<uint32_t>(n);
-        J.ex = g.fqz_tmp.alloc_n<uint32_t>(n);
+        J.flag = g.ev_tmp.alloc_n<uint32_t>(n);
+        J.ex = g.ev_tmp.alloc_n<uint32_t>(n);
         FQZ5_HIP(launch_seq_heads(J, g.stream));
         size_t tb = 0;
         FQZ5_HIP(fqz_exclusive_scan(J.flag, J.ex, int(n), nullptr, tb, g.stream));
-        void *tmp = g.fqz_tmp.alloc_n<uint8_t>(tb);
+        void *tmp = g.ev_tmp.alloc_n<uint8_t>(tb);
         FQZ5_HIP(fqz_exclusive_scan(J.flag, J.ex, int(n), tmp, tb, g.stream));
         uint32_t last[2];
         uint8_t first = 0;
@@ -88,13 +88,13 @@ static void seq_prepare_dev(GpuCtx &g, SeqWork &W, const uint8_t *d_in, uint32_t
         g.sync();
         J.nrun = last[0] + last[1];
         J.lead = seq_class_uc(first) ? 0u : 2u;
-        J.run_start = g.fqz_tmp.alloc_n<uint32_t>(J.nrun);
-        J.cnt = g.fqz_tmp.alloc_n<uint32_t>(J.nrun + 1);
-        J.run_off = g.fqz_tmp.alloc_n<uint32_t>(J.nrun + 1);
+        J.run_start = g.ev_tmp.alloc_n<uint32_t>(J.nrun);
+        J.cnt = g.ev_tmp.alloc_n<uint32_t>(J.nrun + 1);
+        J.run_off = g.ev_tmp.alloc_n<uint32_t>(J.nrun + 1);
         FQZ5_HIP(launch_seq_runs(J, g.stream));
         tb = 0;
         FQZ5_HIP(fqz_exclusive_scan(J.cnt, J.run_off, int(J.nrun + 1), nullptr, tb, g.stream));
-        tmp = g.fqz_tmp.alloc_n<uint8_t>(tb);
+        tmp = g.ev_tmp.alloc_n<uint8_t>(tb);
         FQZ5_HIP(fqz_exclusive_scan(J.cnt, J.run_off, int(J.nrun + 1), tmp, tb, g.stream));
         uint32_t tot = 0;
         g.download(&tot, J.run_off + J.nrun, 1);
@@ -105,15 +105,15 @@ static void seq_prepare_dev(GpuCtx &g, SeqWork &W, const uint8_t *d_in, uint32_t
         nev = uint32_t(ne);
 
         J.nkeys = n * (J.both + 1u);
-        J.key = g.fqz_tmp.alloc_n<uint32_t>(J.nkeys);
-        J.val = g.fqz_tmp.alloc_n<uint64_t>(J.nkeys);
+        J.key = g.ev_tmp.alloc_n<uint32_t>(J.nkeys);
+        J.val = g.ev_tmp.alloc_n<uint64_t>(J.nkeys);
         FQZ5_HIP(launch_seq_ctx(J, g.stream));
-        uint32_t *skey = g.fqz_tmp.alloc_n<uint32_t>(J.nkeys);
-        uint64_t *sval = g.fqz_tmp.alloc_n<uint64_t>(J.nkeys);
+        uint32_t *skey = g.ev_tmp.alloc_n<uint32_t>(J.nkeys);
+        uint64_t *sval = g.ev_tmp.alloc_n<uint64_t>(J.nkeys);
         tb = 0;
         const int kb = 2 * k + 1;
         FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(J.nkeys), kb, nullptr, tb, g.stream));
-        tmp = g.fqz_tmp.alloc_n<uint8_t>(tb);
+        tmp = g.ev_tmp.alloc_n<uint8_t>(tb);
         FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(J.nkeys), kb, tmp, tb, g.stream));
         J.skey = skey;
         J.sval = sval;
@@ -124,6 +124,9 @@ static void seq_prepare_dev(GpuCtx &g, SeqWork &W, const uint8_t *d_in, uint32_t
     FQZ5_HIP(launch_seq_side(J, g.stream));
     FQZ5_HIP(launch_rec_entropy(J.rec, nev, part, EB, g.stream));
     W.nev = nev;
+    // the heads, runs and sorted contexts back to the pool (the records are
+    // what the coder needs): one block's, not every block's, at the peak
+    g.tmp_done(g.ev_tmp);
 }
 
 void seq_encode_prepare(GpuCtx &g, std::vector<SeqEncReq> &reqs) {
