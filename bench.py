@@ -109,14 +109,15 @@ def pmc_traffic(kernel: str, tag: str = ""):
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_pmc{tag}.json")))
     if not files:
-        return None, None
-    ks = json.load(open(files[-1]))["kernels"]
-    for k, v in ks.items():
+        return None, None, None
+    js = json.load(open(files[-1]))
+    for k, v in js["kernels"].items():
         if f"::{kernel}(" in k or f"::{kernel}<" in k:
-            # the step's main launch of the kernel (the largest dispatch)
+            # the step's main launch of the kernel (the largest dispatch);
+            # the file's "note" says how that launch ran (hedged copies)
             b = v.get("hbm_bytes_max_dispatch", v["hbm_bytes_per_dispatch"])
-            return int(b), os.path.relpath(files[-1], ROOT)
-    return None, None
+            return int(b), os.path.relpath(files[-1], ROOT), js.get("note")
+    return None, None, None
 
 
 def cpu_baseline(fastq: str, level: int, threads: int, gpu_blocks, exe_name="fqzcomp5",
@@ -231,6 +232,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
         decode(encode()[0])
     arena0 = lib.arena_bytes()
     lib.arena_peak(reset=True)
+    lib.arena_use_peak(reset=True)
     so = lib.load()
     fq0 = S.trial_counts()
     so.fqz5_profile(1)
@@ -267,7 +269,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     so.fqz5_profile(0)
     fq1 = S.trial_counts()
     arena1 = lib.arena_bytes()
-    arena_pk = lib.arena_peak()
+    arena_pk, arena_use = lib.arena_peak(), lib.arena_use_peak()
     # the exchange's tensors live where the process group's backend wants them
     xdev = dev if world == 1 or dist.get_backend() == "nccl" else torch.device("cpu")
     tm = torch.tensor([dt, t_enc, t_dec], dtype=torch.float64, device=xdev)
@@ -353,7 +355,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                    # chunks included): held before / after the timed steps
                    # and the peak during them
                    "arena_bytes": {"held_start": int(arena0), "held_end": int(arena1),
-                                   "peak": int(arena_pk)},
+                                   "peak_held": int(arena_pk), "peak_in_use": int(arena_use)},
                    # candidates in the timed steps, and how many were provably
                    # losing and skipped their range chain (output unchanged)
                    "fqz_trial": {"tried": fq1[0] - fq0[0], "pruned": fq1[1] - fq0[1],
@@ -377,13 +379,14 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     ms, n, b = per_kernel[name]["ms"], per_kernel[name]["launches"], per_kernel[name]["bytes"]
     avg_ms = ms / max(n, 1)
     ach = (b / max(n, 1)) / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
-    traffic, tsrc = pmc_traffic(name, pmc_tag)
+    traffic, tsrc, tnote = pmc_traffic(name, pmc_tag)
     # the decode launch is bound by its longest rANS chain: one step = one
     # symbol on each of the 4 interleaved states
     longest = max((e - s) for _, s, e, _, _ in run.spans)
     out["roofline"] = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS,
                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 7),
-                       "traffic": traffic, "traffic_source": tsrc, "kernel": name,
+                       "traffic": traffic, "traffic_source": tsrc,
+                       "traffic_note": tnote, "kernel": name,
                        "avg_launch_ms": round(avg_ms, 3),
                        "bytes_per_launch": int(b / max(n, 1)),
                        "enc_avg_ms": round(enc_ms / max(enc_n, 1), 3),
