@@ -62,11 +62,11 @@ sys.path.insert(0, ROOT)
 # the -3 encode waited 100 ms per step behind the LZP3 helper's chain).
 # Must be set before anything initialises HIP.
 # (the rule of capi.cpp's hw_queues_default: FQZ5_HW_QUEUES as given, else
-# an unset value or HIP's default of 4 raised to 32, any other value kept)
+# an unset value or HIP's default of 4 raised to 16, any other value kept)
 if os.environ.get("FQZ5_HW_QUEUES"):
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ["FQZ5_HW_QUEUES"]
 elif os.environ.get("GPU_MAX_HW_QUEUES", "") in ("", "4"):
-    os.environ["GPU_MAX_HW_QUEUES"] = "32"
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 FASTQ_REC = 358          # bytes of FASTQ text per synthetic 150 bp record (avg)
 GAP_S = float(os.environ.get("FQZ5_BENCH_GAP_S", "0") or 0)

@@ -47,7 +47,12 @@ namespace fqz5 {
 // (e.g. the relinked CLI) loads this library before anything touched HIP:
 // FQZ5_HW_QUEUES, when set, is used as given (experiments, fewer queues
 // included); otherwise an unset GPU_MAX_HW_QUEUES or HIP's default of 4 is
-// raised to 32, and any other value the caller chose is kept.
+// raised to 16, and any other value the caller chose is kept.  Not 32: once
+// the helper contexts had mapped 32 queues, every later long kernel ran
+// ~30 % slower (a 44.5M-symbol fqz decode 180 -> 232 ns per symbol after a
+// -5 encode, 180 with 4, 8 or 16 queues): the
+// scheduler time-slices more queues than the hardware maps at once, and the
+// running waves are preempted and restored.
 __attribute__((constructor)) static void hw_queues_default() {
     const char *v = std::getenv("GPU_MAX_HW_QUEUES");
     const char *w = std::getenv("FQZ5_HW_QUEUES");
@@ -55,7 +60,7 @@ __attribute__((constructor)) static void hw_queues_default() {
         setenv("GPU_MAX_HW_QUEUES", w, 1);
         return;
     }
-    if (!v || !*v || std::atoi(v) == 4) setenv("GPU_MAX_HW_QUEUES", "32", 1);
+    if (!v || !*v || std::atoi(v) == 4) setenv("GPU_MAX_HW_QUEUES", "16", 1);
 }
 
 static thread_local std::string g_err;
@@ -422,6 +427,7 @@ const char *fqz5_last_error(void) { return g_err.c_str(); }
 
 uint64_t fqz5_arena_bytes(void) { return arena_bytes(); }
 uint64_t fqz5_arena_peak(int reset) { return ChunkPool::get().peak(reset != 0); }
+uint64_t fqz5_arena_use_peak(int reset) { return ChunkPool::get().use_peak(reset != 0); }
 
 unsigned fqz5_set_hot_min(unsigned min_events) { return fqz_set_hot_min(min_events); }
 

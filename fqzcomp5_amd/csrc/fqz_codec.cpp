@@ -14,6 +14,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "../../include/fqz5_mi355x.h"
@@ -778,12 +780,9 @@ uint8_t *fqz_encode_gpu(int vers, fqz_slice *s, const uint8_t *in, size_t n, siz
 
 static std::atomic<uint64_t> g_dec_blocks[2];
 uint64_t fqz_dec_blocks(bool small) { return g_dec_blocks[small ? 1 : 0].load(); }
-int small_copies() {
-    static const int n = [] {
-        const char *e = std::getenv("FQZ5_SMALL_COPIES");
-        return e ? std::max(1, std::atoi(e)) : 2;
-    }();
-    return n;
+int small_copies() {   // read per launch (experiments change it in-process)
+    const char *e = std::getenv("FQZ5_SMALL_COPIES");
+    return e ? std::max(1, std::atoi(e)) : 2;
 }
 
 struct FqzDecReq::Work {
@@ -797,6 +796,26 @@ struct FqzDecReq::Work {
 };
 
 namespace {
+
+// every set of the small decoder's 4-way cache starts with the fresh models
+// of 4 distinct contexts that map to it (fqz_decode_small.hip, same hash)
+bool small_sets_ok(uint32_t ns) {
+    static std::mutex mu;
+    static std::map<uint32_t, bool> seen;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = seen.find(ns);
+    if (it != seen.end()) return it->second;
+    std::vector<uint8_t> cnt(ns, 0);
+    const uint64_t ns8 = uint64_t(ns << 8) & 0xffffffu;
+    for (uint32_t c = 0; c < uint32_t(FQZ_CTX); c++) {
+        const uint64_t h = (c * 0x9E3779u) & 0xffffffu;
+        uint8_t &k = cnt[size_t((h * ns8) >> 32)];
+        if (k < FQZ_SMALL_WAYS) k++;
+    }
+    bool ok = ns > 0 && (ns << 8) <= 0xffffffu;
+    for (uint8_t k : cnt) ok = ok && k == FQZ_SMALL_WAYS;
+    return seen[ns] = ok;
+}
 
 void dec_lists(GpuCtx &g, FqzDecReq::Work &W) {
     FqzDecJob &D = W.D;
@@ -883,12 +902,14 @@ void fqz_decode_batch(GpuCtx &g, std::vector<FqzDecReq> &reqs) {
             for (uint32_t i = 0; i < nlive; i++) ident = ident && (pm.qtab[i] & 0xffffu) == i;
             for (int i = 0; i < 256; i++) W.dt = W.dt || pm.dtab[i] != 0;
         }
-        W.small = small_decoder_on() && nlive <= FQZ_SMALL_MAX_LIVE && nlive >= 2 && ident && !W.seq_ctx;
+        uint32_t small_ns = fqz_small_sets(uint32_t(G.nparam));
+        if (const char *e = std::getenv("FQZ5_DEC_SETS"))   // tests: force misses
+            small_ns = std::max<uint32_t>(1, std::min<uint32_t>(small_ns, uint32_t(std::atoi(e))));
+        W.small = small_decoder_on() && nlive <= FQZ_SMALL_MAX_LIVE && nlive >= 2 && ident &&
+                  !W.seq_ctx && small_sets_ok(small_ns);
         if (W.small) {
             D.ment = FQZ_SMALL_MODEL_BYTES;
-            D.nsets = fqz_small_sets(uint32_t(G.nparam));
-            if (const char *e = std::getenv("FQZ5_DEC_SETS"))   // tests: force misses
-                D.nsets = std::max<uint32_t>(1, std::min<uint32_t>(D.nsets, uint32_t(std::atoi(e))));
+            D.nsets = small_ns;
             D.back = g.arena.alloc_n<uint8_t>(size_t(FQZ_CTX) * D.ment);
             D.back_hi = nullptr;
             D.hi_bits = nullptr;

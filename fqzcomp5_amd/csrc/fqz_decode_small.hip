@@ -18,9 +18,21 @@
 //                           1..8; with 9 live symbols slot 9's symbol is the
 //                           one missing from the eight)
 //
-// so ~6 280 models fit one direct-mapped LDS cache, and the backing store
-// (65 536 x 24 B = 1.5 MB, pre-filled with fresh models so a miss never
-// asks whether a context was seen) stays in the XCD's L2.
+// so ~6 280 models fit one LDS cache, and the backing store (65 536 x 24 B =
+// 1.5 MB, pre-filled with fresh models so a miss never asks whether a
+// context was seen) stays in the XCD's L2.
+//
+// The cache is 4-way set associative (1 570 sets of 96 bytes): the run's
+// 64 lanes are 4 rows of 16, row w reads way w of the set, the tag test is
+// one v_cmp per lane and the decode ballot is masked to the hit row.  A miss
+// replaces a round-robin victim way.  Measured on the FQZ1 Illumina contexts
+// (tools/fqz_stats.c dump, ~6 270 contexts in a cycle): direct-mapped 8.4 %
+// misses, 4-way LRU 0.43 %, 4-way round robin 0.68 % (GPU counters: 0.7 %).
+//
+// (Measured and not kept: reading the set of the context that slot 1 leads
+// to a symbol early, slot 1 being decoded for ~87 % of the symbols, into a
+// second register set with a twin loop body: 177 -> 213 ns per symbol; the
+// set addresses on the scalar unit instead of three VALU hashes: 226.)
 //
 // The decode of a symbol (lane i holds U_{i+1}, the model of the current
 // context in registers):
@@ -57,6 +69,8 @@ static_assert(S_PAR == FQZ_SMALL_LDS_FIXED, "keep fqz_kernels.h in step");
 static_assert(SPB == FQZ_SMALL_PARAM_BYTES, "keep fqz_kernels.h in step");
 static_assert(sizeof(SmallModels) <= S_RING, "small models");
 constexpr uint32_t ME = FQZ_SMALL_MODEL_BYTES;           // 24
+constexpr uint32_t WAYS = FQZ_SMALL_WAYS, SETB = WAYS * ME;   // a set: 4 models
+static_assert(WAYS == 4 && SETB == 96, "the run's lane rows are the ways");
 
 DEV void stage_s(uint8_t *lds, const In &in) { stage<S_RING>(lds, in); }
 DEV void refill_s(uint8_t *lds, In &in) { refill<S_RING>(lds, in); }
@@ -66,7 +80,7 @@ DEV void refill_s(uint8_t *lds, In &in) { refill<S_RING>(lds, in); }
 DEV uint32_t sset(uint32_t ctx, uint32_t ns8, uint32_t cb) {
     const uint32_t h = ctx * 0x9E3779u;
     const uint32_t set = uint32_t((uint64_t(h & 0xffffffu) * (ns8 & 0xffffffu)) >> 32);
-    return cb + set * ME;
+    return cb + set * SETB;
 }
 
 // the fresh model's words (every live symbol frequency 1, in symbol order)
@@ -140,23 +154,23 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "s_mov_b32 m0, %[done]\n"                                               \
     "s_mov_b32 %[flags], 0\n"                                               \
     "v_add_u32 %[vaddr], %[ma], %[voff]\n"                                  \
-    "v_mov_b32 %[vb], %[ma]\n"                                              \
+    "v_add_u32 %[vb], %[ma], %[vwoff]\n"                                    \
     "ds_read_u16 %[vU], %[vaddr]\n"                                         \
     "ds_read_b64 v[2:3], %[vb] offset:16\n"                                 \
     "10:\n"                                                                 \
     "s_waitcnt lgkmcnt(0)\n"                                                \
     "11:\n"                                                                 \
-    "v_cmp_ne_u16_e32 vcc, %[c], v2\n"                                      \
-    "v_sub_u32_dpp %[t4], %[vU], %[vU] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n" \
+    "v_cmp_eq_u16_e32 vcc, %[c], v2\n"                                      \
+    "v_sub_u32_dpp %[t4], %[vU], %[vU] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n"\
     "v_readlane_b32 %[u], %[pvv], m0\n"                                     \
     "v_lshrrev_b32 %[t6], 16, v2\n"                                         \
     DTU                                                                     \
     "v_cvt_f64_u32 %[d0], %[rng]\n"                                         \
-    "v_sub_u32_dpp %[vsw], %[t4], %[t4] row_shr:1 row_mask:0xf bank_mask:0xf\n" \
+    "v_sub_u32_dpp %[vsw], %[t4], %[t4] row_shr:1 row_mask:0xf bank_mask:0xf\n"\
     "v_cvt_f64_u32 %[d1], %[t6]\n"                                          \
     DTADD                                                                   \
     "v_rcp_f64 %[d2], %[d1]\n"                                              \
-    "s_cbranch_vccnz 60f\n"                                                 \
+    "s_cbranch_vccz 60f\n"                                                  \
     "v_bfe_u32 %[t0], v3, %[vsh4], 4\n"                                     \
     "v_fma_f64 %[d1], -%[d1], %[d2], 1.0\n"                                 \
     "v_cmp_lt_i32_e64 %[SW], -16, %[vsw]\n"                                 \
@@ -171,14 +185,14 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "v_mul_u32_u24 %[t2], 0x9e3779, %[t1]\n"                                \
     "v_mul_lo_u32 %[t3], %[vU], %[t3]\n"                                    \
     "v_mul_hi_u32_u24 %[t2], %[ns8], %[t2]\n"                               \
-    "v_mad_u32_u24 %[t2], %[t2], 24, %[base]\n"                             \
+    "v_mad_u32_u24 %[t2], %[t2], %[v96], %[base]\n"                         \
     "v_cmp_gt_u32_e64 %[G], %[t3], s41\n"                                   \
     "v_and_b32 %[t5], %[vm63], %[t3]\n"                                     \
     "s_nop 1\n"                                                             \
     "s_andn2_b64 %[G], %[G], %[HV]\n"                                       \
+    "s_and_b64 %[G], %[G], vcc\n"                                           \
     "s_ff1_i32_b64 %[k1], %[G]\n"                                           \
-    "s_cmp_ge_u32 %[k1], %[lfast]\n"                                        \
-    "s_cbranch_scc1 12f\n"                                                  \
+    "s_or_b64 %[SW], %[SW], %[lslow]\n"                                     \
     "s_bitcmp1_b64 %[SW], %[k1]\n"                                          \
     "s_cbranch_scc1 12f\n"                                                  \
     "v_readlane_b32 %[pk1], %[t3], %[k1]\n"                                 \
@@ -203,7 +217,7 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "s_mov_b32 %[c], %[cn]\n"                                               \
     "s_mov_b32 %[ma], %[man]\n"                                             \
     "v_add_u32 %[vaddr], %[man], %[voff]\n"                                 \
-    "v_mov_b32 %[vb], %[man]\n"                                             \
+    "v_add_u32 %[vb], %[man], %[vwoff]\n"                                   \
     "ds_read_u16 %[vU], %[vaddr]\n"                                         \
     "ds_read_b64 v[2:3], %[vb] offset:16\n"                                 \
     "s_and_b32 %[z], %[z], 24\n"                                            \
@@ -223,13 +237,18 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     FQS_RENORM_OUT("40", "30")                                              \
     FQS_RENORM_OUT("41", "31")                                              \
     "60:\n"                                                                 \
-    "v_readfirstlane_b32 %[x], v2\n"                                        \
-    "s_and_b32 %[x], %[x], 0xffff\n"                                        \
-    "v_mad_u32_u24 %[t4], %[x], 24, %[voff]\n"                              \
-    "v_mad_u32_u24 %[t5], %[x], 24, 20\n"                                   \
+    "s_add_u32 %[vic], %[vic], 1\n"                                         \
+    "s_and_b32 %[x], %[vic], 3\n"                                           \
+    "s_lshl_b32 %[x], %[x], 4\n"                                            \
+    "s_lshl_b64 %[HV], 0xffff, %[x]\n"                                      \
+    "v_readlane_b32 %[k1], v2, %[x]\n"                                      \
+    "s_mov_b64 exec, %[HV]\n"                                               \
+    "s_and_b32 %[k1], %[k1], 0xffff\n"                                      \
+    "v_mad_u32_u24 %[t4], %[k1], 24, %[vjoff]\n"                            \
+    "v_mad_u32_u24 %[t5], %[k1], 24, 20\n"                                  \
     "global_store_short %[t4], %[vU], %[back]\n"                            \
     "global_store_dword %[t5], v3, %[back]\n"                               \
-    "v_mad_u32_u24 %[t4], %[c], 24, %[voff]\n"                              \
+    "v_mad_u32_u24 %[t4], %[c], 24, %[vjoff]\n"                             \
     "v_mad_u32_u24 %[t5], %[c], 24, 16\n"                                   \
     "global_load_ushort %[vU], %[t4], %[back]\n"                            \
     "global_load_dwordx2 v[2:3], %[t5], %[back]\n"                          \
@@ -239,6 +258,8 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "v_or_b32 v2, %[c], v2\n"                                               \
     "ds_write_b16 %[vaddr], %[vU]\n"                                        \
     "ds_write_b64 %[vb], v[2:3] offset:16\n"                                \
+    "s_mov_b64 exec, -1\n"                                                  \
+    "s_nop 4\n"                                                             \
     "s_branch 11b\n"                                                        \
     "12:\n"                                                                 \
     "s_mov_b32 %[flags], 2\n"                                               \
@@ -275,17 +296,30 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
         for (uint32_t i = l; i < 1024; i += 64) pt[i] = uint16_t(g.p[x].ptab[i]);
         for (uint32_t i = l; i < 256; i += 64) pt[(S_DTAB >> 1) + i] = uint16_t(g.p[x].dtab[i]);
     }
-    // every set holds the fresh model of a context that maps to it (the
-    // backing store holds every context's fresh model), so a set always holds
-    // some context's true state
-    for (uint32_t s = l; s < NS; s += 64) {
-        uint32_t *m = reinterpret_cast<uint32_t *>(lds + CB + s * ME);
-        for (uint32_t w = 0; w < 6; w++) m[w] = fresh_word(w, L, 0);
+    // every way of a set holds the fresh model of a distinct context that
+    // maps to the set (the backing store holds every context's fresh model),
+    // so a way always holds some context's true state: way r takes the r-th
+    // context to claim the set (an LDS counter in way 0's symbol word; the
+    // host checks that every set has at least 4 contexts)
+    for (uint32_t s = l; s < NS; s += 64) *reinterpret_cast<uint32_t *>(lds + CB + s * SETB + 20) = 0u;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    for (uint32_t c = l; c < FQZ_CTX; c += 64) {
+        const uint32_t a = sset(c, NS8, CB);
+        uint32_t *cnt = static_cast<uint32_t *>(__builtin_assume_aligned(lds + a + 20, 4));
+        const uint32_t r = atomicAdd(cnt, 1u);
+        if (r < WAYS) *reinterpret_cast<uint16_t *>(lds + a + r * ME + 16) = uint16_t(c);
     }
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t c = l; c < FQZ_CTX; c += 64)
-        *reinterpret_cast<uint16_t *>(lds + sset(c, NS8, CB) + 16) = uint16_t(c);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    for (uint32_t m = l; m < NS * WAYS; m += 64) {
+        uint8_t *mm = lds + CB + m * ME;
+        for (uint32_t w = 0; w < 4; w++) reinterpret_cast<uint32_t *>(mm)[w] = fresh_word(w, L, 0);
+        *reinterpret_cast<uint16_t *>(mm + 18) = uint16_t(L);
+        reinterpret_cast<uint32_t *>(mm)[5] = fresh_word(5, L, 0);
+    }
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
 
     In in;
     uint32_t code = 0;
@@ -303,7 +337,11 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
     uint32_t ctx = 0, maddr = CB;
     const uint32_t dlane = S_DUMMY + 4 * l;
     const uint16_t *pt16 = reinterpret_cast<const uint16_t *>(lds + S_PAR);
-    const uint32_t voff = l < 8 ? 2 * l : 18;          // lane i: U_{i+1}, lanes 8.. the total
+    // the run's lanes are 4 rows of 16, row w = way w of the set: lane 16w + i
+    // holds U_{i+1} of that way's model, lanes 16w + 8.. its total
+    const uint32_t vjoff = (l & 15u) < 8u ? 2u * (l & 15u) : 18u;
+    const uint32_t vwoff = ME * (l >> 4), voff = vwoff + vjoff;
+    uint32_t vic = 0;                                  // the miss victim: way vic & 3
 
     auto flush = [&]() {
         for (uint32_t o = l * 4; o < fill; o += 256) {
@@ -328,30 +366,36 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
         prevq = sym;
         left--;
     };
-    // ctx's model into its set: the resident model goes back to the store
-    auto ensure = [&]() {
-        const uint32_t tag = U(*reinterpret_cast<const uint16_t *>(lds + maddr + 16));
-        if (tag == ctx) return;
+    // the way of ctx's set that holds its model; on a miss the victim way's
+    // model goes back to the store and ctx's comes in (the run's rule)
+    auto ensure = [&]() -> uint32_t {
+        for (uint32_t w = 0; w < WAYS; w++)
+            if (U(*reinterpret_cast<const uint16_t *>(lds + maddr + w * ME + 16)) == ctx)
+                return maddr + w * ME;
         nmiss++;
-        uint32_t *m32 = reinterpret_cast<uint32_t *>(lds + maddr);
+        vic = U(vic + 1u);
+        const uint32_t wa = maddr + (vic & 3u) * ME;
+        const uint32_t tag = U(*reinterpret_cast<const uint16_t *>(lds + wa + 16));
+        uint32_t *m32 = reinterpret_cast<uint32_t *>(lds + wa);
         const uint32_t mine = l < 6 ? m32[l] : 0u;
         uint32_t *dst = reinterpret_cast<uint32_t *>(J.back + size_t(tag) * ME);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(J.back + size_t(ctx) * ME);
         if (l < 6) __hip_atomic_store(dst + l, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         const uint32_t v = l < 6 ? __hip_atomic_load(src + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0u;
         __builtin_amdgcn_wave_barrier();
-        if (l < 6) m32[l] = v;
+        if (l < 6) m32[l] = l == 4 ? (v & 0xffff0000u) | ctx : v;
         __builtin_amdgcn_wave_barrier();
+        return wa;
     };
     // one symbol with the reference's arithmetic (c_simple_model.h:140-171,
     // fl_bump): halving, bubble steps, the 9th slot, corrupt or truncated
     // streams, the last bytes of the input
     auto slow_symbol = [&]() {
         nslow++;
-        ensure();
-        const uint32_t uw = *reinterpret_cast<const uint16_t *>(lds + maddr + voff);
-        const uint32_t S = U(*reinterpret_cast<const uint32_t *>(lds + maddr + 20));
-        uint32_t total = U(*reinterpret_cast<const uint16_t *>(lds + maddr + 18));
+        const uint32_t wa = ensure();
+        const uint32_t uw = *reinterpret_cast<const uint16_t *>(lds + wa + vjoff);
+        const uint32_t S = U(*reinterpret_cast<const uint32_t *>(lds + wa + 20));
+        uint32_t total = U(*reinterpret_cast<const uint16_t *>(lds + wa + 18));
         uint32_t t = 0;
         if (total && rng >= total) {   // the division stays even when no symbol follows
             rng /= total;
@@ -400,10 +444,10 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
             total = RL(inc, L - 1);
             uint32_t nS = 0;
             for (uint32_t i = 0; i < 8; i++) nS |= (RL(sy, i) & 15u) << (4 * i);
-            if (l < 8) *reinterpret_cast<uint16_t *>(lds + maddr + 2 * l) = uint16_t(live ? inc : total);
+            if (l < 8) *reinterpret_cast<uint16_t *>(lds + wa + 2 * l) = uint16_t(live ? inc : total);
             if (l == 0) {
-                *reinterpret_cast<uint16_t *>(lds + maddr + 18) = uint16_t(total);
-                *reinterpret_cast<uint32_t *>(lds + maddr + 20) = nS;
+                *reinterpret_cast<uint16_t *>(lds + wa + 18) = uint16_t(total);
+                *reinterpret_cast<uint32_t *>(lds + wa + 20) = nS;
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -492,7 +536,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
             uint64_t mAS = 0;
             uint32_t cc = U(ctx), pv = U(prevq), ma = U(maddr);
             uint32_t dd = 0, nm = 0;
-            uint32_t vU = 0, vaddr = 0, vsw = l == 0 ? 0x80000000u : 0u;
+            uint32_t vU = 0, vaddr = 0, vsw = (l & 15u) == 0 ? 0x80000000u : 0u;
             uint64_t scr;
             const uint64_t back = reinterpret_cast<uint64_t>(J.back);
             rng = U(rng);
@@ -508,8 +552,12 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
             ulim = U(ulim);
             const uint32_t base = U(CB), cbig = 0x100000u, c65503 = 65503u;
             const uint32_t ns8 = U(NS8), qlocv = ps.qloc, qmask = U(ps.qmask);
+            // slots past min(L, 8) of every row go to the slow path with
+            // the bubbles (one mask); p_{k-1} of slot 1 (a row's lane 0) is
+            // read from the lane before the row: 0
             const uint32_t lfast = U(L < 8u ? L : 8u), vsh4 = 4u * (l & 7u);
-            const uint32_t vm63 = l == 63 ? 0u : ~0u;   // p_{k-1} of slot 1 read from lane 63: 0
+            const uint64_t lslow = 0x0001000100010001ull * uint64_t(0xffffu & ~((1u << lfast) - 1u));
+            const uint32_t vm63 = (l & 15u) == 15u ? 0u : ~0u;
             const double c19 = 0x1p-19;
             uint32_t u, x, k1, pk, pk1, cn, man, qsk, sym, z, m0s;
             uint64_t G, SW, HV;
@@ -520,7 +568,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
                 : [mAS] "+{v[2:3]}"(mAS), [cw] "+{s[40:41]}"(cw), [win] "+{s[42:43]}"(win),   \
                   [scr] "=&{s[44:45]}"(scr), [rb] "+s"(in.rb), [ub] "+s"(in.ub),               \
                   [rng] "+s"(rng), [dd] "+s"(dd), [done] "+s"(done), [nm] "+s"(nm),            \
-                  [c] "+s"(cc), [qs] "+s"(qs), [pv] "+s"(pv), [ma] "+s"(ma),                   \
+                  [c] "+s"(cc), [qs] "+s"(qs), [pv] "+s"(pv), [ma] "+s"(ma), [vic] "+s"(vic),  \
                   [flags] "=&s"(flags), [vU] "+v"(vU), [vaddr] "+v"(vaddr), [vout] "+v"(vout),  \
                   [vsw] "+v"(vsw), [vb] "=&v"(vb),                                             \
                   [u] "=&s"(u), [x] "=&s"(x), [k1] "=&s"(k1), [pk] "=&s"(pk), [pk1] "=&s"(pk1), \
@@ -530,11 +578,11 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
                   [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6),                              \
                   [d0] "=&v"(d0), [d1] "=&v"(d1), [d2] "=&v"(d2)                               \
                 : [lim] "s"(lim), [ulim] "s"(ulim), [qmask] "s"(qmask), [qshift] "s"(qshift), \
-                  [ns8] "s"(ns8), [base] "s"(base), [lfast] "s"(lfast), [c65503] "s"(c65503), \
+                  [ns8] "s"(ns8), [base] "s"(base), [lslow] "s"(lslow), [c65503] "s"(c65503), \
                   [rbend] "s"(rbend), [bswp] "s"(bswp), [lring] "i"(S_RING), [back] "s"(back),  \
                   [voff] "v"(voff), [vsh4] "v"(vsh4), [qlocv] "v"(qlocv), [cbig] "v"(cbig),   \
                   [c19] "v"(c19), [pvv] "v"(pvv), [dvv] "v"(dvv),                              \
-                  [vm63] "v"(vm63)                                                             \
+                  [vm63] "v"(vm63), [vwoff] "v"(vwoff), [vjoff] "v"(vjoff), [v96] "v"(SETB)    \
                 : "memory", "scc", "vcc"
                 if constexpr (DT)
                     asm volatile(FQS_RUN_ASM(FQS_DT_U, FQS_DT_ADD, FQS_DT_UPD) FQS_OPERANDS);
@@ -553,6 +601,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
                 qs = U(qs);
                 pv = U(pv);
                 ma = U(ma);
+                vic = U(vic);
                 flags = U(flags);
                 cw = (uint64_t(U(uint32_t(cw >> 32))) << 32);
                 win = (uint64_t(U(uint32_t(win >> 32))) << 32) | U(uint32_t(win));

@@ -100,15 +100,18 @@ constexpr uint32_t FQZ_DEC_MAX_LIVE = 126u;   // guard + slots + sentinel in two
 
 // The small-alphabet decoder (fqz_decode_small.hip): models of at most 9
 // live symbols as 24 bytes (u16 cumulative counts of slots 1..8, the tag,
-// the total, the slots' symbols as nibbles) in a direct-mapped LDS cache
-// after FQZ_SMALL_LDS_FIXED bytes and FQZ_SMALL_PARAM_BYTES per parameter
-// block; the backing store is FQZ_CTX models of 24 bytes.
+// the total, the slots' symbols as nibbles) in a 4-way set-associative LDS
+// cache (FqzDecJob::nsets counts sets of FQZ_SMALL_WAYS models) after
+// FQZ_SMALL_LDS_FIXED bytes and FQZ_SMALL_PARAM_BYTES per parameter block;
+// the backing store is FQZ_CTX models of 24 bytes.
 constexpr uint32_t FQZ_SMALL_MAX_LIVE = 9u;
 constexpr uint32_t FQZ_SMALL_MODEL_BYTES = 24u;
+constexpr uint32_t FQZ_SMALL_WAYS = 4u;
 constexpr uint32_t FQZ_SMALL_LDS_FIXED = 10512u;
 constexpr uint32_t FQZ_SMALL_PARAM_BYTES = 2560u;
 constexpr uint32_t fqz_small_sets(uint32_t nparam) {
-    return (163840u - FQZ_SMALL_LDS_FIXED - nparam * FQZ_SMALL_PARAM_BYTES) / FQZ_SMALL_MODEL_BYTES;
+    return (163840u - FQZ_SMALL_LDS_FIXED - nparam * FQZ_SMALL_PARAM_BYTES) /
+           (FQZ_SMALL_WAYS * FQZ_SMALL_MODEL_BYTES);
 }
 
 // Parallel encoder (fqz_kernels.hip): the block becomes a list of coding

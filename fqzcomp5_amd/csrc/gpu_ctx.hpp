@@ -53,6 +53,7 @@ class ChunkPool {
                 *got = it->first;
                 idle_bytes_ -= it->first;
                 idle_.erase(it);
+                use(it->first);
                 return b;
             }
         }
@@ -65,6 +66,7 @@ class ChunkPool {
         std::lock_guard<std::mutex> lk(m_);
         held_ += need;
         peak_ = std::max(peak_, held_);
+        use(need);
         *got = need;
         return b;
     }
@@ -73,6 +75,7 @@ class ChunkPool {
             std::lock_guard<std::mutex> lk(m_);
             idle_.emplace(sz, b);
             idle_bytes_ += sz;
+            in_use_ -= sz;
         }
         if (idle_bytes_ > idle_cap()) trim(idle_cap());
     }
@@ -80,6 +83,7 @@ class ChunkPool {
         (void)hipFree(b);
         std::lock_guard<std::mutex> lk(m_);
         held_ -= sz;
+        in_use_ -= sz;
     }
     // idle chunks back to the device until at most `keep` bytes stay idle
     void trim(size_t keep) {
@@ -103,6 +107,14 @@ class ChunkPool {
         if (reset) peak_ = held_;
         return p;
     }
+    // the most bytes in use at once (held minus idle: what the work itself
+    // needed, without the chunks kept idle for reuse)
+    size_t use_peak(bool reset) {
+        std::lock_guard<std::mutex> lk(m_);
+        const size_t p = use_peak_;
+        if (reset) use_peak_ = in_use_;
+        return p;
+    }
 
   private:
     // Idle chunks kept for reuse: a quarter of the device's memory (or
@@ -119,9 +131,13 @@ class ChunkPool {
         }();
         return c;
     }
+    void use(size_t n) {   // under m_
+        in_use_ += n;
+        use_peak_ = std::max(use_peak_, in_use_);
+    }
     std::mutex m_;
     std::multimap<size_t, void *> idle_;
-    size_t idle_bytes_ = 0, held_ = 0, peak_ = 0;
+    size_t idle_bytes_ = 0, held_ = 0, peak_ = 0, in_use_ = 0, use_peak_ = 0;
 };
 
 // A bump arena over pool chunks; reset() rewinds and returns the chunks.

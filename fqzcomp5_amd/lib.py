@@ -16,11 +16,11 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 # helper contexts' streams need queues of their own (bench.py); effective
 # only when nothing in the process has initialised HIP yet
 # (the rule of capi.cpp's hw_queues_default: FQZ5_HW_QUEUES as given, else
-# an unset value or HIP's default of 4 raised to 32, any other value kept)
+# an unset value or HIP's default of 4 raised to 16, any other value kept)
 if os.environ.get("FQZ5_HW_QUEUES"):
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ["FQZ5_HW_QUEUES"]
 elif os.environ.get("GPU_MAX_HW_QUEUES", "") in ("", "4"):
-    os.environ["GPU_MAX_HW_QUEUES"] = "32"
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 _libc = C.CDLL(None)
 _libc.free.argtypes = [C.c_void_p]
@@ -167,6 +167,15 @@ def arena_peak(reset: bool = False) -> int:
     so.fqz5_arena_peak.restype = C.c_uint64
     so.fqz5_arena_peak.argtypes = [C.c_int]
     return int(so.fqz5_arena_peak(1 if reset else 0))
+
+
+def arena_use_peak(reset: bool = False) -> int:
+    """The most device bytes in use at once (held minus the pool's idle
+    chunks) since the last reset (fqz5_arena_use_peak)."""
+    so = load()
+    so.fqz5_arena_use_peak.restype = C.c_uint64
+    so.fqz5_arena_use_peak.argtypes = [C.c_int]
+    return int(so.fqz5_arena_use_peak(1 if reset else 0))
 
 
 def header_symbols() -> list[str]:

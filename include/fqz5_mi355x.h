@@ -276,9 +276,12 @@ const char *fqz5_last_error(void);
 /* Device bytes the arenas hold, process-wide: the chunks of every
  * thread's contexts, in use or idle in the shared pool (at most
  * $FQZ5_ARENA_IDLE_GB idle).  fqz5_arena_peak: the most held since the last
- * fqz5_arena_peak(1) (reset: 1 starts a new peak from the current holding). */
+ * fqz5_arena_peak(1) (reset: 1 starts a new peak from the current holding).
+ * fqz5_arena_use_peak: the most in use at once (held minus the idle chunks
+ * kept for reuse) since the last fqz5_arena_use_peak(1). */
 uint64_t fqz5_arena_bytes(void);
 uint64_t fqz5_arena_peak(int reset);
+uint64_t fqz5_arena_use_peak(int reset);
 
 /* Kernel timing with HIP events on fqz5_stream() (benchmark roofline).
  * fqz5_profile(1) resets and enables; fqz5_profile_read fills

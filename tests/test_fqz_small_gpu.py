@@ -1,8 +1,9 @@
 """GPU parity of the small-alphabet fqz decoder (fqz_decode_small.hip):
-24-byte models of at most 9 live symbols in a direct-mapped LDS cache.
+24-byte models of at most 9 live symbols in a 4-way set-associative LDS
+cache.
 
 Every case decodes through the C-ABI (fqz_decompress) with the small decoder
-on, with its cache cut to a few sets (FQZ5_DEC_SETS: nearly every symbol
+on, with its cache cut to a few 4-way sets (FQZ5_DEC_SETS: nearly every symbol
 misses, so the write-back / fetch path and its HBM backing store carry the
 decode), and off (the general decoder); all must give the reference's
 bytes.  fqz5_fqz_dec_counts shows which decoder ran."""

@@ -14,6 +14,7 @@ static struct {
     size_t stride;
     unsigned long long n, ksum, kge[8], swaps, halves, same, uniq;
     int prev;
+    FILE *dump;                       /* $FQZ_CTX_DUMP: the context of every symbol, u16 */
     unsigned char seen[65536];
     int tags[8][65536];
     int wtags[6][65536];              /* set-associative: ways consecutive, MRU first */
@@ -50,6 +51,7 @@ static unsigned fl_decode_stats(flist *m, rcoder *c, int cap) {
     S.same += ctx == S.prev;
     S.prev = ctx;
     if (!S.seen[ctx]) { S.seen[ctx] = 1; S.uniq++; }
+    if (S.dump) { const uint16_t c16 = (uint16_t)ctx; fwrite(&c16, 2, 1, S.dump); }
     const uint32_t h = ((uint32_t)ctx * 0x9E3779u) & 0xffffffu;   /* the decoder's set_addr */
     for (int i = 0; i < 6; i++) {
         const unsigned ways = WWAYS[i], nset = WMODELS[i] / ways;
@@ -96,9 +98,11 @@ int main(int argc, char **argv) {
     if (fread(in, 1, (size_t)n, f) != (size_t)n) return 2;
     fclose(f);
     S.prev = -1;
+    if (getenv("FQZ_CTX_DUMP")) S.dump = fopen(getenv("FQZ_CTX_DUMP"), "wb");
     size_t out = 0;
     uint8_t *o = ora_fqz_decompress(in, (size_t)n, &out, NULL, 0, NULL);
     if (!o) { fprintf(stderr, "decode failed\n"); return 1; }
+    if (S.dump) fclose(S.dump);
     printf("{\"n\": %llu, \"k_mean\": %.3f, \"k_gt\": [", S.n, (double)S.ksum / (double)S.n);
     for (int b = 0; b < 8; b++) printf("%s%.4f", b ? ", " : "", (double)S.kge[b] / (double)S.n);
     printf("], \"swap\": %.4f, \"halve\": %.5f, \"same_ctx\": %.4f, \"contexts\": %llu, \"miss\": {",
