@@ -85,6 +85,24 @@ def _rank(rank, world, port, args, q):
         dist.destroy_process_group()
 
 
+def _run_ranks(ps, q, wait=150):
+    """Start the rank processes and collect one result from each; a rank
+    that has not answered within `wait` seconds (under the GPU box's 180 s
+    silence limit) fails the test, and every rank still alive at the end is
+    killed, so no rank outlives its test (a lingering rank held the next
+    test's rendezvous once)."""
+    for p in ps:
+        p.start()
+    try:
+        return [q.get(timeout=wait) for _ in ps]
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -107,11 +125,7 @@ def test_two_ranks_equal_one_process(tmp_path, level):
     port = _free_port()
     ps = [ctx.Process(target=_rank, args=(r, 2, port, (src, two, back, level, 40_000_000), q))
           for r in range(2)]
-    for p in ps:
-        p.start()
-    out = [q.get(timeout=400) for _ in range(2)]
-    for p in ps:
-        p.join(timeout=60)
+    out = _run_ranks(ps, q)
     assert all(e is None for *_, e in out), out
     assert all(p.exitcode == 0 for p in ps)
     assert open(two, "rb").read() == open(one, "rb").read()
@@ -133,11 +147,7 @@ def test_two_ranks_paired_small_windows(tmp_path):
     q = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_rank_pairs, args=(r, 2, port, (r1, r2, two), q)) for r in range(2)]
-    for p in ps:
-        p.start()
-    out = [q.get(timeout=300) for _ in range(2)]
-    for p in ps:
-        p.join(timeout=60)
+    out = _run_ranks(ps, q)
     assert all(e is None for *_, e in out), out
     assert open(two, "rb").read() == open(one, "rb").read()
 
