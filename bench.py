@@ -111,13 +111,19 @@ def pmc_traffic(kernel: str, tag: str = ""):
     if not files:
         return None, None, None
     js = json.load(open(files[-1]))
+    # k_fqz_dec times both fqz decoders (fqz_codec.cpp PK_FQZ_DEC): the
+    # general k_fqz_dec and the small-alphabet k_fqz_dec_small
+    names = [kernel] + (["k_fqz_dec_small"] if kernel == "k_fqz_dec" else [])
+    best = None
     for k, v in js["kernels"].items():
-        if f"::{kernel}(" in k or f"::{kernel}<" in k:
+        if any(f"::{n}(" in k or f"::{n}<" in k for n in names):
             # the step's main launch of the kernel (the largest dispatch);
             # the file's "note" says how that launch ran (hedged copies)
-            b = v.get("hbm_bytes_max_dispatch", v["hbm_bytes_per_dispatch"])
-            return int(b), os.path.relpath(files[-1], ROOT), js.get("note")
-    return None, None, None
+            b = int(v.get("hbm_bytes_max_dispatch", v["hbm_bytes_per_dispatch"]))
+            best = b if best is None else max(best, b)
+    if best is None:
+        return None, None, None
+    return best, os.path.relpath(files[-1], ROOT), js.get("note")
 
 
 def cpu_baseline(fastq: str, level: int, threads: int, gpu_blocks, exe_name="fqzcomp5",
