@@ -1061,6 +1061,56 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             std::thread &t;
             ~Join() { if (t.joinable()) t.join(); }
         } join_names{tn};
+        // fqz quality sections without a sequence context need nothing else
+        // of this call: they decode on the fqz helper context from a thread
+        // of their own, beside the rANS / LZP / sequence-model work, instead
+        // of after it (a -5 Illumina step waited ~0.6 s for the rANS batch
+        // before its 8 s fqz launch).  Those with one wait for the bases.
+        std::vector<FqzDecReq> fqz_early;
+        std::vector<size_t> early_of;                 // fqz index of each early request
+        std::vector<char> is_early(fqz.size(), 0);
+        if (!hmode)
+            for (size_t k = 0; k < fqz.size(); k++) {
+                const FqzDecReq &f = fqz[k];
+                uint32_t tl = 0;
+                const int vk = varint_get(f.h_in, f.h_in + f.in_size, &tl);
+                const bool seqctx = vk > 0 && size_t(vk) + 1 < f.in_size && (f.h_in[vk + 1] & 8u) && f.d_seq;
+                if (seqctx) continue;
+                fqz_early.push_back(f);
+                early_of.push_back(k);
+                is_early[k] = 1;
+            }
+        std::exception_ptr ferr;
+        std::thread tf;
+        GpuCtx *gf = nullptr;
+        if (!fqz_early.empty()) {
+            gf = &gpu_aux(0);
+            tf = std::thread([&] {
+                try {
+                    FQZ5_HIP(hipSetDevice(gf->device));
+                    fqz_decode_batch(*gf, fqz_early);
+                } catch (...) {
+                    ferr = std::current_exception();
+                }
+            });
+        }
+        Join join_fqz{tf};
+        // the sequence-model sections likewise (their own helper context)
+        std::exception_ptr serr;
+        std::thread ts;
+        GpuCtx *gs = nullptr;
+        if (!hmode && !seqd.empty()) {
+            gs = &gpu_aux(AUX_SEQ0);
+            ts = std::thread([&] {
+                try {
+                    FQZ5_HIP(hipSetDevice(gs->device));
+                    seq_decode_batch(*gs, seqd);
+                } catch (...) {
+                    serr = std::current_exception();
+                }
+            });
+        }
+        Join join_seq{ts};
         decompress_batch(g, reqs);
         if (trace)
             std::fprintf(stderr, "decode_sections: %zu bytes to host in %.1f ms, rANS %.1f ms\n", tot,
@@ -1083,10 +1133,24 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
                 R.usize = run[k].out_len;
             }
         }
-        if (!hmode && !seqd.empty()) seq_decode_batch(g, seqd);
+        if (ts.joinable()) ts.join();
+        if (serr) std::rethrow_exception(serr);
         // after the rANS and sequence sections: a quality section's sequence context may
         // be the output of this call's sequence section
-        if (!hmode && !fqz.empty()) fqz_decode_batch(g, fqz);
+        if (!hmode && fqz_early.size() < fqz.size()) {
+            std::vector<FqzDecReq> late;
+            std::vector<size_t> late_of;
+            for (size_t k = 0; k < fqz.size(); k++)
+                if (!is_early[k]) {
+                    late.push_back(fqz[k]);
+                    late_of.push_back(k);
+                }
+            fqz_decode_batch(g, late);
+            for (size_t k = 0; k < late.size(); k++) fqz[late_of[k]] = late[k];
+        }
+        if (tf.joinable()) tf.join();
+        if (ferr) std::rethrow_exception(ferr);
+        for (size_t k = 0; k < fqz_early.size(); k++) fqz[early_of[k]] = fqz_early[k];
         if (hmode) {
             hjobs.join();
             // the quality chains with a sequence context: their block's bases
@@ -1163,6 +1227,8 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         }
         g.reset();
         if (gn) gn->reset();
+        if (gf) gf->reset();
+        if (gs) gs->reset();
         return 0;
     } catch (const std::exception &e) {
         fqz5_set_error(e.what());
