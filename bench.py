@@ -227,7 +227,11 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
         if level >= 7:     # 500 MB / 1 GB blocks: the trial a section at a time
             res, meth_all, sizes, tried, off = S.encode_run_bounded(enc_secs, avail, S.new_state())
         else:
-            res, meth_all, sizes, tried, off = S.encode_run(enc_secs, avail, S.new_state())
+            # -5: the fqz / sequence-model candidates' size intervals first;
+            # when they decide the trial, every block's winner is coded in one
+            # launch (sections.encode_run, bounds)
+            res, meth_all, sizes, tried, off = S.encode_run(enc_secs, avail, S.new_state(),
+                                                            bounds=level == 5)
         run.assemble(res)                          # lengths, header, CRC32
         return res, meth_all, tried, off
 
@@ -367,7 +371,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                    "fqz_trial": {"tried": fq1[0] - fq0[0], "pruned": fq1[1] - fq0[1],
                                  # -7/-9: whether the candidates' size intervals
                                  # decided the trial (else tried again exactly)
-                                 "intervals_decided": S.last_bounds_decided if level >= 7
+                                 "intervals_decided": S.last_bounds_decided if level >= 5
                                  else None}},
     }
     if hyb is not None:

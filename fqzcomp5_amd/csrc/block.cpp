@@ -733,10 +733,21 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         std::vector<int> late_lzp;
         std::vector<std::vector<int>> late_lzp_of(nsec, std::vector<int>(FQZ5_M_LAST, -1));
         std::vector<int> late_name_sec, late_name_meth, late_name_of(nsec, -1);
+        // a candidate the session tried with its range chain skipped (a
+        // bounds-only try or a pruned one) has no bytes: coded now, as a
+        // method the session did not try
+        auto coded_fqz = [&](int i, int m) {
+            const int f = t_sess.fqz_of[i][m];
+            return f >= 0 && !(size_t(f) < t_sess.fqz_lb.size() && t_sess.fqz_lb[size_t(f)] > 0);
+        };
+        auto coded_seq = [&](int i, int m) {
+            const int q = t_sess.seq_of[i][m];
+            return q >= 0 && !(size_t(q) < t_sess.seq_lb.size() && t_sess.seq_lb[size_t(q)] > 0);
+        };
         for (int i = 0; i < nsec; i++) {
             const int m = methods[i];
-            if (m <= 0 || m >= FQZ5_M_LAST || t_sess.req_of[i][m] >= 0 || t_sess.fqz_of[i][m] >= 0 ||
-                t_sess.seq_of[i][m] >= 0 || t_sess.name_of[i][m] >= 0)
+            if (m <= 0 || m >= FQZ5_M_LAST || t_sess.req_of[i][m] >= 0 || coded_fqz(i, m) ||
+                coded_seq(i, m) || t_sess.name_of[i][m] >= 0)
                 continue;
             if (is_name_method(m) && secs[i].sec == FQZ5_SEC_NAME) {
                 late_name_of[i] = int(late_name_sec.size());

@@ -474,7 +474,8 @@ def exchange_sizes(local: np.ndarray, in_sizes: np.ndarray, sec_ids: np.ndarray,
 
 
 def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
-               group=None, speculate: bool = True, prune: bool = True):
+               group=None, speculate: bool = True, prune: bool = True,
+               bounds: bool = False):
     """try -> (exchange) -> replay -> commit for this rank's sections.
 
     speculate: every section tries every method in one GPU launch.  A launch
@@ -487,7 +488,15 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
     prune: fqz and sequence-model candidates that provably cannot win the
     trial skip their range chain (fqz5_set_trial_prune), when this rank holds
     every section the schedule has try them and they form one whole trial
-    window per family."""
+    window per family.
+
+    bounds: first try with every fqz / sequence-model range chain skipped
+    (their size intervals, fqz5_set_trial_bounds); when the intervals decide
+    every choice of the trial (trial_decided), the commit codes the winners
+    in the same session, the trial blocks' beside the others' in one launch,
+    instead of the trial's chains first and the other blocks' after them.
+    Otherwise the exact tries below run as without it.  One rank, the whole
+    input in this call (bounds_usable with final=True)."""
     ins = np.array([s.in_size for s in secs], np.uint32)
     ids = np.array([s.sec for s in secs], np.int32)
     av = np.asarray(avail, np.uint32)
@@ -513,6 +522,18 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
                 continue
             prune = prune and speculate and len(rows) == TRIAL_WINDOW and \
                 bool(((rows >= off) & (rows < off + len(secs))).all())
+        if bounds and _world(group)[0] == 1 and (sched_all & WORK_MASK).any() and \
+                bounds_usable(g_ids0, sched_all, state, final=True):
+            global last_bounds_decided
+            state0 = _copy_state(state)
+            lo, hi = sections_try_bounds(secs, masks)
+            tried = np.zeros(len(secs), np.uint32)
+            meth_all = trial_replay(ids, ins, lo, avail, state, tried)
+            last_bounds_decided = trial_decided(lo, hi, ids, ins, tried, sched_all, state0,
+                                                final=True)
+            if last_bounds_decided:
+                return sections_commit(secs, meth_all), meth_all, lo, tried, 0
+            C.memmove(C.byref(state), C.byref(state0), C.sizeof(TrialState))
     so = _load()
     prev = so.fqz5_set_trial_prune(1 if prune else 0)
     try:

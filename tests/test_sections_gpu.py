@@ -163,3 +163,34 @@ def test_bounded_run_equals_run(level, kind, nreads, blk, bounds):
     assert all(r.status == 0 for r in dres)
     torch.cuda.synchronize()
     assert run_b.roundtrip_ok()
+
+
+@pytest.mark.parametrize("level,kind,nreads,blk", [(5, "illumina", 60000, 2_000_000),
+                                                   (5, "novaseq", 60000, 2_000_000),
+                                                   (7, "ont", 500, 1_500_000)])
+def test_run_bounds_first_equals_run(level, kind, nreads, blk):
+    """encode_run(bounds=True): the tries give the fqz / sequence-model size
+    intervals only; when they decide the trial the commit codes the winners
+    in the same session (skipped candidates coded late, the rANS ones
+    reused), else the exact tries run.  Same choices and bytes as
+    encode_run, and the blocks decode back."""
+    reads = GEN[kind](nreads, seed=17)
+    blocks = synth.split_blocks(reads, blk)
+    assert len(blocks) >= 4
+    dev = torch.device("cuda", 0)
+    av = S.masks(level, True)
+    run = S.Run(reads, blocks, dev, names=False)
+    res_a, meth_a, _, tried_a, _ = S.encode_run(run.enc_secs(), av, S.new_state())
+    got_a = [run.chosen(res_a, i) for i in range(len(res_a))]
+    run_b = S.Run(reads, blocks, dev, names=False)
+    res_b, meth_b, _, tried_b, _ = S.encode_run(run_b.enc_secs(), av, S.new_state(), bounds=True)
+    print(f"-{level} {kind}: intervals decided the trial: {S.last_bounds_decided}")
+    assert all(r.status == 0 for r in res_b)
+    assert list(meth_a) == list(meth_b)
+    assert list(tried_a) == list(tried_b)
+    for i in range(len(res_b)):
+        assert run_b.chosen(res_b, i) == got_a[i], i
+    dres = S.decode(run_b.dec_secs(res_b))
+    assert all(r.status == 0 for r in dres)
+    torch.cuda.synchronize()
+    assert run_b.roundtrip_ok()
