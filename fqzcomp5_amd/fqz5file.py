@@ -788,7 +788,8 @@ def _code_window(W, sink: _Sink, level: int, pos: int, index: list, av, state, g
         for q in range(per[b]):
             secs[sec0[b] + q] = local[run.blk_sec0[j] + q]
     res, meth, _ = S.encode_window(secs, ids, ins, owner, av, state, group,
-                                   bounded=level >= 7, final=W.final)
+                                   bounded=level >= 7, final=W.final,
+                                   bounds_first=5 <= level < 7)
     mine = [j for j, b in enumerate(need) if blk_owner[b] == rk]
     full_res = [None] * len(local)
     for j, b in enumerate(need):

@@ -722,7 +722,7 @@ def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
                   state: TrialState, group=None, bounded: bool = False,
                   chunk_bytes: int = 600_000_000, prune: bool = True,
                   commit_bytes: int = 2_400_000_000, bounds: bool = True,
-                  final: bool = False):
+                  final: bool = False, bounds_first: bool = False):
     """Code the sections of consecutive blocks (file order) over the ranks of
     `group`; every rank passes the same section ids / input sizes / owners,
     its Section for every section it holds the data of (None elsewhere) and
@@ -741,6 +741,10 @@ def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
     chunk_bytes, no pruning, every section coded again at commit, in chunks
     of commit_bytes; with `bounds`, the work candidates' size intervals
     first, as in encode_run_bounded; final: the input ends with this call).
+    bounds_first (not bounded, one rank): encode_run's bounds option, the
+    work candidates' size intervals first and, when they decide the trial,
+    the commit in the same session (-5: the trial blocks' fqz chains beside
+    the other blocks' in one launch).
     Returns (results: SectionResult per section or None when not owned,
     methods of every section, sizes)."""
     ws, rk = _world(group)
@@ -796,25 +800,42 @@ def encode_window(secs: list, ids, ins, owner, avail: np.ndarray,
             so.fqz5_set_trial_prune(prev)
         return lo, hi
 
+    pre = None                     # (sizes, tried, methods) decided by bounds_first
     if bounded:
         local, hi_local = bounded_tries(use_bounds)
     else:
-        # pruning of a family: its trial window whole in this call
-        for fam in (FQZ_MASK, SEQ_MASK):
-            frows = np.nonzero(sched & fam)[0]
-            if len(frows):
-                prune = prune and len(frows) == TRIAL_WINDOW
-        prev = so.fqz5_set_trial_prune(1 if prune else 0)
-        try:
-            if rows:
-                local[rows] = sections_try([secs[i] for i in rows], masks[rows])
-        finally:
-            so.fqz5_set_trial_prune(prev)
-    sizes = allreduce_min(local, group)
-    tried = np.zeros(n, np.uint32)
-    meth = trial_replay(ids, ins, sizes, av, state, tried)
+        if bounds_first and ws == 1 and rows and bool((sched & WORK_MASK).any()) and \
+                bounds_usable(ids, sched, state, final):
+            global last_bounds_decided
+            lo = np.full((n, M_LAST), np.iinfo(np.uint32).max, np.uint32)
+            hi = lo.copy()
+            lo[rows], hi[rows] = sections_try_bounds([secs[i] for i in rows], masks[rows])
+            t0 = np.zeros(n, np.uint32)
+            m0 = trial_replay(ids, ins, lo, av, state, t0)
+            last_bounds_decided = trial_decided(lo, hi, ids, ins, t0, sched, state0, final)
+            if last_bounds_decided:
+                pre = (lo, t0, m0)
+            else:
+                C.memmove(C.byref(state), C.byref(state0), C.sizeof(TrialState))
+        if pre is None:
+            # pruning of a family: its trial window whole in this call
+            for fam in (FQZ_MASK, SEQ_MASK):
+                frows = np.nonzero(sched & fam)[0]
+                if len(frows):
+                    prune = prune and len(frows) == TRIAL_WINDOW
+            prev = so.fqz5_set_trial_prune(1 if prune else 0)
+            try:
+                if rows:
+                    local[rows] = sections_try([secs[i] for i in rows], masks[rows])
+            finally:
+                so.fqz5_set_trial_prune(prev)
+    if pre is not None:
+        sizes, tried, meth = pre
+    else:
+        sizes = allreduce_min(local, group)
+        tried = np.zeros(n, np.uint32)
+        meth = trial_replay(ids, ins, sizes, av, state, tried)
     if use_bounds:
-        global last_bounds_decided
         hi_all = allreduce_min(hi_local, group)
         for _ in range(M_LAST):
             pairs = set()
