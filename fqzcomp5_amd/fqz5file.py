@@ -164,7 +164,7 @@ def parse_paired(text_d, len1: int, blk_size: int):
     if n1 and fa1 != fa2:
         raise _lib.NativeError("paired files: one FASTA, one FASTQ")
     w = C.sizeof(FastqRec)
-    recs = torch.stack([r1.view(n1, w), r2[:n1 * w].view(n1, w)], 1).reshape(-1) if n1 else r1
+    recs = _ts(torch.stack([r1.view(n1, w), r2[:n1 * w].view(n1, w)], 1).reshape(-1)) if n1 else r1
     del r1, r2
     pair = rs1.astype(np.uint64) + rs2[:n1].astype(np.uint64)
     if n1 and int(pair.max()) >= 2 ** 32:
@@ -392,7 +392,7 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
             continue
         cut = [e[k - 1] for e in ends]
         if paired:
-            text_d = torch.cat([devs[0][:cut[0]], devs[1][:cut[1]]])
+            text_d = _ts(torch.cat([devs[0][:cut[0]], devs[1][:cut[1]]]))
             len1 = cut[0]
         else:
             text_d, len1 = devs[0][:cut[0]], None
@@ -408,8 +408,8 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
             if n1 and fa1 != fa2:
                 raise _lib.NativeError("paired files: one FASTA, one FASTQ")
             w = C.sizeof(FastqRec)
-            recs = torch.stack([r1.view(n1, w), r2[:n1 * w].view(n1, w)], 1).reshape(-1) \
-                if n1 else r1
+            recs = _ts(torch.stack([r1.view(n1, w), r2[:n1 * w].view(n1, w)], 1).reshape(-1)
+                       if n1 else r1)
             del r1, r2
             pair = rs1.astype(np.uint64) + rs2[:n1].astype(np.uint64)
             if n1 and int(pair.max()) >= 2 ** 32:
@@ -450,6 +450,17 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
 # split, fqzcomp5.c:423-623; dispatch :3051-3120.
 # ---------------------------------------------------------------------------
 H2D = [0]          # input text bytes this process uploaded (tests, bench)
+
+
+def _ts(t):
+    """`t`, made by a torch op on torch's current stream, complete before the
+    library reads it on its own stream (the ordering contract of the
+    device-pointer entry points, include/fqz5_mi355x.h): a paired window's
+    concatenated text was read before its copy had landed, now and then."""
+    import torch
+    if t is not None and t.is_cuda:
+        torch.cuda.current_stream(t.device).synchronize()
+    return t
 
 
 def _upload(buf, device: str):
@@ -556,7 +567,7 @@ def _scan(f: _PosFile, P: int, Wn: int, device: str, group, fasta=None) -> _Scan
         end = nxt[0] if nxt else _record_end(f, int(starts[-1]), fasta)
         text = t[int(starts[0]) - (lo - 1):]
         if end > hi:
-            text = torch.cat([text, _upload(f.read(hi, end), device)])
+            text = _ts(torch.cat([text, _upload(f.read(hi, end), device)]))
         else:
             text = text[:end - int(starts[0])]
         sc.hi = end
@@ -603,7 +614,7 @@ def _need_text(f: _PosFile, sc: _Scan, ranges, device: str):
             pieces.append(_upload(f.read(a, e), device))
     if not pieces:
         return torch.empty(0, dtype=torch.uint8, device=device)
-    return torch.cat(pieces) if len(pieces) > 1 else pieces[0]
+    return _ts(torch.cat(pieces)) if len(pieces) > 1 else pieces[0]
 
 
 def _merge(ranges):
@@ -663,13 +674,13 @@ class _RankWindow:
             text_d = texts[0]
             recs, _, nrec, _ = _index_text(text_d, 0, lens[0])
         else:
-            text_d = torch.cat(texts) if lens[1] else texts[0]
+            text_d = _ts(torch.cat(texts)) if lens[1] else texts[0]
             r1, _, n1, _ = _index_text(text_d, 0, lens[0])
             r2, _, n2, _ = _index_text(text_d, lens[0], lens[1])
             if n1 != n2:
                 raise _lib.NativeError("window gather: R1 and R2 record counts differ")
             w = C.sizeof(FastqRec)
-            recs = torch.stack([r1.view(n1, w), r2.view(n2, w)], 1).reshape(-1) if n1 else r1
+            recs = _ts(torch.stack([r1.view(n1, w), r2.view(n2, w)], 1).reshape(-1)) if n1 else r1
             nrec = 2 * n1
         if nrec != int(loc[-1]):
             raise _lib.NativeError("window gather: record count differs from the scan")
@@ -941,13 +952,19 @@ def compress_file(src: str, dst: str, level: int = 3, blk_size: int | None = Non
     _barrier(group)
     sink = _Sink(dst, False)
     srcs = [_Src(src)] + ([_Src(src2)] if src2 else [])
+    ok = False
     try:
-        return _encode_stream(srcs, sink, level, blk_size, device, group, window_bytes)
+        n = _encode_stream(srcs, sink, level, blk_size, device, group, window_bytes)
+        ok = True
+        return n
     finally:
         sink.close()
         for s in srcs:
             s.close()
-        _barrier(group)
+        # (not after an error: the other ranks may be inside a collective,
+        # and a barrier here would pair with it and hide the error)
+        if ok:
+            _barrier(group)
 
 
 def _blocks_of(data):
@@ -1128,7 +1145,7 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges
         idx1.append((at, at + k))
         idx2.append((at + k, at + n))
         at += n
-    cat = lambda rs: torch.cat([text[a:b] for a, b in rs]) if rs else text[:0]
+    cat = lambda rs: _ts(torch.cat([text[a:b] for a, b in rs])) if rs else text[:0]
     return cat(idx1), cat(idx2)
 
 

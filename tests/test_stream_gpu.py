@@ -66,8 +66,10 @@ def test_windows_paired_equal_cli(tmp_path):
 
 
 def _rank(rank, world, port, args, q):
+    import faulthandler
     import torch
     import torch.distributed as dist
+    faulthandler.dump_traceback_later(120, exit=False)   # a hung rank shows where
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.init()
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -91,10 +93,18 @@ def _run_ranks(ps, q, wait=150):
     silence limit) fails the test, and every rank still alive at the end is
     killed, so no rank outlives its test (a lingering rank held the next
     test's rendezvous once)."""
+    import queue
     for p in ps:
         p.start()
+    out = []
     try:
-        return [q.get(timeout=wait) for _ in ps]
+        for _ in ps:
+            try:
+                out.append(q.get(timeout=wait))
+            except queue.Empty:
+                raise AssertionError(f"a rank did not answer within {wait} s; "
+                                     f"the others answered {out}") from None
+        return out
     finally:
         for p in ps:
             p.join(timeout=30)
@@ -153,8 +163,10 @@ def test_two_ranks_paired_small_windows(tmp_path):
 
 
 def _rank_pairs(rank, world, port, args, q):
+    import faulthandler
     import torch
     import torch.distributed as dist
+    faulthandler.dump_traceback_later(120, exit=False)   # a hung rank shows where
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.init()
     dist.init_process_group("gloo", rank=rank, world_size=world)
