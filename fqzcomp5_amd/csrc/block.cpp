@@ -124,6 +124,7 @@ struct TrySession {
     std::vector<SeqEncReq> seq;                   // sequence CM candidates
     std::vector<uint64_t> seq_lb;                 // pruned candidates: size lower bound (else 0)
     std::vector<uint64_t> fqz_ub, seq_ub;         // pruned candidates: size upper bound
+    std::vector<char> fqz_skip, seq_skip;         // range chain skipped: no bytes yet
     std::vector<std::vector<int>> seq_of;
     std::vector<uint32_t> upper;                  // the sizes matrix with upper bounds
     std::deque<std::vector<uint32_t>> recs;       // their (rewritable) lengths / flags
@@ -606,6 +607,8 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             }
             tf.join();
             if (ferr) std::rethrow_exception(ferr);
+            t_sess.fqz_skip.insert(t_sess.fqz_skip.end(), skip_f.begin(), skip_f.end());
+            t_sess.seq_skip.insert(t_sess.seq_skip.end(), skip_s.begin(), skip_s.end());
             for (size_t k = 0; k < fq.size(); k++) {
                 t_sess.fqz_lb.push_back(skip_f[k] ? fqz_size_lower_bound(fq[k]) : 0);
                 t_sess.fqz_ub.push_back(skip_f[k] ? fqz_size_upper_bound(fq[k]) : 0);
@@ -628,6 +631,8 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             t_sess.seq_lb.assign(sq.size(), 0);
             t_sess.fqz_ub.assign(fq.size(), 0);
             t_sess.seq_ub.assign(sq.size(), 0);
+            t_sess.fqz_skip.assign(fq.size(), 0);
+            t_sess.seq_skip.assign(sq.size(), 0);
             g_fqz_tried += fq.size() + sq.size();
         }
         t_sess.open = true;
@@ -738,11 +743,11 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         // method the session did not try
         auto coded_fqz = [&](int i, int m) {
             const int f = t_sess.fqz_of[i][m];
-            return f >= 0 && !(size_t(f) < t_sess.fqz_lb.size() && t_sess.fqz_lb[size_t(f)] > 0);
+            return f >= 0 && !(size_t(f) < t_sess.fqz_skip.size() && t_sess.fqz_skip[size_t(f)]);
         };
         auto coded_seq = [&](int i, int m) {
             const int q = t_sess.seq_of[i][m];
-            return q >= 0 && !(size_t(q) < t_sess.seq_lb.size() && t_sess.seq_lb[size_t(q)] > 0);
+            return q >= 0 && !(size_t(q) < t_sess.seq_skip.size() && t_sess.seq_skip[size_t(q)]);
         };
         for (int i = 0; i < nsec; i++) {
             const int m = methods[i];

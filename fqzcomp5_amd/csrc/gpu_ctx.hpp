@@ -50,10 +50,11 @@ class ChunkPool {
             auto it = idle_.lower_bound(need);
             if (it != idle_.end()) {
                 void *b = it->second;
-                *got = it->first;
-                idle_bytes_ -= it->first;
+                const size_t sz = it->first;
                 idle_.erase(it);
-                use(it->first);
+                *got = sz;
+                idle_bytes_ -= sz;
+                use(sz);
                 return b;
             }
         }
@@ -71,13 +72,15 @@ class ChunkPool {
         return b;
     }
     void give(void *b, size_t sz) {
+        bool over;
         {
             std::lock_guard<std::mutex> lk(m_);
             idle_.emplace(sz, b);
             idle_bytes_ += sz;
             in_use_ -= sz;
+            over = idle_bytes_ > idle_cap();
         }
-        if (idle_bytes_ > idle_cap()) trim(idle_cap());
+        if (over) trim(idle_cap());
     }
     void drop(void *b, size_t sz) {
         (void)hipFree(b);

@@ -297,23 +297,29 @@ int seq_decode(const uint8_t *in, uint32_t in_size, const uint32_t *lens, int nr
         }
         return true;
     };
+    // a valid stream has at most one empty run in a row (the first, or one
+    // before a class switch): more means a damaged stream that would
+    // otherwise switch classes forever without output
+    int empty_runs = 0;
     for (uint32_t i = 0; i < n;) {
         uint32_t run = 0, r2;
         do {
             r2 = list_decode(run_m[state], rc);
             run += r2;
-        } while (r2 == 255);
-        if (i + run > n) run = n - i;
+        } while (r2 == 255 && run <= n - i);
+        if (run > n - i) run = n - i;
+        if (run == 0 && ++empty_runs > 2) return -1;
+        if (run) empty_runs = 0;
         if (state != 2) {
             const char *bases = state == 1 ? "acgt" : "ACGT";
             for (uint32_t j = 0; j < run; j++) {
                 uint8_t *F = cm + size_t(last) * 4;
                 const uint32_t tot = uint32_t(F[0]) + F[1] + F[2] + F[3];
                 const uint32_t t = rc.target(tot);
+                if (t >= tot) return -1;                 // a damaged stream
                 uint32_t acc = 0;
                 int b = 0;
-                while (acc + F[b] <= t) acc += F[b++];   // (b < 4 for every valid stream)
-                if (b > 3) return -1;
+                while (acc + F[b] <= t) acc += F[b++];   // b < 4: t < tot
                 rc.take(acc, F[b]);
                 small_update(F, 4, tot, b);
                 last = ((last << 2) + uint32_t(b)) & mask;

@@ -119,3 +119,26 @@ def test_seq_host_random_vs_oracle():
         meth, k, both = METHODS[t % len(METHODS)]
         c = o.encode(seq, lens, both, k)
         assert lib.seq_decode(c, lens, both, k, len(seq), host=True) == seq, (t, meth)
+
+
+def test_seq_host_damaged():
+    """Cut and byte-flipped SEQ streams: the host decoder returns an error or
+    some bytes, and never reads past its k-mer model table (host_dec.cpp's
+    symbol search is bounded by the model total)."""
+    o = binding.seq_oracle()
+    rng = np.random.default_rng(23)
+    alpha = np.frombuffer(b"ACGTACGTACGTacgtNN", np.uint8)
+    for t in range(24):
+        nrec = int(rng.integers(1, 60))
+        lens = [int(x) for x in rng.integers(1, 300, nrec)]
+        seq = rng.choice(alpha, sum(lens)).tobytes()
+        meth, k, both = METHODS[t % len(METHODS)]
+        c = o.encode(seq, lens, both, k)
+        bad = bytearray(c)
+        for j in rng.integers(4, len(c), 1 + t % 5):
+            bad[int(j)] ^= int(rng.integers(1, 256))
+        for stream in (bytes(bad), c[:len(c) // 2], c[:7]):
+            try:
+                lib.seq_decode(stream, lens, both, k, len(seq), host=True)
+            except RuntimeError:
+                pass
