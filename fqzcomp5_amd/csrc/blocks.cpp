@@ -119,36 +119,52 @@ int fqz5_blocks_assemble(const fqz5_block_parts *parts, int n, uint8_t *d_out,
 
 int fqz5_block_parse(const uint8_t *d_block, uint64_t avail, fqz5_block_view *v,
                      uint32_t *lens, uint32_t lens_cap) {
+    return fqz5_block_parse_v(d_block, avail, FQZ5_V11, v, lens, lens_cap);
+}
+
+int fqz5_block_parse_v(const uint8_t *d_block, uint64_t avail, int version,
+                       fqz5_block_view *v, uint32_t *lens, uint32_t lens_cap) {
     GpuCtx *gp = nullptr;
     try {
+        if (version < FQZ5_V11 || version > FQZ5_VOLD)
+            throw GpuError("fqz5_block_parse: unknown container version");
         GpuCtx &g = gpu();
         gp = &g;
         std::memset(v, 0, sizeof *v);
+        // the name section's offset: after [size][nrec][crc] (v1.1), or
+        // after [size][nrec] (v1.0 and the headerless format have no CRC
+        // field, fqzcomp5.c:2300-2318)
+        const uint64_t hd = version == FQZ5_V11 ? 12 : 8;
         auto get = [&](uint64_t at, uint64_t n, uint8_t *dst) {   // GET (:2282-2288)
             if (at + n > avail) throw GpuError("fqz5_block_parse: block truncated");
             g.download(dst, d_block + at, n);
             g.sync();
         };
         uint8_t h[21];
-        get(0, 21, h);
+        get(0, hd + 9, h);
         std::memcpy(&v->block_size, h, 4);
         std::memcpy(&v->nrec, h + 4, 4);
-        uint32_t crc_stored, c_len;
-        std::memcpy(&crc_stored, h + 8, 4);
-        if (uint64_t(v->block_size) + 4 > avail || v->block_size < 8)
+        uint32_t c_len;
+        if (uint64_t(v->block_size) + 4 > avail || v->block_size < hd - 4)
             throw GpuError("fqz5_block_parse: block size past the data");
         const uint64_t end = uint64_t(v->block_size) + 4;
-        uint32_t *d_crc = g.arena.alloc_n<uint32_t>(1);
-        crc32_dev(g, 0, d_block + 12, v->block_size - 8, d_crc);   // (:2309-2317)
-        uint32_t crc = 0;
-        g.download(&crc, d_crc, 1);
-        g.sync();
-        v->crc_ok = crc == crc_stored;
-        std::memcpy(&v->name_ulen, h + 12, 4);
-        std::memcpy(&c_len, h + 17, 4);
-        v->name_off = 12;
+        if (version == FQZ5_V11) {
+            uint32_t crc_stored;
+            std::memcpy(&crc_stored, h + 8, 4);
+            uint32_t *d_crc = g.arena.alloc_n<uint32_t>(1);
+            crc32_dev(g, 0, d_block + 12, v->block_size - 8, d_crc);   // (:2309-2317)
+            uint32_t crc = 0;
+            g.download(&crc, d_crc, 1);
+            g.sync();
+            v->crc_ok = crc == crc_stored;
+        } else {
+            v->crc_ok = 1;                             // (no check, :2306)
+        }
+        std::memcpy(&v->name_ulen, h + hd, 4);
+        std::memcpy(&c_len, h + hd + 5, 4);
+        v->name_off = uint32_t(hd);
         v->name_size = 9 + c_len;
-        uint64_t o = 12ull + 9 + c_len;
+        uint64_t o = hd + 9 + c_len;
         uint8_t lh[6];
         uint64_t lens_sum = 0;
         get(o, 1, lh);

@@ -967,30 +967,61 @@ def compress_file(src: str, dst: str, level: int = 3, blk_size: int | None = Non
             _barrier(group)
 
 
-def _blocks_of(data):
-    """Block byte ranges of a .fqz5 (walking block_size fields up to the
-    index, fqzcomp5.c:3754-3772); a block that runs past the data or the
-    index is an error (the reference's read fails there)."""
-    data = memoryview(data).cast("B")
-    if len(data) < 16 or bytes(data[:8]) != MAGIC:
-        raise ValueError("not an FQZ5 v1.1 file")
-    (idx,) = struct.unpack_from("<Q", data, 8)
-    if idx > len(data) or (idx and idx < 16):
-        raise ValueError("truncated .fqz5: index offset past the end of the file")
-    end = idx if idx else len(data)
-    p, out = 16, []
+V11, V10, VOLD = 0, 1, 2                        # read_header's results (fqzcomp5.c:2577)
+MAGIC_V10 = b"FQZ5\x01\x00\x00\x00"             # :155
+
+
+class Blocks(list):
+    """Block byte ranges of a container, with its version: V11 (CRC field in
+    every block), V10 or VOLD (none; VOLD files have no file header either)."""
+    version = V11
+
+    def __init__(self, ranges=(), version: int = V11):
+        super().__init__(ranges)
+        self.version = version
+
+
+def _version_of(head: bytes, size: int):
+    """read_header (fqzcomp5.c:2578-2603): (version, first block offset,
+    index offset or 0).  A file with neither magic is the old headerless
+    format: blocks from offset 0 to the end, no index."""
+    if len(head) >= 8 and head[:8] in (MAGIC, MAGIC_V10):
+        if len(head) < 16:
+            raise ValueError("truncated .fqz5: no index offset after the magic")
+        (idx,) = struct.unpack_from("<Q", head, 8)
+        if idx > size or (idx and idx < 16):
+            raise ValueError("truncated .fqz5: index offset past the end of the file")
+        return (V11 if head[:8] == MAGIC else V10), 16, idx
+    return VOLD, 0, 0
+
+
+def _walk(read4, start: int, end: int, version: int) -> Blocks:
+    """The block_size walk of decode (fqzcomp5.c:3769-3797) from `start` up
+    to `end` (the index or the end of the file); a block that runs past it is
+    an error (the reference's read fails there)."""
+    hd = 12 if version == V11 else 8
+    p, out = start, Blocks(version=version)
     while p < end:
-        if p + 4 > end:
+        h = read4(p) if p + 4 <= end else b""
+        if len(h) < 4:
             raise ValueError("truncated .fqz5: a block header runs past the end")
-        (bsz,) = struct.unpack_from("<I", data, p)
-        if p + 4 + bsz > end or bsz < 8:
+        (bsz,) = struct.unpack("<I", h)
+        if p + 4 + bsz > end or bsz + 4 < hd:
             raise ValueError("truncated .fqz5: a block runs past the end of the file")
         out.append((p, p + 4 + bsz))
         p += 4 + bsz
     return out
 
 
-def block_fields(data, s: int, e: int) -> dict:
+def _blocks_of(data) -> Blocks:
+    """Block byte ranges of a .fqz5 held in memory (any version the
+    reference reads)."""
+    data = memoryview(data).cast("B")
+    version, start, idx = _version_of(bytes(data[:16]), len(data))
+    return _walk(lambda p: bytes(data[p:p + 4]), start, idx if idx else len(data), version)
+
+
+def block_fields(data, s: int, e: int, version: int = V11) -> dict:
     """The header fields of the block data[s:e] read on the host, as
     decode_block reads them (fqzcomp5.c:2290-2420): record count, the name,
     sequence and quality sections' sizes, the lengths section.  Raises
@@ -1004,7 +1035,9 @@ def block_fields(data, s: int, e: int) -> dict:
             raise ValueError("corrupt block: header runs past the block")
         return struct.unpack_from(fmt, d, at), at + z
 
-    (bsz, nrec, _crc), p = get("<III", s)
+    (bsz, nrec), p = get("<II", s)
+    if version == V11:
+        _crc, p = get("<I", p)
     if s + 4 + bsz != e:
         raise ValueError("corrupt block: block size field")
     (nu, _st, nc), p = get("<IBI", p)
@@ -1054,7 +1087,8 @@ def check_blocks(data, ranges=None) -> list[dict]:
     """block_fields of every block (host only)."""
     if ranges is None:
         ranges = _blocks_of(data)
-    return [block_fields(data, s, e) for s, e in ranges]
+    v = getattr(ranges, "version", V11)
+    return [block_fields(data, s, e, v) for s, e in ranges]
 
 
 def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges=None):
@@ -1067,6 +1101,7 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges
     so = _load()
     if ranges is None:
         ranges = _blocks_of(data)
+    version = getattr(ranges, "version", V11)
     if not ranges:
         return torch.empty(0, dtype=torch.uint8, device=device)
     try:
@@ -1078,8 +1113,9 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges
         v = S.BlockView()
         (nrec,) = struct.unpack_from("<I", data, s + 4)
         ln = np.zeros(max(nrec, 1), np.uint32)
-        _check(S._load_blk().fqz5_block_parse(buf.data_ptr() + s, e - s, C.byref(v),
-                                              ln.ctypes.data_as(C.POINTER(C.c_uint32)), len(ln)),
+        _check(S._load_blk().fqz5_block_parse_v(buf.data_ptr() + s, e - s, version, C.byref(v),
+                                                ln.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                len(ln)),
                "fqz5_block_parse")
         if not v.crc_ok:
             raise _lib.NativeError("block CRC mismatch")
@@ -1170,46 +1206,34 @@ def decompress_paired_bytes(data: bytes, plus_name: bool = False,
     return t1.cpu().numpy().tobytes(), t2.cpu().numpy().tobytes()
 
 
-def _file_blocks(f, size: int):
-    """Block byte ranges of a .fqz5 file: from the index when the header
-    names one (write_index, fqzcomp5.c:2606), else by walking the block
-    size fields; checked against the file size."""
+def _file_blocks(f, size: int) -> Blocks:
+    """Block byte ranges of a .fqz5 file (any version the reference reads),
+    walking the block size fields up to the index; checked against the file
+    size."""
     f.seek(0)
-    head = f.read(16)
-    if len(head) < 16 or head[:8] != MAGIC:
-        raise ValueError("not an FQZ5 v1.1 file")
-    (idx,) = struct.unpack_from("<Q", head, 8)
-    if idx > size or (idx and idx < 16):
-        raise ValueError("truncated .fqz5: index offset past the end of the file")
-    end = idx if idx else size
-    out, p = [], 16
-    while p < end:
+    version, start, idx = _version_of(f.read(16), size)
+
+    def read4(p):
         f.seek(p)
-        h = f.read(4)
-        if len(h) < 4:
-            raise ValueError("truncated .fqz5: a block header runs past the end")
-        (bsz,) = struct.unpack("<I", h)
-        if p + 4 + bsz > end or bsz < 8:
-            raise ValueError("truncated .fqz5: a block runs past the end of the file")
-        out.append((p, p + 4 + bsz))
-        p += 4 + bsz
-    return out
+        return f.read(4)
+    return _walk(read4, start, idx if idx else size, version)
 
 
-def _block_text_size(f, s: int, e: int, plus_name: bool) -> int:
+def _block_text_size(f, s: int, e: int, plus_name: bool, version: int = V11) -> int:
     """The FASTQ (or FASTA) text size of block [s, e) of an open .fqz5, from
     its headers alone (a few small reads): output_fastq writes '@' name '\n'
     seq '\n' '+' [name] '\n' qual '\n' per record (fqzcomp5.c:3441-3480),
     output_fasta '>' name '\n' seq '\n' (:3503-3517); the name section
     decodes to each name and a '\0'."""
+    hd = 12 if version == V11 else 8
     f.seek(s)
-    h = f.read(21)
-    if len(h) < 21:
+    h = f.read(hd + 9)
+    if len(h) < hd + 9:
         raise ValueError("truncated .fqz5: a block header runs past the end")
     nrec, = struct.unpack_from("<I", h, 4)
-    name_ulen, = struct.unpack_from("<I", h, 12)
-    c_len, = struct.unpack_from("<I", h, 17)
-    p = s + 21 + c_len
+    name_ulen, = struct.unpack_from("<I", h, hd)
+    c_len, = struct.unpack_from("<I", h, hd + 5)
+    p = s + hd + 9 + c_len
     f.seek(p)
     nb = f.read(1)
     if not nb:
@@ -1293,7 +1317,7 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
         else:
             # one output: every block's text size from its headers, so this
             # rank's text starts at the sum over the blocks before its first
-            sizes = [_block_text_size(f, s, e, plus_name) for s, e in ranges]
+            sizes = [_block_text_size(f, s, e, plus_name, ranges.version) for s, e in ranges]
             at = sum(sizes[:mine[0]]) if mine else 0
             if rk == 0:
                 _Sink(dst, True).close()
@@ -1315,7 +1339,8 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
                 hv = host.numpy()
                 buf = host.to(device)      # blocking: block parsing runs on the library's streams
                 texts = _decode(hv, buf, plus_name, device, pairs=dst2 is not None,
-                                ranges=[(ranges[b][0] - a, ranges[b][1] - a) for b in gb])
+                                ranges=Blocks([(ranges[b][0] - a, ranges[b][1] - a) for b in gb],
+                                              ranges.version))
                 if dst2 is None:
                     texts = (texts,)
                 for j, t in enumerate(texts):

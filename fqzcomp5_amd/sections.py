@@ -928,6 +928,9 @@ def _load_blk():
         so.fqz5_block_parse.restype = C.c_int
         so.fqz5_block_parse.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(BlockView),
                                         C.POINTER(C.c_uint32), C.c_uint32]
+        so.fqz5_block_parse_v.restype = C.c_int
+        so.fqz5_block_parse_v.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.POINTER(BlockView),
+                                          C.POINTER(C.c_uint32), C.c_uint32]
         _bound_blk = True
     return so
 

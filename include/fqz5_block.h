@@ -198,6 +198,17 @@ typedef struct {                  /* one block read back (decode_block) */
 int fqz5_block_parse(const uint8_t *d_block, uint64_t avail, fqz5_block_view *v,
                      uint32_t *lens, uint32_t lens_cap);
 
+/* The same for a block of any container version the reference decodes
+ * (read_header, fqzcomp5.c:2576-2602; decode_block :2290-2318):
+ * FQZ5_V11 `FQZ5\1\1\0\0` blocks carry [u32 size][u32 nrec][u32 crc32];
+ * FQZ5_V10 `FQZ5\1\0\0\0` and FQZ5_VOLD (no file header) blocks have no CRC
+ * field ([u32 size][u32 nrec], the name section at offset 8) and report
+ * crc_ok = 1, as the reference skips the check for them.
+ * fqz5_block_parse(...) is fqz5_block_parse_v(..., FQZ5_V11, ...). */
+enum { FQZ5_V11 = 0, FQZ5_V10 = 1, FQZ5_VOLD = 2 };
+int fqz5_block_parse_v(const uint8_t *d_block, uint64_t avail, int version,
+                       fqz5_block_view *v, uint32_t *lens, uint32_t lens_cap);
+
 #ifdef __cplusplus
 }
 #endif

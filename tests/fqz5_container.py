@@ -88,3 +88,37 @@ def read(path):
         blocks.append(Block(nrec, crc_ok, names, fixed, seq, qual))
         p = bend
     return blocks
+
+
+MAGIC_V10 = b"FQZ5\x01\x00\x00\x00"     # fqzcomp5.c:155
+
+
+def downgrade(buf: bytes, version: str) -> bytes:
+    """A v1.1 container rewritten in an older layout the reference still
+    decodes (read_header, fqzcomp5.c:2578-2603; decode_block :2300-2318):
+    "v1.0": magic FQZ5\\1\\0\\0\\0, no CRC field in the blocks (block_size 4
+    smaller), the index offsets moved to match; "old": no file header, no CRC
+    fields and no index (the decoder reads blocks up to the end)."""
+    assert buf[:8] == MAGIC and version in ("v1.0", "old")
+    (idx,) = struct.unpack_from("<Q", buf, 8)
+    end = idx if idx else len(buf)
+    p, blocks = 16, []
+    while p < end:
+        (bsz,) = struct.unpack_from("<I", buf, p)
+        blk = buf[p:p + 4 + bsz]
+        blocks.append(struct.pack("<I", bsz - 4) + blk[4:8] + blk[12:])
+        p += 4 + bsz
+    if version == "old":
+        return b"".join(blocks)
+    out, offs, at = [], [], 16
+    for b in blocks:
+        offs.append(at)
+        at += len(b)
+    tail = b""
+    if idx:
+        (n,) = struct.unpack_from("<I", buf, idx + 8)
+        assert n == len(blocks)
+        ent = [struct.unpack_from("<QII", buf, idx + 12 + 16 * i) for i in range(n)]
+        tail = buf[idx:idx + 12] + b"".join(struct.pack("<QII", o, u, r)
+                                            for o, (_, u, r) in zip(offs, ent))
+    return MAGIC_V10 + struct.pack("<Q", at if idx else 0) + b"".join(blocks) + tail
