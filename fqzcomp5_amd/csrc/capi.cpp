@@ -143,8 +143,19 @@ int host_decode_mode() {
 // (fqz5_sections_try: LZP3, fqz and sequence-model candidates beside the
 // rANS candidates).
 static thread_local std::unique_ptr<GpuCtx> g_aux[AUX_CTXS];
+// fqz5_stream_wait's event, once recorded: a helper context created later
+// waits for it too (its streams then see the caller's producer work)
+static thread_local hipEvent_t g_wait_ev = nullptr;
+static thread_local bool g_wait_armed = false;
+static void ctx_wait(GpuCtx &c, hipEvent_t ev) {
+    FQZ5_HIP(hipStreamWaitEvent(c.stream, ev, 0));
+    FQZ5_HIP(hipStreamWaitEvent(c.stream2, ev, 0));
+}
 GpuCtx &gpu_aux(int k) {
-    if (!g_aux[k]) g_aux[k].reset(new GpuCtx(std::getenv("FQZ5_AUX_NORMAL_PRIO") == nullptr));
+    if (!g_aux[k]) {
+        g_aux[k].reset(new GpuCtx(std::getenv("FQZ5_AUX_NORMAL_PRIO") == nullptr));
+        if (g_wait_armed) ctx_wait(*g_aux[k], g_wait_ev);
+    }
     return *g_aux[k];
 }
 void gpu_aux_reset_all() {
@@ -390,13 +401,17 @@ int fqz5_rans_uncompress_batch(fqz5_rans_job *jobs, int n) {
 
 int fqz5_stream_wait(void *stream) {
     try {
+        // one event per thread, re-recorded: every stream of the calling
+        // thread's contexts (its own and the helper contexts the entry
+        // points hand work to) waits for the work enqueued on `stream` so
+        // far (device-side, no host sync)
         GpuCtx &g = gpu();
-        // one event per thread, re-recorded: the library stream waits for
-        // the work enqueued on `stream` so far (device-side, no host sync)
-        static thread_local hipEvent_t ev = nullptr;
-        if (!ev) FQZ5_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        FQZ5_HIP(hipEventRecord(ev, static_cast<hipStream_t>(stream)));
-        FQZ5_HIP(hipStreamWaitEvent(g.stream, ev, 0));
+        if (!g_wait_ev) FQZ5_HIP(hipEventCreateWithFlags(&g_wait_ev, hipEventDisableTiming));
+        FQZ5_HIP(hipEventRecord(g_wait_ev, static_cast<hipStream_t>(stream)));
+        ctx_wait(g, g_wait_ev);
+        for (auto &a : g_aux)
+            if (a) ctx_wait(*a, g_wait_ev);
+        g_wait_armed = true;
         return 0;
     } catch (const std::exception &e) {
         g_err = e.what();

@@ -92,6 +92,7 @@ def _index_text(text_d, at: int, n: int):
     recs = torch.empty(max_rec * C.sizeof(FastqRec), dtype=torch.uint8, device=text_d.device)
     rsz = np.zeros(max_rec, np.uint32)
     nrec = C.c_uint64(0)
+    _lib.after_torch()
     fasta = _check(so.fqz5_fastq_index(text_d.data_ptr() + at, n, recs.data_ptr(), max_rec,
                                        C.byref(nrec), rsz.ctypes.data), "fqz5_fastq_index") == 1
     nrec = int(nrec.value)
@@ -164,7 +165,7 @@ def parse_paired(text_d, len1: int, blk_size: int):
     if n1 and fa1 != fa2:
         raise _lib.NativeError("paired files: one FASTA, one FASTQ")
     w = C.sizeof(FastqRec)
-    recs = _ts(torch.stack([r1.view(n1, w), r2[:n1 * w].view(n1, w)], 1).reshape(-1)) if n1 else r1
+    recs = torch.stack([r1.view(n1, w), r2[:n1 * w].view(n1, w)], 1).reshape(-1) if n1 else r1
     del r1, r2
     pair = rs1.astype(np.uint64) + rs2[:n1].astype(np.uint64)
     if n1 and int(pair.max()) >= 2 ** 32:
@@ -309,19 +310,11 @@ class _Sink:
 
 
 def _allgather_obj(x, group):
-    import torch.distributed as dist
-    ws, _ = S._world(group)
-    if ws == 1:
-        return [x]
-    out = [None] * ws
-    dist.all_gather_object(out, x, group=group)
-    return out
+    return S.xchg(x, group)
 
 
 def _barrier(group):
-    import torch.distributed as dist
-    if S._world(group)[0] > 1:
-        dist.barrier(group=group)
+    S.barrier(group)
 
 
 def _complete_records(text_d, n: int, eof: bool) -> tuple[list[int], bool]:
@@ -392,7 +385,7 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
             continue
         cut = [e[k - 1] for e in ends]
         if paired:
-            text_d = _ts(torch.cat([devs[0][:cut[0]], devs[1][:cut[1]]]))
+            text_d = torch.cat([devs[0][:cut[0]], devs[1][:cut[1]]])
             len1 = cut[0]
         else:
             text_d, len1 = devs[0][:cut[0]], None
@@ -408,8 +401,8 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
             if n1 and fa1 != fa2:
                 raise _lib.NativeError("paired files: one FASTA, one FASTQ")
             w = C.sizeof(FastqRec)
-            recs = _ts(torch.stack([r1.view(n1, w), r2[:n1 * w].view(n1, w)], 1).reshape(-1)
-                       if n1 else r1)
+            recs = (torch.stack([r1.view(n1, w), r2[:n1 * w].view(n1, w)], 1).reshape(-1)
+                    if n1 else r1)
             del r1, r2
             pair = rs1.astype(np.uint64) + rs2[:n1].astype(np.uint64)
             if n1 and int(pair.max()) >= 2 ** 32:
@@ -450,17 +443,6 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
 # split, fqzcomp5.c:423-623; dispatch :3051-3120.
 # ---------------------------------------------------------------------------
 H2D = [0]          # input text bytes this process uploaded (tests, bench)
-
-
-def _ts(t):
-    """`t`, made by a torch op on torch's current stream, complete before the
-    library reads it on its own stream (the ordering contract of the
-    device-pointer entry points, include/fqz5_mi355x.h): a paired window's
-    concatenated text was read before its copy had landed, now and then."""
-    import torch
-    if t is not None and t.is_cuda:
-        torch.cuda.current_stream(t.device).synchronize()
-    return t
 
 
 def _upload(buf, device: str):
@@ -567,7 +549,7 @@ def _scan(f: _PosFile, P: int, Wn: int, device: str, group, fasta=None) -> _Scan
         end = nxt[0] if nxt else _record_end(f, int(starts[-1]), fasta)
         text = t[int(starts[0]) - (lo - 1):]
         if end > hi:
-            text = _ts(torch.cat([text, _upload(f.read(hi, end), device)]))
+            text = torch.cat([text, _upload(f.read(hi, end), device)])
         else:
             text = text[:end - int(starts[0])]
         sc.hi = end
@@ -614,7 +596,7 @@ def _need_text(f: _PosFile, sc: _Scan, ranges, device: str):
             pieces.append(_upload(f.read(a, e), device))
     if not pieces:
         return torch.empty(0, dtype=torch.uint8, device=device)
-    return _ts(torch.cat(pieces)) if len(pieces) > 1 else pieces[0]
+    return torch.cat(pieces) if len(pieces) > 1 else pieces[0]
 
 
 def _merge(ranges):
@@ -674,13 +656,13 @@ class _RankWindow:
             text_d = texts[0]
             recs, _, nrec, _ = _index_text(text_d, 0, lens[0])
         else:
-            text_d = _ts(torch.cat(texts)) if lens[1] else texts[0]
+            text_d = torch.cat(texts) if lens[1] else texts[0]
             r1, _, n1, _ = _index_text(text_d, 0, lens[0])
             r2, _, n2, _ = _index_text(text_d, lens[0], lens[1])
             if n1 != n2:
                 raise _lib.NativeError("window gather: R1 and R2 record counts differ")
             w = C.sizeof(FastqRec)
-            recs = _ts(torch.stack([r1.view(n1, w), r2.view(n2, w)], 1).reshape(-1)) if n1 else r1
+            recs = torch.stack([r1.view(n1, w), r2.view(n2, w)], 1).reshape(-1) if n1 else r1
             nrec = 2 * n1
         if nrec != int(loc[-1]):
             raise _lib.NativeError("window gather: record count differs from the scan")
@@ -753,6 +735,7 @@ class _LocalWindow:
         for b in range(nb):
             a, e = int(W.first[b]), int(W.first[b + 1])
             sz = (C.c_uint64 * 3)()
+            _lib.after_torch()
             _check(so.fqz5_fastq_gather(W.text_d.data_ptr(), W.recs.data_ptr(), a, e, None,
                                         None, None, None, None, sz), "fqz5_fastq_gather")
             self.name_bytes.append(int(sz[0]))
@@ -886,6 +869,7 @@ def _gather_ranges(text_d, recs, ranges, fasta: bool, pair_flags: bool):
     sizes = []
     for a, b in ranges:
         sz = (C.c_uint64 * 3)()
+        _lib.after_torch()
         _check(so.fqz5_fastq_gather(text_d.data_ptr(), recs.data_ptr(), a, b, None, None, None,
                                     None, None, sz), "fqz5_fastq_gather")
         sizes.append((int(sz[0]), int(sz[1])))
@@ -901,6 +885,7 @@ def _gather_ranges(text_d, recs, ranges, fasta: bool, pair_flags: bool):
         ln = np.zeros(max(b - a, 1), np.uint32)
         fl = np.zeros(max(b - a, 1), np.uint32)
         sz = (C.c_uint64 * 3)()
+        _lib.after_torch()
         _check(so.fqz5_fastq_gather(text_d.data_ptr(), recs.data_ptr(), a, b,
                                     name_d.data_ptr() + no, seq_d.data_ptr() + so_,
                                     None if fasta else qual_d.data_ptr() + so_, ln.ctypes.data,
@@ -947,24 +932,22 @@ def compress_file(src: str, dst: str, level: int = 3, blk_size: int | None = Non
     process per GPU, every rank calling with the same arguments; the file
     equals the single-process one byte for byte.  Returns the file size."""
     ws, rk = S._world(group)
-    if rk == 0:
-        _Sink(dst, True).close()              # create / truncate before anyone writes
-    _barrier(group)
-    sink = _Sink(dst, False)
-    srcs = [_Src(src)] + ([_Src(src2)] if src2 else [])
-    ok = False
-    try:
-        n = _encode_stream(srcs, sink, level, blk_size, device, group, window_bytes)
-        ok = True
+    # every rank fails together (S.ranks_fail_together): the body's last
+    # exchange is the final barrier, taken on every path
+    with S.ranks_fail_together(group):
+        if rk == 0:
+            _Sink(dst, True).close()              # create / truncate before anyone writes
+        _barrier(group)
+        sink = _Sink(dst, False)
+        srcs = [_Src(src)] + ([_Src(src2)] if src2 else [])
+        try:
+            n = _encode_stream(srcs, sink, level, blk_size, device, group, window_bytes)
+        finally:
+            sink.close()
+            for s in srcs:
+                s.close()
+        _barrier(group)
         return n
-    finally:
-        sink.close()
-        for s in srcs:
-            s.close()
-        # (not after an error: the other ranks may be inside a collective,
-        # and a barrier here would pair with it and hide the error)
-        if ok:
-            _barrier(group)
 
 
 V11, V10, VOLD = 0, 1, 2                        # read_header's results (fqzcomp5.c:2577)
@@ -1109,6 +1092,7 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges
     except ValueError as err:
         raise _lib.NativeError(str(err)) from None
     views, lens = [], []
+    _lib.after_torch()
     for s, e in ranges:
         v = S.BlockView()
         (nrec,) = struct.unpack_from("<I", data, s + 4)
@@ -1168,6 +1152,7 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges
         sizes.append(int(size.value))
         r1.append(int(s1.value))
     text = torch.empty(max(sum(sizes), 1), dtype=torch.uint8, device=device)
+    _lib.after_torch()
     at = 0
     for a, n in zip(args, sizes):
         size, s1 = C.c_uint64(0), C.c_uint64(0)
@@ -1181,7 +1166,7 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges
         idx1.append((at, at + k))
         idx2.append((at + k, at + n))
         at += n
-    cat = lambda rs: _ts(torch.cat([text[a:b] for a, b in rs])) if rs else text[:0]
+    cat = lambda rs: torch.cat([text[a:b] for a, b in rs]) if rs else text[:0]
     return cat(idx1), cat(idx2)
 
 
@@ -1284,111 +1269,112 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
     files needs its decoded names).  Returns the text bytes written."""
     import os
     ws, rk = S._world(group)
-    outs = [dst] + ([dst2] if dst2 is not None else [])
-    if ws > 1 and any(d.endswith(".gz") for d in outs):
-        raise ValueError("gzip output needs a single process")
-    size = os.path.getsize(src)
-    single = ws == 1
-    spill = not single and dst2 is not None
-    with open(src, "rb") as f:
-        ranges = _file_blocks(f, size)
-        nb = len(ranges)
-        mine = [b for b in range(nb) if (b * ws) // max(nb, 1) == rk] if nb else []
-        wb = window_bytes or DEFAULT_WINDOW
-        groups, cur, tot = [], [], 0
-        for b in mine:
-            z = ranges[b][1] - ranges[b][0]
-            if cur and tot + z > wb:
+    with S.ranks_fail_together(group):
+        outs = [dst] + ([dst2] if dst2 is not None else [])
+        if ws > 1 and any(d.endswith(".gz") for d in outs):
+            raise ValueError("gzip output needs a single process")
+        size = os.path.getsize(src)
+        single = ws == 1
+        spill = not single and dst2 is not None
+        with open(src, "rb") as f:
+            ranges = _file_blocks(f, size)
+            nb = len(ranges)
+            mine = [b for b in range(nb) if (b * ws) // max(nb, 1) == rk] if nb else []
+            wb = window_bytes or DEFAULT_WINDOW
+            groups, cur, tot = [], [], 0
+            for b in mine:
+                z = ranges[b][1] - ranges[b][0]
+                if cur and tot + z > wb:
+                    groups.append(cur)
+                    cur, tot = [], 0
+                cur.append(b)
+                tot += z
+            if cur:
                 groups.append(cur)
-                cur, tot = [], 0
-            cur.append(b)
-            tot += z
-        if cur:
-            groups.append(cur)
-        gz = [d.endswith(".gz") for d in outs]
-        streams, sinks, at = [], [], 0
-        if single:
-            import gzip
-            streams = [gzip.GzipFile(filename="", mode="wb", compresslevel=6, mtime=0,
-                                     fileobj=open(d, "wb")) if z else open(d, "wb")
-                       for d, z in zip(outs, gz)]
-        elif spill:
-            streams = [open(f"{d}.part{rk}", "wb") for d in outs]
-        else:
-            # one output: every block's text size from its headers, so this
-            # rank's text starts at the sum over the blocks before its first
-            sizes = [_block_text_size(f, s, e, plus_name, ranges.version) for s, e in ranges]
-            at = sum(sizes[:mine[0]]) if mine else 0
-            if rk == 0:
-                _Sink(dst, True).close()
-            _barrier(group)
-            sinks = [_Sink(dst, False)]
-        written = [0 for _ in outs]
-        try:
-            for gb in groups:
-                a, e = ranges[gb[0]][0], ranges[gb[-1]][1]
-                host = _pinned(e - a)
-                f.seek(a)
-                mv = memoryview(host.numpy())
-                got = 0
-                while got < e - a:
-                    k = f.readinto(mv[got:])
-                    if not k:
-                        raise OSError(f"{src}: short read")
-                    got += k
-                hv = host.numpy()
-                buf = host.to(device)      # blocking: block parsing runs on the library's streams
-                texts = _decode(hv, buf, plus_name, device, pairs=dst2 is not None,
-                                ranges=Blocks([(ranges[b][0] - a, ranges[b][1] - a) for b in gb],
-                                              ranges.version))
-                if dst2 is None:
-                    texts = (texts,)
-                for j, t in enumerate(texts):
-                    out = _pinned(int(t.numel()))
-                    out.copy_(t)
-                    if sinks:
-                        want = sum(sizes[b] for b in gb)
-                        if int(t.numel()) != want:
-                            raise _lib.NativeError("decoded text size differs from the block headers'")
-                        sinks[j].write_at(at + written[j], out.numpy())
-                    else:
-                        streams[j].write(memoryview(out.numpy()))
-                    written[j] += int(t.numel())
-                    del out
-                del buf, host, texts
-        finally:
-            for st in streams:
-                if isinstance(st, __import__("gzip").GzipFile):
-                    raw = st.fileobj          # (close() drops the reference)
-                    st.close()
-                    raw.close()
-                else:
-                    st.close()
-            for sk in sinks:
-                sk.close()
-    if single:
-        return sum(written)
-    all_w = _allgather_obj(written, group)
-    if spill:
-        # the spill files into place at their offsets from the ranks' sizes
-        for j, d in enumerate(outs):
-            if rk == 0:
-                _Sink(d, True).close()
-        _barrier(group)
-        for j, d in enumerate(outs):
-            off = sum(w[j] for w in all_w[:rk])
-            sink = _Sink(d, False)
-            part = f"{d}.part{rk}"
+            gz = [d.endswith(".gz") for d in outs]
+            streams, sinks, at = [], [], 0
+            if single:
+                import gzip
+                streams = [gzip.GzipFile(filename="", mode="wb", compresslevel=6, mtime=0,
+                                         fileobj=open(d, "wb")) if z else open(d, "wb")
+                           for d, z in zip(outs, gz)]
+            elif spill:
+                streams = [open(f"{d}.part{rk}", "wb") for d in outs]
+            else:
+                # one output: every block's text size from its headers, so this
+                # rank's text starts at the sum over the blocks before its first
+                sizes = [_block_text_size(f, s, e, plus_name, ranges.version) for s, e in ranges]
+                at = sum(sizes[:mine[0]]) if mine else 0
+                if rk == 0:
+                    _Sink(dst, True).close()
+                _barrier(group)
+                sinks = [_Sink(dst, False)]
+            written = [0 for _ in outs]
             try:
-                with open(part, "rb") as pf:
-                    for c in iter(lambda: pf.read(1 << 26), b""):
-                        sink.write_at(off, c)
-                        off += len(c)
+                for gb in groups:
+                    a, e = ranges[gb[0]][0], ranges[gb[-1]][1]
+                    host = _pinned(e - a)
+                    f.seek(a)
+                    mv = memoryview(host.numpy())
+                    got = 0
+                    while got < e - a:
+                        k = f.readinto(mv[got:])
+                        if not k:
+                            raise OSError(f"{src}: short read")
+                        got += k
+                    hv = host.numpy()
+                    buf = host.to(device)      # blocking: block parsing runs on the library's streams
+                    texts = _decode(hv, buf, plus_name, device, pairs=dst2 is not None,
+                                    ranges=Blocks([(ranges[b][0] - a, ranges[b][1] - a) for b in gb],
+                                                  ranges.version))
+                    if dst2 is None:
+                        texts = (texts,)
+                    for j, t in enumerate(texts):
+                        out = _pinned(int(t.numel()))
+                        out.copy_(t)
+                        if sinks:
+                            want = sum(sizes[b] for b in gb)
+                            if int(t.numel()) != want:
+                                raise _lib.NativeError("decoded text size differs from the block headers'")
+                            sinks[j].write_at(at + written[j], out.numpy())
+                        else:
+                            streams[j].write(memoryview(out.numpy()))
+                        written[j] += int(t.numel())
+                        del out
+                    del buf, host, texts
             finally:
-                sink.close()
-                os.unlink(part)
-    _barrier(group)
-    return sum(sum(w) for w in all_w)
+                for st in streams:
+                    if isinstance(st, __import__("gzip").GzipFile):
+                        raw = st.fileobj          # (close() drops the reference)
+                        st.close()
+                        raw.close()
+                    else:
+                        st.close()
+                for sk in sinks:
+                    sk.close()
+        if single:
+            return sum(written)
+        all_w = _allgather_obj(written, group)
+        if spill:
+            # the spill files into place at their offsets from the ranks' sizes
+            for j, d in enumerate(outs):
+                if rk == 0:
+                    _Sink(d, True).close()
+            _barrier(group)
+            for j, d in enumerate(outs):
+                off = sum(w[j] for w in all_w[:rk])
+                sink = _Sink(d, False)
+                part = f"{d}.part{rk}"
+                try:
+                    with open(part, "rb") as pf:
+                        for c in iter(lambda: pf.read(1 << 26), b""):
+                            sink.write_at(off, c)
+                            off += len(c)
+                finally:
+                    sink.close()
+                    os.unlink(part)
+        _barrier(group)
+        return sum(sum(w) for w in all_w)
 
 
 def _write_out(path: str, data) -> None:

@@ -411,6 +411,20 @@ def stream_wait(stream: int) -> None:
         raise NativeError("fqz5_stream_wait failed: " + last_error())
 
 
+def after_torch() -> None:
+    """The ordering contract of the device-pointer calls for buffers torch
+    made: the calling thread's library streams (and its helper contexts')
+    wait, device-side, for the work enqueued so far on torch's current
+    stream (a torch.cat output, a buffer the caching allocator reused).
+    Called before every device-pointer entry point of sections / fqz5file;
+    a no-op while torch has not initialised the GPU."""
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is None or not torch.cuda.is_initialized():
+        return
+    stream_wait(torch.cuda.current_stream().cuda_stream)
+
+
 def crc32_dev(ptr: int, n: int, crc: int = 0) -> int:
     """crc32 of n device bytes at ptr (fqz5_crc32_dev)."""
     out = C.c_uint32(0)

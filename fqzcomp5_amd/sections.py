@@ -200,6 +200,7 @@ def sections_try(secs: list[Section], masks: np.ndarray) -> np.ndarray:
     sizes = np.zeros(len(secs) * M_LAST, np.uint32)
     av = np.ascontiguousarray(masks, np.uint32)
     assert len(av) == len(secs)
+    _lib.after_torch()
     rc = so.fqz5_sections_try(_arr(Section, secs), len(secs),
                               av.ctypes.data_as(C.POINTER(C.c_uint32)),
                               sizes.ctypes.data_as(C.POINTER(C.c_uint32)))
@@ -428,6 +429,7 @@ def sections_commit(secs: list[Section], methods: np.ndarray) -> list[SectionRes
     so = _load()
     res = (SectionResult * len(secs))()
     m = np.ascontiguousarray(methods, np.int32)
+    _lib.after_torch()
     rc = so.fqz5_sections_commit(_arr(Section, secs), len(secs),
                                  m.ctypes.data_as(C.POINTER(C.c_int32)), res)
     if rc:
@@ -438,37 +440,89 @@ def sections_commit(secs: list[Section], methods: np.ndarray) -> list[SectionRes
 def decode(secs: list[Section]) -> list[SectionResult]:
     so = _load()
     res = (SectionResult * len(secs))()
+    _lib.after_torch()
     if so.fqz5_decode_sections(_arr(Section, secs), len(secs), res):
         raise _lib.NativeError("fqz5_decode_sections: " + _lib.last_error())
     return list(res)
 
 
+class PeerError(RuntimeError):
+    """Another rank of the group failed (its error envelope arrived in an
+    exchange); raised on every rank that was waiting for it."""
+
+
+def xchg(obj, group=None) -> list:
+    """Every rank's `obj` (rank order): the one collective of the encode and
+    decode paths, all_gather_object with an error envelope.  All the paths'
+    exchanges (sizes, minima, barriers) go through it, so a failing rank's
+    error envelope (ranks_fail_together) always pairs with the exchange its
+    peers are waiting in, whichever it is, and every rank raises."""
+    ws, _ = _world(group)
+    if ws == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * ws
+    dist.all_gather_object(out, ("ok", obj), group=group)
+    for r, (st, m) in enumerate(out):
+        if st != "ok":
+            raise PeerError(f"rank {r} failed: {m}")
+    return [m for _, m in out]
+
+
+class ranks_fail_together:
+    """Context of one multi-rank call (compress_file, decompress_file, a
+    bench step): every rank calls it with the same exchanges.  A rank whose
+    body raises sends one error envelope as its next exchange: its peers are
+    all blocked in that same exchange (no rank can pass an exchange this
+    rank has not joined), receive the error and raise PeerError, so every
+    rank fails at once instead of waiting for the process group's timeout.
+    The body must end with an exchange (a final barrier) so that no peer can
+    have left before a failure inside it."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, ev, tb):
+        if ev is None or isinstance(ev, PeerError) or _world(self.group)[0] == 1:
+            return False
+        import torch.distributed as dist
+        out = [None] * _world(self.group)[0]
+        try:
+            dist.all_gather_object(out, ("err", repr(ev)[:400]), group=self.group)
+        except Exception:          # the group itself is gone: nothing to tell
+            pass
+        return False
+
+
+def barrier(group=None) -> None:
+    """A barrier as an exchange (xchg), so that it can carry a peer's error."""
+    xchg(None, group)
+
+
 def exchange_sizes(local: np.ndarray, in_sizes: np.ndarray, sec_ids: np.ndarray,
                    group=None):
     """All-gather the candidate sizes of every rank's sections (rank-major =
-    file order).  This is the only collective on the encode path: the trial
-    state of later blocks depends on the first blocks' candidates."""
-    import torch
+    file order).  This is the only exchange of the encode path: the trial
+    state of later blocks depends on the first blocks' candidates (KB
+    messages: latency-bound, so one all_gather_object, xchg)."""
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized():
         return local, in_sizes, sec_ids, 0
-    ws, rk = dist.get_world_size(group), dist.get_rank(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) \
-        if dist.get_backend(group) == "nccl" else torch.device("cpu")
-    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
-    ns = [torch.zeros_like(n) for _ in range(ws)]
-    dist.all_gather(ns, n, group=group)
-    nmax = int(max(int(x) for x in ns))
-    pack = np.zeros((nmax, M_LAST + 2), np.int64)
-    pack[:local.shape[0], :M_LAST] = local
-    pack[:local.shape[0], M_LAST] = in_sizes
-    pack[:local.shape[0], M_LAST + 1] = sec_ids
-    t = torch.from_numpy(pack).to(dev)
-    outs = [torch.zeros_like(t) for _ in range(ws)]
-    dist.all_gather(outs, t, group=group)
-    rows = [o[:int(k)].cpu().numpy() for o, k in zip(outs, ns)]
+    if group is None:             # (here: the default group, all ranks)
+        group = dist.group.WORLD
+    ws, rk = _world(group)
+    if ws == 1:
+        return local, in_sizes, sec_ids, 0
+    pack = np.zeros((local.shape[0], M_LAST + 2), np.int64)
+    pack[:, :M_LAST] = local
+    pack[:, M_LAST] = in_sizes
+    pack[:, M_LAST + 1] = sec_ids
+    rows = xchg(pack, group)
     allp = np.concatenate(rows, 0)
-    off = sum(int(k) for k in ns[:rk])
+    off = sum(int(r.shape[0]) for r in rows[:rk])
     return (allp[:, :M_LAST].astype(np.uint32), allp[:, M_LAST].astype(np.uint32),
             allp[:, M_LAST + 1].astype(np.int32), off)
 
@@ -694,16 +748,11 @@ def _world(group):
 
 
 def allreduce_min(a: np.ndarray, group) -> np.ndarray:
-    """Element-wise minimum over the ranks of `group` (int64 on the wire)."""
-    import torch
-    import torch.distributed as dist
+    """Element-wise minimum over the ranks of `group` (an exchange, xchg)."""
     if _world(group)[0] == 1:
         return a
-    dev = torch.device("cuda", torch.cuda.current_device()) \
-        if dist.get_backend(group) == "nccl" else torch.device("cpu")
-    t = torch.from_numpy(np.ascontiguousarray(a, np.int64)).to(dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
-    return t.cpu().numpy().astype(a.dtype)
+    parts = xchg(np.ascontiguousarray(a, np.int64), group)
+    return np.minimum.reduce(parts).astype(a.dtype)
 
 
 def work_share(methods: list[int], world: int, rank: int) -> int:
@@ -1153,6 +1202,7 @@ class Run:
                                        device=self.seq_d.device)
         self.blk_off = off
         out = np.zeros(len(parts), np.uint32)
+        _lib.after_torch()
         rc = so.fqz5_blocks_assemble(_arr(BlockParts, parts), len(parts), self.blk_buf.data_ptr(),
                                      off.ctypes.data_as(C.POINTER(C.c_uint64)),
                                      out.ctypes.data_as(C.POINTER(C.c_uint32)))
@@ -1171,6 +1221,7 @@ class Run:
         s, e = int(self.blk_off[b]), int(self.blk_off[b + 1])
         nrec = len(self.lens[b])
         lens = np.zeros(max(nrec, 1), np.uint32)
+        _lib.after_torch()
         if so.fqz5_block_parse(self.blk_buf.data_ptr() + s, e - s, C.byref(v),
                                lens.ctypes.data_as(C.POINTER(C.c_uint32)), len(lens)):
             raise _lib.NativeError("fqz5_block_parse: " + _lib.last_error())

@@ -247,9 +247,10 @@ void *fqz5_stream(void);
  *  - outputs: every device output is written when the call returns (the
  *    calls synchronise fqz5_stream() before returning), so any stream may
  *    read it afterwards.
- * fqz5_stream_wait: the calling thread's fqz5_stream() waits for all work
- * enqueued on `stream` (a hipStream_t; NULL = the null stream) so far.
- * Returns 0 or -1. */
+ * fqz5_stream_wait: the calling thread's fqz5_stream() — and every stream
+ * the calling thread's entry points hand work to (its helper contexts,
+ * existing or created later) — waits for all work enqueued on `stream` (a
+ * hipStream_t; NULL = the null stream) so far.  Returns 0 or -1. */
 int fqz5_stream_wait(void *stream);
 
 /* 1 if a HIP device is usable, else 0 (and fqz5_last_error() is set). */
