@@ -72,8 +72,17 @@ FASTQ_REC = 358          # bytes of FASTQ text per synthetic 150 bp record (avg)
 GAP_S = float(os.environ.get("FQZ5_BENCH_GAP_S", "0") or 0)
 BLK = 100_000_000        # -3 / -5 block size (fqzcomp5.c:4896,4904)
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8 TB/s spec
-# fqz5_profile_read_all's kernels (include/fqz5_mi355x.h)
-PROF_KERNELS = ["k_enc_chain", "k_rans_dec", "k_fqz_dec", "k_fqz_rc", "k_seq_dec"]
+# fqz5_profile_read_all's kernels, in its order (include/fqz5_mi355x.h); each
+# launch timed by HIP events around it on its own stream.  k_enc_replay is
+# the emitting pass (rocprof: k_enc_replay<true>), k_enc_replay0 the
+# counting pass (k_enc_replay<false>); k_fqz_dec both fqz decoders
+PROF_KERNELS = ["k_enc_chain", "k_rans_dec", "k_fqz_dec", "k_fqz_rc", "k_seq_dec",
+                "k_enc_chain2w", "k_enc_replay", "k_seq_model", "k_fqz_model_hot",
+                "k_fqz_ev_fill", "k_lzp_dec", "k_enc_replay0"]
+# rocprof kernel names of a PROF_KERNELS entry (pmc_traffic)
+ROCPROF_NAMES = {"k_fqz_dec": ["k_fqz_dec", "k_fqz_dec_small"],
+                 "k_enc_replay": ["k_enc_replay<true>"],
+                 "k_enc_replay0": ["k_enc_replay<false>"]}
 
 
 def log(*a):
@@ -111,12 +120,11 @@ def pmc_traffic(kernel: str, tag: str = ""):
     if not files:
         return None, None, None
     js = json.load(open(files[-1]))
-    # k_fqz_dec times both fqz decoders (fqz_codec.cpp PK_FQZ_DEC): the
-    # general k_fqz_dec and the small-alphabet k_fqz_dec_small
-    names = [kernel] + (["k_fqz_dec_small"] if kernel == "k_fqz_dec" else [])
+    names = ROCPROF_NAMES.get(kernel, [kernel])
     best = None
     for k, v in js["kernels"].items():
-        if any(f"::{n}(" in k or f"::{n}<" in k for n in names):
+        if any(f"::{n}(" in k or (f"::{n}<" in k if "<" not in n else f"::{n}(" in k)
+               for n in names):
             # the step's main launch of the kernel (the largest dispatch);
             # the file's "note" says how that launch ran (hedged copies)
             b = int(v.get("hbm_bytes_max_dispatch", v["hbm_bytes_per_dispatch"]))
@@ -199,11 +207,13 @@ def t1_check(reads, blocks, level, gpu_blocks, nblk: int, timeout: int = 900):
 
 
 def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local, dist,
-            scaling="weak", pmc_tag="", dropin=False, t1_blocks=0, hybrid=False):
+            scaling="weak", pmc_tag="", dropin=False, t1_blocks=0, gpu_only=False):
     """One workload: warmup + `steps` timed steps (barrier + synchronize on
-    both sides, max over ranks) and the result fields of its JSON line.
-    hybrid: then time the decode again with the adaptive-model chains on host
-    cores beside the GPU (fqz5_set_host_decode(1)), reported apart."""
+    both sides, max over ranks) and the result fields of its JSON line.  The
+    decode places each adaptive-model chain (fqz quality, sequence model) on
+    a host core or the GPU by its measured cost (fqz5_set_host_decode(2), the
+    library's default).  gpu_only: then time the decode again with every
+    chain on the GPU (fqz5_set_host_decode(0)), reported apart."""
     import torch
     from fqzcomp5_amd import lib, sections as S, synth
 
@@ -245,6 +255,8 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     lib.arena_use_peak(reset=True)
     so = lib.load()
     fq0 = S.trial_counts()
+    ch0 = (C.c_uint64 * 2)()
+    so.fqz5_decode_chain_counts(ch0)
     so.fqz5_profile(1)
     if world > 1:
         dist.barrier()
@@ -293,14 +305,15 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     # ---- correctness: every decoded section equals its input -------------
     ok = all(r.status == 0 for r in res) and all(r.status == 0 for r in dres)
     ok = ok and run.roundtrip_ok()
-    # ---- the same decode with the fqz / sequence-model chains on host
-    # cores (the library's own C++ decoders, host_dec.cpp) beside the GPU's
-    # rANS and names; the GPU-only figures above stay the item's numbers ----
-    hyb = None
-    if hybrid:
-        prev = so.fqz5_set_host_decode(1)
+    chains = (C.c_uint64 * 2)()
+    so.fqz5_decode_chain_counts(chains)      # (the timed steps': less ch0)
+    # ---- the same decode with every fqz / sequence-model chain on the GPU
+    # (fqz5_set_host_decode(0)); the figures above stay the item's numbers --
+    gonly = None
+    if gpu_only:
+        prev = so.fqz5_set_host_decode(0)
         try:
-            decode(res)                            # warm: the host model buffers
+            decode(res)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -312,19 +325,18 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                 hs.append(time.perf_counter() - b)
         finally:
             so.fqz5_set_host_decode(prev)
-        h_ok = all(r.status == 0 for r in hres) and run.roundtrip_ok()
+        g_ok = all(r.status == 0 for r in hres) and run.roundtrip_ok()
         th = torch.tensor([sum(hs)], dtype=torch.float64,
                           device=dev if world == 1 or dist.get_backend() == "nccl" else torch.device("cpu"))
         if world > 1:
             dist.all_reduce(th, op=dist.ReduceOp.MAX)
-        t_hdec = float(th.item())
-        hyb = {"dec_ms_per_step": round(t_hdec / steps * 1e3, 2),
-               "dec_MBps": round(fq_all * steps / t_hdec / 1e6, 2),
-               "value": round(fq_all * steps / (t_enc + t_hdec) / 1e6, 2),
-               "host_threads": int(so.fqz5_host_threads()),
-               "roundtrip_ok": bool(h_ok),
-               "note": "decode with fqz quality and sequence-model sections on host cores "
-                       "(fqz5_set_host_decode(1)); encode as above; same bytes"}
+        t_gdec = float(th.item())
+        gonly = {"dec_ms_per_step": round(t_gdec / steps * 1e3, 2),
+                 "dec_MBps": round(fq_all * steps / t_gdec / 1e6, 2),
+                 "value": round(fq_all * steps / (t_enc + t_gdec) / 1e6, 2),
+                 "roundtrip_ok": bool(g_ok),
+                 "note": "the same decode with every fqz / sequence-model chain on the GPU "
+                         "(fqz5_set_host_decode(0)); encode as above; same bytes"}
     comp_bytes = int(run.blk_off[-1])
     shape = {"illumina": "illumina 150 bp, Illumina names, 8-level binned quals",
              "novaseq": "novaseq 150 bp, Illumina names, NovaSeq 4-level i.i.d. quals",
@@ -374,8 +386,12 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                                  "intervals_decided": S.last_bounds_decided if level >= 5
                                  else None}},
     }
-    if hyb is not None:
-        out["hybrid"] = hyb
+    out["decode_chains"] = {"host": int(chains[0] - ch0[0]), "gpu": int(chains[1] - ch0[1]),
+                            "host_threads": int(so.fqz5_host_threads()),
+                            "rule": "each fqz / sequence-model chain where its measured cost "
+                                    "finishes the decode soonest (fqz5_set_host_decode(2))"}
+    if gonly is not None:
+        out["gpu_only"] = gonly
     # ---- roofline of the dominant kernel ---------------------------------
     # every chain kernel's launch time from HIP events on the stream it runs
     # on (fqz5_profile_read_all: rANS encode / decode, fqz decode, the fqz
@@ -629,7 +645,7 @@ def main():
                                          else args.gb * world, min(args.steps, 2),
                                          min(args.warmup, 1), not args.no_cpu, threads, world,
                                          rank, local, dist, scaling=args.scaling,
-                                         pmc_tag="_l5i", t1_blocks=4, hybrid=True)
+                                         pmc_tag="_l5i", t1_blocks=4, gpu_only=True)
     if rank == 0 and world == 1 and not args.no_crc:
         out["crc32"] = crc_item(lib, torch)
     if rank == 0:

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <functional>
 #include <thread>
 #include <deque>
 #include <memory>
@@ -217,6 +218,7 @@ std::atomic<int> g_prune{0};
 // and codes the winners at commit (encode_run_bounded).
 std::atomic<int> g_bounds{0};
 std::atomic<uint64_t> g_fqz_tried{0}, g_fqz_pruned{0};
+std::atomic<uint64_t> g_chains_host{0}, g_chains_gpu{0};   // fqz5_decode_chain_counts
 
 // Which requests of one family of work candidates (fqz methods FQZ0..FQZ4 on
 // quality sections, or the sequence models SEQ10..SEQ14B) to skip, from the
@@ -327,6 +329,11 @@ int fqz5_sections_try_upper(uint32_t *upper, int nsec) {
     }
     std::memcpy(upper, t_sess.upper.data(), t_sess.upper.size() * sizeof(uint32_t));
     return 0;
+}
+
+void fqz5_decode_chain_counts(uint64_t *out2) {
+    out2[0] = g_chains_host.load();
+    out2[1] = g_chains_gpu.load();
 }
 
 void fqz5_trial_counts(uint64_t *out2) {
@@ -1005,51 +1012,97 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             who.push_back(i);
         }
         const auto t1 = std::chrono::steady_clock::now();
-        // ---- the adaptive-model chains on host cores (fqz5_set_host_decode):
-        // sequence-model sections and quality sections without a sequence
-        // context start now, beside the GPU's rANS and names; quality
-        // sections with one wait for their block's bases ---------------------
+        // ---- where each adaptive-model chain decodes (host_decode_mode():
+        // 0 the GPU, 1 host cores, 2 by the chains' measured costs,
+        // host::plan).  A quality chain with a sequence context waits for
+        // its block's bases; when those come from a host chain it runs on
+        // the host too (its bases are there) ----------------------------------
+        const int hmode = host_decode_mode();
+        std::vector<int> fqz_kind(fqz.size(), host::CK_FQZ), fqz_src(fqz.size(), -1);
+        for (size_t k = 0; k < fqz.size(); k++) {
+            const FqzDecReq &f = fqz[k];
+            uint32_t tl = 0;
+            const int vk = varint_get(f.h_in, f.h_in + f.in_size, &tl);
+            if (vk > 0 && size_t(vk) + 1 < f.in_size && (f.h_in[vk + 1] & 8u) && f.d_seq) {
+                fqz_kind[k] = host::CK_FQZ_SEQ;
+                for (size_t m = 0; m < seqd.size(); m++)
+                    if (seqd[m].d_out == f.d_seq) fqz_src[k] = int(m);
+            }
+        }
+        std::vector<char> seq_on_host(seqd.size(), hmode == 1), fqz_on_host(fqz.size(), hmode == 1);
+        if (hmode == 3) {                 // (tests: every other chain on the host)
+            for (size_t m = 0; m < seqd.size(); m++) seq_on_host[m] = m % 2 == 0;
+            for (size_t k = 0; k < fqz.size(); k++) fqz_on_host[k] = (seqd.size() + k) % 2 == 0;
+        }
+        if (hmode == 2 && !(seqd.empty() && fqz.empty())) {
+            std::vector<uint64_t> n;
+            std::vector<int> kind;
+            for (const SeqDecReq &q : seqd) { n.push_back(q.n); kind.push_back(host::CK_SEQ); }
+            for (size_t k = 0; k < fqz.size(); k++) { n.push_back(fqz[k].out_cap); kind.push_back(fqz_kind[k]); }
+            const std::vector<char> on = host::plan(n, kind, host::threads());
+            for (size_t m = 0; m < seqd.size(); m++) seq_on_host[m] = on[m];
+            for (size_t k = 0; k < fqz.size(); k++) fqz_on_host[k] = on[seqd.size() + k];
+        }
+        for (size_t k = 0; k < fqz.size(); k++)
+            if (fqz_src[k] >= 0 && seq_on_host[size_t(fqz_src[k])]) fqz_on_host[k] = 1;
+        g_chains_host += uint64_t(std::count(seq_on_host.begin(), seq_on_host.end(), 1) +
+                                  std::count(fqz_on_host.begin(), fqz_on_host.end(), 1));
+        g_chains_gpu += uint64_t(std::count(seq_on_host.begin(), seq_on_host.end(), 0) +
+                                 std::count(fqz_on_host.begin(), fqz_on_host.end(), 0));
+        // ---- the host chains: sequence-model sections and quality sections
+        // without a sequence context start now, beside the GPU's rANS and
+        // names; quality sections with one wait for their block's bases
         struct HostChain { uint8_t *buf = nullptr; size_t cap = 0, n = 0; int sec = -1; bool ok = false; };
         std::vector<HostChain> hc;
-        std::vector<size_t> hc_fqz;                   // fqz index of each host fqz chain
-        std::vector<int> hc_kind;                     // 0 seq, 1 fqz (no sequence), 2 fqz (sequence)
-        host::Jobs hjobs;
-        const int hmode = host_decode_mode();
-        if (hmode) {
-            for (size_t k = 0; k < seqd.size(); k++) {
-                HostChain c;
-                c.cap = c.n = seqd[k].n;
-                c.buf = g.staging.alloc(c.cap + 1);
-                c.sec = who_seq[k];
-                hc.push_back(c);
-                hc_fqz.push_back(k);
-                hc_kind.push_back(0);
-            }
-            for (size_t k = 0; k < fqz.size(); k++) {
-                const FqzDecReq &f = fqz[k];
-                uint32_t tl = 0;
-                const int vk = varint_get(f.h_in, f.h_in + f.in_size, &tl);
-                const bool seqctx = vk > 0 && size_t(vk) + 1 < f.in_size && (f.h_in[vk + 1] & 8u) && f.d_seq;
-                HostChain c;
-                c.cap = f.out_cap;
-                c.buf = g.staging.alloc(c.cap + 1);
-                c.sec = who_fqz[k];
-                hc.push_back(c);
-                hc_fqz.push_back(k);
-                hc_kind.push_back(seqctx ? 2 : 1);
-            }
-            hjobs.start(hc.size(), [&](size_t j) {
-                HostChain &c = hc[j];
-                if (hc_kind[j] == 0) {
-                    const SeqDecReq &q = seqd[hc_fqz[j]];
-                    c.ok = host::seq_decode(seq_h[hc_fqz[j]], q.in_size, q.lens, q.nrec, q.both, q.k, c.buf,
-                                            q.n) == 0;
-                } else if (hc_kind[j] == 1) {
-                    const FqzDecReq &f = fqz[hc_fqz[j]];
-                    c.ok = host::fqz_decode(f.h_in, f.in_size, c.buf, c.cap, &c.n, nullptr, 0, nullptr, 0) == 0;
-                }
-            });
+        std::vector<size_t> hc_idx;                   // seqd / fqz index of each host chain
+        std::vector<int> hc_kind;                     // host::ChainKind
+        for (size_t k = 0; k < seqd.size(); k++) {
+            if (!seq_on_host[k]) continue;
+            HostChain c;
+            c.cap = c.n = seqd[k].n;
+            c.buf = g.staging.alloc(c.cap + 1);
+            c.sec = who_seq[k];
+            hc.push_back(c);
+            hc_idx.push_back(k);
+            hc_kind.push_back(host::CK_SEQ);
         }
+        for (size_t k = 0; k < fqz.size(); k++) {
+            if (!fqz_on_host[k]) continue;
+            HostChain c;
+            c.cap = fqz[k].out_cap;
+            c.buf = g.staging.alloc(c.cap + 1);
+            c.sec = who_fqz[k];
+            hc.push_back(c);
+            hc_idx.push_back(k);
+            hc_kind.push_back(fqz_kind[k]);
+        }
+        auto timed = [](int kind, size_t n, const std::function<bool()> &fn) {
+            const auto a = std::chrono::steady_clock::now();
+            const bool ok = fn();
+            const double ns = std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - a).count();
+            if (ok && n >= (1u << 20)) host::chain_measured(kind, false, ns / double(n));
+            return ok;
+        };
+        host::Jobs hjobs;
+        std::vector<size_t> early_h;                  // host chains that start now
+        for (size_t j = 0; j < hc.size(); j++)
+            if (hc_kind[j] != host::CK_FQZ_SEQ) early_h.push_back(j);
+        hjobs.start(early_h.size(), [&](size_t t) {
+            const size_t j = early_h[t];
+            HostChain &c = hc[j];
+            if (hc_kind[j] == host::CK_SEQ) {
+                const SeqDecReq &q = seqd[hc_idx[j]];
+                c.ok = timed(host::CK_SEQ, q.n, [&] {
+                    return host::seq_decode(seq_h[hc_idx[j]], q.in_size, q.lens, q.nrec, q.both, q.k,
+                                            c.buf, q.n) == 0;
+                });
+            } else {
+                const FqzDecReq &f = fqz[hc_idx[j]];
+                c.ok = timed(host::CK_FQZ, c.cap, [&] {
+                    return host::fqz_decode(f.h_in, f.in_size, c.buf, c.cap, &c.n, nullptr, 0, nullptr, 0) == 0;
+                });
+            }
+        });
         // the name sections on their helper context, beside the chains: their
         // host rebuild overlaps the GPU's rANS / fqz / sequence decoding
         // The name sections decode on their helper context beside the chains.
@@ -1077,7 +1130,14 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             std::thread &t;
             ~Join() { if (t.joinable()) t.join(); }
         } join_names{tn};
-        // fqz quality sections without a sequence context need nothing else
+        // a GPU batch's time over its longest chain: the chain cost the plan reads
+        auto gpu_timed = [](int kind, uint64_t longest, const std::function<void()> &fn) {
+            const auto a = std::chrono::steady_clock::now();
+            fn();
+            const double ns = std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - a).count();
+            if (longest >= (1u << 20)) host::chain_measured(kind, true, ns / double(longest));
+        };
+        // GPU quality sections without a sequence context need nothing else
         // of this call: they decode on the fqz helper context from a thread
         // of their own, beside the rANS / LZP / sequence-model work, instead
         // of after it (a -5 Illumina step waited ~0.6 s for the rANS batch
@@ -1085,17 +1145,14 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         std::vector<FqzDecReq> fqz_early;
         std::vector<size_t> early_of;                 // fqz index of each early request
         std::vector<char> is_early(fqz.size(), 0);
-        if (!hmode)
-            for (size_t k = 0; k < fqz.size(); k++) {
-                const FqzDecReq &f = fqz[k];
-                uint32_t tl = 0;
-                const int vk = varint_get(f.h_in, f.h_in + f.in_size, &tl);
-                const bool seqctx = vk > 0 && size_t(vk) + 1 < f.in_size && (f.h_in[vk + 1] & 8u) && f.d_seq;
-                if (seqctx) continue;
-                fqz_early.push_back(f);
-                early_of.push_back(k);
-                is_early[k] = 1;
-            }
+        uint64_t early_longest = 0;
+        for (size_t k = 0; k < fqz.size(); k++) {
+            if (fqz_on_host[k] || fqz_kind[k] == host::CK_FQZ_SEQ) continue;
+            fqz_early.push_back(fqz[k]);
+            early_of.push_back(k);
+            is_early[k] = 1;
+            early_longest = std::max<uint64_t>(early_longest, fqz[k].out_cap);
+        }
         std::exception_ptr ferr;
         std::thread tf;
         GpuCtx *gf = nullptr;
@@ -1104,23 +1161,32 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             tf = std::thread([&] {
                 try {
                     FQZ5_HIP(hipSetDevice(gf->device));
-                    fqz_decode_batch(*gf, fqz_early);
+                    gpu_timed(host::CK_FQZ, early_longest, [&] { fqz_decode_batch(*gf, fqz_early); });
                 } catch (...) {
                     ferr = std::current_exception();
                 }
             });
         }
         Join join_fqz{tf};
-        // the sequence-model sections likewise (their own helper context)
+        // the GPU's sequence-model sections likewise (their own helper context)
+        std::vector<SeqDecReq> seq_gpu;
+        std::vector<size_t> seq_gpu_of;
+        uint64_t seq_longest = 0;
+        for (size_t m = 0; m < seqd.size(); m++)
+            if (!seq_on_host[m]) {
+                seq_gpu.push_back(seqd[m]);
+                seq_gpu_of.push_back(m);
+                seq_longest = std::max<uint64_t>(seq_longest, seqd[m].n);
+            }
         std::exception_ptr serr;
         std::thread ts;
         GpuCtx *gs = nullptr;
-        if (!hmode && !seqd.empty()) {
+        if (!seq_gpu.empty()) {
             gs = &gpu_aux(AUX_SEQ0);
             ts = std::thread([&] {
                 try {
                     FQZ5_HIP(hipSetDevice(gs->device));
-                    seq_decode_batch(*gs, seqd);
+                    gpu_timed(host::CK_SEQ, seq_longest, [&] { seq_decode_batch(*gs, seq_gpu); });
                 } catch (...) {
                     serr = std::current_exception();
                 }
@@ -1151,39 +1217,50 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         }
         if (ts.joinable()) ts.join();
         if (serr) std::rethrow_exception(serr);
-        // after the rANS and sequence sections: a quality section's sequence context may
-        // be the output of this call's sequence section
-        if (!hmode && fqz_early.size() < fqz.size()) {
+        for (size_t i = 0; i < seq_gpu.size(); i++) seqd[seq_gpu_of[i]] = seq_gpu[i];
+        // after the rANS and sequence sections: a quality section's sequence
+        // context may be the output of this call's sequence section (a GPU
+        // one: host-decoded bases make their quality chain a host chain)
+        {
             std::vector<FqzDecReq> late;
             std::vector<size_t> late_of;
+            uint64_t longest = 0;
             for (size_t k = 0; k < fqz.size(); k++)
-                if (!is_early[k]) {
+                if (!is_early[k] && !fqz_on_host[k]) {
                     late.push_back(fqz[k]);
                     late_of.push_back(k);
+                    longest = std::max<uint64_t>(longest, fqz[k].out_cap);
                 }
-            fqz_decode_batch(g, late);
-            for (size_t k = 0; k < late.size(); k++) fqz[late_of[k]] = late[k];
+            if (!late.empty()) {
+                gpu_timed(host::CK_FQZ_SEQ, longest, [&] { fqz_decode_batch(g, late); });
+                for (size_t k = 0; k < late.size(); k++) fqz[late_of[k]] = late[k];
+            }
         }
         if (tf.joinable()) tf.join();
         if (ferr) std::rethrow_exception(ferr);
         for (size_t k = 0; k < fqz_early.size(); k++) fqz[early_of[k]] = fqz_early[k];
-        if (hmode) {
+        if (!hc.empty()) {
             hjobs.join();
             // the quality chains with a sequence context: their block's bases
             // on the host (a host-decoded sequence section's buffer, or a copy
             // of the GPU's output), per record pointers as the reference's s->seq
             std::vector<std::vector<const uint8_t *>> recp(hc.size());
             for (size_t j = 0; j < hc.size(); j++) {
-                if (hc_kind[j] != 2) continue;
-                const FqzDecReq &f = fqz[hc_fqz[j]];
+                if (hc_kind[j] != host::CK_FQZ_SEQ) continue;
+                const FqzDecReq &f = fqz[hc_idx[j]];
                 const uint8_t *bases = nullptr;
+                bool host_src = false;
                 for (size_t m = 0; m < hc.size(); m++)
-                    if (hc_kind[m] == 0 && secs[hc[m].sec].out == f.d_seq) bases = hc[m].ok ? hc[m].buf : nullptr;
+                    if (hc_kind[m] == host::CK_SEQ && secs[hc[m].sec].out == f.d_seq) {
+                        bases = hc[m].ok ? hc[m].buf : nullptr;
+                        host_src = true;
+                    }
                 uint64_t nb = 0;
                 for (int r = 0; r < f.nrec; r++) nb += f.lens[r];
                 if (!bases) {
                     uint8_t *b = g.staging.alloc(nb + 1);
-                    g.download(b, f.d_seq, nb);
+                    if (!host_src) g.download(b, f.d_seq, nb);
+                    else std::memset(b, 0, nb + 1);   // (its sequence chain failed)
                     bases = b;
                 }
                 recp[j].resize(size_t(std::max(f.nrec, 1)));
@@ -1197,12 +1274,14 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             host::Jobs hb;
             std::vector<size_t> late;
             for (size_t j = 0; j < hc.size(); j++)
-                if (hc_kind[j] == 2) late.push_back(j);
+                if (hc_kind[j] == host::CK_FQZ_SEQ) late.push_back(j);
             hb.start(late.size(), [&](size_t t) {
                 HostChain &c = hc[late[t]];
-                const FqzDecReq &f = fqz[hc_fqz[late[t]]];
-                c.ok = host::fqz_decode(f.h_in, f.in_size, c.buf, c.cap, &c.n, nullptr, 0,
-                                        recp[late[t]].data(), f.nrec) == 0;
+                const FqzDecReq &f = fqz[hc_idx[late[t]]];
+                c.ok = timed(host::CK_FQZ_SEQ, c.cap, [&] {
+                    return host::fqz_decode(f.h_in, f.in_size, c.buf, c.cap, &c.n, nullptr, 0,
+                                            recp[late[t]].data(), f.nrec) == 0;
+                });
             });
             hb.join();
             for (HostChain &c : hc) {
@@ -1231,12 +1310,14 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
             R.status = reqs[k].ok ? 0 : -1;
             R.usize = reqs[k].out_size;
         }
-        for (size_t k = 0; k < seqd.size() && !hmode; k++) {
+        for (size_t k = 0; k < seqd.size(); k++) {
+            if (seq_on_host[k]) continue;
             fqz5_section_result &R = res[who_seq[k]];
             R.status = seqd[k].ok ? 0 : -1;
             R.usize = seqd[k].n;
         }
-        for (size_t k = 0; k < fqz.size() && !hmode; k++) {
+        for (size_t k = 0; k < fqz.size(); k++) {
+            if (fqz_on_host[k]) continue;
             fqz5_section_result &R = res[who_fqz[k]];
             R.status = fqz[k].ok ? 0 : -1;
             R.usize = uint32_t(fqz[k].out_size);

@@ -76,6 +76,50 @@ void prof_add(int kernel, double ms, double bytes) {
     g_prof[kernel][2] += bytes;
 }
 bool prof_on() { return g_prof_on.load(); }
+
+struct ProfPending { int kernel; hipEvent_t a, b; double bytes; };
+static std::vector<ProfPending> g_prof_pend;          // under g_prof_mu
+ProfSpan::ProfSpan(int k, hipStream_t st) : s(st) {
+    if (!prof_on()) return;
+    if (hipEventCreate(&a) != hipSuccess) { a = nullptr; return; }
+    if (hipEventRecord(a, s) != hipSuccess) { (void)hipEventDestroy(a); a = nullptr; return; }
+    kernel = k;
+}
+long ProfSpan::end(double bytes) {
+    if (kernel < 0) return -1;
+    hipEvent_t b = nullptr;
+    if (hipEventCreate(&b) != hipSuccess || hipEventRecord(b, s) != hipSuccess) {
+        if (b) (void)hipEventDestroy(b);
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_pend.push_back({kernel, a, b, bytes});
+    a = nullptr;
+    kernel = -1;
+    return long(g_prof_pend.size()) - 1;
+}
+ProfSpan::~ProfSpan() {
+    if (a) (void)hipEventDestroy(a);
+}
+void prof_bytes(long token, double bytes) {
+    if (token < 0) return;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    if (size_t(token) < g_prof_pend.size()) g_prof_pend[size_t(token)].bytes = bytes;
+}
+// the queued spans into the table (their events complete first); under g_prof_mu
+static void prof_drain() {
+    for (ProfPending &p : g_prof_pend) {
+        float ms = 0;
+        if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            g_prof[p.kernel][0] += ms;
+            g_prof[p.kernel][1] += 1;
+            g_prof[p.kernel][2] += p.bytes;
+        }
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    g_prof_pend.clear();
+}
 static thread_local std::unique_ptr<GpuCtx> g_ctx;
 
 GpuCtx &gpu() {
@@ -132,7 +176,8 @@ int host_decode_mode() {
     int v = g_host_dec.load();
     if (v < 0) {
         const char *e = std::getenv("FQZ5_HOST_DECODE");
-        v = e ? std::atoi(e) : 0;
+        v = e ? std::atoi(e) : 2;
+        if (v < 0 || v > 3) v = 2;
         g_host_dec.store(v);
     }
     return v;
@@ -450,7 +495,7 @@ int fqz5_host_threads(void) { return host::threads(); }
 
 int fqz5_set_host_decode(int mode) {
     const int prev = host_decode_mode();
-    g_host_dec.store(mode ? 1 : 0);
+    g_host_dec.store(mode < 0 || mode > 3 ? 2 : mode);
     return prev;
 }
 
@@ -478,6 +523,7 @@ void fqz5_profile(int on) {
         g.prof.on = on != 0;
         {
             std::lock_guard<std::mutex> lk(g_prof_mu);
+            prof_drain();
             for (int k = 0; k < PK_N; k++) g_prof[k][0] = g_prof[k][1] = g_prof[k][2] = 0;
         }
         g_prof_on.store(on != 0);
@@ -488,6 +534,7 @@ void fqz5_profile(int on) {
 
 int fqz5_profile_read_all(double *out, int nk) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
+    prof_drain();
     const int n = nk < int(PK_N) ? nk : int(PK_N);
     for (int k = 0; k < n; k++)
         for (int j = 0; j < 3; j++) out[3 * k + j] = g_prof[k][j];

@@ -571,7 +571,11 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         J.skey = skey;
         J.sval = sval;
         J.code = g.ev_tmp.alloc_n<uint64_t>(nev);
-        FQZ5_HIP(launch_fqz_events(J, 1, g.stream));
+        {
+            ProfSpan sp(PK_FQZ_EV_FILL, g.stream);
+            FQZ5_HIP(launch_fqz_events(J, 1, g.stream));
+            sp.end(double(R->n));
+        }
         size_t tb = 0;
         FQZ5_HIP(fqz_sort_by_model(J.key, skey, J.val, sval, int(nev), int(FQZ_MODEL_BITS),
                                    nullptr, tb, g.stream));
@@ -611,7 +615,15 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
             stride = std::max(stride, 1u + std::min(FQZ_M_SEL, J.nev / std::max(hot_min, 1u) + 1));
         uint32_t *hot = g.fqz_tmp.alloc_n<uint32_t>(size_t(stride) * size_t(np));
         g.memset0(hot, size_t(stride) * size_t(np) * 4);
-        FQZ5_HIP(launch_fqz_model_pass(g.upload(jobs), np, hot, stride, hot_min, g.stream));
+        const FqzEvJob *d_jobs = g.upload(jobs);
+        double qb = 0;
+        for (FqzEncReq *R : par) qb += double(R->n);
+        if (hot_min) {
+            ProfSpan sp(PK_FQZ_MODEL_HOT, g.stream);
+            FQZ5_HIP(launch_fqz_model_hot(d_jobs, np, hot, stride, hot_min, g.stream));
+            sp.end(qb);
+        }
+        FQZ5_HIP(launch_fqz_model_pass(d_jobs, np, hot_min, g.stream));
         // the entropy of each block's events and the coder's slack: lower
         // and upper bounds of its size
         constexpr uint32_t EB = 1024;

@@ -160,8 +160,12 @@ hipError_t launch_fqz_events(const FqzEvJob &j, int phase, hipStream_t s);
 constexpr uint32_t FQZ_HOT_GRID = 64;            // waves per job for hot models
 constexpr uint32_t FQZ_HOT_GRID_MAX = 2048;     // at most, one per hot model
 constexpr uint32_t FQZ_HOT_MIN = 16384;
-hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t *hot,
-                                 uint32_t stride, uint32_t hot_min, hipStream_t s);
+// (the hot models first, then the pass over the rest: launch_fqz_model_hot
+// before launch_fqz_model_pass on the same stream)
+hipError_t launch_fqz_model_hot(const FqzEvJob *d_jobs, int njobs, uint32_t *hot,
+                                uint32_t stride, uint32_t hot_min, hipStream_t s);
+hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t hot_min,
+                                 hipStream_t s);
 hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
 // per workgroup b: sum over its events of log2(total / freq) (after the model
 // pass) in partial[b], of -log2(1 - total 2^-24) in partial[nblk + b]

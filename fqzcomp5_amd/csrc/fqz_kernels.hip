@@ -867,8 +867,23 @@ hipError_t launch_fqz_expand(const FqzEvJob &j, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t *hot,
-                                 uint32_t stride, uint32_t hot_min, hipStream_t s) {
+hipError_t launch_fqz_model_hot(const FqzEvJob *d_jobs, int njobs, uint32_t *hot,
+                                uint32_t stride, uint32_t hot_min, hipStream_t s) {
+    if (!njobs || !hot_min) return hipSuccess;
+    hipLaunchKernelGGL(k_fqz_hot_list, dim3((FQZ_M_SEL + 255) / 256, njobs), dim3(256), 0, s,
+                       d_jobs, hot, stride, hot_min);
+    // a wave per hot model (up to stride - 1 of them per block), at
+    // least FQZ_HOT_GRID: the launch then lasts as long as the longest
+    // model's chain, not a wave's share of a thousand models (-7 ONT:
+    // ~1 000 hot models per FQZ0 candidate)
+    const uint32_t grid = std::min(std::max(stride - 1, FQZ_HOT_GRID), FQZ_HOT_GRID_MAX);
+    hipLaunchKernelGGL(k_fqz_model_hot, dim3(grid, njobs), dim3(64), 0, s, d_jobs,
+                       hot, stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t hot_min,
+                                 hipStream_t s) {
     constexpr uint32_t lds = 256 * sizeof(FList<FQZ_QSYMS>);
     constexpr uint32_t nblk = (FQZ_NMODELS + 255) / 256;
     static bool attr = false;
@@ -878,17 +893,6 @@ hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t *ho
         attr = true;
     }
     if (!njobs) return hipSuccess;
-    if (hot_min) {
-        hipLaunchKernelGGL(k_fqz_hot_list, dim3((FQZ_M_SEL + 255) / 256, njobs), dim3(256), 0, s,
-                           d_jobs, hot, stride, hot_min);
-        // a wave per hot model (up to stride - 1 of them per block), at
-        // least FQZ_HOT_GRID: the launch then lasts as long as the longest
-        // model's chain, not a wave's share of a thousand models (-7 ONT:
-        // ~1 000 hot models per FQZ0 candidate)
-        const uint32_t grid = std::min(std::max(stride - 1, FQZ_HOT_GRID), FQZ_HOT_GRID_MAX);
-        hipLaunchKernelGGL(k_fqz_model_hot, dim3(grid, njobs), dim3(64), 0, s, d_jobs,
-                           hot, stride);
-    }
     hipLaunchKernelGGL(k_fqz_model_pass, dim3(nblk * uint32_t(njobs)), dim3(256), lds, s,
                        d_jobs, nblk, hot_min);
     return hipGetLastError();

@@ -287,9 +287,30 @@ class PinnedArena {
 // family, filled from every context (helper contexts included) while
 // fqz5_profile(1) is on: launch time, launches, algorithmic bytes (the
 // kernel's input plus output of its jobs).
-enum ProfKernel { PK_ENC_CHAIN, PK_RANS_DEC, PK_FQZ_DEC, PK_FQZ_RC, PK_SEQ_DEC, PK_N };
+enum ProfKernel {
+    PK_ENC_CHAIN, PK_RANS_DEC, PK_FQZ_DEC, PK_FQZ_RC, PK_SEQ_DEC,           // (the first five: r01-r04)
+    PK_ENC_CHAIN2W, PK_ENC_REPLAY, PK_SEQ_MODEL, PK_FQZ_MODEL_HOT, PK_FQZ_EV_FILL, PK_LZP_DEC,
+    PK_ENC_REPLAY0, PK_N
+};
 void prof_add(int kernel, double ms, double bytes);
 bool prof_on();
+// One kernel launch timed on its own stream: begin() records an event before
+// the launch, end() one after it and queues the pair; fqz5_profile_read_all
+// synchronises the queued events and adds their spans (so no launch site
+// waits for its kernel).  `bytes` (algorithmic input + output) may be set
+// after end() with prof_bytes(token) once known.  No-ops while profiling is
+// off (token -1).
+struct ProfSpan {
+    int kernel = -1;
+    hipStream_t s = nullptr;
+    hipEvent_t a = nullptr;
+    ProfSpan(int k, hipStream_t st);
+    long end(double bytes);
+    ProfSpan(const ProfSpan &) = delete;
+    ProfSpan &operator=(const ProfSpan &) = delete;
+    ~ProfSpan();
+};
+void prof_bytes(long token, double bytes);
 
 struct KernelProfile {
     bool on = false;

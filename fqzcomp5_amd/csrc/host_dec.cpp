@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
 #include <vector>
 
@@ -352,6 +353,51 @@ int seq_decode(const uint8_t *in, uint32_t in_size, const uint32_t *lens, int nr
         else state = ns ? 1 : 0;
     }
     return 0;
+}
+
+namespace {
+// ns per symbol [kind][gpu]: priors from r04 on MI355X boxes (host: this
+// file's decoders on one core of the box, the -5 Illumina hybrid step; GPU:
+// k_fqz_dec_small 170-190, the general decoder with sequence contexts
+// 350-470, k_seq_dec 290-380)
+std::atomic<double> g_ns[CK_N][2] = {{{30.0}, {330.0}}, {{16.0}, {180.0}}, {{24.0}, {400.0}}};
+}  // namespace
+
+double chain_ns(int kind, bool gpu) { return g_ns[kind][gpu ? 1 : 0].load(std::memory_order_relaxed); }
+
+void chain_measured(int kind, bool gpu, double ns) {
+    if (!(ns > 0.0) || kind < 0 || kind >= CK_N) return;
+    std::atomic<double> &a = g_ns[kind][gpu ? 1 : 0];
+    double cur = a.load(std::memory_order_relaxed);
+    // an exponential average: a chain's cost moves with its data
+    while (!a.compare_exchange_weak(cur, 0.5 * cur + 0.5 * ns, std::memory_order_relaxed)) {}
+}
+
+std::vector<char> plan(const std::vector<uint64_t> &n, const std::vector<int> &kind, int threads) {
+    std::vector<char> host(n.size(), 0);
+    std::vector<size_t> ord(n.size());
+    for (size_t i = 0; i < ord.size(); i++) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+        return double(n[a]) * chain_ns(kind[a], false) > double(n[b]) * chain_ns(kind[b], false);
+    });
+    std::vector<double> core(size_t(std::max(threads, 1)), 0.0);   // each core's finish time
+    double gpu_t = 0.0;
+    for (size_t i : ord) {
+        auto lo = std::min_element(core.begin(), core.end());
+        const double th = *lo + double(n[i]) * chain_ns(kind[i], false);
+        const double tg = double(n[i]) * chain_ns(kind[i], true);
+        double cmax = 0.0;
+        for (double c : core) cmax = std::max(cmax, c);
+        const double on_host = std::max({cmax, th, gpu_t});
+        const double on_gpu = std::max({cmax, gpu_t, tg});
+        if (on_host <= on_gpu) {
+            *lo = th;
+            host[i] = 1;
+        } else {
+            gpu_t = std::max(gpu_t, tg);
+        }
+    }
+    return host;
 }
 
 int threads() {

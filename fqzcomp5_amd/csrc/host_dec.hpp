@@ -27,6 +27,22 @@ int seq_decode(const uint8_t *in, uint32_t in_size, const uint32_t *lens, int nr
 // process may use (at most 16, the CPU share of one GPU on the MI355X boxes).
 int threads();
 
+// Which adaptive-model decode chains of a fqz5_decode_sections call run on
+// host cores and which on the GPU (host_decode_mode() 2, the default).  A
+// chain is serial whichever side runs it: on a host core it costs
+// n x host_ns, and a host core takes one chain at a time; on the GPU each
+// chain has a wave of its own (the launch lasts as long as its longest
+// chain, n x gpu_ns).  The per-symbol costs start at committed measurements
+// (profiles/r04_fqz_dec_bench.txt) and follow what this
+// process measures: every host chain's time, and every GPU batch's time over
+// its longest chain.  plan() places the chains longest first, each where the
+// call's finish time (the later of the host cores' and the GPU's) grows
+// least; ties go to the host.
+enum ChainKind { CK_SEQ = 0, CK_FQZ = 1, CK_FQZ_SEQ = 2, CK_N };
+double chain_ns(int kind, bool gpu);
+void chain_measured(int kind, bool gpu, double ns_per_symbol);
+std::vector<char> plan(const std::vector<uint64_t> &n, const std::vector<int> &kind, int threads);
+
 // fn(i) for i in [0, n) on up to threads() host threads, started by start()
 // and waited for by join() (or the destructor); the work list is shared, so
 // long and short jobs balance.

@@ -101,7 +101,12 @@ void lzp_decode_batch(GpuCtx &g, std::vector<LzpDecReq> &reqs) {
         J.out_len = lens + r;
         J.status = st + r;
     }
-    FQZ5_HIP(launch_lzp_dec(g.upload(js), int(js.size()), g.stream));
+    const LzpDecJob *d_js = g.upload(js);
+    ProfSpan sp(PK_LZP_DEC, g.stream);
+    FQZ5_HIP(launch_lzp_dec(d_js, int(js.size()), g.stream));
+    double b = 0;
+    for (const LzpDecReq &r : reqs) b += double(r.in_len) + r.cap;
+    sp.end(b);
     std::vector<uint32_t> L(reqs.size());
     std::vector<int32_t> S(reqs.size());
     g.download(L.data(), lens, L.size());

@@ -619,26 +619,46 @@ void Compressor::stage_encode() {
         eall.push_back(e);
         lds_r = std::max(lds_r, enc_replay_lds_bytes(j.o1, uint32_t(j.A)));
     }
-    EventPair ev((g_.prof.on || prof_on()) && !order.empty(), g_.stream);
+    EventPair ev(g_.prof.on && !order.empty(), g_.stream);
     lds_s = g_.chain_lds(lds_s, ejs.size() + ejb.size());
     lds_b = g_.chain_lds(lds_b, ejs.size() + ejb.size());
+    // per-kernel spans (fqz5_profile_read_all): their bytes once the
+    // output lengths are known, below
+    long tk_2w = -1, tk_1w = -1, tk_r0 = -1, tk_r1 = -1;
     if (!ejs.empty()) {
         const EncJob *d = g_.upload(ejs);
         const EncJob *db = ejb.empty() ? nullptr : g_.upload(ejb);
         g_.fork();
-        FQZ5_HIP(launch_enc_chain2w(d, int(ejs.size()), lds_s, g_.stream2));
-        if (db) FQZ5_HIP(launch_enc_chain(db, int(ejb.size()), lds_b, g_.stream));
+        {
+            ProfSpan sp(PK_ENC_CHAIN2W, g_.stream2);
+            FQZ5_HIP(launch_enc_chain2w(d, int(ejs.size()), lds_s, g_.stream2));
+            tk_2w = sp.end(0);
+        }
+        if (db) {
+            ProfSpan sp(PK_ENC_CHAIN, g_.stream);
+            FQZ5_HIP(launch_enc_chain(db, int(ejb.size()), lds_b, g_.stream));
+            tk_1w = sp.end(0);
+        }
         g_.join();
     } else if (!ejb.empty()) {
-        FQZ5_HIP(launch_enc_chain(g_.upload(ejb), int(ejb.size()), lds_b, g_.stream));
+        const EncJob *db = g_.upload(ejb);
+        ProfSpan sp(PK_ENC_CHAIN, g_.stream);
+        FQZ5_HIP(launch_enc_chain(db, int(ejb.size()), lds_b, g_.stream));
+        tk_1w = sp.end(0);
     }
     if (!eall.empty()) {
         const EncJob *d_all = g_.upload(eall);
         const uint32_t *d_items = g_.upload(items);
         const int nit = int(items.size() / 2);
-        FQZ5_HIP(launch_enc_replay(d_all, d_items, nit, false, lds_r, g_.stream));
+        {
+            ProfSpan sp(PK_ENC_REPLAY0, g_.stream);
+            FQZ5_HIP(launch_enc_replay(d_all, d_items, nit, false, lds_r, g_.stream));
+            tk_r0 = sp.end(0);
+        }
         FQZ5_HIP(launch_enc_scan(d_all, int(eall.size()), g_.stream));
+        ProfSpan sp(PK_ENC_REPLAY, g_.stream);
         FQZ5_HIP(launch_enc_replay(d_all, d_items, nit, true, lds_r, g_.stream));
+        tk_r1 = sp.end(0);
     }
     ev.stop(g_.stream);
     const double tc = trace ? now() : 0;
@@ -646,14 +666,22 @@ void Compressor::stage_encode() {
     g_.download(lens.data(), d_lens, jobs_.size());
     g_.sync();
     const double td = trace ? now() : 0;
-    if (ev.on) {
-        const double ms = ev.ms();
-        double bytes = 0;
-        for (int i : order) bytes += double(jobs_[i].n) + lens[i];
-        g_.prof.enc_ms += ms;
-        g_.prof.enc_launches += 1;
-        g_.prof.enc_bytes += bytes;
-        if (prof_on()) prof_add(PK_ENC_CHAIN, ms, bytes);
+    if (ev.on || tk_r1 >= 0) {
+        double bytes = 0, b2w = 0, b1w = 0;
+        for (int i : order) {
+            const double b = double(jobs_[i].n) + lens[i];
+            bytes += b;
+            (enc_chain_2w(jobs_[i].o1, jobs_[i].nx, uint32_t(jobs_[i].A)) ? b2w : b1w) += b;
+        }
+        prof_bytes(tk_2w, b2w);
+        prof_bytes(tk_1w, b1w);
+        prof_bytes(tk_r0, bytes);
+        prof_bytes(tk_r1, bytes);
+        if (ev.on) {
+            g_.prof.enc_ms += ev.ms();
+            g_.prof.enc_launches += 1;
+            g_.prof.enc_bytes += bytes;
+        }
     }
     for (size_t i = 0; i < jobs_.size(); i++) jobs_[i].payload = jobs_[i].n ? lens[i] : 0;
     for (size_t i = nmain; i < jobs_.size(); i++) finish_job(jobs_[i]);

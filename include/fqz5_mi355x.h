@@ -153,13 +153,18 @@ char *fqz5_seq_decode_host(unsigned char *in, unsigned int in_size, unsigned int
                            unsigned int out_size);
 
 /* Where fqz5_decode_sections (fqz5_block.h) runs the adaptive-model chains
- * (fqz quality sections, SEQ10..SEQ14B sequence sections): 0 = on the GPU
- * (default unless $FQZ5_HOST_DECODE is set), 1 = on host cores (up to
- * $FQZ5_HOST_THREADS threads) beside the GPU's rANS, LZP and name work.
- * Output bytes do not depend on it.  Returns the previous setting. */
+ * (fqz quality sections, SEQ10..SEQ14B sequence sections): 0 = on the GPU,
+ * 1 = on host cores (up to $FQZ5_HOST_THREADS threads) beside the GPU's
+ * rANS, LZP and name work, 2 = each chain where its measured cost finishes
+ * the call soonest (the default; $FQZ5_HOST_DECODE overrides it); 3 =
+ * every other chain on host cores (tests of the mixed placement).  Output
+ * bytes do not depend on it.  Returns the previous setting. */
 int fqz5_set_host_decode(int mode);
 /* The host threads that leg uses. */
 int fqz5_host_threads(void);
+/* Adaptive-model chains fqz5_decode_sections placed so far: out2[0] on host
+ * cores, out2[1] on the GPU. */
+void fqz5_decode_chain_counts(uint64_t *out2);
 
 /* ---- CRC32 (zlib crc32, fqzcomp5.c:2268-2269, :2310-2311, :4443, :4670) --- */
 
@@ -291,11 +296,16 @@ uint64_t fqz5_arena_use_peak(int reset);
 void fqz5_profile(int on);
 void fqz5_profile_read(double *out6);
 
-/* The chain kernels of every codec family, from every context of the
+/* The long kernels of every codec family, from every context of the
  * process (helper contexts included) since fqz5_profile(1): per kernel
- * {launch ms, launches, algorithmic bytes} in the order k_enc_chain (rANS
- * encode), k_rans_dec, k_fqz_dec, k_fqz_rc (fqz and sequence-model range
- * chains), k_seq_dec.  Fills min(nk, count) kernels; returns the count. */
+ * {launch ms, launches, algorithmic bytes}, each launch timed by HIP events
+ * around it on its own stream, in the order k_enc_chain (rANS encode, one
+ * wave per chain), k_rans_dec, k_fqz_dec (both fqz decoders), k_fqz_rc (fqz
+ * and sequence-model range chains), k_seq_dec, k_enc_chain2w (rANS encode,
+ * two waves per chain), k_enc_replay (the emitting pass), k_seq_model,
+ * k_fqz_model_hot (with its k_fqz_hot_list), k_fqz_ev_fill, k_lzp_dec,
+ * k_enc_replay (the counting pass).  Fills min(nk, count) kernels; returns
+ * the count. */
 int fqz5_profile_read_all(double *out, int nk);
 
 /* fqz encoder: quality models with at least `min_events` events in a block

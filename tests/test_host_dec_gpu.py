@@ -1,8 +1,11 @@
-"""The block decoder's host-core leg (fqz5_set_host_decode): with the
-adaptive-model chains (fqz quality, SEQ10..SEQ14B sequence sections) on host
-threads beside the GPU's rANS / LZP / name work, every file decodes to the
-same text as the GPU-only decode, at the presets that choose those methods."""
-import numpy as np
+"""Where the block decoder runs its adaptive-model chains (fqz quality,
+SEQ10..SEQ14B sequence sections; fqz5_set_host_decode): every placement — all
+on the GPU (0), all on host threads beside the GPU's rANS / LZP / name work
+(1), by measured cost (2, the default), every other chain on the host (3:
+a GPU sequence chain feeding a host quality chain and the reverse) — decodes
+every file to its text, at the presets that choose those methods."""
+import ctypes as C
+
 import pytest
 
 from fqzcomp5_amd import fqz5file, lib, synth
@@ -23,21 +26,35 @@ def _text(kind, n):
     return synth.fastq_chunk(r, 0, r.num_records).tobytes()
 
 
+def _chains(so):
+    c = (C.c_uint64 * 2)()
+    so.fqz5_decode_chain_counts(c)
+    return int(c[0]), int(c[1])
+
+
 @pytest.mark.parametrize("kind,level", [("illumina", 5), ("novaseq", 5), ("illumina", 7),
                                         ("ont", 7), ("illumina", 9)])
-def test_host_leg_equals_gpu(kind, level):
+def test_every_placement_decodes(kind, level):
     text = _text(kind, 6000)
     z = fqz5file.compress_bytes(text, level, blk_size=300_000)
     so = lib.load()
-    prev = so.fqz5_set_host_decode(1)
+    prev = so.fqz5_set_host_decode(2)
     try:
-        host = fqz5file.decompress_bytes(z)
+        for mode in (0, 1, 2, 3):
+            so.fqz5_set_host_decode(mode)
+            h0, g0 = _chains(so)
+            assert fqz5file.decompress_bytes(z) == text, mode
+            h1, g1 = _chains(so)
+            if mode == 0:
+                assert h1 == h0
+            if mode == 1:
+                assert g1 == g0
     finally:
         so.fqz5_set_host_decode(prev)
-    so.fqz5_set_host_decode(0)
-    try:
-        gpu = fqz5file.decompress_bytes(z)
-    finally:
-        so.fqz5_set_host_decode(prev)
-    assert host == text
-    assert gpu == text
+
+
+def test_default_is_cost_model():
+    so = lib.load()
+    prev = so.fqz5_set_host_decode(2)
+    so.fqz5_set_host_decode(prev)
+    assert prev == 2
