@@ -126,6 +126,7 @@ __global__ void k_fq_records(const uint8_t *t, const uint64_t *nl, uint64_t nrec
     R.seq_len = uint32_t(strip_cr(t, s1, e1) - s1);
     R.qual = s3;
     R.fasta = 0;
+    R.end = e3 + 1;
     const uint32_t ql = uint32_t(strip_cr(t, s3, e3) - s3);
     if (ql != R.seq_len) bad = 1;                     // kseq -2 (:213-216)
     recs[r] = R;
@@ -195,8 +196,163 @@ __global__ void k_fa_records(const uint8_t *t, uint64_t len, const uint64_t *nl,
         R.qual = se;
         R.seq_len = n;
         R.fasta = 1;
+        R.end = se;
         recs[r] = R;
         rec_size[r] = R.name_len + 1 + n;             // qual.l = 0 (:472)
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Wrapped (multi-line) FASTQ, as kseq_read reads it (kseq.h:194-216): after
+// the header, sequence lines up to a line starting with '+' (empty lines
+// skipped; a line starting with '@' or '>' would end the record without
+// qualities), then quality lines until their bytes reach the sequence's
+// length.  The record that starts at a '@' line is fixed by the lines after
+// it alone, so every '@' line is tried as a header in parallel (its '+' line,
+// sequence length and last quality line by binary searches over the line
+// tables) and yields the '@' line the next record would start at; the true
+// records are the chain of those links from line 0, walked on the host over
+// one int per '@' line.  Lines: `cls` the first byte (0 empty, 1 a lone
+// '\r'), `ls` the bytes kseq keeps (a trailing '\r' dropped, KS_SEP_LINE
+// :141), P their prefix sums.  Refused (never guessed): a record without a
+// '+' line, qualities longer than the bases, a lone-'\r' line before the
+// first kept byte of a sequence or quality block (kseq keeps that '\r'),
+// bytes other than empty lines between records.
+// ---------------------------------------------------------------------------
+constexpr int32_t ML_END = -1, ML_MORE = -2, ML_BAD = -3;
+
+__global__ void k_ml_lines(const uint8_t *t, const uint64_t *nl, uint64_t nlines, uint8_t *cls,
+                           uint32_t *ls, uint32_t *f_at, uint32_t *f_stop, uint32_t *f_cr) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= nlines) return;
+    const uint64_t s = i ? nl[i - 1] + 1 : 0, e = nl[i];
+    const uint64_t L = e - s;
+    uint8_t c = L ? t[s] : uint8_t(0);
+    const bool cr = L && t[e - 1] == '\r';
+    if (L == 1 && cr) c = 1;
+    cls[i] = c;
+    ls[i] = uint32_t(L - (cr ? 1 : 0));
+    f_at[i] = c == '@';
+    f_stop[i] = c == '@' || c == '+' || c == '>';
+    f_cr[i] = c == 1;
+}
+
+__global__ void k_ends4(const uint64_t *nl, uint64_t n4, uint64_t len, uint64_t *ends) {
+    const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (r < n4) ends[r] = nl[4 * r + 3] + 1 < len ? nl[4 * r + 3] + 1 : len;
+}
+
+__global__ void k_widen(const uint32_t *in, uint64_t *out, uint64_t n) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+
+__global__ void k_ml_scatter(const uint32_t *flag, const uint32_t *pos, uint64_t n, uint32_t *list) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n && flag[i]) list[pos[i]] = uint32_t(i);
+}
+
+// first index of sorted a[0..n) with a[i] >= x (n if none)
+__device__ __forceinline__ uint32_t lower_u32(const uint32_t *a, uint32_t n, uint32_t x) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (a[m] < x) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
+// '@' line ats[a] taken as a header: next[a] = the '@' index of the next
+// record (ML_END: none, the rest empty; ML_MORE: the text ends inside the
+// record and more is coming; ML_BAD: not a record kseq reads the same way)
+// a lone-'\r' line in the block of lines [a, b) before any kept byte: kseq
+// would keep that '\r' (its strip needs two bytes, kseq.h:141)
+__device__ __forceinline__ bool lone_cr_first(const uint64_t *P, const uint32_t *crs, uint32_t ncr,
+                                              uint32_t a, uint32_t b) {
+    const uint32_t i = lower_u32(crs, ncr, a);
+    return i < ncr && crs[i] < b && P[crs[i]] == P[a];
+}
+
+__global__ void k_ml_cand(const uint8_t *cls, const uint64_t *P, const uint32_t *crs, uint32_t ncr,
+                          uint32_t nlines, const uint32_t *ats, uint32_t nat, const uint32_t *stops,
+                          uint32_t nst, int eof, int32_t *next, uint32_t *jq, uint32_t *kq,
+                          uint32_t *slen) {
+    const uint32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= nat) return;
+    const uint32_t h = ats[a];
+    const int32_t short_ = eof ? ML_BAD : ML_MORE;
+    int32_t r = ML_BAD;
+    uint32_t j = 0, k = 0, sl = 0;
+    do {
+        const uint32_t js = lower_u32(stops, nst, h + 1);
+        if (js >= nst) { r = short_; break; }            // no '+' line yet
+        j = stops[js];
+        if (cls[j] != '+') break;                         // a record without qualities
+        const uint64_t seq_len = P[j] - P[h + 1];
+        if (seq_len > 0xffffffffull || lone_cr_first(P, crs, ncr, h + 1, j)) break;
+        sl = uint32_t(seq_len);
+        if (j + 1 >= nlines) { r = short_; break; }       // no quality line yet
+        const uint64_t base = P[j + 1];
+        // the smallest k >= j + 1 with P[k + 1] - base >= seq_len
+        uint32_t lo = j + 1, hi = nlines;
+        while (lo < hi) {
+            const uint32_t m = lo + ((hi - lo) >> 1);
+            if (P[m + 1] - base >= seq_len) hi = m; else lo = m + 1;
+        }
+        if (lo >= nlines) { r = short_; break; }
+        k = lo;
+        if (P[k + 1] - base != seq_len || lone_cr_first(P, crs, ncr, j + 1, k + 1)) break;   // kseq -2
+        const uint32_t an = lower_u32(ats, nat, k + 1);
+        const uint32_t stop = an < nat ? ats[an] : nlines;
+        if (P[stop] != P[k + 1]) { r = an < nat ? ML_BAD : short_; break; }   // bytes between records
+        r = an < nat ? int32_t(an) : (eof ? ML_END : ML_MORE);
+    } while (false);
+    next[a] = r;
+    jq[a] = j;
+    kq[a] = k;
+    slen[a] = sl;
+}
+
+// record r of the chain: header line, first sequence line, first quality line
+__global__ void k_ml_records(const uint8_t *t, uint64_t len, const uint64_t *nl, uint32_t nlines,
+                             const uint32_t *chain, uint64_t nrec, const uint32_t *ats, const uint32_t *jq,
+                             const uint32_t *kq, const uint32_t *slen, fqz5_fastq_rec *recs,
+                             uint32_t *rec_size, uint64_t *ends) {
+    const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    const uint32_t a = chain[r], h = ats[a], j = jq[a], k = kq[a];
+    const uint64_t s0 = h ? nl[h - 1] + 1 : 0, e0 = nl[h];
+    fqz5_fastq_rec R;
+    header(t, s0, e0, R);
+    R.seq = e0 + 1 < len ? e0 + 1 : len;
+    R.qual = nl[j] + 1 < len ? nl[j] + 1 : len;
+    R.seq_len = slen[a];
+    R.fasta = 2;
+    R.end = nl[k] + 1 < len ? nl[k] + 1 : len;
+    if (recs) recs[r] = R;
+    if (rec_size) rec_size[r] = R.name_len + 1 + 2 * R.seq_len;   // (:472)
+    if (ends) ends[r] = R.end;
+    (void)nlines;
+}
+
+// kseq's joined lines (kseq.h:194-198, :213): n kept bytes from text offset
+// s on, every '\n' and a '\r' before a '\n' skipped.  One wave; sub: 33 for
+// qualities.
+__device__ void ml_copy(const uint8_t *t, uint64_t tlen, uint64_t s, uint32_t n, uint8_t *out,
+                        uint8_t sub) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint32_t w = 0;
+    for (uint64_t base = s; w < n && base < tlen; base += 64) {
+        const uint64_t p = base + lane;
+        const bool in = p < tlen;
+        const uint8_t c = in ? t[p] : uint8_t('\n');
+        const uint8_t c1 = p + 1 < tlen ? t[p + 1] : uint8_t(0);
+        const bool keep = in && c != '\n' && !(c == '\r' && c1 == '\n');
+        const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
+        const uint32_t at = w + uint32_t(__builtin_popcountll(km & below));
+        if (keep && at < n) out[at] = uint8_t(c - sub);
+        w += uint32_t(__builtin_popcountll(km));
     }
 }
 
@@ -229,11 +385,16 @@ __global__ void k_fq_gather(const uint8_t *t, const fqz5_fastq_rec *recs, uint64
     }
     if (lane == 0) o[w] = 0;
     uint8_t *so = seq + soff[k];
-    if (R.fasta) {                                    // lines joined (fa_seq)
+    if (R.fasta == 1) {                               // lines joined (fa_seq)
         fa_seq(t, R.seq, R.qual, so);
         return;
     }
     uint8_t *qo = qual + soff[k];
+    if (R.fasta == 2) {                               // wrapped FASTQ: lines joined
+        ml_copy(t, R.end, R.seq, R.seq_len, so, 0);
+        ml_copy(t, R.end, R.qual, R.seq_len, qo, 33);
+        return;
+    }
     for (uint32_t i = lane; i < R.seq_len; i += 64) {
         so[i] = t[R.seq + i];
         qo[i] = uint8_t(t[R.qual + i] - 33);
@@ -332,6 +493,165 @@ template <class T> void excl_sum(GpuCtx &g, const T *in, T *out, uint64_t n) {
     FQZ5_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, int(n), g.stream));
     void *tmp = g.arena.alloc_n<uint8_t>(tb ? tb : 1);
     FQZ5_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, int(n), g.stream));
+}
+
+// Wrapped-FASTQ records of the text whose lines end at lines[0..nlines)
+// (see k_ml_cand): the records into d_recs (device, may be NULL) with their
+// sizes (h_rec_size, host, may be NULL) and text ends (h_ends, may be NULL);
+// returns their number.  eof: the text ends the input (else a record it cuts
+// off is left out).  Throws on text kseq would not read as these records.
+uint64_t ml_index(GpuCtx &g, const uint8_t *d_text, uint64_t len, const uint64_t *lines, uint64_t nlines,
+                  int eof, fqz5_fastq_rec *d_recs, uint64_t max_rec, uint32_t *h_rec_size,
+                  std::vector<uint64_t> *h_ends) {
+    if (nlines >= (1ull << 31)) throw GpuError("fastq: too many lines");
+    const uint32_t n = uint32_t(nlines);
+    if (!n) return 0;
+    uint8_t *cls = g.arena.alloc_n<uint8_t>(size_t(n) + 1);
+    uint32_t *ls = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
+    uint32_t *fa = g.arena.alloc_n<uint32_t>(size_t(n) + 1), *fs = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
+    uint32_t *fc = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
+    hipLaunchKernelGGL(k_ml_lines, grid_for(n, 256), dim3(256), 0, g.stream, d_text, lines, nlines, cls, ls,
+                       fa, fs, fc);
+    FQZ5_HIP(hipGetLastError());
+    g.memset0(ls + n, 4);
+    g.memset0(fa + n, 4);
+    g.memset0(fs + n, 4);
+    g.memset0(fc + n, 4);
+    // P: kept bytes before each line (u64: widened first)
+    uint64_t *ls64 = g.arena.alloc_n<uint64_t>(size_t(n) + 1);
+    uint64_t *P = g.arena.alloc_n<uint64_t>(size_t(n) + 2);
+    hipLaunchKernelGGL(k_widen, grid_for(uint64_t(n) + 1, 256), dim3(256), 0, g.stream, ls, ls64, uint64_t(n) + 1);
+    FQZ5_HIP(hipGetLastError());
+    excl_sum(g, ls64, P, uint64_t(n) + 1);
+    uint32_t *pa = g.arena.alloc_n<uint32_t>(size_t(n) + 1), *ps = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
+    uint32_t *pc = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
+    excl_sum(g, fa, pa, uint64_t(n) + 1);
+    excl_sum(g, fs, ps, uint64_t(n) + 1);
+    excl_sum(g, fc, pc, uint64_t(n) + 1);
+    uint32_t cnt[3] = {0, 0, 0};
+    g.download(&cnt[0], pa + n, 1);
+    g.download(&cnt[1], ps + n, 1);
+    g.download(&cnt[2], pc + n, 1);
+    g.sync();
+    const uint32_t nat = cnt[0], nst = cnt[1], ncr = cnt[2];
+    uint32_t *ats = g.arena.alloc_n<uint32_t>(size_t(nat) + 1), *stops = g.arena.alloc_n<uint32_t>(size_t(nst) + 1);
+    uint32_t *crs = g.arena.alloc_n<uint32_t>(size_t(ncr) + 1);
+    hipLaunchKernelGGL(k_ml_scatter, grid_for(n, 256), dim3(256), 0, g.stream, fa, pa, uint64_t(n), ats);
+    hipLaunchKernelGGL(k_ml_scatter, grid_for(n, 256), dim3(256), 0, g.stream, fs, ps, uint64_t(n), stops);
+    hipLaunchKernelGGL(k_ml_scatter, grid_for(n, 256), dim3(256), 0, g.stream, fc, pc, uint64_t(n), crs);
+    FQZ5_HIP(hipGetLastError());
+    if (!nat) {                            // no header: only empty lines are no records
+        uint64_t tot = 0;
+        g.download(&tot, P + n, 1);
+        g.sync();
+        if (tot) throw GpuError("fastq: text without a FASTQ header line");
+        return 0;
+    }
+    int32_t *nx = g.arena.alloc_n<int32_t>(nat);
+    uint32_t *jq = g.arena.alloc_n<uint32_t>(nat), *kq = g.arena.alloc_n<uint32_t>(nat);
+    uint32_t *sl = g.arena.alloc_n<uint32_t>(nat);
+    hipLaunchKernelGGL(k_ml_cand, grid_for(nat, 256), dim3(256), 0, g.stream, cls, P, crs, ncr, n, ats, nat,
+                       stops, nst, eof, nx, jq, kq, sl);
+    FQZ5_HIP(hipGetLastError());
+    std::vector<int32_t> hn(nat);
+    uint32_t a0 = 0;
+    uint64_t before = 0;
+    g.download(hn.data(), nx, nat);
+    g.download(&a0, ats, 1);
+    g.sync();
+    g.download(&before, P + a0, 1);
+    g.sync();
+    if (before) throw GpuError("fastq: text before the first FASTQ header line");
+    // the records: the chain of next-header links from the first '@' line
+    std::vector<uint32_t> chain;
+    for (uint32_t a = 0;;) {
+        chain.push_back(a);
+        const int32_t r = hn[a];
+        if (r >= 0) {
+            if (uint32_t(r) <= a) throw GpuError("fastq: record chain does not advance");
+            a = uint32_t(r);
+            continue;
+        }
+        if (r == ML_END) break;
+        if (r == ML_MORE && !eof) {
+            chain.pop_back();
+            break;
+        }
+        char msg[160];
+        std::snprintf(msg, sizeof msg, "fastq: record %zu is not a FASTQ record kseq reads (a record without "
+                      "a '+' line, qualities longer than the bases, or bytes between records)",
+                      chain.size() - 1);
+        throw GpuError(msg);
+    }
+    const uint64_t nrec = chain.size();
+    if (d_recs && nrec > max_rec) throw GpuError("fastq: more records than max_rec");
+    if (!nrec) return 0;
+    const uint32_t *d_chain = g.upload(chain);
+    uint32_t *rs = h_rec_size ? g.arena.alloc_n<uint32_t>(nrec) : nullptr;
+    uint64_t *ends = h_ends ? g.arena.alloc_n<uint64_t>(nrec) : nullptr;
+    hipLaunchKernelGGL(k_ml_records, grid_for(nrec, 256), dim3(256), 0, g.stream, d_text, len, lines, n, d_chain,
+                       nrec, ats, jq, kq, sl, d_recs, rs, ends);
+    FQZ5_HIP(hipGetLastError());
+    if (rs) g.download(h_rec_size, rs, nrec);
+    if (ends) {
+        h_ends->resize(size_t(nrec));
+        g.download(h_ends->data(), ends, nrec);
+    }
+    g.sync();
+    return nrec;
+}
+
+// lines of d_text (newline positions, plus the text end when the text does
+// not end in '\n' and `eof`); *nlines receives their count
+uint64_t *text_lines(GpuCtx &g, const uint8_t *d_text, uint64_t len, bool eof, uint64_t *nlines) {
+    uint64_t nn = 0;
+    uint64_t *nl = find_delims(g, d_text, len, '\n', &nn);
+    uint8_t last = '\n';
+    if (len) {
+        g.download(&last, d_text + len - 1, 1);
+        g.sync();
+    }
+    *nlines = nn;
+    if (!(eof && len && last != '\n')) return nl;
+    uint64_t *lines = g.arena.alloc_n<uint64_t>(size_t(nn) + 1);
+    if (nn) FQZ5_HIP(hipMemcpyAsync(lines, nl, nn * 8, hipMemcpyDeviceToDevice, g.stream));
+    uint64_t *st = reinterpret_cast<uint64_t *>(g.staging.alloc(8));
+    *st = len;
+    FQZ5_HIP(hipMemcpyAsync(lines + nn, st, 8, hipMemcpyHostToDevice, g.stream));
+    *nlines = nn + 1;
+    return lines;
+}
+
+// 4-line FASTQ check of the complete groups of lines: records into d_recs
+// (scratch when NULL); true when every group is a 4-line record and (eof)
+// the lines after them are empty
+bool four_line(GpuCtx &g, const uint8_t *d_text, const uint64_t *lines, uint64_t nlines, bool eof,
+               fqz5_fastq_rec *d_recs, uint32_t *rs, uint64_t *n4out) {
+    const uint64_t n4 = nlines / 4;
+    *n4out = n4;
+    if (eof && nlines % 4) {
+        std::vector<uint64_t> tail(size_t(nlines % 4) + 1);
+        const uint64_t first = n4 * 4;
+        g.download(tail.data() + 1, lines + first, nlines - first);
+        if (first) g.download(tail.data(), lines + first - 1, 1);
+        g.sync();
+        uint64_t prev = first ? tail[0] : uint64_t(-1);
+        for (uint64_t k = 1; k <= nlines - first; k++) {
+            if (tail[k] != prev + 1) return false;
+            prev = tail[k];
+        }
+    }
+    if (!n4) return true;
+    if (!d_recs) d_recs = g.arena.alloc_n<fqz5_fastq_rec>(size_t(n4));
+    if (!rs) rs = g.arena.alloc_n<uint32_t>(size_t(n4));
+    int32_t *st = g.arena.alloc_n<int32_t>(1);
+    g.memset0(st, 4);
+    hipLaunchKernelGGL(k_fq_records, grid_for(n4, 256), dim3(256), 0, g.stream, d_text, lines, n4, d_recs, rs, st);
+    FQZ5_HIP(hipGetLastError());
+    int32_t status = 0;
+    g.download(&status, st, 1);
+    g.sync();
+    return status >= 0;
 }
 
 }  // namespace
@@ -437,6 +757,70 @@ int fqz5_fastq_index(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs
         *nrec = n4;
         g.reset();
         return fasta ? 1 : 0;
+    } catch (const std::exception &e) {
+        fqz5_set_error(e.what());
+        try { if (gp) gp->reset(); } catch (...) {}
+        return -1;
+    }
+}
+
+int fqz5_fastq_index_any(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs,
+                         uint64_t max_rec, uint64_t *nrec, uint32_t *h_rec_size) {
+    const int r = fqz5_fastq_index(d_text, len, d_recs, max_rec, nrec, h_rec_size);
+    if (r >= 0) return r;
+    // not FASTA, not 4-line FASTQ: kseq's wrapped records
+    GpuCtx *gp = nullptr;
+    try {
+        GpuCtx &g = gpu();
+        gp = &g;
+        uint8_t first_byte = 0;
+        if (len) {
+            g.download(&first_byte, d_text, 1);
+            g.sync();
+        }
+        if (first_byte == '>') return -1;       // (FASTA's own error stands)
+        uint64_t nlines = 0;
+        const uint64_t *lines = text_lines(g, d_text, len, true, &nlines);
+        *nrec = ml_index(g, d_text, len, lines, nlines, 1, d_recs, max_rec, h_rec_size, nullptr);
+        g.reset();
+        return 0;
+    } catch (const std::exception &e) {
+        fqz5_set_error(e.what());
+        try { if (gp) gp->reset(); } catch (...) {}
+        return -1;
+    }
+}
+
+int fqz5_fastq_record_ends(const uint8_t *d_text, uint64_t len, int eof, uint64_t *h_ends,
+                           uint64_t max_ends, uint64_t *n_ends) {
+    GpuCtx *gp = nullptr;
+    try {
+        GpuCtx &g = gpu();
+        gp = &g;
+        *n_ends = 0;
+        uint64_t nlines = 0;
+        const uint64_t *lines = text_lines(g, d_text, len, eof != 0, &nlines);
+        std::vector<uint64_t> ends;
+        uint64_t n4 = 0;
+        if (four_line(g, d_text, lines, nlines, eof != 0, nullptr, nullptr, &n4)) {
+            // record r ends after line 4r + 3 (load_seqs_kseq's 4-line records)
+            ends.resize(size_t(n4));
+            if (n4) {
+                uint64_t *e = g.arena.alloc_n<uint64_t>(size_t(n4));
+                hipLaunchKernelGGL(k_ends4, grid_for(n4, 256), dim3(256), 0, g.stream, lines, n4, len, e);
+                FQZ5_HIP(hipGetLastError());
+                g.download(ends.data(), e, n4);
+                g.sync();
+            }
+        } else {
+            ml_index(g, d_text, len, lines, nlines, eof, nullptr, 0, nullptr, &ends);
+        }
+        if (eof && len && (ends.empty() || ends.back() != len)) ends.push_back(len);
+        if (ends.size() > max_ends) throw GpuError("fastq: more records than max_ends");
+        std::memcpy(h_ends, ends.data(), ends.size() * 8);
+        *n_ends = ends.size();
+        g.reset();
+        return 0;
     } catch (const std::exception &e) {
         fqz5_set_error(e.what());
         try { if (gp) gp->reset(); } catch (...) {}

@@ -43,7 +43,7 @@ class FastqRec(C.Structure):
     """fqz5_fastq_rec (include/fqz5_fastq.h)"""
     _fields_ = [("name", C.c_uint64), ("comment", C.c_uint64), ("seq", C.c_uint64),
                 ("qual", C.c_uint64), ("name_len", C.c_uint32), ("comment_len", C.c_uint32),
-                ("seq_len", C.c_uint32), ("fasta", C.c_uint32)]
+                ("seq_len", C.c_uint32), ("fasta", C.c_uint32), ("end", C.c_uint64)]
 
 
 _bound = False
@@ -56,6 +56,11 @@ def _load():
         so.fqz5_fastq_index.restype = C.c_int
         so.fqz5_fastq_index.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                         C.POINTER(C.c_uint64), C.c_void_p]
+        so.fqz5_fastq_index_any.restype = C.c_int
+        so.fqz5_fastq_index_any.argtypes = so.fqz5_fastq_index.argtypes
+        so.fqz5_fastq_record_ends.restype = C.c_int
+        so.fqz5_fastq_record_ends.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_void_p,
+                                              C.c_uint64, C.POINTER(C.c_uint64)]
         so.fqz5_fastq_blocks.restype = C.c_int
         so.fqz5_fastq_blocks.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_int]
         so.fqz5_fastq_gather.restype = C.c_int
@@ -79,26 +84,30 @@ def _check(rc, what):
     return rc
 
 
-def _index_text(text_d, at: int, n: int):
+def _index_text(text_d, at: int, n: int, wrapped: bool = False):
     """fqz5_fastq_index of text_d[at:at+n]: (records as bytes on the
-    device, their load_seqs_kseq sizes, count, is FASTA)."""
+    device, their load_seqs_kseq sizes, count, is FASTA).  wrapped: any
+    layout kseq reads, wrapped FASTQ included (fqz5_fastq_index_any; the
+    multi-rank windows, which count records in lines, keep 4-line FASTQ)."""
     import torch
     so = _load()
     part = text_d[at:at + n]
-    # records <= lines / 4, FASTA records <= lines (+1 for a last line
-    # without '\n')
-    lpr = 1 if n and int(part[0].item()) == ord(">") else 4
+    # records <= lines / 4 (wrapped: / 3, a record without bases), FASTA
+    # records <= lines (+1 for a last line without '\n')
+    lpr = 1 if n and int(part[0].item()) == ord(">") else (3 if wrapped else 4)
     max_rec = (int((part == 10).sum().item()) + 1) // lpr + 1 if n else 1
     recs = torch.empty(max_rec * C.sizeof(FastqRec), dtype=torch.uint8, device=text_d.device)
     rsz = np.zeros(max_rec, np.uint32)
     nrec = C.c_uint64(0)
     _lib.after_torch()
-    fasta = _check(so.fqz5_fastq_index(text_d.data_ptr() + at, n, recs.data_ptr(), max_rec,
-                                       C.byref(nrec), rsz.ctypes.data), "fqz5_fastq_index") == 1
+    fn = so.fqz5_fastq_index_any if wrapped else so.fqz5_fastq_index
+    fasta = _check(fn(text_d.data_ptr() + at, n, recs.data_ptr(), max_rec,
+                      C.byref(nrec), rsz.ctypes.data), "fqz5_fastq_index") == 1
     nrec = int(nrec.value)
     if at and nrec:                     # offsets into the whole text
         v = recs[:nrec * C.sizeof(FastqRec)].view(torch.int64).view(nrec, -1)
         v[:, :4] += at
+        v[:, 6] += at                   # (end)
     return recs[:nrec * C.sizeof(FastqRec)], rsz[:nrec], nrec, fasta
 
 
@@ -144,7 +153,7 @@ def parse_fastq(text_d, blk_size: int):
     its blocks, every section input gathered in HBM.  FASTA blocks have no
     quality section (fqzcomp5.c:2237-2264)."""
     so = _load()
-    recs, rsz, nrec, fasta = _index_text(text_d, 0, int(text_d.numel()))
+    recs, rsz, nrec, fasta = _index_text(text_d, 0, int(text_d.numel()), wrapped=True)
     run = _gather(text_d, recs, _blocks(so, rsz, blk_size), fasta, False)
     del recs
     return run
@@ -158,8 +167,8 @@ def parse_paired(text_d, len1: int, blk_size: int):
     R2 ending before R1 is an error; R2 records past R1's end are not read."""
     import torch
     so = _load()
-    r1, rs1, n1, fa1 = _index_text(text_d, 0, len1)
-    r2, rs2, n2, fa2 = _index_text(text_d, len1, int(text_d.numel()) - len1)
+    r1, rs1, n1, fa1 = _index_text(text_d, 0, len1, wrapped=True)
+    r2, rs2, n2, fa2 = _index_text(text_d, len1, int(text_d.numel()) - len1, wrapped=True)
     if n2 < n1:
         raise _lib.NativeError("unpaired read detected: R2 file ended before R1")
     if n1 and fa1 != fa2:
@@ -331,8 +340,14 @@ def _complete_records(text_d, n: int, eof: bool) -> tuple[list[int], bool]:
         starts = ((t[1:] == ord(">")) & (t[:-1] == 10)).nonzero().flatten() + 1
         ends = starts.cpu().tolist()
     else:
-        nl = (t == 10).nonzero().flatten()
-        ends = (nl[3::4] + 1).cpu().tolist()
+        # 4-line records, or kseq's wrapped ones (fqz5_fastq_record_ends)
+        cap = int((t == 10).sum().item()) // 3 + 2
+        buf = np.zeros(cap, np.uint64)
+        cnt = C.c_uint64(0)
+        _lib.after_torch()
+        _check(_load().fqz5_fastq_record_ends(text_d.data_ptr(), n, int(bool(eof)), buf.ctypes.data,
+                                              cap, C.byref(cnt)), "fqz5_fastq_record_ends")
+        ends = buf[:int(cnt.value)].tolist()
     if eof and (not ends or ends[-1] != n):
         ends.append(n)
     del torch
@@ -391,11 +406,11 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
             text_d, len1 = devs[0][:cut[0]], None
         del devs
         if len1 is None:
-            recs, rsz, nrec, fasta = _index_text(text_d, 0, int(text_d.numel()))
+            recs, rsz, nrec, fasta = _index_text(text_d, 0, int(text_d.numel()), wrapped=True)
             first = _blocks(so, rsz, blk)
         else:
-            r1, rs1, n1, fa1 = _index_text(text_d, 0, len1)
-            r2, rs2, n2, fa2 = _index_text(text_d, len1, int(text_d.numel()) - len1)
+            r1, rs1, n1, fa1 = _index_text(text_d, 0, len1, wrapped=True)
+            r2, rs2, n2, fa2 = _index_text(text_d, len1, int(text_d.numel()) - len1, wrapped=True)
             if n2 < n1:
                 raise _lib.NativeError("unpaired read detected: R2 file ended before R1")
             if n1 and fa1 != fa2:

@@ -41,7 +41,10 @@ typedef struct {                  /* one record of the text */
     uint64_t name, comment, seq, qual;        /* offsets */
     uint32_t name_len, comment_len, seq_len;  /* kseq's name.l, comment.l, seq.l */
     uint32_t fasta;                           /* 1: FASTA, its sequence lines
-                                                 in [seq, qual) */
+                                                 in [seq, qual); 2: wrapped
+                                                 FASTQ, sequence and quality
+                                                 lines from seq and qual */
+    uint64_t end;                             /* the record's text end */
 } fqz5_fastq_rec;
 
 /* Index the records of d_text[0..len) (device) into d_recs (device, max_rec
@@ -50,6 +53,21 @@ typedef struct {                  /* one record of the text */
  * load_seqs_kseq size. */
 int fqz5_fastq_index(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs,
                      uint64_t max_rec, uint64_t *nrec, uint32_t *h_rec_size);
+
+/* fqz5_fastq_index for every layout kseq_read reads (kseq.h:178-218): 4-line
+ * FASTQ, FASTA, and wrapped FASTQ (sequence and quality split over several
+ * lines each; records with fasta = 2).  fqz5_fastq_index itself takes 4-line
+ * FASTQ and FASTA only (the multi-GPU windows count records in lines). */
+int fqz5_fastq_index_any(const uint8_t *d_text, uint64_t len, fqz5_fastq_rec *d_recs,
+                         uint64_t max_rec, uint64_t *nrec, uint32_t *h_rec_size);
+
+/* The ends (exclusive text offsets, increasing) of the complete FASTQ
+ * records of d_text[0..len) (device; 4-line or wrapped): a record that the
+ * text cuts off is left out unless eof (then the text end closes the last
+ * one).  h_ends (host) holds up to max_ends; *n_ends receives the count.
+ * Returns 0, or -1 on text that is not FASTQ kseq reads the same way. */
+int fqz5_fastq_record_ends(const uint8_t *d_text, uint64_t len, int eof, uint64_t *h_ends,
+                           uint64_t max_ends, uint64_t *n_ends);
 
 /* Block starts (host): first[k] = the first record of block k, first[n] =
  * nrec.  Returns n, or -1 when more than max_blocks. */

@@ -82,10 +82,15 @@ def test_crlf_and_no_final_newline(tmp_path):
         assert fqz5file.compress_bytes(t, 3) == want
 
 
-def test_not_4line_fastq_fails_loudly():
-    bad = b"@r1\nACGT\nACGT\n+\nIIIIIIII\n"            # a two-line sequence
-    with pytest.raises(lib.NativeError):
-        fqz5file.compress_bytes(bad, 3)
+def test_not_fastq_fails_loudly():
+    """Text kseq_read refuses (kseq.h:212-216: -2) is refused; wrapped FASTQ
+    is read (tests/test_wrapped_fastq_gpu.py)."""
+    for bad in (b"@r1\nACGT\n+\nIII\n",                  # qualities short (EOF)
+                b"@r1\nACGT\n+\nIIIII\n@r2\nA\n+\nI\n",   # qualities long
+                b"@r1\nAC\nGT\n+\nII\n@r2\nA\n+\nI\n",   # wrapped, one quality short
+                b"@r1\nACGT\n+\nIIII\nxx\n@r2\nA\n+\nI\n"):   # bytes between records
+        with pytest.raises(lib.NativeError):
+            fqz5file.compress_bytes(bad, 3)
     with pytest.raises(lib.NativeError):                  # FASTQ record in FASTA text
         fqz5file.compress_bytes(b">r1\nACGT\n@r2\nAC\n+\nII\n", 3)
     with pytest.raises(lib.NativeError):                  # a '+' line in FASTA text

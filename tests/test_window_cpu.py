@@ -7,7 +7,7 @@ sections.encode_window), on the CPU.
   the trial sections' work candidates (fqz, sequence models, LZP3) are split
   over the ranks by method and each is tried exactly once, and the collective
   is the only exchange (fqzcomp5.c:1899-1958 trial, :3108-3115 offsets).
-* the window cut rule (_complete_records) on FASTQ and FASTA text.
+* the window cut rule (_complete_records) on FASTA text.
 * the .fqz5 reader's checks: truncated files and blocks whose sizes disagree
   are refused on the host, before any device work.
 """
@@ -173,12 +173,8 @@ def test_work_share_partitions_methods():
 
 
 def test_window_cut_rules():
-    fq = b"@a\nAC\n+\nII\n@b\nGT\n+\nII\n@c\nA"
-    t = torch.frombuffer(bytearray(fq), dtype=torch.uint8)
-    ends, fa = fqz5file._complete_records(t, len(fq), False)
-    assert not fa and ends == [11, 22]
-    ends, _ = fqz5file._complete_records(t, len(fq), True)
-    assert ends == [11, 22, len(fq)]
+    """FASTA on the host (the FASTQ rule runs on the GPU:
+    test_wrapped_fastq_gpu.py::test_record_ends)."""
     fa_txt = b">x\nACGT\nAC\n>y 1\nGG\n\n>z\nT"
     t = torch.frombuffer(bytearray(fa_txt), dtype=torch.uint8)
     ends, fa = fqz5file._complete_records(t, len(fa_txt), False)

@@ -1,0 +1,69 @@
+"""Wrapped (multi-line) FASTQ through the GPU file path, as kseq_read reads
+it (kseq.h:194-216; fastq.hip's parallel record chain, fqz5_fastq_index_any
+and fqz5_fastq_record_ends): for each case of tests/wrapped_cases.py the
+.fqz5 equals the reference CLI's (-t1, 1 MB blocks; md5s in
+tests/golden/wrapped.json, made by tests/golden/make_wrapped.py) at -1, -3
+and -5, and decoding it gives the CLI's -d text (4-line records).  Also:
+small windows cut inside wrapped records, the window cut rule on 4-line and
+wrapped text, and text kseq refuses."""
+import hashlib
+import json
+import os
+
+import pytest
+import torch
+
+from fqzcomp5_amd import fqz5file, lib
+from wrapped_cases import CASES
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "wrapped.json")))
+md5 = lambda b: hashlib.md5(b).hexdigest()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need():
+    if not lib.device_ok():
+        pytest.fail("no GPU: " + lib.last_error())
+
+
+@pytest.fixture(scope="module")
+def texts():
+    return {k: f() for k, f in CASES.items()}
+
+
+@pytest.mark.parametrize("g", GOLD, ids=[f"{g['case']}-{g['level']}" for g in GOLD])
+def test_wrapped_vs_reference(texts, g):
+    text = texts[g["case"]]
+    assert md5(text) == g["fastq_md5"]
+    z = fqz5file.compress_bytes(text, g["level"], blk_size=1_000_000)
+    assert (len(z), md5(z)) == (g["fqz5_len"], g["fqz5_md5"])
+    back = fqz5file.decompress_bytes(z)
+    assert (len(back), md5(back)) == (g["dec_len"], g["dec_md5"])
+
+
+def test_wrapped_small_windows(texts, tmp_path):
+    """compress_file with windows far smaller than a block: every window cut
+    falls inside wrapped records and must move to a record end."""
+    g = next(x for x in GOLD if x["case"] == "illumina70" and x["level"] == 3)
+    src, dst = str(tmp_path / "w.fastq"), str(tmp_path / "w.fqz5")
+    open(src, "wb").write(texts["illumina70"])
+    fqz5file.compress_file(src, dst, 3, blk_size=1_000_000, window_bytes=300_001)
+    assert md5(open(dst, "rb").read()) == g["fqz5_md5"]
+
+
+def test_record_ends():
+    fq = b"@a\nAC\n+\nII\n@b\nGT\n+\nII\n@c\nA"
+    t = torch.frombuffer(bytearray(fq), dtype=torch.uint8).cuda()
+    ends, fa = fqz5file._complete_records(t, len(fq), False)
+    assert not fa and ends == [11, 22]
+    ends, _ = fqz5file._complete_records(t, len(fq), True)
+    assert ends == [11, 22, len(fq)]
+    # wrapped: the second record's qualities start with '@' and '+'
+    w = b"@a\nAC\nG\n+\nII\nI\n@b\nGTAC\n+\n@+\nII\n@c\nAA\n+\nI"
+    t = torch.frombuffer(bytearray(w), dtype=torch.uint8).cuda()
+    ends, fa = fqz5file._complete_records(t, len(w), False)
+    assert not fa and ends == [w.index(b"@b"), w.index(b"@c")]
+    ends, _ = fqz5file._complete_records(t, len(w), True)
+    assert ends[-1] == len(w)
