@@ -66,6 +66,17 @@ struct EncJob {
     uint32_t nchunks;       // ceil(steps / enc_chunk_steps(nx))
 };
 
+// O1 encoder tables of more than ENC_TAB_LDS_MAX bytes at 16 B per entry
+// (alphabets over 64) stay in global memory, compact: 4 B per (context,
+// symbol), freq | start << 13 (freq <= 4096, start < 4096), expanded to the
+// 16-B symbol when the chain's entries are staged and in the replay, with
+// the reciprocal of each frequency from an LDS table (enc_rcp_lds).  A
+// quarter of the bytes per symbol read, and a 256-symbol table (256 KB)
+// stays in the XCD's L2 beside the other streams' (1 MB each did not).
+constexpr uint32_t ENC_TAB_LDS_MAX = 65536;
+constexpr uint32_t ENC_RCP_N = 4097;                      // frequencies 0..4096
+__host__ __device__ inline bool enc_tab_compact(bool o1, uint32_t A) { return o1 && A * A * 16u > ENC_TAB_LDS_MAX; }
+
 // Encoder chunk: steps between state checkpoints (chain and replay agree).
 inline uint32_t enc_chunk_steps(int nx) { return 1024u / uint32_t(nx); }
 // Replay: chunks handled by one 1024-thread workgroup.

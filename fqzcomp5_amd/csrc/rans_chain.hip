@@ -79,11 +79,38 @@ static DEV void st8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
 constexpr uint32_t ENC_ENT = 1024;                        // entries per chunk
 constexpr uint32_t ENC_ENT_BYTES = (ENC_ENT + 512) * 16;  // + chain over-read
 constexpr uint32_t ENC_LDS_BASE = ENC_ENT_BYTES + 256;    // + remap
-constexpr uint32_t ENC_TAB_LDS_MAX = 65536;
 constexpr int REPLAY_THREADS = 1024;
 constexpr int ENC_W = 16;                    // replay: steps per byte batch
 
 template <int NX> constexpr uint32_t enc_chunk() { return ENC_ENT / NX; }
+
+// The reciprocal of every frequency (RansEncSymbolInit, rANS_word.h:201-272:
+// ceil(2^(s+31) / f), s = ceil(log2 f); ~0 below 2) into LDS, by `nthr`
+// threads; the caller synchronises.
+static DEV void enc_rcp_lds(uint32_t *rc, int tid, int nthr) {
+    for (int f = tid; f < int(ENC_RCP_N); f += nthr) {
+        if (f < 2) { rc[f] = ~0u; continue; }
+        const uint32_t s = 32u - uint32_t(__builtin_clz(uint32_t(f) - 1u));
+        rc[f] = uint32_t(((1ull << (s + 31)) + uint64_t(f) - 1) / uint64_t(f));
+    }
+}
+// a compact entry (freq | start << 13) as the 16-B encoder symbol
+// (make_encsym, rans_format.hpp)
+static DEV uint4 enc_expand(uint32_t c, int bits, const uint32_t *rc) {
+    const uint32_t f = c & 0x1fffu, start = c >> 13;
+    uint4 e;
+    e.y = ((RANS_LOW_D >> bits) << 16) * f - 1u;
+    uint32_t sh = 0;
+    e.x = rc[f];
+    if (f < 2) {
+        e.z = start + (1u << bits) - 1u;
+    } else {
+        sh = 31u - uint32_t(__builtin_clz(f - 1u));
+        e.z = start;
+    }
+    e.w = (((1u << bits) - f) & 0xffffu) | (sh << 16);
+    return e;
+}
 
 template <bool O1, int NX>
 static DEV uint32_t enc_steps(uint32_t n) {
@@ -98,18 +125,22 @@ static DEV void chain_body(const EncJob &J) {
     uint4 *ent = reinterpret_cast<uint4 *>(lds);
     uint8_t *rm = lds + ENC_ENT_BYTES;
     uint4 *ltab = reinterpret_cast<uint4 *>(lds + ENC_LDS_BASE);
+    uint32_t *rc = reinterpret_cast<uint32_t *>(lds + ENC_LDS_BASE);   // (!TLDS: compact table)
 
     const int l = int(threadIdx.x);
     const uint32_t n = J.n;
     const uint32_t A = uint32_t(J.A);
     const uint4 *gtab = reinterpret_cast<const uint4 *>(J.tab);
+    const uint32_t *ctab = reinterpret_cast<const uint32_t *>(J.tab);
     if (TLDS) {
         const uint32_t ntab = O1 ? A * A : 256u;
         for (uint32_t i = l; i < ntab; i += 64) ltab[i] = gtab[i];
+    } else {
+        enc_rcp_lds(rc, l, 64);
     }
     if (O1)
         for (int i = l; i < 256; i += 64) rm[i] = J.remap[i];
-    const uint4 *tab = TLDS ? ltab : gtab;
+    const uint4 *tab = ltab;
 
     const uint32_t isz = n / NX;
     const uint32_t T = enc_steps<O1, NX>(n);
@@ -153,7 +184,7 @@ static DEV void chain_body(const EncJob &J) {
                 ok = NX * S * j + i < n;
                 idx = sb[r];
             }
-            uint4 e = tab[ok ? idx : 0u];
+            uint4 e = TLDS ? tab[ok ? idx : 0u] : enc_expand(ctab[ok ? idx : 0u], J.bits, rc);
             if (!ok) e = ID;
             ent[(S - 1 - kk) * NX + z] = e;
         }
@@ -387,18 +418,22 @@ static DEV void replay_body(const EncJob &J, uint32_t c0) {
     uint8_t *lds = reinterpret_cast<uint8_t *>(chain_lds);
     uint8_t *rm = lds;
     uint4 *ltab = reinterpret_cast<uint4 *>(lds + 256);
+    uint32_t *rc = reinterpret_cast<uint32_t *>(lds + 256);   // (!TLDS: compact table)
     const int tid = int(threadIdx.x);
     const uint32_t n = J.n;
     const uint32_t A = uint32_t(J.A);
     const uint4 *gtab = reinterpret_cast<const uint4 *>(J.tab);
+    const uint32_t *ctab = reinterpret_cast<const uint32_t *>(J.tab);
     if (TLDS) {
         const uint32_t ntab = O1 ? A * A : 256u;
         for (uint32_t i = tid; i < ntab; i += REPLAY_THREADS) ltab[i] = gtab[i];
+    } else {
+        enc_rcp_lds(rc, tid, REPLAY_THREADS);
     }
     if (O1)
         for (int i = tid; i < 256; i += REPLAY_THREADS) rm[i] = J.remap[i];
     __syncthreads();
-    const uint4 *tab = TLDS ? ltab : gtab;
+    const uint4 *tab = ltab;
 
     const int l = tid & 63;
     const uint32_t c = c0 + uint32_t(tid >> 6) * G + uint32_t(l / NX);
@@ -441,7 +476,7 @@ static DEV void replay_body(const EncJob &J, uint32_t c0) {
             if (ok[w]) {
                 const int64_t k = khi - int64_t(t0) - w;
                 const uint32_t idx = O1 ? uint32_t(rm[k ? b[w + 1] : 0u]) * A + rm[b[w]] : b[w];
-                e = tab[idx];
+                e = TLDS ? tab[idx] : enc_expand(ctab[idx], J.bits, rc);
             }
             const uint32_t xo = x;
             const bool cf = xo > e.y;
@@ -510,7 +545,7 @@ __global__ __launch_bounds__(1024) void k_enc_scan(const EncJob *jobs) {
 
 uint32_t enc_lds_bytes(int o1, uint32_t A) {
     const uint32_t ntab = o1 ? A * A : 256u;
-    return ENC_LDS_BASE + (ntab * 16u <= ENC_TAB_LDS_MAX ? ntab * 16u : 0u);
+    return ENC_LDS_BASE + (ntab * 16u <= ENC_TAB_LDS_MAX ? ntab * 16u : ENC_RCP_N * 4u);
 }
 
 // Jobs that run k_enc_chain2w (NX=4, table in LDS) and their LDS.
@@ -524,7 +559,7 @@ uint32_t enc_2w_lds_bytes(int o1, uint32_t A) {
 
 uint32_t enc_replay_lds_bytes(int o1, uint32_t A) {
     const uint32_t ntab = o1 ? A * A : 256u;
-    return 256u + (ntab * 16u <= ENC_TAB_LDS_MAX ? ntab * 16u : 0u);
+    return 256u + (ntab * 16u <= ENC_TAB_LDS_MAX ? ntab * 16u : ENC_RCP_N * 4u);
 }
 
 // ===========================================================================

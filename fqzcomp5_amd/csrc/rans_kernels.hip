@@ -608,7 +608,10 @@ __global__ __launch_bounds__(256) void k_enc_tab(const EncTabItem *items) {
         }
         e.cmpl_sh = (((1u << bits) - f) & 0xffff) | (sh << 16);
     }
-    it.out[r * A + t] = e;
+    if (enc_tab_compact(true, A))                     // (kernels.h: 4 B per entry)
+        reinterpret_cast<uint32_t *>(it.out)[r * A + t] = f | (start << 13);
+    else
+        it.out[r * A + t] = e;
 }
 
 hipError_t launch_enc_tab(const EncTabItem *d_items, int nitems, hipStream_t s) {

@@ -78,6 +78,34 @@ def _load():
     return so
 
 
+# $FQZ5_FILE_TRACE: host wall time per stage of compress_file /
+# decompress_file on stderr (read, upload, parse, gather, codec, assemble,
+# download, write); the stages end with what the library synchronises
+_TRACE = {}
+
+
+class _stage:
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        import time
+        self.t = time.perf_counter()
+
+    def __exit__(self, *a):
+        import time
+        _TRACE[self.name] = _TRACE.get(self.name, 0.0) + time.perf_counter() - self.t
+
+
+def _trace_dump(what: str) -> None:
+    import os
+    import sys
+    if os.environ.get("FQZ5_FILE_TRACE") and _TRACE:
+        print(f"[fqz5file] {what}: " + ", ".join(f"{k} {1e3 * v:.1f} ms" for k, v in _TRACE.items()),
+              file=sys.stderr, flush=True)
+    _TRACE.clear()
+
+
 def _check(rc, what):
     if rc < 0:
         raise _lib.NativeError(f"{what}: {_lib.last_error()}")
@@ -376,19 +404,22 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
     paired = len(srcs) == 2
     want = wbytes
     while True:
-        for s in srcs:
-            s.fill(want)
+        with _stage("read"):
+            for s in srcs:
+                s.fill(want)
         devs, ends = [], []
         for s in srcs:
-            if s.buf:
-                cpu = torch.frombuffer(s.buf, dtype=torch.uint8)
-                d = cpu.to(device)            # blocking (pageable): done before the parse
-                H2D[0] += int(cpu.numel())
-                del cpu
-            else:
-                d = torch.empty(0, dtype=torch.uint8, device=device)
+            with _stage("upload"):
+                if s.buf:
+                    cpu = torch.frombuffer(s.buf, dtype=torch.uint8)
+                    d = cpu.to(device)            # blocking (pageable): done before the parse
+                    H2D[0] += int(cpu.numel())
+                    del cpu
+                else:
+                    d = torch.empty(0, dtype=torch.uint8, device=device)
             devs.append(d)
-            ends.append(_complete_records(d, int(d.numel()), s.eof)[0])
+            with _stage("record_ends"):
+                ends.append(_complete_records(d, int(d.numel()), s.eof)[0])
         k = min(len(e) for e in ends) if paired else len(ends[0])
         r1_done = srcs[0].eof and k == len(ends[0])      # all of R1 in the window
         if paired and not r1_done and srcs[1].eof and k == len(ends[1]):
@@ -406,8 +437,9 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
             text_d, len1 = devs[0][:cut[0]], None
         del devs
         if len1 is None:
-            recs, rsz, nrec, fasta = _index_text(text_d, 0, int(text_d.numel()), wrapped=True)
-            first = _blocks(so, rsz, blk)
+            with _stage("parse"):
+                recs, rsz, nrec, fasta = _index_text(text_d, 0, int(text_d.numel()), wrapped=True)
+                first = _blocks(so, rsz, blk)
         else:
             r1, rs1, n1, fa1 = _index_text(text_d, 0, len1, wrapped=True)
             r2, rs2, n2, fa2 = _index_text(text_d, len1, int(text_d.numel()) - len1, wrapped=True)
@@ -790,15 +822,17 @@ def _code_window(W, sink: _Sink, level: int, pos: int, index: list, av, state, g
     need = sorted({b for b in range(nb)
                    if blk_owner[b] == rk or sched[sec0[b]:sec0[b + 1]].any()})
     # the needed blocks' section inputs, gathered in HBM
-    run = W.gather(need)
+    with _stage("gather"):
+        run = W.gather(need)
     secs = [None] * int(sec0[-1])
     local = run.enc_secs()
     for j, b in enumerate(need):
         for q in range(per[b]):
             secs[sec0[b] + q] = local[run.blk_sec0[j] + q]
-    res, meth, _ = S.encode_window(secs, ids, ins, owner, av, state, group,
-                                   bounded=level >= 7, final=W.final,
-                                   bounds_first=5 <= level < 7)
+    with _stage("codec"):
+        res, meth, _ = S.encode_window(secs, ids, ins, owner, av, state, group,
+                                       bounded=level >= 7, final=W.final,
+                                       bounds_first=5 <= level < 7)
     mine = [j for j, b in enumerate(need) if blk_owner[b] == rk]
     full_res = [None] * len(local)
     for j, b in enumerate(need):
@@ -811,7 +845,8 @@ def _code_window(W, sink: _Sink, level: int, pos: int, index: list, av, state, g
                 raise _lib.NativeError("section coding failed: " + _lib.last_error())
     sizes = []
     if mine:
-        run.assemble(full_res, mine)
+        with _stage("assemble"):
+            run.assemble(full_res, mine)
         sizes = [int(run.blk_off[i + 1] - run.blk_off[i]) for i in range(len(mine))]
     all_sizes = _allgather_obj(sizes, group)
     # blocks in file order: rank-contiguous, so rank-major order
@@ -820,10 +855,12 @@ def _code_window(W, sink: _Sink, level: int, pos: int, index: list, av, state, g
     starts = np.concatenate([[0], np.cumsum(flat)]).astype(np.int64) + pos
     if mine:
         end = int(run.blk_off[len(mine)])
-        host = _pinned(end)
-        host.copy_(run.blk_buf[:end])
+        with _stage("download"):
+            host = _pinned(end)
+            host.copy_(run.blk_buf[:end])
         b0 = need[mine[0]]
-        sink.write_at(int(starts[b0]), host.numpy())
+        with _stage("write"):
+            sink.write_at(int(starts[b0]), host.numpy())
         del host
     for b in range(nb):
         index.append((int(starts[b]), W.seq_bytes[b], W.nrec[b]))
@@ -873,6 +910,7 @@ def _encode_stream(srcs: list, sink: _Sink, level: int, blk_size: int | None, de
         total = pos + len(idx)
     else:
         total = 0
+    _trace_dump(f"encode -{level}")
     return int(_allgather_obj(total, group)[0])
 
 
@@ -1328,25 +1366,31 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
             try:
                 for gb in groups:
                     a, e = ranges[gb[0]][0], ranges[gb[-1]][1]
-                    host = _pinned(e - a)
-                    f.seek(a)
-                    mv = memoryview(host.numpy())
-                    got = 0
-                    while got < e - a:
-                        k = f.readinto(mv[got:])
-                        if not k:
-                            raise OSError(f"{src}: short read")
-                        got += k
-                    hv = host.numpy()
-                    buf = host.to(device)      # blocking: block parsing runs on the library's streams
-                    texts = _decode(hv, buf, plus_name, device, pairs=dst2 is not None,
-                                    ranges=Blocks([(ranges[b][0] - a, ranges[b][1] - a) for b in gb],
-                                                  ranges.version))
+                    with _stage("read"):
+                        host = _pinned(e - a)
+                        f.seek(a)
+                        mv = memoryview(host.numpy())
+                        got = 0
+                        while got < e - a:
+                            k = f.readinto(mv[got:])
+                            if not k:
+                                raise OSError(f"{src}: short read")
+                            got += k
+                        hv = host.numpy()
+                    with _stage("upload"):
+                        buf = host.to(device)      # blocking: block parsing runs on the library's streams
+                    with _stage("decode"):
+                        texts = _decode(hv, buf, plus_name, device, pairs=dst2 is not None,
+                                        ranges=Blocks([(ranges[b][0] - a, ranges[b][1] - a)
+                                                       for b in gb], ranges.version))
                     if dst2 is None:
                         texts = (texts,)
                     for j, t in enumerate(texts):
-                        out = _pinned(int(t.numel()))
-                        out.copy_(t)
+                        with _stage("download"):
+                            out = _pinned(int(t.numel()))
+                            out.copy_(t)
+                        st_w = _stage("write")
+                        st_w.__enter__()
                         if sinks:
                             want = sum(sizes[b] for b in gb)
                             if int(t.numel()) != want:
@@ -1355,6 +1399,7 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
                         else:
                             streams[j].write(memoryview(out.numpy()))
                         written[j] += int(t.numel())
+                        st_w.__exit__()
                         del out
                     del buf, host, texts
             finally:
@@ -1367,6 +1412,7 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
                         st.close()
                 for sk in sinks:
                     sk.close()
+        _trace_dump("decode")
         if single:
             return sum(written)
         all_w = _allgather_obj(written, group)
