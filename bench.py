@@ -448,6 +448,9 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
         if t1_blocks:
             out["cpu_baseline"]["t1_blocks"] = t1_check(reads, blocks, level, gpu_blocks, t1_blocks)
     del run, reads
+    # the pool's idle chunks back to the device between items (the next
+    # item's arenas start empty)
+    so.fqz5_arenas_release()
     torch.cuda.empty_cache()
     return out
 
