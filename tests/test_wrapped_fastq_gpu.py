@@ -65,5 +65,11 @@ def test_record_ends():
     t = torch.frombuffer(bytearray(w), dtype=torch.uint8).cuda()
     ends, fa = fqz5file._complete_records(t, len(w), False)
     assert not fa and ends == [w.index(b"@b"), w.index(b"@c")]
-    ends, _ = fqz5file._complete_records(t, len(w), True)
-    assert ends[-1] == len(w)
+    # at the end of the input the cut-off record is an error (kseq -2)...
+    with pytest.raises(lib.NativeError):
+        fqz5file._complete_records(t, len(w), True)
+    # ... and a complete one closes the text
+    w2 = w + b"I"
+    t2 = torch.frombuffer(bytearray(w2), dtype=torch.uint8).cuda()
+    ends, _ = fqz5file._complete_records(t2, len(w2), True)
+    assert ends == [w.index(b"@b"), w.index(b"@c"), len(w2)]
