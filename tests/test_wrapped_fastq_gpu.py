@@ -58,8 +58,12 @@ def test_record_ends():
     t = torch.frombuffer(bytearray(fq), dtype=torch.uint8).cuda()
     ends, fa = fqz5file._complete_records(t, len(fq), False)
     assert not fa and ends == [11, 22]
-    ends, _ = fqz5file._complete_records(t, len(fq), True)
-    assert ends == [11, 22, len(fq)]
+    with pytest.raises(lib.NativeError):          # "@c\nA" at the end: no qualities
+        fqz5file._complete_records(t, len(fq), True)
+    fq2 = fq + b"\n+\nI"                          # (no final newline)
+    t2 = torch.frombuffer(bytearray(fq2), dtype=torch.uint8).cuda()
+    ends, _ = fqz5file._complete_records(t2, len(fq2), True)
+    assert ends == [11, 22, len(fq2)]
     # wrapped: the second record's qualities start with '@' and '+'
     w = b"@a\nAC\nG\n+\nII\nI\n@b\nGTAC\n+\n@+\nII\n@c\nAA\n+\nI"
     t = torch.frombuffer(bytearray(w), dtype=torch.uint8).cuda()
