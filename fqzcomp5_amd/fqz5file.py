@@ -386,10 +386,11 @@ def _barrier(group):
     S.barrier(group)
 
 
-def _complete_records(text_d, n: int, eof: bool) -> tuple[list[int], bool]:
-    """Record ends of text_d[:n] (exclusive offsets, increasing) that are
-    known to be complete, and whether the text is FASTA.  FASTQ: after every
-    4th line; FASTA: before every header line after the first; at the end of
+def _complete_records(text_d, n: int, eof: bool):
+    """Record ends of text_d[:n] (exclusive offsets, increasing; a list or a
+    uint64 array) that are known to be complete, and whether the text is
+    FASTA.  FASTQ: after each record (fqz5_fastq_record_ends: 4-line or
+    wrapped); FASTA: before every header line after the first; at the end of
     the input, the end of the text closes the last record."""
     import torch
     if n == 0:
@@ -407,7 +408,11 @@ def _complete_records(text_d, n: int, eof: bool) -> tuple[list[int], bool]:
         _lib.after_torch()
         _check(_load().fqz5_fastq_record_ends(text_d.data_ptr(), n, int(bool(eof)), buf.ctypes.data,
                                               cap, C.byref(cnt)), "fqz5_fastq_record_ends")
-        ends = buf[:int(cnt.value)].tolist()
+        # (an array: the window needs the count and one end, not 3M Python ints)
+        ends = buf[:int(cnt.value)]
+        if eof and (not len(ends) or int(ends[-1]) != n):
+            ends = np.append(ends, np.uint64(n))
+        return ends, fasta
     if eof and (not ends or ends[-1] != n):
         ends.append(n)
     del torch
@@ -461,7 +466,7 @@ def _next_window(srcs: list, blk: int, wbytes: int, device: str):
                 return None
             want *= 2
             continue
-        cut = [e[k - 1] for e in ends]
+        cut = [int(e[k - 1]) for e in ends]
         if paired:
             text_d = torch.cat([devs[0][:cut[0]], devs[1][:cut[1]]])
             len1 = cut[0]

@@ -39,5 +39,5 @@ timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format cs
     python3 bench.py $B5I --steps 1 --warmup 0 > $OUT/fetch5i.log 2>&1
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/l5i/write -o write -- \
     python3 bench.py $B5I --steps 1 --warmup 0 > $OUT/write5i.log 2>&1
-python3 tools/pmc_summary.py $OUT/l5i $OUT/pmc_l5i.json "k_fqz_dec_small runs FQZ5_SMALL_COPIES (default 2) hedged copies per block, each with its own 1.5 MB backing store" > /dev/null
+python3 tools/pmc_summary.py $OUT/l5i $OUT/pmc_l5i.json "the fqz quality chains decode on host cores by the default placement (fqz5_set_host_decode(2))" > /dev/null
 echo done
