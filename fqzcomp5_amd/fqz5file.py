@@ -327,18 +327,52 @@ class _Src:
         self.buf = nb
         mv = memoryview(self.buf)
         try:
-            while at < want:
-                k = self.f.readinto(mv[at:at + min(want - at, 1 << 28)])
-                if not k:
-                    break
-                at += k
-                self.pos += k
+            if self.path is not None and want - at >= (64 << 20):
+                got = self._pread_parallel(mv, at, want)
+            else:
+                got = 0
+                while at + got < want:
+                    k = self.f.readinto(mv[at + got:at + got + min(want - at - got, 1 << 28)])
+                    if not k:
+                        break
+                    got += k
+            at += got
+            self.pos += got
         finally:
             del mv
         if at < want:                         # (the file shrank under us)
             del self.buf[at:]
         if self.pos >= self.size:
             self.eof = True
+
+    def _pread_parallel(self, mv, a: int, b: int) -> int:
+        """Bytes [pos, pos + b - a) of the file into mv[a:b] by positioned
+        reads on several threads (the page-cache copy runs at ~4 GB/s on one
+        core; the reads release the GIL)."""
+        import os
+        from concurrent.futures import ThreadPoolExecutor
+        fd, base = self.f.fileno(), self.pos
+        step = 32 << 20
+        parts = [(o, min(o + step, b)) for o in range(a, b, step)]
+
+        def one(p):
+            o, e = p
+            n = 0
+            while o + n < e:
+                k = os.preadv(fd, [mv[o + n:e]], base + (o - a) + n)
+                if k <= 0:
+                    break
+                n += k
+            return n
+        with ThreadPoolExecutor(max_workers=min(8, len(parts))) as ex:
+            got = list(ex.map(one, parts))
+        # the reads are contiguous only up to the first short one
+        total = 0
+        for (o, e), n in zip(parts, got):
+            total += n
+            if n < e - o:
+                break
+        return total
 
     def advance(self, n: int) -> None:
         del self.buf[:n]
