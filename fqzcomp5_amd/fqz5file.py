@@ -957,16 +957,19 @@ def _encode_stream(srcs: list, sink: _Sink, level: int, blk_size: int | None, de
     at = [0] * len(srcs)
     try:
         while True:
-            if files:
-                W = _next_window_ranks(files, at, blk, wbytes, device, group)
-            else:
-                w0 = _next_window(srcs, blk, wbytes, device)
-                W = _LocalWindow(w0, srcs, ws) if w0 is not None else None
+            with _stage("window"):
+                if files:
+                    W = _next_window_ranks(files, at, blk, wbytes, device, group)
+                else:
+                    w0 = _next_window(srcs, blk, wbytes, device)
+                    W = _LocalWindow(w0, srcs, ws) if w0 is not None else None
             if W is None:
                 break
-            pos = _code_window(W, sink, level, pos, index, av, state, group)
-            W.advance()
-            del W
+            with _stage("code_window"):
+                pos = _code_window(W, sink, level, pos, index, av, state, group)
+            with _stage("advance"):
+                W.advance()
+                del W
     finally:
         for f in files or []:
             f.close()
