@@ -62,11 +62,11 @@ sys.path.insert(0, ROOT)
 # the -3 encode waited 100 ms per step behind the LZP3 helper's chain).
 # Must be set before anything initialises HIP.
 # (the rule of capi.cpp's hw_queues_default: FQZ5_HW_QUEUES as given, else
-# an unset value or HIP's default of 4 raised to 16, any other value kept)
+# an unset value or HIP's default of 4 raised to 20, any other value kept)
 if os.environ.get("FQZ5_HW_QUEUES"):
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ["FQZ5_HW_QUEUES"]
 elif os.environ.get("GPU_MAX_HW_QUEUES", "") in ("", "4"):
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    os.environ["GPU_MAX_HW_QUEUES"] = "20"
 
 FASTQ_REC = 358          # bytes of FASTQ text per synthetic 150 bp record (avg)
 GAP_S = float(os.environ.get("FQZ5_BENCH_GAP_S", "0") or 0)
@@ -82,7 +82,8 @@ PROF_KERNELS = ["k_enc_chain", "k_rans_dec", "k_fqz_dec", "k_fqz_rc", "k_seq_dec
 # rocprof kernel names of a PROF_KERNELS entry (pmc_traffic)
 ROCPROF_NAMES = {"k_fqz_dec": ["k_fqz_dec", "k_fqz_dec_small"],
                  "k_enc_replay": ["k_enc_replay<true>"],
-                 "k_enc_replay0": ["k_enc_replay<false>"]}
+                 "k_enc_replay0": ["k_enc_replay<false>"],
+                 "k_seq_model": ["k_seq_model_runs", "k_seq_model"]}
 
 
 def log(*a):

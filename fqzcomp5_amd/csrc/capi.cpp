@@ -47,10 +47,10 @@ namespace fqz5 {
 // (e.g. the relinked CLI) loads this library before anything touched HIP:
 // FQZ5_HW_QUEUES, when set, is used as given (experiments, fewer queues
 // included); otherwise an unset GPU_MAX_HW_QUEUES or HIP's default of 4 is
-// raised to 16, and any other value the caller chose is kept.  Not 32: once
+// raised to 20, and any other value the caller chose is kept.  Not 32: once
 // the helper contexts had mapped 32 queues, every later long kernel ran
 // ~30 % slower (a 44.5M-symbol fqz decode 180 -> 232 ns per symbol after a
-// -5 encode, 180 with 4, 8 or 16 queues): the
+// -5 encode, 180 with 4, 8, 16 or 20 queues): the
 // scheduler time-slices more queues than the hardware maps at once, and the
 // running waves are preempted and restored.
 __attribute__((constructor)) static void hw_queues_default() {
@@ -60,7 +60,7 @@ __attribute__((constructor)) static void hw_queues_default() {
         setenv("GPU_MAX_HW_QUEUES", w, 1);
         return;
     }
-    if (!v || !*v || std::atoi(v) == 4) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+    if (!v || !*v || std::atoi(v) == 4) setenv("GPU_MAX_HW_QUEUES", "20", 1);
 }
 
 static thread_local std::string g_err;
@@ -194,7 +194,7 @@ static thread_local hipEvent_t g_wait_ev = nullptr;
 static thread_local bool g_wait_armed = false;
 static void ctx_wait(GpuCtx &c, hipEvent_t ev) {
     FQZ5_HIP(hipStreamWaitEvent(c.stream, ev, 0));
-    FQZ5_HIP(hipStreamWaitEvent(c.stream2, ev, 0));
+    if (c.stream2) FQZ5_HIP(hipStreamWaitEvent(c.stream2, ev, 0));   // (a later one forks from stream)
 }
 GpuCtx &gpu_aux(int k) {
     if (!g_aux[k]) {
@@ -209,7 +209,7 @@ void gpu_aux_reset_all() {
 }
 static void release_ctx(GpuCtx &c) {
     c.sync();
-    FQZ5_HIP(hipStreamSynchronize(c.stream2));
+    if (c.stream2) FQZ5_HIP(hipStreamSynchronize(c.stream2));
     c.arena.release();
     c.fqz_tmp.release();
     c.lzp_tmp.release();

@@ -62,77 +62,79 @@ Records walk_records(int nrec, const uint32_t *lens, const uint32_t *flags, size
 
 // The statistics and auto-tuning of fqz_qual_stats (fqzcomp_qual.c:424-704)
 // with the histograms from the GPU.  Updates pm and the caller's flags.
-void tune(GpuCtx &g, Param &pm, int nrec, uint32_t *flags, const Records &R,
-          const uint8_t *d_q, size_t n, uint32_t qhist[256]) {
+// Staged so that the requests of a batch share their round trips: launch()
+// for each, one sync, mid() for each (it launches the per-class histograms
+// when the average-quality split is searched), one sync, finish() for each.
+struct Tune {
+    Param *pm = nullptr;
+    int nrec = 0;
+    uint32_t *flags = nullptr;
+    const Records *R = nullptr;
+    uint32_t *qhist = nullptr;
     int max_sel = 0, has_r2 = 0;
-    for (int r = 0; r < nrec; r++) {
-        max_sel = std::max(max_sel, int(flags[r] >> 16));
-        if (flags[r] & F_READ2) has_r2 = 1;
-    }
-    const uint32_t W = R.walked;
-    // ---- GPU: per-record averages / dups, (len & 127, q) histograms ----
-    std::vector<uint2> chunks;
-    for (uint32_t r = 0; r < W;) {
-        uint32_t e = r, bytes = 0;
-        while (e < W && (e == r || bytes + R.len[e] <= 65535u)) bytes += R.len[e++];
-        chunks.push_back(make_uint2(r, e));
-        r = e;
-    }
     FqzStatJob J{};
-    J.q = d_q;
-    J.off = g.upload(R.off);
-    J.len = g.upload(R.len);
-    J.flags = g.upload(R.flags);
-    J.nrec = W;
-    J.rec_avg = g.arena.alloc_n<uint32_t>(W + 1);
-    J.avg_hist = g.arena.alloc_n<uint32_t>(NAVG);
-    J.dups = g.arena.alloc_n<uint32_t>(1);
-    J.chunks = g.upload(chunks);
-    J.h1 = g.arena.alloc_n<uint32_t>(NPOS * 256);
-    J.h2 = g.arena.alloc_n<uint32_t>(NPOS * 256);
-    J.b4 = g.arena.alloc_n<uint32_t>(4 * NPOS * 256);
-    g.memset0(J.rec_avg, (W + 1) * 4);
-    g.memset0(J.avg_hist, NAVG * 4);
-    g.memset0(J.dups, 4);
-    g.memset0(J.h1, NPOS * 256 * 4);
-    g.memset0(J.h2, NPOS * 256 * 4);
-    g.memset0(J.b4, 4 * NPOS * 256 * 4);
-    FQZ5_HIP(launch_fqz_records(J, g.stream));
-    FQZ5_HIP(launch_fqz_hist(J, int(chunks.size()), 0, g.stream));
-    std::vector<uint32_t> h1(NPOS * 256), h2(NPOS * 256), ahist(NAVG), ravg(W + 1);
+    std::vector<uint2> chunks;
+    std::vector<uint32_t> h1, h2, ahist, ravg, amap, b4;
     uint32_t dups = 0;
-    g.download(h1.data(), J.h1, h1.size());
-    g.download(h2.data(), J.h2, h2.size());
-    g.download(ahist.data(), J.avg_hist, ahist.size());
-    g.download(ravg.data(), J.rec_avg, ravg.size());
-    g.download(&dups, J.dups, 1);
-    g.sync();
+    bool classes = false;
 
-    std::vector<uint64_t> t1(NPOS, 0), t2(NPOS, 0);
-    for (int j = 0; j < NPOS; j++)
-        for (int s = 0; s < 256; s++) {
-            const uint32_t a = h1[size_t(j) * 256 + s], b = h2[size_t(j) * 256 + s];
-            qhist[s] += a + b;
-            t1[size_t(j)] += a;
-            t2[size_t(j)] += b;
+    void launch(GpuCtx &g, Param &p, int nr, uint32_t *fl, const Records &rec,
+                const uint8_t *d_q, uint32_t *qh) {
+        pm = &p, nrec = nr, flags = fl, R = &rec, qhist = qh;
+        for (int r = 0; r < nrec; r++) {
+            max_sel = std::max(max_sel, int(flags[r] >> 16));
+            if (flags[r] & F_READ2) has_r2 = 1;
         }
-    pm.dedup = ((W + 1) / (dups + 1) < 500);
-    pm.max_sym = pm.nsym = 0;
-    for (int s = 0; s < 256; s++)
-        if (qhist[s]) pm.max_sym = s, pm.nsym++;
+        const uint32_t W = R->walked;
+        // ---- GPU: per-record averages / dups, (len & 127, q) histograms ----
+        for (uint32_t r = 0; r < W;) {
+            uint32_t e = r, bytes = 0;
+            while (e < W && (e == r || bytes + R->len[e] <= 65535u)) bytes += R->len[e++];
+            chunks.push_back(make_uint2(r, e));
+            r = e;
+        }
+        J.q = d_q;
+        J.off = g.upload(R->off);
+        J.len = g.upload(R->len);
+        J.flags = g.upload(R->flags);
+        J.nrec = W;
+        J.rec_avg = g.arena.alloc_n<uint32_t>(W + 1);
+        J.avg_hist = g.arena.alloc_n<uint32_t>(NAVG);
+        J.dups = g.arena.alloc_n<uint32_t>(1);
+        J.chunks = g.upload(chunks);
+        J.h1 = g.arena.alloc_n<uint32_t>(NPOS * 256);
+        J.h2 = g.arena.alloc_n<uint32_t>(NPOS * 256);
+        J.b4 = g.arena.alloc_n<uint32_t>(4 * NPOS * 256);
+        g.memset0(J.rec_avg, (W + 1) * 4);
+        g.memset0(J.avg_hist, NAVG * 4);
+        g.memset0(J.dups, 4);
+        g.memset0(J.h1, NPOS * 256 * 4);
+        g.memset0(J.h2, NPOS * 256 * 4);
+        g.memset0(J.b4, 4 * NPOS * 256 * 4);
+        FQZ5_HIP(launch_fqz_records(J, g.stream));
+        FQZ5_HIP(launch_fqz_hist(J, int(chunks.size()), 0, g.stream));
+        h1.resize(NPOS * 256), h2.resize(NPOS * 256), ahist.resize(NAVG), ravg.resize(W + 1);
+        g.download(h1.data(), J.h1, h1.size());
+        g.download(h2.data(), J.h2, h2.size());
+        g.download(ahist.data(), J.avg_hist, ahist.size());
+        g.download(ravg.data(), J.rec_avg, ravg.size());
+        g.download(&dups, J.dups, 1);
+    }
 
-    // per-record average of every record (unwalked ones: 0, as calloc)
-    auto rec_avg = [&](int r) -> uint32_t {
-        if (nrec <= 0) return ravg[0];
-        return uint32_t(r) < W ? ravg[size_t(r)] : 0u;
-    };
-
-    if (pm.qa != 0) {
+    void mid(GpuCtx &g) {
+        const uint32_t W = R->walked;
+        for (int j = 0; j < NPOS; j++)
+            for (int s = 0; s < 256; s++) qhist[s] += h1[size_t(j) * 256 + s] + h2[size_t(j) * 256 + s];
+        pm->dedup = ((W + 1) / (dups + 1) < 500);
+        pm->max_sym = pm->nsym = 0;
+        for (int s = 0; s < 256; s++)
+            if (qhist[s]) pm->max_sym = s, pm->nsym++;
+        if (pm->qa == 0) return;
         // rank the averages into four classes (fqzcomp_qual.c:522-557)
-        const double f0 = pm.nsym > 8 ? 0.2 : 0.05;
-        const double f1 = pm.nsym > 8 ? 0.5 : 0.22;
-        const double f2 = pm.nsym > 8 ? 0.8 : 0.60;
-        std::vector<uint32_t> amap(ahist);
+        const double f0 = pm->nsym > 8 ? 0.2 : 0.05;
+        const double f1 = pm->nsym > 8 ? 0.5 : 0.22;
+        const double f2 = pm->nsym > 8 ? 0.8 : 0.60;
+        amap = ahist;
         const double cut[3] = {f0, f1, f2};
         int total = 0, k = 0;
         for (int cls = 0; cls < 3; cls++) {
@@ -147,94 +149,112 @@ void tune(GpuCtx &g, Param &pm, int nrec, uint32_t *flags, const Records &R,
         J.amap = g.upload(amap);
         FQZ5_HIP(launch_fqz_hist(J, int(chunks.size()), 1, g.stream));
         FQZ5_HIP(launch_fqz_hist(J, int(chunks.size()), 2, g.stream));
-        std::vector<uint32_t> b4(4 * NPOS * 256);
+        b4.resize(4 * NPOS * 256);
         g.download(b4.data(), J.b4, b4.size());
-        g.sync();
-        auto B4 = [&](int c, int j, int s) { return double(b4[(size_t(c) * NPOS + j) * 256 + s]); };
-        // counts per (class, position) and the merged 2-class / 1-class bins
-        std::vector<double> n4(4 * NPOS, 0);
-        for (int c = 0; c < 4; c++)
-            for (int j = 0; j < NPOS; j++)
-                for (int s = 0; s < 256; s++) n4[size_t(c) * NPOS + j] += B4(c, j, s);
-        double e1 = 0, e2 = 0, e4 = 0;
-        for (int j = 0; j < NPOS; j++) {
-            const double c20 = n4[size_t(0) * NPOS + j] + n4[size_t(1) * NPOS + j];
-            const double c21 = n4[size_t(2) * NPOS + j] + n4[size_t(3) * NPOS + j];
-            const double c1 = c20 + c21;
-            for (int s = 0; s < 256; s++) {
-                const double a0 = B4(0, j, s), a1 = B4(1, j, s), a2 = B4(2, j, s), a3 = B4(3, j, s);
-                const double q20 = a0 + a1, q21 = a2 + a3, q1 = q20 + q21;
-                if (q1) e1 += q1 * std::log(q1 / c1);
-                if (q20) e2 += q20 * std::log(q20 / c20);
-                if (q21) e2 += q21 * std::log(q21 / c21);
-                if (a0) e4 += a0 * std::log(a0 / n4[size_t(0) * NPOS + j]);
-                if (a1) e4 += a1 * std::log(a1 / n4[size_t(1) * NPOS + j]);
-                if (a2) e4 += a2 * std::log(a2 / n4[size_t(2) * NPOS + j]);
-                if (a3) e4 += a3 * std::log(a3 / n4[size_t(3) * NPOS + j]);
-            }
-        }
-        e1 /= -std::log(2) / 8;
-        e2 /= -std::log(2) / 8;
-        e4 /= -std::log(2) / 8;
-        const double m = pm.qa > 0 ? 1 : 0.98;
-        if ((pm.qa == -1 || pm.qa >= 4) && e4 + nrec / 4 < e2 * m + nrec / 8 && e4 + nrec / 4 < e1 * m) {
-            for (int r = 0; r < nrec; r++) flags[r] |= amap[std::min(2559u, rec_avg(r))] << 16;
-            pm.sel = true;
-            max_sel = 3;
-        } else if ((pm.qa == -1 || pm.qa >= 2) && e2 + nrec / 8 < e1 * m) {
-            for (int r = 0; r < nrec; r++) flags[r] |= (amap[std::min(2559u, rec_avg(r))] >> 1) << 16;
-            pm.sel = true;
-            max_sel = 1;
-        }
-        if (pm.qa == -1) {
-            if (pm.pbits > 0 && pm.dbits > 0) {
-                pm.sloc = pm.dloc - 1;
-                pm.pbits--;
-                pm.dbits--;
-                pm.dloc++;
-            } else if (pm.dbits >= 2) {
-                pm.sloc = pm.dloc;
-                pm.dbits -= 2;
-                pm.dloc += 2;
-            } else if (pm.qbits >= 2) {
-                pm.qbits -= 2;
-                pm.ploc -= 2;
-                pm.sloc = unsigned(16 - 2 - pm.r2);
-                if (pm.qbits == 6 && pm.qshift == 5) pm.qbits--;
-            }
-            pm.qa = 4;
-        }
+        classes = true;
     }
 
-    if (has_r2 || pm.r2) {   // READ1 / READ2 split (fqzcomp_qual.c:658-695)
-        double e1 = 0, e2 = 0;
-        for (int j = 0; j < NPOS; j++) {
-            if (!t1[size_t(j)] || !t2[size_t(j)]) continue;
-            for (int s = 0; s < 256; s++) {
-                const double a = h1[size_t(j) * 256 + s], b = h2[size_t(j) * 256 + s];
-                const double ab = a + b;
-                if (!ab) continue;
-                e1 -= ab * std::log(ab / double(t1[size_t(j)] + t2[size_t(j)]));
-                if (a) e2 -= a * std::log(a / double(t1[size_t(j)]));
-                if (b) e2 -= b * std::log(b / double(t2[size_t(j)]));
+    void finish() {
+        Param &p = *pm;
+        const uint32_t W = R->walked;
+        // per-record average of every record (unwalked ones: 0, as calloc)
+        auto rec_avg = [&](int r) -> uint32_t {
+            if (nrec <= 0) return ravg[0];
+            return uint32_t(r) < W ? ravg[size_t(r)] : 0u;
+        };
+        if (classes) {
+            auto B4 = [&](int c, int j, int s) { return double(b4[(size_t(c) * NPOS + j) * 256 + s]); };
+            // counts per (class, position) and the merged 2-class / 1-class bins
+            std::vector<double> n4(4 * NPOS, 0);
+            for (int c = 0; c < 4; c++)
+                for (int j = 0; j < NPOS; j++)
+                    for (int s = 0; s < 256; s++) n4[size_t(c) * NPOS + j] += B4(c, j, s);
+            double e1 = 0, e2 = 0, e4 = 0;
+            for (int j = 0; j < NPOS; j++) {
+                const double c20 = n4[size_t(0) * NPOS + j] + n4[size_t(1) * NPOS + j];
+                const double c21 = n4[size_t(2) * NPOS + j] + n4[size_t(3) * NPOS + j];
+                const double c1 = c20 + c21;
+                for (int s = 0; s < 256; s++) {
+                    const double a0 = B4(0, j, s), a1 = B4(1, j, s), a2 = B4(2, j, s), a3 = B4(3, j, s);
+                    const double q20 = a0 + a1, q21 = a2 + a3, q1 = q20 + q21;
+                    if (q1) e1 += q1 * std::log(q1 / c1);
+                    if (q20) e2 += q20 * std::log(q20 / c20);
+                    if (q21) e2 += q21 * std::log(q21 / c21);
+                    if (a0) e4 += a0 * std::log(a0 / n4[size_t(0) * NPOS + j]);
+                    if (a1) e4 += a1 * std::log(a1 / n4[size_t(1) * NPOS + j]);
+                    if (a2) e4 += a2 * std::log(a2 / n4[size_t(2) * NPOS + j]);
+                    if (a3) e4 += a3 * std::log(a3 / n4[size_t(3) * NPOS + j]);
+                }
+            }
+            e1 /= -std::log(2) / 8;
+            e2 /= -std::log(2) / 8;
+            e4 /= -std::log(2) / 8;
+            const double m = p.qa > 0 ? 1 : 0.98;
+            if ((p.qa == -1 || p.qa >= 4) && e4 + nrec / 4 < e2 * m + nrec / 8 && e4 + nrec / 4 < e1 * m) {
+                for (int r = 0; r < nrec; r++) flags[r] |= amap[std::min(2559u, rec_avg(r))] << 16;
+                p.sel = true;
+                max_sel = 3;
+            } else if ((p.qa == -1 || p.qa >= 2) && e2 + nrec / 8 < e1 * m) {
+                for (int r = 0; r < nrec; r++) flags[r] |= (amap[std::min(2559u, rec_avg(r))] >> 1) << 16;
+                p.sel = true;
+                max_sel = 1;
+            }
+            if (p.qa == -1) {
+                if (p.pbits > 0 && p.dbits > 0) {
+                    p.sloc = p.dloc - 1;
+                    p.pbits--;
+                    p.dbits--;
+                    p.dloc++;
+                } else if (p.dbits >= 2) {
+                    p.sloc = p.dloc;
+                    p.dbits -= 2;
+                    p.dloc += 2;
+                } else if (p.qbits >= 2) {
+                    p.qbits -= 2;
+                    p.ploc -= 2;
+                    p.sloc = unsigned(16 - 2 - p.r2);
+                    if (p.qbits == 6 && p.qshift == 5) p.qbits--;
+                }
+                p.qa = 4;
             }
         }
-        e1 /= std::log(2) * 8;
-        e2 /= std::log(2) * 8;
-        const double m = pm.r2 > 0 ? 1 : 0.95;
-        if (e2 + (8 + nrec / 8) < e1 * m) {
-            for (int r = 0; r < nrec; r++) {
-                const uint32_t sel = flags[r] >> 16;
-                flags[r] = (flags[r] & 0xffff) | ((sel * 2 + ((flags[r] & F_READ2) ? 1 : 0)) << 16);
-                max_sel = std::max(max_sel, int(flags[r] >> 16));
+
+        if (has_r2 || p.r2) {   // READ1 / READ2 split (fqzcomp_qual.c:658-695)
+            std::vector<uint64_t> t1(NPOS, 0), t2(NPOS, 0);
+            for (int j = 0; j < NPOS; j++)
+                for (int s = 0; s < 256; s++) {
+                    t1[size_t(j)] += h1[size_t(j) * 256 + s];
+                    t2[size_t(j)] += h2[size_t(j) * 256 + s];
+                }
+            double e1 = 0, e2 = 0;
+            for (int j = 0; j < NPOS; j++) {
+                if (!t1[size_t(j)] || !t2[size_t(j)]) continue;
+                for (int s = 0; s < 256; s++) {
+                    const double a = h1[size_t(j) * 256 + s], b = h2[size_t(j) * 256 + s];
+                    const double ab = a + b;
+                    if (!ab) continue;
+                    e1 -= ab * std::log(ab / double(t1[size_t(j)] + t2[size_t(j)]));
+                    if (a) e2 -= a * std::log(a / double(t1[size_t(j)]));
+                    if (b) e2 -= b * std::log(b / double(t2[size_t(j)]));
+                }
+            }
+            e1 /= std::log(2) * 8;
+            e2 /= std::log(2) * 8;
+            const double m = p.r2 > 0 ? 1 : 0.95;
+            if (e2 + (8 + nrec / 8) < e1 * m) {
+                for (int r = 0; r < nrec; r++) {
+                    const uint32_t sel = flags[r] >> 16;
+                    flags[r] = (flags[r] & 0xffff) | ((sel * 2 + ((flags[r] & F_READ2) ? 1 : 0)) << 16);
+                    max_sel = std::max(max_sel, int(flags[r] >> 16));
+                }
             }
         }
+        if (max_sel > 0) {
+            p.sel = true;
+            p.max_sel = max_sel;
+        }
     }
-    if (max_sel > 0) {
-        pm.sel = true;
-        pm.max_sel = max_sel;
-    }
-}
+};
 
 // The rest of fqz_pick_parameters (fqzcomp_qual.c:842-1000).
 void pick_finish(Global &g, Param &pm, int strat, int nrec, const uint32_t *lens,
@@ -446,26 +466,46 @@ uint32_t fqz_hot_min() { return hot_min_var().load(); }
 uint32_t fqz_set_hot_min(uint32_t v) { return hot_min_var().exchange(v); }
 
 void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
-    std::vector<FqzEncReq *> par;
-    for (FqzEncReq &R : reqs) {
+    // fqz_pick_parameters of every request without caller parameters, their
+    // statistics round trips shared (Tune)
+    struct Pick {
+        Records rec;
+        Tune t;
+        uint32_t qhist[256] = {0};
+    };
+    std::vector<Pick> picks(reqs.size());
+    std::vector<size_t> tuned;
+    for (size_t i = 0; i < reqs.size(); i++) {
+        FqzEncReq &R = reqs[i];
         R.ok = false;
         R.out.clear();
         R.w = std::make_shared<FqzEncReq::Work>();
+        if (R.gp) continue;
+        Global &G = R.w->G;
+        pick_begin(G, R.vers, R.strat, R.nrec, R.lens, R.n);
+        picks[i].rec = walk_records(R.nrec, R.lens, R.flags, R.n);
+        picks[i].t.launch(g, G.p[0], R.nrec, R.flags, picks[i].rec, R.d_in, picks[i].qhist);
+        tuned.push_back(i);
+    }
+    if (!tuned.empty()) {
+        g.sync();
+        for (size_t i : tuned) picks[i].t.mid(g);
+        g.sync();
+        for (size_t i : tuned) {
+            FqzEncReq &R = reqs[i];
+            picks[i].t.finish();
+            pick_finish(R.w->G, R.w->G.p[0], R.strat, R.nrec, R.lens, R.flags, R.n, picks[i].qhist);
+        }
+    }
+    std::vector<FqzEncReq *> par;
+    for (FqzEncReq &R : reqs) {
         FqzEncReq::Work &W = *R.w;
         Global &G = W.G;
         const int nrec = R.nrec;
         const size_t n = R.n;
         const uint64_t *d_soff =
             (R.d_seq && nrec > 0) ? seq_offsets(g, nrec, R.lens) : nullptr;
-        if (!R.gp) {
-            pick_begin(G, R.vers, R.strat, nrec, R.lens, n);
-            uint32_t qhist[256] = {0};
-            const Records Rec = walk_records(nrec, R.lens, R.flags, n);
-            tune(g, G.p[0], nrec, R.flags, Rec, R.d_in, n, qhist);
-            pick_finish(G, G.p[0], R.strat, nrec, R.lens, R.flags, n, qhist);
-        } else {
-            copy_gparams(G, R.gp);
-        }
+        if (R.gp) copy_gparams(G, R.gp);
         const bool have_seq = nrec > 0 && (R.d_seq || (R.h_seq && R.h_seq[0]));
         if (!have_seq) {
             for (Param &pm : G.p) pm.bbits = pm.bloc = 0;

@@ -35,8 +35,9 @@ struct GpuError : std::runtime_error {
 // arena.  An arena takes chunks from the pool as it grows and gives them all
 // back at reset() (after its stream has drained), so the device footprint
 // is the peak of what the contexts use at the same time, not the sum of each
-// context's own peak.  Idle chunks beyond a quarter
-// of the device's memory ($FQZ5_ARENA_IDLE_GB) go back to the device.
+// context's own peak.  Idle chunks beyond keep_idle()
+// (a quarter of the device's memory or the work's peak, whichever is more)
+// go back to the device.
 class ChunkPool {
   public:
     static ChunkPool &get() {
@@ -73,14 +74,16 @@ class ChunkPool {
     }
     void give(void *b, size_t sz) {
         bool over;
+        size_t keep;
         {
             std::lock_guard<std::mutex> lk(m_);
             idle_.emplace(sz, b);
             idle_bytes_ += sz;
             in_use_ -= sz;
-            over = idle_bytes_ > idle_cap();
+            keep = keep_idle();
+            over = idle_bytes_ > keep;
         }
-        if (over) trim(idle_cap());
+        if (over) trim(keep);
     }
     void drop(void *b, size_t sz) {
         (void)hipFree(b);
@@ -120,27 +123,39 @@ class ChunkPool {
     }
 
   private:
-    // Idle chunks kept for reuse: a quarter of the device's memory (or
-    // $FQZ5_ARENA_IDLE_GB).  Trimming calls hipFree, which waits for every
-    // kernel on the device to finish: a trim in the middle of a step stalls
-    // the calling thread behind the longest chain (measured: the names
-    // helper of a -3 step blocked ~150 ms), so steady state must not trim.
-    static size_t idle_cap() {
-        static const size_t c = [] {
-            if (const char *e = std::getenv("FQZ5_ARENA_IDLE_GB")) return size_t(std::atof(e) * 1e9);
+    // Idle chunks kept for reuse: a quarter of the device's memory, or the
+    // most the work has had in use at once when that is more (at most 70 %
+    // of the device); $FQZ5_ARENA_IDLE_GB fixes it.  Trimming calls hipFree,
+    // which waits for every kernel on the device to finish: a trim in the
+    // middle of a step stalls the calling thread behind the longest chain
+    // (measured: the names helper of a -3 step blocked ~150 ms), and a pool
+    // trimmed below a step's peak allocates it again next step (-5 NovaSeq:
+    // peak 102 GB in use against a 72 GB cap), so steady state must not trim.
+    static size_t dev_total() {
+        static const size_t t = [] {
             size_t fr = 0, tot = 0;
             if (hipMemGetInfo(&fr, &tot) != hipSuccess || !tot) tot = size_t(64) << 30;
-            return tot / 4;
+            return tot;
         }();
-        return c;
+        return t;
+    }
+    size_t keep_idle() const {   // under m_
+        static const long fixed = [] {
+            const char *e = std::getenv("FQZ5_ARENA_IDLE_GB");
+            return e ? long(std::atof(e) * 1e9) : -1L;
+        }();
+        if (fixed >= 0) return size_t(fixed);
+        const size_t tot = dev_total();
+        return std::min(tot / 10 * 7, std::max(tot / 4, max_use_));
     }
     void use(size_t n) {   // under m_
         in_use_ += n;
         use_peak_ = std::max(use_peak_, in_use_);
+        max_use_ = std::max(max_use_, in_use_);
     }
     std::mutex m_;
     std::multimap<size_t, void *> idle_;
-    size_t idle_bytes_ = 0, held_ = 0, peak_ = 0, in_use_ = 0, use_peak_ = 0;
+    size_t idle_bytes_ = 0, held_ = 0, peak_ = 0, in_use_ = 0, use_peak_ = 0, max_use_ = 0;
 };
 
 // A bump arena over pool chunks; reset() rewinds and returns the chunks.
@@ -347,7 +362,7 @@ struct EventPair {
 struct GpuCtx {
     KernelProfile prof;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;   // second queue for concurrent launches
+    hipStream_t stream2 = nullptr;   // second queue for concurrent launches (fork() makes it)
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     DevArena arena;
     // scratch of one codec's batch (its event tables, sort and scan
@@ -359,6 +374,7 @@ struct GpuCtx {
     PinnedArena staging;
     int device = 0;
     int cus = 256;                   // compute units (MI355X: 256)
+    int prio_ = 0;                   // the streams' priority
 
     // Dynamic LDS for a launch of `jobs` single-wave chain workgroups: while
     // there are no more chains than CUs, ask for more than half a CU's LDS
@@ -387,9 +403,8 @@ struct GpuCtx {
         FQZ5_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         int lo = 0, hi = 0;
         FQZ5_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        const int prio = high_prio ? hi : lo;
-        FQZ5_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio));
-        FQZ5_HIP(hipStreamCreateWithPriority(&stream2, hipStreamNonBlocking, prio));
+        prio_ = high_prio ? hi : lo;
+        FQZ5_HIP(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_));
         FQZ5_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
         FQZ5_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
     }
@@ -399,13 +414,20 @@ struct GpuCtx {
         if (stream2) (void)hipStreamDestroy(stream2);
         if (stream) (void)hipStreamDestroy(stream);
     }
-    // stream2 waits for everything queued on stream so far
+    // stream2 waits for everything queued on stream so far.  stream2 is
+    // made here, on first use: HIP maps streams onto a fixed number of
+    // hardware queues, and an idle stream2 per context would take one that
+    // a working stream then has to share (its kernels queue behind the
+    // other stream's: -5 NovaSeq's quality chains waited ~330 ms behind a
+    // sequence model).
     void fork() {
+        if (!stream2) FQZ5_HIP(hipStreamCreateWithPriority(&stream2, hipStreamNonBlocking, prio_));
         FQZ5_HIP(hipEventRecord(fork_ev, stream));
         FQZ5_HIP(hipStreamWaitEvent(stream2, fork_ev, 0));
     }
     // stream waits for everything queued on stream2 so far
     void join() {
+        if (!stream2) return;
         FQZ5_HIP(hipEventRecord(join_ev, stream2));
         FQZ5_HIP(hipStreamWaitEvent(stream, join_ev, 0));
     }

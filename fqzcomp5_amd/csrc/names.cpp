@@ -131,7 +131,14 @@ void name_add_lzp(GpuCtx &g, NameEnc &E, const uint8_t *d_names, std::vector<Lzp
 }
 
 void name_add_requests(GpuCtx &g, NameEnc &E, const std::vector<LzpEncReq> &lz,
-                       std::vector<CompressReq> &reqs) {
+                       std::vector<CompressReq> &reqs, const NameEnc *lead) {
+    if (lead) {                                     // the same comments and flags
+        E.lzp = lead->lzp;
+        E.req_main = lead->req_main;
+        E.req_flag = lead->req_flag;
+        if (E.tok_ok) tok3_add_requests(g, E.tok, reqs);
+        return;
+    }
     if (E.lzp >= 0) {                               // rans_compress_4x16(lzp_out, .., 5)
         CompressReq r;
         r.d_in = lz[size_t(E.lzp)].d_out;
@@ -232,12 +239,32 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
             err0 = std::current_exception();
         }
     });
+    // tok3's tokens do not depend on its level (the level only picks each
+    // stream's rANS methods, tokenise_name3.c:1275-1366): candidates of one
+    // section and strategy tokenise once and copy the rest
+    std::vector<std::vector<size_t>> groups;
+    for (size_t k : late) {
+        auto same = [&](const std::vector<size_t> &gr) {
+            const size_t j = gr[0];
+            return h_names[j] == h_names[k] && lens[j] == lens[k] &&
+                   name_strat(methods[j]) == name_strat(methods[k]);
+        };
+        auto it = std::find_if(groups.begin(), groups.end(), same);
+        if (it == groups.end()) groups.push_back({k});
+        else it->push_back(k);
+    }
     try {
-        on_threads(late.size(), [&](size_t i) {
-            const size_t k = late[i];
+        on_threads(groups.size(), [&](size_t i) {
+            const std::vector<size_t> &gr = groups[i];
+            const size_t k = gr[0];
             if (ready) FQZ5_HIP(hipEventSynchronize((*ready)[k]));
             name_prepare(h_names[k], lens[k], name_strat(methods[k]), name_level(methods[k]),
                          jobs[k]);
+            for (size_t x = 1; x < gr.size(); x++) {
+                NameEnc &E = jobs[gr[x]];
+                E = jobs[k];
+                E.level = E.tok.level = name_level(methods[gr[x]]);
+            }
         });
     } catch (...) {
         gpu_early.join();
@@ -247,10 +274,12 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
     gpu_early.join();
     if (err0) std::rethrow_exception(err0);
     const double t1b = trace() ? now_ms() : 0;
-    for (size_t k : late) name_add_lzp(g, jobs[k], d_names[k], lz1);
+    for (const auto &gr : groups) name_add_lzp(g, jobs[gr[0]], d_names[gr[0]], lz1);
     if (!lz1.empty()) lzp_encode_batch(g, lz1);
     const double t2 = trace() ? now_ms() : 0;
-    for (size_t k : late) name_add_requests(g, jobs[k], lz1, rq1);
+    for (const auto &gr : groups)
+        for (size_t x = 0; x < gr.size(); x++)
+            name_add_requests(g, jobs[gr[x]], lz1, rq1, x ? &jobs[gr[0]] : nullptr);
     if (!rq1.empty()) compress_batch(g, rq1);
     const double t3 = trace() ? now_ms() : 0;
     for (size_t k : early) name_assemble(g, jobs[k], rq0);

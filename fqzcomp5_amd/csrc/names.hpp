@@ -52,9 +52,11 @@ void name_prepare(const uint8_t *h_names, uint32_t len, int strat, int level, Na
 // the comments, uploaded).
 void name_add_lzp(GpuCtx &g, NameEnc &E, const uint8_t *d_names, std::vector<LzpEncReq> &lz);
 // Stage 2, after lzp_encode_batch: every rANS request (tok3 streams, lzp
-// outputs at order 5, flags at order 129).
+// outputs at order 5, flags at order 129).  lead: a strat-2 candidate of the
+// same section whose requests E shares for everything but the tok3 streams
+// (E's level differs).
 void name_add_requests(GpuCtx &g, NameEnc &E, const std::vector<LzpEncReq> &lz,
-                       std::vector<CompressReq> &reqs);
+                       std::vector<CompressReq> &reqs, const NameEnc *lead = nullptr);
 // Stage 3, after compress_batch: E.out, E.ok.
 void name_assemble(GpuCtx &g, NameEnc &E, const std::vector<CompressReq> &reqs);
 // All stages for a set of candidates on context g (hosts stages on up to

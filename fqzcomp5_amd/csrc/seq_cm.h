@@ -39,6 +39,7 @@ struct SeqJob {
 hipError_t launch_seq_heads(const SeqJob &j, hipStream_t s);
 hipError_t launch_seq_runs(const SeqJob &j, hipStream_t s);       // run starts, cnt
 hipError_t launch_seq_ctx(const SeqJob &j, hipStream_t s);        // keys / values
+hipError_t launch_seq_ev(const SeqJob &j, hipStream_t s);         // byte -> event index
 hipError_t launch_seq_model(const SeqJob &j, hipStream_t s);      // context events -> rec
 hipError_t launch_seq_side(const SeqJob &j, hipStream_t s);       // run / literal / state -> rec
 

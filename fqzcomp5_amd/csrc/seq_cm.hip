@@ -18,6 +18,9 @@
 //   side          run-length digits, literal bytes and class switches
 // Decoder.  Each symbol selects the next context, so a block is one chain
 // (k_seq_dec).
+#include <algorithm>
+#include <cstdlib>
+
 #include "fqz_model.hpp"
 #include "seq_cm.h"
 
@@ -140,12 +143,17 @@ __global__ void k_seq_ev(SeqJob J) {
     J.ev[p] = sym_event(J, p);
 }
 
-// one thread per context: the head of its run in the sorted order walks it
-__global__ void k_seq_model(SeqJob J) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= J.nkeys) return;
+// The model pass: per context, the head of its run in the sorted order walks
+// it.  One lane per run rather than one per sorted event: with
+// one lane per event only the run heads work (one lane in ~5 at SEQ12B's
+// 89M events over 16.7M contexts) and the waves that hold them stay
+// resident for their longest walk.  A workgroup takes a tile of `span`
+// sorted events (about 256 runs), lists the heads in it in LDS and walks
+// them 256 at a time; a run that starts in the tile may end past it.
+constexpr uint32_t SEQ_SPAN_MAX = 8192;
+
+DEV void seq_walk(const SeqJob &J, uint32_t i) {
     const uint32_t key = J.skey[i];
-    if (key > J.mask || (i > 0 && J.skey[i - 1] == key)) return;
     uint32_t F = 0x01010101u;
     for (uint32_t j = i; j < J.nkeys && J.skey[j] == key; j++) {
         const uint64_t v = J.sval[j];
@@ -158,6 +166,44 @@ __global__ void k_seq_model(SeqJob J) {
         }
         F = sm4_bump(F, sym, tot);
     }
+}
+
+// (the one-lane-per-event form, $FQZ5_SEQ_MODEL_EVENTS: experiments)
+__global__ void k_seq_model(SeqJob J) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= J.nkeys) return;
+    const uint32_t key = J.skey[i];
+    if (key > J.mask || (i > 0 && J.skey[i - 1] == key)) return;
+    seq_walk(J, i);
+}
+
+__global__ __launch_bounds__(256) void k_seq_model_runs(SeqJob J, uint32_t span) {
+    __shared__ uint32_t heads[SEQ_SPAN_MAX];
+    __shared__ uint32_t wcnt[4], nh_s;
+    const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63u;
+    const uint64_t base = uint64_t(blockIdx.x) * span;
+    if (t == 0) nh_s = 0;
+    __syncthreads();
+    for (uint32_t c = 0; c < span; c += 256) {
+        const uint64_t i = base + c + t;
+        bool h = false;
+        if (i < J.nkeys) {
+            const uint32_t key = J.skey[i];
+            h = key <= J.mask && (i == 0 || J.skey[i - 1] != key);
+        }
+        const uint64_t m = __ballot(h);
+        if (l == 0) wcnt[w] = uint32_t(__popcll(m));
+        __syncthreads();
+        uint32_t off = nh_s;
+        for (uint32_t q = 0; q < w; q++) off += wcnt[q];
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+        if (h) heads[off + r] = uint32_t(i);
+        __syncthreads();
+        if (t == 0) nh_s += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        __syncthreads();
+    }
+    const uint32_t nh = nh_s;
+    for (uint32_t h = t; h < nh; h += 256) seq_walk(J, heads[h]);
 }
 
 // the run-length, literal and state models over the runs in stream order
@@ -737,9 +783,24 @@ hipError_t launch_seq_ctx(const SeqJob &j, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_seq_model(const SeqJob &j, hipStream_t s) {
+hipError_t launch_seq_ev(const SeqJob &j, hipStream_t s) {
     if (j.n) hipLaunchKernelGGL(k_seq_ev, grid_of(j.n), dim3(256), 0, s, j);
-    if (j.nkeys) hipLaunchKernelGGL(k_seq_model, grid_of(j.nkeys), dim3(256), 0, s, j);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_model(const SeqJob &j, hipStream_t s) {
+    if (!j.nkeys) return hipGetLastError();
+    static const bool per_event = std::getenv("FQZ5_SEQ_MODEL_EVENTS") != nullptr;
+    if (per_event) {
+        hipLaunchKernelGGL(k_seq_model, grid_of(j.nkeys), dim3(256), 0, s, j);
+        return hipGetLastError();
+    }
+    // ~256 runs per tile: the mean run is the events over the contexts
+    const uint64_t nctx = std::min<uint64_t>(uint64_t(j.mask) + 1, j.nkeys);
+    const uint64_t run = std::min<uint64_t>((j.nkeys + nctx - 1) / nctx, SEQ_SPAN_MAX / 256);
+    const uint32_t span = uint32_t(256 * std::max<uint64_t>(run, 1));
+    hipLaunchKernelGGL(k_seq_model_runs, dim3(unsigned((j.nkeys + span - 1) / span)), dim3(256), 0, s,
+                       j, span);
     return hipGetLastError();
 }
 

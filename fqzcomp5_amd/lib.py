@@ -16,11 +16,11 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 # helper contexts' streams need queues of their own (bench.py); effective
 # only when nothing in the process has initialised HIP yet
 # (the rule of capi.cpp's hw_queues_default: FQZ5_HW_QUEUES as given, else
-# an unset value or HIP's default of 4 raised to 16, any other value kept)
+# an unset value or HIP's default of 4 raised to 20, any other value kept)
 if os.environ.get("FQZ5_HW_QUEUES"):
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ["FQZ5_HW_QUEUES"]
 elif os.environ.get("GPU_MAX_HW_QUEUES", "") in ("", "4"):
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    os.environ["GPU_MAX_HW_QUEUES"] = "20"
 
 _libc = C.CDLL(None)
 _libc.free.argtypes = [C.c_void_p]
