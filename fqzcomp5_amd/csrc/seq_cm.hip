@@ -144,13 +144,24 @@ __global__ void k_seq_ev(SeqJob J) {
 }
 
 // The model pass: per context, the head of its run in the sorted order walks
-// it.  One lane per run rather than one per sorted event: with
-// one lane per event only the run heads work (one lane in ~5 at SEQ12B's
-// 89M events over 16.7M contexts) and the waves that hold them stay
-// resident for their longest walk.  A workgroup takes a tile of `span`
-// sorted events (about 256 runs), lists the heads in it in LDS and walks
-// them 256 at a time; a run that starts in the tile may end past it.
-constexpr uint32_t SEQ_SPAN_MAX = 8192;
+// it (its counts are a serial recurrence over its events).  The walks are
+// latency-bound (a dependent load of the next event per step), so their
+// length, not the event count, sets the kernel's time: the contexts that
+// every record starts from are the longest (fqzcomp5.c:1176-1199: each
+// record restarts at the seed context, so it alone holds one event per
+// record, ~300k in a 100 MB block; the next ones a quarter of that, ...).
+// Walked one step per ~0.8 us that one run took the whole ~250 ms launch.
+//   short runs  one lane each (the lane walks its run)
+//   long runs   one wave each, 64 events per round: a coalesced load of the
+//               round's events, the count recurrence over them in scalar
+//               registers (each lane takes its event's counts with
+//               v_writelane), then every lane's record write in parallel
+// A workgroup takes a tile of `span` sorted events (about 256 runs), lists
+// the heads in it in LDS, walks its long runs a wave each and then its short
+// runs a lane each; a run that starts in the tile may end past it (the last
+// one counts as long).
+constexpr uint32_t SEQ_SPAN_MAX = 4096;
+constexpr uint32_t SEQ_LONG = 48;             // events: a wave rather than a lane
 
 DEV void seq_walk(const SeqJob &J, uint32_t i) {
     const uint32_t key = J.skey[i];
@@ -168,6 +179,53 @@ DEV void seq_walk(const SeqJob &J, uint32_t i) {
     }
 }
 
+// Events U.. of a round: lane U takes the counts before its event, then
+// they count it (scalar registers; the lane index is an immediate, as gfx9's
+// constant bus allows one SGPR per VALU op).
+template <int U>
+DEV void seq_wave_steps(uint32_t cnt, uint32_t sym, uint32_t &F, uint32_t &myF) {
+    if constexpr (U < 64) {
+        if (U >= cnt) return;
+        const uint32_t su = uint32_t(__builtin_amdgcn_readlane(int(sym), U));
+        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(myF) : "s"(F), "i"(U));
+        const uint32_t tot = (F & 255u) + ((F >> 8) & 255u) + ((F >> 16) & 255u) + (F >> 24);
+        F += 1u << (8u * su);
+        if (tot >= 255u) F -= (F >> 1) & 0x7F7F7F7Fu;
+        seq_wave_steps<U + 1>(cnt, sym, F, myF);
+    }
+}
+
+// the run at i by all 64 lanes of the calling wave (i uniform)
+DEV void seq_walk_wave(const SeqJob &J, uint32_t i) {
+    const uint32_t l = threadIdx.x & 63u;
+    const uint32_t key = __builtin_amdgcn_readfirstlane(J.skey[i]);
+    uint32_t F = 0x01010101u;
+    uint32_t j = i + l;
+    bool in = j < J.nkeys && J.skey[j] == key;
+    uint64_t v = in ? J.sval[j] : 0ull;
+    for (;;) {
+        const uint64_t m = __ballot(in);
+        const uint32_t cnt = uint32_t(__popcll(m));   // a prefix of the lanes (sorted keys)
+        if (!cnt) break;
+        // the next round's events load while this round's recurrence runs
+        const uint32_t jn = j + 64u;
+        const bool in_n = cnt == 64u && jn < J.nkeys && J.skey[jn] == key;
+        const uint64_t vn = in_n ? J.sval[jn] : 0ull;
+        const uint32_t sym = uint32_t(v) & 3u;
+        uint32_t myF = 0;
+        seq_wave_steps<0>(cnt, sym, F, myF);
+        if (in) {
+            const uint32_t ord = uint32_t(v >> 8);
+            if (!(ord & 1u))
+                J.rec[J.ev[ord >> 1]] = rc_rec((myF >> (8u * sym)) & 255u, sm4_cum(myF, sym), sm4_total(myF));
+        }
+        if (cnt < 64u) break;
+        j = jn;
+        in = in_n;
+        v = vn;
+    }
+}
+
 // (the one-lane-per-event form, $FQZ5_SEQ_MODEL_EVENTS: experiments)
 __global__ void k_seq_model(SeqJob J) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -179,6 +237,7 @@ __global__ void k_seq_model(SeqJob J) {
 
 __global__ __launch_bounds__(256) void k_seq_model_runs(SeqJob J, uint32_t span) {
     __shared__ uint32_t heads[SEQ_SPAN_MAX];
+    __shared__ uint8_t lng[SEQ_SPAN_MAX];
     __shared__ uint32_t wcnt[4], nh_s;
     const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63u;
     const uint64_t base = uint64_t(blockIdx.x) * span;
@@ -203,7 +262,20 @@ __global__ __launch_bounds__(256) void k_seq_model_runs(SeqJob J, uint32_t span)
         __syncthreads();
     }
     const uint32_t nh = nh_s;
-    for (uint32_t h = t; h < nh; h += 256) seq_walk(J, heads[h]);
+    for (uint32_t h = t; h < nh; h += 256)
+        lng[h] = (h + 1 == nh || heads[h + 1] - heads[h] >= SEQ_LONG) ? 1 : 0;
+    __syncthreads();
+    // long runs: wave w takes those at list positions = w mod 4
+    for (uint32_t c = 0; c < nh; c += 64) {
+        uint64_t m = __ballot(c + l < nh && lng[c + l] && ((c + l) & 3u) == w);
+        while (m) {
+            const uint32_t b = uint32_t(__builtin_ctzll(m));
+            m &= m - 1;
+            seq_walk_wave(J, heads[c + b]);
+        }
+    }
+    for (uint32_t h = t; h < nh; h += 256)
+        if (!lng[h]) seq_walk(J, heads[h]);
 }
 
 // the run-length, literal and state models over the runs in stream order
