@@ -55,7 +55,18 @@ double now_ms() {
 }
 }  // namespace
 
-void name_prepare(const uint8_t *h, uint32_t name_len, int strat, int level, NameEnc &E) {
+void name_prepare(const uint8_t *h, uint32_t name_len, int strat, int level, NameEnc &E,
+                  bool pipelined) {
+    name_split(h, name_len, strat, level, E);
+    name_tokenise(E, pipelined, nullptr);
+}
+
+void name_tokenise(NameEnc &E, bool pipelined, const T3Found *found) {
+    if (E.strat == 0) return;
+    E.tok_ok = tok3_tokenise(E.ids.data(), int(E.ids.size()), E.level, 0, E.tok, pipelined, found);
+}
+
+void name_split(const uint8_t *h, uint32_t name_len, int strat, int level, NameEnc &E) {
     E = NameEnc();
     E.strat = strat;
     E.level = level;
@@ -63,7 +74,6 @@ void name_prepare(const uint8_t *h, uint32_t name_len, int strat, int level, Nam
     if (strat == 0) return;                         // lzp + rANS only
     if (strat == 1) {
         E.ids.assign(h, h + name_len);
-        E.tok_ok = tok3_tokenise(E.ids.data(), int(name_len), level, 0, E.tok);
         return;
     }
     // strat 2: split each name into the read id (less a /1 or /2 suffix),
@@ -108,7 +118,6 @@ void name_prepare(const uint8_t *h, uint32_t name_len, int strat, int level, Nam
     }
     E.ids.resize(size_t(cp1 - E.ids.data()));
     E.comments.resize(size_t(cp2 - E.comments.data()));
-    E.tok_ok = tok3_tokenise(E.ids.data(), int(E.ids.size()), level, 0, E.tok);
 }
 
 void name_add_lzp(GpuCtx &g, NameEnc &E, const uint8_t *d_names, std::vector<LzpEncReq> &lz) {
@@ -220,6 +229,55 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
         (name_strat(methods[k]) == 0 ? early : late).push_back(k);
     std::vector<LzpEncReq> lz0, lz1;
     std::vector<CompressReq> rq0, rq1;
+    // tok3's tokens do not depend on its level (the level only picks each
+    // stream's rANS methods, tokenise_name3.c:1275-1366): candidates of one
+    // section and strategy tokenise once and copy the rest
+    std::vector<std::vector<size_t>> groups;
+    for (size_t k : late) {
+        auto same = [&](const std::vector<size_t> &gr) {
+            const size_t j = gr[0];
+            return h_names[j] == h_names[k] && lens[j] == lens[k] &&
+                   name_strat(methods[j]) == name_strat(methods[k]);
+        };
+        auto it = std::find_if(groups.begin(), groups.end(), same);
+        if (it == groups.end()) groups.push_back({k});
+        else it->push_back(k);
+    }
+    // every section's trie searches in one GPU batch (tok3_search.hip), so
+    // the host threads only code the tokens; a section the batch could not
+    // take searches on the host ($FQZ5_TOK3_GPU=0: all of them)
+    static const bool gpu_search = [] {
+        const char *e = std::getenv("FQZ5_TOK3_GPU");
+        return !e || std::atoi(e) != 0;
+    }();
+    std::vector<Tok3SearchJob> sj(groups.size());
+    for (size_t i = 0; i < groups.size(); i++) {
+        // the sections themselves, on the device: strat 2 searches the read
+        // ids in place (split mode), strat 1 the names
+        const size_t k = groups[i][0];
+        sj[i].h_blk = reinterpret_cast<const char *>(h_names[k]);
+        sj[i].d_blk = d_names[k];
+        sj[i].len = lens[k];
+        sj[i].split = name_strat(methods[k]) == 2;
+    }
+    // the ids (strat 2) or names (strat 1) of each section on the host, on
+    // the host threads; the batch search waits for the sections' host
+    // copies only through h_blk's last bytes
+    on_threads(groups.size(), [&](size_t i) {
+        const size_t k = groups[i][0];
+        if (ready) FQZ5_HIP(hipEventSynchronize((*ready)[k]));
+        name_split(h_names[k], lens[k], name_strat(methods[k]), name_level(methods[k]), jobs[k]);
+    });
+    const double ts = trace() ? now_ms() : 0;
+    if (gpu_search && !groups.empty()) {
+        std::vector<Tok3SearchJob *> sp;
+        for (size_t i = 0; i < groups.size(); i++)
+            if (lens[groups[i][0]]) sp.push_back(&sj[i]);
+        if (!sp.empty()) tok3_search_batch(g, sp);
+    }
+    const double tsd = trace() ? now_ms() : 0;
+    size_t on_host = 0;
+    for (size_t i = 0; i < groups.size(); i++) on_host += !sj[i].ok;
     double t_early = 0;
     std::exception_ptr err0;
     std::thread gpu_early([&] {
@@ -239,27 +297,15 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
             err0 = std::current_exception();
         }
     });
-    // tok3's tokens do not depend on its level (the level only picks each
-    // stream's rANS methods, tokenise_name3.c:1275-1366): candidates of one
-    // section and strategy tokenise once and copy the rest
-    std::vector<std::vector<size_t>> groups;
-    for (size_t k : late) {
-        auto same = [&](const std::vector<size_t> &gr) {
-            const size_t j = gr[0];
-            return h_names[j] == h_names[k] && lens[j] == lens[k] &&
-                   name_strat(methods[j]) == name_strat(methods[k]);
-        };
-        auto it = std::find_if(groups.begin(), groups.end(), same);
-        if (it == groups.end()) groups.push_back({k});
-        else it->push_back(k);
-    }
+    // fewer host-searched sections than host threads: each tokenises on two
+    // (its trie searches ahead on the second), so its names take ~60 % as long
+    const size_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const bool pipelined = on_host < hw;
     try {
         on_threads(groups.size(), [&](size_t i) {
             const std::vector<size_t> &gr = groups[i];
             const size_t k = gr[0];
-            if (ready) FQZ5_HIP(hipEventSynchronize((*ready)[k]));
-            name_prepare(h_names[k], lens[k], name_strat(methods[k]), name_level(methods[k]),
-                         jobs[k]);
+            name_tokenise(jobs[k], pipelined, sj[i].ok ? sj[i].found.data() : nullptr);
             for (size_t x = 1; x < gr.size(); x++) {
                 NameEnc &E = jobs[gr[x]];
                 E = jobs[k];
@@ -285,11 +331,12 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
     for (size_t k : early) name_assemble(g, jobs[k], rq0);
     for (size_t k : late) name_assemble(g, jobs[k], rq1);
     if (trace())
-        std::fprintf(stderr, "names encode: %zu candidates, tokenise %.1f ms (TLZP3 on the GPU "
-                     "beside it: done at %.1f ms), waited %.1f ms, lzp %.1f ms, %zu rANS "
-                     "streams %.1f ms, assemble %.1f ms\n", jobs.size(), t1 - t0,
-                     early.empty() ? 0.0 : t_early - t0, t1b - t1, t2 - t1b,
-                     rq0.size() + rq1.size(), t3 - t2, now_ms() - t3);
+        std::fprintf(stderr, "names encode: %zu candidates, split %.1f ms, GPU trie searches "
+                     "%.1f ms (%zu of %zu sections on the host), tokenise %.1f ms (TLZP3 on the "
+                     "GPU beside it: done at %.1f ms), waited %.1f ms, lzp %.1f ms, %zu rANS "
+                     "streams %.1f ms, assemble %.1f ms\n", jobs.size(), ts - t0, tsd - ts, on_host,
+                     groups.size(), t1 - tsd, early.empty() ? 0.0 : t_early - t0, t1b - t1,
+                     t2 - t1b, rq0.size() + rq1.size(), t3 - t2, now_ms() - t3);
 }
 
 // ---------------------------------------------------------------------------

@@ -47,7 +47,12 @@ struct NameEnc {
 
 // Host stage (any thread): copy / split and tokenise.  h_names: the block's
 // names ('\0' after each), len bytes.
-void name_prepare(const uint8_t *h_names, uint32_t len, int strat, int level, NameEnc &E);
+void name_prepare(const uint8_t *h_names, uint32_t len, int strat, int level, NameEnc &E,
+                  bool pipelined = false);
+// = name_split (the copy / split into E.ids) + name_tokenise (found: the
+// names' trie searches done beforehand, tok3_search_batch)
+void name_split(const uint8_t *h_names, uint32_t len, int strat, int level, NameEnc &E);
+void name_tokenise(NameEnc &E, bool pipelined, const T3Found *found);
 // Device stage 1: the lzp inputs (strat 0: the names at d_names; strat 2:
 // the comments, uploaded).
 void name_add_lzp(GpuCtx &g, NameEnc &E, const uint8_t *d_names, std::vector<LzpEncReq> &lz);

@@ -19,12 +19,18 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <thread>
 #include <vector>
 
 #include "../../include/fqz5_mi355x.h"
 #include "rans_codec.hpp"
 #include "rans_format.hpp"
 #include "tok3.hpp"
+#include "tok3_search.h"
+#include "names.hpp"
 
 namespace fqz5 {
 void fqz5_set_error(const char *msg);   // capi.cpp
@@ -214,6 +220,9 @@ struct Trie {
     }
 };
 
+// search_trie's results for one name (Trie::search here, or k_t3_find)
+using Found = T3Found;
+
 // ---------------------------------------------------------------------------
 struct Encoder {
     std::vector<std::vector<uint8_t>> desc = std::vector<std::vector<uint8_t>>(MAX_TBLOCKS);
@@ -257,9 +266,16 @@ struct Encoder {
 
     // encode_name (:697-1020), mode 1
     bool name(char *nm, int len) {
-        int is_fixed, fixed_len, exact;
+        Found f;
+        f.pnum = trie.search(nm, size_t(len), uint32_t(counter), &f.exact, &f.is_fixed, &f.fixed_len);
+        return name(nm, len, f);
+    }
+    // ... with the trie search's results for this name
+    bool name(char *nm, int len, const Found &f) {
+        int is_fixed = f.is_fixed;
+        const int fixed_len = f.fixed_len, exact = f.exact;
         const int cnum = counter++;
-        int pnum = trie.search(nm, size_t(len), uint32_t(cnum), &exact, &is_fixed, &fixed_len);
+        int pnum = f.pnum;
         if (pnum < 0) pnum = cnum ? cnum - 1 : 0;
         Last &C = lc[size_t(cnum)];
         const Last &P = lc[size_t(pnum)];
@@ -433,7 +449,44 @@ int put_varint(uint8_t *out, uint32_t v) {
 
 }  // namespace
 
-bool tok3_tokenise(char *blk, int len, int level, int use_arith, Tok3Enc &T) {
+// The names loop in two threads: the trie search of each name (~60 % of the
+// time, cache misses) runs ahead on a helper thread and publishes its
+// results in batches; this thread codes each name once its search is done.
+// The same names in the same order, so the same streams.
+static bool tokenise_pipelined(Encoder &E, char *blk, int len) {
+    std::vector<uint32_t> st, ln;                      // names (:1487-1505)
+    for (int i = 0, j = 0; i < len; j = ++i) {
+        while (i < len && static_cast<signed char>(blk[i]) >= ' ') i++;
+        if (i >= len) break;
+        if (blk[i] != '\0' && blk[i] != '\n') return false;
+        blk[i] = '\0';
+        st.push_back(uint32_t(j));
+        ln.push_back(uint32_t(i - j));
+    }
+    const size_t nn = st.size();
+    std::vector<Found> found(nn);
+    std::atomic<size_t> done{0};
+    std::atomic<bool> stop{false};
+    constexpr size_t BATCH = 256;
+    std::thread th([&] {
+        for (size_t k = 0; k < nn && !stop.load(std::memory_order_relaxed); k++) {
+            Found &f = found[k];
+            f.pnum = E.trie.search(blk + st[k], ln[k], uint32_t(k), &f.exact, &f.is_fixed, &f.fixed_len);
+            if ((k + 1) % BATCH == 0 || k + 1 == nn) done.store(k + 1, std::memory_order_release);
+        }
+    });
+    bool ok = true;
+    for (size_t k = 0; k < nn && ok; k++) {
+        while (done.load(std::memory_order_acquire) <= k) std::this_thread::yield();
+        ok = E.name(blk + st[k], int(ln[k]), found[k]);
+    }
+    stop.store(true);
+    th.join();
+    return ok;
+}
+
+bool tok3_tokenise(char *blk, int len, int level, int use_arith, Tok3Enc &T, bool pipelined,
+                   const T3Found *found) {
     T = Tok3Enc();
     T.level = level;
     T.use_arith = use_arith;
@@ -445,19 +498,32 @@ bool tok3_tokenise(char *blk, int len, int level, int use_arith, Tok3Enc &T) {
     if (nreads <= 0 || nreads > 10000000) return false;     // create_context (:172-187)
     Encoder E;
     E.lc.resize(size_t(nreads) + 1);
-    E.trie.nodes.reserve(size_t(len) / 4 + 16);
+    if (!found) E.trie.nodes.reserve(size_t(len) / 4 + 16);
     // the trie of all names (:1469-1482) is built inside the search (Trie::
     // search); its loop's line ends give last_start (it cannot fail: its
     // lines hold no byte >= 0x80)
     for (i = len - 1; i >= 0; i--)
         if (blk[i] <= '\n') { last_start = i + 1; break; }
     T.last_start = last_start;
-    for (i = j = 0; i < len; j = ++i) {                // names (:1487-1505)
-        while (i < len && static_cast<signed char>(blk[i]) >= ' ') i++;
-        if (i >= len) break;
-        if (blk[i] != '\0' && blk[i] != '\n') return false;
-        blk[i] = '\0';
-        if (!E.name(&blk[j], i - j)) return false;
+    if (found) {                                      // the searches done (tok3_search_batch)
+        size_t k = 0;
+        for (i = j = 0; i < len; j = ++i) {
+            while (i < len && static_cast<signed char>(blk[i]) >= ' ') i++;
+            if (i >= len) break;
+            if (blk[i] != '\0' && blk[i] != '\n') return false;
+            blk[i] = '\0';
+            if (!E.name(&blk[j], i - j, found[k++])) return false;
+        }
+    } else if (!pipelined) {
+        for (i = j = 0; i < len; j = ++i) {            // names (:1487-1505)
+            while (i < len && static_cast<signed char>(blk[i]) >= ' ') i++;
+            if (i >= len) break;
+            if (blk[i] != '\0' && blk[i] != '\n') return false;
+            blk[i] = '\0';
+            if (!E.name(&blk[j], i - j)) return false;
+        }
+    } else if (!tokenise_pipelined(E, blk, len)) {
+        return false;
     }
     // drop the type stream of a column that is all MATCH bar its first
     // entry while the column has other streams (:1531-1553)
@@ -476,6 +542,157 @@ bool tok3_tokenise(char *blk, int len, int level, int use_arith, Tok3Enc &T) {
     T.max_tok = E.max_tok;
     T.desc = std::move(E.desc);
     return true;
+}
+
+bool tok3_name_extents(const char *blk, uint32_t len, std::vector<uint32_t> &st,
+                       std::vector<uint32_t> &ln) {
+    st.clear();
+    ln.clear();
+    for (uint32_t i = 0, j = 0; i < len; j = ++i) {
+        while (i < len && static_cast<signed char>(blk[i]) >= ' ') i++;
+        if (i >= len) break;
+        if (blk[i] != '\0' && blk[i] != '\n') return false;
+        st.push_back(j);
+        ln.push_back(i - j);
+    }
+    return !st.empty() && st.size() <= 10000000u;    // create_context's limits (:172-187)
+}
+
+void tok3_search_batch(GpuCtx &g, std::vector<Tok3SearchJob *> &jobs) {
+    // each block up to its last terminator (the loop ignores the rest)
+    std::vector<uint32_t> off;
+    std::vector<Tok3SearchJob *> run;
+    uint64_t nbytes = 0;
+    for (Tok3SearchJob *J : jobs) {
+        J->ok = false;
+        J->found.clear();
+        uint32_t tl = J->len;
+        while (tl > 0 && J->h_blk[tl - 1] != '\0' && J->h_blk[tl - 1] != '\n') tl--;
+        // (split: the section's last name must end in '\0', as name_split's
+        // last id does)
+        if (J->split && (tl != J->len || !J->d_blk)) continue;
+        if (!tl || nbytes + tl + 64 >= (1ull << 31)) continue;
+        off.push_back(uint32_t(nbytes));
+        nbytes += tl;
+        J->len = tl;
+        run.push_back(J);
+    }
+    if (run.empty()) return;
+    off.push_back(uint32_t(nbytes));
+    // (FQZ5_STEP_TRACE: the stages' GPU time from events on the stream)
+    static const bool trace = std::getenv("FQZ5_STEP_TRACE") != nullptr;
+    std::vector<hipEvent_t> ev;
+    auto mark = [&] {
+        if (!trace) return;
+        hipEvent_t e;
+        FQZ5_HIP(hipEventCreate(&e));
+        FQZ5_HIP(hipEventRecord(e, g.stream));
+        ev.push_back(e);
+    };
+    const auto h0 = std::chrono::steady_clock::now();
+    mark();
+    const uint32_t B = uint32_t(nbytes), S = uint32_t(run.size());
+    T3Batch b{};
+    uint8_t *bytes = g.arena.alloc_n<uint8_t>(size_t(B) + 64);
+    g.memset0(bytes + B, 64);
+    for (size_t r = 0; r < run.size(); r++) {
+        Tok3SearchJob &J = *run[r];
+        if (J.d_blk) {
+            FQZ5_HIP(hipMemcpyAsync(bytes + off[r], J.d_blk, J.len, hipMemcpyDeviceToDevice, g.stream));
+        } else if (J.h_pinned) {
+            FQZ5_HIP(hipMemcpyAsync(bytes + off[r], J.h_pinned, J.len, hipMemcpyHostToDevice, g.stream));
+        } else {
+            uint8_t *h = g.staging.alloc(J.len);
+            std::memcpy(h, J.h_blk, J.len);
+            FQZ5_HIP(hipMemcpyAsync(bytes + off[r], h, J.len, hipMemcpyHostToDevice, g.stream));
+        }
+    }
+    mark();
+    b.bytes = bytes;
+    b.nbytes = B;
+    b.nblk = S;
+    b.off = g.upload(off);
+    std::vector<uint8_t> split(S);
+    for (size_t r = 0; r < run.size(); r++) split[r] = run[r]->split ? 1 : 0;
+    b.split = g.upload(split);
+    b.term = g.arena.alloc_n<uint32_t>(B);
+    b.tix = g.arena.alloc_n<uint32_t>(B);
+    b.bad = g.arena.alloc_n<uint32_t>(S);
+    b.name0 = g.arena.alloc_n<uint32_t>(S);
+    b.lset = g.arena.alloc_n<uint32_t>(size_t(S) * (T3_LSET_BITS / 32));
+    g.memset0(b.bad, S * 4);
+    g.memset0(b.lset, size_t(S) * (T3_LSET_BITS / 32) * 4);
+    auto scan = [&](const uint32_t *in, uint32_t *out, uint32_t n) {
+        size_t tb = 0;
+        FQZ5_HIP(t3_scan(in, out, n, nullptr, tb, g.stream));
+        void *tmp = g.arena.alloc_n<uint8_t>(tb);
+        FQZ5_HIP(t3_scan(in, out, n, tmp, tb, g.stream));
+    };
+    auto total = [&](const uint32_t *ex, const uint32_t *in, uint32_t n) {   // ex[n-1] + in[n-1]
+        uint32_t t[2];
+        g.download(&t[0], ex + n - 1, 1);
+        g.download(&t[1], in + n - 1, 1);
+        g.sync();
+        return t[0] + t[1];
+    };
+    FQZ5_HIP(t3_launch(b, 0, g.stream));
+    scan(b.term, b.tix, B);
+    const uint32_t N = total(b.tix, b.term, B);        // (the buffer ends with a terminator)
+    b.nnames = N;
+    b.end = g.arena.alloc_n<uint32_t>(N);
+    b.st = g.arena.alloc_n<uint32_t>(N);
+    b.len = g.arena.alloc_n<uint32_t>(N);
+    b.sec = g.arena.alloc_n<uint32_t>(N);
+    b.cnt = g.arena.alloc_n<uint32_t>(N);
+    b.poff = g.arena.alloc_n<uint32_t>(N);
+    FQZ5_HIP(t3_launch(b, 1, g.stream));
+    FQZ5_HIP(t3_launch(b, 2, g.stream));
+    scan(b.cnt, b.poff, N);
+    const uint32_t P = total(b.poff, b.cnt, N);
+    mark();
+    b.npairs = P;
+    b.key = g.arena.alloc_n<uint64_t>(P);
+    b.val = g.arena.alloc_n<uint32_t>(P);
+    uint64_t *skey = g.arena.alloc_n<uint64_t>(P);
+    uint32_t *sval = g.arena.alloc_n<uint32_t>(P);
+    b.skey = skey;
+    b.sval = sval;
+    b.pname = g.arena.alloc_n<uint32_t>(P);
+    b.pdepth = g.arena.alloc_n<uint32_t>(P);
+    b.V = g.arena.alloc_n<uint32_t>(P);
+    b.fmt = g.arena.alloc_n<int4>(N);
+    b.found = g.arena.alloc_n<T3Found>(N);
+    FQZ5_HIP(t3_launch(b, 3, g.stream));
+    mark();
+    size_t tb = 0;
+    FQZ5_HIP(t3_sort(b.key, skey, b.val, sval, P, nullptr, tb, g.stream));
+    void *tmp = g.arena.alloc_n<uint8_t>(tb);
+    FQZ5_HIP(t3_sort(b.key, skey, b.val, sval, P, tmp, tb, g.stream));
+    mark();
+    FQZ5_HIP(t3_launch(b, 4, g.stream));
+    mark();
+    std::vector<T3Found> found(N);
+    std::vector<uint32_t> bad(S), name0(S);
+    g.download(found.data(), b.found, N);
+    g.download(bad.data(), b.bad, S);
+    g.download(name0.data(), b.name0, S);
+    mark();
+    g.sync();
+    if (trace) {
+        float ms[6] = {0};
+        for (size_t i = 0; i + 1 < ev.size() && i < 6; i++) FQZ5_HIP(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]));
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        std::fprintf(stderr, "tok3 search: %u blocks, %u names, %u bytes, %u pairs: uploads %.1f, "
+                     "names %.1f, pairs %.1f, sort %.1f, find %.1f, download %.1f ms; %.1f ms in all\n",
+                     S, N, B, P, ms[0], ms[1], ms[2], ms[3], ms[4], ms[5],
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count());
+    }
+    for (size_t r = 0; r < run.size(); r++) {
+        if (bad[r]) continue;                           // refused, or a hash collision: the host trie
+        const size_t a = name0[r], e = r + 1 < run.size() ? name0[r + 1] : N;
+        run[r]->found.assign(found.begin() + long(a), found.begin() + long(e));
+        run[r]->ok = true;
+    }
 }
 
 void tok3_add_requests(GpuCtx &g, Tok3Enc &T, std::vector<CompressReq> &reqs) {
@@ -970,10 +1187,15 @@ long long fqz5_tok3_tokenise_bytes(const char *blk, int len, int level) {
 
 // Host stage only: FNV-1a of every token stream (index, size, bytes) of
 // `blk`, for CPU regression tests of the tokeniser; 0 on failure.
+unsigned long long fqz5_tok3_tokenise_digest_mode(const char *blk, int len, int level, int pipelined);
 unsigned long long fqz5_tok3_tokenise_digest(const char *blk, int len, int level) {
+    return fqz5_tok3_tokenise_digest_mode(blk, len, level, 0);
+}
+// (tests: pipelined 1 runs the trie searches on a second thread)
+unsigned long long fqz5_tok3_tokenise_digest_mode(const char *blk, int len, int level, int pipelined) {
     std::vector<char> b(blk, blk + std::max(len, 0));
     Tok3Enc T;
-    if (!tok3_tokenise(b.data(), len, level, 0, T)) return 0;
+    if (!tok3_tokenise(b.data(), len, level, 0, T, pipelined != 0)) return 0;
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](uint8_t v) { h = (h ^ v) * 1099511628211ull; };
     for (size_t i = 0; i < T.desc.size(); i++) {
@@ -1036,6 +1258,56 @@ uint8_t *tok3_decode_names(uint8_t *in, uint32_t sz, uint32_t *out_len) {
     *out_len = uint32_t(o.size());
     return out;
     GUARD_END((gp ? (void)gp->reset() : (void)0, nullptr))
+}
+
+// (tests) the GPU batch search against the host trie on `nblk` blocks back
+// to back (lens[i] bytes each): mismatching names, or -1 - i when block i's
+// GPU search was refused or failed its checks.  split: the blocks are name
+// sections, searched in split mode against the host trie over name_split's
+// read ids.
+long long fqz5_tok3_search_check(const char *blks, const uint32_t *lens, int nblk, int split) {
+    GUARD_BEGIN
+    GpuCtx &g = gpu();
+    std::vector<std::vector<char>> copy(size_t(std::max(nblk, 0)));
+    std::vector<Tok3SearchJob> jobs(copy.size());
+    std::vector<Tok3SearchJob *> jp;
+    size_t off = 0;
+    for (size_t i = 0; i < copy.size(); i++) {
+        copy[i].assign(blks + off, blks + off + lens[i]);
+        off += lens[i];
+        jobs[i].h_blk = copy[i].data();
+        jobs[i].len = lens[i];
+        jobs[i].split = split != 0;
+        if (split) jobs[i].d_blk = g.upload(reinterpret_cast<const uint8_t *>(copy[i].data()), lens[i]);
+        jp.push_back(&jobs[i]);
+    }
+    tok3_search_batch(g, jp);
+    g.reset();
+    long long bad = 0;
+    for (size_t i = 0; i < copy.size(); i++) {
+        if (!jobs[i].ok) return -1 - (long long)i;
+        std::vector<char> ids = copy[i];
+        if (split) {
+            NameEnc E;
+            name_split(reinterpret_cast<const uint8_t *>(copy[i].data()), lens[i], 2, 3, E);
+            ids = E.ids;
+        }
+        std::vector<uint32_t> st, ln;
+        if (!tok3_name_extents(ids.data(), uint32_t(ids.size()), st, ln)) return -1 - (long long)i;
+        if (st.size() != jobs[i].found.size()) return -1000 - (long long)i;
+        Trie t;
+        for (size_t k = 0; k < st.size(); k++) {
+            char *nm = ids.data() + st[k];
+            nm[ln[k]] = '\0';
+            Found f;
+            f.pnum = t.search(nm, ln[k], uint32_t(k), &f.exact, &f.is_fixed, &f.fixed_len);
+            const T3Found &G = jobs[i].found[k];
+            bad += (f.pnum != G.pnum || f.exact != G.exact || f.is_fixed != G.is_fixed ||
+                    f.fixed_len != G.fixed_len);
+        }
+    }
+    return bad;
+    GUARD_END(-1000000)
 }
 
 }  // extern "C"

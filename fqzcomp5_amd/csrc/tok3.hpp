@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "rans_codec.hpp"
+#include "tok3_search.h"
 
 namespace fqz5 {
 
@@ -30,7 +31,36 @@ struct Tok3Enc {
 
 // Tokenise `len` bytes of names ('\n' or '\0' terminated; terminators are
 // rewritten to '\0' in place).  false where tok3_encode_names returns NULL.
-bool tok3_tokenise(char *blk, int len, int level, int use_arith, Tok3Enc &T);
+// pipelined: the trie searches on a second thread, ahead of the coding
+// (for callers with host cores to spare; the same result).
+// found (optional): every name's trie search done beforehand
+// (tok3_search_batch), so only the coding runs here.
+bool tok3_tokenise(char *blk, int len, int level, int use_arith, Tok3Enc &T,
+                   bool pipelined = false, const T3Found *found = nullptr);
+
+// The trie searches of a batch of name blocks on the GPU (tok3_search.hip):
+// per block its names' search results, or ok = false (a block the tokenise
+// loop refuses, or one whose checks found a hash collision: search it on
+// the host).  h_blk: the block's bytes on the host (its names' extents come
+// from there); d_blk: a device copy (or nullptr: h_blk is uploaded).
+// h_pinned: a pinned host copy to upload from instead.  split: the block is
+// a name section ('\0' after each name) of which the read ids are searched
+// (strat 2: name_split's ids, without building them); d_blk required.
+struct Tok3SearchJob {
+    const char *h_blk = nullptr;
+    const uint8_t *d_blk = nullptr;
+    const uint8_t *h_pinned = nullptr;
+    uint32_t len = 0;
+    bool split = false;
+    std::vector<T3Found> found;
+    bool ok = false;
+};
+// The names of a block as the tokenise loop visits them (:1487-1505): false
+// when the loop fails (a byte that is neither a name byte nor '\0' / '\n')
+// or create_context would (no names, more than 10M).
+bool tok3_name_extents(const char *blk, uint32_t len, std::vector<uint32_t> &st,
+                       std::vector<uint32_t> &ln);
+void tok3_search_batch(GpuCtx &g, std::vector<Tok3SearchJob *> &jobs);
 // Each stream's candidate methods (compress(), tokenise_name3.c:1268-1417) as
 // rANS requests appended to `reqs` (no requests when use_arith).
 void tok3_add_requests(GpuCtx &g, Tok3Enc &T, std::vector<CompressReq> &reqs);

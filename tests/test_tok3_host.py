@@ -27,3 +27,20 @@ def test_token_stream_digests():
     for k, data in got_cases.items():
         for lv, d in want[k].items():
             assert f"{M.digest(so, data, int(lv)):016x}" == d, (k, lv)
+
+
+@pytest.mark.skipif(not os.path.exists(SO), reason="library not built")
+def test_pipelined_search_same_streams():
+    """tok3_tokenise(pipelined): the trie searches on a second thread ahead
+    of the coding (names.cpp uses it when sections are fewer than host
+    threads) give the same token streams."""
+    so = C.CDLL(SO)
+    f = so.fqz5_tok3_tokenise_digest_mode
+    f.restype = C.c_ulonglong
+    f.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int]
+    want = json.load(open(os.path.join(HERE, "golden", "tok3_digests.json")))
+    for k, data in M.cases().items():
+        for lv, d in want[k].items():
+            assert f"{f(data, len(data), int(lv), 1):016x}" == d, (k, lv)
+    bad = b"a\0b\tc\0"                         # a tab ends a name: NULL both ways
+    assert f(bad, len(bad), 3, 1) == f(bad, len(bad), 3, 0) == 0
