@@ -790,13 +790,52 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
             late_of[i] = int(late.size());
             late.push_back(std::move(r));
         }
+        // The late fqz encodes (-5 Illumina: every block's quality section;
+        // their range chains, ~1.2 s for a 100 MB block, are the commit's
+        // long pole) start first, in groups on the helper contexts (the
+        // sequence models' ones, idle now), so that each group's chains start
+        // when its own model pass is done, and the other late encodes run
+        // beside them on this thread.
+        static const bool no_aux = std::getenv("FQZ5_NO_AUX") != nullptr;
+        std::vector<std::vector<FqzEncReq>> fgrp;
+        std::vector<std::exception_ptr> ferr;
+        std::vector<std::thread> fth;
+        struct JoinAll {
+            std::vector<std::thread> &t;
+            ~JoinAll() { for (auto &x : t) if (x.joinable()) x.join(); }
+        } join_f{fth};
+        const bool fqz_aux = !late_fqz.empty() && !no_aux;
+        if (fqz_aux) {
+            const size_t ng = std::min<size_t>(late_fqz.size(), size_t(AUX_NSEQ));
+            fgrp.resize(ng);
+            ferr.resize(ng);
+            for (size_t k = 0; k < late_fqz.size(); k++) fgrp[k % ng].push_back(std::move(late_fqz[k]));
+            for (size_t q = 0; q < ng; q++) {
+                GpuCtx &c = gpu_aux(int(AUX_SEQ0 + q));
+                fth.emplace_back([&c, &grp = fgrp[q], &e = ferr[q]] {
+                    try {
+                        FQZ5_HIP(hipSetDevice(c.device));
+                        fqz_encode_batch(c, grp);
+                    } catch (...) {
+                        e = std::current_exception();
+                    }
+                });
+            }
+        }
         add_lzp3(g, secs, late_lzp, late, late_lzp_of);
         for (int i : late_lzp) late_of[i] = late_lzp_of[size_t(i)][LZP3];
         if (!late.empty()) compress_batch(g, late);
-        if (!late_fqz.empty()) fqz_encode_batch(g, late_fqz);
+        if (!late_fqz.empty() && !fqz_aux) fqz_encode_batch(g, late_fqz);
         if (!late_seq.empty()) seq_encode_batch(g, late_seq);
         std::vector<NameEnc> late_names;
         encode_name_jobs(g, secs, late_name_sec, late_name_meth, late_names);
+        if (fqz_aux) {
+            for (auto &t : fth) t.join();
+            for (auto &e : ferr)
+                if (e) std::rethrow_exception(e);
+            const size_t ng = fgrp.size();
+            for (size_t k = 0; k < late_fqz.size(); k++) late_fqz[k] = std::move(fgrp[k % ng][k / ng]);
+        }
         std::vector<const Layout *> ls;
         std::vector<uint8_t *> dsts;
         std::vector<Layout> framed(nsec);
@@ -864,7 +903,7 @@ int fqz5_sections_commit(const fqz5_section *secs, int nsec, const int32_t *meth
         const double t3 = step_trace() ? now_ms() : 0;
         // the fqz candidates of the try live in the aux arena: rewind it too,
         // or every step's trial buffers take fresh chunks (the r01 bench OOM)
-        if (t_sess.aux) gpu_aux_reset_all();
+        if (t_sess.aux || fqz_aux) gpu_aux_reset_all();
         // the session's host buffers (candidate tables, layouts, the name
         // candidates' token streams: ~100 MB, mostly munmap) are freed by a
         // detached thread, off the caller's path; nothing refers to them now

@@ -9,6 +9,7 @@
 // parameters on the host and runs the serial decode kernel.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -801,8 +802,19 @@ uint64_t fqz_size_lower_bound(const FqzEncReq &r) { return r.w ? r.w->lb : 0; }
 uint64_t fqz_size_upper_bound(const FqzEncReq &r) { return r.w && r.w->lb ? r.w->ub : 0; }
 
 void fqz_encode_batch(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
+    static const bool trace = std::getenv("FQZ5_STEP_TRACE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     fqz_encode_prepare(g, reqs);
+    const auto t1 = std::chrono::steady_clock::now();
     fqz_encode_finish(g, reqs, nullptr);
+    if (trace) {
+        size_t n = 0;
+        for (const FqzEncReq &R : reqs) n = std::max(n, R.n);
+        std::fprintf(stderr, "fqz encode: %zu requests (largest %zu symbols): prepare %.1f ms, "
+                     "range chains + bytes %.1f ms\n", reqs.size(), n,
+                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
+    }
 }
 
 uint8_t *fqz_encode_gpu(int vers, fqz_slice *s, const uint8_t *in, size_t n, size_t *out_size,
