@@ -643,7 +643,11 @@ int fqz5_sections_try(const fqz5_section *secs, int nsec, const uint32_t *masks,
             g_fqz_tried += fq.size() + sq.size();
         }
         t_sess.open = true;
-        if (step_trace()) std::fprintf(stderr, "sections_try: %.1f ms\n", now_ms() - t0);
+        if (step_trace())
+            std::fprintf(stderr, "sections_try: %.1f ms (device / pinned allocations so far %llu, "
+                         "frees %llu)\n", now_ms() - t0,
+                         (unsigned long long)ChunkPool::alloc_calls().load(),
+                         (unsigned long long)ChunkPool::free_calls().load());
         // sizes as compress_with_methods sees them: UINT_MAX when not run,
         // 0 when the codec returned NULL (out_len = *out_size = 0); a
         // skipped candidate's lower bound here, its upper bound in `upper`

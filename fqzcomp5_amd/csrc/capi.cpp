@@ -198,7 +198,14 @@ static void ctx_wait(GpuCtx &c, hipEvent_t ev) {
 }
 GpuCtx &gpu_aux(int k) {
     if (!g_aux[k]) {
-        g_aux[k].reset(new GpuCtx(std::getenv("FQZ5_AUX_NORMAL_PRIO") == nullptr));
+        // Normal priority, as this thread's context ($FQZ5_AUX_HIGH_PRIO=1:
+        // the device's highest, rounds 2-4).  With the helpers at high
+        // priority the -3 encode's pack stage waited ~220 ms behind the plain
+        // rANS helper's chain in about half the steps (encode 300 ms on
+        // average, 230-400; all at normal priority 254, 228-296); the -5
+        // items were within their noise either way.
+        const bool high = std::getenv("FQZ5_AUX_HIGH_PRIO") != nullptr;
+        g_aux[k].reset(new GpuCtx(high));
         if (g_wait_armed) ctx_wait(*g_aux[k], g_wait_ev);
     }
     return *g_aux[k];

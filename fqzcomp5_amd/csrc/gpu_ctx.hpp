@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -60,6 +61,7 @@ class ChunkPool {
             }
         }
         void *b = nullptr;
+        alloc_calls().fetch_add(1, std::memory_order_relaxed);
         hipError_t e = hipMalloc(&b, need);
         if (e != hipSuccess) {              // the idle chunks back to the device, once more
             trim(0);
@@ -92,6 +94,10 @@ class ChunkPool {
         in_use_ -= sz;
     }
     // idle chunks back to the device until at most `keep` bytes stay idle
+    // hipMalloc / hipHostMalloc / hipFree calls so far (FQZ5_STEP_TRACE:
+    // calls inside a step can stall it)
+    static std::atomic<uint64_t> &alloc_calls() { static std::atomic<uint64_t> n{0}; return n; }
+    static std::atomic<uint64_t> &free_calls() { static std::atomic<uint64_t> n{0}; return n; }
     void trim(size_t keep) {
         std::vector<std::pair<size_t, void *>> out;
         {
@@ -104,6 +110,7 @@ class ChunkPool {
                 idle_.erase(it);
             }
         }
+        free_calls().fetch_add(out.size(), std::memory_order_relaxed);
         for (auto &c : out) (void)hipFree(c.second);
     }
     size_t held() { std::lock_guard<std::mutex> lk(m_); return held_; }
@@ -280,6 +287,7 @@ class PinnedArena {
         }
         size_t sz = n > (size_t(64) << 20) ? n : (size_t(64) << 20);
         Chunk c{nullptr, sz, n};
+        ChunkPool::alloc_calls().fetch_add(1, std::memory_order_relaxed);
         FQZ5_HIP(hipHostMalloc(reinterpret_cast<void **>(&c.base), sz, hipHostMallocDefault));
         chunks_.push_back(c);
         cur_ = chunks_.size() - 1;
@@ -392,9 +400,8 @@ struct GpuCtx {
         return lds;
     }
 
-    // high_prio: the streams of a helper context (gpu_aux) get the device's
-    // highest priority, so that the short kernels of the trial's work
-    // candidates are dispatched ahead of the rANS batch's long chains.
+    // high_prio: the streams get the device's highest priority
+    // ($FQZ5_AUX_HIGH_PRIO=1 for the helper contexts, gpu_aux).
     explicit GpuCtx(bool high_prio = false) {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)

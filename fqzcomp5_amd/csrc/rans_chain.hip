@@ -978,14 +978,16 @@ static DEV void store_slab_o0(uint16_t *ring, uint32_t s, int z, uint4 v) {
 }
 
 // Register decoder (K > 0, O0 only): the stream's K <= 8 symbols cover the
-// 2^bits slots, and per symbol i a key = start_i << 16 | (0xffff - f_i)
-// lives in a register (uniform).  With T = slot << 16 | 0xffff, the symbol
-// holding the slot is the one whose key is the largest <= T, i.e. the
-// smallest T - key_i (the keys above T wrap to >= 2^32 - 2^28), and that
-// difference is (slot - start) << 16 | f: K subtractions and a v_min3 tree,
-// no table read (~64 cycles on the chain) and no compare whose SGPR result a
-// select would wait for (~20 cycles each).  The slot is still what the group
-// keeps.
+// 2^bits slots, and per symbol i a key = (start_i << (32 - bits)) - f_i
+// lives in a register (uniform).  With T = x << (32 - bits) (the slot in the
+// top bits, one shift), the symbol holding the slot is the one whose start
+// is the largest <= slot, i.e. the smallest T - key_i (larger starts wrap
+// past 2^32 - 2^(32-bits)), and that difference is (slot - start) <<
+// (32 - bits) | f: K subtractions and a v_min3 tree, no table read (~64
+// cycles on the chain) and no compare whose SGPR result a select would wait
+// for (~20 cycles each).  The slot is still what the group keeps.  (Round 5:
+// keys with the slot at bit 16, T = (x & mask) << 16 | 0xffff, cost one more
+// dependent op: 139-152 -> 129-147 cycles a step, tools/dec_probe_run.py.)
 template <bool O1, int K = 0>
 static DEV void dec4_lean_body(const DecJob &J) {
     constexpr int NX = 4;
@@ -1032,9 +1034,12 @@ static DEV void dec4_lean_body(const DecJob &J) {
         (__attribute__((address_space(3))) uint16_t *)(ring)));
     uint16_t *myob = obuf + (l & 3) * G;
     uint32_t KEY[K > 0 ? K : 1];
+    // keys start << (32 - bits) - f: T = x << (32 - bits) is one shift, and
+    // T - key = (slot - start) << (32 - bits) | f (f <= 2^bits < 2^(32 - bits))
+    const uint32_t ksh = 32u - uint32_t(bits);
 #pragma unroll
     for (int i = 0; i < (K > 0 ? K : 1); i++)
-        KEY[i] = K > 0 ? (J.reg[i] & 0xffffu) << 16 | (0xffffu - (J.reg[i] >> 16)) : 0u;
+        KEY[i] = K > 0 ? ((J.reg[i] & 0xffffu) << ksh) - (J.reg[i] >> 16) : 0u;
 #ifdef FQZ5_CHAIN_PROBE
     const uint64_t pr0 = __builtin_amdgcn_s_memtime(), rr0 = __builtin_amdgcn_s_memrealtime();
     uint64_t t_steps = 0, n_steps = 0;
@@ -1068,13 +1073,13 @@ static DEV void dec4_lean_body(const DecJob &J) {
                         // selection
                         const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
                         __builtin_amdgcn_sched_barrier(0);
-                        const uint32_t T = (x & mask) << 16 | 0xffffu;
-                        a[u] = T >> 16;
+                        const uint32_t T = x << ksh;
+                        a[u] = x & mask;
                         const uint32_t xh = x >> bits;
                         uint32_t d = T - KEY[0];
 #pragma unroll
                         for (int i = 1; i < K; i++) d = min(d, T - KEY[i]);
-                        const uint32_t xd = __umul24(d & 0xffffu, xh) + (d >> 16);
+                        const uint32_t xd = __umul24(d & ((1u << ksh) - 1u), xh) + (d >> ksh);
                         const bool c = xd < RANS_LOW_D;
                         const uint64_t m = __ballot(c);
                         const uint32_t r16 = __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u) << 4;

@@ -3,10 +3,10 @@
 # (FQZ5_STEP_TRACE: try / commit / per-family timings on stderr), then the
 # rocprofv3 kernel-trace summaries of the three bench items (tools/profile.sh
 # phase a without its bench run).  Outputs under gpurun_out/diag_<tag>.
-# $PHASES picks the parts (default all): trace5 trace5i kt3 kt5 kt5i.
+# $PHASES picks the parts (default all): trace5 trace3 trace5i kt3 kt5 kt5i.
 set -euo pipefail
 TAG=${1:-r05}
-PHASES=${PHASES:-"trace5 trace5i kt3 kt5 kt5i"}
+PHASES=${PHASES:-"trace5 trace3 trace5i kt3 kt5 kt5i"}
 OUT=gpurun_out/diag_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -17,6 +17,10 @@ has() { [[ " $PHASES " == *" $1 "* ]]; }
 if has trace5; then
     FQZ5_STEP_TRACE=1 FQZ5_FQZ_SEGSTATS=1 timeout -k 10 300 python3 bench.py $B5 --steps 2 --warmup 1 \
         > $OUT/trace5.json 2> $OUT/trace5.log
+fi
+if has trace3; then
+    FQZ5_STEP_TRACE=1 timeout -k 10 300 python3 bench.py $B3 --steps 3 --warmup 1 \
+        > $OUT/trace3.json 2> $OUT/trace3.log
 fi
 if has trace5i; then
     FQZ5_STEP_TRACE=1 timeout -k 10 300 python3 bench.py $B5I --steps 2 --warmup 1 \
