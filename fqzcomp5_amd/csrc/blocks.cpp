@@ -5,6 +5,7 @@
 // The sections themselves are coded by block.cpp (fqz5_sections_*).
 #include <algorithm>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "../../include/fqz5_block.h"
@@ -221,6 +222,167 @@ int fqz5_block_parse_v(const uint8_t *d_block, uint64_t avail, int version,
             throw GpuError("fqz5_block_parse: record lengths do not sum to the bases");
         g.reset();
         return 0;
+    } catch (const std::exception &e) {
+        fqz5_set_error(e.what());
+        try { if (gp) gp->reset(); } catch (...) {}
+        return -1;
+    }
+}
+
+// Many blocks at once: the same fields as fqz5_block_parse_v, with every
+// block's header reads of one kind batched into one round trip (5 syncs for
+// the whole batch instead of ~6 per block; a -5 decode of 38 blocks parsed
+// them one call per block).
+int fqz5_blocks_parse_v(const uint8_t *const *d_blocks, const uint64_t *avail, int n,
+                        int version, fqz5_block_view *views, uint32_t *const *lens,
+                        const uint32_t *lens_cap, int32_t *status) {
+    GpuCtx *gp = nullptr;
+    try {
+        if (version < FQZ5_V11 || version > FQZ5_VOLD)
+            throw GpuError("fqz5_block_parse: unknown container version");
+        GpuCtx &g = gpu();
+        gp = &g;
+        const size_t N = size_t(std::max(n, 0));
+        const uint64_t hd = version == FQZ5_V11 ? 12 : 8;
+        std::vector<std::string> err(N);
+        std::vector<uint64_t> end(N), o(N), lens_sum(N);
+        auto fail = [&](size_t i, const char *m) { if (err[i].empty()) err[i] = m; };
+        auto ok = [&](size_t i) { return err[i].empty(); };
+        // host staging for the reads of one round
+        auto round = [&](const std::vector<uint64_t> &at, const std::vector<uint64_t> &len,
+                         std::vector<std::vector<uint8_t>> &out) {
+            out.assign(N, {});
+            for (size_t i = 0; i < N; i++) {
+                if (!ok(i) || !len[i]) continue;
+                if (at[i] + len[i] > avail[i]) { fail(i, "fqz5_block_parse: block truncated"); continue; }
+                out[i].resize(len[i]);
+                g.download(out[i].data(), d_blocks[i] + at[i], len[i]);
+            }
+        };
+        std::vector<std::vector<uint8_t>> h;
+        std::vector<uint64_t> at(N, 0), len(N, hd + 9);
+        round(at, len, h);
+        g.sync();
+        uint32_t *d_crc = g.arena.alloc_n<uint32_t>(std::max<size_t>(N, 1));
+        std::vector<uint32_t> crc_stored(N, 0), crc(N, 0);
+        for (size_t i = 0; i < N; i++) {
+            fqz5_block_view *v = &views[i];
+            std::memset(v, 0, sizeof *v);
+            if (!ok(i)) continue;
+            std::memcpy(&v->block_size, h[i].data(), 4);
+            std::memcpy(&v->nrec, h[i].data() + 4, 4);
+            if (uint64_t(v->block_size) + 4 > avail[i] || v->block_size < hd - 4) {
+                fail(i, "fqz5_block_parse: block size past the data");
+                continue;
+            }
+            end[i] = uint64_t(v->block_size) + 4;
+            if (version == FQZ5_V11) {
+                std::memcpy(&crc_stored[i], h[i].data() + 8, 4);
+                crc32_dev(g, 0, d_blocks[i] + 12, v->block_size - 8, d_crc + i);   // (:2309-2317)
+            } else {
+                v->crc_ok = 1;                         // (no check, :2306)
+            }
+            uint32_t c_len;
+            std::memcpy(&v->name_ulen, h[i].data() + hd, 4);
+            std::memcpy(&c_len, h[i].data() + hd + 5, 4);
+            v->name_off = uint32_t(hd);
+            v->name_size = 9 + c_len;
+            o[i] = hd + 9 + c_len;
+        }
+        // the lengths section's first bytes (and the CRCs)
+        for (size_t i = 0; i < N; i++) {
+            at[i] = o[i];
+            len[i] = ok(i) ? std::min<uint64_t>(6, end[i] - std::min(end[i], o[i])) : 0;
+            if (ok(i) && !len[i]) fail(i, "fqz5_block_parse: block truncated");
+        }
+        round(at, len, h);
+        if (version == FQZ5_V11 && N) g.download(crc.data(), d_crc, N);
+        g.sync();
+        std::vector<uint64_t> vat(N, 0), vlen(N, 0);
+        std::vector<char> varlen(N, 0);
+        for (size_t i = 0; i < N; i++) {
+            fqz5_block_view *v = &views[i];
+            if (version == FQZ5_V11) v->crc_ok = crc[i] == crc_stored[i];
+            if (!ok(i)) continue;
+            const uint8_t *lh = h[i].data();
+            if (lh[0] > 0) {                           // fixed length (:2385-2395)
+                uint32_t fl = 0;
+                const int vl = varint_get(lh + 1, lh + h[i].size(), &fl);
+                if (!vl) { fail(i, "fqz5_block_parse: bad fixed length"); continue; }
+                v->fixed_len = int32_t(fl);
+                if (lens[i])
+                    for (uint32_t r = 0; r < std::min(v->nrec, lens_cap[i]); r++) lens[i][r] = fl;
+                lens_sum[i] = uint64_t(fl) * v->nrec;
+                o[i] += 1 + uint64_t(vl);
+            } else {                                   // [0][u32 blen][varints] (:2396-2408)
+                if (h[i].size() < 5) { fail(i, "fqz5_block_parse: block truncated"); continue; }
+                varlen[i] = 1;
+                o[i] += 5;
+                vat[i] = o[i];
+                vlen[i] = std::min<uint64_t>(5ull * v->nrec, end[i] - std::min(end[i], o[i]));
+            }
+        }
+        round(vat, vlen, h);                           // variable lengths' varints
+        g.sync();
+        for (size_t i = 0; i < N; i++) {
+            fqz5_block_view *v = &views[i];
+            if (!ok(i) || !vlen[i]) {
+                if (ok(i) && varlen[i] && v->nrec) fail(i, "fqz5_block_parse: bad length varint");
+                continue;
+            }
+            const uint8_t *p = h[i].data(), *pe = p + h[i].size();
+            uint64_t sum = 0;
+            for (uint32_t r = 0; r < v->nrec; r++) {
+                uint32_t x = 0;
+                const int vl = varint_get(p, pe, &x);
+                if (!vl) { fail(i, "fqz5_block_parse: bad length varint"); break; }
+                if (lens[i] && r < lens_cap[i]) lens[i][r] = x;
+                sum += x;
+                p += vl;
+            }
+            lens_sum[i] = sum;
+            o[i] += uint64_t(p - h[i].data());
+        }
+        for (size_t i = 0; i < N; i++) { at[i] = o[i]; len[i] = ok(i) ? 9 : 0; }
+        round(at, len, h);                             // seq (:2415-2419)
+        g.sync();
+        for (size_t i = 0; i < N; i++) {
+            fqz5_block_view *v = &views[i];
+            if (!ok(i)) continue;
+            uint32_t c_len;
+            std::memcpy(&v->seq_ulen, h[i].data() + 1, 4);
+            std::memcpy(&c_len, h[i].data() + 5, 4);
+            v->seq_off = uint32_t(o[i]);
+            v->seq_size = 9 + c_len;
+            o[i] += 9ull + c_len;
+            at[i] = o[i];
+        }
+        round(at, len, h);                             // qual (:2471-2487)
+        g.sync();
+        int bad = 0;
+        for (size_t i = 0; i < N; i++) {
+            fqz5_block_view *v = &views[i];
+            if (ok(i)) {
+                uint32_t c_len;
+                std::memcpy(&v->qual_ulen, h[i].data() + 1, 4);
+                std::memcpy(&c_len, h[i].data() + 5, 4);
+                v->qual_off = uint32_t(o[i]);
+                v->qual_size = 9 + c_len;
+                o[i] += 9ull + c_len;
+                if (o[i] > end[i]) fail(i, "fqz5_block_parse: sections past the block end");
+            }
+            if (ok(i)) {
+                const bool fasta = v->qual_ulen == 0 && v->qual_size == 9;
+                if (!fasta && v->qual_ulen != v->seq_ulen)
+                    fail(i, "fqz5_block_parse: quality and sequence sizes differ");
+                else if (lens_sum[i] != v->seq_ulen)
+                    fail(i, "fqz5_block_parse: record lengths do not sum to the bases");
+            }
+            status[i] = ok(i) ? 0 : -1;
+            if (!ok(i) && !bad++) fqz5_set_error(err[i].c_str());
+        }
+        g.reset();
+        return bad ? -1 : 0;
     } catch (const std::exception &e) {
         fqz5_set_error(e.what());
         try { if (gp) gp->reset(); } catch (...) {}

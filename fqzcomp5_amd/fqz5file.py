@@ -1260,18 +1260,12 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges
     except ValueError as err:
         raise _lib.NativeError(str(err)) from None
     views, lens = [], []
-    _lib.after_torch()
-    for s, e in ranges:
-        v = S.BlockView()
-        (nrec,) = struct.unpack_from("<I", data, s + 4)
-        ln = np.zeros(max(nrec, 1), np.uint32)
-        _check(S._load_blk().fqz5_block_parse_v(buf.data_ptr() + s, e - s, version, C.byref(v),
-                                                ln.ctypes.data_as(C.POINTER(C.c_uint32)),
-                                                len(ln)),
-               "fqz5_block_parse")
+    nrecs = [struct.unpack_from("<I", data, s + 4)[0] for s, _ in ranges]
+    parsed = S.parse_blocks([buf.data_ptr() + s for s, _ in ranges], [e - s for s, e in ranges],
+                            nrecs, version)
+    for v, ln in parsed:
         if not v.crc_ok:
             raise _lib.NativeError("block CRC mismatch")
-        ln = ln[:v.nrec]
         # the decoders write u_len bytes into outputs sized by the block's
         # own fields: refuse fields that disagree (decode_block allocates
         # from them, fqzcomp5.c:2433-2519)

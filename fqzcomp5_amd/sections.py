@@ -977,6 +977,11 @@ def _load_blk():
         so.fqz5_block_parse.restype = C.c_int
         so.fqz5_block_parse.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(BlockView),
                                         C.POINTER(C.c_uint32), C.c_uint32]
+        so.fqz5_blocks_parse_v.restype = C.c_int
+        so.fqz5_blocks_parse_v.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), C.c_int,
+                                           C.c_int, C.POINTER(BlockView),
+                                           C.POINTER(C.POINTER(C.c_uint32)),
+                                           C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]
         so.fqz5_block_parse_v.restype = C.c_int
         so.fqz5_block_parse_v.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.POINTER(BlockView),
                                           C.POINTER(C.c_uint32), C.c_uint32]
@@ -1001,6 +1006,23 @@ def block_lengths(lens: np.ndarray, fixed_len: int) -> bytes:
     if n < 0:
         raise _lib.NativeError("fqz5_block_lengths")
     return buf.raw[:n]
+
+
+def parse_blocks(ptrs, sizes, nrecs, version: int = 0):
+    """fqz5_blocks_parse_v over device blocks (addresses, byte sizes, record
+    counts from the headers): per block its BlockView and record lengths."""
+    so = _load_blk()
+    n = len(ptrs)
+    views = (BlockView * max(n, 1))()
+    lens = [np.zeros(max(k, 1), np.uint32) for k in nrecs]
+    lp = (C.POINTER(C.c_uint32) * max(n, 1))(*[x.ctypes.data_as(C.POINTER(C.c_uint32)) for x in lens])
+    caps = (C.c_uint32 * max(n, 1))(*[len(x) for x in lens])
+    st = (C.c_int32 * max(n, 1))()
+    _lib.after_torch()
+    if so.fqz5_blocks_parse_v((C.c_void_p * max(n, 1))(*ptrs), (C.c_uint64 * max(n, 1))(*sizes), n,
+                              version, views, lp, caps, st):
+        raise _lib.NativeError("fqz5_block_parse: " + _lib.last_error())
+    return [(views[i], lens[i][:views[i].nrec]) for i in range(n)]
 
 
 class Run:
@@ -1228,11 +1250,16 @@ class Run:
         return v, lens[:v.nrec]
 
     def block_dec_secs(self) -> list[Section]:
-        """Decode sections that read the assembled blocks (after parse)."""
+        """Decode sections that read the assembled blocks (after parse: one
+        batched fqz5_blocks_parse_v for all of them)."""
         out = []
         base = self.blk_buf.data_ptr()
+        parsed = parse_blocks([base + int(self.blk_off[b]) for b in range(len(self.blocks))],
+                              [int(self.blk_off[b + 1] - self.blk_off[b])
+                               for b in range(len(self.blocks))],
+                              [len(self.lens[b]) for b in range(len(self.blocks))])
         for b in range(len(self.blocks)):
-            v, lens = self.parse(b)
+            v, lens = parsed[b]
             if not v.crc_ok:
                 raise _lib.NativeError(f"block {b}: CRC mismatch")
             if not np.array_equal(lens, self.lens[b]):

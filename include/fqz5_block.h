@@ -209,6 +209,16 @@ enum { FQZ5_V11 = 0, FQZ5_V10 = 1, FQZ5_VOLD = 2 };
 int fqz5_block_parse_v(const uint8_t *d_block, uint64_t avail, int version,
                        fqz5_block_view *v, uint32_t *lens, uint32_t lens_cap);
 
+/* The same parse for n blocks at once (d_blocks[i], avail[i] bytes; lens[i]
+ * with lens_cap[i] entries, or NULL): every block's header reads of one kind
+ * share one round trip (5 for the batch, instead of ~6 per block).
+ * status[i] = 0 or -1 per block; returns -1 when any block failed
+ * (fqz5_last_error: the first failure).  Replaces a loop of decode_block's
+ * header reads (fqzcomp5.c:2300-2487) over the blocks. */
+int fqz5_blocks_parse_v(const uint8_t *const *d_blocks, const uint64_t *avail, int n,
+                        int version, fqz5_block_view *views, uint32_t *const *lens,
+                        const uint32_t *lens_cap, int32_t *status);
+
 #ifdef __cplusplus
 }
 #endif
