@@ -695,24 +695,33 @@ void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
     const int np = int(js.size());
     if (!np) return;
     std::vector<FqzEvJob> rj;
-    for (FqzEvJob *J : js) {
+    // per job: the hedge claim word and the total-1 flag, zeroed
+    uint32_t *d_words = g.fqz_tmp.alloc_n<uint32_t>(2 * size_t(np));
+    g.memset0(d_words, 2 * size_t(np) * 4);
+    uint32_t max_nev = 0;
+    for (int k = 0; k < np; k++) {
+        FqzEvJob *J = js[size_t(k)];
         J->addend = g.fqz_tmp.alloc_n<uint32_t>(J->nev);
         J->shifts = g.fqz_tmp.alloc_n<uint32_t>(J->nev + 1);
+        J->ck = g.fqz_tmp.alloc_n<uint32_t>(J->nev / 64 + 1);
+        J->t1 = d_words + np + k;
         J->done = nullptr;
+        max_nev = std::max(max_nev, J->nev);
         rj.push_back(*J);
     }
     // hedge: each range chain on 2-4 CUs
     HedgeShare share(size_t(g.cus));
     const size_t copies = hedge_copies(rj.size(), share.cus);
     if (copies > 1) {
-        uint32_t *d_done = g.fqz_tmp.alloc_n<uint32_t>(rj.size());
-        g.memset0(d_done, rj.size() * 4);
-        for (size_t k = 0; k < rj.size(); k++) rj[k].done = d_done + k;
+        for (size_t k = 0; k < rj.size(); k++) rj[k].done = d_words + k;
         for (size_t c = 1; c < copies; c++) rj.insert(rj.end(), rj.begin(), rj.begin() + long(np));
     }
+    const FqzEvJob *d_rj = g.upload(rj);
+    FQZ5_HIP(launch_fqz_rc(d_rj, int(rj.size()), np, max_nev, 0, g.stream));
     EventPair ev(prof_on(), g.stream);
-    FQZ5_HIP(launch_fqz_rc(g.upload(rj), int(rj.size()), g.stream));
+    FQZ5_HIP(launch_fqz_rc(d_rj, int(rj.size()), np, max_nev, 1, g.stream));
     ev.stop(g.stream);
+    FQZ5_HIP(launch_fqz_rc(d_rj, int(rj.size()), np, max_nev, 2, g.stream));
     std::vector<uint32_t> P(size_t(np), 0);
     for (int k = 0; k < np; k++) {
         FqzEvJob &J = *js[size_t(k)];
@@ -727,10 +736,10 @@ void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
         g.download(&P[size_t(k)], pos + J.nev, 1);
     }
     g.sync();
-    if (ev.on) {   // 16 B of event record in, q and the byte-shift count out per event
+    if (ev.on) {   // the chain reads 16 B of event record per event
         double ev_n = 0;
         for (FqzEvJob *J : js) ev_n += J->nev;
-        prof_add(PK_FQZ_RC, ev.ms(), ev_n * 21.0);
+        prof_add(PK_FQZ_RC, ev.ms(), ev_n * 16.0);
     }
     for (int k = 0; k < np; k++) {
         FqzEvJob &J = *js[size_t(k)];
@@ -763,7 +772,7 @@ void fqz_encode_finish(GpuCtx &g, std::vector<FqzEncReq> &reqs, const std::vecto
     for (int k = 0; k < np; k++) {
         FqzEncReq::Work &W = *par[size_t(k)]->w;
         FqzEvJob &J = W.J;
-        J.rec = g.fqz_tmp.alloc_n<uint4>(J.nev);
+        J.rec = g.fqz_tmp.alloc_n<uint4>(J.nev + RC_PAD);
         FQZ5_HIP(launch_fqz_expand(J, g.stream));
         J.out = W.E.out;
         J.out_len = W.E.out_len;

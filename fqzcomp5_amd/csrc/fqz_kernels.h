@@ -140,7 +140,8 @@ struct FqzEvJob {
     uint32_t *seg_lo, *seg_hi;  // per model: its range in the sorted order
     uint64_t *code;             // per sorted event: cum | freq << 16 | total << 32
     uint8_t *scratch;           // the non-quality models
-    uint4 *rec;                 // per event: {RN(1/total) (2 words), freq | cum << 16, 0}
+    uint4 *rec;                 // per event: {RN(1/total) (2 words), freq, cum}; the range
+                                // chain turns the first two into ceil(2^64 / total)
     uint32_t *addend;           // per event: cum * (range / total)
     uint32_t *shifts;           // per event: coder byte shifts, then their scan
     const uint32_t *pos;        // exclusive scan of shifts
@@ -151,7 +152,11 @@ struct FqzEvJob {
     uint8_t *out;
     uint32_t *out_len;
     uint32_t *done;             // hedged range chain: claim word (zeroed; ~0 = a copy finished)
+    uint32_t *ck;               // range chain: the range before every 64th event
+    uint32_t *t1;               // range chain: a total of 1 seen (zeroed)
 };
+// records of room J.rec needs past nev (the range chain's last loads)
+constexpr uint32_t RC_PAD = 128;
 
 hipError_t launch_fqz_events(const FqzEvJob &j, int phase, hipStream_t s);
 // batched over the blocks of a request list: d_jobs in device memory
@@ -166,7 +171,11 @@ hipError_t launch_fqz_model_hot(const FqzEvJob *d_jobs, int njobs, uint32_t *hot
                                 uint32_t stride, uint32_t hot_min, hipStream_t s);
 hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t hot_min,
                                  hipStream_t s);
-hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, hipStream_t s);
+// the range chain of d_jobs[0, njobs) (hedge copies after the first nbase):
+// phase 0 the records' totals into multipliers, 1 the chain, 2 every
+// event's q and byte shifts (max_nev: the most events of a job)
+hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, int nbase, uint32_t max_nev,
+                         int phase, hipStream_t s);
 // per workgroup b: sum over its events of log2(total / freq) (after the model
 // pass) in partial[b], of -log2(1 - total 2^-24) in partial[nblk + b]
 hipError_t launch_fqz_entropy(const FqzEvJob &j, double *partial, uint32_t nblk, hipStream_t s);

@@ -666,21 +666,79 @@ __global__ void k_fqz_expand(FqzEvJob J) {
 // Phase 4: the range coder over the events in stream order (RC_Encode,
 // c_range_coder.h:133-145).  The only serial dependence is the range:
 //   q = range / total;  range = renorm(q * freq)
-// so one lane computes just that chain and records per event the amount
-// added to `low` (cum * q, < 2^32) and the number of byte shifts.  The
-// division is exact through the double reciprocal: for range < 2^32 and
-// total <= 65519, |range * RN(1/total) - range/total| < 2^-20, below the
-// distance 1/total to the next integer, so adding 2^-19 and truncating
-// gives floor(range/total).  Events go through LDS in blocks of RC_BLK:
-// all lanes load block b+1 into registers (coalesced) before lane 0 runs
-// the chain over block b, then flush block b's outputs and stage block b+1,
-// so the chain never waits for memory.  The chain carries only the range
-// (7 dependent instructions per event: cvt, fma, cvt, mul, ffbh, and,
-// shift) and records q; the flush recomputes each event's byte-shift count
-// from q * freq in parallel.  The staged events are split into reciprocals
-// and frequencies so that lane 0 reads 8 events with 10 LDS instructions.
-constexpr uint32_t RC_BLK = 1024;
-constexpr uint32_t RC_PER = RC_BLK / 64;         // events per lane per block
+// k_rc_magic first turns each record's RN(1/total) into M = ceil(2^64 /
+// total) (total = rint(1 / RN(1/total)) exactly; M = 0 stands for total 1),
+// so that q = (range * M) >> 64 exactly: range < 2^32 keeps the error of M
+// below range / 2^64 < 2^-32, under the distance 1/total of range/total to the
+// next integer.  k_fqz_rc runs the chain on the scalar unit: the range lives
+// in an SGPR, the records come in 8 at a time by two s_load_dwordx16 (double
+// buffered: a chunk's loads go out right after the wait for the previous
+// one), and an event costs 9 scalar instructions (3 multiplies, add,
+// add-with-carry, multiply, find-first-bit, and, shift), no vector work and
+// no LDS.  The chain keeps only each group of 64 events' starting range (a
+// lane of a vector register, stored per RC_BLK events); k_fqz_rc_replay then
+// recomputes every event's q and byte-shift count, one lane per group, all in
+// parallel.  The scalar loads run ahead of nothing: every RC_BLK events the
+// wave warms L2 with the next RC_BLK events' records by vector loads.
+constexpr uint32_t RC_GRP = 64;                  // events per kept range
+constexpr uint32_t RC_BLK = RC_GRP * 64;         // events per store of kept ranges
+constexpr uint32_t RC_CH = 8;                    // events per scalar-load chunk
+
+typedef uint32_t rc_u32x16 __attribute__((ext_vector_type(16)));
+typedef const __attribute__((address_space(4))) rc_u32x16 *rc_cp16;
+struct RcChunk { rc_u32x16 a, b; };
+DEV RcChunk rc_chunk(const uint4 *p) {
+    RcChunk c;
+    c.a = ((rc_cp16)p)[0];
+    c.b = ((rc_cp16)p)[1];
+    return c;
+}
+
+// one event: q = (R * M) >> 64 (T1: M = 0 means q = R), R = renorm(q * f)
+template <bool T1>
+DEV uint32_t rc_sstep(uint32_t R, uint32_t ml, uint32_t mh, uint32_t f) {
+    uint32_t q, t1, t2, t3;
+    if constexpr (T1) {
+        uint32_t x;
+        asm("s_or_b32 %4, %6, %7\n\t"
+            "s_cselect_b32 %4, 0, %5\n\t"
+            "s_mul_hi_u32 %1, %5, %6\n\t"
+            "s_mul_i32 %2, %5, %7\n\t"
+            "s_mul_hi_u32 %3, %5, %7\n\t"
+            "s_add_u32 %1, %2, %1\n\t"
+            "s_addc_u32 %0, %3, %4"
+            : "=s"(q), "=&s"(t1), "=&s"(t2), "=&s"(t3), "=&s"(x)
+            : "s"(R), "s"(ml), "s"(mh)
+            : "scc");
+    } else {
+        asm("s_mul_hi_u32 %1, %4, %5\n\t"
+            "s_mul_i32 %2, %4, %6\n\t"
+            "s_mul_hi_u32 %3, %4, %6\n\t"
+            "s_add_u32 %1, %2, %1\n\t"
+            "s_addc_u32 %0, %3, 0"
+            : "=s"(q), "=&s"(t1), "=&s"(t2), "=&s"(t3)
+            : "s"(R), "s"(ml), "s"(mh)
+            : "scc");
+    }
+    R = q * f;
+    return R << (uint32_t(__builtin_clz(R)) & 24u);
+}
+
+template <bool T1>
+DEV void rc_chunk_steps(uint32_t &R, const RcChunk &X, RcChunk &Y, const uint4 *next) {
+    R = rc_sstep<T1>(R, X.a[0], X.a[1], X.a[2]);   // (waits for X's loads)
+    __builtin_amdgcn_sched_barrier(0);
+    Y = rc_chunk(next);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (uint32_t i = 1; i < RC_CH; i++)
+        R = i < 4 ? rc_sstep<T1>(R, X.a[4 * i], X.a[4 * i + 1], X.a[4 * i + 2])
+                  : rc_sstep<T1>(R, X.b[4 * i - 16], X.b[4 * i - 15], X.b[4 * i - 14]);
+    // all of X stays live to here: no temporary may take a register that
+    // a load still in flight will write
+    asm volatile("" ::"s"(X.a), "s"(X.b));
+    __builtin_amdgcn_sched_barrier(0);
+}
 
 #ifdef FQZ5_RC_PROBE
 __device__ uint64_t g_rcprobe[4];
@@ -689,115 +747,109 @@ extern "C" int fqz5_rc_probe_read(uint64_t *out) {
 }
 #endif
 
-__global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
-    const FqzEvJob J = load_job(Js + blockIdx.x);   // one wave per block of a batch
-    __shared__ double s_rd[RC_BLK];
-    __shared__ uint32_t s_f[RC_BLK];
-    __shared__ uint32_t s_q[RC_BLK];
-    const int l = int(threadIdx.x);
-    uint32_t rng = 0xFFFFFFFFu;
-    const double bias = 1.0 / 524288.0;           // 2^-19
-    const uint32_t nev = J.nev;
-    // bounds-checked buffer accesses: loads past the end read 0, stores past
-    // the end are dropped, so the staging has no branches
+// J.rec has RC_PAD records of room past nev: the last group's chunks read
+// into it (and the range past nev is never used).
+template <bool T1>
+DEV void rc_chain(const FqzEvJob &J) {
+    const uint32_t l = threadIdx.x;
+    const uint32_t nev = J.nev, ngrp = (nev + RC_GRP - 1) / RC_GRP;
+    const auto rck = __builtin_amdgcn_make_buffer_rsrc(J.ck, 0, ngrp * 4u, 0x00020000);
     const auto rrec = __builtin_amdgcn_make_buffer_rsrc(J.rec, 0, nev * 16u, 0x00020000);
-    const auto radd = __builtin_amdgcn_make_buffer_rsrc(J.addend, 0, nev * 4u, 0x00020000);
-    const auto rsh = __builtin_amdgcn_make_buffer_rsrc(J.shifts, 0, nev * 4u, 0x00020000);
-    uint4 pf[RC_PER];
-    auto fetch = [&](uint32_t base) {
+    uint32_t R = 0xFFFFFFFFu;
+    // L2 warming: 8 dwords per lane, one per 128-byte line of the next RC_BLK
+    // records; their values are folded in one block later (so the wait for
+    // them never stalls the chain) and stored nowhere
+    uint32_t warm[8], sink = 0;
 #pragma unroll
-        for (uint32_t r = 0; r < RC_PER; r++) {
-            const uint32_t i = base + uint32_t(l) + 64u * r;
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rrec, i * 16u, 0, 0);
-            pf[r] = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-    };
-    auto stage = [&]() {
-#pragma unroll
-        for (uint32_t r = 0; r < RC_PER; r++) {
-            const uint32_t i = uint32_t(l) + 64u * r;
-            s_rd[i] = __longlong_as_double((long long)(uint64_t(pf[r].y) << 32 | pf[r].x));
-            s_f[i] = pf[r].z;
-        }
-    };
-    fetch(0);
-    stage();
-    __syncthreads();
+    for (uint32_t r = 0; r < 8; r++)
+        warm[r] = __builtin_amdgcn_raw_buffer_load_b32(rrec, (r * 64u + l) * 128u, 0, 0);
 #ifdef FQZ5_RC_PROBE
-    uint64_t pc = 0;
     const uint64_t p0 = __builtin_amdgcn_s_memtime();
 #endif
+    RcChunk A = rc_chunk(J.rec), B;
     for (uint32_t base = 0; base < nev; base += RC_BLK) {
-        const uint32_t cnt = min(RC_BLK, nev - base);
-        if (base + RC_BLK < nev) fetch(base + RC_BLK);
+        const uint32_t blk = base / RC_BLK;
         // hedged launch (done != nullptr): 2-4 copies of the chain on
         // different CUs compute identical outputs.  *done is a claim word
         // (as in rans_chain.hip): the copy that starts this block first
         // writes it; ~0 means a copy has finished, and the others leave
         // after their current block.  The old value is looked at after it.
-        const uint32_t blk = base / RC_BLK;
         uint32_t hedge = 0u;
         if (J.done && l == 0)
             hedge = __hip_atomic_fetch_max(J.done, blk + 1u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-#ifdef FQZ5_RC_PROBE
-        const uint64_t c0 = __builtin_amdgcn_s_memtime();
-#endif
-        if (l == 0) {
-            // renorm: range <<= clz & 24 (range >= 1 always)
-            auto step = [&](double rd, uint32_t f) {
-                const uint32_t q = uint32_t(__fma_rn(double(rng), rd, bias));
-                rng = q * f;
-                rng <<= uint32_t(__builtin_clz(rng)) & 24u;
-                return q;
-            };
-            for (uint32_t i = 0; i < cnt; i += 8) {     // past cnt: harmless (rng unused after)
-                double rd[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) rd[u] = s_rd[i + u];
-                const uint4 f0 = *reinterpret_cast<const uint4 *>(s_f + i);
-                const uint4 f1 = *reinterpret_cast<const uint4 *>(s_f + i + 4);
-                uint4 q0, q1;
-                q0.x = step(rd[0], f0.x);
-                q0.y = step(rd[1], f0.y);
-                q0.z = step(rd[2], f0.z);
-                q0.w = step(rd[3], f0.w);
-                q1.x = step(rd[4], f1.x);
-                q1.y = step(rd[5], f1.y);
-                q1.z = step(rd[6], f1.z);
-                q1.w = step(rd[7], f1.w);
-                *reinterpret_cast<uint4 *>(s_q + i) = q0;
-                *reinterpret_cast<uint4 *>(s_q + i + 4) = q1;
+        for (uint32_t r = 0; r < 8; r++) {
+            sink ^= warm[r];
+            warm[r] = __builtin_amdgcn_raw_buffer_load_b32(
+                rrec, (base + RC_BLK) * 16u + (r * 64u + l) * 128u, 0, 0);
+        }
+        const uint32_t groups = min(64u, (nev - base + RC_GRP - 1) / RC_GRP);
+        uint32_t v = 0;
+        for (uint32_t g = 0; g < groups; g++) {
+            v = l == g ? R : v;
+            const uint4 *gp = J.rec + base + g * RC_GRP;
+#pragma unroll 1
+            for (uint32_t o = 0; o < RC_GRP; o += 2 * RC_CH) {
+                rc_chunk_steps<T1>(R, A, B, gp + o + RC_CH);
+                rc_chunk_steps<T1>(R, B, A, gp + o + 2 * RC_CH);
             }
         }
-        __syncthreads();
-#ifdef FQZ5_RC_PROBE
-        pc += __builtin_amdgcn_s_memtime() - c0;
-#endif
         hedge = __builtin_amdgcn_readlane(hedge, 0);
-        if (hedge <= blk) {
-#pragma unroll
-            for (uint32_t r = 0; r < RC_PER; r++) {
-                const uint32_t i = uint32_t(l) + 64u * r;   // q here; cum * q in k_fqz_accum
-                const uint32_t q = s_q[i];
-                const uint32_t k = (uint32_t(__builtin_clz((q * s_f[i]) | 1u)) & 24u) >> 3;
-                __builtin_amdgcn_raw_buffer_store_b32(q, radd, (base + i) * 4u, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(k, rsh, (base + i) * 4u, 0, 0);
-            }
-        }
-        if (base + RC_BLK < nev) stage();
-        __syncthreads();
+        if (hedge <= blk) __builtin_amdgcn_raw_buffer_store_b32(v, rck, (blk * 64u + l) * 4u, 0, 0);
         if (hedge == ~0u) return;
     }
     if (J.done && l == 0)
         __hip_atomic_store(J.done, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (never true: keeps the warming loads)
+    if (sink == 0x9e3779b9u && nev == 0u) J.ck[0] = sink;
 #ifdef FQZ5_RC_PROBE
     if (l == 0 && blockIdx.x == 0) {
         g_rcprobe[0] = __builtin_amdgcn_s_memtime() - p0;
-        g_rcprobe[1] = pc;
+        g_rcprobe[1] = 0;
         g_rcprobe[2] = nev;
     }
 #endif
+}
+
+__global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
+    const FqzEvJob J = load_job(Js + blockIdx.x);   // one wave per block of a batch
+    if (*J.t1) rc_chain<true>(J);
+    else rc_chain<false>(J);
+}
+
+// each event's q and byte-shift count from its group's starting range
+__global__ __launch_bounds__(256) void k_fqz_rc_replay(const FqzEvJob *Js) {
+    const FqzEvJob J = load_job(Js + blockIdx.y);
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (J.nev + RC_GRP - 1) / RC_GRP) return;
+    uint32_t R = J.ck[g];
+    const uint32_t e1 = min(J.nev, (g + 1) * RC_GRP);
+    for (uint32_t e = g * RC_GRP; e < e1; e++) {
+        const uint4 r = J.rec[e];
+        const uint64_t M = uint64_t(r.y) << 32 | r.x;
+        const uint32_t q = M ? uint32_t(__umul64hi(uint64_t(R), M)) : R;
+        const uint32_t nr = q * r.z;
+        const uint32_t c = uint32_t(__builtin_clz(nr | 1u)) & 24u;
+        J.addend[e] = q;   // cum * q in k_fqz_accum
+        J.shifts[e] = c >> 3;
+        R = nr << c;
+    }
+}
+
+// each record's RN(1/total) into M = ceil(2^64 / total); *t1 set if a total is 1
+__global__ __launch_bounds__(256) void k_rc_magic(const FqzEvJob *Js) {
+    const FqzEvJob J = load_job(Js + blockIdx.y);
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= J.nev) return;
+    uint2 *p = reinterpret_cast<uint2 *>(J.rec + e);
+    const uint2 w = *p;
+    const double rd = __longlong_as_double((long long)(uint64_t(w.y) << 32 | w.x));
+    const uint32_t t = uint32_t(rint(1.0 / rd));
+    uint64_t M = 0;
+    if (t > 1) M = ~0ull / t + 1;
+    else *J.t1 = 1u;
+    *p = make_uint2(uint32_t(M), uint32_t(M >> 32));
 }
 
 // The coder's output is the base-256 number S = sum_i addend_i *
@@ -898,8 +950,20 @@ hipError_t launch_fqz_model_pass(const FqzEvJob *d_jobs, int njobs, uint32_t hot
     return hipGetLastError();
 }
 
-hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, hipStream_t s) {
-    if (njobs) hipLaunchKernelGGL(k_fqz_rc, dim3(njobs), dim3(64), 0, s, d_jobs);
+hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, int nbase, uint32_t max_nev,
+                         int phase, hipStream_t s) {
+    if (!njobs || !nbase) return hipSuccess;
+    if (phase != 1 && !max_nev) return hipSuccess;
+    if (phase == 0)
+        hipLaunchKernelGGL(k_rc_magic, dim3((max_nev + 255) / 256, uint32_t(nbase)), dim3(256), 0, s,
+                           d_jobs);
+    else if (phase == 1)
+        hipLaunchKernelGGL(k_fqz_rc, dim3(uint32_t(njobs)), dim3(64), 0, s, d_jobs);
+    else {
+        const uint32_t ngrp = (max_nev + RC_GRP - 1) / RC_GRP;
+        hipLaunchKernelGGL(k_fqz_rc_replay, dim3((ngrp + 255) / 256, uint32_t(nbase)), dim3(256), 0,
+                           s, d_jobs);
+    }
     return hipGetLastError();
 }
 
