@@ -695,16 +695,15 @@ void rc_backend(GpuCtx &g, std::vector<FqzEvJob *> &js) {
     const int np = int(js.size());
     if (!np) return;
     std::vector<FqzEvJob> rj;
-    // per job: the hedge claim word and the total-1 flag, zeroed
-    uint32_t *d_words = g.fqz_tmp.alloc_n<uint32_t>(2 * size_t(np));
-    g.memset0(d_words, 2 * size_t(np) * 4);
+    // per job: the hedge claim word, zeroed
+    uint32_t *d_words = g.fqz_tmp.alloc_n<uint32_t>(size_t(np));
+    g.memset0(d_words, size_t(np) * 4);
     uint32_t max_nev = 0;
     for (int k = 0; k < np; k++) {
         FqzEvJob *J = js[size_t(k)];
         J->addend = g.fqz_tmp.alloc_n<uint32_t>(J->nev);
         J->shifts = g.fqz_tmp.alloc_n<uint32_t>(J->nev + 1);
         J->ck = g.fqz_tmp.alloc_n<uint32_t>(J->nev / 64 + 1);
-        J->t1 = d_words + np + k;
         J->done = nullptr;
         max_nev = std::max(max_nev, J->nev);
         rj.push_back(*J);

@@ -141,7 +141,7 @@ struct FqzEvJob {
     uint64_t *code;             // per sorted event: cum | freq << 16 | total << 32
     uint8_t *scratch;           // the non-quality models
     uint4 *rec;                 // per event: {RN(1/total) (2 words), freq, cum}; the range
-                                // chain turns the first two into ceil(2^64 / total)
+                                // chain turns the first two into total's magic number, shift
     uint32_t *addend;           // per event: cum * (range / total)
     uint32_t *shifts;           // per event: coder byte shifts, then their scan
     const uint32_t *pos;        // exclusive scan of shifts
@@ -153,7 +153,6 @@ struct FqzEvJob {
     uint32_t *out_len;
     uint32_t *done;             // hedged range chain: claim word (zeroed; ~0 = a copy finished)
     uint32_t *ck;               // range chain: the range before every 64th event
-    uint32_t *t1;               // range chain: a total of 1 seen (zeroed)
 };
 // records of room J.rec needs past nev (the range chain's last loads)
 constexpr uint32_t RC_PAD = 128;

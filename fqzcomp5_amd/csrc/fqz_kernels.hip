@@ -666,20 +666,23 @@ __global__ void k_fqz_expand(FqzEvJob J) {
 // Phase 4: the range coder over the events in stream order (RC_Encode,
 // c_range_coder.h:133-145).  The only serial dependence is the range:
 //   q = range / total;  range = renorm(q * freq)
-// k_rc_magic first turns each record's RN(1/total) into M = ceil(2^64 /
-// total) (total = rint(1 / RN(1/total)) exactly; M = 0 stands for total 1),
-// so that q = (range * M) >> 64 exactly: range < 2^32 keeps the error of M
-// below range / 2^64 < 2^-32, under the distance 1/total of range/total to the
-// next integer.  k_fqz_rc runs the chain on the scalar unit: the range lives
-// in an SGPR, the records come in 8 at a time by two s_load_dwordx16 (double
-// buffered: a chunk's loads go out right after the wait for the previous
-// one), and an event costs 9 scalar instructions (3 multiplies, add,
-// add-with-carry, multiply, find-first-bit, and, shift), no vector work and
-// no LDS.  The chain keeps only each group of 64 events' starting range (a
-// lane of a vector register, stored per RC_BLK events); k_fqz_rc_replay then
-// recomputes every event's q and byte-shift count, one lane per group, all in
-// parallel.  The scalar loads run ahead of nothing: every RC_BLK events the
-// wave warms L2 with the next RC_BLK events' records by vector loads.
+// k_rc_magic first turns each record's RN(1/total) into the divisor's
+// round-up magic number (Granlund & Montgomery 1994, thm 4.2, N = 32):
+// total t = rint(1 / RN(1/t)) exactly, l = ceil(log2 t), m = floor(2^32
+// (2^l - t) / t) + 1 < 2^32; then for every range R < 2^32
+//   q = floor(R / t) = (mulhi(R, m) + R) >> l    (a 33-bit sum)
+// (t = 1: m = 1, l = 0; a power of two: m = 1).  k_fqz_rc runs the chain on
+// the scalar unit: the range lives in an SGPR, the records come in 8 at a
+// time by two s_load_dwordx16 (double buffered: a chunk's loads go out right
+// after the wait for the previous one), and an event costs 8 scalar
+// instructions (multiply-high, add, add-with-carry, 64-bit shift, multiply,
+// find-first-bit, and, shift), no vector work and no LDS.  One wave issues
+// about one instruction per 4 cycles, so the count is the cost.  The chain
+// keeps only each group of 64 events' starting range (a lane of a vector
+// register, stored per RC_BLK events); k_fqz_rc_replay then recomputes every
+// event's q and byte-shift count, one lane per group, all in parallel.  The
+// scalar loads run ahead of nothing: every RC_BLK events the wave warms L2
+// with the next RC_BLK events' records by vector loads.
 constexpr uint32_t RC_GRP = 64;                  // events per kept range
 constexpr uint32_t RC_BLK = RC_GRP * 64;         // events per store of kept ranges
 constexpr uint32_t RC_CH = 8;                    // events per scalar-load chunk
@@ -694,46 +697,22 @@ DEV RcChunk rc_chunk(const uint4 *p) {
     return c;
 }
 
-// one event: q = (R * M) >> 64 (T1: M = 0 means q = R), R = renorm(q * f)
-template <bool T1>
-DEV uint32_t rc_sstep(uint32_t R, uint32_t ml, uint32_t mh, uint32_t f) {
-    uint32_t q, t1, t2, t3;
-    if constexpr (T1) {
-        uint32_t x;
-        asm("s_or_b32 %4, %6, %7\n\t"
-            "s_cselect_b32 %4, 0, %5\n\t"
-            "s_mul_hi_u32 %1, %5, %6\n\t"
-            "s_mul_i32 %2, %5, %7\n\t"
-            "s_mul_hi_u32 %3, %5, %7\n\t"
-            "s_add_u32 %1, %2, %1\n\t"
-            "s_addc_u32 %0, %3, %4"
-            : "=s"(q), "=&s"(t1), "=&s"(t2), "=&s"(t3), "=&s"(x)
-            : "s"(R), "s"(ml), "s"(mh)
-            : "scc");
-    } else {
-        asm("s_mul_hi_u32 %1, %4, %5\n\t"
-            "s_mul_i32 %2, %4, %6\n\t"
-            "s_mul_hi_u32 %3, %4, %6\n\t"
-            "s_add_u32 %1, %2, %1\n\t"
-            "s_addc_u32 %0, %3, 0"
-            : "=s"(q), "=&s"(t1), "=&s"(t2), "=&s"(t3)
-            : "s"(R), "s"(ml), "s"(mh)
-            : "scc");
-    }
+// one event, record {m, l, f, cum}: q = (mulhi(R, m) + R) >> l, R = renorm(q * f)
+DEV uint32_t rc_sstep(uint32_t R, uint32_t m, uint32_t l, uint32_t f) {
+    const uint32_t q = uint32_t((uint64_t(__umulhi(R, m)) + R) >> l);
     R = q * f;
     return R << (uint32_t(__builtin_clz(R)) & 24u);
 }
 
-template <bool T1>
 DEV void rc_chunk_steps(uint32_t &R, const RcChunk &X, RcChunk &Y, const uint4 *next) {
-    R = rc_sstep<T1>(R, X.a[0], X.a[1], X.a[2]);   // (waits for X's loads)
+    R = rc_sstep(R, X.a[0], X.a[1], X.a[2]);   // (waits for X's loads)
     __builtin_amdgcn_sched_barrier(0);
     Y = rc_chunk(next);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (uint32_t i = 1; i < RC_CH; i++)
-        R = i < 4 ? rc_sstep<T1>(R, X.a[4 * i], X.a[4 * i + 1], X.a[4 * i + 2])
-                  : rc_sstep<T1>(R, X.b[4 * i - 16], X.b[4 * i - 15], X.b[4 * i - 14]);
+        R = i < 4 ? rc_sstep(R, X.a[4 * i], X.a[4 * i + 1], X.a[4 * i + 2])
+                  : rc_sstep(R, X.b[4 * i - 16], X.b[4 * i - 15], X.b[4 * i - 14]);
     // all of X stays live to here: no temporary may take a register that
     // a load still in flight will write
     asm volatile("" ::"s"(X.a), "s"(X.b));
@@ -749,8 +728,8 @@ extern "C" int fqz5_rc_probe_read(uint64_t *out) {
 
 // J.rec has RC_PAD records of room past nev: the last group's chunks read
 // into it (and the range past nev is never used).
-template <bool T1>
-DEV void rc_chain(const FqzEvJob &J) {
+__global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
+    const FqzEvJob J = load_job(Js + blockIdx.x);   // one wave per block of a batch
     const uint32_t l = threadIdx.x;
     const uint32_t nev = J.nev, ngrp = (nev + RC_GRP - 1) / RC_GRP;
     const auto rck = __builtin_amdgcn_make_buffer_rsrc(J.ck, 0, ngrp * 4u, 0x00020000);
@@ -789,10 +768,10 @@ DEV void rc_chain(const FqzEvJob &J) {
         for (uint32_t g = 0; g < groups; g++) {
             v = l == g ? R : v;
             const uint4 *gp = J.rec + base + g * RC_GRP;
-#pragma unroll 1
+#pragma unroll
             for (uint32_t o = 0; o < RC_GRP; o += 2 * RC_CH) {
-                rc_chunk_steps<T1>(R, A, B, gp + o + RC_CH);
-                rc_chunk_steps<T1>(R, B, A, gp + o + 2 * RC_CH);
+                rc_chunk_steps(R, A, B, gp + o + RC_CH);
+                rc_chunk_steps(R, B, A, gp + o + 2 * RC_CH);
             }
         }
         hedge = __builtin_amdgcn_readlane(hedge, 0);
@@ -812,12 +791,6 @@ DEV void rc_chain(const FqzEvJob &J) {
 #endif
 }
 
-__global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
-    const FqzEvJob J = load_job(Js + blockIdx.x);   // one wave per block of a batch
-    if (*J.t1) rc_chain<true>(J);
-    else rc_chain<false>(J);
-}
-
 // each event's q and byte-shift count from its group's starting range
 __global__ __launch_bounds__(256) void k_fqz_rc_replay(const FqzEvJob *Js) {
     const FqzEvJob J = load_job(Js + blockIdx.y);
@@ -827,8 +800,7 @@ __global__ __launch_bounds__(256) void k_fqz_rc_replay(const FqzEvJob *Js) {
     const uint32_t e1 = min(J.nev, (g + 1) * RC_GRP);
     for (uint32_t e = g * RC_GRP; e < e1; e++) {
         const uint4 r = J.rec[e];
-        const uint64_t M = uint64_t(r.y) << 32 | r.x;
-        const uint32_t q = M ? uint32_t(__umul64hi(uint64_t(R), M)) : R;
+        const uint32_t q = uint32_t((uint64_t(__umulhi(R, r.x)) + R) >> r.y);
         const uint32_t nr = q * r.z;
         const uint32_t c = uint32_t(__builtin_clz(nr | 1u)) & 24u;
         J.addend[e] = q;   // cum * q in k_fqz_accum
@@ -837,7 +809,7 @@ __global__ __launch_bounds__(256) void k_fqz_rc_replay(const FqzEvJob *Js) {
     }
 }
 
-// each record's RN(1/total) into M = ceil(2^64 / total); *t1 set if a total is 1
+// each record's RN(1/total) into {m, l} (k_fqz_rc)
 __global__ __launch_bounds__(256) void k_rc_magic(const FqzEvJob *Js) {
     const FqzEvJob J = load_job(Js + blockIdx.y);
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -846,10 +818,9 @@ __global__ __launch_bounds__(256) void k_rc_magic(const FqzEvJob *Js) {
     const uint2 w = *p;
     const double rd = __longlong_as_double((long long)(uint64_t(w.y) << 32 | w.x));
     const uint32_t t = uint32_t(rint(1.0 / rd));
-    uint64_t M = 0;
-    if (t > 1) M = ~0ull / t + 1;
-    else *J.t1 = 1u;
-    *p = make_uint2(uint32_t(M), uint32_t(M >> 32));
+    const uint32_t l = t > 1 ? 32u - uint32_t(__clz(int(t - 1))) : 0u;
+    const uint32_t m = uint32_t((((uint64_t(1) << l) - t) << 32) / t + 1);
+    *p = make_uint2(m, l);
 }
 
 // The coder's output is the base-256 number S = sum_i addend_i *
