@@ -149,6 +149,43 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "s_or_b64 s[42:43], s[42:43], s[44:45]\n"                               \
     "s_branch " RETL "b\n"
 
+// Probe build (-DFQZ5_SMALL_PROBE, tools/dec_small_probe.sh): s_memtime
+// stamps at the symbol's top (A, past the model-read wait), after q
+// (B: the rcp/Newton division, with the context terms interleaved), after
+// the ballot's branch (C: p_i, the next set's hash, the ballot), after the
+// model write-back (D: readlanes, coder, +16 update) and at the loop end (E:
+// the next model read issued); E to the next A is the wait for that read.
+// Each stamp is an SMEM read and the loop end waits for them, so the probe
+// build runs slower than the plain one (both are reported).
+#ifdef FQZ5_SMALL_PROBE
+#define FQS_PA "s_memtime s[46:47]\n"
+#define FQS_PB "s_memtime s[48:49]\n"
+#define FQS_PC "s_memtime s[50:51]\n"
+#define FQS_PD "s_memtime s[52:53]\n"
+#define FQS_PE                                                              \
+    "s_memtime s[54:55]\n"                                                  \
+    "s_waitcnt lgkmcnt(0)\n"                                                \
+    "s_sub_u32 %[x], s48, s46\n"                                            \
+    "s_add_u32 %[pr1], %[pr1], %[x]\n"                                      \
+    "s_sub_u32 %[x], s50, s48\n"                                            \
+    "s_add_u32 %[pr2], %[pr2], %[x]\n"                                      \
+    "s_sub_u32 %[x], s52, s50\n"                                            \
+    "s_add_u32 %[pr3], %[pr3], %[x]\n"                                      \
+    "s_sub_u32 %[x], s54, s52\n"                                            \
+    "s_add_u32 %[pr4], %[pr4], %[x]\n"                                      \
+    "s_sub_u32 %[x], s46, s56\n"                                            \
+    "s_add_u32 %[pr5], %[pr5], %[x]\n"                                      \
+    "s_mov_b64 s[56:57], s[54:55]\n"
+#define FQS_P0 "s_memtime s[56:57]\n"
+#else
+#define FQS_PA ""
+#define FQS_PB ""
+#define FQS_PC ""
+#define FQS_PD ""
+#define FQS_PE ""
+#define FQS_P0 ""
+#endif
+
 #define FQS_RUN_ASM(DTU, DTADD, DTUPD)                                      \
     "s_mov_b32 %[m0s], m0\n"                                                \
     "s_mov_b32 m0, %[done]\n"                                               \
@@ -157,9 +194,11 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "v_add_u32 %[vb], %[ma], %[vwoff]\n"                                    \
     "ds_read_u16 %[vU], %[vaddr]\n"                                         \
     "ds_read_b64 v[2:3], %[vb] offset:16\n"                                 \
+    FQS_P0                                                                  \
     "10:\n"                                                                 \
     "s_waitcnt lgkmcnt(0)\n"                                                \
     "11:\n"                                                                 \
+    FQS_PA                                                                  \
     "v_cmp_eq_u16_e32 vcc, %[c], v2\n"                                      \
     "v_sub_u32_dpp %[t4], %[vU], %[vU] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0\n"\
     "v_readlane_b32 %[u], %[pvv], m0\n"                                     \
@@ -182,6 +221,7 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "v_lshl_add_u32 %[t1], %[t1], %[qlocv], %[u]\n"                         \
     "v_and_b32 %[t1], 0xffff, %[t1]\n"                                      \
     "v_cvt_u32_f64 %[t3], %[d0]\n"                                          \
+    FQS_PB                                                                  \
     "v_mul_u32_u24 %[t2], 0x9e3779, %[t1]\n"                                \
     "v_mul_lo_u32 %[t3], %[vU], %[t3]\n"                                    \
     "v_mul_hi_u32_u24 %[t2], %[ns8], %[t2]\n"                               \
@@ -195,6 +235,7 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "s_or_b64 %[SW], %[SW], %[lslow]\n"                                     \
     "s_bitcmp1_b64 %[SW], %[k1]\n"                                          \
     "s_cbranch_scc1 12f\n"                                                  \
+    FQS_PC                                                                  \
     "v_readlane_b32 %[pk1], %[t3], %[k1]\n"                                 \
     "s_sub_u32 %[pk], %[k1], 1\n"                                           \
     "v_readlane_b32 %[pk], %[t5], %[pk]\n"                                  \
@@ -212,6 +253,7 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "s_lshl_b32 %[qs], %[qsk], %[qshift]\n"                                 \
     "s_add_u32 m0, m0, 1\n"                                                 \
     "ds_write_b16 %[vaddr], %[vU]\n"                                        \
+    FQS_PD                                                                  \
     "s_cmp_eq_u32 %[cn], %[c]\n"                                            \
     "s_cbranch_scc1 20f\n"                                                  \
     "s_mov_b32 %[c], %[cn]\n"                                               \
@@ -223,6 +265,7 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "s_and_b32 %[z], %[z], 24\n"                                            \
     "s_cbranch_scc1 40f\n"                                                  \
     "30:\n"                                                                 \
+    FQS_PE                                                                  \
     "s_cmp_lt_u32 m0, %[lim]\n"                                             \
     "s_cbranch_scc1 10b\n"                                                  \
     "s_branch 90f\n"                                                        \
@@ -231,6 +274,7 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
     "s_and_b32 %[z], %[z], 24\n"                                            \
     "s_cbranch_scc1 41f\n"                                                  \
     "31:\n"                                                                 \
+    FQS_PE                                                                  \
     "s_cmp_lt_u32 m0, %[lim]\n"                                             \
     "s_cbranch_scc1 11b\n"                                                  \
     "s_branch 90f\n"                                                        \
@@ -274,6 +318,18 @@ DEV uint32_t fresh_word(uint32_t w, uint32_t L, uint32_t ctx) {
 // the decoder: one workgroup (one wave) per block of the batch.  DT: some
 // parameter block has delta terms (dtab not all zero).
 // ---------------------------------------------------------------------------
+#ifdef FQZ5_SMALL_PROBE
+// cycles per segment (A-B, B-C, C-D, D-E, E-A) summed over every fast
+// symbol of every launch since the last read, and the symbols
+__device__ unsigned long long g_fqsprobe[6];
+extern "C" int fqz5_small_probe_read(uint64_t *out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fqsprobe), sizeof(g_fqsprobe));
+    const unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_fqsprobe), z, sizeof(z));
+    return int(e);
+}
+#endif
+
 template <bool DT>
 __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -563,6 +619,16 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
             uint64_t G, SW, HV;
             uint32_t t0, t1, t2, t3, t4, t5, t6, vb;
             double d0, d1, d2;
+#ifdef FQZ5_SMALL_PROBE
+            uint32_t pr1 = 0, pr2 = 0, pr3 = 0, pr4 = 0, pr5 = 0;
+            uint64_t ps0, ps1, ps2, ps3, ps4, ps5;
+#define FQS_PROBE_OPS , [pr1] "+s"(pr1), [pr2] "+s"(pr2), [pr3] "+s"(pr3), [pr4] "+s"(pr4), \
+    [pr5] "+s"(pr5), [ps0] "=&{s[46:47]}"(ps0), [ps1] "=&{s[48:49]}"(ps1),                      \
+    [ps2] "=&{s[50:51]}"(ps2), [ps3] "=&{s[52:53]}"(ps3), [ps4] "=&{s[54:55]}"(ps4),          \
+    [ps5] "=&{s[56:57]}"(ps5)
+#else
+#define FQS_PROBE_OPS
+#endif
             for (;;) {
 #define FQS_OPERANDS                                                                           \
                 : [mAS] "+{v[2:3]}"(mAS), [cw] "+{s[40:41]}"(cw), [win] "+{s[42:43]}"(win),   \
@@ -576,7 +642,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
                   [z] "=&s"(z), [m0s] "=&s"(m0s), [G] "=&s"(G), [SW] "=&s"(SW), [HV] "=&s"(HV), \
                   [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3),             \
                   [t4] "=&v"(t4), [t5] "=&v"(t5), [t6] "=&v"(t6),                              \
-                  [d0] "=&v"(d0), [d1] "=&v"(d1), [d2] "=&v"(d2)                               \
+                  [d0] "=&v"(d0), [d1] "=&v"(d1), [d2] "=&v"(d2) FQS_PROBE_OPS                  \
                 : [lim] "s"(lim), [ulim] "s"(ulim), [qmask] "s"(qmask), [qshift] "s"(qshift), \
                   [ns8] "s"(ns8), [base] "s"(base), [lslow] "s"(lslow), [c65503] "s"(c65503), \
                   [rbend] "s"(rbend), [bswp] "s"(bswp), [lring] "i"(S_RING), [back] "s"(back),  \
@@ -589,6 +655,7 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
                 else
                     asm volatile(FQS_RUN_ASM(FQS_NONE, FQS_NONE, FQS_NONE) FQS_OPERANDS);
 #undef FQS_OPERANDS
+#undef FQS_PROBE_OPS
                 // (the compiler takes every output of an asm with VGPR outputs
                 // for divergent: the scalar ones are re-read as uniform)
                 rng = U(rng);
@@ -605,6 +672,17 @@ __global__ __launch_bounds__(64) void k_fqz_dec_small(const FqzDecJob *Js) {
                 flags = U(flags);
                 cw = (uint64_t(U(uint32_t(cw >> 32))) << 32);
                 win = (uint64_t(U(uint32_t(win >> 32))) << 32) | U(uint32_t(win));
+#ifdef FQZ5_SMALL_PROBE
+                if (l == 0 && blockIdx.x == 0) {
+                    atomicAdd(&g_fqsprobe[0], (unsigned long long)U(pr1));
+                    atomicAdd(&g_fqsprobe[1], (unsigned long long)U(pr2));
+                    atomicAdd(&g_fqsprobe[2], (unsigned long long)U(pr3));
+                    atomicAdd(&g_fqsprobe[3], (unsigned long long)U(pr4));
+                    atomicAdd(&g_fqsprobe[4], (unsigned long long)U(pr5));
+                    atomicAdd(&g_fqsprobe[5], (unsigned long long)U(done));
+                }
+                pr1 = pr2 = pr3 = pr4 = pr5 = 0;
+#endif
                 if (flags == 2 || done == lim) break;
                 in.W = win;   // the input window needs a refill
                 refill_s(lds, in);
