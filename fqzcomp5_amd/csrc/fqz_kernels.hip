@@ -791,21 +791,50 @@ __global__ __launch_bounds__(64) void k_fqz_rc(const FqzEvJob *Js) {
 #endif
 }
 
-// each event's q and byte-shift count from its group's starting range
-__global__ __launch_bounds__(256) void k_fqz_rc_replay(const FqzEvJob *Js) {
+// each event's q and byte-shift count from its group's starting range: a
+// wave per 64 groups, lane t replays group t.  The records come in and the
+// outputs go out through LDS, RP_CH events of every group at a time, so
+// that a load or store instruction covers whole runs of consecutive events
+// (a lane reading its own group straight from HBM strides 1 KB per lane).
+constexpr uint32_t RP_CH = 16;
+__global__ __launch_bounds__(64) void k_fqz_rc_replay(const FqzEvJob *Js) {
     const FqzEvJob J = load_job(Js + blockIdx.y);
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= (J.nev + RC_GRP - 1) / RC_GRP) return;
-    uint32_t R = J.ck[g];
-    const uint32_t e1 = min(J.nev, (g + 1) * RC_GRP);
-    for (uint32_t e = g * RC_GRP; e < e1; e++) {
-        const uint4 r = J.rec[e];
-        const uint32_t q = uint32_t((uint64_t(__umulhi(R, r.x)) + R) >> r.y);
-        const uint32_t nr = q * r.z;
-        const uint32_t c = uint32_t(__builtin_clz(nr | 1u)) & 24u;
-        J.addend[e] = q;   // cum * q in k_fqz_accum
-        J.shifts[e] = c >> 3;
-        R = nr << c;
+    const uint32_t nev = J.nev, ngrp = (nev + RC_GRP - 1) / RC_GRP;
+    const uint32_t g0 = blockIdx.x * 64u;
+    if (g0 >= ngrp) return;
+    __shared__ uint4 s_rec[64][RP_CH + 1];
+    __shared__ uint32_t s_q[64][RP_CH + 1], s_k[64][RP_CH + 1];
+    const uint32_t t = threadIdx.x;
+    uint32_t R = g0 + t < ngrp ? J.ck[g0 + t] : 0u;
+    for (uint32_t c = 0; c < RC_GRP; c += RP_CH) {
+#pragma unroll 4
+        for (uint32_t r = 0; r < RP_CH; r++) {
+            const uint32_t j = r * 64u + t, gg = j / RP_CH, ee = j % RP_CH;
+            const uint32_t e = (g0 + gg) * RC_GRP + c + ee;
+            s_rec[gg][ee] = e < nev ? J.rec[e] : make_uint4(0, 0, 0, 0);
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (uint32_t ee = 0; ee < RP_CH; ee++) {   // (past nev: never stored)
+            const uint4 rr = s_rec[t][ee];
+            const uint32_t q = uint32_t((uint64_t(__umulhi(R, rr.x)) + R) >> rr.y);
+            const uint32_t nr = q * rr.z;
+            const uint32_t sh = uint32_t(__builtin_clz(nr | 1u)) & 24u;
+            s_q[t][ee] = q;          // cum * q in k_fqz_accum
+            s_k[t][ee] = sh >> 3;
+            R = nr << sh;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (uint32_t r = 0; r < RP_CH; r++) {
+            const uint32_t j = r * 64u + t, gg = j / RP_CH, ee = j % RP_CH;
+            const uint32_t e = (g0 + gg) * RC_GRP + c + ee;
+            if (e < nev) {
+                J.addend[e] = s_q[gg][ee];
+                J.shifts[e] = s_k[gg][ee];
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -932,7 +961,7 @@ hipError_t launch_fqz_rc(const FqzEvJob *d_jobs, int njobs, int nbase, uint32_t 
         hipLaunchKernelGGL(k_fqz_rc, dim3(uint32_t(njobs)), dim3(64), 0, s, d_jobs);
     else {
         const uint32_t ngrp = (max_nev + RC_GRP - 1) / RC_GRP;
-        hipLaunchKernelGGL(k_fqz_rc_replay, dim3((ngrp + 255) / 256, uint32_t(nbase)), dim3(256), 0,
+        hipLaunchKernelGGL(k_fqz_rc_replay, dim3((ngrp + 63) / 64, uint32_t(nbase)), dim3(64), 0,
                            s, d_jobs);
     }
     return hipGetLastError();
