@@ -1439,7 +1439,8 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
         single = ws == 1
         spill = not single and dst2 is not None
         with open(src, "rb") as f:
-            ranges = _file_blocks(f, size)
+            with _stage("index"):
+                ranges = _file_blocks(f, size)
             nb = len(ranges)
             mine = [b for b in range(nb) if (b * ws) // max(nb, 1) == rk] if nb else []
             wb = window_bytes or DEFAULT_WINDOW
@@ -1456,6 +1457,8 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
             gz = [d.endswith(".gz") for d in outs]
             streams, sinks, at = [], [], 0
             plain = []                        # single process: plain outputs by positioned writes
+            st_open = _stage("open")
+            st_open.__enter__()
             if single:
                 import gzip
                 streams = [gzip.GzipFile(filename="", mode="wb", compresslevel=6, mtime=0,
@@ -1473,6 +1476,7 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
                     _Sink(dst, True).close()
                 _barrier(group)
                 sinks = [_Sink(dst, False)]
+            st_open.__exit__()
             written = [0 for _ in outs]
             try:
                 for gb in groups:
@@ -1514,8 +1518,11 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
                         written[j] += int(t.numel())
                         st_w.__exit__()
                         del out
-                    del buf, host, texts
+                    with _stage("free"):
+                        del buf, host, texts
             finally:
+                st_close = _stage("close")
+                st_close.__enter__()
                 for sk in plain:
                     if sk is not None:
                         sk.close()
@@ -1530,6 +1537,7 @@ def decompress_file(src: str, dst: str, plus_name: bool = False, device: str = "
                         st.close()
                 for sk in sinks:
                     sk.close()
+                st_close.__exit__()
         _trace_dump("decode")
         if single:
             return sum(written)

@@ -14,7 +14,11 @@ r = synth.illumina(int(gb * 1e9 / 358), seed=1)
 with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
     src, out, back = (os.path.join(td, n) for n in ("in.fastq", "out.fqz5", "back.fastq"))
     n = synth.write_fastq(r, src)
-    for rep in range(2):
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    for rep in range(reps):
+        for pth in (out, back):          # fresh outputs, as the bench's
+            if os.path.exists(pth):
+                os.unlink(pth)
         t0 = time.perf_counter()
         fqz5file.compress_file(src, out, level)
         t1 = time.perf_counter()
