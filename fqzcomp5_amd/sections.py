@@ -567,8 +567,13 @@ def encode_run(secs: list[Section], avail: np.ndarray, state: TrialState,
         sched = sched_all[off:off + len(secs)]
         # rANS candidates stay speculative (chain-bound, nearly free in one
         # launch); fqz candidates cost in proportion to their work, so only
-        # the scheduled trial sections try them
-        masks = (av[ids] & SPEC) | (sched & WORK_MASK) if speculate else sched
+        # the scheduled trial sections try them.  So does TLZP3 here: its lzp
+        # pass and order-5 chain over every block's names ended after the
+        # tokenisers, the names helper's long pole at -5 (a block after the
+        # trial codes it at commit if it wins)
+        NAME_WORK = 1 << TLZP3
+        masks = ((av[ids] & np.uint32(SPEC & ~NAME_WORK & 0xFFFFFFFF)) |
+                 (sched & np.uint32(WORK_MASK | NAME_WORK)) if speculate else sched)
         # pruning needs each family's trial window whole on this rank
         for fam in (FQZ_MASK, SEQ_MASK):
             rows = np.nonzero(sched_all & fam)[0]
