@@ -278,6 +278,23 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
     const double tsd = trace() ? now_ms() : 0;
     size_t on_host = 0;
     for (size_t i = 0; i < groups.size(); i++) on_host += !sj[i].ok;
+    // the comments' lzp passes (strat 2) need the split only: their inputs go
+    // up now and the passes run on the GPU thread below while the host
+    // tokenises (a candidate whose tokenising then fails is dropped at
+    // assembly, as before)
+    // (the requests here, their uploads on the GPU thread: a ~200 MB pageable
+    // copy on this thread delayed the tokenising by ~50 ms at -5)
+    std::vector<const char *> lz1_host;
+    for (const auto &gr : groups) {
+        NameEnc &E = jobs[gr[0]];
+        if (E.strat != 2 || E.comments.empty()) continue;
+        LzpEncReq r;
+        r.d_in = nullptr;
+        r.n = uint32_t(E.comments.size());
+        E.lzp = int(lz1.size());
+        lz1.push_back(r);
+        lz1_host.push_back(E.comments.data());
+    }
     double t_early = 0;
     std::exception_ptr err0;
     std::thread gpu_early([&] {
@@ -290,6 +307,9 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
                 name_add_lzp(g, jobs[k], d_names[k], lz0);
             }
             if (!lz0.empty()) lzp_encode_batch(g, lz0);
+            for (size_t i = 0; i < lz1.size(); i++)
+                lz1[i].d_in = g.upload(reinterpret_cast<const uint8_t *>(lz1_host[i]), lz1[i].n);
+            if (!lz1.empty()) lzp_encode_batch(g, lz1);
             for (size_t k : early) name_add_requests(g, jobs[k], lz0, rq0);
             if (!rq0.empty()) compress_batch(g, rq0);
             if (trace()) t_early = now_ms();
@@ -320,9 +340,7 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
     gpu_early.join();
     if (err0) std::rethrow_exception(err0);
     const double t1b = trace() ? now_ms() : 0;
-    for (const auto &gr : groups) name_add_lzp(g, jobs[gr[0]], d_names[gr[0]], lz1);
-    if (!lz1.empty()) lzp_encode_batch(g, lz1);
-    const double t2 = trace() ? now_ms() : 0;
+    const double t2 = t1b;
     for (const auto &gr : groups)
         for (size_t x = 0; x < gr.size(); x++)
             name_add_requests(g, jobs[gr[x]], lz1, rq1, x ? &jobs[gr[0]] : nullptr);
@@ -332,10 +350,11 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
     for (size_t k : late) name_assemble(g, jobs[k], rq1);
     if (trace())
         std::fprintf(stderr, "names encode: %zu candidates, split %.1f ms, GPU trie searches "
-                     "%.1f ms (%zu of %zu sections on the host), tokenise %.1f ms (TLZP3 on the "
-                     "GPU beside it: done at %.1f ms), waited %.1f ms, lzp %.1f ms, %zu rANS "
+                     "%.1f ms (%zu of %zu sections on the host), tokenise %.1f ms (TLZP3 and the "
+                     "comment lzp passes on the GPU beside it: done at %.1f ms), waited %.1f ms, "
+                     "lzp %.1f ms, %zu rANS "
                      "streams %.1f ms, assemble %.1f ms\n", jobs.size(), ts - t0, tsd - ts, on_host,
-                     groups.size(), t1 - tsd, early.empty() ? 0.0 : t_early - t0, t1b - t1,
+                     groups.size(), t1 - tsd, t_early ? t_early - t0 : 0.0, t1b - t1,
                      t2 - t1b, rq0.size() + rq1.size(), t3 - t2, now_ms() - t3);
 }
 
