@@ -467,6 +467,19 @@ uint32_t fqz_hot_min() { return hot_min_var().load(); }
 uint32_t fqz_set_hot_min(uint32_t v) { return hot_min_var().exchange(v); }
 
 void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
+    // $FQZ5_STEP_TRACE: the stages' times (a sync after each: the trace
+    // perturbs the overlap it measures)
+    static const bool trace = std::getenv("FQZ5_STEP_TRACE") != nullptr;
+    using clk = std::chrono::steady_clock;
+    std::vector<std::pair<const char *, double>> st;
+    auto t_prev = clk::now();
+    auto mark = [&](const char *what) {
+        if (!trace) return;
+        g.sync();
+        const auto t = clk::now();
+        st.emplace_back(what, std::chrono::duration<double, std::milli>(t - t_prev).count());
+        t_prev = t;
+    };
     // fqz_pick_parameters of every request without caller parameters, their
     // statistics round trips shared (Tune)
     struct Pick {
@@ -597,6 +610,7 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         g.download(&W.last[1], J.nev_rec + nrec - 1, 1);
     }
     g.sync();
+    mark("pick + counts");
 
     // events of every block, sorted by model; then one model pass for all
     std::vector<FqzEvJob> jobs;
@@ -634,6 +648,7 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         J.scratch = g.fqz_tmp.alloc_n<uint8_t>(8192);
         jobs.push_back(J);
     }
+    mark("events + sort");
     const int np = int(par.size());
     if (np && std::getenv("FQZ5_FQZ_SEGSTATS")) {   // diagnostics: events per model
         for (int k = 0; k < np; k++) {
@@ -665,6 +680,7 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
             sp.end(qb);
         }
         FQZ5_HIP(launch_fqz_model_pass(d_jobs, np, hot_min, g.stream));
+        mark("model passes");
         // the entropy of each block's events and the coder's slack: lower
         // and upper bounds of its size
         constexpr uint32_t EB = 1024;
@@ -684,8 +700,14 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
             W.lb = uint64_t(W.hdr.size()) + rc_bytes_lower(bits) + 5;
             W.ub = uint64_t(W.hdr.size()) + rc_bytes_upper(bits, slack) + 5;
         }
+        mark("entropy");
     }
     g.tmp_done(g.sort_tmp);                // the unsorted events back to the pool
+    if (trace && !st.empty()) {
+        std::string line = "fqz prepare:";
+        for (auto &x : st) line += " " + std::string(x.first) + " " + std::to_string(int(x.second * 10) / 10.0).substr(0, 6) + " ms,";
+        std::fprintf(stderr, "%s\n", line.c_str());
+    }
 }
 
 // The range coder back end for event jobs whose rec[] holds every event in
