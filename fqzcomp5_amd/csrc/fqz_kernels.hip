@@ -405,30 +405,60 @@ DEV bool fqz_is_hot(uint32_t m, uint32_t cnt, uint32_t live, uint32_t hot_min) {
     return hot_min && m < FQZ_M_SEL && live <= FQZ_HOT_LIVE && cnt >= hot_min;
 }
 
+#ifdef FQZ5_MP_PROBE
+// the slowest lane of the model pass: {cycles << 24 | model, its events}
+__device__ unsigned long long g_mpprobe[2];
+extern "C" int fqz5_mp_probe_read(uint64_t *out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mpprobe), sizeof(g_mpprobe));
+    const unsigned long long z[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_mpprobe), z, sizeof(z));
+    return int(e);
+}
+#endif
+
 __global__ __launch_bounds__(256) void k_fqz_model_pass(const FqzEvJob *Js, uint32_t nblk,
                                                         uint32_t hot_min) {
     FList<FQZ_QSYMS> *lm = reinterpret_cast<FList<FQZ_QSYMS> *>(fqz_lds);   // 256 models
     const FqzEvJob J = load_job(Js + blockIdx.x / nblk);
     const uint32_t m = (blockIdx.x % nblk) * blockDim.x + threadIdx.x;
+    static_assert(5 * sizeof(FList<256>) + 2 * sizeof(FList<2>) <= 256 * sizeof(FList<FQZ_QSYMS>),
+                  "header models in the pass's LDS");
+    static_assert(FQZ_M_SEL % 256 == 0 && FQZ_NMODELS - FQZ_M_SEL <= 256,
+                  "the header models share one workgroup");
     if (m >= FQZ_NMODELS) return;
     const uint32_t lo = J.seg_lo[m], hi = J.seg_hi[m];
     if (lo >= hi) return;
     const FqzDevGlobal &g = *J.g;
     if (fqz_is_hot(m, hi - lo, g.max_sym + 1, hot_min)) return;
+#ifdef FQZ5_MP_PROBE
+    const uint64_t c0 = __builtin_amdgcn_s_memtime();
+#endif
     if (m < FQZ_M_SEL) {
         FList<FQZ_QSYMS> *ml = &lm[threadIdx.x];
         fl_init(ml, int(g.max_sym) + 1);
         model_run(ml, J, lo, hi);
     } else if (m < FQZ_M_REV) {
-        FList<256> *mg = reinterpret_cast<FList<256> *>(J.scratch) + (m - FQZ_M_SEL);
+        // the header models (selector, 4 length bytes; then REV and DUP) in
+        // the LDS of the last workgroup, whose other lanes hold no model: in
+        // global scratch their searches and halvings (a length model codes
+        // one event per record) made this lane the pass's longest, 145 ms
+        // on a -5 Illumina block
+        FList<256> *mg = reinterpret_cast<FList<256> *>(fqz_lds) + (m - FQZ_M_SEL);
         fl_init(mg, m == FQZ_M_SEL ? int(g.max_sel) + 1 : 256);
         model_run(mg, J, lo, hi);
     } else {
-        FList<2> *mg = reinterpret_cast<FList<2> *>(J.scratch + 5 * sizeof(FList<256>)) +
+        FList<2> *mg = reinterpret_cast<FList<2> *>(reinterpret_cast<uint8_t *>(fqz_lds) +
+                                                    5 * sizeof(FList<256>)) +
                        (m - FQZ_M_REV);
         fl_init(mg, 2);
         model_run(mg, J, lo, hi);
     }
+#ifdef FQZ5_MP_PROBE
+    const uint64_t dc = __builtin_amdgcn_s_memtime() - c0;
+    const unsigned long long key = ((unsigned long long)(dc >> 4) << 24) | m;
+    const unsigned long long old = atomicMax(&g_mpprobe[0], key);
+    if (key > old) atomicExch(&g_mpprobe[1], (unsigned long long)(hi - lo));
+#endif
 }
 
 // The hot models of each block: list[0] = count, list[1..] = model ids.
