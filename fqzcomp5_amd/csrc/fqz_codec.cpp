@@ -622,7 +622,7 @@ void fqz_encode_prepare(GpuCtx &g, std::vector<FqzEncReq> &reqs) {
         J.key = g.sort_tmp.alloc_n<uint32_t>(nev);
         J.val = g.sort_tmp.alloc_n<uint64_t>(nev);
         uint32_t *skey = g.ev_tmp.alloc_n<uint32_t>(nev);
-        uint64_t *sval = g.ev_tmp.alloc_n<uint64_t>(nev);
+        uint64_t *sval = g.ev_tmp.alloc_n<uint64_t>(nev + 2);   // + room: model_run reads pairs
         J.skey = skey;
         J.sval = sval;
         J.code = g.ev_tmp.alloc_n<uint64_t>(nev);

@@ -349,20 +349,29 @@ template <int CAP> DEV void model_run(FList<CAP> *m, const FqzEvJob &J, uint32_t
     // while this batch is coded, so a lane waits for memory only when a
     // batch codes faster than a load returns.
     uint32_t s1 = m->sy[1], f1 = m->fr[1], tot = m->total;
+    // (sval has 2 events of room past nev, so a pair's load never straddles
+    // the end of the range)
     const auto rsv = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(J.sval), 0,
-                                                       J.nev * 8u, 0x00020000);
-    uint32_t sn[B];
+                                                       J.nev * 8u + 16u, 0x00020000);
+    // two events per load and per store: 32 of each per batch kept a
+    // lane's memory operations at the 63 the counter allows, so every batch
+    // waited out a full HBM round trip (the length models' ~297K events per
+    // block ran at ~640 cycles each)
+    const auto rcd = __builtin_amdgcn_make_buffer_rsrc(J.code, 0, J.nev * 8u, 0x00020000);
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+    u32x4_t pn[B / 2];
     auto fetch = [&](uint32_t k) {
 #pragma unroll
-        for (uint32_t u = 0; u < B; u++)
-            sn[u] = __builtin_amdgcn_raw_buffer_load_b32(rsv, (k + u) * 8u, 0, 0);
+        for (uint32_t v = 0; v < B / 2; v++)
+            pn[v] = __builtin_amdgcn_raw_buffer_load_b128(rsv, (k + 2 * v) * 8u, 0, 0);
     };
     fetch(lo);
     for (uint32_t k0 = lo; k0 < hi; k0 += B) {
         const uint32_t nb = min(B, hi - k0);
         uint32_t sv[B];
 #pragma unroll
-        for (uint32_t u = 0; u < B; u++) sv[u] = sn[u] & 0xffu;
+        for (uint32_t u = 0; u < B; u++) sv[u] = (u & 1 ? pn[u / 2][2] : pn[u / 2][0]) & 0xffu;
         if (k0 + B < hi) fetch(k0 + B);
         uint64_t cd[B];
 #pragma unroll
@@ -389,8 +398,17 @@ template <int CAP> DEV void model_run(FList<CAP> *m, const FqzEvJob &J, uint32_t
             }
         }
 #pragma unroll
-        for (uint32_t u = 0; u < B; u++)
-            if (u < nb) J.code[k0 + u] = cd[u];
+        for (uint32_t v = 0; v < B / 2; v++) {
+            const uint32_t u = 2 * v;
+            if (u + 1 < nb) {
+                u32x4_t w = {uint32_t(cd[u]), uint32_t(cd[u] >> 32), uint32_t(cd[u + 1]),
+                             uint32_t(cd[u + 1] >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b128(w, rcd, (k0 + u) * 8u, 0, 0);
+            } else if (u < nb) {   // (the next model's events are another lane's)
+                u32x2_t w = {uint32_t(cd[u]), uint32_t(cd[u] >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b64(w, rcd, (k0 + u) * 8u, 0, 0);
+            }
+        }
     }
     m->fr[1] = uint16_t(f1);
     m->total = tot;
