@@ -207,8 +207,30 @@ def t1_check(reads, blocks, level, gpu_blocks, nblk: int, timeout: int = 900):
         return {"error": str(e)[-300:]}
 
 
+def t1_pin(gpu_blocks, golden: str, fastq_md5=None):
+    """The GPU's blocks of the whole workload against the md5s of the
+    single-threaded reference's file recorded by a committed script
+    (tests/golden/make_golden_l5_novaseq.py: oracle/_ref/fqzcomp5 -5 -t1 on
+    the same seeded input): the md5 of all block bytes, and per block."""
+    import hashlib
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", golden)))
+    h = hashlib.md5()
+    each = []
+    for b in gpu_blocks:
+        h.update(b)
+        each.append(hashlib.md5(b).hexdigest())
+    same = [a == b for a, b in zip(each, g["block_md5s"])]
+    out = {"t1_file_md5_match": h.hexdigest() == g["blocks_md5"] and len(each) == g["blocks"],
+           "t1_blocks_matching": f"{sum(same)}/{g['blocks']}",
+           "gpu_blocks": len(each), "pinned_by": f"tests/golden/{golden} ({g['cmd']}, "
+                                                 f"{g['ref_seconds']} s when made)"}
+    if fastq_md5 is not None:
+        out["input_md5_match"] = fastq_md5 == g["in_md5"]
+    return out
+
+
 def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local, dist,
-            scaling="weak", pmc_tag="", dropin=False, t1_blocks=0, gpu_only=False):
+            scaling="weak", pmc_tag="", dropin=False, t1_blocks=0, gpu_only=False, pin=None):
     """One workload: warmup + `steps` timed steps (barrier + synchronize on
     both sides, max over ranks) and the result fields of its JSON line.  The
     decode places each adaptive-model chain (fqz quality, sequence model) on
@@ -405,7 +427,13 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
     name = max(PROF_KERNELS, key=lambda k: per_kernel[k]["ms"])
     ms, n, b = per_kernel[name]["ms"], per_kernel[name]["launches"], per_kernel[name]["bytes"]
     avg_ms = ms / max(n, 1)
-    ach = (b / max(n, 1)) / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
+    # the algorithmic bytes of a step are the FASTQ text plus
+    # the .fqz5 bytes it encodes or decodes (this rank's); the kernel's
+    # launches of a step share them, so a launch's share is the step's bytes
+    # over its launches per step (the kernel's own stream bytes beside it)
+    alg_step = fq_local + comp_bytes
+    alg_launch = alg_step * steps / max(n, 1)
+    ach = alg_launch / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
     traffic, tsrc, tnote = pmc_traffic(name, pmc_tag)
     # the decode launch is bound by its longest rANS chain: one step = one
     # symbol on each of the 4 interleaved states
@@ -415,7 +443,13 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                        "traffic": traffic, "traffic_source": tsrc,
                        "traffic_note": tnote, "kernel": name,
                        "avg_launch_ms": round(avg_ms, 3),
-                       "bytes_per_launch": int(b / max(n, 1)),
+                       "bytes_per_launch": int(alg_launch),
+                       "bytes_rule": "SURVEY §8 d3: FASTQ + .fqz5 bytes of a step "
+                                     f"({fq_local} + {comp_bytes} B on rank 0) over the "
+                                     "kernel's launches per step",
+                       "launches_per_step": round(n / max(steps, 1), 3),
+                       "kernel_ms_per_step": round(ms / max(steps, 1), 3),
+                       "stream_bytes_per_launch": int(b / max(n, 1)),
                        "enc_avg_ms": round(enc_ms / max(enc_n, 1), 3),
                        "dec_avg_ms": round(dec_ms / max(dec_n, 1), 3),
                        "kernels": per_kernel,
@@ -424,12 +458,24 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                                   "dec_ns_per_step_longest": round(
                                       dec_ms / max(dec_n, 1) * 1e6 / max(longest // 4, 1), 2)}}
     # ---- CPU baseline (rank 0, N=1): the reference CLI on the same text -----
+    # pinned: this workload's whole file was coded by the -t1 reference and
+    # its md5s committed (the rank-0 file of a 1-GPU weak run is that input)
+    pinned = pin is not None and rank == 0 and world == 1 and scaling == "weak"
+    if pinned and not cpu:
+        out["t1_pin"] = t1_pin([run.block_bytes(b) for b in range(len(blocks))], pin)
     if rank == 0 and world == 1 and cpu:
         import tempfile
         gpu_blocks = [run.block_bytes(b) for b in range(len(blocks))]
         with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
             fastq = os.path.join(td, "w.fastq")
             synth.write_fastq(reads, fastq)
+            if pinned:
+                import hashlib
+                hm = hashlib.md5()
+                with open(fastq, "rb") as fz:
+                    for c in iter(lambda: fz.read(1 << 24), b""):
+                        hm.update(c)
+                pin_res = t1_pin(gpu_blocks, pin, hm.hexdigest())
             try:
                 out["cpu_baseline"] = cpu_baseline(fastq, level, cpu_threads, gpu_blocks,
                                                    timeout=600 if level <= 5 else 1000)
@@ -446,7 +492,9 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                 out["cpu_baseline"] = {"error": str(e)[-300:]}
             if dropin:
                 out["dropin_cli"] = dropin_item(fastq, level, cpu_threads)
-        if t1_blocks:
+        if pinned:
+            out["cpu_baseline"].update(pin_res)
+        elif t1_blocks:
             out["cpu_baseline"]["t1_blocks"] = t1_check(reads, blocks, level, gpu_blocks, t1_blocks)
     del run, reads
     # the pool's idle chunks back to the device between items (the next
@@ -639,7 +687,7 @@ def main():
         out["level5"] = measure(5, "novaseq", 4.0 if args.scaling == "weak" else 4.0 * world,
                                 args.steps, args.warmup, not args.no_cpu, threads, world,
                                 rank, local, dist, scaling=args.scaling, pmc_tag="_l5",
-                                t1_blocks=4)
+                                t1_blocks=4, pin="l5_novaseq.json")
         # -5 on configs[1]'s data: the random-walk binned Illumina qualities,
         # where the trial picks fqz (FQZ1/FQZ3, fqzcomp5.c:4906-4907), so the
         # fqz range coder and decoder are in the timed region; each block's

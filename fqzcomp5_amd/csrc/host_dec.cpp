@@ -17,6 +17,7 @@
 // update) stored as parallel u16 frequency / u8 symbol arrays; the 4- and
 // 2-symbol sequence models (c_small_model.h: +1, halved at a total of 255)
 // as four u8 counts.
+#include <sched.h>
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
@@ -400,11 +401,32 @@ std::vector<char> plan(const std::vector<uint64_t> &n, const std::vector<int> &k
     return host;
 }
 
+int cores_of_rank() {
+    // the cores this process may run on (its affinity mask, which
+    // hardware_concurrency() ignores: a cgroup or taskset share), split
+    // evenly among the ranks of this node that share it
+    // ($LOCAL_WORLD_SIZE, set by torch.distributed.run), and no more than
+    // the per-GPU CPU share the box states ($OMP_NUM_THREADS)
+    int n = 0;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = int(std::max(1u, std::thread::hardware_concurrency()));
+    if (const char *e = std::getenv("LOCAL_WORLD_SIZE")) {
+        const int w = std::atoi(e);
+        if (w > 1) n /= w;
+    }
+    if (const char *e = std::getenv("OMP_NUM_THREADS")) {
+        const int o = std::atoi(e);
+        if (o > 0) n = std::min(n, o);
+    }
+    return std::max(1, n);
+}
+
 int threads() {
     static const int n = [] {
         if (const char *e = std::getenv("FQZ5_HOST_THREADS")) return std::max(1, std::atoi(e));
-        const unsigned hw = std::thread::hardware_concurrency();
-        return int(std::min(16u, std::max(1u, hw)));
+        return std::min(16, cores_of_rank());
     }();
     return n;
 }

@@ -23,9 +23,14 @@ int fqz_decode(const uint8_t *in, size_t in_size, uint8_t *out, size_t out_cap, 
 int seq_decode(const uint8_t *in, uint32_t in_size, const uint32_t *lens, int nrec, int both, int k,
                uint8_t *out, uint32_t n);
 
-// Host threads for the chains: $FQZ5_HOST_THREADS, else the cores this
-// process may use (at most 16, the CPU share of one GPU on the MI355X boxes).
+// Host threads of the library's pools (the decode chains, the name
+// tokenisers, the table builders): $FQZ5_HOST_THREADS, else this rank's
+// share of the cores: the process's affinity mask divided by
+// $LOCAL_WORLD_SIZE, capped by $OMP_NUM_THREADS and at 16 (the CPU share of
+// one GPU on the MI355X boxes).
 int threads();
+// the cores share above without the cap of 16
+int cores_of_rank();
 
 // Which adaptive-model decode chains of a fqz5_decode_sections call run on
 // host cores and which on the GPU (host_decode_mode() 2, the default).  A

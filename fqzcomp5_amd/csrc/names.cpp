@@ -12,6 +12,7 @@
 #include <mutex>
 #include <thread>
 
+#include "host_dec.hpp"
 #include "names.hpp"
 #include "rans_format.hpp"
 
@@ -23,7 +24,7 @@ uint32_t get32(const uint8_t *p) { uint32_t v; std::memcpy(&v, p, 4); return v; 
 
 // fn(i) for i < n on up to 16 host threads
 template <class F> void on_threads(size_t n, F fn) {
-    const size_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t hw = size_t(host::threads());
     if (n <= 1 || hw == 1) {
         for (size_t i = 0; i < n; i++) fn(i);
         return;
@@ -319,7 +320,7 @@ void names_encode_batch(GpuCtx &g, std::vector<NameEnc> &jobs,
     });
     // fewer host-searched sections than host threads: each tokenises on two
     // (its trie searches ahead on the second), so its names take ~60 % as long
-    const size_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t hw = size_t(host::threads());
     const bool pipelined = on_host < hw;
     try {
         on_threads(groups.size(), [&](size_t i) {

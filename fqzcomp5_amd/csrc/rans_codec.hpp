@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "gpu_ctx.hpp"
+#include "host_dec.hpp"
 
 namespace fqz5 {
 
@@ -19,7 +20,7 @@ namespace fqz5 {
 // serialised tables; decoder: slot tables) spread over up to 16 threads: a
 // -3/-5 batch has thousands of stripe jobs.  fn(i) must touch item i only.
 template <class F> inline void host_parallel(size_t n, F fn) {
-    const size_t hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t hw = size_t(host::threads());
     if (n < 64 || hw == 1) {
         for (size_t i = 0; i < n; i++) fn(i);
         return;

@@ -240,7 +240,9 @@ __global__ void k_t3_find(T3Batch B) {
         const uint32_t v = B.V[q1 - 1];
         exact = v != T3_NONE;
         from = exact ? int(v - n0) : self;
-        if (exact && !same_prefix(B, v, k, L)) ok = false;
+        // v == k: a collision of the name with itself at another depth (the
+        // prefix check passes trivially there): the host trie decides
+        if (exact && (v == k || !same_prefix(B, v, k, L))) ok = false;
     }
     if (!exact && fm.x >= 1 && uint32_t(fm.x) <= L) {
         uint32_t v = T3_NONE;
@@ -249,7 +251,7 @@ __global__ void k_t3_find(T3Batch B) {
             if (B.pdepth[q] == uint32_t(fm.x)) { v = B.V[q]; seen = true; break; }
         if (!seen) ok = false;                         // (cannot happen: P is a pair depth)
         p3 = v != T3_NONE ? int(v - n0) : self;
-        if (v != T3_NONE && !same_prefix(B, v, k, uint32_t(fm.x))) ok = false;
+        if (v != T3_NONE && (v == k || !same_prefix(B, v, k, uint32_t(fm.x)))) ok = false;
     }
     if (!exact && p3 == -1) {
         const uint8_t *s = B.bytes + st;
@@ -257,7 +259,7 @@ __global__ void k_t3_find(T3Batch B) {
             const uint32_t d = B.pdepth[q], v = B.V[q];
             if (v == T3_NONE || !ps(s[d - 1])) continue;
             from_punct = int(v - n0);
-            if (!same_prefix(B, v, k, d)) ok = false;
+            if (v == k || !same_prefix(B, v, k, d)) ok = false;
             break;
         }
     }

@@ -19,11 +19,16 @@ offset, u32 bases, u32 records}.  Encoding follows a single-threaded (-t1)
 reference run: the codec trial runs over the blocks in file order, so the
 file equals the reference CLI's `-<level> -t1` output byte for byte.
 
-Scope: 4-line FASTQ and FASTA with any line wrapping (text starting with
-'>': blocks without a quality section, decoded to output_fasta's one-line
-text, fqzcomp5.c:2258-2264, :3503-3517); the parser refuses multi-line FASTQ
-records with an error (there is no host parse).  Files of any size stream
-through in windows of whole records (see below), on one or several ranks.
+Scope: 4-line FASTQ, wrapped (multi-line) FASTQ as kseq_read reads it
+(kseq.h:194-216; fastq.hip's record chain) and FASTA with any line wrapping
+(text starting with '>': blocks without a quality section, decoded to
+output_fasta's one-line text, fqzcomp5.c:2258-2264, :3503-3517).  Files of
+any size stream through in windows of whole records (see below), on one or
+several ranks; over several ranks a window of 4-line FASTQ or FASTA is read
+once (each rank its share), a window holding wrapped FASTQ whole by every
+rank.  Refused with an error (there is no host parse): the two layouts of
+kseq's that fastq.hip does not follow (a lone '\\r' line before a block's
+first kept byte, kseq.h:141; bytes between records, :180-186).
 """
 from __future__ import annotations
 
@@ -127,7 +132,7 @@ def _index_text(text_d, at: int, n: int, wrapped: bool = False):
     recs = torch.empty(max_rec * C.sizeof(FastqRec), dtype=torch.uint8, device=text_d.device)
     rsz = np.zeros(max_rec, np.uint32)
     nrec = C.c_uint64(0)
-    _lib.after_torch()
+    _lib.after_torch(text_d.device)
     fn = so.fqz5_fastq_index_any if wrapped else so.fqz5_fastq_index
     fasta = _check(fn(text_d.data_ptr() + at, n, recs.data_ptr(), max_rec,
                       C.byref(nrec), rsz.ctypes.data), "fqz5_fastq_index") == 1
@@ -403,16 +408,39 @@ class _Src:
 
 
 class _Sink:
-    """Positioned writes into the output file (or a bytearray)."""
+    """Positioned writes into the output file (or a bytearray).  A pipe, FIFO
+    or terminal (/dev/stdout) cannot take pwrite (ESPIPE): there the writes
+    go out sequentially, any that arrive ahead of the stream position held
+    until the bytes before them have been written."""
 
     def __init__(self, path: str | None, create: bool):
         import os
+        import stat
         self.path, self.mem, self.fd = path, None, None
+        self.seq, self.pos, self.held = False, 0, {}
         if path is None:
             self.mem = bytearray()
         else:
             flags = os.O_WRONLY | (os.O_CREAT | os.O_TRUNC if create else 0)
             self.fd = os.open(path, flags, 0o644)
+            self.seq = not stat.S_ISREG(os.fstat(self.fd).st_mode)
+
+    def _write_seq(self, off: int, mv) -> None:
+        import os
+        if off != self.pos:
+            if off < self.pos:
+                raise ValueError("sequential output: a write before the stream position")
+            self.held[off] = bytes(mv)
+            return
+        while True:
+            while len(mv):
+                k = os.write(self.fd, mv)
+                mv = mv[k:]
+                self.pos += k
+            nxt = self.held.pop(self.pos, None)
+            if nxt is None:
+                return
+            mv = memoryview(nxt)
 
     def write_at(self, off: int, data) -> None:
         import os
@@ -421,6 +449,9 @@ class _Sink:
             if len(self.mem) < off + len(mv):
                 self.mem.extend(b"\0" * (off + len(mv) - len(self.mem)))
             self.mem[off:off + len(mv)] = mv
+            return
+        if self.seq:
+            self._write_seq(off, mv)
             return
         if len(mv) >= (64 << 20):
             # large writes in 32 MB parts on several threads (the page-cache
@@ -445,8 +476,11 @@ class _Sink:
     def close(self) -> None:
         import os
         if self.fd is not None:
+            held, self.held = self.held, {}
             os.close(self.fd)
             self.fd = None
+            if held:
+                raise ValueError("sequential output: a gap before the held writes")
 
 
 def _allgather_obj(x, group):
@@ -687,6 +721,11 @@ def _scan(f: _PosFile, P: int, Wn: int, device: str, group, fasta=None) -> _Scan
     if fasta is None:
         fasta = got[0][1] == ord(">")
     base = sum(c for c, _ in got[:rk])
+    # four: this range reads as 4-line FASTQ (every line 4k a '@' line, every
+    # line 4k + 2 a '+' line), where kseq's record is exactly those 4 lines;
+    # wrapped FASTQ (or blank lines among the records) fails it and the
+    # window is read whole instead (_next_window_ranks)
+    four = True
     if n:
         if fasta:
             st = nl & (t[1:n + 1] == ord(">"))
@@ -694,6 +733,8 @@ def _scan(f: _PosFile, P: int, Wn: int, device: str, group, fasta=None) -> _Scan
             # (an '@' line: blank lines after the last record start none)
             line = torch.cumsum(nl.to(torch.int64), 0) + (base - 1)
             st = nl & (line % 4 == 0) & (t[1:n + 1] == ord("@"))
+            four = not bool((nl & (line % 4 == 2) & (t[1:n + 1] != ord("+"))).any().item()) \
+                and not bool((nl & (line % 4 == 0) & (t[1:n + 1] != ord("@"))).any().item())
         starts = (st.nonzero().flatten() + lo).cpu().numpy().astype(np.int64)
     else:
         starts = np.zeros(0, np.int64)
@@ -704,7 +745,8 @@ def _scan(f: _PosFile, P: int, Wn: int, device: str, group, fasta=None) -> _Scan
     sc = _Scan()
     sc.fasta = fasta
     sc.lo = int(starts[0]) if starts.size else hi
-    if starts.size:
+    nrec = -1
+    if starts.size and four:
         end = nxt[0] if nxt else _record_end(f, int(starts[-1]), fasta)
         text = t[int(starts[0]) - (lo - 1):]
         if end > hi:
@@ -712,9 +754,12 @@ def _scan(f: _PosFile, P: int, Wn: int, device: str, group, fasta=None) -> _Scan
         else:
             text = text[:end - int(starts[0])]
         sc.hi = end
-        recs, rsz, nrec, fa = _index_text(text, 0, int(text.numel()))
-        if nrec != starts.size:
-            raise _lib.NativeError("window scan: the record parse disagrees with the line count")
+        try:
+            recs, rsz, nrec, fa = _index_text(text, 0, int(text.numel()))
+        except _lib.NativeError:
+            four = False              # (every rank still takes the exchanges below)
+        four = four and nrec == starts.size
+    if starts.size and four:
         w = C.sizeof(FastqRec)
         u = recs.view(nrec, w)[:, 32:44].contiguous().view(torch.int32).view(nrec, 3).cpu().numpy()
         nsz = (u[:, 0] + np.where(u[:, 1] > 0, u[:, 1] + 1, 0) + 1).astype(np.uint64)
@@ -723,9 +768,14 @@ def _scan(f: _PosFile, P: int, Wn: int, device: str, group, fasta=None) -> _Scan
         text, sc.hi = t[:0], hi
         rsz = np.zeros(0, np.uint32)
         nsz = slen = np.zeros(0, np.uint64)
+        if not four:
+            starts = np.zeros(0, np.int64)
     del t, nl
     sc.text = text                       # this rank's records' text, [lo, hi) of the file
-    parts = _allgather_np((starts, rsz.astype(np.uint32), nsz, slen, sc.hi), group)
+    parts = _allgather_np((starts, rsz.astype(np.uint32), nsz, slen, sc.hi, four), group)
+    sc.four = all(p[5] for p in parts)
+    if not sc.four:
+        return sc
     sc.start = np.concatenate([p[0] for p in parts]).astype(np.int64)
     sc.rsz = np.concatenate([p[1] for p in parts]).astype(np.uint32)
     sc.nsz = np.concatenate([p[2] for p in parts]).astype(np.uint64)
@@ -839,9 +889,16 @@ class _RankWindow:
         self.pos[:] = self.next_pos
 
 
+WRAPPED = object()
+
+
 def _next_window_ranks(files, pos, blk: int, wbytes: int, device: str, group):
     """The next window of the inputs at file offsets `pos`, read once over
-    the ranks; None at the end of the input."""
+    the ranks; None at the end of the input; WRAPPED when the window is not
+    4-line FASTQ (or FASTA), whose record starts the line count cannot give:
+    wrapped FASTQ, whose kseq records (kseq.h:194-216) only a walk from a
+    known record start finds (the caller then reads the window whole on
+    every rank, _LocalWindow)."""
     so = _load()
     paired = len(files) == 2
     want = wbytes
@@ -853,6 +910,8 @@ def _next_window_ranks(files, pos, blk: int, wbytes: int, device: str, group):
         scans = [_scan(files[0], pos[0], wn[0], device, group)]
         if paired:
             scans.append(_scan(files[1], pos[1], wn[1], device, group))
+        if not all(sc.four for sc in scans):
+            return WRAPPED
             if scans[0].n and scans[1].n and scans[0].fasta != scans[1].fasta:
                 raise _lib.NativeError("paired files: one FASTA, one FASTQ")
         k = min(s.n for s in scans)
@@ -995,13 +1054,21 @@ def _encode_stream(srcs: list, sink: _Sink, level: int, blk_size: int | None, de
     # several ranks on plain files: each reads its share of every window once
     files = [_PosFile(s.path) for s in srcs] \
         if ws > 1 and all(s.path and not s.gz for s in srcs) else None
+    opened = list(files or [])
     at = [0] * len(srcs)
     try:
         while True:
             with _stage("window"):
-                if files:
-                    W = _next_window_ranks(files, at, blk, wbytes, device, group)
-                else:
+                W = _next_window_ranks(files, at, blk, wbytes, device, group) if files else None
+                if W is WRAPPED:
+                    # wrapped FASTQ: from here on every rank reads each window
+                    # whole and walks its records (fqz5_fastq_record_ends); the
+                    # mapped sources start at the window's offsets
+                    for s_, a in zip(srcs, at):
+                        s_.base = s_.pos = a
+                        s_.eof = False
+                    files = None
+                if not files:
                     w0 = _next_window(srcs, blk, wbytes, device)
                     W = _LocalWindow(w0, srcs, ws) if w0 is not None else None
             if W is None:
@@ -1012,7 +1079,7 @@ def _encode_stream(srcs: list, sink: _Sink, level: int, blk_size: int | None, de
                 W.advance()
                 del W
     finally:
-        for f in files or []:
+        for f in opened:
             f.close()
     if rk == 0:
         if index:
@@ -1135,8 +1202,12 @@ class Blocks(list):
 def _version_of(head: bytes, size: int):
     """read_header (fqzcomp5.c:2578-2603): (version, first block offset,
     index offset or 0).  A file with neither magic is the old headerless
-    format: blocks from offset 0 to the end, no index."""
-    if len(head) >= 8 and head[:8] in (MAGIC, MAGIC_V10):
+    format: blocks from offset 0 to the end, no index.  Fewer than 8 bytes
+    (an empty file included) is an error, as read_header's short fread of
+    the magic is (:2581-2582)."""
+    if len(head) < 8 or size < 8:
+        raise ValueError("not an .fqz5 file: shorter than the 8-byte magic")
+    if head[:8] in (MAGIC, MAGIC_V10):
         if len(head) < 16:
             raise ValueError("truncated .fqz5: no index offset after the magic")
         (idx,) = struct.unpack_from("<Q", head, 8)
@@ -1314,7 +1385,7 @@ def _decode(data, buf, plus_name: bool, device: str, pairs: bool = False, ranges
         sizes.append(int(size.value))
         r1.append(int(s1.value))
     text = torch.empty(max(sum(sizes), 1), dtype=torch.uint8, device=device)
-    _lib.after_torch()
+    _lib.after_torch(device)
     at = 0
     for a, n in zip(args, sizes):
         size, s1 = C.c_uint64(0), C.c_uint64(0)

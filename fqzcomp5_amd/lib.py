@@ -411,18 +411,25 @@ def stream_wait(stream: int) -> None:
         raise NativeError("fqz5_stream_wait failed: " + last_error())
 
 
-def after_torch() -> None:
+def after_torch(dev=None) -> None:
     """The ordering contract of the device-pointer calls for buffers torch
     made: the calling thread's library streams (and its helper contexts')
     wait, device-side, for the work enqueued so far on torch's current
-    stream (a torch.cat output, a buffer the caching allocator reused).
-    Called before every device-pointer entry point of sections / fqz5file;
-    a no-op while torch has not initialised the GPU."""
+    stream of the current device and, when `dev` (the device of the buffers
+    the call reads) is another one, on that device's current stream too (a
+    torch.cat output, a buffer the caching allocator reused).  Called before
+    every device-pointer entry point of sections / fqz5file; a no-op while
+    torch has not initialised the GPU."""
     import sys
     torch = sys.modules.get("torch")
     if torch is None or not torch.cuda.is_initialized():
         return
-    stream_wait(torch.cuda.current_stream().cuda_stream)
+    cur = torch.cuda.current_device()
+    stream_wait(torch.cuda.current_stream(cur).cuda_stream)
+    if dev is not None:
+        d = torch.device(dev)
+        if d.type == "cuda" and d.index is not None and d.index != cur:
+            stream_wait(torch.cuda.current_stream(d).cuda_stream)
 
 
 def crc32_dev(ptr: int, n: int, crc: int = 0) -> int:

@@ -1229,7 +1229,7 @@ class Run:
                                        device=self.seq_d.device)
         self.blk_off = off
         out = np.zeros(len(parts), np.uint32)
-        _lib.after_torch()
+        _lib.after_torch(self.seq_d.device)
         rc = so.fqz5_blocks_assemble(_arr(BlockParts, parts), len(parts), self.blk_buf.data_ptr(),
                                      off.ctypes.data_as(C.POINTER(C.c_uint64)),
                                      out.ctypes.data_as(C.POINTER(C.c_uint32)))
@@ -1248,7 +1248,7 @@ class Run:
         s, e = int(self.blk_off[b]), int(self.blk_off[b + 1])
         nrec = len(self.lens[b])
         lens = np.zeros(max(nrec, 1), np.uint32)
-        _lib.after_torch()
+        _lib.after_torch(self.seq_d.device)
         if so.fqz5_block_parse(self.blk_buf.data_ptr() + s, e - s, C.byref(v),
                                lens.ctypes.data_as(C.POINTER(C.c_uint32)), len(lens)):
             raise _lib.NativeError("fqz5_block_parse: " + _lib.last_error())

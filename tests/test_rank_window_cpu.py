@@ -198,3 +198,63 @@ def test_rank_windows_match_one_process(tmp_path, kind):
     # and agree on the owners and sizes
     assert [w["owner"] for w in res[0][1]] == [w["owner"] for w in res[1][1]]
     assert [w["nbytes"] for w in res[0][1]] == [w["nbytes"] for w in res[1][1]]
+
+
+def _rank_kind(rank, world, port, args, q):
+    """The kind of each window _next_window_ranks returns (WRAPPED or a
+    window of nb blocks), advancing over the 4-line windows."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fqz5file._index_text = _py_index
+    fqz5file._gather_ranges = _fake_gather
+    try:
+        path, blk, wb = args
+        files = [fqz5file._PosFile(path)]
+        at = [0]
+        kinds = []
+        while True:
+            W = fqz5file._next_window_ranks(files, at, blk, wb, "cpu", dist.group.WORLD)
+            if W is None:
+                break
+            if W is fqz5file.WRAPPED:
+                kinds.append(("wrapped", at[0]))
+                break
+            kinds.append(("four", W.nb))
+            W.advance()
+        q.put((rank, kinds, 0, None))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, None, 0, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rank_windows_detect_wrapped(tmp_path):
+    """a wrapped FASTQ (kseq.h:194-216) cannot be split
+    by the 4-line count; every rank must see WRAPPED for the first window
+    that holds wrapped records, at the same file offset, after the 4-line
+    windows before it (the file path then reads those windows whole,
+    fqz5file._encode_stream; its bytes: tests/test_stream_gpu.py)."""
+    from wrapped_cases import illumina70
+    four = synth.illumina(9000, seed=3, with_names=True)
+    head = synth.fastq_chunk(four, 0, four.num_records).tobytes()
+    p = str(tmp_path / "w.fq")
+    open(p, "wb").write(head + illumina70())
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_kind, args=(r, 2, port, (p, 1_000_000, 1_500_000), q))
+          for r in range(2)]
+    for x in ps:
+        x.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda x: x[0])
+    for x in ps:
+        x.join(timeout=60)
+    assert all(r[3] is None for r in res), res
+    k0, k1 = res[0][1], res[1][1]
+    assert k0 == k1
+    assert k0[-1][0] == "wrapped" and any(k == "four" for k, _ in k0[:-1]), k0
+    # the wrapped window starts at a record boundary inside the 4-line head
+    assert 0 < k0[-1][1] <= len(head)
+    assert head[k0[-1][1]:k0[-1][1] + 1] == b"@"

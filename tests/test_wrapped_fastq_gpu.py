@@ -77,3 +77,24 @@ def test_record_ends():
     t2 = torch.frombuffer(bytearray(w2), dtype=torch.uint8).cuda()
     ends, _ = fqz5file._complete_records(t2, len(w2), True)
     assert list(ends) == [w.index(b"@b"), w.index(b"@c"), len(w2)]
+
+
+def test_wrapped_two_ranks(texts, tmp_path):
+    """a wrapped FASTQ coded over two ranks (gloo, both on
+    this GPU; fqz5file's rank windows detect the wrapped records and read
+    those windows whole on every rank) equals the reference CLI's -3 -t1
+    file, and decodes on two ranks to the CLI's -d text."""
+    import torch.multiprocessing as mp
+    from test_stream_gpu import _free_port, _rank, _run_ranks
+    g = next(x for x in GOLD if x["case"] == "illumina70" and x["level"] == 3)
+    src, dst, back = (str(tmp_path / x) for x in ("w.fastq", "w.fqz5", "b.fastq"))
+    open(src, "wb").write(texts["illumina70"])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank, args=(r, 2, port, (src, dst, back, 3, 1_500_000), q))
+          for r in range(2)]
+    out = _run_ranks(ps, q)
+    assert all(e is None for *_, e in out), out
+    assert md5(open(dst, "rb").read()) == g["fqz5_md5"]
+    assert md5(open(back, "rb").read()) == g["dec_md5"]
