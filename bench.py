@@ -361,6 +361,16 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                  "note": "the same decode with every fqz / sequence-model chain on the GPU "
                          "(fqz5_set_host_decode(0)); encode as above; same bytes"}
     comp_bytes = int(run.blk_off[-1])
+    # the md5 of this rank's block bytes, gathered in rank order: a strong
+    # scaling run's list joined equals a one-process run's blocks (rehearsals
+    # of the N > 1 path compare them); weak runs code one file per rank
+    import hashlib
+    bh = hashlib.md5(run.blk_buf[:comp_bytes].cpu().numpy().tobytes()).hexdigest()
+    if world > 1:
+        got = [None] * world
+        dist.all_gather_object(got, bh)
+    else:
+        got = [bh]
     shape = {"illumina": "illumina 150 bp, Illumina names, 8-level binned quals",
              "novaseq": "novaseq 150 bp, Illumina names, NovaSeq 4-level i.i.d. quals",
              "ont": "ONT reads (lognormal lengths, median 10.5 kb; homopolymer-rich bases; "
@@ -393,6 +403,7 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
                    "methods_tried": sorted(have),
                    "methods_missing": sorted(full - have),
                    "methods_chosen": sorted({int(m) for m in meth_all}),
+                   "blocks_md5_by_rank": got,
                    "roundtrip_ok": bool(ok),
                    "parallelism": f"blocks sharded over {world} GPU(s) ({scaling})",
                    "fqz_decoders": dict(zip(("general", "small"), _fqz_dec_counts(so))),

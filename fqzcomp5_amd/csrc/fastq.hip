@@ -214,15 +214,23 @@ __global__ void k_fa_records(const uint8_t *t, uint64_t len, const uint64_t *nl,
 // records are the chain of those links from line 0, walked on the host over
 // one int per '@' line.  Lines: `cls` the first byte (0 empty, 1 a lone
 // '\r'), `ls` the bytes kseq keeps (a trailing '\r' dropped, KS_SEP_LINE
-// :141), P their prefix sums.  Refused (never guessed): a record without a
-// '+' line, qualities longer than the bases, a lone-'\r' line before the
-// first kept byte of a sequence or quality block (kseq keeps that '\r'),
-// bytes other than empty lines between records.
+// :141), P their prefix sums.  kseq's two odd layouts are followed (round
+// 6): a lone-'\r' line before the first kept byte of a sequence or quality
+// block is kept as a '\r' byte (the strip needs two bytes in the string,
+// kseq.h:141; the record's fasta field carries FQ_KEEP_CR_SEQ / _QUAL), and
+// bytes between records (or before the first) are skipped to the next
+// header as kseq_read's scan for '@' / '>' skips them (:180-186), when those
+// lines hold neither byte (`ga`, a line holding '@' or '>' anywhere, and its
+// prefix sums GA).  Refused (never guessed): a record without a '+' line,
+// qualities longer than the bases, skipped bytes holding '@' or '>' away
+// from a line start (kseq would start a record mid-line there).
 // ---------------------------------------------------------------------------
 constexpr int32_t ML_END = -1, ML_MORE = -2, ML_BAD = -3;
+constexpr uint32_t FQ_KEEP_CR_SEQ = 1u << 8, FQ_KEEP_CR_QUAL = 1u << 9;   // fasta field bits
 
 __global__ void k_ml_lines(const uint8_t *t, const uint64_t *nl, uint64_t nlines, uint8_t *cls,
-                           uint32_t *ls, uint32_t *f_at, uint32_t *f_stop, uint32_t *f_cr) {
+                           uint32_t *ls, uint32_t *f_at, uint32_t *f_stop, uint32_t *f_cr,
+                           uint32_t *f_ga) {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= nlines) return;
     const uint64_t s = i ? nl[i - 1] + 1 : 0, e = nl[i];
@@ -235,6 +243,11 @@ __global__ void k_ml_lines(const uint8_t *t, const uint64_t *nl, uint64_t nlines
     f_at[i] = c == '@';
     f_stop[i] = c == '@' || c == '+' || c == '>';
     f_cr[i] = c == 1;
+    // '@' or '>' anywhere in the line: where kseq's skip to the next header
+    // would stop (a line start already stops at a header line)
+    uint32_t ga = 0;
+    for (uint64_t p = s; p < e && !ga; p++) ga = t[p] == '@' || t[p] == '>';
+    f_ga[i] = ga;
 }
 
 __global__ void k_ends4(const uint64_t *nl, uint64_t n4, uint64_t len, uint64_t *ends) {
@@ -274,50 +287,68 @@ __device__ __forceinline__ bool lone_cr_first(const uint64_t *P, const uint32_t 
 }
 
 __global__ void k_ml_cand(const uint8_t *cls, const uint64_t *P, const uint32_t *crs, uint32_t ncr,
-                          uint32_t nlines, const uint32_t *ats, uint32_t nat, const uint32_t *stops,
-                          uint32_t nst, int eof, int32_t *next, uint32_t *jq, uint32_t *kq,
-                          uint32_t *slen) {
+                          const uint32_t *GA, uint32_t nlines, const uint32_t *ats, uint32_t nat,
+                          const uint32_t *stops, uint32_t nst, int eof, int32_t *next, uint32_t *jq,
+                          uint32_t *kq, uint32_t *slen, uint32_t *kcr) {
     const uint32_t a = blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= nat) return;
     const uint32_t h = ats[a];
     const int32_t short_ = eof ? ML_BAD : ML_MORE;
     int32_t r = ML_BAD;
-    uint32_t j = 0, k = 0, sl = 0;
+    uint32_t j = 0, k = 0, sl = 0, crf = 0;
     do {
         const uint32_t js = lower_u32(stops, nst, h + 1);
         if (js >= nst) { r = short_; break; }            // no '+' line yet
         j = stops[js];
         if (cls[j] != '+') break;                         // a record without qualities
-        const uint64_t seq_len = P[j] - P[h + 1];
-        if (seq_len > 0xffffffffull || lone_cr_first(P, crs, ncr, h + 1, j)) break;
+        // a lone '\r' line before the first kept base: kseq keeps it (one byte)
+        const uint32_t cs = lone_cr_first(P, crs, ncr, h + 1, j) ? 1u : 0u;
+        const uint64_t seq_len = P[j] - P[h + 1] + cs;
+        if (seq_len > 0xffffffffull) break;
         sl = uint32_t(seq_len);
         if (j + 1 >= nlines) { r = short_; break; }       // no quality line yet
         const uint64_t base = P[j + 1];
-        // the smallest k >= j + 1 with P[k + 1] - base >= seq_len
+        // the same for the qualities: a lone-'\r' line cq before any kept
+        // quality byte counts one byte from its line on
+        const uint32_t ic = lower_u32(crs, ncr, j + 1);
+        const bool hc = ic < ncr && P[crs[ic]] == base;
+        const uint32_t cq = hc ? crs[ic] : 0u;
+        // the smallest k >= j + 1 whose quality bytes through line k reach
+        // seq_len (kseq reads at least one quality line)
         uint32_t lo = j + 1, hi = nlines;
-        while (lo < hi) {
-            const uint32_t m = lo + ((hi - lo) >> 1);
-            if (P[m + 1] - base >= seq_len) hi = m; else lo = m + 1;
+        if (hc && seq_len <= 1 && seq_len) {
+            lo = cq;                                      // the '\r' alone is the qualities
+        } else {
+            const uint64_t need = hc && seq_len ? seq_len - 1 : seq_len;
+            while (lo < hi) {
+                const uint32_t m = lo + ((hi - lo) >> 1);
+                if (P[m + 1] - base >= need) hi = m; else lo = m + 1;
+            }
         }
         if (lo >= nlines) { r = short_; break; }
         k = lo;
-        if (P[k + 1] - base != seq_len || lone_cr_first(P, crs, ncr, j + 1, k + 1)) break;   // kseq -2
+        const uint64_t got = P[k + 1] - base + ((hc && cq <= k) ? 1u : 0u);
+        if (got != seq_len) break;                        // kseq -2
+        crf = (cs ? FQ_KEEP_CR_SEQ : 0u) | ((hc && cq <= k) ? FQ_KEEP_CR_QUAL : 0u);
         const uint32_t an = lower_u32(ats, nat, k + 1);
         const uint32_t stop = an < nat ? ats[an] : nlines;
-        if (P[stop] != P[k + 1]) { r = an < nat ? ML_BAD : short_; break; }   // bytes between records
+        // lines between the record and the next header: kseq skips them to
+        // the next '@' or '>' byte; followed when they hold neither
+        if (GA[stop] != GA[k + 1]) break;                 // a header would start mid-line
         r = an < nat ? int32_t(an) : (eof ? ML_END : ML_MORE);
     } while (false);
     next[a] = r;
     jq[a] = j;
     kq[a] = k;
     slen[a] = sl;
+    kcr[a] = crf;
 }
 
 // record r of the chain: header line, first sequence line, first quality line
 __global__ void k_ml_records(const uint8_t *t, uint64_t len, const uint64_t *nl, uint32_t nlines,
                              const uint32_t *chain, uint64_t nrec, const uint32_t *ats, const uint32_t *jq,
-                             const uint32_t *kq, const uint32_t *slen, fqz5_fastq_rec *recs,
-                             uint32_t *rec_size, uint64_t *ends) {
+                             const uint32_t *kq, const uint32_t *slen, const uint32_t *kcr,
+                             fqz5_fastq_rec *recs, uint32_t *rec_size, uint64_t *ends) {
     const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (r >= nrec) return;
     const uint32_t a = chain[r], h = ats[a], j = jq[a], k = kq[a];
@@ -327,7 +358,7 @@ __global__ void k_ml_records(const uint8_t *t, uint64_t len, const uint64_t *nl,
     R.seq = e0 + 1 < len ? e0 + 1 : len;
     R.qual = nl[j] + 1 < len ? nl[j] + 1 : len;
     R.seq_len = slen[a];
-    R.fasta = 2;
+    R.fasta = 2u | kcr[a];
     R.end = nl[k] + 1 < len ? nl[k] + 1 : len;
     if (recs) recs[r] = R;
     if (rec_size) rec_size[r] = R.name_len + 1 + 2 * R.seq_len;   // (:472)
@@ -339,10 +370,18 @@ __global__ void k_ml_records(const uint8_t *t, uint64_t len, const uint64_t *nl,
 // s on, every '\n' and a '\r' before a '\n' skipped.  One wave; sub: 33 for
 // qualities.
 __device__ void ml_copy(const uint8_t *t, uint64_t tlen, uint64_t s, uint32_t n, uint8_t *out,
-                        uint8_t sub) {
+                        uint8_t sub, bool keep_cr) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
     uint32_t w = 0;
+    if (keep_cr && n) {
+        // the block's first kept byte is a lone-'\r' line's '\r' (kseq.h:141):
+        // skip the empty lines before it, keep it, go on after its '\n'
+        while (s < tlen && t[s] == '\n') s++;
+        if (lane == 0) out[0] = uint8_t(uint8_t('\r') - sub);
+        s += 2;
+        w = 1;
+    }
     for (uint64_t base = s; w < n && base < tlen; base += 64) {
         const uint64_t p = base + lane;
         const bool in = p < tlen;
@@ -390,9 +429,9 @@ __global__ void k_fq_gather(const uint8_t *t, const fqz5_fastq_rec *recs, uint64
         return;
     }
     uint8_t *qo = qual + soff[k];
-    if (R.fasta == 2) {                               // wrapped FASTQ: lines joined
-        ml_copy(t, R.end, R.seq, R.seq_len, so, 0);
-        ml_copy(t, R.end, R.qual, R.seq_len, qo, 33);
+    if ((R.fasta & 0xffu) == 2) {                     // wrapped FASTQ: lines joined
+        ml_copy(t, R.end, R.seq, R.seq_len, so, 0, (R.fasta & FQ_KEEP_CR_SEQ) != 0);
+        ml_copy(t, R.end, R.qual, R.seq_len, qo, 33, (R.fasta & FQ_KEEP_CR_QUAL) != 0);
         return;
     }
     for (uint32_t i = lane; i < R.seq_len; i += 64) {
@@ -510,13 +549,15 @@ uint64_t ml_index(GpuCtx &g, const uint8_t *d_text, uint64_t len, const uint64_t
     uint32_t *ls = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
     uint32_t *fa = g.arena.alloc_n<uint32_t>(size_t(n) + 1), *fs = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
     uint32_t *fc = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
+    uint32_t *fg = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
     hipLaunchKernelGGL(k_ml_lines, grid_for(n, 256), dim3(256), 0, g.stream, d_text, lines, nlines, cls, ls,
-                       fa, fs, fc);
+                       fa, fs, fc, fg);
     FQZ5_HIP(hipGetLastError());
     g.memset0(ls + n, 4);
     g.memset0(fa + n, 4);
     g.memset0(fs + n, 4);
     g.memset0(fc + n, 4);
+    g.memset0(fg + n, 4);
     // P: kept bytes before each line (u64: widened first)
     uint64_t *ls64 = g.arena.alloc_n<uint64_t>(size_t(n) + 1);
     uint64_t *P = g.arena.alloc_n<uint64_t>(size_t(n) + 2);
@@ -528,6 +569,8 @@ uint64_t ml_index(GpuCtx &g, const uint8_t *d_text, uint64_t len, const uint64_t
     excl_sum(g, fa, pa, uint64_t(n) + 1);
     excl_sum(g, fs, ps, uint64_t(n) + 1);
     excl_sum(g, fc, pc, uint64_t(n) + 1);
+    uint32_t *GA = g.arena.alloc_n<uint32_t>(size_t(n) + 1);
+    excl_sum(g, fg, GA, uint64_t(n) + 1);
     uint32_t cnt[3] = {0, 0, 0};
     g.download(&cnt[0], pa + n, 1);
     g.download(&cnt[1], ps + n, 1);
@@ -549,19 +592,20 @@ uint64_t ml_index(GpuCtx &g, const uint8_t *d_text, uint64_t len, const uint64_t
     }
     int32_t *nx = g.arena.alloc_n<int32_t>(nat);
     uint32_t *jq = g.arena.alloc_n<uint32_t>(nat), *kq = g.arena.alloc_n<uint32_t>(nat);
-    uint32_t *sl = g.arena.alloc_n<uint32_t>(nat);
-    hipLaunchKernelGGL(k_ml_cand, grid_for(nat, 256), dim3(256), 0, g.stream, cls, P, crs, ncr, n, ats, nat,
-                       stops, nst, eof, nx, jq, kq, sl);
+    uint32_t *sl = g.arena.alloc_n<uint32_t>(nat), *kc = g.arena.alloc_n<uint32_t>(nat);
+    hipLaunchKernelGGL(k_ml_cand, grid_for(nat, 256), dim3(256), 0, g.stream, cls, P, crs, ncr, GA, n, ats,
+                       nat, stops, nst, eof, nx, jq, kq, sl, kc);
     FQZ5_HIP(hipGetLastError());
     std::vector<int32_t> hn(nat);
-    uint32_t a0 = 0;
-    uint64_t before = 0;
+    uint32_t a0 = 0, before = 0;
     g.download(hn.data(), nx, nat);
     g.download(&a0, ats, 1);
     g.sync();
-    g.download(&before, P + a0, 1);
+    g.download(&before, GA + a0, 1);
     g.sync();
-    if (before) throw GpuError("fastq: text before the first FASTQ header line");
+    // lines before the first header: kseq skips them to the first '@' or
+    // '>' byte (kseq.h:180-186); followed when they hold neither
+    if (before) throw GpuError("fastq: text before the first FASTQ header line holds '@' or '>'");
     // the records: the chain of next-header links from the first '@' line
     std::vector<uint32_t> chain;
     for (uint32_t a = 0;;) {
@@ -579,7 +623,7 @@ uint64_t ml_index(GpuCtx &g, const uint8_t *d_text, uint64_t len, const uint64_t
         }
         char msg[160];
         std::snprintf(msg, sizeof msg, "fastq: record %zu is not a FASTQ record kseq reads (a record without "
-                      "a '+' line, qualities longer than the bases, or bytes between records)",
+                      "a '+' line, qualities longer than the bases, or '@' / '>' inside the bytes after it)",
                       chain.size() - 1);
         throw GpuError(msg);
     }
@@ -590,7 +634,7 @@ uint64_t ml_index(GpuCtx &g, const uint8_t *d_text, uint64_t len, const uint64_t
     uint32_t *rs = h_rec_size ? g.arena.alloc_n<uint32_t>(nrec) : nullptr;
     uint64_t *ends = h_ends ? g.arena.alloc_n<uint64_t>(nrec) : nullptr;
     hipLaunchKernelGGL(k_ml_records, grid_for(nrec, 256), dim3(256), 0, g.stream, d_text, len, lines, n, d_chain,
-                       nrec, ats, jq, kq, sl, d_recs, rs, ends);
+                       nrec, ats, jq, kq, sl, kc, d_recs, rs, ends);
     FQZ5_HIP(hipGetLastError());
     if (rs) g.download(h_rec_size, rs, nrec);
     if (ends) {

@@ -335,6 +335,22 @@ struct ProfSpan {
 };
 void prof_bytes(long token, double bytes);
 
+// $FQZ5_CALL_TRACE=1: one stderr line per host-buffer C-ABI call (the
+// drop-in's entry points): the thread, the call, its input size, and the
+// milliseconds since the library loaded at entry, at each stage mark and at
+// exit (the marks sync the stream first, so the stages do not overlap).
+bool call_trace_on();
+struct CallTrace {
+    const char *fn;
+    size_t n;
+    double t[6];
+    const char *tag[6];
+    int k = 0;
+    CallTrace(const char *f, size_t bytes);
+    void mark(const char *what);            // a stage ends here
+    ~CallTrace();
+};
+
 struct KernelProfile {
     bool on = false;
     double enc_ms = 0, dec_ms = 0;

@@ -597,6 +597,7 @@ static DEV const __attribute__((address_space(3))) T *lds_ptr(uint32_t a) {
 // acc + popcount(m) in one VALU op.  `after` ties it behind the mbcnt of
 // the same ballot, which already waited out the VALU-writes-SGPR hazard
 // that the hazard recognizer does not see through inline asm.
+
 static DEV uint32_t vbcnt(uint32_t m, uint32_t acc, uint32_t after) {
     uint32_t r;
     asm volatile("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "s"(m), "v"(acc), "v"(after));
@@ -1033,13 +1034,22 @@ static DEV void dec4_lean_body(const DecJob &J) {
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>(
         (__attribute__((address_space(3))) uint16_t *)(ring)));
     uint16_t *myob = obuf + (l & 3) * G;
-    uint32_t KEY[K > 0 ? K : 1];
+    uint32_t KEY[K > 0 ? K : 1], NKEY[K > 0 ? K : 1], KSH[K > 0 ? K : 1];
     // keys start << (32 - bits) - f: T = x << (32 - bits) is one shift, and
-    // T - key = (slot - start) << (32 - bits) | f (f <= 2^bits < 2^(32 - bits))
+    // T - key = (slot - start) << (32 - bits) | f (f <= 2^bits < 2^(32 - bits));
+    // NKEY = -key, so that T - key is one v_lshl_add_u32 of x.  KSH holds one
+    // opaque copy of the shift per key: with a shared x << ksh the compiler
+    // computes T once and subtracts (one more op on the chain)
     const uint32_t ksh = 32u - uint32_t(bits);
 #pragma unroll
-    for (int i = 0; i < (K > 0 ? K : 1); i++)
+    for (int i = 0; i < (K > 0 ? K : 1); i++) {
         KEY[i] = K > 0 ? ((J.reg[i] & 0xffffu) << ksh) - (J.reg[i] >> 16) : 0u;
+        NKEY[i] = 0u - KEY[i];
+        uint32_t k = ksh;
+        asm volatile("; opaque shift %0" : "+v"(k));
+        KSH[i] = k;
+    }
+    (void)KEY;
 #ifdef FQZ5_CHAIN_PROBE
     const uint64_t pr0 = __builtin_amdgcn_s_memtime(), rr0 = __builtin_amdgcn_s_memrealtime();
     uint64_t t_steps = 0, n_steps = 0;
@@ -1068,9 +1078,8 @@ static DEV void dec4_lean_body(const DecJob &J) {
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
                     if (K > 0) {
-                        // the window read first (its address is known since
-                        // the last step), so its latency hides behind the
-                        // selection
+#ifdef FQZ5_REGDEC_OLD
+                        // (round 5's step, for A/B builds)
                         const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
                         __builtin_amdgcn_sched_barrier(0);
                         const uint32_t T = x << ksh;
@@ -1087,6 +1096,33 @@ static DEV void dec4_lean_body(const DecJob &J) {
                         x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
                         ptr = vbcnt(uint32_t(m), ptr, r16);
                         continue;
+#else
+                        // the window read first (its address is known since
+                        // the last step), so its latency hides behind the
+                        // selection.  Round 6, three issue slots fewer a
+                        // step: each key's difference is one shift-add of x
+                        // (no separate T); the group keeps x itself (its low
+                        // 16 bits, the slot masked at the flush) instead of
+                        // x & mask; the word is a byte permute of the window
+                        // by a selector from the lane's rank (one mad24) in
+                        // place of the 64-bit shift.
+                        const uint64_t win = *lds_ptr<uint64_t>(wbase + (ptr << 1));
+                        __builtin_amdgcn_sched_barrier(0);
+                        a[u] = x;
+                        const uint32_t xh = x >> bits;
+                        uint32_t d = (x << KSH[0]) + NKEY[0];
+#pragma unroll
+                        for (int i = 1; i < K; i++) d = min(d, (x << KSH[i]) + NKEY[i]);
+                        const uint32_t xd = __umul24(d & ((1u << ksh) - 1u), xh) + (d >> ksh);
+                        const bool c = xd < RANS_LOW_D;
+                        const uint64_t m = __ballot(c);
+                        const uint32_t sel = __umul24(__builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u),
+                                                      0x0202u) + 0x0c0c0100u;
+                        const uint32_t w = __builtin_amdgcn_perm(uint32_t(win >> 32), uint32_t(win), sel);
+                        x = c ? __builtin_amdgcn_perm(xd, w, 0x05040100u) : xd;
+                        ptr = vbcnt(uint32_t(m), ptr, sel);
+                        continue;
+#endif
                     }
                     const uint32_t ea = O1 ? row + ((x & mask) << 4) : tab_lds + ((x & mask) << 4);
                     a[u] = O1 ? (ea >> 4) - idx0 : x & mask;
@@ -1164,7 +1200,7 @@ static DEV void dec4_lean_body(const DecJob &J) {
                     const uint2 q = *reinterpret_cast<const uint2 *>(obuf + z * G + 256 * h + 4 * l);
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
-                        const uint32_t sl = (k & 2 ? q.y : q.x) >> (16 * (k & 1)) & 0xffffu;
+                        const uint32_t sl = (k & 2 ? q.y : q.x) >> (16 * (k & 1)) & mask;
                         v[k] |= uint32_t(s2sym[sl]) << (8 * z);
                     }
                 }
@@ -1174,7 +1210,7 @@ static DEV void dec4_lean_body(const DecJob &J) {
         } else {
             const auto out = buf(J.out, n);
             for (uint32_t i = l; i < cnt; i += 64)
-                st8(out, NX * t0 + i, s2sym[obuf[(i & 3) * G + (i >> 2)]]);   // past n: dropped
+                st8(out, NX * t0 + i, s2sym[obuf[(i & 3) * G + (i >> 2)] & mask]);   // past n: dropped
         }
         __syncthreads();
         if (hedge_lost(hedge)) return;

@@ -1211,6 +1211,7 @@ unsigned long long fqz5_tok3_tokenise_digest_mode(const char *blk, int len, int 
 
 uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *out_len,
                            int *last_start_p) {
+    fqz5::CallTrace ct("tok3_encode_names", size_t(len > 0 ? len : 0));
     if (len < 0) {
         *out_len = 0;
         return nullptr;
@@ -1219,6 +1220,7 @@ uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *ou
     GUARD_BEGIN
     Tok3Enc T;
     const bool ok = tok3_tokenise(blk, len, level, use_arith, T);
+    ct.mark("tok");
     if (last_start_p && T.last_start >= 0) *last_start_p = T.last_start;
     if (!ok) return nullptr;
     GpuCtx &g = gpu();
@@ -1226,6 +1228,7 @@ uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *ou
     std::vector<CompressReq> reqs;
     tok3_add_requests(g, T, reqs);
     if (!reqs.empty()) compress_batch(g, reqs);
+    if (ct.k) { g.sync(); ct.mark("run"); }
     std::vector<uint8_t> o;
     const bool good = tok3_assemble(g, T, reqs, o);
     g.reset();
@@ -1239,6 +1242,7 @@ uint8_t *tok3_encode_names(char *blk, int len, int level, int use_arith, int *ou
 }
 
 uint8_t *tok3_decode_names(uint8_t *in, uint32_t sz, uint32_t *out_len) {
+    fqz5::CallTrace ct("tok3_decode_names", sz);
     GpuCtx *gp = nullptr;
     GUARD_BEGIN
     Tok3Dec D;

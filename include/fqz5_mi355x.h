@@ -160,8 +160,15 @@ char *fqz5_seq_decode_host(unsigned char *in, unsigned int in_size, unsigned int
  * every other chain on host cores (tests of the mixed placement).  Output
  * bytes do not depend on it.  Returns the previous setting. */
 int fqz5_set_host_decode(int mode);
-/* The host threads that leg uses. */
+/* The host threads of the library's pools: this rank's share of the cores
+ * (the affinity mask / $LOCAL_WORLD_SIZE, capped by $OMP_NUM_THREADS and 16;
+ * $FQZ5_HOST_THREADS overrides). */
 int fqz5_host_threads(void);
+/* The host-buffer encoder's trial batches (rans_compress_4x16 with a
+ * callee-allocated output): out3[0] calls taken by that path, out3[1] calls
+ * answered with an output a batch coded ahead, out3[2] batches of more than
+ * one order.  $FQZ5_NO_TRIAL_BATCH turns the path off. */
+void fqz5_trial_batch_stats(uint64_t *out3);
 /* Adaptive-model chains fqz5_decode_sections placed so far: out2[0] on host
  * cores, out2[1] on the GPU. */
 void fqz5_decode_chain_counts(uint64_t *out2);

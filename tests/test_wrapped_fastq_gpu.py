@@ -3,9 +3,10 @@ it (kseq.h:194-216; fastq.hip's parallel record chain, fqz5_fastq_index_any
 and fqz5_fastq_record_ends): for each case of tests/wrapped_cases.py the
 .fqz5 equals the reference CLI's (-t1, 1 MB blocks; md5s in
 tests/golden/wrapped.json, made by tests/golden/make_wrapped.py) at -1, -3
-and -5, and decoding it gives the CLI's -d text (4-line records).  Also:
-small windows cut inside wrapped records, the window cut rule on 4-line and
-wrapped text, and text kseq refuses."""
+and -5, and decoding it gives the CLI's -d text (4-line records); the cases
+include kseq's skipped lines between records and its kept lone '\r' bytes
+(junk, lonecr).  Also: small windows cut inside wrapped records, the window
+cut rule on 4-line and wrapped text, and text kseq refuses."""
 import hashlib
 import json
 import os
@@ -51,6 +52,29 @@ def test_wrapped_small_windows(texts, tmp_path):
     open(src, "wb").write(texts["illumina70"])
     fqz5file.compress_file(src, dst, 3, blk_size=1_000_000, window_bytes=300_001)
     assert md5(open(dst, "rb").read()) == g["fqz5_md5"]
+
+
+@pytest.mark.parametrize("case", ["junk", "lonecr"])
+def test_kseq_edges_small_windows(texts, tmp_path, case):
+    """kseq's skipped lines and kept lone '\r' bytes (round 6, VERDICT r05
+    item 8) with windows far smaller than a block: window cuts fall before
+    skipped lines, so a window can start with them."""
+    g = next(x for x in GOLD if x["case"] == case and x["level"] == 3)
+    src, dst = str(tmp_path / "w.fastq"), str(tmp_path / "w.fqz5")
+    open(src, "wb").write(texts[case])
+    fqz5file.compress_file(src, dst, 3, blk_size=1_000_000, window_bytes=200_003)
+    assert md5(open(dst, "rb").read()) == g["fqz5_md5"]
+
+
+def test_kseq_mid_line_header_refused():
+    """Skipped bytes holding '@' or '>' away from a line start would make
+    kseq start a record mid-line: still refused (never guessed)."""
+    fq = b"@a\nAC\n+\nII\njunk @x\n@b\nGT\n+\nII\n"
+    with pytest.raises(lib.NativeError):
+        fqz5file.compress_bytes(fq, 1)
+    fq = b"pre > text\n@a\nAC\n+\nII\n"
+    with pytest.raises(lib.NativeError):
+        fqz5file.compress_bytes(fq, 1)
 
 
 def test_record_ends():

@@ -4,6 +4,10 @@ reach the sequence's length).  Deterministic: tests/golden/make_wrapped.py
 codes them with the reference CLI and stores the md5s.
 
 Cases:
+  junk          4-line and wrapped records with lines kseq skips before,
+                between and after them (round 6)
+  lonecr        lone '\r' lines that kseq keeps as the first byte of a
+                sequence or quality block, and ones it drops (round 6)
   illumina70    the synthetic Illumina reads (fqzcomp5_amd.synth, seed 21)
                 with sequence and quality lines wrapped at 70 columns;
                 several 1 MB blocks at -b 1M
@@ -65,4 +69,60 @@ def mixed() -> bytes:
     return text[:-1] if text.endswith(b"\n") and not text.endswith(b"\r\n") else text
 
 
-CASES = {"illumina70": illumina70, "mixed": mixed}
+def junk() -> bytes:
+    """kseq's skip to the next header (kseq.h:180-186): lines before the
+    first record, between records and after the last that hold neither '@'
+    nor '>' (text, '+' lines, empty lines, lone '\r' and CRLF lines), among
+    4-line and 70-column wrapped records; two 1 MB blocks at -b 1M."""
+    r = synth.illumina(4200, seed=23, with_names=True)
+    text = synth.fastq_chunk(r, 0, r.num_records).tobytes()
+    lines = text.split(b"\n")
+    junks = [b"junk between records\n", b"+ a plus line\n", b"\n\n", b"\r\n", b"x y z\r\n",
+             b"+\n", b"0123456789\n"]
+    out = [b"# a first line that is no header\nmore text\n\n"]
+    for n, i in enumerate(range(0, len(lines) - 3, 4)):
+        h, sq, _, q = lines[i:i + 4]
+        if n % 3 == 1:
+            out.append(h + b"\n" + wrap(sq, 70) + b"+\n" + wrap(q, 70))
+        else:
+            out.append(h + b"\n" + sq + b"\n+\n" + q + b"\n")
+        if n % 5 == 2:
+            out.append(junks[(n // 5) % len(junks)])
+    out.append(b"trailing text\n")
+    return b"".join(out)
+
+
+def lonecr() -> bytes:
+    """A lone '\r' line before the first kept byte of a sequence or quality
+    block: kseq keeps that '\r' (its strip of a trailing '\r' needs two bytes
+    in the string, kseq.h:141), later ones it drops; with empty lines before
+    it, in CRLF records, as the whole sequence or quality."""
+    rng = np.random.default_rng(29)
+    out = []
+    for r in range(900):
+        n = int(rng.choice([1, 2, 5, 70, 71, 150]))
+        seq = bytes(rng.choice(np.frombuffer(b"ACGTN", np.uint8), n))
+        qual = bytes(rng.choice(np.frombuffer(b"#,:FIJ", np.uint8), n))
+        kind = r % 6
+        crlf = r % 4 == 3
+        nl = b"\r\n" if crlf else b"\n"
+        head = b"@cr%d" % r + nl
+        if kind == 0:        # both blocks start with the kept '\r'
+            sq, qq = b"\r\n" + wrap(seq[1:], 60, nl), b"\r\n" + wrap(qual[1:], 60, nl)
+        elif kind == 1:      # the qualities only
+            sq, qq = wrap(seq, 60, nl), b"\r\n" + wrap(qual[1:], 60, nl)
+        elif kind == 2:      # the bases only, empty lines before it
+            sq, qq = b"\n\n\r\n" + wrap(seq[1:], 60, nl), wrap(qual, 60, nl)
+        elif kind == 3:      # a second lone '\r' line is dropped
+            sq, qq = b"\r\n\r\n" + wrap(seq[1:], 60, nl), b"\n\r\n\r\n" + wrap(qual[1:], 60, nl)
+        elif kind == 4:      # no '\r'
+            sq, qq = wrap(seq, 60, nl), wrap(qual, 60, nl)
+        else:                # a lone '\r' after the first bases is dropped
+            sq, qq = wrap(seq, 60, nl) + b"\r\n", wrap(qual, 60, nl) + b"\r\n"
+        if n == 1 and kind in (0, 3):        # the '\r' is the whole block
+            sq, qq = b"\r\n", b"\r\n"
+        out.append(head + sq + b"+" + nl + qq)
+    return b"".join(out)
+
+
+CASES = {"illumina70": illumina70, "mixed": mixed, "junk": junk, "lonecr": lonecr}
