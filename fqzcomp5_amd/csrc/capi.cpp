@@ -82,6 +82,9 @@ __attribute__((constructor)) static void early_init_start() {
     if (std::getenv("FQZ5_NO_EARLY_INIT")) return;
     if (dlsym(RTLD_DEFAULT, "Py_IsInitialized")) return;
     hw_queues_default();                    // (its environment first: runs before HIP starts)
+    // every code object of the library loaded at start, by that thread,
+    // rather than each on its first kernel launch inside a call
+    setenv("HIP_ENABLE_DEFERRED_LOADING", "0", 0);
     try {
         g_early = std::thread([] {
             int n = 0;
@@ -352,9 +355,13 @@ struct TrialCache {
     ~TrialCache() { drop_ready(); }
 };
 static thread_local TrialCache t_trial;
-static thread_local std::vector<int> t_prev_asked;     // this thread's previous input
+static thread_local std::vector<int> t_pat;            // this thread's last multi-order input
 static std::mutex g_pat_mu;
 static std::vector<int> g_pat;                         // the last multi-order input of any thread
+// Before any input was asked for several orders: the preset trials' rANS
+// orders (RANS0, RANS1, RANS129, RANS193), which compress_with_methods
+// starts with RANS0 (the lowest method bit, fqzcomp5.c:1979-1998)
+static const std::vector<int> k_trial_default{0, 1, 129, 193};
 static std::atomic<uint64_t> g_trial_stats[3];         // calls, served from a batch, batches > 1
 static bool trial_batch_on() {
     static const bool on = std::getenv("FQZ5_NO_TRIAL_BATCH") == nullptr;
@@ -384,12 +391,10 @@ static unsigned char *rans_compress_trial(const unsigned char *in, unsigned int 
             if (std::find(c.asked.begin(), c.asked.end(), o) == c.asked.end() && !c.ready.count(o))
                 want.push_back(o);
     } else {
-        if (c.valid) {
-            t_prev_asked = c.asked;
-            if (c.asked.size() >= 2) {
-                std::lock_guard<std::mutex> lk(g_pat_mu);
-                g_pat = c.asked;
-            }
+        if (c.valid && c.asked.size() >= 2) {
+            t_pat = c.asked;
+            std::lock_guard<std::mutex> lk(g_pat_mu);
+            g_pat = c.asked;
         }
         c.drop_ready();
         c.valid = false;
@@ -398,14 +403,18 @@ static unsigned char *rans_compress_trial(const unsigned char *in, unsigned int 
         c.n = in_size;
         c.valid = true;
         c.asked.assign(1, order);
-        std::vector<int> pat;
-        if (t_prev_asked.size() >= 2) {
-            pat = t_prev_asked;
-        } else if (t_prev_asked.empty()) {            // no history on this thread yet
+        // a trial asks its orders in a fixed sequence: a call for the first
+        // order of the last trial seen (this thread's, else any thread's,
+        // else the presets') starts another, and the rest is coded with it.
+        // A block past the trial asks one order, its section's winner, on
+        // each input: only when that winner is the trial's first order is
+        // the batch coded for nothing (beside a chain at least as long).
+        std::vector<int> pat = t_pat;
+        if (pat.empty()) {
             std::lock_guard<std::mutex> lk(g_pat_mu);
-            pat = g_pat;
+            pat = g_pat.empty() ? k_trial_default : g_pat;
         }
-        if (std::find(pat.begin(), pat.end(), order) != pat.end())
+        if (!pat.empty() && pat[0] == order)
             for (int o : pat)
                 if (o != order) want.push_back(o);
     }

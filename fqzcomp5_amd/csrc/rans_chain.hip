@@ -1142,11 +1142,11 @@ static DEV void dec4_lean_body(const DecJob &J) {
                     ptr = vbcnt(uint32_t(m), ptr, r16);
                     if (O1) row = e.w;
                 }
+                // pairs of low halves (a register decoder's a[] hold whole x)
+                auto pk = [](uint32_t lo, uint32_t hi) { return __builtin_amdgcn_perm(hi, lo, 0x05040100u); };
                 uint4 *o = reinterpret_cast<uint4 *>(myob + (t - t0));
-                o[0] = make_uint4(a[0] | a[1] << 16, a[2] | a[3] << 16, a[4] | a[5] << 16,
-                                  a[6] | a[7] << 16);
-                o[1] = make_uint4(a[8] | a[9] << 16, a[10] | a[11] << 16, a[12] | a[13] << 16,
-                                  a[14] | a[15] << 16);
+                o[0] = make_uint4(pk(a[0], a[1]), pk(a[2], a[3]), pk(a[4], a[5]), pk(a[6], a[7]));
+                o[1] = make_uint4(pk(a[8], a[9]), pk(a[10], a[11]), pk(a[12], a[13]), pk(a[14], a[15]));
             }
 #ifdef FQZ5_CHAIN_PROBE
             t_steps += __builtin_amdgcn_s_memtime() - ps0;

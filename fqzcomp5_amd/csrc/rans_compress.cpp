@@ -16,6 +16,8 @@
 // Each stage is one launch over all streams of the batch.  The reference's
 // capacity failures (NULL returns) are decided in stage 6 from sizes: they
 // never change the bytes of a successful call.
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <algorithm>
 #include <map>
 #include <chrono>
@@ -502,7 +504,7 @@ void Compressor::stage_tables() {
     const double tb = trace ? now() : 0;
     host_parallel(o1jobs.size(), [&](size_t k) { build_o1(jobs_[o1jobs[k]], &h[jobs_[o1jobs[k]].f1_off]); });
     if (trace)
-        std::fprintf(stderr, "tables: o1 hist %.1f ms, build_o1 %.1f ms (%zu jobs, %u pairs)\n",
+        std::fprintf(stderr, "[tid %ld] tables: o1 hist %.1f ms, build_o1 %.1f ms (%zu jobs, %u pairs)\n", long(syscall(SYS_gettid)),
                      tb - ta, now() - tb, o1jobs.size(), total);
 }
 
@@ -687,8 +689,8 @@ void Compressor::stage_encode() {
     for (size_t i = nmain; i < jobs_.size(); i++) finish_job(jobs_[i]);
     for (size_t i = 0; i < nmain; i++) finish_job(jobs_[i]);
     if (trace)
-        std::fprintf(stderr, "encode: tables %.1f ms (%zu syms), uploads+launch %.1f ms, "
-                     "wait %.1f ms, finish %.1f ms\n", tb - ta, nsyms + all_syms.size(), tc - tb,
+        std::fprintf(stderr, "[tid %ld] encode: tables %.1f ms (%zu syms), uploads+launch %.1f ms, "
+                     "wait %.1f ms, finish %.1f ms\n", long(syscall(SYS_gettid)), tb - ta, nsyms + all_syms.size(), tc - tb,
                      td - tc, now() - td);
 }
 
@@ -891,7 +893,7 @@ void Compressor::run(std::vector<CompressReq> &reqs) {
                    std::chrono::steady_clock::now().time_since_epoch()).count();
     };
     const double t0 = trace ? now() : 0;
-    if (trace) std::fprintf(stderr, "compress: leaves %.1f ms\n", t0 - t_enter);
+    if (trace) std::fprintf(stderr, "[tid %ld] compress: leaves %.1f ms\n", long(syscall(SYS_gettid)), t0 - t_enter);
     stage_pack();
     const double t1 = trace ? now() : 0;
     stage_rle();
@@ -920,15 +922,15 @@ void Compressor::run(std::vector<CompressReq> &reqs) {
     stage_encode();
     const double t5 = trace ? now() : 0;
     if (trace)
-        std::fprintf(stderr, "compress: pack %.1f ms, rle %.1f ms, jobs %.1f ms, tables %.1f ms, "
-                     "encode %.1f ms (%zu requests, %zu jobs)\n", t1 - t0, t2 - t1, t3 - t2,
+        std::fprintf(stderr, "[tid %ld] compress: pack %.1f ms, rle %.1f ms, jobs %.1f ms, tables %.1f ms, "
+                     "encode %.1f ms (%zu requests, %zu jobs)\n", long(syscall(SYS_gettid)), t1 - t0, t2 - t1, t3 - t2,
                      t4 - t3, t5 - t4, reqs.size(), jobs_.size());
     struct Done {
         bool on;
         double t;
         ~Done() {
             if (on)
-                std::fprintf(stderr, "compress: layouts %.1f ms\n",
+                std::fprintf(stderr, "[tid %ld] compress: layouts %.1f ms\n", long(syscall(SYS_gettid)),
                              std::chrono::duration<double, std::milli>(
                                  std::chrono::steady_clock::now().time_since_epoch()).count() - t);
         }
@@ -973,7 +975,7 @@ void compress_batch(GpuCtx &g, std::vector<CompressReq> &reqs) {
     // them, so a detached thread frees them off the caller's critical path.
     if (c->njobs() > 1000) std::thread([p = c.release()] { delete p; }).detach();
     else c.reset();
-    if (trace) std::fprintf(stderr, "compress: teardown %.1f ms\n", now() - t0);
+    if (trace) std::fprintf(stderr, "[tid %ld] compress: teardown %.1f ms\n", long(syscall(SYS_gettid)), now() - t0);
 }
 
 // ---------------------------------------------------------------------------

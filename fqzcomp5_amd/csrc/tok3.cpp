@@ -1249,9 +1249,11 @@ uint8_t *tok3_decode_names(uint8_t *in, uint32_t sz, uint32_t *out_len) {
     if (!tok3_dec_parse(in, sz, D)) return nullptr;
     GpuCtx &g = gpu();
     gp = &g;
+    ct.mark("ctx");
     std::vector<DecompressReq> reqs;
     tok3_dec_add_requests(g, D, nullptr, reqs);
     if (!reqs.empty()) decompress_batch(g, reqs);
+    if (ct.k) { g.sync(); ct.mark("run"); }
     std::vector<uint8_t> o;
     const bool good = tok3_dec_finish(g, D, reqs, o);
     g.reset();

@@ -17,7 +17,7 @@ t timeout -k 10 120 $CPU -$LV -t16 /tmp/w.fastq /tmp/c.fqz5
 t timeout -k 10 120 $CPU -d -t16 /tmp/c.fqz5 /tmp/c.fq
 t timeout -k 10 120 $GPU -$LV -t16 /tmp/w.fastq /tmp/g.fqz5
 t timeout -k 10 120 $GPU -d -t16 /tmp/c.fqz5 /tmp/g.fq
-FQZ5_CALL_TRACE=1 t timeout -k 10 120 $GPU -$LV -t16 /tmp/w.fastq /tmp/g.fqz5 2> $OUT/enc_calls.txt
+FQZ5_CALL_TRACE=1 FQZ5_STEP_TRACE=1 t timeout -k 10 120 $GPU -$LV -t16 /tmp/w.fastq /tmp/g.fqz5 2> $OUT/enc_calls.txt
 FQZ5_CALL_TRACE=1 t timeout -k 10 120 $GPU -d -t16 /tmp/c.fqz5 /tmp/g.fq 2> $OUT/dec_calls.txt
 cmp /tmp/c.fq /tmp/w.fastq && cmp /tmp/g.fq /tmp/w.fastq && cmp /tmp/c.fqz5 /tmp/g.fqz5 && echo same >> $OUT/times.txt
 cat $OUT/times.txt

@@ -34,6 +34,14 @@ for k in ('level5','level5_illumina'):
 print('cpu', {k:d.get('cpu_baseline',{}).get(k) for k in ('value','enc_MBps','dec_MBps','blocks_match_gpu')})
 print('dropin', json.dumps(d.get('dropin_cli'))[:900])
 " ;;
+    n2)   # the N = 2 path rehearsed on one GPU (gloo), strong scaling, beside
+          # the one-process run's blocks split the same way
+      FQZ5_BENCH_SPLIT=2 timeout -k 10 600 python -u bench.py --steps 3 --warmup 1 --no-level5 --no-dropin --no-cpu --no-crc > $O/${TAG}_n1split.json 2> $O/${TAG}_n1split.log || { echo N1SPLIT failed; tail -5 $O/${TAG}_n1split.log; exit 1; }
+      FQZ5_BENCH_SHARE_GPU=1 timeout -k 10 900 python -u bench.py --gpus 2 --steps 3 --warmup 1 --scaling strong --no-level5 --no-dropin --no-cpu --no-crc > $O/${TAG}_n2.json 2> $O/${TAG}_n2.log || { echo N2 failed; tail -20 $O/${TAG}_n2.log; exit 1; }
+      python3 -c "
+import json; L=lambda f: json.loads(open(f).read().strip().splitlines()[-1]); a=L('$O/${TAG}_n1split.json'); b=L('$O/${TAG}_n2.json')
+print('n1 split', a['config']['blocks_md5_by_rank'], a['value']); print('n2', b['config']['blocks_md5_by_rank'], b['value'], b['n_gpus'])
+print('N2_BLOCKS_EQUAL', a['config']['blocks_md5_by_rank'] == b['config']['blocks_md5_by_rank'])" ;;
     dropin)
       timeout -k 10 600 bash tools/dropin_trace.sh $O/${TAG}_dropin > $O/${TAG}_dropin.log 2>&1
       rc=$?; tail -12 $O/${TAG}_dropin.log; [ $rc = 0 ] || { echo "DROPIN rc=$rc"; exit 1; } ;;
