@@ -12,8 +12,6 @@
 #include <csignal>
 #include <execinfo.h>
 #include <unistd.h>
-#include <dlfcn.h>
-#include <thread>
 #include <sys/syscall.h>
 #include <chrono>
 
@@ -68,34 +66,6 @@ __attribute__((constructor)) static void hw_queues_default() {
 }
 
 static thread_local std::string g_err;
-
-// A C host (the relinked CLI: the library's first call comes ~100 ms after
-// the process starts, once it has read its first block) pays the HIP
-// runtime's start-up (~200 ms) inside that first call.  So when the library
-// is loaded into a process that is not a Python interpreter (which starts
-// HIP itself, through torch, when it wants to), a thread starts the runtime
-// and the device at load, beside the host's own start; the library's
-// destructor joins it, so a host that exits at once never leaves it running.
-// $FQZ5_NO_EARLY_INIT=1 turns it off.
-static std::thread g_early;
-__attribute__((constructor)) static void early_init_start() {
-    if (std::getenv("FQZ5_NO_EARLY_INIT")) return;
-    if (dlsym(RTLD_DEFAULT, "Py_IsInitialized")) return;
-    hw_queues_default();                    // (its environment first: runs before HIP starts)
-    // every code object of the library loaded at start, by that thread,
-    // rather than each on its first kernel launch inside a call
-    setenv("HIP_ENABLE_DEFERRED_LOADING", "0", 0);
-    try {
-        g_early = std::thread([] {
-            int n = 0;
-            if (hipGetDeviceCount(&n) == hipSuccess && n > 0) (void)hipFree(nullptr);
-        });
-    } catch (...) {
-    }
-}
-__attribute__((destructor)) static void early_init_join() {
-    if (g_early.joinable()) g_early.join();
-}
 
 // the process-wide kernel profile (gpu_ctx.hpp: ProfKernel)
 static std::mutex g_prof_mu;
@@ -173,7 +143,7 @@ CallTrace::CallTrace(const char *f, size_t bytes) : fn(f), n(bytes) {
     k = 1;
 }
 void CallTrace::mark(const char *what) {
-    if (!k || k >= 5) return;
+    if (!k || k >= 9) return;
     t[k] = since_load_ms();
     tag[k++] = what;
 }
@@ -326,24 +296,8 @@ static uint32_t header_size(const uint8_t *in, uint32_t len, bool *ok) {
 // (rans_compress_4x16, callee-allocated) take this path, so the capacity
 // semantics of rans_compress_to_4x16 are untouched.  $FQZ5_NO_TRIAL_BATCH
 // turns it off.
-struct PinnedBuf {
-    uint8_t *p = nullptr;
-    size_t cap = 0;
-    void ensure(size_t n) {
-        if (n <= cap) return;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-        const size_t c = std::max(n, size_t(1) << 20);
-        FQZ5_HIP(hipHostMalloc(reinterpret_cast<void **>(&p), c, hipHostMallocDefault));
-        cap = c;
-    }
-    ~PinnedBuf() {
-        if (p) (void)hipHostFree(p);
-    }
-};
 struct TrialCache {
-    PinnedBuf in;                 // the input's bytes: the upload source and the comparison
+    std::vector<uint8_t> in;      // the input's bytes: the upload source and the comparison
     uint32_t n = 0;
     bool valid = false;
     std::vector<int> asked;       // orders asked for on this input, in call order
@@ -370,10 +324,10 @@ static bool trial_batch_on() {
 constexpr uint32_t TRIAL_MIN_BYTES = 1u << 16;         // smaller inputs: the plain call
 
 static unsigned char *rans_compress_trial(const unsigned char *in, unsigned int in_size,
-                                          unsigned int *out_size, int order) {
+                                          unsigned int *out_size, int order, CallTrace &ct) {
     TrialCache &c = t_trial;
     g_trial_stats[0]++;
-    const bool same = c.valid && c.n == in_size && std::memcmp(c.in.p, in, in_size) == 0;
+    const bool same = c.valid && c.n == in_size && std::memcmp(c.in.data(), in, in_size) == 0;
     std::vector<int> want{order};
     if (same) {
         if (std::find(c.asked.begin(), c.asked.end(), order) == c.asked.end())
@@ -398,8 +352,8 @@ static unsigned char *rans_compress_trial(const unsigned char *in, unsigned int 
         }
         c.drop_ready();
         c.valid = false;
-        c.in.ensure(in_size);
-        std::memcpy(c.in.p, in, in_size);
+        if (c.in.size() < in_size) c.in.resize(in_size);
+        std::memcpy(c.in.data(), in, in_size);
         c.n = in_size;
         c.valid = true;
         c.asked.assign(1, order);
@@ -419,9 +373,10 @@ static unsigned char *rans_compress_trial(const unsigned char *in, unsigned int 
                 if (o != order) want.push_back(o);
     }
     if (want.size() > 1) g_trial_stats[2]++;
+    ct.mark("copy");
     GpuCtx &g = gpu();
-    uint8_t *d_in = g.arena.alloc_n<uint8_t>(in_size);
-    FQZ5_HIP(hipMemcpyAsync(d_in, c.in.p, in_size, hipMemcpyHostToDevice, g.stream));
+    const uint8_t *d_in = g.upload_sync(c.in.data(), in_size);
+    if (ct.k) { g.sync(); ct.mark("up"); }
     std::vector<CompressReq> reqs(want.size());
     for (size_t i = 0; i < want.size(); i++) {
         reqs[i].d_in = d_in;
@@ -430,6 +385,7 @@ static unsigned char *rans_compress_trial(const unsigned char *in, unsigned int 
         reqs[i].cap = compress_bound(in_size, want[i]);
     }
     compress_batch(g, reqs);
+    if (ct.k) { g.sync(); ct.mark("run"); }
     unsigned char *asked = nullptr;
     uint32_t asked_sz = 0;
     for (size_t i = 0; i < reqs.size(); i++) {
@@ -446,6 +402,7 @@ static unsigned char *rans_compress_trial(const unsigned char *in, unsigned int 
             c.ready[want[i]] = {dst, sz};
         }
     }
+    ct.mark("down");
     g.reset();
     if (!asked) {
         *out_size = 0;
@@ -513,13 +470,11 @@ unsigned char *rans_compress_to_4x16(unsigned char *in, unsigned int in_size,
     GUARD_BEGIN
     CallTrace ct("rans_compress", in_size);
     if (!out && in && in_size >= TRIAL_MIN_BYTES && trial_batch_on()) {
-        unsigned char *r = rans_compress_trial(in, in_size, out_size, order);
-        if (ct.k) ct.mark("trial");
-        return r;
+        return rans_compress_trial(in, in_size, out_size, order, ct);
     }
     GpuCtx &g = gpu();
     std::vector<CompressReq> reqs(1);
-    reqs[0].d_in = g.upload(in, in_size);
+    reqs[0].d_in = g.upload_sync(in, in_size);
     if (ct.k) { g.sync(); ct.mark("up"); }
     reqs[0].n = in_size;
     reqs[0].order = order;
@@ -565,7 +520,7 @@ unsigned char *rans_uncompress_to_4x16(unsigned char *in, unsigned int in_size,
     GpuCtx &g = gpu();
     std::vector<DecompressReq> reqs(1);
     reqs[0].h_in = in;
-    reqs[0].d_in = g.upload(in, in_size);
+    reqs[0].d_in = g.upload_sync(in, in_size);
     if (ct.k) { g.sync(); ct.mark("up"); }
     reqs[0].in_size = in_size;
     reqs[0].out_cap = cap;

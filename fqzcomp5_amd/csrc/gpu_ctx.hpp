@@ -285,7 +285,9 @@ class PinnedArena {
                 return p;
             }
         }
-        size_t sz = n > (size_t(64) << 20) ? n : (size_t(64) << 20);
+        // (8 MB chunks: pinning 64 MB on a thread's first upload took ~100-200 ms
+        // with several new threads at once, the drop-in CLI's workers)
+        size_t sz = n > (size_t(8) << 20) ? n : (size_t(8) << 20);
         Chunk c{nullptr, sz, n};
         ChunkPool::alloc_calls().fetch_add(1, std::memory_order_relaxed);
         FQZ5_HIP(hipHostMalloc(reinterpret_cast<void **>(&c.base), sz, hipHostMallocDefault));
@@ -343,8 +345,8 @@ bool call_trace_on();
 struct CallTrace {
     const char *fn;
     size_t n;
-    double t[6];
-    const char *tag[6];
+    double t[10];
+    const char *tag[10];
     int k = 0;
     CallTrace(const char *f, size_t bytes);
     void mark(const char *what);            // a stage ends here
@@ -472,6 +474,20 @@ struct GpuCtx {
             std::memcpy(st, h, n * sizeof(T));
             FQZ5_HIP(hipMemcpyAsync(d, st, n * sizeof(T), hipMemcpyHostToDevice, stream));
         }
+        return d;
+    }
+    // A host-buffer call's input (the drop-in entry points, an idle stream):
+    // copied from the caller's memory through the runtime's shared staging
+    // and waited for, so the caller's buffer may die after it.  Large
+    // inputs through the thread's own pinned staging instead meant pinning
+    // a chunk of their size (hipHostMalloc) on each worker thread's first
+    // call: 150-570 ms with the drop-in CLI's workers starting together
+    // (profiles/r06_dropin_*).  Small ones keep the staging (cheap).
+    template <class T> T *upload_sync(const T *h, size_t n) {
+        if (n * sizeof(T) < (size_t(1) << 20)) return upload(h, n);
+        T *d = arena.alloc_n<T>(n);
+        FQZ5_HIP(hipMemcpyAsync(d, h, n * sizeof(T), hipMemcpyHostToDevice, stream));
+        sync();
         return d;
     }
     // Rewind both arenas; only after everything queued has completed.

@@ -84,11 +84,13 @@ def test_crlf_and_no_final_newline(tmp_path):
 
 def test_not_fastq_fails_loudly():
     """Text kseq_read refuses (kseq.h:212-216: -2) is refused; wrapped FASTQ
-    is read (tests/test_wrapped_fastq_gpu.py)."""
+    and lines kseq skips between records are read (tests/
+    test_wrapped_fastq_gpu.py); skipped bytes with a '@' away from a line
+    start (kseq would start a record mid-line) stay refused."""
     for bad in (b"@r1\nACGT\n+\nIII\n",                  # qualities short (EOF)
                 b"@r1\nACGT\n+\nIIIII\n@r2\nA\n+\nI\n",   # qualities long
                 b"@r1\nAC\nGT\n+\nII\n@r2\nA\n+\nI\n",   # wrapped, one quality short
-                b"@r1\nACGT\n+\nIIII\nxx\n@r2\nA\n+\nI\n"):   # bytes between records
+                b"@r1\nACGT\n+\nIIII\nx@x\n@r2\nA\n+\nI\n"):   # a header mid-line
         with pytest.raises(lib.NativeError):
             fqz5file.compress_bytes(bad, 3)
     with pytest.raises(lib.NativeError):                  # FASTQ record in FASTA text
