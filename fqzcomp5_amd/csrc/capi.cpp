@@ -301,12 +301,14 @@ struct TrialCache {
     uint32_t n = 0;
     bool valid = false;
     std::vector<int> asked;       // orders asked for on this input, in call order
-    std::map<int, std::pair<uint8_t *, uint32_t>> ready;   // coded ahead, not yet asked
-    void drop_ready() {
-        for (auto &kv : ready) free(kv.second.first);
+    // coded ahead, not yet asked: kept in device memory (its own arena) and
+    // brought down only when asked (a batch call brings down one output)
+    std::map<int, std::pair<uint8_t *, uint32_t>> ready;
+    DevArena dev;
+    void drop_ready() {                      // (no queued work uses dev: batches sync)
         ready.clear();
+        dev.reset();
     }
-    ~TrialCache() { drop_ready(); }
 };
 static thread_local TrialCache t_trial;
 static thread_local std::vector<int> t_pat;            // this thread's last multi-order input
@@ -334,8 +336,11 @@ static unsigned char *rans_compress_trial(const unsigned char *in, unsigned int 
             c.asked.push_back(order);
         auto it = c.ready.find(order);
         if (it != c.ready.end()) {
-            unsigned char *r = it->second.first;
-            *out_size = it->second.second;
+            const uint32_t sz = it->second.second;
+            auto *r = static_cast<unsigned char *>(malloc(compress_bound(in_size, order)));
+            if (!r) { *out_size = 0; return nullptr; }
+            if (sz) FQZ5_HIP(hipMemcpy(r, it->second.first, sz, hipMemcpyDeviceToHost));
+            *out_size = sz;
             c.ready.erase(it);
             g_trial_stats[1]++;
             return r;
@@ -388,19 +393,27 @@ static unsigned char *rans_compress_trial(const unsigned char *in, unsigned int 
     if (ct.k) { g.sync(); ct.mark("run"); }
     unsigned char *asked = nullptr;
     uint32_t asked_sz = 0;
+    std::vector<const Layout *> keep;
+    std::vector<uint8_t *> keep_at;
     for (size_t i = 0; i < reqs.size(); i++) {
         if (!reqs[i].ok) continue;                     // (a speculated order: not kept)
         const uint32_t sz = layout_size(reqs[i].out);
-        const size_t alloc = i == 0 ? compress_bound(in_size, want[i]) : std::max<size_t>(sz, 1);
-        auto *dst = static_cast<unsigned char *>(malloc(alloc));
-        if (!dst) continue;
-        write_layout_host(g, reqs[i].out, dst);
         if (i == 0) {
+            auto *dst = static_cast<unsigned char *>(malloc(compress_bound(in_size, want[i])));
+            if (!dst) continue;
+            write_layout_host(g, reqs[i].out, dst);
             asked = dst;
             asked_sz = sz;
         } else {
-            c.ready[want[i]] = {dst, sz};
+            uint8_t *d = c.dev.alloc_n<uint8_t>(std::max<uint32_t>(sz, 1));
+            keep.push_back(&reqs[i].out);
+            keep_at.push_back(d);
+            c.ready[want[i]] = {d, sz};
         }
+    }
+    if (!keep.empty()) {                               // one copy launch for all of them
+        write_layouts_dev(g, keep, keep_at);
+        g.sync();
     }
     ct.mark("down");
     g.reset();
