@@ -70,6 +70,7 @@ elif os.environ.get("GPU_MAX_HW_QUEUES", "") in ("", "4"):
 
 FASTQ_REC = 358          # bytes of FASTQ text per synthetic 150 bp record (avg)
 GAP_S = float(os.environ.get("FQZ5_BENCH_GAP_S", "0") or 0)
+STEP_TRACE = bool(os.environ.get("FQZ5_STEP_TRACE"))   # per-phase decode times on stderr
 BLK = 100_000_000        # -3 / -5 block size (fqzcomp5.c:4896,4904)
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8 TB/s spec
 # fqz5_profile_read_all's kernels, in its order (include/fqz5_mi355x.h); each
@@ -269,7 +270,17 @@ def measure(level, kind, gb, steps, warmup, cpu, cpu_threads, world, rank, local
         return res, meth_all, tried, off
 
     def decode(res):
-        return S.decode(run.block_dec_secs())      # parse + CRC check, sections
+        if not STEP_TRACE:
+            return S.decode(run.block_dec_secs())  # parse + CRC check, sections
+        a = time.perf_counter()
+        secs = run.block_dec_secs()
+        b = time.perf_counter()
+        out = S.decode(secs)
+        c = time.perf_counter()
+        torch.cuda.synchronize()
+        log(f"[bench] decode: parse {1e3*(b-a):.1f} ms, sections {1e3*(c-b):.1f} ms, "
+            f"sync {1e3*(time.perf_counter()-c):.1f} ms")
+        return out
 
     for _ in range(warmup):
         decode(encode()[0])

@@ -942,6 +942,13 @@ int fqz5_encode_sections(const fqz5_section *secs, int nsec, const uint32_t *ava
 }
 
 int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result *res) {
+    // (trace) entry to exit, the locals' destructors included
+    struct ExitTrace {
+        double t;
+        ~ExitTrace() {
+            if (t) std::fprintf(stderr, "decode_sections: entry to exit %.1f ms\n", now_ms() - t);
+        }
+    } exit_trace{step_trace() ? now_ms() : 0.0};
     try {
         GpuCtx &g = gpu();
         static const bool trace = std::getenv("FQZ5_STEP_TRACE") != nullptr;
@@ -1154,6 +1161,7 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         // the CUs and the names' short kernels find the rest free (their
         // host rebuild needs no CU at all).
         std::exception_ptr nerr;
+        double t_names_up = 0;                        // (trace) the names' upload done
         std::thread tn;
         GpuCtx *gn = nullptr;
         std::unique_ptr<HedgeShare> nshare;
@@ -1169,9 +1177,10 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
                     // stream, -5 NovaSeq's 590 MB of names added ~50 ms)
                     for (size_t k = 0; k < nd.size(); k++)
                         if (nd[k].ok && nd[k].u_len)
-                            FQZ5_HIP(hipMemcpyAsync(secs[who_name[k]].out, nd[k].names.data(),
+                            FQZ5_HIP(hipMemcpyAsync(secs[who_name[k]].out, nd[k].names,
                                                     nd[k].u_len, hipMemcpyHostToDevice, gn->stream));
                     gn->sync();                       // (nd's buffers are the sources)
+                    if (trace) t_names_up = now_ms();
                 } catch (...) {
                     nerr = std::current_exception();
                 }
@@ -1245,6 +1254,7 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         }
         Join join_seq{ts};
         decompress_batch(g, reqs);
+        const double t_rans = trace ? now_ms() : 0;
         if (trace)
             std::fprintf(stderr, "decode_sections: %zu bytes to host in %.1f ms, rANS %.1f ms\n", tot,
                          std::chrono::duration<double, std::milli>(t1 - t0).count(),
@@ -1343,9 +1353,11 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
                     FQZ5_HIP(hipMemcpyAsync(secs[c.sec].out, c.buf, c.n, hipMemcpyHostToDevice, g.stream));
             }
         }
+        const double t_hc = trace ? now_ms() : 0;
         if (tn.joinable()) tn.join();
         nshare.reset();
         if (nerr) std::rethrow_exception(nerr);
+        const double t_nj = trace ? now_ms() : 0;
         for (size_t k = 0; k < nd.size(); k++) {
             fqz5_section_result &R = res[who_name[k]];
             if (!nd[k].ok) continue;                    // (uploaded by the names thread)
@@ -1374,6 +1386,12 @@ int fqz5_decode_sections(const fqz5_section *secs, int nsec, fqz5_section_result
         if (gn) gn->reset();
         if (gf) gf->reset();
         if (gs) gs->reset();
+        if (trace) {
+            const double tb = std::chrono::duration<double, std::milli>(t0.time_since_epoch()).count();
+            std::fprintf(stderr, "decode_sections: from its start: rANS done %.1f, host chains joined "
+                         "%.1f, names uploaded %.1f, names joined %.1f, reset %.1f ms\n", t_rans - tb,
+                         t_hc - tb, t_names_up ? t_names_up - tb : -1.0, t_nj - tb, now_ms() - tb);
+        }
         return 0;
     } catch (const std::exception &e) {
         fqz5_set_error(e.what());

@@ -424,12 +424,15 @@ void name_dec_fetch(GpuCtx &g, NameDec &D, const std::vector<DecompressReq> &req
                     const std::vector<LzpDecReq> &lz) {
     D.fetched = false;
     D.ok = false;
-    D.names.assign(D.u_len, 0);
+    D.names = D.fl = D.out2 = nullptr;
+    D.fl_len = D.out2_len = 0;
     if (D.strat == 0) {
         if (D.lzp < 0 || !lz[size_t(D.lzp)].ok) return;
         const uint32_t n = std::min(lz[size_t(D.lzp)].out_len, D.u_len);
-        g.download(D.names.data(), D.d_lout, n);
+        D.names = g.staging.alloc(size_t(D.u_len) + 1);
+        g.download(D.names, D.d_lout, n);
         g.sync();
+        std::memset(D.names + n, 0, D.u_len - n);
         D.fetched = true;
         return;
     }
@@ -437,13 +440,19 @@ void name_dec_fetch(GpuCtx &g, NameDec &D, const std::vector<DecompressReq> &req
     if (D.strat == 2) {
         if (D.req_flag < 0 || !reqs[size_t(D.req_flag)].ok) return;
         if (D.clen2 && (D.lzp < 0 || !lz[size_t(D.lzp)].ok)) return;
-        D.fl.resize(reqs[size_t(D.req_flag)].out_size);
-        g.download(D.fl.data(), D.d_flag, D.fl.size());
+        D.fl_len = reqs[size_t(D.req_flag)].out_size;
+        D.fl = g.staging.alloc(size_t(D.fl_len) + 1);
+        g.download(D.fl, D.d_flag, D.fl_len);
         if (D.clen2) {
-            D.out2.resize(lz[size_t(D.lzp)].out_len);
-            g.download(D.out2.data(), D.d_lout, D.out2.size());
+            D.out2_len = lz[size_t(D.lzp)].out_len;
+            D.out2 = g.staging.alloc(size_t(D.out2_len) + 1);
+            g.download(D.out2, D.d_lout, D.out2_len);
         }
         g.sync();
+        // the stitch writes up to u_len + 2 bytes a record (fqzcomp5.c:1683-1777)
+        D.names = g.staging.alloc(size_t(D.u_len) + size_t(D.fl_len) * 2 + 1);
+    } else {
+        D.names = g.staging.alloc(size_t(D.u_len) + 1);
     }
     D.fetched = true;
 }
@@ -458,19 +467,21 @@ void name_dec_rebuild(NameDec &D) {
     std::vector<uint8_t> out1;
     if (!tok3_dec_rebuild(D.tok, out1)) return;
     if (D.strat == 1) {
-        std::memcpy(D.names.data(), out1.data(), std::min<size_t>(out1.size(), D.u_len));
+        const size_t n = std::min<size_t>(out1.size(), D.u_len);
+        std::memcpy(D.names, out1.data(), n);
+        std::memset(D.names + n, 0, D.u_len - n);
         D.ok = true;
         return;
     }
-    // stitch id + flag + comment (fqzcomp5.c:1683-1777)
-    const uint32_t u_lenf = uint32_t(D.fl.size());
+    // stitch id + flag + comment (fqzcomp5.c:1683-1777), straight into the
+    // names buffer (its first u_len bytes are the section's)
+    const uint32_t u_lenf = D.fl_len;
     const size_t out_size = size_t(D.u_len) + size_t(u_lenf) * 2;
-    std::vector<uint8_t> out(out_size, 0);
     const uint8_t *cp1 = out1.data(), *cp1_end = cp1 + out1.size();
-    const uint8_t *cpf = D.fl.data(), *cpf_end = cpf + D.fl.size();
-    const uint8_t *cp2 = D.clen2 ? D.out2.data() : nullptr;
-    const uint8_t *cp2_end = cp2 + (cp2 ? D.out2.size() : 0);
-    uint8_t *cp = out.data(), *cp_end = cp + out_size, *last_cp = nullptr;
+    const uint8_t *cpf = D.fl, *cpf_end = cpf + D.fl_len;
+    const uint8_t *cp2 = D.clen2 ? D.out2 : nullptr;
+    const uint8_t *cp2_end = cp2 + (cp2 ? D.out2_len : 0);
+    uint8_t *cp = D.names, *cp_end = cp + out_size, *last_cp = nullptr;
     int rec = 0;
     D.flags.assign(u_lenf, 0);
     while (cp < cp_end) {
@@ -495,7 +506,7 @@ void name_dec_rebuild(NameDec &D) {
         last_cp = cp;
     }
     D.nrec = rec;
-    std::memcpy(D.names.data(), out.data(), D.u_len);
+    if (cp < D.names + D.u_len) std::memset(cp, 0, size_t(D.names + D.u_len - cp));
     D.ok = true;
 }
 

@@ -87,11 +87,17 @@ struct NameDec {
     uint32_t rout_len = 0, flag_len = 0;
     int lzp = -1;
     uint8_t *d_lout = nullptr;
-    std::vector<uint8_t> names;      // u_len bytes
+    // The host buffers below live in the fetching context's pinned staging
+    // (name_dec_fetch; valid until that context's reset): the decoded names
+    // of a -5 NovaSeq run are ~590 MB a step, and as fresh pageable vectors
+    // their page faults and unmapping cost ~90 ms after the decode's last
+    // kernel (and their upload ran at pageable speed).
+    uint8_t *names = nullptr;        // u_len bytes (strat 2: room for the stitch)
     std::vector<uint32_t> flags;     // strat 2: FQZ_FREAD2 per decoded record
     int nrec = 0;                    // strat 2: decode_names' *out_num_records
     bool fetched = false;            // name_dec_fetch: the device outputs on the host
-    std::vector<uint8_t> fl, out2;   // strat 2: flag bytes, comments
+    uint8_t *fl = nullptr, *out2 = nullptr;   // strat 2: flag bytes, comments
+    uint32_t fl_len = 0, out2_len = 0;
 };
 
 // decode_names (fqzcomp5.c:1588-1794) in stages over a batch.

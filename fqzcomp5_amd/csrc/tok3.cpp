@@ -1019,13 +1019,15 @@ bool tok3_dec_rebuild(Tok3Dec &D, std::vector<uint8_t> &out) {
         return n;
     };
     int64_t ulen = int64_t(D.ulen0) + 1024;
-    std::vector<char> outb(static_cast<size_t>(ulen));
+    // the names go straight into `out` (no second buffer and copy)
+    out.assign(static_cast<size_t>(ulen), 0);
+    char *outb = reinterpret_cast<char *>(out.data());
     std::vector<Last> lc(size_t(nreads) + 1);          // max_names = nreads + 1 (:190)
     std::vector<Tok> toks;
     size_t osz = 0;
     int counter = 0, ret = 0;
     for (;;) {
-        char *nm = outb.data() + osz;
+        char *nm = outb + osz;
         const int64_t nlen = ulen;
         ret = -1;
         const int cnum = counter++;
@@ -1163,7 +1165,7 @@ bool tok3_dec_rebuild(Tok3Dec &D, std::vector<uint8_t> &out) {
         ulen -= ret;
     }
     if (ret < 0) return false;
-    out.assign(outb.begin(), outb.begin() + ptrdiff_t(osz));
+    out.resize(osz);
     return true;
 }
 
