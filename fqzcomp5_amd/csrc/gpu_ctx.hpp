@@ -539,34 +539,43 @@ inline size_t hedge_copies(size_t jobs, size_t cus) {
     const size_t c = cus / jobs;
     return c < 1 ? 1 : (c > 4 ? 4 : c);
 }
-// Copies per chain of a launch, from the chains' step counts: one each,
-// then the CUs left over, one copy at a time in turn, to the chains of at
-// least half the longest length (they set the launch time; a shorter
-// chain finishes in time on any CU), up to HEDGE_MAX copies each.  The slowest CUs
-// run a chain ~40 % slower than the fastest, so the
-// long chains gain the most from more draws.  All ones when hedging is off.
+// Copies per chain of a launch, from the chains' costs (steps, or steps
+// times the decoder's time per step): one each, then the CUs left over, one
+// copy at a time, to the chain of at least half the largest cost with the
+// most cost per copy (equal costs: in turn), up to HEDGE_MAX copies each.
+// Those chains set the launch time (a cheaper chain finishes in time on any
+// CU). The slowest CUs run a chain ~40 % slower than the fastest (DESIGN.md
+// section 4), so the costly chains gain the most from more draws.  All ones
+// when hedging is off.
 constexpr int HEDGE_MAX = 24;   // copies of one chain at most
-inline std::vector<int> hedge_plan(const std::vector<uint64_t> &steps, size_t cus) {
-    std::vector<int> c(steps.size(), 1);
+inline std::vector<int> hedge_plan(const std::vector<double> &cost, size_t cus) {
+    std::vector<int> c(cost.size(), 1);
     static const size_t cap_waves = [] {   // experiments: $FQZ5_HEDGE_WAVES caps the launch
         const char *e = std::getenv("FQZ5_HEDGE_WAVES");
         return e ? size_t(std::strtoul(e, nullptr, 10)) : size_t(0);
     }();
     if (cap_waves && cap_waves < cus) cus = cap_waves;
-    if (!hedge_chains() || steps.empty() || steps.size() >= cus) return c;
-    uint64_t mx = 0;
-    for (uint64_t s : steps) mx = s > mx ? s : mx;
+    if (!hedge_chains() || cost.empty() || cost.size() >= cus) return c;
+    double mx = 0;
+    for (double s : cost) mx = s > mx ? s : mx;
     std::vector<size_t> longs;
-    for (size_t i = 0; i < steps.size(); i++)
-        if (2 * steps[i] >= mx) longs.push_back(i);
-    size_t spare = cus - steps.size();
-    for (int round = 1; round < HEDGE_MAX && spare; round++)
-        for (size_t i : longs) {
-            if (!spare) break;
-            c[i]++;
-            spare--;
+    for (size_t i = 0; i < cost.size(); i++)
+        if (2 * cost[i] >= mx) longs.push_back(i);
+    for (size_t spare = cus - cost.size(); spare; spare--) {
+        size_t best = longs.size();
+        for (size_t k = 0; k < longs.size(); k++) {
+            const size_t i = longs[k];
+            if (c[i] >= HEDGE_MAX) continue;
+            if (best == longs.size() ||
+                cost[i] * c[longs[best]] > cost[longs[best]] * c[i]) best = k;
         }
+        if (best == longs.size()) break;
+        c[longs[best]]++;
+    }
     return c;
+}
+inline std::vector<int> hedge_plan(const std::vector<uint64_t> &steps, size_t cus) {
+    return hedge_plan(std::vector<double>(steps.begin(), steps.end()), cus);
 }
 
 // XCD-grouped layout of a hedged launch: workgroup b runs on XCD b % 8

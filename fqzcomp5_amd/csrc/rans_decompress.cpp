@@ -435,8 +435,16 @@ void Decompressor::run_djs(const std::vector<int> &ids) {
     EventPair ev((g_.prof.on || prof_on()) && !ord.empty(), g_.stream);
     // hedge: the long streams several times on different CUs, while the
     // copies fit one per CU (hedge_plan)
-    std::vector<uint64_t> steps;
-    for (const DecJob &d : djs) steps.push_back(uint64_t(d.n) / uint32_t(d.nx));
+    // a chain's cost: its steps, those of the table decoders weighted by
+    // their time per step against the O0 register decoder's
+    // ($FQZ5_HEDGE_TABW; 1 = by steps alone)
+    static const double tabw = [] {
+        const char *e = std::getenv("FQZ5_HEDGE_TABW");
+        return e ? std::atof(e) : 1.0;
+    }();
+    std::vector<double> steps;
+    for (const DecJob &d : djs)
+        steps.push_back(double(d.n / uint32_t(d.nx)) * (d.nreg ? 1.0 : tabw));
     HedgeShare share(size_t(g_.cus));          // held until the launch is synchronised
     const std::vector<int> cp = hedge_plan(steps, share.cus);
     if (std::any_of(cp.begin(), cp.end(), [](int c) { return c > 1; })) {
