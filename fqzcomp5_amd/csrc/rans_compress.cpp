@@ -41,7 +41,7 @@ namespace fqz5 {
 namespace {
 
 constexpr uint32_t HIST_SLICE = 1u << 17;
-constexpr uint32_t HIST1_BIG_SLICE = (1u << 16) - 64;   // 16-bit counters (k_hist1<true>)
+constexpr uint32_t HIST1_BIG_SLICE = 1u << 22;   // 16-bit counters that spill (k_hist1<true>)
 constexpr uint32_t NONE32 = 0xffffffffu;
 
 struct EJ {                       // one rANS entropy stream to encode

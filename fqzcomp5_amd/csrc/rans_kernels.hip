@@ -90,8 +90,15 @@ __global__ __launch_bounds__(256) void k_hist0(const HistItem *items,
 //   A*A < 16384: the bins live in LDS in C privatised copies (C = 32 down
 //                to 1 as A*A grows, within 64 KB);
 //   larger (packed bytes, A up to 256): 16-bit counters, two per LDS word,
-//                128 KB for all 65536 bins; a slice holds fewer than 65536
-//                bytes (HIST_SLICE) so no counter overflows.
+//                128 KB for all 65536 bins.  A counter that reaches 0x8000
+//                spills: the add that saw 0x7fff takes 0x8000 back out of LDS
+//                and adds it to the global count (the other adds that can
+//                land in between are a few hundred, far from the 16-bit
+//                limit), so a workgroup takes a multi-MB slice and flushes its
+//                65536 bins once per slice.  (With 64 KB slices a -5 NovaSeq
+//                step's packed candidates were ~24 000 workgroups that each
+//                flushed every bin by global atomics: ~110 ms, with the
+//                128 KB-LDS workgroups holding every CU meanwhile.)
 template <bool BIG>
 __global__ __launch_bounds__(256) void k_hist1(const Hist1Item *items,
                                                uint32_t *counts) {
@@ -124,8 +131,16 @@ __global__ __launch_bounds__(256) void k_hist1(const Hist1Item *items,
             const int64_t q = p0 + k;
             if (q >= int64_t(it.begin) && q < int64_t(it.end)) {
                 const uint32_t b = (q == 0 ? uint32_t(rm[0]) : p) * A + c;   // byte 0: context 0
-                if (BIG) atomicAdd(&bins[b >> 1], 1u << (16 * (b & 1)));
-                else atomicAdd(&mine[b], 1u);
+                if (BIG) {
+                    const uint32_t sh = 16u * (b & 1u);
+                    const uint32_t old = atomicAdd(&bins[b >> 1], 1u << sh);
+                    if (((old >> sh) & 0xffffu) == 0x7fffu) {
+                        atomicSub(&bins[b >> 1], 0x8000u << sh);
+                        atomicAdd(&gout[b], 0x8000u);
+                    }
+                } else {
+                    atomicAdd(&mine[b], 1u);
+                }
             }
             p = c;
         }

@@ -116,6 +116,35 @@ def test_capacity_semantics_vs_oracle():
             assert got == exp, (len(d), hex(o), cap)
 
 
+def test_o1_big_alphabet_counter_spills():
+    """O1 pair counts of a >= 128-symbol alphabet (k_hist1<true>: 16-bit LDS
+    counters that spill at 0x8000, 4 MB slices): one pair repeated ~3M times
+    (many spills of one bin), a second hot pair, and a 9 MB input (three
+    slices), against the oracle's bytes, O1 alone and after PACK/RLE."""
+    ora = binding.oracle()
+    rng = np.random.default_rng(11)
+    n = 9_000_000
+    d = rng.integers(0, 200, n, dtype=np.uint8)
+    d[1_000_000:4_000_000] = 7                      # pair (7, 7): ~3M counts
+    d[5_000_000:7_000_000:2] = 9                    # pairs (9, x) / (x, 9)
+    d[5_000_001:7_000_000:2] = 250
+    data = d.tobytes()
+    for o in (1, 5, 65):
+        exp = ora.rans_compress(data, o)
+        got = lib.rans_compress(data, o)
+        assert got == exp, hex(o)
+        assert lib.rans_uncompress(got) == data, hex(o)
+    # packed bytes: 16 symbols, 2 per byte -> up to 256 packed values
+    q = (rng.integers(0, 16, n, dtype=np.uint8) + 33)
+    q[2_000_000:6_000_000] = 40
+    qd = q.tobytes()
+    for o in (129, 193):
+        exp = ora.rans_compress(qd, o)
+        got = lib.rans_compress(qd, o)
+        assert got == exp, hex(o)
+        assert lib.rans_uncompress(got) == qd, hex(o)
+
+
 def test_large_q40_roundtrip():
     from fqzcomp5_amd import synth
     r = synth.illumina(20000, seed=3, binned=False)
