@@ -241,7 +241,10 @@ GpuCtx &gpu_aux(int k) {
         // rANS helper's chain in about half the steps (encode 300 ms on
         // average, 230-400; all at normal priority 254, 228-296); the -5
         // items were within their noise either way.
-        const bool high = std::getenv("FQZ5_AUX_HIGH_PRIO") != nullptr;
+        // ($FQZ5_FQZ_HIGH_PRIO=1: the fqz helper alone at high priority,
+        // for experiments on the -5 try's fqz statistics round trips)
+        const bool high = std::getenv("FQZ5_AUX_HIGH_PRIO") != nullptr ||
+                          (k == 0 && std::getenv("FQZ5_FQZ_HIGH_PRIO") != nullptr);
         g_aux[k].reset(new GpuCtx(high));
         if (g_wait_armed) ctx_wait(*g_aux[k], g_wait_ev);
     }

@@ -1013,13 +1013,22 @@ def block_lengths(lens: np.ndarray, fixed_len: int) -> bytes:
     return buf.raw[:n]
 
 
-def parse_blocks(ptrs, sizes, nrecs, version: int = 0):
+def parse_blocks(ptrs, sizes, nrecs, version: int = 0, lens_out=None):
     """fqz5_blocks_parse_v over device blocks (addresses, byte sizes, record
-    counts from the headers): per block its BlockView and record lengths."""
+    counts from the headers): per block its BlockView and record lengths.
+    lens_out: the callers' length arrays to fill (uint32, one per block, at
+    least max(nrec, 1) long; a caller that parses the same blocks every step
+    keeps them, instead of ~45 MB of fresh pages a -5 NovaSeq step)."""
     so = _load_blk()
     n = len(ptrs)
     views = (BlockView * max(n, 1))()
-    lens = [np.zeros(max(k, 1), np.uint32) for k in nrecs]
+    if lens_out is not None:
+        lens = lens_out
+        if len(lens) != n or any(len(x) < max(k, 1) or x.dtype != np.uint32
+                                 for x, k in zip(lens, nrecs)):
+            raise ValueError("parse_blocks: lens_out does not fit the blocks")
+    else:
+        lens = [np.zeros(max(k, 1), np.uint32) for k in nrecs]
     lp = (C.POINTER(C.c_uint32) * max(n, 1))(*[x.ctypes.data_as(C.POINTER(C.c_uint32)) for x in lens])
     caps = (C.c_uint32 * max(n, 1))(*[len(x) for x in lens])
     st = (C.c_int32 * max(n, 1))()
@@ -1259,10 +1268,13 @@ class Run:
         batched fqz5_blocks_parse_v for all of them)."""
         out = []
         base = self.blk_buf.data_ptr()
+        nrecs = [len(self.lens[b]) for b in range(len(self.blocks))]
+        if getattr(self, "_plens", None) is None:
+            self._plens = [np.zeros(max(k, 1), np.uint32) for k in nrecs]
         parsed = parse_blocks([base + int(self.blk_off[b]) for b in range(len(self.blocks))],
                               [int(self.blk_off[b + 1] - self.blk_off[b])
                                for b in range(len(self.blocks))],
-                              [len(self.lens[b]) for b in range(len(self.blocks))])
+                              nrecs, lens_out=self._plens)
         for b in range(len(self.blocks)):
             v, lens = parsed[b]
             if not v.crc_ok:
