@@ -284,44 +284,117 @@ __global__ void k_fqz_ev_count(FqzEvJob J) {
 
 // Phase 1: the events of each record in stream order (compress_block_fqz2f
 // record header, fqzcomp_qual.c:1119-1192, then one event per quality).
-__global__ void k_fqz_ev_fill(FqzEvJob J) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= J.nrec) return;
+// A wave takes 64 records, whose events are one contiguous range of the
+// list and whose quality bytes one contiguous range of q.  Per window of
+// EVW events: the wave stages the window's quality bytes into LDS with
+// coalesced loads, each lane generates its own record's events of the
+// window in order (the context chain is serial within a record) into LDS,
+// packed as model << 8 | symbol, and the wave writes the window out with
+// consecutive lanes on consecutive events.  The parameter tables are read
+// from an LDS copy.  (Up to round 6 one thread per record read its bytes and
+// wrote its events itself: every load and store touched 64 lines, ~300 B of
+// HBM traffic per event at -5 Illumina, profiles/r06_pmc_l5i.json.)
+constexpr uint32_t EVW = 4096;          // events per window
+constexpr uint32_t EVQ = 8192;          // quality bytes staged per window
+__global__ __launch_bounds__(64) void k_fqz_ev_fill(FqzEvJob J) {
+    __shared__ uint32_t win[EVW];
+    __shared__ uint32_t qst[EVQ / 4];
+    __shared__ FqzDevParam pm;
+    const uint32_t lane = threadIdx.x;
     const FqzDevGlobal &g = *J.g;
-    const FqzDevParam &pm = g.p[0];
-    uint32_t e = J.ev_off[r];
-    const uint32_t len = J.len[r];
-    const bool dup = J.dup[r];
-    auto put = [&](uint32_t model, uint32_t sym) {
-        J.key[e] = model;
-        J.val[e] = (uint64_t(e) << 8) | sym;
-        e++;
-    };
-    Ctx st{};
-    if (pm.sel || (g.gflags & 1u)) {
-        st.sel = J.sel[r];
-        put(FQZ_M_SEL, st.sel);
+    {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(&g.p[0]);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(&pm);
+        static_assert(sizeof(FqzDevParam) % 4 == 0, "parameter copy by words");
+        for (uint32_t i = lane; i < sizeof(FqzDevParam) / 4; i += 64u) dst[i] = src[i];
     }
-    if (!pm.fixed || r == 0)
-        for (uint32_t b = 0; b < 4; b++) put(FQZ_M_LEN + b, (len >> (8 * b)) & 0xffu);
-    if (g.gflags & 4u) put(FQZ_M_REV, (J.flags[r] & 16u) ? 1u : 0u);
-    if (pm.dedup) put(FQZ_M_DUP, dup);
-    if (dup) return;
+    __syncthreads();
+    const uint32_t r0 = blockIdx.x * 64u;
+    const uint32_t r = r0 + lane;
+    const bool act = r < J.nrec;
+    const uint32_t rend = min(r0 + 64u, J.nrec);
+    const uint32_t E0 = J.ev_off[r0];
+    const uint32_t E1 = rend < J.nrec ? J.ev_off[rend] : J.nev;
+    const uint64_t qtot = J.off[J.nrec - 1] + J.len[J.nrec - 1];
+    uint32_t e = act ? J.ev_off[r] : E1;
+    const uint32_t e_end = act ? (r + 1 < J.nrec ? J.ev_off[r + 1] : J.nev) : E1;
+    const uint32_t len = act ? J.len[r] : 0u;
+    const bool dup = act && J.dup[r];
+    const bool has_sel = pm.sel || (g.gflags & 1u);
+    const bool has_len = !pm.fixed || r == 0;
+    const bool has_rev = (g.gflags & 4u) != 0u;
+    const uint32_t nh = (has_sel ? 1u : 0u) + (has_len ? 4u : 0u) + (has_rev ? 1u : 0u) +
+                        (pm.dedup ? 1u : 0u);
+    Ctx st{};
+    if (act && has_sel) st.sel = J.sel[r];
+    const uint32_t rev = act && has_rev && (J.flags[r] & 16u) ? 1u : 0u;
     st.left = len;
     const uint8_t *sp = nullptr, *se = nullptr;
-    if (J.seq && J.seq_off[r] != ~0ull) {
+    if (act && !dup && J.seq && J.seq_off[r] != ~0ull) {
         const uint8_t *s0 = J.seq + J.seq_off[r];
         sp = s0 + pm.boff;
         se = s0 + len;
         for (uint32_t b = 0; b < pm.boff; b++) st.seq = (st.seq << 2) | base2(s0[b]);
     }
-    const uint8_t *q = J.q + J.off[r];
-    uint32_t ctx = pm.ctx0;
-    for (uint32_t t = 0; t < len; t++) {
-        const uint32_t sym = pm.qmap[q[t]];
-        const uint32_t base = sp && sp < se ? base2(*sp++) : 0u;
-        put(ctx, sym);
-        ctx = next_ctx(pm, st, sym, base);
+    const uint64_t qoff = act ? J.off[r] : 0ull;
+    uint32_t ctx = pm.ctx0, h = 0, t = 0;
+    // header event i of the record: selector, four length bytes, reverse
+    // flag, duplicate flag (each only where the parameters code it)
+    auto header = [&](uint32_t i) -> uint32_t {
+        if (has_sel) { if (i == 0) return FQZ_M_SEL << 8 | st.sel; i--; }
+        if (has_len) { if (i < 4) return (FQZ_M_LEN + i) << 8 | ((len >> (8 * i)) & 0xffu); i -= 4; }
+        if (has_rev) { if (i == 0) return FQZ_M_REV << 8 | rev; i--; }
+        return FQZ_M_DUP << 8 | (dup ? 1u : 0u);
+    };
+    const uint8_t *qsb = reinterpret_cast<const uint8_t *>(qst);
+    for (uint32_t w0 = E0; w0 < E1; w0 += EVW) {
+        const uint32_t wend = min(w0 + EVW, E1);
+        const uint32_t stop = min(wend, e_end);
+        // the window's quality bytes start at the first lane (records are
+        // in lane order) that codes a quality symbol in it; a byte past the
+        // staged range (duplicate records in between) is read from q
+        const bool inq = e < stop && (h >= nh || nh - h < stop - e);
+        const uint64_t qm = __ballot(inq);
+        uint64_t qb = 0;
+        if (qm) {
+            const int fl = __builtin_ctzll(qm);
+            const uint64_t qpos = qoff + t;
+            qb = (uint64_t(__shfl(uint32_t(qpos >> 32), fl)) << 32 | __shfl(uint32_t(qpos), fl)) & ~3ull;
+            for (uint32_t i = lane; i < EVQ / 4; i += 64u) {
+                const uint64_t a = qb + 4ull * i;
+                uint32_t v = 0;
+                if (a + 4 <= qtot) {
+                    v = *reinterpret_cast<const uint32_t *>(J.q + a);
+                } else {
+                    for (uint32_t k = 0; k < 4; k++)
+                        if (a + k < qtot) v |= uint32_t(J.q[a + k]) << (8 * k);
+                }
+                qst[i] = v;
+            }
+        }
+        __syncthreads();
+        for (; e < stop; e++) {
+            uint32_t v;
+            if (h < nh) {
+                v = header(h++);
+            } else {
+                const uint64_t p = qoff + t - qb;
+                const uint32_t raw = p < EVQ ? qsb[p] : J.q[qoff + t];
+                t++;
+                const uint32_t sym = pm.qmap[raw];
+                const uint32_t base = sp && sp < se ? base2(*sp++) : 0u;
+                v = ctx << 8 | sym;
+                ctx = next_ctx(pm, st, sym, base);
+            }
+            win[e - w0] = v;
+        }
+        __syncthreads();
+        for (uint32_t i = lane; i < wend - w0; i += 64u) {
+            const uint32_t v = win[i];
+            J.key[w0 + i] = v >> 8;
+            J.val[w0 + i] = (uint64_t(w0 + i) << 8) | (v & 0xffu);
+        }
+        __syncthreads();
     }
 }
 
@@ -956,7 +1029,7 @@ hipError_t launch_fqz_events(const FqzEvJob &j, int phase, hipStream_t s) {
     if (phase == 0 && j.nrec)
         hipLaunchKernelGGL(k_fqz_ev_count, dim3((j.nrec + 255) / 256), dim3(256), 0, s, j);
     else if (phase == 1 && j.nrec)
-        hipLaunchKernelGGL(k_fqz_ev_fill, dim3((j.nrec + 255) / 256), dim3(256), 0, s, j);
+        hipLaunchKernelGGL(k_fqz_ev_fill, dim3((j.nrec + 63) / 64), dim3(64), 0, s, j);
     else if (phase == 2 && j.nev)
         hipLaunchKernelGGL(k_fqz_segments, dim3((j.nev + 255) / 256), dim3(256), 0, s, j);
     return hipGetLastError();
