@@ -29,17 +29,16 @@ struct SeqJob {
     uint32_t *run_start;                // per run (nrun)
     uint32_t *cnt, *run_off;            // per run D + 1 (and 0 at nrun), its exclusive scan
     uint32_t *key;                      // per context event (interleaved fw/rv): context id
-    uint64_t *val;                      //   (2p + rv) << 8 | symbol
+    uint64_t *val;                      //   (2e + rv) << 8 | symbol, e the event index of
+                                        //   the forward symbol of the byte
     const uint32_t *skey;               // the same, sorted by context
     const uint64_t *sval;
-    uint32_t *ev;                       // per byte: the event index of its symbol
     uint4 *rec;                         // per coding event: {RN(1/total) (2 words), freq, cum}
 };
 
 hipError_t launch_seq_heads(const SeqJob &j, hipStream_t s);
 hipError_t launch_seq_runs(const SeqJob &j, hipStream_t s);       // run starts, cnt
 hipError_t launch_seq_ctx(const SeqJob &j, hipStream_t s);        // keys / values
-hipError_t launch_seq_ev(const SeqJob &j, hipStream_t s);         // byte -> event index
 hipError_t launch_seq_model(const SeqJob &j, hipStream_t s);      // context events -> rec
 hipError_t launch_seq_side(const SeqJob &j, hipStream_t s);       // run / literal / state -> rec
 

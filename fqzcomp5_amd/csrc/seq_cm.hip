@@ -101,46 +101,79 @@ __global__ void k_seq_run_cnt(SeqJob J) {
     J.cnt[r] = (end - J.run_start[r]) / 255u + 2u;
 }
 
-// one thread per record segment (contexts restart at its start)
-__global__ void k_seq_ctx(SeqJob J) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= J.nseg) return;
-    const uint32_t mask = J.mask, inval = mask + 1u, top = 2u * J.k - 2u;
-    uint32_t fw = seed_fw(mask), rv = seed_rv(J.k, mask);
-    const uint32_t stride = J.both ? 2u : 1u;
-    for (uint32_t p = J.seg[s]; p < J.seg[s + 1]; p++) {
-        const uint32_t c = J.in[p];
-        const uint32_t i = stride * p;
-        if (seq_class(c) < 2u) {
-            const uint32_t b = seq_code(c);
-            J.key[i] = fw;
-            J.val[i] = (uint64_t(2u * p) << 8) | b;
-            fw = ((fw << 2) + b) & mask;
-            if (J.both) {
-                const uint32_t b2 = rv & 3u;
-                rv = (rv >> 2) + ((3u - b) << top);
-                J.key[i + 1] = rv;
-                J.val[i + 1] = (uint64_t(2u * p + 1u) << 8) | b2;
-            }
-        } else {
-            J.key[i] = inval;
-            if (J.both) J.key[i + 1] = inval;
-        }
-    }
-}
-
 // event index of the symbol at byte p (seq_cm.h)
 DEV uint32_t sym_event(const SeqJob &J, uint32_t p) {
     const uint32_t r = J.ex[p] + J.flag[p] - 1u;
     return p + J.lead + J.run_off[r] + J.cnt[r] - 1u;
 }
 
-// the event index of every byte (coalesced, so that the model pass below
-// does one random read per event instead of four)
-__global__ void k_seq_ev(SeqJob J) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= J.n) return;
-    J.ev[p] = sym_event(J, p);
+// The context events, a wave per 64 record segments (contexts restart at a
+// segment's start; the 64 segments are one contiguous range of bytes and of
+// events).  Per window of SEQ_CTX_W bytes: the wave stages the bytes and
+// each forward symbol's event index (sym_event) into LDS with coalesced
+// loads, each lane walks its own segment's bytes of the window (the k-mers
+// are a serial recurrence) into LDS, and the wave writes the window's keys
+// and values out as whole lines.  The value carries the event index of the
+// forward symbol, so the model pass writes its record without a gather.
+// (Up to round 6 one thread per segment wrote its events itself and a
+// separate pass, k_seq_ev, kept a byte -> event table for the model pass to
+// gather from: ~8.5 GB of HBM traffic per k_seq_ctx dispatch and one random
+// read per event in k_seq_model_runs, profiles/r06_pmc_l5.json.)
+constexpr uint32_t SEQ_CTX_W = 2048;
+__global__ __launch_bounds__(64) void k_seq_ctx(SeqJob J) {
+    __shared__ uint8_t cin[SEQ_CTX_W];
+    __shared__ uint32_t cev[SEQ_CTX_W];
+    __shared__ uint32_t okey[2 * SEQ_CTX_W];
+    __shared__ uint8_t osym[2 * SEQ_CTX_W];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t s0 = blockIdx.x * 64u;
+    const uint32_t s = s0 + lane;
+    const bool act = s < J.nseg;
+    const uint32_t send = min(s0 + 64u, J.nseg);
+    const uint32_t P0 = J.seg[s0], P1 = J.seg[send];
+    uint32_t p = act ? J.seg[s] : P1;
+    const uint32_t pend = act ? J.seg[s + 1] : P1;
+    const uint32_t mask = J.mask, inval = mask + 1u, top = 2u * J.k - 2u;
+    const uint32_t both = J.both, sh = both ? 1u : 0u;
+    uint32_t fw = seed_fw(mask), rv = seed_rv(J.k, mask);
+    for (uint32_t w0 = P0; w0 < P1; w0 += SEQ_CTX_W) {
+        const uint32_t wn = min(SEQ_CTX_W, P1 - w0);
+        for (uint32_t i = lane; i < wn; i += 64u) {
+            const uint32_t c = J.in[w0 + i];
+            cin[i] = uint8_t(c);
+            cev[i] = seq_class(c) < 2u ? sym_event(J, w0 + i) : 0u;
+        }
+        __syncthreads();
+        const uint32_t stop = min(pend, w0 + wn);
+        for (; p < stop; p++) {
+            const uint32_t o = (p - w0) << sh;
+            const uint32_t c = cin[p - w0];
+            if (seq_class(c) < 2u) {
+                const uint32_t b = seq_code(c);
+                okey[o] = fw;
+                osym[o] = uint8_t(b);
+                fw = ((fw << 2) + b) & mask;
+                if (both) {
+                    const uint32_t b2 = rv & 3u;
+                    rv = (rv >> 2) + ((3u - b) << top);
+                    okey[o + 1] = rv;
+                    osym[o + 1] = uint8_t(b2);
+                }
+            } else {
+                okey[o] = inval;
+                if (both) okey[o + 1] = inval;
+            }
+        }
+        __syncthreads();
+        const uint64_t e0 = uint64_t(w0) << sh;
+        for (uint32_t i = lane; i < (wn << sh); i += 64u) {
+            const uint32_t k = okey[i];
+            J.key[e0 + i] = k;
+            J.val[e0 + i] = k == inval ? 0ull
+                                       : (uint64_t(2u * cev[i >> sh] + (i & sh)) << 8) | osym[i];
+        }
+        __syncthreads();
+    }
 }
 
 // The model pass: per context, the head of its run in the sorted order walks
@@ -172,8 +205,7 @@ DEV void seq_walk(const SeqJob &J, uint32_t i) {
         const uint32_t ord = uint32_t(v >> 8);
         const uint32_t tot = sm4_total(F);
         if (!(ord & 1u)) {
-            const uint32_t p = ord >> 1;
-            J.rec[J.ev[p]] = rc_rec((F >> (8u * sym)) & 255u, sm4_cum(F, sym), tot);
+            J.rec[ord >> 1] = rc_rec((F >> (8u * sym)) & 255u, sm4_cum(F, sym), tot);
         }
         F = sm4_bump(F, sym, tot);
     }
@@ -217,7 +249,7 @@ DEV void seq_walk_wave(const SeqJob &J, uint32_t i) {
         if (in) {
             const uint32_t ord = uint32_t(v >> 8);
             if (!(ord & 1u))
-                J.rec[J.ev[ord >> 1]] = rc_rec((myF >> (8u * sym)) & 255u, sm4_cum(myF, sym), sm4_total(myF));
+                J.rec[ord >> 1] = rc_rec((myF >> (8u * sym)) & 255u, sm4_cum(myF, sym), sm4_total(myF));
         }
         if (cnt < 64u) break;
         j = jn;
@@ -851,12 +883,7 @@ hipError_t launch_seq_runs(const SeqJob &j, hipStream_t s) {
 }
 
 hipError_t launch_seq_ctx(const SeqJob &j, hipStream_t s) {
-    if (j.nseg && j.n) hipLaunchKernelGGL(k_seq_ctx, grid_of(j.nseg), dim3(256), 0, s, j);
-    return hipGetLastError();
-}
-
-hipError_t launch_seq_ev(const SeqJob &j, hipStream_t s) {
-    if (j.n) hipLaunchKernelGGL(k_seq_ev, grid_of(j.n), dim3(256), 0, s, j);
+    if (j.nseg && j.n) hipLaunchKernelGGL(k_seq_ctx, dim3((j.nseg + 63) / 64), dim3(64), 0, s, j);
     return hipGetLastError();
 }
 

@@ -119,8 +119,6 @@ static void seq_prepare_dev(GpuCtx &g, SeqWork &W, const uint8_t *d_in, uint32_t
         J.sval = sval;
     }
     J.rec = g.fqz_tmp.alloc_n<uint4>(nev + RC_PAD);
-    J.ev = g.fqz_tmp.alloc_n<uint32_t>(n ? n : 1);
-    FQZ5_HIP(launch_seq_ev(J, g.stream));
     {
         ProfSpan sp(PK_SEQ_MODEL, g.stream);
         FQZ5_HIP(launch_seq_model(J, g.stream));

@@ -161,7 +161,14 @@ __global__ void k_t3_names(T3Batch B) {
     B.st[k] = st;
     B.len[k] = L;
     B.sec[k] = s;
-    if (L < T3_LSET_BITS) atomicOr(&B.lset[s * (T3_LSET_BITS / 32) + L / 32], 1u << (L % 32));
+    // the length set: most names of a block share a few lengths, so the bit
+    // is read first and set only when it is still clear (one atomic per new
+    // length, not one per name on the same word: -5 NovaSeq, ~24 ms a launch)
+    if (L < T3_LSET_BITS) {
+        uint32_t *w = &B.lset[s * (T3_LSET_BITS / 32) + L / 32];
+        const uint32_t bit = 1u << (L % 32);
+        if (!(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(w, bit);
+    }
 }
 
 // the depths at which name k enters a pair (its walk has L bytes)
@@ -183,27 +190,55 @@ __global__ void k_t3_count(T3Batch B) {
 }
 
 // per name: its pairs (key, pair number) in depth order, each pair's name
-// and depth; name_format's results
-__global__ void k_t3_pairs(T3Batch B) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= B.nnames) return;
-    const uint32_t st = B.st[k], L = B.len[k], sec = B.sec[k];
+// and depth; name_format's results.  A wave takes 64 names, whose pairs are
+// one contiguous range; per window of T3W pairs each lane walks its own name
+// (the prefix hash is serial) into LDS and the wave writes the window out
+// as whole lines.  (Round 6: one thread per name writing its own pairs made
+// every store touch 64 lines: 14.4 GB of HBM traffic in the -5 NovaSeq
+// dispatch, 11.4 GB of it writes, profiles/r06_pmc_l5.json.)
+constexpr uint32_t T3W = 2048;
+__global__ __launch_bounds__(64) void k_t3_pairs(T3Batch B) {
+    __shared__ uint64_t wkey[T3W];
+    __shared__ uint32_t wdep[T3W];
+    __shared__ uint8_t wln[T3W];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t k0 = blockIdx.x * 64u;
+    const uint32_t k = k0 + lane;
+    const bool act = k < B.nnames;
+    const uint32_t kend = min(k0 + 64u, B.nnames);
+    const uint32_t Q0 = B.poff[k0];
+    const uint32_t Q1 = kend < B.nnames ? B.poff[kend] : B.npairs;
+    uint32_t q = act ? B.poff[k] : Q1;
+    const uint32_t st = act ? B.st[k] : 0u, L = act ? B.len[k] : 0u, sec = act ? B.sec[k] : 0u;
     const uint32_t *lset = B.lset + sec * (T3_LSET_BITS / 32);
     const uint8_t *s = B.bytes + st;
-    int is_fixed, fixed_len;
-    const int pl = name_format(s, L, &is_fixed, &fixed_len);
-    B.fmt[k] = make_int4(pl, is_fixed, fixed_len, 0);
+    if (act) {
+        int is_fixed, fixed_len;
+        const int pl = name_format(s, L, &is_fixed, &fixed_len);
+        B.fmt[k] = make_int4(pl, is_fixed, fixed_len, 0);
+    }
     uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t(sec) * 0xd6e8feb86659fd93ull);
-    uint32_t q = B.poff[k];
-    for (uint32_t d = 1; d <= L; d++) {
-        h = (h + s[d - 1] + 1) * 0x100000001b3ull;
-        h ^= h >> 29;
-        if (!t3_depth(B, lset, s, d, L)) continue;
-        B.key[q] = mix64(h + uint64_t(d) * 0x9fb21c651e98df25ull) >> (64 - T3_KEY_BITS);
-        B.val[q] = q;
-        B.pname[q] = k;
-        B.pdepth[q] = d;
-        q++;
+    uint32_t d = 1;
+    for (uint32_t w0 = Q0; w0 < Q1; w0 += T3W) {
+        const uint32_t wend = min(w0 + T3W, Q1);
+        for (; q < wend && d <= L; d++) {
+            h = (h + s[d - 1] + 1) * 0x100000001b3ull;
+            h ^= h >> 29;
+            if (!t3_depth(B, lset, s, d, L)) continue;
+            wkey[q - w0] = mix64(h + uint64_t(d) * 0x9fb21c651e98df25ull) >> (64 - T3_KEY_BITS);
+            wdep[q - w0] = d;
+            wln[q - w0] = uint8_t(lane);
+            q++;
+        }
+        __syncthreads();
+        for (uint32_t i = lane; i < wend - w0; i += 64u) {
+            const uint32_t qq = w0 + i;
+            B.key[qq] = wkey[i];
+            B.val[qq] = qq;
+            B.pname[qq] = k0 + wln[i];
+            B.pdepth[qq] = wdep[i];
+        }
+        __syncthreads();
     }
 }
 
@@ -302,7 +337,7 @@ hipError_t t3_launch(const T3Batch &b, int stage, hipStream_t s) {
         }
         break;
     case 3:
-        if (b.nnames) hipLaunchKernelGGL(k_t3_pairs, grid(b.nnames), dim3(256), 0, s, b);
+        if (b.nnames) hipLaunchKernelGGL(k_t3_pairs, dim3((b.nnames + 63) / 64), dim3(64), 0, s, b);
         break;
     case 4:
         if (b.npairs) hipLaunchKernelGGL(k_t3_pred, grid(b.npairs), dim3(256), 0, s, b);
