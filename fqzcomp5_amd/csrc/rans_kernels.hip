@@ -189,17 +189,37 @@ __global__ __launch_bounds__(256) void k_unpack(const PackItem *items) {
 
 // STRIPE (rANS_static4x16pr.c:1283-1309): byte i goes to stripe i%N at
 // offset i/N.  `dir` 0 = transpose (encode), 1 = untranspose (decode,
-// utils.h:79 unstripe).  One thread per byte.
+// utils.h:79 unstripe).  A workgroup takes a tile of N*C interleaved bytes
+// (C = STRIPE_TILE / N of each stripe): the interleaved side moves through
+// LDS with consecutive threads on consecutive bytes, and so does each
+// stripe's run of C bytes.  (Up to round 6 one thread per byte scattered
+// to N stripes: -5 NovaSeq up to 16.5 GB of HBM traffic in a dispatch,
+// profiles/r06_pmc_l5.json.)
+constexpr uint32_t STRIPE_TILE = 32768;
 __global__ __launch_bounds__(256) void k_stripe(const StripeItem *items) {
+    __shared__ uint8_t t[STRIPE_TILE];
     const StripeItem it = items[blockIdx.y];
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= it.n) return;
-    uint32_t s = i % it.N, o = i / it.N;
-    // start of stripe s: stripes < n%N are one longer
-    uint32_t q = it.n / it.N, r = it.n % it.N;
-    uint32_t base = s * q + (s < r ? s : r);
-    if (it.dir == 0) it.out[base + o] = it.in[i];
-    else it.out[i] = it.in[base + o];
+    const uint32_t N = it.N, C = STRIPE_TILE / N, T = N * C;
+    const uint64_t i0 = uint64_t(blockIdx.x) * T;
+    if (i0 >= it.n) return;
+    const uint32_t q = it.n / N, r = it.n % N;
+    const uint32_t o0 = blockIdx.x * C;
+    const uint32_t tn = uint32_t(min(uint64_t(T), uint64_t(it.n) - i0));
+    if (it.dir == 0) {
+        for (uint32_t k = threadIdx.x; k < tn; k += 256) t[k] = it.in[i0 + k];
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < T; k += 256) {
+            const uint32_t s = k / C, o = o0 + (k - s * C);
+            if (o < q + (s < r ? 1u : 0u)) it.out[s * q + min(s, r) + o] = t[(o - o0) * N + s];
+        }
+    } else {
+        for (uint32_t k = threadIdx.x; k < T; k += 256) {
+            const uint32_t s = k / C, o = o0 + (k - s * C);
+            if (o < q + (s < r ? 1u : 0u)) t[(o - o0) * N + s] = it.in[s * q + min(s, r) + o];
+        }
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < tn; k += 256) it.out[i0 + k] = t[k];
+    }
 }
 
 __global__ __launch_bounds__(256) void k_gather(const GatherItem *items, int n,
@@ -533,7 +553,8 @@ hipError_t launch_pack(const PackItem *d_items, int nitems, uint32_t max_out,
 hipError_t launch_stripe(const StripeItem *d_items, int nitems, uint32_t max_n,
                          hipStream_t s) {
     if (!nitems || !max_n) return hipSuccess;
-    dim3 g((max_n + 255) / 256, nitems);
+    // tiles of at least STRIPE_TILE - 254 interleaved bytes (N <= 255)
+    dim3 g((max_n + STRIPE_TILE - 255) / (STRIPE_TILE - 254), nitems);
     hipLaunchKernelGGL(k_stripe, g, dim3(256), 0, s, d_items);
     return hipGetLastError();
 }
