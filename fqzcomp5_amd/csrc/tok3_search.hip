@@ -172,9 +172,10 @@ __global__ void k_t3_names(T3Batch B) {
 }
 
 // the depths at which name k enters a pair (its walk has L bytes)
-__device__ __forceinline__ bool t3_depth(const T3Batch &B, const uint32_t *lset, const uint8_t *s,
+// (c: the name's byte d - 1)
+__device__ __forceinline__ bool t3_depth(const T3Batch &B, const uint32_t *lset, uint8_t c,
                                          uint32_t d, uint32_t L) {
-    return d == L || ps(s[d - 1]) || d == 6 || d == 36 || d == 60 || d >= T3_LSET_BITS ||
+    return d == L || ps(c) || d == 6 || d == 36 || d == 60 || d >= T3_LSET_BITS ||
            ((lset[d / 32] >> (d % 32)) & 1u);
 }
 
@@ -185,7 +186,7 @@ __global__ void k_t3_count(T3Batch B) {
     const uint32_t *lset = B.lset + B.sec[k] * (T3_LSET_BITS / 32);
     const uint8_t *s = B.bytes + st;
     uint32_t c = 0;
-    for (uint32_t d = 1; d <= L; d++) c += t3_depth(B, lset, s, d, L);
+    for (uint32_t d = 1; d <= L; d++) c += t3_depth(B, lset, s[d - 1], d, L);
     B.cnt[k] = c;
 }
 
@@ -193,14 +194,17 @@ __global__ void k_t3_count(T3Batch B) {
 // and depth; name_format's results.  A wave takes 64 names, whose pairs are
 // one contiguous range; per window of T3W pairs each lane walks its own name
 // (the prefix hash is serial) into LDS and the wave writes the window out
-// as whole lines.  (Round 6: one thread per name writing its own pairs made
-// every store touch 64 lines: 14.4 GB of HBM traffic in the -5 NovaSeq
-// dispatch, 11.4 GB of it writes, profiles/r06_pmc_l5.json.)
-constexpr uint32_t T3W = 2048;
+// as whole lines.  The walks read the names' bytes from an LDS copy of the
+// wave's first T3NB bytes (the names lie back to back), past it from HBM.
+// (Round 6: one thread per name writing its own pairs made every store touch
+// 64 lines: 14.4 GB of HBM traffic in the -5 NovaSeq dispatch, 11.4 GB of it
+// writes, profiles/r06_pmc_l5.json.)
+constexpr uint32_t T3W = 1024, T3NB = 4096;
 __global__ __launch_bounds__(64) void k_t3_pairs(T3Batch B) {
     __shared__ uint64_t wkey[T3W];
     __shared__ uint32_t wdep[T3W];
     __shared__ uint8_t wln[T3W];
+    __shared__ uint32_t nb32[T3NB / 4];
     const uint32_t lane = threadIdx.x;
     const uint32_t k0 = blockIdx.x * 64u;
     const uint32_t k = k0 + lane;
@@ -217,14 +221,30 @@ __global__ __launch_bounds__(64) void k_t3_pairs(T3Batch B) {
         const int pl = name_format(s, L, &is_fixed, &fixed_len);
         B.fmt[k] = make_int4(pl, is_fixed, fixed_len, 0);
     }
+    const uint32_t st0 = B.st[k0];
+    for (uint32_t i = lane; i < T3NB / 4; i += 64u) {
+        const uint32_t a = st0 + 4u * i;
+        uint32_t v = 0;
+        if (uint64_t(a) + 4 <= B.nbytes) {
+            v = *reinterpret_cast<const uint32_t *>(B.bytes + a);
+        } else {
+            for (uint32_t j = 0; j < 4; j++)
+                if (a + j < B.nbytes) v |= uint32_t(B.bytes[a + j]) << (8 * j);
+        }
+        nb32[i] = v;
+    }
+    __syncthreads();
+    const uint8_t *nb = reinterpret_cast<const uint8_t *>(nb32);
+    const uint32_t rel = st - st0;
     uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t(sec) * 0xd6e8feb86659fd93ull);
     uint32_t d = 1;
     for (uint32_t w0 = Q0; w0 < Q1; w0 += T3W) {
         const uint32_t wend = min(w0 + T3W, Q1);
         for (; q < wend && d <= L; d++) {
-            h = (h + s[d - 1] + 1) * 0x100000001b3ull;
+            const uint32_t c = rel + d - 1 < T3NB ? nb[rel + d - 1] : s[d - 1];
+            h = (h + c + 1) * 0x100000001b3ull;
             h ^= h >> 29;
-            if (!t3_depth(B, lset, s, d, L)) continue;
+            if (!t3_depth(B, lset, uint8_t(c), d, L)) continue;
             wkey[q - w0] = mix64(h + uint64_t(d) * 0x9fb21c651e98df25ull) >> (64 - T3_KEY_BITS);
             wdep[q - w0] = d;
             wln[q - w0] = uint8_t(lane);
